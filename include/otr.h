@@ -1,0 +1,144 @@
+/*
+ * otr.h — C-ABI of libotr.so, the MI355X-native drop-in for Open Traffic Reporter's
+ * matching hot path (trace JSON → map-match → OSMLR segment / speed JSON).
+ *
+ * Plain C: pointers, sizes, status codes.  No torch or HIP types cross this line.
+ * Every entry point names the reference interface it replaces.
+ *
+ * Threading: otr_configure() is process-global and not thread-safe (call once, as
+ * reporter_service.py:284 / simple_reporter.py:132 call valhalla.Configure once).
+ * An otr_matcher is owned by one thread at a time (reporter_service.py:51-52 keeps
+ * one valhalla.SegmentMatcher per thread); matchers share the read-only graph that
+ * otr_configure placed in HBM.
+ */
+#ifndef OTR_H
+#define OTR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (HTTP codes of reporter_service.py:209-245 are kept) ---- */
+#define OTR_OK 0
+#define OTR_BAD_REQUEST 400   /* reporter_service.py:214,219,225,231,235 */
+#define OTR_MATCH_ERROR 500   /* reporter_service.py:244-245 */
+#define OTR_NOT_CONFIGURED 503
+#define OTR_DEVICE_ERROR 504
+
+typedef struct otr_matcher otr_matcher;
+
+/* Replaces valhalla.Configure(conf_path) (reporter_service.py:284, simple_reporter.py:132).
+ * Reads a Valhalla-style JSON config: {"meili": {"default": {...}, "auto": {...}, ...},
+ * "otr": {"graph": "<flattened graph file>", "device": 0}} (meili values:
+ * Dockerfile:14-17,42-49).  Loads the graph once and uploads it to HBM.  Returns
+ * OTR_OK or an error code; otr_last_error() holds the message. */
+int otr_configure(const char* config_json_path);
+
+/* Same, with the config given as a JSON string (for embedders without files). */
+int otr_configure_json(const char* config_json, size_t len);
+
+/* Replaces valhalla.SegmentMatcher() (reporter_service.py:52, simple_reporter.py:133). */
+otr_matcher* otr_matcher_new(void);
+void otr_matcher_free(otr_matcher* m);
+
+/* Replaces SegmentMatcher.Match(json) -> str (reporter_service.py:240,
+ * simple_reporter.py:166): trace JSON in, {"segments":[...],"mode":...} out
+ * (schema README.md:288-300).  *out is owned by the library: release with otr_free.
+ * Returns OTR_OK, or an error code with *out = {"error":"..."}. */
+int otr_match(otr_matcher* m, const char* json, size_t len, char** out, size_t* out_len);
+
+/* Replaces the HTTP POST /report round trip (Batch.java:68 → reporter_service.py
+ * handle_request 209-245): request validation, Match, then report() with
+ * report_levels / transition_levels from match_options (reporter_service.py:228-235).
+ * Returns 200 with the report() JSON, or 400/500 with {"error":"..."} carrying the
+ * reference's messages.  threshold_sec < 0 selects THRESHOLD_SEC or 15
+ * (reporter_service.py:55-58). */
+int otr_report(otr_matcher* m, const char* json, size_t len, int threshold_sec, char** out, size_t* out_len);
+
+/* report() alone (reporter_service.py:79-179) over a Match() output string and the
+ * original trace JSON; for callers that already hold a match (simple_reporter.py:168). */
+int otr_report_segments(const char* match_json, size_t match_len, const char* trace_json, size_t trace_len,
+                        int threshold_sec, const int32_t* report_levels, int n_report_levels,
+                        const int32_t* transition_levels, int n_transition_levels, char** out, size_t* out_len);
+
+void otr_free(char* p);
+const char* otr_last_error(void);
+
+/* ---- batched throughput API (new; the reference matches one trace per call) ---- */
+
+#define OTR_MEM_HOST 0
+#define OTR_MEM_DEVICE 1
+
+typedef struct otr_trace_batch {
+  int32_t n_traces;
+  int32_t memory;              /* OTR_MEM_HOST or OTR_MEM_DEVICE (pointers in HBM) */
+  const int64_t* trace_offsets;  /* n_traces+1 probe offsets */
+  const double* lat;
+  const double* lon;
+  const int64_t* time;         /* epoch seconds */
+  const float* accuracy;       /* metres, NULL or <0 entries = not given */
+  const uint8_t* mode;         /* per trace: 0 auto, 1 bicycle, 2 pedestrian */
+  uint32_t report_levels;      /* bit mask of OSMLR levels, simple_reporter --report-levels */
+  uint32_t transition_levels;  /* bit mask, --transition-levels */
+  int32_t threshold_sec;       /* report() tail threshold, 15 */
+  int32_t quantisation;        /* hour bucket seconds, 3600 (simple_reporter.py:343) */
+  int64_t hist_base_time;      /* histogram covers [base, base + hist_hours*quantisation) */
+  int32_t hist_hours;
+  int32_t flags;               /* OTR_BATCH_* */
+} otr_trace_batch;
+
+#define OTR_BATCH_COPY_OUT 1   /* fill the host arrays of otr_batch_result */
+#define OTR_BATCH_TIMING 2     /* record per-kernel HIP-event timings */
+
+#define OTR_NO_ID 0xFFFFFFFFFFFFFFFFull
+#define OTR_HIST_BINS 8        /* speed bins of 20 km/h: [0,20) … [140,∞) */
+
+/* All pointers below are owned by the matcher and stay valid until the next batch
+ * call or otr_matcher_free.  Host arrays are filled only with OTR_BATCH_COPY_OUT;
+ * the device histogram is always produced. */
+typedef struct otr_batch_result {
+  int32_t n_traces;
+  int64_t n_probes;
+  int64_t n_states;
+  int64_t n_route;
+  int64_t n_seg;
+  int64_t n_rep;
+  int64_t n_rows;              /* simple_reporter tile rows (after filter + hour fan-out) */
+  int32_t status;              /* OTR_OK or first error */
+  int32_t n_overflow_traces;   /* traces whose search exceeded the largest LDS table */
+  /* host copies (OTR_BATCH_COPY_OUT) — same layout as oracle/oracle.h orc_result */
+  int64_t* trace_state_off;  int64_t* state_probe;  int32_t* cand_count;
+  uint32_t* cand_edge;  double* cand_p;  double* cand_sqd;   /* n_states * 64 slots */
+  int32_t* winner;  int32_t* subpath;
+  int64_t* trace_route_off;  uint32_t* route_edge;
+  int64_t* trace_seg_off;  uint64_t* seg_id;  double* seg_start;  double* seg_end;
+  int32_t* seg_length;  int32_t* seg_queue;  uint8_t* seg_internal;
+  int32_t* seg_begin_shape;  int32_t* seg_end_shape;  int64_t* seg_way_off;  uint32_t* seg_way;
+  int64_t* trace_rep_off;  uint64_t* rep_id;  uint64_t* rep_next;  double* rep_t0;  double* rep_t1;
+  int32_t* rep_length;  int32_t* rep_queue;  int32_t* shape_used;  int32_t* stats;  double* stats_len;
+  /* device outputs */
+  uint32_t* d_hist;            /* [hist_hours][n_segments][OTR_HIST_BINS] observation counts */
+  int64_t hist_len;            /* elements */
+  /* algorithmic byte counters, summed over the batch */
+  uint64_t counters[8];        /* 0 cells visited, 1 segment tests, 2 candidates, 3 settled nodes,
+                                  4 relaxed edges, 5 route tasks, 6 viterbi cells, 7 output segments */
+  float kernel_ms[16];         /* OTR_BATCH_TIMING: per-stage device time */
+} otr_batch_result;
+
+int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result* out);
+
+/* graph facts for callers sizing histograms */
+int otr_graph_info(int64_t* n_nodes, int64_t* n_edges, int64_t* n_segments);
+
+/* device + stream the matcher runs on (hipStream_t as void*), for callers that
+ * place inputs in HBM themselves and bracket timing */
+void* otr_matcher_stream(otr_matcher* m);
+int otr_device(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

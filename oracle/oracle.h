@@ -1,0 +1,131 @@
+/*
+ * oracle.h — CPU restatement of the reference's map-matching hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load liboracle.so, and only as the checker / the timed CPU
+ * baseline.  The product (libotr.so) never links or calls it.
+ *
+ * What it restates (file:line in /root/reference unless UPSTREAM):
+ *   - trace request semantics: reporter_service.py:184-245, simple_reporter.py:136-168
+ *   - the matcher, Valhalla meili 2.3.6 (UPSTREAM, NOT present in this container,
+ *     PPA pin Dockerfile:7,29-32): candidate search, emission, bounded one-to-many
+ *     routing, transition, Viterbi, route construction, OSMLR segment formation
+ *     (output schema README.md:269-302).  PARITY WITH MEILI IS UNPINNED: no meili
+ *     source, binary, tile or golden output exists here or in the reference's tests
+ *     (SURVEY.md §8c).  This file is the written-down algorithm the HIP path must
+ *     match bit-exactly; DESIGN.md §3 lists every rule re-derived here.
+ *   - report(): reporter_service.py:79-179 (pinned by tests/golden/report_cases.json)
+ *   - filter + hour bucketing: simple_reporter.py:176-196 (tests/golden/bucket_cases.json)
+ *   - privacy cull: simple_reporter.py:218-239 (tests/golden/cull_cases.json)
+ */
+#ifndef OTR_ORACLE_H
+#define OTR_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORC_KMAX 64
+#define ORC_INVALID_SEGMENT_ID 0x3fffffffffffull /* simple_reporter.py:43 */
+#define ORC_NO_ID 0xFFFFFFFFFFFFFFFFull
+
+typedef struct orc_params {
+  double sigma_z;                    /* 4.07  Dockerfile:14 */
+  double beta;                       /* 3     Dockerfile:15 */
+  double max_route_distance_factor;  /* 5     Dockerfile:16 */
+  double max_route_time_factor;      /* 2     Dockerfile:17 (not applied) */
+  double breakage_distance;          /* 2000  generate_test_trace.py:48 */
+  double interpolation_distance;     /* 10 */
+  double search_radius;              /* 50    generate_test_trace.py:51 */
+  double max_search_radius;          /* 100 */
+  double gps_accuracy;               /* 5 */
+  double turn_penalty_factor;        /* 0     generate_test_trace.py:47 */
+  int32_t max_candidates;            /* <= ORC_KMAX */
+  int32_t threshold_sec;             /* 15    reporter_service.py:55 */
+} orc_params;
+
+typedef struct orc_graph orc_graph;
+
+orc_graph* orc_graph_load(const char* path);
+void orc_graph_free(orc_graph* g);
+
+/* One batch of traces in, everything the parity tests compare out.  All output
+ * arrays are malloc'd by the oracle and released with orc_result_free. */
+typedef struct orc_result {
+  int32_t n_traces;
+  /* states (selected probes), concatenated over traces */
+  int64_t n_states;
+  int64_t* trace_state_off;   /* n_traces+1 */
+  int64_t* state_probe;       /* global probe index */
+  int32_t* cand_count;        /* n_states */
+  uint32_t* cand_edge;        /* n_states*ORC_KMAX */
+  double* cand_p;             /* fraction along edge */
+  double* cand_sqd;           /* squared snap distance, m^2 */
+  int32_t* winner;            /* n_states; -1 = no candidate / not matched */
+  int32_t* subpath;           /* n_states; sub-path ordinal within trace, -1 if none */
+  /* matched route: edges per trace; a 0xFFFFFFFF entry separates sub-paths */
+  int64_t* trace_route_off;   /* n_traces+1 */
+  uint32_t* route_edge;
+  int64_t n_route;
+  /* traffic segments (README.md:288-300) */
+  int64_t* trace_seg_off;     /* n_traces+1 */
+  int64_t n_seg;
+  uint64_t* seg_id;           /* ORC_NO_ID when absent */
+  double* seg_start;
+  double* seg_end;
+  int32_t* seg_length;
+  int32_t* seg_queue;
+  uint8_t* seg_internal;
+  int32_t* seg_begin_shape;
+  int32_t* seg_end_shape;
+  int64_t* seg_way_off;       /* n_seg+1 */
+  uint32_t* seg_way;
+  /* report() output per trace */
+  int64_t* trace_rep_off;     /* n_traces+1 */
+  int64_t n_rep;
+  uint64_t* rep_id;
+  uint64_t* rep_next;         /* ORC_NO_ID when next_id absent */
+  double* rep_t0;
+  double* rep_t1;
+  int32_t* rep_length;
+  int32_t* rep_queue;
+  int32_t* shape_used;        /* per trace, -1 = absent */
+  int32_t* stats;             /* per trace 7 counts: successful, unreported, discontinuities,
+                                 invalid_speeds, invalid_times, unassociated, (pad) */
+  double* stats_len;          /* per trace 2: successful_length, unreported_length */
+} orc_result;
+
+/* lat/lon/time/accuracy are per probe, trace_off has n_traces+1 entries,
+ * accuracy < 0 means "not given"; mode[t]: 0 auto, 1 bicycle, 2 pedestrian. */
+int orc_match_batch(const orc_graph* g, const orc_params* p, int32_t n_traces, const int64_t* trace_off,
+                    const double* lat, const double* lon, const int64_t* time, const float* accuracy,
+                    const uint8_t* mode, uint32_t report_levels_mask, uint32_t transition_levels_mask,
+                    int32_t n_threads, orc_result* out);
+void orc_result_free(orc_result* r);
+
+/* report() alone over explicit segment arrays (pinned by golden vectors).
+ * seg_has_id/has_length flags model Python's None. */
+typedef struct orc_report_out {
+  int32_t n_rep;
+  int32_t shape_used;          /* -1 = key absent */
+  int32_t counts[6];
+  double lengths[2];
+  int32_t length_set[2];       /* 0 => the Python int 0 was never replaced */
+} orc_report_out;
+
+int orc_report(int32_t n, const uint8_t* has_id, const uint64_t* seg_id, const double* start,
+               const double* end, const uint8_t* internal, const int32_t* queue, const uint8_t* has_length,
+               const int32_t* length, const int32_t* begin_shape, int64_t trace_end_time, double threshold,
+               uint32_t report_levels_mask, uint32_t transition_levels_mask, uint64_t* rep_id, uint64_t* rep_next,
+               double* rep_t0, double* rep_t1, int32_t* rep_length, int32_t* rep_queue, orc_report_out* out);
+
+/* per-trace routing query used by the transition-parity tests */
+int orc_route_dist(const orc_graph* g, uint32_t src_edge, double src_p, uint32_t dst_edge, double dst_p,
+                   double bound, uint32_t mode_bit, double* out_dist);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,96 @@
+"""Builds every native artefact in-tree (no JIT cache, so the .so files travel to the GPU box).
+
+  reporter_amd/libotr.so            product: HIP kernels (gfx950) + C-ABI (include/otr.h)
+  reporter_amd/tools/libotrgen.so   workload generator (bench/test infrastructure)
+  oracle/liboracle.so               CPU oracle (test infrastructure, plain C)
+
+libotr.so links the HIP runtime that ships with the installed PyTorch when there is
+one, so that a Python process using torch.distributed and libotr shares ONE HIP
+runtime (two copies in one process would each own the device).
+"""
+import importlib.util
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, 'reporter_amd')
+CSRC = os.path.join(PKG, 'csrc')
+BUILD = os.path.join(ROOT, 'build', 'obj')
+ARCH = os.environ.get('OTR_OFFLOAD_ARCH', 'gfx950')
+HIPCC = shutil.which('hipcc') or '/opt/rocm/bin/hipcc'
+
+HIP_FLAGS = ['--offload-arch=' + ARCH, '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-fno-fast-math',
+             '-Wall', '-Wno-unused-function', '-Wno-unused-variable', '-Wno-unused-but-set-variable',
+             '-I' + os.path.join(ROOT, 'include')]
+
+
+def hip_runtime_dir():
+    spec = importlib.util.find_spec('torch')
+    if spec and spec.origin:
+        d = os.path.join(os.path.dirname(spec.origin), 'lib')
+        if os.path.exists(os.path.join(d, 'libamdhip64.so')):
+            return d, 'libamdhip64.so'
+    return '/opt/rocm/lib', 'libamdhip64.so.7'
+
+
+def _run(cmd, cwd=None):
+    r = subprocess.run(cmd, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout)
+        raise RuntimeError('build step failed: ' + ' '.join(cmd))
+    return r.stdout
+
+
+def _newer(target, sources):
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(s) <= t for s in sources)
+
+
+def build_otr(force=False):
+    os.makedirs(BUILD, exist_ok=True)
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
+    headers += [os.path.join(ROOT, 'include', f) for f in os.listdir(os.path.join(ROOT, 'include'))]
+    objs = []
+    for src in ('otr_engine.hip', 'otr_api.cpp'):
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, src + '.o')
+        objs.append(o)
+        if force or not _newer(o, [s] + headers):
+            lang = [] if src.endswith('.hip') else ['-x', 'hip']
+            _run([HIPCC] + HIP_FLAGS + lang + ['-c', s, '-o', o])
+    lib = os.path.join(PKG, 'libotr.so')
+    if force or not _newer(lib, objs):
+        rdir, rname = hip_runtime_dir()
+        _run(['g++', '-shared', '-o', lib] + objs +
+             ['-L' + rdir, '-l:' + rname, '-Wl,-rpath,' + rdir, '-Wl,--no-undefined', '-lpthread'])
+    return lib
+
+
+def build_gen(force=False):
+    src = os.path.join(PKG, 'tools', 'otrgen.cpp')
+    lib = os.path.join(PKG, 'tools', 'libotrgen.so')
+    if force or not _newer(lib, [src, os.path.join(ROOT, 'include', 'otr_graph_format.h')]):
+        _run(['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-o', lib, src])
+    return lib
+
+
+def build_oracle(force=False):
+    args = ['make', '-C', os.path.join(ROOT, 'oracle')]
+    if force:
+        args += ['-B']
+    _run(args)
+    return os.path.join(ROOT, 'oracle', 'liboracle.so')
+
+
+def build_all(force=False):
+    build_gen(force)
+    build_oracle(force)
+    return build_otr(force)
+
+
+if __name__ == '__main__':
+    print(build_all(force='--force' in sys.argv))

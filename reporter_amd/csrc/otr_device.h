@@ -1,0 +1,112 @@
+// otr_device.h — device-side views, parameters and deterministic geometry shared by
+// the HIP kernels (otr_kernels.hip) and the host engine (otr_engine.hip).
+//
+// Floating-point contract: everything on a decision path is IEEE
+// binary64 +,-,*,/,sqrt compiled with -ffp-contract=off, and cos() is the fixed
+// Taylor polynomial below, so the kernels reproduce the CPU oracle bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/otr_graph_format.h"
+
+#define OTR_KMAX 64          // candidate slots per state (lanes of one wave)
+#define OTR_MODES 3          // auto, bicycle, pedestrian
+#define OTR_WAVE 64
+
+namespace otr {
+
+constexpr double kMetersPerDeg = 20037581.187 / 180.0;  // Batch.java:36
+
+struct MatchParams {          // one per travel mode (meili.default + meili.<mode>)
+  double sigma_z;             // Dockerfile:14
+  double beta;                // Dockerfile:15
+  double max_route_distance_factor;  // Dockerfile:16
+  double breakage_distance;
+  double interpolation_distance;
+  double search_radius;
+  double max_search_radius;
+  double gps_accuracy;
+  double inv2s2;              // 1 / (sigma_z * sigma_z * 2)
+  double inv_beta;            // 1 / beta
+  int32_t kmax;               // max_candidates <= OTR_KMAX
+  int32_t pad;
+};
+
+struct ModeParams {
+  MatchParams m[OTR_MODES];
+  double delta;               // distance-bucket width of the routing search (metres)
+};
+
+struct DevGraph {
+  const uint32_t* node_row;
+  const uint32_t* rev_row;
+  const uint32_t* rev_edge;
+  const uint32_t* edge_src;
+  const uint32_t* edge_dst;
+  const float* edge_len;
+  const uint32_t* edge_attr;
+  const uint32_t* edge_shape;
+  const uint32_t* edge_seg;
+  const uint32_t* edge_way;
+  const int2* shape_ll;        // (lat_e6, lon_e6)
+  const unsigned long long* seg_id;
+  const uint32_t* seg_len;
+  const uint32_t* cell_row;
+  const uint32_t* cell_edge;
+  const uint4* edge_pack;      // {dst, len bits, attr, 0}: one 16-B load per relaxed edge
+  uint32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
+  double grid_min_lat, grid_min_lon, grid_cell_deg;
+};
+
+// cos of an angle in degrees, |deg| <= 90: Taylor series to x^22 (Horner).
+__host__ __device__ inline double cos_deg(double deg) {
+  double x = deg * (3.14159265358979323846 / 180.0);
+  double x2 = x * x;
+  double r = -1.0 / 1124000727777607680000.0;
+  r = r * x2 + 1.0 / 2432902008176640000.0;
+  r = r * x2 - 1.0 / 6402373705728000.0;
+  r = r * x2 + 1.0 / 20922789888000.0;
+  r = r * x2 - 1.0 / 87178291200.0;
+  r = r * x2 + 1.0 / 479001600.0;
+  r = r * x2 - 1.0 / 3628800.0;
+  r = r * x2 + 1.0 / 40320.0;
+  r = r * x2 - 1.0 / 720.0;
+  r = r * x2 + 1.0 / 24.0;
+  r = r * x2 - 1.0 / 2.0;
+  r = r * x2 + 1.0;
+  return r;
+}
+
+// equirectangular distance in metres (Batch.java:37-41, lat/lon in binary64)
+__host__ __device__ inline double gc_dist(double lat1, double lon1, double lat2, double lon2) {
+  double x = (lon1 - lon2) * kMetersPerDeg * cos_deg(0.5 * (lat1 + lat2));
+  double y = (lat1 - lat2) * kMetersPerDeg;
+  return sqrt(x * x + y * y);
+}
+
+__host__ __device__ inline double e6(int32_t v) { return (double)v * 1e-6; }
+
+// route bound B = min(breakage, factor * max(g, interpolation_distance))  
+__host__ __device__ inline double route_bound(const MatchParams& p, double g) {
+  double gf = g > p.interpolation_distance ? g : p.interpolation_distance;
+  double b = p.max_route_distance_factor * gf;
+  return b > p.breakage_distance ? p.breakage_distance : b;
+}
+
+__device__ inline uint32_t hmix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ inline int lane_id() { return (int)__lane_id(); }
+
+__device__ inline int prefix_count(unsigned long long mask) {
+  return __popcll(mask & ((1ull << lane_id()) - 1ull));
+}
+
+}  // namespace otr

@@ -1,0 +1,65 @@
+// otr_engine.h — host-side engine: HBM graph replica, per-matcher workspace and the
+// batched pipeline (K0..K8).  Internal C++ interface between otr_engine.hip and the
+// C-ABI in otr_api.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/otr.h"
+#include "otr_device.h"
+
+namespace otr {
+
+struct Config {
+  ModeParams mp;
+  std::string graph_path;
+  int device = 0;
+};
+
+ModeParams default_mode_params();
+void finalize_params(MatchParams* p);
+
+// The configured graph, resident in HBM (one replica per process/GPU).
+struct GraphState {
+  bool ready = false;
+  int device = 0;
+  DevGraph dg{};
+  ModeParams defaults{};
+  std::vector<void*> allocs;
+  uint64_t n_nodes = 0, n_edges = 0, n_segments = 0;
+  // host copy of the few arrays the JSON path needs
+  std::vector<unsigned long long> seg_id;
+};
+
+GraphState& graph_state();
+int engine_configure(const Config& cfg, std::string* err);
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct Matcher {
+  hipStream_t stream = nullptr;
+  std::vector<DevBuf> bufs;
+  // host result storage (OTR_BATCH_COPY_OUT)
+  std::vector<int64_t> h_trace_state_off, h_state_probe, h_trace_route_off, h_trace_seg_off, h_seg_way_off,
+      h_trace_rep_off;
+  std::vector<int32_t> h_cand_count, h_winner, h_subpath, h_seg_length, h_seg_queue, h_seg_bshape, h_seg_eshape,
+      h_rep_length, h_rep_queue, h_shape_used, h_stats;
+  std::vector<uint32_t> h_cand_edge, h_route_edge, h_seg_way;
+  std::vector<double> h_cand_p, h_cand_sqd, h_seg_start, h_seg_end, h_rep_t0, h_rep_t1, h_stats_len;
+  std::vector<unsigned long long> h_seg_id, h_rep_id, h_rep_next;
+  std::vector<uint8_t> h_seg_internal;
+  hipEvent_t ev[20];
+  bool ev_init = false;
+
+  template <class T>
+  T* need(int slot, size_t n);
+  int run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err);
+  ~Matcher();
+};
+
+}  // namespace otr

@@ -1,0 +1,703 @@
+// otr_engine.hip — graph upload (flattened CSR + grid → HBM) and the batched
+// matching pipeline on one HIP stream.  Kernels: otr_kernels.h.
+#include <hipcub/hipcub.hpp>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "otr_engine.h"
+#include "otr_kernels.h"
+
+namespace otr {
+
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      if (err) *err = std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x;    \
+      return OTR_DEVICE_ERROR;                                                           \
+    }                                                                                    \
+  } while (0)
+
+void finalize_params(MatchParams* p) {
+  p->inv2s2 = 1.0 / (p->sigma_z * p->sigma_z * 2.0);
+  p->inv_beta = 1.0 / p->beta;
+  if (p->kmax > OTR_KMAX) p->kmax = OTR_KMAX;
+  if (p->kmax < 1) p->kmax = 1;
+}
+
+ModeParams default_mode_params() {
+  ModeParams mp{};
+  for (int m = 0; m < OTR_MODES; ++m) {
+    MatchParams& p = mp.m[m];
+    p.sigma_z = 4.07;                   // Dockerfile:14
+    p.beta = 3.0;                       // Dockerfile:15
+    p.max_route_distance_factor = 5.0;  // Dockerfile:16
+    p.breakage_distance = 2000.0;
+    p.interpolation_distance = 10.0;
+    p.search_radius = 50.0;
+    p.max_search_radius = 100.0;
+    p.gps_accuracy = 5.0;
+    p.kmax = 32;
+    finalize_params(&p);
+  }
+  mp.delta = 100.0;
+  return mp;
+}
+
+GraphState& graph_state() {
+  static GraphState gs;
+  return gs;
+}
+
+int engine_configure(const Config& cfg, std::string* err) {
+  GraphState& gs = graph_state();
+  int fd = open(cfg.graph_path.c_str(), O_RDONLY);
+  if (fd < 0) {
+    if (err) *err = "cannot open graph file " + cfg.graph_path + ": " + strerror(errno);
+    return OTR_BAD_REQUEST;
+  }
+  struct stat st;
+  fstat(fd, &st);
+  void* map = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+  close(fd);
+  if (map == MAP_FAILED) {
+    if (err) *err = "cannot map graph file";
+    return OTR_BAD_REQUEST;
+  }
+  const char* base = (const char*)map;
+  otr_graph_header h;
+  memcpy(&h, base, sizeof(h));
+  if (memcmp(h.magic, OTR_GRAPH_MAGIC, 8) != 0 || h.version != OTR_GRAPH_VERSION ||
+      h.array_offset[OTR_A_END] > (uint64_t)st.st_size) {
+    munmap(map, (size_t)st.st_size);
+    if (err) *err = "not an OTR graph file: " + cfg.graph_path;
+    return OTR_BAD_REQUEST;
+  }
+  HIPCHK(hipSetDevice(cfg.device));
+  for (void* p : gs.allocs) (void)hipFree(p);
+  gs.allocs.clear();
+  auto up = [&](int a, size_t bytes) -> void* {
+    void* d = nullptr;
+    if (hipMalloc(&d, bytes ? bytes : 16) != hipSuccess) return nullptr;
+    if (bytes) (void)hipMemcpy(d, base + h.array_offset[a], bytes, hipMemcpyHostToDevice);
+    gs.allocs.push_back(d);
+    return d;
+  };
+  DevGraph& g = gs.dg;
+  g.node_row = (const uint32_t*)up(OTR_A_NODE_ROW, 4ull * (h.n_nodes + 1));
+  g.rev_row = (const uint32_t*)up(OTR_A_REV_ROW, 4ull * (h.n_nodes + 1));
+  g.rev_edge = (const uint32_t*)up(OTR_A_REV_EDGE, 4ull * h.n_edges);
+  g.edge_src = (const uint32_t*)up(OTR_A_EDGE_SRC, 4ull * h.n_edges);
+  g.edge_dst = (const uint32_t*)up(OTR_A_EDGE_DST, 4ull * h.n_edges);
+  g.edge_len = (const float*)up(OTR_A_EDGE_LEN, 4ull * h.n_edges);
+  g.edge_attr = (const uint32_t*)up(OTR_A_EDGE_ATTR, 4ull * h.n_edges);
+  g.edge_shape = (const uint32_t*)up(OTR_A_EDGE_SHAPE, 4ull * (h.n_edges + 1));
+  g.edge_seg = (const uint32_t*)up(OTR_A_EDGE_SEG, 4ull * h.n_edges);
+  g.edge_way = (const uint32_t*)up(OTR_A_EDGE_WAY, 4ull * h.n_edges);
+  g.shape_ll = (const int2*)up(OTR_A_SHAPE_LL, 8ull * h.n_shape);
+  g.seg_id = (const unsigned long long*)up(OTR_A_SEG_ID, 8ull * h.n_segments);
+  g.seg_len = (const uint32_t*)up(OTR_A_SEG_LEN, 4ull * h.n_segments);
+  g.cell_row = (const uint32_t*)up(OTR_A_CELL_ROW, 4ull * (h.n_cells + 1));
+  g.cell_edge = (const uint32_t*)up(OTR_A_CELL_EDGE, 4ull * h.n_cell_entries);
+  // routing view: {dst, len bits, attr, 0} per edge, one dwordx4 per relaxation
+  {
+    std::vector<uint4> pack(h.n_edges);
+    const uint32_t* dst = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_DST]);
+    const uint32_t* len = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_LEN]);
+    const uint32_t* attr = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_ATTR]);
+    for (uint32_t e = 0; e < h.n_edges; ++e) pack[e] = make_uint4(dst[e], len[e], attr[e], 0u);
+    void* d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(uint4) * (pack.size() + 1)));
+    gs.allocs.push_back(d);
+    HIPCHK(hipMemcpy(d, pack.data(), sizeof(uint4) * pack.size(), hipMemcpyHostToDevice));
+    g.edge_pack = (const uint4*)d;
+  }
+  for (void* p : gs.allocs)
+    if (!p) {
+      munmap(map, (size_t)st.st_size);
+      if (err) *err = "device allocation for the graph failed";
+      return OTR_DEVICE_ERROR;
+    }
+  g.n_nodes = h.n_nodes;
+  g.n_edges = h.n_edges;
+  g.n_segments = h.n_segments;
+  g.grid_rows = h.grid_rows;
+  g.grid_cols = h.grid_cols;
+  g.grid_min_lat = h.grid_min_lat;
+  g.grid_min_lon = h.grid_min_lon;
+  g.grid_cell_deg = h.grid_cell_deg;
+  gs.n_nodes = h.n_nodes;
+  gs.n_edges = h.n_edges;
+  gs.n_segments = h.n_segments;
+  gs.seg_id.assign((const unsigned long long*)(base + h.array_offset[OTR_A_SEG_ID]),
+                   (const unsigned long long*)(base + h.array_offset[OTR_A_SEG_ID]) + h.n_segments);
+  munmap(map, (size_t)st.st_size);
+  gs.defaults = cfg.mp;
+  gs.device = cfg.device;
+  gs.ready = true;
+  return OTR_OK;
+}
+
+// ---------------------------------------------------------------------------------
+// workspace slots
+// ---------------------------------------------------------------------------------
+enum Slot {
+  S_TRACE_OFF, S_LAT, S_LON, S_TIME, S_ACC, S_MODE,
+  S_STATE_CNT, S_TRACE_STATE_OFF, S_STATE_PROBE, S_STATE_TRACE,
+  S_CAND_EDGE, S_CAND_P, S_CAND_SQD, S_CAND_COUNT,
+  S_PREV, S_G, S_BOUND, S_FORCED, S_NTASK, S_NTRANS, S_TASK_OFF, S_TRANS_OFF,
+  S_TASK_STATE, S_TASK_SRC, S_TASK_OVF, S_TRANS,
+  S_BP, S_BRK, S_END_WIN, S_WINNER, S_SUBPATH,
+  S_PATH_OFF, S_PATH_LEN, S_PATH, S_STEP_OVF,
+  S_CAP, S_CAP_OFF, S_POS, S_ACT,
+  S_ROUTE, S_ROUTE_N, S_SEG_ID, S_SEG_START, S_SEG_END, S_SEG_LEN, S_SEG_QUEUE, S_SEG_INTERNAL,
+  S_SEG_BSHAPE, S_SEG_ESHAPE, S_SEG_INDEX, S_SEG_N, S_SEG_WAY_N, S_SEG_WAY, S_WAY_N,
+  S_REP_ID, S_REP_NEXT, S_REP_T0, S_REP_T1, S_REP_LEN, S_REP_QUEUE, S_REP_SEG, S_REP_N,
+  S_SHAPE_USED, S_STATS, S_STATS_LEN, S_HIST, S_COUNTERS, S_SCAN_TMP, S_LIST, S_MISC,
+  S_NUM
+};
+
+template <class T>
+T* Matcher::need(int slot, size_t n) {
+  if ((int)bufs.size() < S_NUM) bufs.resize(S_NUM);
+  DevBuf& b = bufs[slot];
+  size_t bytes = (n ? n : 1) * sizeof(T);
+  if (b.bytes < bytes) {
+    if (b.p) (void)hipFree(b.p);
+    size_t nb = bytes + bytes / 4;
+    if (hipMalloc(&b.p, nb) != hipSuccess) {
+      b.p = nullptr;
+      b.bytes = 0;
+      return nullptr;
+    }
+    b.bytes = nb;
+  }
+  return (T*)b.p;
+}
+
+Matcher::~Matcher() {
+  for (auto& b : bufs)
+    if (b.p) (void)hipFree(b.p);
+  if (ev_init)
+    for (auto& e : ev) (void)hipEventDestroy(e);
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+// per-trace output capacity: route/segment/way/report slots
+__global__ void k_capacity(int32_t n_traces, const int64_t* trace_state_off, const int32_t* cand_count,
+                           const int32_t* path_len, int64_t* cap) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_traces) return;
+  int64_t c = 2;
+  for (int64_t s = trace_state_off[t]; s < trace_state_off[t + 1]; ++s) {
+    if (cand_count[s] <= 0) continue;
+    c += 3;
+    if (path_len[s] > 0) c += path_len[s];
+  }
+  cap[t] = c;
+}
+
+__global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+__global__ void k_collect(int64_t n, const int32_t* flag, int64_t* list, unsigned long long* count) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && flag[i]) list[atomicAdd(count, 1ull)] = i;
+}
+
+// states that need a path: a step inside a sub-path
+__global__ void k_step_list(int64_t n_states, const int64_t* prev, const uint8_t* brk, const int32_t* cand_count,
+                            int64_t* list, unsigned long long* count) {
+  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n_states && cand_count[s] > 0 && prev[s] >= 0 && !brk[s]) list[atomicAdd(count, 1ull)] = s;
+}
+
+static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+
+int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err) {
+  GraphState& gs = graph_state();
+  if (!gs.ready) {
+    if (err) *err = "otr_configure has not been called";
+    return OTR_NOT_CONFIGURED;
+  }
+  HIPCHK(hipSetDevice(gs.device));
+  if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  if (!ev_init) {
+    for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+    ev_init = true;
+  }
+  const bool timing = (in->flags & OTR_BATCH_TIMING) != 0;
+  int evn = 0;
+  auto mark = [&]() {
+    if (timing && evn < 20) (void)hipEventRecord(ev[evn++], stream);
+  };
+  memset(out, 0, sizeof(*out));
+  const int32_t T = in->n_traces;
+  out->n_traces = T;
+  if (T <= 0) return OTR_OK;
+  const DevGraph& g = gs.dg;
+  BatchDev b{};
+  b.n_traces = T;
+  int64_t N = 0;
+  if (in->memory == OTR_MEM_HOST) {
+    N = in->trace_offsets[T];
+    int64_t* d_off = need<int64_t>(S_TRACE_OFF, T + 1);
+    double* d_lat = need<double>(S_LAT, N);
+    double* d_lon = need<double>(S_LON, N);
+    int64_t* d_time = need<int64_t>(S_TIME, N);
+    uint8_t* d_mode = need<uint8_t>(S_MODE, T);
+    float* d_acc = in->accuracy ? need<float>(S_ACC, N) : nullptr;
+    if (!d_off || !d_lat || !d_lon || !d_time || !d_mode || (in->accuracy && !d_acc)) {
+      if (err) *err = "device allocation failed";
+      return OTR_DEVICE_ERROR;
+    }
+    HIPCHK(hipMemcpyAsync(d_off, in->trace_offsets, 8 * (T + 1), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_lat, in->lat, 8 * N, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_lon, in->lon, 8 * N, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_time, in->time, 8 * N, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_mode, in->mode, T, hipMemcpyHostToDevice, stream));
+    if (d_acc) HIPCHK(hipMemcpyAsync(d_acc, in->accuracy, 4 * N, hipMemcpyHostToDevice, stream));
+    b.trace_off = d_off;
+    b.lat = d_lat;
+    b.lon = d_lon;
+    b.time = d_time;
+    b.mode = d_mode;
+    b.acc = d_acc;
+  } else {
+    HIPCHK(hipMemcpyAsync(&N, in->trace_offsets + T, 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    b.trace_off = in->trace_offsets;
+    b.lat = in->lat;
+    b.lon = in->lon;
+    b.time = in->time;
+    b.mode = in->mode;
+    b.acc = in->accuracy;
+  }
+  out->n_probes = N;
+  unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, 16);
+  HIPCHK(hipMemsetAsync(d_counters, 0, 16 * 8, stream));
+  size_t scan_bytes = 0;
+  auto scan = [&](const int64_t* src, int64_t* dst_np1, int64_t n) -> int {
+    // dst[0] = 0, dst[1..n] = inclusive prefix sums
+    HIPCHK(hipMemsetAsync(dst_np1, 0, 8, stream));
+    if (n == 0) return OTR_OK;
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, src, dst_np1 + 1, (int)n, stream));
+    void* tmp = need<char>(S_SCAN_TMP, tb > scan_bytes ? tb : scan_bytes);
+    scan_bytes = scan_bytes > tb ? scan_bytes : tb;
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, src, dst_np1 + 1, (int)n, stream));
+    return OTR_OK;
+  };
+  auto read_i64 = [&](const int64_t* p, int64_t* v) -> int {
+    HIPCHK(hipMemcpyAsync(v, p, 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    return OTR_OK;
+  };
+  int rc;
+  mark();  // 0
+  // ---- K0: states
+  int64_t* state_cnt = need<int64_t>(S_STATE_CNT, T);
+  int64_t* trace_state_off = need<int64_t>(S_TRACE_STATE_OFF, T + 1);
+  k_select_states<<<grid_for(T, 256), 256, 0, stream>>>(b, mp, state_cnt, nullptr, nullptr, nullptr);
+  if ((rc = scan(state_cnt, trace_state_off, T))) return rc;
+  int64_t S = 0;
+  if ((rc = read_i64(trace_state_off + T, &S))) return rc;
+  out->n_states = S;
+  int64_t* state_probe = need<int64_t>(S_STATE_PROBE, S);
+  int32_t* state_trace = need<int32_t>(S_STATE_TRACE, S);
+  k_select_states<<<grid_for(T, 256), 256, 0, stream>>>(b, mp, state_cnt, trace_state_off, state_probe,
+                                                        state_trace);
+  mark();  // 1
+  // ---- K1: candidates
+  CandBuf cb;
+  cb.edge = need<uint32_t>(S_CAND_EDGE, (size_t)S * OTR_KMAX);
+  cb.p = need<double>(S_CAND_P, (size_t)S * OTR_KMAX);
+  cb.sqd = need<double>(S_CAND_SQD, (size_t)S * OTR_KMAX);
+  cb.count = need<int32_t>(S_CAND_COUNT, S);
+  if (!cb.edge || !cb.p || !cb.sqd || !cb.count) {
+    if (err) *err = "device allocation failed (candidates)";
+    return OTR_DEVICE_ERROR;
+  }
+  if (S > 0) {
+    unsigned gridc = (unsigned)(S < 1048576 ? S : 1048576);
+    k_candidates<<<gridc, 64, 0, stream>>>(g, b, mp, S, state_probe, state_trace, cb, d_counters);
+  }
+  mark();  // 2
+  // ---- K_link + task map
+  StepBuf sb;
+  sb.prev = need<int64_t>(S_PREV, S);
+  sb.g = need<double>(S_G, S);
+  sb.bound = need<double>(S_BOUND, S);
+  sb.forced = need<uint8_t>(S_FORCED, S);
+  sb.ntask = need<int64_t>(S_NTASK, S);
+  sb.ntrans = need<int64_t>(S_NTRANS, S);
+  int64_t* task_off = need<int64_t>(S_TASK_OFF, S + 1);
+  int64_t* trans_off = need<int64_t>(S_TRANS_OFF, S + 1);
+  k_link<<<grid_for(T, 256), 256, 0, stream>>>(b, mp, trace_state_off, state_probe, cb.count, sb);
+  if ((rc = scan(sb.ntask, task_off, S))) return rc;
+  if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
+  int64_t NT = 0, NTR = 0;
+  if ((rc = read_i64(task_off + S, &NT))) return rc;
+  if ((rc = read_i64(trans_off + S, &NTR))) return rc;
+  int64_t* task_state = need<int64_t>(S_TASK_STATE, NT);
+  int32_t* task_src = need<int32_t>(S_TASK_SRC, NT);
+  int32_t* task_ovf = need<int32_t>(S_TASK_OVF, NT);
+  double* trans = need<double>(S_TRANS, NTR);
+  if (!task_state || !task_src || !task_ovf || !trans) {
+    if (err) *err = "device allocation failed (transitions)";
+    return OTR_DEVICE_ERROR;
+  }
+  if (S > 0) k_taskmap<<<grid_for(S, 256), 256, 0, stream>>>(S, task_off, task_state, task_src);
+  if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
+  mark();  // 3
+  // ---- K3/K4: routing + transition costs
+  RouteArgs ra{};
+  ra.task_state = task_state;
+  ra.task_src = task_src;
+  ra.task_list = nullptr;
+  ra.n_tasks = NT;
+  ra.prev = sb.prev;
+  ra.g = sb.g;
+  ra.bound = sb.bound;
+  ra.forced = sb.forced;
+  ra.trans_off = trans_off;
+  ra.trans = trans;
+  ra.cand_count = cb.count;
+  ra.cand_edge = cb.edge;
+  ra.cand_p = cb.p;
+  ra.state_trace = state_trace;
+  ra.mode = b.mode;
+  ra.delta = mp.delta;
+  for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
+  ra.overflow_flag = task_ovf;
+  if (NT > 0) {
+    unsigned gr = (unsigned)(NT < 4194304 ? NT : 4194304);
+    k_route<512><<<gr, 64, 0, stream>>>(g, ra, d_counters);
+    // overflow retry with the large table
+    int64_t* list = need<int64_t>(S_LIST, NT);
+    unsigned long long* cnt = need<unsigned long long>(S_MISC, 4);
+    HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
+    k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
+    unsigned long long novf = 0;
+    HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    if (novf > 0) {
+      HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
+      RouteArgs rb = ra;
+      rb.task_list = list;
+      rb.n_tasks = (int64_t)novf;
+      k_route<8192><<<(unsigned)(novf < 65536 ? novf : 65536), 64, 0, stream>>>(g, rb, d_counters);
+      HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
+      k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
+      HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      out->n_overflow_traces += (int32_t)novf;
+    }
+  }
+  mark();  // 4
+  // ---- K5: Viterbi
+  ViterbiArgs va{};
+  va.n_traces = T;
+  va.trace_state_off = trace_state_off;
+  va.cand_count = cb.count;
+  va.cand_sqd = cb.sqd;
+  va.prev = sb.prev;
+  va.trans_off = trans_off;
+  va.trans = trans;
+  va.mode = b.mode;
+  for (int m = 0; m < OTR_MODES; ++m) va.inv2s2[m] = mp.m[m].inv2s2;
+  va.bp = need<int8_t>(S_BP, (size_t)S * OTR_KMAX);
+  va.brk = need<uint8_t>(S_BRK, S);
+  va.end_win = need<int32_t>(S_END_WIN, S);
+  va.winner = need<int32_t>(S_WINNER, S);
+  va.subpath = need<int32_t>(S_SUBPATH, S);
+  k_viterbi<<<(unsigned)(T < 1048576 ? T : 1048576), 64, 0, stream>>>(va, d_counters);
+  mark();  // 5
+  // ---- K6: winner paths
+  int64_t* path_off = need<int64_t>(S_PATH_OFF, S);
+  int32_t* path_len = need<int32_t>(S_PATH_LEN, S);
+  if (S > 0) k_fill_i32<<<grid_for(S, 256), 256, 0, stream>>>(path_len, S, 0);
+  {
+    int64_t* steps = need<int64_t>(S_LIST, S > NT ? S : NT);
+    unsigned long long* cnt = need<unsigned long long>(S_MISC, 4);
+    HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
+    if (S > 0) k_step_list<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, cnt);
+    unsigned long long nsteps = 0;
+    HIPCHK(hipMemcpyAsync(&nsteps, cnt, 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    int64_t capacity = (int64_t)nsteps * 24 + 1024;
+    for (int attempt = 0; attempt < 4 && nsteps > 0; ++attempt) {
+      uint32_t* path = need<uint32_t>(S_PATH, capacity);
+      int32_t* step_ovf = need<int32_t>(S_STEP_OVF, nsteps + 1);
+      if (!path || !step_ovf) {
+        if (err) *err = "device allocation failed (paths)";
+        return OTR_DEVICE_ERROR;
+      }
+      HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
+      HIPCHK(hipMemsetAsync(cnt + 1, 0, 16, stream));  // cursor, cap flag
+      PathArgs pa{};
+      pa.steps = steps;
+      pa.n_steps = (int64_t)nsteps;
+      pa.prev = sb.prev;
+      pa.bound = sb.bound;
+      pa.brk = va.brk;
+      pa.winner = va.winner;
+      pa.cand_edge = cb.edge;
+      pa.cand_p = cb.p;
+      pa.state_trace = state_trace;
+      pa.mode = b.mode;
+      pa.delta = mp.delta;
+      pa.path_off = path_off;
+      pa.path_len = path_len;
+      pa.path = path;
+      pa.cursor = cnt + 1;
+      pa.capacity = capacity;
+      pa.overflow_flag = step_ovf;
+      pa.cap_flag = (int32_t*)(cnt + 2);
+      k_paths<512><<<(unsigned)(nsteps < 4194304 ? nsteps : 4194304), 64, 0, stream>>>(g, pa, nullptr,
+                                                                                      (int64_t)nsteps);
+      // large-table retry for table overflows
+      int64_t* rl = need<int64_t>(S_TASK_STATE, NT > (int64_t)nsteps ? NT : (int64_t)nsteps);  // reuse
+      unsigned long long* c2 = cnt + 3;
+      HIPCHK(hipMemsetAsync(c2, 0, 8, stream));
+      k_collect<<<grid_for(nsteps, 256), 256, 0, stream>>>((int64_t)nsteps, step_ovf, rl, c2);
+      unsigned long long host[3] = {0, 0, 0};
+      HIPCHK(hipMemcpyAsync(host, cnt + 1, 24, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      if (host[2] > 0) {
+        HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
+        k_paths<8192><<<(unsigned)(host[2] < 65536 ? host[2] : 65536), 64, 0, stream>>>(g, pa, rl,
+                                                                                        (int64_t)host[2]);
+        HIPCHK(hipMemcpyAsync(host, cnt + 1, 16, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+      }
+      if ((int32_t)(host[1] & 0xFFFFFFFFu) == 0) break;  // cap flag clear: done
+      capacity = (int64_t)host[0] + (int64_t)host[0] / 2 + 1024;  // grow and redo
+    }
+  }
+  mark();  // 6
+  // ---- K7: stitching, segments, report()
+  int64_t* cap = need<int64_t>(S_CAP, T);
+  int64_t* cap_off = need<int64_t>(S_CAP_OFF, T + 1);
+  k_capacity<<<grid_for(T, 256), 256, 0, stream>>>(T, trace_state_off, cb.count, path_len, cap);
+  if ((rc = scan(cap, cap_off, T))) return rc;
+  int64_t C = 0;
+  if ((rc = read_i64(cap_off + T, &C))) return rc;
+  SegArgs sa{};
+  sa.b = b;
+  sa.trace_state_off = trace_state_off;
+  sa.state_probe = state_probe;
+  sa.cand_count = cb.count;
+  sa.cand_edge = cb.edge;
+  sa.cand_p = cb.p;
+  sa.prev = sb.prev;
+  sa.brk = va.brk;
+  sa.winner = va.winner;
+  sa.path_off = path_off;
+  sa.path_len = path_len;
+  sa.path = (const uint32_t*)need<uint32_t>(S_PATH, 1);
+  sa.pos = need<double>(S_POS, S);
+  sa.act = need<int64_t>(S_ACT, S);
+  sa.cap_off = cap_off;
+  sa.route = need<uint32_t>(S_ROUTE, C);
+  sa.route_n = need<int64_t>(S_ROUTE_N, T);
+  sa.seg_id = need<unsigned long long>(S_SEG_ID, C);
+  sa.seg_start = need<double>(S_SEG_START, C);
+  sa.seg_end = need<double>(S_SEG_END, C);
+  sa.seg_length = need<int32_t>(S_SEG_LEN, C);
+  sa.seg_queue = need<int32_t>(S_SEG_QUEUE, C);
+  sa.seg_internal = need<uint8_t>(S_SEG_INTERNAL, C);
+  sa.seg_bshape = need<int32_t>(S_SEG_BSHAPE, C);
+  sa.seg_eshape = need<int32_t>(S_SEG_ESHAPE, C);
+  sa.seg_index = need<uint32_t>(S_SEG_INDEX, C);
+  sa.seg_n = need<int64_t>(S_SEG_N, T);
+  sa.seg_way_n = need<int64_t>(S_SEG_WAY_N, C);
+  sa.seg_way = need<uint32_t>(S_SEG_WAY, C);
+  sa.way_n = need<int64_t>(S_WAY_N, T);
+  sa.rep_id = need<unsigned long long>(S_REP_ID, C);
+  sa.rep_next = need<unsigned long long>(S_REP_NEXT, C);
+  sa.rep_t0 = need<double>(S_REP_T0, C);
+  sa.rep_t1 = need<double>(S_REP_T1, C);
+  sa.rep_length = need<int32_t>(S_REP_LEN, C);
+  sa.rep_queue = need<int32_t>(S_REP_QUEUE, C);
+  sa.rep_seg = need<uint32_t>(S_REP_SEG, C);
+  sa.rep_n = need<int64_t>(S_REP_N, T);
+  sa.shape_used = need<int32_t>(S_SHAPE_USED, T);
+  sa.stats = need<int32_t>(S_STATS, 7 * (size_t)T);
+  sa.stats_len = need<double>(S_STATS_LEN, 2 * (size_t)T);
+  sa.threshold = (double)(in->threshold_sec >= 0 ? in->threshold_sec : 15);
+  sa.report_levels = in->report_levels;
+  sa.transition_levels = in->transition_levels;
+  k_segments<<<grid_for(T, 64), 64, 0, stream>>>(g, sa, d_counters);
+  mark();  // 7
+  // ---- K8: hour buckets → histogram
+  HistArgs ha{};
+  ha.b = b;
+  ha.cap_off = cap_off;
+  ha.rep_n = sa.rep_n;
+  ha.rep_id = sa.rep_id;
+  ha.rep_t0 = sa.rep_t0;
+  ha.rep_t1 = sa.rep_t1;
+  ha.rep_length = sa.rep_length;
+  ha.rep_queue = sa.rep_queue;
+  ha.rep_seg = sa.rep_seg;
+  ha.quantisation = in->quantisation > 0 ? in->quantisation : 3600;
+  ha.base_time = in->hist_base_time;
+  ha.hours = in->hist_hours;
+  ha.n_segments = g.n_segments;
+  ha.n_rows = d_counters + 8;
+  size_t hist_len = (size_t)(in->hist_hours > 0 ? in->hist_hours : 0) * g.n_segments * OTR_HIST_BINS;
+  ha.hist = hist_len ? need<uint32_t>(S_HIST, hist_len) : nullptr;
+  if (hist_len) HIPCHK(hipMemsetAsync(ha.hist, 0, hist_len * 4, stream));
+  k_histogram<<<grid_for(T, 256), 256, 0, stream>>>(ha);
+  mark();  // 8
+  HIPCHK(hipGetLastError());
+  unsigned long long hc[16];
+  HIPCHK(hipMemcpyAsync(hc, d_counters, sizeof(hc), hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  for (int k = 0; k < 8; ++k) out->counters[k] = hc[k];
+  out->counters[5] = (uint64_t)NT;
+  out->n_rows = (int64_t)hc[8];
+  out->d_hist = ha.hist;
+  out->hist_len = (int64_t)hist_len;
+  if (timing)
+    for (int k = 0; k + 1 < evn && k < 16; ++k) (void)hipEventElapsedTime(&out->kernel_ms[k], ev[k], ev[k + 1]);
+  // ---- copy-out (tests / JSON path), compacting the capacity layout
+  std::vector<int64_t> route_n(T), seg_n(T), way_n(T), rep_n(T), h_cap_off(T + 1);
+  HIPCHK(hipMemcpy(route_n.data(), sa.route_n, 8 * T, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(seg_n.data(), sa.seg_n, 8 * T, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(rep_n.data(), sa.rep_n, 8 * T, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(way_n.data(), sa.way_n, 8 * T, hipMemcpyDeviceToHost));
+  int64_t nroute = 0, nseg = 0, nrep = 0;
+  for (int t = 0; t < T; ++t) {
+    nroute += route_n[t];
+    nseg += seg_n[t];
+    nrep += rep_n[t];
+  }
+  out->n_route = nroute;
+  out->n_seg = nseg;
+  out->n_rep = nrep;
+  out->status = out->n_overflow_traces ? OTR_MATCH_ERROR : OTR_OK;
+  if (!(in->flags & OTR_BATCH_COPY_OUT)) return OTR_OK;
+  HIPCHK(hipMemcpy(h_cap_off.data(), cap_off, 8 * (T + 1), hipMemcpyDeviceToHost));
+  auto dl = [&](auto& vec, const void* src, size_t n) -> int {
+    vec.resize(n ? n : 1);
+    if (n) HIPCHK(hipMemcpy(vec.data(), src, n * sizeof(vec[0]), hipMemcpyDeviceToHost));
+    return OTR_OK;
+  };
+  if ((rc = dl(h_trace_state_off, trace_state_off, T + 1))) return rc;
+  if ((rc = dl(h_state_probe, state_probe, S))) return rc;
+  if ((rc = dl(h_cand_count, cb.count, S))) return rc;
+  if ((rc = dl(h_cand_edge, cb.edge, (size_t)S * OTR_KMAX))) return rc;
+  if ((rc = dl(h_cand_p, cb.p, (size_t)S * OTR_KMAX))) return rc;
+  if ((rc = dl(h_cand_sqd, cb.sqd, (size_t)S * OTR_KMAX))) return rc;
+  if ((rc = dl(h_winner, va.winner, S))) return rc;
+  if ((rc = dl(h_subpath, va.subpath, S))) return rc;
+  if ((rc = dl(h_shape_used, sa.shape_used, T))) return rc;
+  if ((rc = dl(h_stats, sa.stats, 7 * (size_t)T))) return rc;
+  if ((rc = dl(h_stats_len, sa.stats_len, 2 * (size_t)T))) return rc;
+  // capacity-layout arrays
+  std::vector<uint32_t> c_route, c_way, c_seg_index;
+  std::vector<unsigned long long> c_seg_id, c_rep_id, c_rep_next;
+  std::vector<double> c_ss, c_se, c_t0, c_t1;
+  std::vector<int32_t> c_sl, c_sq, c_sb, c_sx, c_rl, c_rq;
+  std::vector<uint8_t> c_si;
+  std::vector<int64_t> c_swn;
+  if ((rc = dl(c_route, sa.route, C))) return rc;
+  if ((rc = dl(c_way, sa.seg_way, C))) return rc;
+  if ((rc = dl(c_seg_id, sa.seg_id, C))) return rc;
+  if ((rc = dl(c_ss, sa.seg_start, C))) return rc;
+  if ((rc = dl(c_se, sa.seg_end, C))) return rc;
+  if ((rc = dl(c_sl, sa.seg_length, C))) return rc;
+  if ((rc = dl(c_sq, sa.seg_queue, C))) return rc;
+  if ((rc = dl(c_si, sa.seg_internal, C))) return rc;
+  if ((rc = dl(c_sb, sa.seg_bshape, C))) return rc;
+  if ((rc = dl(c_sx, sa.seg_eshape, C))) return rc;
+  if ((rc = dl(c_swn, sa.seg_way_n, C))) return rc;
+  if ((rc = dl(c_rep_id, sa.rep_id, C))) return rc;
+  if ((rc = dl(c_rep_next, sa.rep_next, C))) return rc;
+  if ((rc = dl(c_t0, sa.rep_t0, C))) return rc;
+  if ((rc = dl(c_t1, sa.rep_t1, C))) return rc;
+  if ((rc = dl(c_rl, sa.rep_length, C))) return rc;
+  if ((rc = dl(c_rq, sa.rep_queue, C))) return rc;
+  h_trace_route_off.assign(T + 1, 0);
+  h_trace_seg_off.assign(T + 1, 0);
+  h_trace_rep_off.assign(T + 1, 0);
+  h_route_edge.clear();
+  h_seg_id.clear(); h_seg_start.clear(); h_seg_end.clear(); h_seg_length.clear(); h_seg_queue.clear();
+  h_seg_internal.clear(); h_seg_bshape.clear(); h_seg_eshape.clear(); h_seg_way_off.assign(1, 0); h_seg_way.clear();
+  h_rep_id.clear(); h_rep_next.clear(); h_rep_t0.clear(); h_rep_t1.clear(); h_rep_length.clear();
+  h_rep_queue.clear();
+  for (int t = 0; t < T; ++t) {
+    const int64_t co = h_cap_off[t];
+    for (int64_t k = 0; k < route_n[t]; ++k) h_route_edge.push_back(c_route[co + k]);
+    int64_t wk = co;
+    for (int64_t k = 0; k < seg_n[t]; ++k) {
+      h_seg_id.push_back(c_seg_id[co + k]);
+      h_seg_start.push_back(c_ss[co + k]);
+      h_seg_end.push_back(c_se[co + k]);
+      h_seg_length.push_back(c_sl[co + k]);
+      h_seg_queue.push_back(c_sq[co + k]);
+      h_seg_internal.push_back(c_si[co + k]);
+      h_seg_bshape.push_back(c_sb[co + k]);
+      h_seg_eshape.push_back(c_sx[co + k]);
+      for (int64_t w = 0; w < c_swn[co + k]; ++w) h_seg_way.push_back(c_way[wk + w]);
+      wk += c_swn[co + k];
+      h_seg_way_off.push_back((int64_t)h_seg_way.size());
+    }
+    for (int64_t k = 0; k < rep_n[t]; ++k) {
+      h_rep_id.push_back(c_rep_id[co + k]);
+      h_rep_next.push_back(c_rep_next[co + k]);
+      h_rep_t0.push_back(c_t0[co + k]);
+      h_rep_t1.push_back(c_t1[co + k]);
+      h_rep_length.push_back(c_rl[co + k]);
+      h_rep_queue.push_back(c_rq[co + k]);
+    }
+    h_trace_route_off[t + 1] = (int64_t)h_route_edge.size();
+    h_trace_seg_off[t + 1] = (int64_t)h_seg_id.size();
+    h_trace_rep_off[t + 1] = (int64_t)h_rep_id.size();
+  }
+  auto P = [](auto& v) { return v.empty() ? nullptr : v.data(); };
+  out->trace_state_off = P(h_trace_state_off);
+  out->state_probe = P(h_state_probe);
+  out->cand_count = P(h_cand_count);
+  out->cand_edge = P(h_cand_edge);
+  out->cand_p = P(h_cand_p);
+  out->cand_sqd = P(h_cand_sqd);
+  out->winner = P(h_winner);
+  out->subpath = P(h_subpath);
+  out->trace_route_off = P(h_trace_route_off);
+  out->route_edge = P(h_route_edge);
+  out->trace_seg_off = P(h_trace_seg_off);
+  out->seg_id = (uint64_t*)P(h_seg_id);
+  out->seg_start = P(h_seg_start);
+  out->seg_end = P(h_seg_end);
+  out->seg_length = P(h_seg_length);
+  out->seg_queue = P(h_seg_queue);
+  out->seg_internal = P(h_seg_internal);
+  out->seg_begin_shape = P(h_seg_bshape);
+  out->seg_end_shape = P(h_seg_eshape);
+  out->seg_way_off = P(h_seg_way_off);
+  out->seg_way = P(h_seg_way);
+  out->trace_rep_off = P(h_trace_rep_off);
+  out->rep_id = (uint64_t*)P(h_rep_id);
+  out->rep_next = (uint64_t*)P(h_rep_next);
+  out->rep_t0 = P(h_rep_t0);
+  out->rep_t1 = P(h_rep_t1);
+  out->rep_length = P(h_rep_length);
+  out->rep_queue = P(h_rep_queue);
+  out->shape_used = P(h_shape_used);
+  out->stats = P(h_stats);
+  out->stats_len = P(h_stats_len);
+  return OTR_OK;
+}
+
+}  // namespace otr

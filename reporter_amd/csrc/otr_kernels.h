@@ -1,0 +1,1041 @@
+// otr_kernels.h — the HIP kernels of the matching hot path (gfx950, wave64).
+//
+//   K0 k_select_states   thread/trace   interpolation_distance state selection
+//   K1 k_candidates      wave/state     grid-cell edge projection, LDS top-K
+//   K2 (emission)        fused into K5  sq_dist / (2 sigma_z^2)
+//   K_link               thread/trace   active-state chain, g, route bound
+//   K3 k_route           wave/(step,src) bounded one-to-many search, LDS hash
+//   K4 (transition)      epilogue of K3 |route - g| / beta
+//   K5 k_viterbi         wave/trace     fp64 min-sum Viterbi + backtrack
+//   K6 k_paths           wave/step      winner path reconstruction
+//   K7 k_segments        thread/trace   route stitch, OSMLR segments, report()
+//   K8 k_histogram       thread/trace   simple_reporter filter + hour buckets
+//
+// Every decision-path expression mirrors oracle/oracle.c operation for operation
+// (DESIGN.md §3); the tests compare the two bit for bit.
+#pragma once
+#include "otr_device.h"
+#include "otr_report.h"
+
+namespace otr {
+
+struct BatchDev {
+  int32_t n_traces;
+  const int64_t* trace_off;
+  const double* lat;
+  const double* lon;
+  const int64_t* time;
+  const float* acc;
+  const uint8_t* mode;
+};
+
+// ------------------------------------------------------------------------------
+// K0: state selection (thread per trace).  Pass 1 counts, pass 2 writes.
+// ------------------------------------------------------------------------------
+__global__ void k_select_states(BatchDev b, ModeParams mp, int64_t* state_cnt, const int64_t* state_off,
+                                int64_t* state_probe, int32_t* state_trace) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= b.n_traces) return;
+  const int64_t lo = b.trace_off[t], hi = b.trace_off[t + 1];
+  const MatchParams& P = mp.m[b.mode[t] < OTR_MODES ? b.mode[t] : 0];
+  int64_t cnt = 0, last = lo;
+  int64_t base = state_off ? state_off[t] : 0;
+  for (int64_t i = lo; i < hi; ++i) {
+    bool st = (i == lo || i == hi - 1) ||
+              gc_dist(b.lat[last], b.lon[last], b.lat[i], b.lon[i]) >= P.interpolation_distance;
+    if (st) {
+      if (state_off) {
+        state_probe[base + cnt] = i;
+        state_trace[base + cnt] = t;
+      }
+      ++cnt;
+      last = i;
+    }
+  }
+  if (!state_off) state_cnt[t] = cnt;
+}
+
+// ------------------------------------------------------------------------------
+// K1: candidate search, one wave (block of 64) per state.
+// ------------------------------------------------------------------------------
+struct CandBuf {
+  uint32_t* edge;   // [n_states][OTR_KMAX]
+  double* p;
+  double* sqd;
+  int32_t* count;
+};
+
+__device__ inline bool cand_less(double da, uint32_t ea, double db, uint32_t eb) {
+  return da < db || (da == db && ea < eb);
+}
+
+__global__ __launch_bounds__(64) void k_candidates(DevGraph g, BatchDev b, ModeParams mp, int64_t n_states,
+                                                   const int64_t* state_probe, const int32_t* state_trace,
+                                                   CandBuf out, unsigned long long* counters) {
+  __shared__ double s_d2[2][2 * OTR_WAVE];
+  __shared__ double s_p[2][2 * OTR_WAVE];
+  __shared__ uint32_t s_e[2][2 * OTR_WAVE];
+  const int lane = threadIdx.x;
+  for (int64_t s = blockIdx.x; s < n_states; s += gridDim.x) {
+    const int64_t probe = state_probe[s];
+    const int mode = b.mode[state_trace[s]] < OTR_MODES ? b.mode[state_trace[s]] : 0;
+    const MatchParams& P = mp.m[mode];
+    const uint32_t mode_bit = 1u << mode;
+    const int kmax = P.kmax;
+    const double plat = b.lat[probe], plon = b.lon[probe];
+    const double a = (b.acc && b.acc[probe] >= 0.f) ? (double)b.acc[probe] : P.gps_accuracy;
+    double radius = P.search_radius > a ? P.search_radius : a;
+    if (radius > P.max_search_radius) radius = P.max_search_radius;
+    const double mpl = kMetersPerDeg * cos_deg(plat);
+    const double cd = g.grid_cell_deg;
+    const double dlat = radius / kMetersPerDeg, dlon = radius / mpl;
+    int64_t r0 = (int64_t)floor((plat - dlat - OTR_GRID_PAD_DEG - g.grid_min_lat) / cd);
+    int64_t r1 = (int64_t)floor((plat + dlat + OTR_GRID_PAD_DEG - g.grid_min_lat) / cd);
+    int64_t c0 = (int64_t)floor((plon - dlon - OTR_GRID_PAD_DEG - g.grid_min_lon) / cd);
+    int64_t c1 = (int64_t)floor((plon + dlon + OTR_GRID_PAD_DEG - g.grid_min_lon) / cd);
+    if (r0 < 0) r0 = 0;
+    if (c0 < 0) c0 = 0;
+    if (r1 > (int64_t)g.grid_rows - 1) r1 = (int64_t)g.grid_rows - 1;
+    if (c1 > (int64_t)g.grid_cols - 1) c1 = (int64_t)g.grid_cols - 1;
+    const double r2 = radius * radius;
+    int n = 0, buf = 0;
+    unsigned long long tests = 0;
+    for (int64_t r = r0; r <= r1; ++r)
+      for (int64_t c = c0; c <= c1; ++c) {
+        const uint32_t cell = (uint32_t)(r * g.grid_cols + c);
+        const uint32_t beg = g.cell_row[cell], end = g.cell_row[cell + 1];
+        for (uint32_t base = beg; base < end; base += OTR_WAVE) {
+          const uint32_t q = base + lane;
+          bool ok = false;
+          double best = 0, frac = 0;
+          uint32_t e = 0;
+          if (q < end) {
+            e = g.cell_edge[q];
+            if (g.edge_attr[e] & mode_bit) {
+              best = __builtin_huge_val();
+              double best_along = 0.0, bqx = 0.0, bqy = 0.0, acc = 0.0;
+              const uint32_t k0 = g.edge_shape[e], k1 = g.edge_shape[e + 1];
+              int2 pa = g.shape_ll[k0];
+              for (uint32_t k = k0; k + 1 < k1; ++k) {
+                const int2 pb = g.shape_ll[k + 1];
+                const double ax = (e6(pa.y) - plon) * mpl;
+                const double ay = (e6(pa.x) - plat) * kMetersPerDeg;
+                const double bx = (e6(pb.y) - plon) * mpl;
+                const double by = (e6(pb.x) - plat) * kMetersPerDeg;
+                const double dx = bx - ax, dy = by - ay;
+                const double l2 = dx * dx + dy * dy;
+                double t = 0.0;
+                if (l2 > 0.0) {
+                  t = -(ax * dx + ay * dy) / l2;
+                  if (t < 0.0) t = 0.0;
+                  if (t > 1.0) t = 1.0;
+                }
+                const double qx = ax + t * dx, qy = ay + t * dy;
+                const double d2 = qx * qx + qy * qy;
+                const double sl = sqrt(l2);
+                if (d2 < best) {
+                  best = d2;
+                  best_along = acc + t * sl;
+                  bqx = qx;
+                  bqy = qy;
+                }
+                acc = acc + sl;
+                pa = pb;
+              }
+              tests += k1 - k0 - 1;
+              if (best <= r2) {
+                const double slat = plat + bqy / kMetersPerDeg, slon = plon + bqx / mpl;
+                const int64_t sr = (int64_t)floor((slat - g.grid_min_lat) / cd);
+                const int64_t sc = (int64_t)floor((slon - g.grid_min_lon) / cd);
+                ok = (sr == r && sc == c);
+                frac = acc > 0.0 ? best_along / acc : 0.0;
+              }
+            }
+          }
+          const unsigned long long mask = __ballot(ok);
+          if (mask) {
+            if (ok) {
+              const int pos = n + prefix_count(mask);
+              s_d2[buf][pos] = best;
+              s_p[buf][pos] = frac;
+              s_e[buf][pos] = e;
+            }
+            n += __popcll(mask);
+            __syncthreads();
+            if (n > kmax) {  // rank-compact to the kmax best (all (d2,edge) keys distinct)
+              for (int idx = lane; idx < n; idx += OTR_WAVE) {
+                const double d = s_d2[buf][idx];
+                const uint32_t ee = s_e[buf][idx];
+                int rank = 0;
+                for (int m = 0; m < n; ++m) rank += cand_less(s_d2[buf][m], s_e[buf][m], d, ee);
+                if (rank < kmax) {
+                  s_d2[buf ^ 1][rank] = d;
+                  s_p[buf ^ 1][rank] = s_p[buf][idx];
+                  s_e[buf ^ 1][rank] = ee;
+                }
+              }
+              __syncthreads();
+              buf ^= 1;
+              n = kmax;
+            }
+          }
+        }
+      }
+    // final ordering
+    const size_t o = (size_t)s * OTR_KMAX;
+    for (int idx = lane; idx < n; idx += OTR_WAVE) {
+      const double d = s_d2[buf][idx];
+      const uint32_t ee = s_e[buf][idx];
+      int rank = 0;
+      for (int m = 0; m < n; ++m) rank += cand_less(s_d2[buf][m], s_e[buf][m], d, ee);
+      out.edge[o + rank] = ee;
+      out.p[o + rank] = s_p[buf][idx];
+      out.sqd[o + rank] = d;
+    }
+    if (lane == 0) out.count[s] = n;
+    // algorithmic-byte counters
+    for (int off = 32; off > 0; off >>= 1) tests += __shfl_xor(tests, off);
+    if (lane == 0 && counters) {
+      atomicAdd(&counters[0], (unsigned long long)((r1 - r0 + 1) * (c1 - c0 + 1)));
+      atomicAdd(&counters[1], tests);
+      atomicAdd(&counters[2], (unsigned long long)n);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------
+// K_link: per trace, chain active states (K>0) into steps.
+// ------------------------------------------------------------------------------
+struct StepBuf {
+  int64_t* prev;      // previous active state of the same trace, -1 none, -2 inactive
+  double* g;          // great-circle distance prev→s
+  double* bound;      // route bound
+  uint8_t* forced;    // g > breakage_distance
+  int64_t* ntask;     // K[prev] for steps, else 0
+  int64_t* ntrans;    // K[prev]*K[s]
+};
+
+__global__ void k_link(BatchDev b, ModeParams mp, const int64_t* trace_state_off, const int64_t* state_probe,
+                       const int32_t* cand_count, StepBuf st) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= b.n_traces) return;
+  const MatchParams& P = mp.m[b.mode[t] < OTR_MODES ? b.mode[t] : 0];
+  int64_t last = -1;
+  for (int64_t s = trace_state_off[t]; s < trace_state_off[t + 1]; ++s) {
+    st.ntask[s] = 0;
+    st.ntrans[s] = 0;
+    if (cand_count[s] <= 0) {
+      st.prev[s] = -2;
+      continue;
+    }
+    st.prev[s] = last;
+    if (last >= 0) {
+      const int64_t ia = state_probe[last], ib = state_probe[s];
+      const double gcd = gc_dist(b.lat[ia], b.lon[ia], b.lat[ib], b.lon[ib]);
+      st.g[s] = gcd;
+      st.forced[s] = gcd > P.breakage_distance;
+      st.bound[s] = route_bound(P, gcd);
+      st.ntask[s] = cand_count[last];
+      st.ntrans[s] = (int64_t)cand_count[last] * cand_count[s];
+    }
+    last = s;
+  }
+}
+
+__global__ void k_taskmap(int64_t n_states, const int64_t* task_off, int64_t* task_state, int32_t* task_src) {
+  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_states) return;
+  for (int64_t k = task_off[s]; k < task_off[s + 1]; ++k) {
+    task_state[k] = s;
+    task_src[k] = (int32_t)(k - task_off[s]);
+  }
+}
+
+// ------------------------------------------------------------------------------
+// Bounded one-to-many search, one wave, node labels in an LDS hash table.
+//
+// Distance-bucketed label correcting: each round takes every pending node whose
+// label is below (minimum pending label + delta), relaxes its out-edges with LDS
+// 64-bit atomicMin on the binary64 bit pattern (positive doubles order like u64),
+// and re-queues improved nodes.  The fixed point is the minimal left-to-right
+// binary64 path sum — the same value the oracle's binary-heap Dijkstra settles —
+// and a node whose label is below the minimum pending label is final, so the
+// search stops as soon as every target is final or provably beyond the bound.
+// ------------------------------------------------------------------------------
+template <int CAP>
+struct SearchLds {
+  uint32_t key[CAP];              // node id | INQ bit, 0xFFFFFFFF empty
+  unsigned long long dist[CAP];   // binary64 bits
+  uint16_t pend[CAP];
+  uint16_t work[CAP];
+  int n_pend, n_work, n_keys, overflow, all_done;
+};
+
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kInq = 0x80000000u;
+constexpr unsigned long long kInfBits = 0x7FF0000000000000ull;
+
+template <int CAP>
+__device__ inline int lds_find(const SearchLds<CAP>& L, uint32_t node) {
+  uint32_t h = hmix(node) & (CAP - 1);
+  for (int probe = 0; probe < CAP; ++probe) {
+    const uint32_t k = L.key[h];
+    if (k == kEmpty) return -1;
+    if ((k & ~kInq) == node) return (int)h;
+    h = (h + 1) & (CAP - 1);
+  }
+  return -1;
+}
+
+template <int CAP>
+__device__ inline int lds_insert(SearchLds<CAP>& L, uint32_t node) {
+  uint32_t h = hmix(node) & (CAP - 1);
+  for (int probe = 0; probe < CAP; ++probe) {
+    uint32_t k = L.key[h];
+    if (k == kEmpty) {
+      const uint32_t old = atomicCAS(&L.key[h], kEmpty, node);
+      if (old == kEmpty) {
+        const int nk = atomicAdd(&L.n_keys, 1);
+        if (nk >= (CAP * 3) / 4) L.overflow = 1;
+        return (int)h;
+      }
+      k = old;
+    }
+    if ((k & ~kInq) == node) return (int)h;
+    h = (h + 1) & (CAP - 1);
+  }
+  L.overflow = 1;
+  return -1;
+}
+
+template <int CAP>
+__device__ inline void search_init(SearchLds<CAP>& L) {
+  for (int k = threadIdx.x; k < CAP; k += OTR_WAVE) {
+    L.key[k] = kEmpty;
+    L.dist[k] = kInfBits;
+  }
+  if (threadIdx.x == 0) {
+    L.n_pend = 0;
+    L.n_work = 0;
+    L.n_keys = 0;
+    L.overflow = 0;
+    L.all_done = 0;
+  }
+  __syncthreads();
+}
+
+// Target j (lane j < n_tgt) resolved?  tnode==kEmpty: nothing to search for.
+template <int CAP>
+__device__ inline bool target_resolved(const SearchLds<CAP>& L, uint32_t tnode, double tpart, double bound,
+                                       double dmin, bool pend_empty) {
+  if (tnode == kEmpty) return true;
+  if (pend_empty) return true;
+  const int sl = lds_find(L, tnode);
+  if (sl >= 0 && __longlong_as_double((long long)L.dist[sl]) < dmin) return true;
+  return dmin + tpart > bound;
+}
+
+// Runs the search from `start` (label d0).  Lanes j < n_tgt hold target node tnode
+// and target partial length tpart.  Returns false on LDS-table overflow.
+template <int CAP>
+__device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_bit, uint32_t start, double d0,
+                           double bound, double delta, uint32_t tnode, double tpart, int n_tgt,
+                           unsigned long long* settled, unsigned long long* relaxed) {
+  const int lane = threadIdx.x;
+  if (lane == 0) {
+    const int sl = lds_insert(L, start);
+    L.dist[sl] = (unsigned long long)__double_as_longlong(d0);
+    L.key[sl] |= kInq;
+    L.pend[0] = (uint16_t)sl;
+    L.n_pend = 1;
+  }
+  __syncthreads();
+  unsigned long long my_settled = 0, my_relaxed = 0;
+  for (;;) {
+    const int np = L.n_pend;
+    // minimum pending label (wave reduce)
+    double dmin = __builtin_huge_val();
+    for (int k = lane; k < np; k += OTR_WAVE) {
+      const double d = __longlong_as_double((long long)L.dist[L.pend[k]]);
+      dmin = d < dmin ? d : dmin;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const double o = __shfl_xor(dmin, off);
+      dmin = o < dmin ? o : dmin;
+    }
+    const bool res = lane >= n_tgt || target_resolved(L, tnode, tpart, bound, dmin, np == 0);
+    if (__ballot(!res) == 0ull || np == 0) break;
+    // split pending into this round's work (label < dmin + delta) and the rest
+    const double theta = dmin + delta;
+    int kept = 0, nw = 0;
+    for (int base = 0; base < np; base += OTR_WAVE) {
+      const int k = base + lane;
+      uint16_t sl = 0;
+      bool take = false;
+      if (k < np) {
+        sl = L.pend[k];
+        take = __longlong_as_double((long long)L.dist[sl]) < theta;
+      }
+      const unsigned long long mt = __ballot(take), mk = __ballot(k < np && !take);
+      __syncthreads();
+      if (take) {
+        L.work[nw + prefix_count(mt)] = sl;
+        atomicAnd(&L.key[sl], ~kInq);
+      } else if (k < np) {
+        L.pend[kept + prefix_count(mk)] = sl;
+      }
+      nw += __popcll(mt);
+      kept += __popcll(mk);
+      __syncthreads();
+    }
+    if (lane == 0) L.n_pend = kept;
+    __syncthreads();
+    // relax the work list
+    for (int base = 0; base < nw; base += OTR_WAVE) {
+      const int k = base + lane;
+      if (k < nw) {
+        const int ws = L.work[k];
+        const uint32_t u = L.key[ws] & ~kInq;
+        const double du = __longlong_as_double((long long)L.dist[ws]);
+        ++my_settled;
+        for (uint32_t e = g.node_row[u]; e < g.node_row[u + 1]; ++e) {
+          const uint4 pk = g.edge_pack[e];
+          ++my_relaxed;
+          if (!(pk.z & mode_bit)) continue;
+          const double nd = du + (double)__uint_as_float(pk.y);
+          if (nd > bound) continue;
+          const int sl = lds_insert(L, pk.x);
+          if (sl < 0) break;
+          const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
+          const unsigned long long old = atomicMin(&L.dist[sl], nb);
+          if (nb < old) {
+            const uint32_t ok = atomicOr(&L.key[sl], kInq);
+            if (!(ok & kInq)) {
+              const int p = atomicAdd(&L.n_pend, 1);
+              if (p < CAP) L.pend[p] = (uint16_t)sl;
+              else L.overflow = 1;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (L.overflow) break;
+  }
+  if (settled) *settled += my_settled;
+  if (relaxed) *relaxed += my_relaxed;
+  __syncthreads();
+  return !L.overflow;
+}
+
+// ------------------------------------------------------------------------------
+// K3 + K4: one wave per (step, source candidate): search, then transition costs.
+// ------------------------------------------------------------------------------
+struct RouteArgs {
+  const int64_t* task_state;
+  const int32_t* task_src;
+  const int64_t* task_list;   // optional indirection (overflow retry), else null
+  int64_t n_tasks;
+  const int64_t* prev;
+  const double* g;
+  const double* bound;
+  const uint8_t* forced;
+  const int64_t* trans_off;
+  double* trans;
+  const int32_t* cand_count;
+  const uint32_t* cand_edge;
+  const double* cand_p;
+  const int32_t* state_trace;
+  const uint8_t* mode;
+  double delta;
+  double inv_beta[OTR_MODES];
+  int32_t* overflow_flag;     // per task
+};
+
+template <int CAP>
+__global__ __launch_bounds__(64) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
+  __shared__ SearchLds<CAP> L;
+  const int lane = threadIdx.x;
+  unsigned long long settled = 0, relaxed = 0;
+  for (int64_t w = blockIdx.x; w < a.n_tasks; w += gridDim.x) {
+    const int64_t task = a.task_list ? a.task_list[w] : w;
+    const int64_t s = a.task_state[task];
+    const int i = a.task_src[task];
+    const int64_t sp = a.prev[s];
+    const int Kb = a.cand_count[s];
+    const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+    const uint32_t mode_bit = 1u << mode;
+    const double bound = a.bound[s], gcd = a.g[s];
+    const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
+    const double pi = a.cand_p[sp * OTR_KMAX + i];
+    const double leni = (double)gr.edge_len[ei];
+    double* row = a.trans + a.trans_off[s] + (int64_t)i * Kb;
+    // targets: lane j
+    uint32_t ej = 0, tnode = kEmpty;
+    double pj = 0, tpart = 0;
+    bool same = false;
+    if (lane < Kb) {
+      ej = a.cand_edge[s * OTR_KMAX + lane];
+      pj = a.cand_p[s * OTR_KMAX + lane];
+      same = (ej == ei && pj >= pi);
+      if (!same) {
+        tnode = gr.edge_src[ej];
+        tpart = pj * (double)gr.edge_len[ej];
+      }
+    }
+    if (a.forced[s]) {
+      if (lane < Kb) row[lane] = __builtin_huge_val();
+      continue;
+    }
+    const double d0 = (1.0 - pi) * leni;
+    const bool need = __ballot(lane < Kb && !same) != 0ull;
+    bool ok = true;
+    search_init<CAP>(L);
+    if (need && d0 <= bound)
+      ok = search_run<CAP>(L, gr, mode_bit, gr.edge_dst[ei], d0, bound, a.delta, tnode, tpart, Kb, &settled,
+                           &relaxed);
+    if (!ok) {
+      if (lane == 0) a.overflow_flag[task] = 1;
+      continue;
+    }
+    if (lane < Kb) {
+      double r = __builtin_huge_val();
+      if (same) {
+        r = (pj - pi) * leni;
+      } else if (need && d0 <= bound) {
+        const int sl = lds_find(L, tnode);
+        if (sl >= 0) r = __longlong_as_double((long long)L.dist[sl]) + tpart;
+      }
+      row[lane] = r <= bound ? fabs(r - gcd) * a.inv_beta[mode] : __builtin_huge_val();
+    }
+    __syncthreads();
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    settled += __shfl_xor(settled, off);
+    relaxed += __shfl_xor(relaxed, off);
+  }
+  if (lane == 0 && counters) {
+    atomicAdd(&counters[3], settled);
+    atomicAdd(&counters[4], relaxed);
+  }
+}
+
+// ------------------------------------------------------------------------------
+// K5: fp64 Viterbi, one wave per trace, lane j = candidate of the current state.
+// ------------------------------------------------------------------------------
+struct ViterbiArgs {
+  int32_t n_traces;
+  const int64_t* trace_state_off;
+  const int32_t* cand_count;
+  const double* cand_sqd;
+  const int64_t* prev;
+  const int64_t* trans_off;
+  const double* trans;
+  const uint8_t* mode;
+  double inv2s2[OTR_MODES];
+  int8_t* bp;          // [n_states][OTR_KMAX]
+  uint8_t* brk;        // sub-path starts here
+  int32_t* end_win;    // winner of a state that ends a sub-path
+  int32_t* winner;
+  int32_t* subpath;
+};
+
+__device__ inline void argmin_lane(double c, int j, double* oc, int* oj) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const double c2 = __shfl_xor(c, off);
+    const int j2 = __shfl_xor(j, off);
+    if (c2 < c || (c2 == c && j2 < j)) {
+      c = c2;
+      j = j2;
+    }
+  }
+  *oc = c;
+  *oj = j;
+}
+
+__global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long long* counters) {
+  __shared__ double s_cost[OTR_KMAX];
+  const int lane = threadIdx.x;
+  unsigned long long cells = 0;
+  for (int t = blockIdx.x; t < a.n_traces; t += gridDim.x) {
+    const double inv2s2 = a.inv2s2[a.mode[t] < OTR_MODES ? a.mode[t] : 0];
+    const int64_t so = a.trace_state_off[t], eo = a.trace_state_off[t + 1];
+    int64_t prev_s = -1;
+    int Kp = 0;
+    for (int64_t s = so; s < eo; ++s) {
+      const int K = a.cand_count[s];
+      if (K <= 0) continue;
+      double emis = 0.0;
+      if (lane < K) emis = a.cand_sqd[s * OTR_KMAX + lane] * inv2s2;
+      double cost = __builtin_huge_val();
+      int bi = -1;
+      bool brk = prev_s < 0;
+      if (!brk) {
+        double best = __builtin_huge_val();
+        if (lane < K) {
+          const double* tr = a.trans + a.trans_off[s];
+          for (int i = 0; i < Kp; ++i) {
+            const double ti = tr[(int64_t)i * K + lane];
+            const double ci = s_cost[i];
+            if (ti == __builtin_huge_val() || ci == __builtin_huge_val()) continue;
+            const double c = ci + ti;
+            if (c < best) {
+              best = c;
+              bi = i;
+            }
+          }
+        }
+        cells += (unsigned long long)Kp;
+        const bool any = __ballot(lane < K && bi >= 0) != 0ull;
+        if (!any) {
+          brk = true;
+          bi = -1;
+        } else {
+          cost = bi >= 0 ? best + emis : __builtin_huge_val();
+        }
+      }
+      if (brk) {
+        if (prev_s >= 0) {  // previous sub-path ends at prev_s
+          double mc;
+          int mj;
+          argmin_lane(lane < Kp ? s_cost[lane] : __builtin_huge_val(), lane < Kp ? lane : OTR_KMAX, &mc, &mj);
+          if (lane == 0) a.end_win[prev_s] = mj;
+        }
+        cost = emis;
+        bi = -1;
+      }
+      if (lane < K) a.bp[s * OTR_KMAX + lane] = (int8_t)bi;
+      if (lane == 0) a.brk[s] = brk ? 1 : 0;
+      __syncthreads();
+      if (lane < K) s_cost[lane] = cost;
+      __syncthreads();
+      prev_s = s;
+      Kp = K;
+    }
+    if (prev_s >= 0) {
+      double mc;
+      int mj;
+      argmin_lane(lane < Kp ? s_cost[lane] : __builtin_huge_val(), lane < Kp ? lane : OTR_KMAX, &mc, &mj);
+      if (lane == 0) a.end_win[prev_s] = mj;
+    }
+    __syncthreads();
+    // backtrack (lane 0), then sub-path ordinals
+    if (lane == 0) {
+      int cur = -1;
+      bool next_brk = true;  // "state after this one starts a sub-path" (true past the end)
+      for (int64_t s = eo - 1; s >= so; --s) {
+        if (a.cand_count[s] <= 0) {
+          a.winner[s] = -1;
+          a.subpath[s] = -1;
+          continue;
+        }
+        if (next_brk) cur = a.end_win[s];
+        a.winner[s] = cur;
+        const bool b = a.brk[s] != 0;
+        if (!b) cur = a.bp[s * OTR_KMAX + cur];
+        next_brk = b;
+      }
+      int sp = -1;
+      for (int64_t s = so; s < eo; ++s) {
+        if (a.cand_count[s] <= 0) continue;
+        if (a.brk[s]) ++sp;
+        a.subpath[s] = sp;
+      }
+    }
+    __syncthreads();
+  }
+  for (int off = 32; off > 0; off >>= 1) cells += __shfl_xor(cells, off);
+  if (lane == 0 && counters) atomicAdd(&counters[6], cells);
+}
+
+// ------------------------------------------------------------------------------
+// K6: winner path reconstruction, one wave per step (state s with prev >= 0,
+// not a sub-path start).  Single-target search, then predecessor walk: among the
+// in-edges (u→v) with label(u) + len == label(v) take the smallest edge id.
+// ------------------------------------------------------------------------------
+struct PathArgs {
+  const int64_t* steps;        // state ids to reconstruct
+  int64_t n_steps;
+  const int64_t* prev;
+  const double* bound;
+  const uint8_t* brk;
+  const int32_t* winner;
+  const uint32_t* cand_edge;
+  const double* cand_p;
+  const int32_t* state_trace;
+  const uint8_t* mode;
+  double delta;
+  int64_t* path_off;           // per state
+  int32_t* path_len;           // per state; -1 = same-edge step
+  uint32_t* path;              // bump-allocated edge list
+  unsigned long long* cursor;
+  int64_t capacity;
+  int32_t* overflow_flag;      // per step index (table overflow)
+  int32_t* cap_flag;           // global: path buffer too small
+};
+
+template <int CAP>
+__device__ int walk_preds(const SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_bit, uint32_t S, uint32_t T,
+                          uint32_t* out, int64_t out_n) {
+  const int lane = threadIdx.x;
+  uint32_t v = T;
+  int n = 0;
+  while (v != S) {
+    const int sv = lds_find(L, v);
+    if (sv < 0) return -1;
+    const double dv = __longlong_as_double((long long)L.dist[sv]);
+    uint32_t best = kEmpty;
+    for (uint32_t base = g.rev_row[v]; base < g.rev_row[v + 1]; base += OTR_WAVE) {
+      const uint32_t r = base + lane;
+      uint32_t cand = kEmpty;
+      if (r < g.rev_row[v + 1]) {
+        const uint32_t ed = g.rev_edge[r];
+        if (g.edge_attr[ed] & mode_bit) {
+          const int su = lds_find(L, g.edge_src[ed]);
+          if (su >= 0 && __longlong_as_double((long long)L.dist[su]) + (double)g.edge_len[ed] == dv) cand = ed;
+        }
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = __shfl_xor(cand, off);
+        cand = o < cand ? o : cand;
+      }
+      best = cand < best ? cand : best;
+    }
+    if (best == kEmpty) return -1;
+    if (out && lane == 0) out[out_n - 1 - n] = best;
+    ++n;
+    v = g.edge_src[best];
+  }
+  return n;
+}
+
+template <int CAP>
+__global__ __launch_bounds__(64) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, int64_t n_list) {
+  __shared__ SearchLds<CAP> L;
+  const int lane = threadIdx.x;
+  for (int64_t w = blockIdx.x; w < n_list; w += gridDim.x) {
+    const int64_t k = step_list ? step_list[w] : w;
+    const int64_t s = a.steps[k];
+    const int64_t sp = a.prev[s];
+    const int wi = a.winner[sp], wj = a.winner[s];
+    const uint32_t ei = a.cand_edge[sp * OTR_KMAX + wi], ej = a.cand_edge[s * OTR_KMAX + wj];
+    const double pi = a.cand_p[sp * OTR_KMAX + wi], pj = a.cand_p[s * OTR_KMAX + wj];
+    if (ej == ei && pj >= pi) {
+      if (lane == 0) a.path_len[s] = -1;
+      continue;
+    }
+    const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+    const uint32_t mode_bit = 1u << mode;
+    const double d0 = (1.0 - pi) * (double)gr.edge_len[ei];
+    const uint32_t S = gr.edge_dst[ei], T = gr.edge_src[ej];
+    search_init<CAP>(L);
+    const bool ok = search_run<CAP>(L, gr, mode_bit, S, d0, a.bound[s], a.delta, lane == 0 ? T : kEmpty,
+                                    pj * (double)gr.edge_len[ej], 1, nullptr, nullptr);
+    if (!ok) {
+      if (lane == 0) a.overflow_flag[k] = 1;
+      continue;
+    }
+    const int n = walk_preds<CAP>(L, gr, mode_bit, S, T, nullptr, 0);
+    if (n < 0) {
+      if (lane == 0) a.overflow_flag[k] = 2;
+      continue;
+    }
+    int64_t off = 0;
+    if (lane == 0) off = (int64_t)atomicAdd(a.cursor, (unsigned long long)n);
+    off = __shfl(off, 0);
+    if (off + n > a.capacity) {
+      if (lane == 0) *a.cap_flag = 1;
+      continue;
+    }
+    walk_preds<CAP>(L, gr, mode_bit, S, T, a.path + off, n);
+    if (lane == 0) {
+      a.path_off[s] = off;
+      a.path_len[s] = n;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------
+// K7: route stitching, OSMLR traffic segments and report(), one thread per trace.
+// Output slots are at capacity offsets (cap_off), counts in *_n.
+// ------------------------------------------------------------------------------
+struct SegArgs {
+  BatchDev b;
+  const int64_t* trace_state_off;
+  const int64_t* state_probe;
+  const int32_t* cand_count;
+  const uint32_t* cand_edge;
+  const double* cand_p;
+  const int64_t* prev;
+  const uint8_t* brk;
+  const int32_t* winner;
+  const int64_t* path_off;
+  const int32_t* path_len;
+  const uint32_t* path;
+  double* pos;                 // scratch per state
+  int64_t* act;                // scratch per state: compact active state list
+  const int64_t* cap_off;      // per trace capacity offset (route/segments/ways/reports)
+  uint32_t* route;  int64_t* route_n;
+  unsigned long long* seg_id;  double* seg_start;  double* seg_end;  int32_t* seg_length;
+  int32_t* seg_queue;  uint8_t* seg_internal;  int32_t* seg_bshape;  int32_t* seg_eshape;
+  uint32_t* seg_index;  int64_t* seg_n;
+  int64_t* seg_way_n;  uint32_t* seg_way;  int64_t* way_n;
+  unsigned long long* rep_id;  unsigned long long* rep_next;  double* rep_t0;  double* rep_t1;
+  int32_t* rep_length;  int32_t* rep_queue;  uint32_t* rep_seg;  int64_t* rep_n;
+  int32_t* shape_used;  int32_t* stats;  double* stats_len;
+  double threshold;
+  uint32_t report_levels, transition_levels;
+};
+
+struct TimeCursor {  // time_at() of the oracle with a forward-moving pointer
+  const double* pos;
+  const double* tm;
+  int n, k;
+  __device__ double at(double s) {
+    while (k < n - 2 && s > pos[k + 1]) ++k;
+    if (pos[k + 1] > pos[k]) return tm[k] + (tm[k + 1] - tm[k]) * ((s - pos[k]) / (pos[k + 1] - pos[k]));
+    return tm[k];
+  }
+};
+
+__global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.b.n_traces) return;
+  const int64_t so = a.trace_state_off[t], eo = a.trace_state_off[t + 1];
+  const int64_t lo_probe = a.b.trace_off[t], n_probe = a.b.trace_off[t + 1] - lo_probe;
+  const int64_t co = a.cap_off[t];
+  uint32_t* route = a.route + co;
+  int64_t nr = 0, nseg = 0, nway = 0;
+  // compact active states
+  int na = 0;
+  int64_t* act = a.act + so;
+  for (int64_t s = so; s < eo; ++s)
+    if (a.cand_count[s] > 0) act[na++] = s;
+  double* pos = a.pos + so;  // indexed by active ordinal
+  // time stamps of active states are read from the batch (double(time))
+  bool first_sub = true;
+  int k = 0;
+  while (k < na) {
+    const int sa = k;
+    int e_ = k + 1;
+    while (e_ < na && !a.brk[act[e_]]) ++e_;
+    const int sb = e_ - 1;
+    k = e_;
+    if (sb == sa) {
+      first_sub = false;
+      continue;
+    }
+    if (nr) route[nr++] = 0xFFFFFFFFu;
+    // pass 1: positions of the sub-path's states
+    pos[sa] = 0.0;
+    for (int q = sa + 1; q <= sb; ++q) {
+      const int64_t si = act[q - 1], sj = act[q];
+      const uint32_t ei = a.cand_edge[si * OTR_KMAX + a.winner[si]], ej = a.cand_edge[sj * OTR_KMAX + a.winner[sj]];
+      const double pi = a.cand_p[si * OTR_KMAX + a.winner[si]], pj = a.cand_p[sj * OTR_KMAX + a.winner[sj]];
+      if (ej == ei && pj >= pi) {
+        pos[q] = pos[q - 1] + (pj - pi) * (double)g.edge_len[ei];
+        continue;
+      }
+      double s = pos[q - 1] + (1.0 - pi) * (double)g.edge_len[ei];
+      const int32_t pl = a.path_len[sj];
+      for (int z = 0; z < pl; ++z) s = s + (double)g.edge_len[a.path[a.path_off[sj] + z]];
+      pos[q] = s + pj * (double)g.edge_len[ej];
+    }
+    // state times (binary64 of the integer epoch seconds)
+    // pass 2: portions → groups, streaming
+    const int nst = sb - sa + 1;
+    double* tms = a.pos + eo + 0;  // not used: times read on the fly below
+    (void)tms;
+    // time cursor over (pos, time) of states sa..sb; times materialised in a small ring
+    // (we need random access by k in TimeCursor): reuse `act` tail? keep it simple:
+    // materialise into the per-state scratch after `pos` (pos has eo-so slots; use
+    // the second half of a.act reinterpreted is unsafe) — use a local fetcher instead.
+    struct {
+      const double* pos;
+      const int64_t* act;
+      const int64_t* probe;
+      const int64_t* time;
+      int base, n, k;
+      __device__ double tm(int q) const { return (double)time[probe[act[base + q]]]; }
+      __device__ double at(double s) {
+        while (k < n - 2 && s > pos[base + k + 1]) ++k;
+        const double p0 = pos[base + k], p1 = pos[base + k + 1];
+        const double t0 = tm(k), t1 = tm(k + 1);
+        if (p1 > p0) return t0 + (t1 - t0) * ((s - p0) / (p1 - p0));
+        return t0;
+      }
+    } tc = {pos, act, a.state_probe, a.b.time, sa, nst, 0};
+    // shape-index cursor: last state q (relative) with pos <= s
+    int sh_q = 0;
+    const int64_t lo = first_sub ? 0 : a.state_probe[act[sa]] - lo_probe;
+    const int64_t hi = (k < na) ? a.state_probe[act[k]] - lo_probe - 1 : n_probe - 1;
+    first_sub = false;
+    auto shape_at = [&](double s) -> int32_t {
+      while (sh_q + 1 < nst && pos[sa + sh_q + 1] <= s) ++sh_q;
+      int64_t r = (sh_q + 1 < nst) ? a.state_probe[act[sa + sh_q + 1]] - lo_probe - 1 : hi;
+      return (int32_t)(r < lo ? lo : r);
+    };
+    // group state
+    bool have = false;
+    uint32_t gkey = 0, gfirst_e = 0, glast_e = 0, glast_way = 0;
+    bool ginternal = false, gfirst_is_route_first = false;
+    double gs0 = 0, gs1 = 0;
+    int64_t gway_start = 0;
+    bool any_portion = false;
+    auto finalize = [&](bool is_last_portion) {
+      double st = -1.0, et = -1.0;
+      int32_t length = -1;
+      if (gkey != OTR_NO_SEGMENT) {
+        if (!gfirst_is_route_first && (g.edge_attr[gfirst_e] & OTR_ATTR_SEG_BEGIN)) st = tc.at(gs0);
+        if (!is_last_portion && (g.edge_attr[glast_e] & OTR_ATTR_SEG_END)) et = tc.at(gs1);
+        if (st != -1.0 && et != -1.0) length = (int32_t)g.seg_len[gkey];
+        a.seg_id[co + nseg] = g.seg_id[gkey];
+      } else {
+        if (!gfirst_is_route_first) st = tc.at(gs0);
+        if (!is_last_portion) et = tc.at(gs1);
+        a.seg_id[co + nseg] = OTR_NO_ID_U64;
+      }
+      a.seg_start[co + nseg] = st;
+      a.seg_end[co + nseg] = et;
+      a.seg_length[co + nseg] = length;
+      a.seg_queue[co + nseg] = 0;
+      a.seg_internal[co + nseg] = (gkey == OTR_NO_SEGMENT && ginternal) ? 1 : 0;
+      a.seg_index[co + nseg] = gkey;
+      a.seg_bshape[co + nseg] = shape_at(gs0);
+      a.seg_eshape[co + nseg] = shape_at(gs1);
+      a.seg_way_n[co + nseg] = nway - gway_start;
+      ++nseg;
+    };
+    auto portion = [&](uint32_t e, double s0, double s1) {
+      bool cont = false;
+      if (have) {
+        if (gkey != OTR_NO_SEGMENT) {
+          cont = g.edge_seg[e] == gkey && !(g.edge_attr[glast_e] & OTR_ATTR_SEG_END) &&
+                 !(g.edge_attr[e] & OTR_ATTR_SEG_BEGIN);
+        } else {
+          const bool ie = (g.edge_attr[e] & OTR_ATTR_INTERNAL) != 0;
+          cont = g.edge_seg[e] == OTR_NO_SEGMENT && ie == ginternal;
+        }
+        if (!cont) finalize(false);
+      }
+      if (!cont) {
+        have = true;
+        gkey = g.edge_seg[e];
+        ginternal = (g.edge_attr[e] & OTR_ATTR_INTERNAL) != 0;
+        gfirst_e = e;
+        gfirst_is_route_first = !any_portion;
+        gs0 = s0;
+        gway_start = nway;
+      }
+      const uint32_t w = g.edge_way[e];
+      if (nway == gway_start || w != glast_way) {
+        a.seg_way[co + nway++] = w;
+        glast_way = w;
+      }
+      glast_e = e;
+      gs1 = s1;
+      any_portion = true;
+    };
+    // walk the sub-path again emitting portions
+    {
+      const int64_t s0i = act[sa];
+      uint32_t cur_e = a.cand_edge[s0i * OTR_KMAX + a.winner[s0i]];
+      double cur_s0 = 0.0;
+      route[nr++] = cur_e;
+      for (int q = sa + 1; q <= sb; ++q) {
+        const int64_t si = act[q - 1], sj = act[q];
+        const uint32_t ei = a.cand_edge[si * OTR_KMAX + a.winner[si]];
+        const uint32_t ej = a.cand_edge[sj * OTR_KMAX + a.winner[sj]];
+        const double pi = a.cand_p[si * OTR_KMAX + a.winner[si]], pj = a.cand_p[sj * OTR_KMAX + a.winner[sj]];
+        if (ej == ei && pj >= pi) continue;
+        const double end_s = pos[q - 1] + (1.0 - pi) * (double)g.edge_len[ei];
+        portion(cur_e, cur_s0, end_s);
+        double s = end_s;
+        const int32_t pl = a.path_len[sj];
+        for (int z = 0; z < pl; ++z) {
+          const uint32_t ed = a.path[a.path_off[sj] + z];
+          const double s1 = s + (double)g.edge_len[ed];
+          portion(ed, s, s1);
+          route[nr++] = ed;
+          s = s1;
+        }
+        cur_e = ej;
+        cur_s0 = s;
+        route[nr++] = cur_e;
+      }
+      portion(cur_e, cur_s0, pos[sb]);
+      finalize(true);
+    }
+  }
+  a.route_n[t] = nr;
+  a.seg_n[t] = nseg;
+  a.way_n[t] = nway;
+  // report() over this trace's segments (reporter_service.py:79-179)
+  ReportStats rs;
+  const int64_t end_t = n_probe > 0 ? a.b.time[lo_probe + n_probe - 1] : 0;
+  report_segments((int32_t)nseg, a.seg_id + co, a.seg_start + co, a.seg_end + co, a.seg_internal + co,
+                  a.seg_queue + co, nullptr, a.seg_length + co, a.seg_bshape + co, a.seg_index + co, end_t,
+                  a.threshold, a.report_levels, a.transition_levels, a.rep_id + co, a.rep_next + co,
+                  a.rep_t0 + co, a.rep_t1 + co, a.rep_length + co, a.rep_queue + co, a.rep_seg + co, &rs);
+  a.rep_n[t] = rs.n_rep;
+  a.shape_used[t] = rs.shape_used;
+  for (int q = 0; q < 6; ++q) a.stats[7 * t + q] = rs.counts[q];
+  a.stats[7 * t + 6] = 0;
+  a.stats_len[2 * t] = rs.lengths[0];
+  a.stats_len[2 * t + 1] = rs.lengths[1];
+  if (counters) atomicAdd(&counters[7], (unsigned long long)nseg);
+}
+
+// ------------------------------------------------------------------------------
+// K8: simple_reporter filter + hour bucketing (simple_reporter.py:176-196) into a
+// dense [hour][segment][speed bin] count histogram; one thread per trace.
+// ------------------------------------------------------------------------------
+struct HistArgs {
+  BatchDev b;
+  const int64_t* cap_off;
+  const int64_t* rep_n;
+  const unsigned long long* rep_id;
+  const double* rep_t0;
+  const double* rep_t1;
+  const int32_t* rep_length;
+  const int32_t* rep_queue;
+  const uint32_t* rep_seg;
+  int64_t quantisation;
+  int64_t base_time;
+  int32_t hours;
+  uint32_t n_segments;
+  uint32_t* hist;
+  unsigned long long* n_rows;
+};
+
+__global__ void k_histogram(HistArgs a) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.b.n_traces) return;
+  const int64_t lo = a.b.trace_off[t], hi = a.b.trace_off[t + 1];
+  if (hi <= lo) return;
+  const int64_t first = a.b.time[lo], last = a.b.time[hi - 1];
+  const int64_t co = a.cap_off[t];
+  unsigned long long rows = 0;
+  for (int64_t r = 0; r < a.rep_n[t]; ++r) {
+    const double t0 = a.rep_t0[co + r], t1 = a.rep_t1[co + r];
+    const int32_t len = a.rep_length[co + r];
+    if (!bucket_keep(t0, t1, len, a.rep_queue[co + r])) continue;
+    const BucketSpan sp = bucket_span(t0, t1, first, last, a.quantisation);
+    if (!sp.ok) continue;
+    const double kmh = ((double)len / (t1 - t0)) * 3.6;
+    int bin = (int)(kmh / 20.0);
+    bin = bin < 0 ? 0 : (bin > OTR_HIST_BINS - 1 ? OTR_HIST_BINS - 1 : bin);
+    const uint32_t seg = a.rep_seg[co + r];
+    for (int64_t bk = sp.min_bucket; bk <= sp.max_bucket; ++bk) {
+      ++rows;
+      const int64_t h = (bk * a.quantisation - a.base_time) / a.quantisation;
+      if (h >= 0 && h < a.hours && seg < a.n_segments && a.hist)
+        atomicAdd(&a.hist[((size_t)h * a.n_segments + seg) * OTR_HIST_BINS + bin], 1u);
+    }
+  }
+  if (rows) atomicAdd(a.n_rows, rows);
+}
+
+}  // namespace otr

@@ -1,0 +1,131 @@
+"""Host-side handle over libotr: configuration and the batched matching API.
+
+Mirrors the reference's process model: `configure()` once per process
+(valhalla.Configure, reporter_service.py:284), one `Matcher` per thread
+(reporter_service.py:51-52).
+"""
+import ctypes
+import json
+import os
+import tempfile
+
+import numpy as np
+
+from . import _lib
+
+P = ctypes.POINTER
+
+MODES = {'auto': 0, 'bicycle': 1, 'pedestrian': 2}
+
+
+def default_config(graph_path, device=0, **meili_default):
+    """Valhalla-style config dict (meili values Dockerfile:14-17,42-49)."""
+    d = {'sigma_z': 4.07, 'beta': 3, 'max_route_distance_factor': 5, 'max_route_time_factor': 2,
+         'breakage_distance': 2000, 'interpolation_distance': 10, 'search_radius': 50,
+         'max_search_radius': 100, 'gps_accuracy': 5.0, 'turn_penalty_factor': 0, 'max_candidates': 32}
+    d.update(meili_default)
+    return {'meili': {'default': d, 'auto': {}, 'bicycle': {}, 'pedestrian': {}},
+            'otr': {'graph': os.path.abspath(graph_path), 'device': device}}
+
+
+def configure(config):
+    """Configure from a path or a dict; raises RuntimeError on failure."""
+    L = _lib.lib()
+    if isinstance(config, dict):
+        s = json.dumps(config).encode()
+        rc = L.otr_configure_json(s, len(s))
+    else:
+        rc = L.otr_configure(os.fspath(config).encode())
+    if rc != 0:
+        raise RuntimeError('otr_configure failed (%d): %s' % (rc, _lib.last_error()))
+
+
+def graph_info():
+    a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    rc = _lib.lib().otr_graph_info(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+    if rc != 0:
+        raise RuntimeError('not configured')
+    return a.value, b.value, c.value
+
+
+class Matcher:
+    def __init__(self):
+        self._L = _lib.lib()
+        self._h = self._L.otr_matcher_new()
+        self._keep = []
+
+    def close(self):
+        if self._h:
+            self._L.otr_matcher_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return self._L.otr_matcher_stream(self._h)
+
+    # --- JSON drop-in entry points ------------------------------------------------
+    def match_json(self, trace_json):
+        """SegmentMatcher.Match(json) -> str (reporter_service.py:240)."""
+        s = trace_json.encode() if isinstance(trace_json, str) else trace_json
+        out, n = ctypes.c_void_p(), ctypes.c_size_t()
+        rc = self._L.otr_match(self._h, s, len(s), ctypes.byref(out), ctypes.byref(n))
+        body = _lib.take_string(out, n)
+        if rc != 0:
+            raise RuntimeError(json.loads(body).get('error', body) if body else _lib.last_error())
+        return body
+
+    def report_json(self, trace_json, threshold_sec=-1):
+        """POST /report: returns (http_code, body) exactly as handle_request (209-245)."""
+        s = trace_json.encode() if isinstance(trace_json, str) else trace_json
+        out, n = ctypes.c_void_p(), ctypes.c_size_t()
+        rc = self._L.otr_report(self._h, s, len(s), threshold_sec, ctypes.byref(out), ctypes.byref(n))
+        return rc, _lib.take_string(out, n)
+
+    # --- batched API ----------------------------------------------------------------
+    def match_batch(self, traces, report_levels=(0, 1), transition_levels=(0, 1), threshold_sec=15,
+                    quantisation=3600, hist_base_time=0, hist_hours=0, copy_out=True, timing=False,
+                    device_arrays=None):
+        """Match a gen.Traces-like SoA batch.  With device_arrays (dict of device
+        pointers: trace_offsets, lat, lon, time, accuracy, mode) the inputs are
+        already resident in HBM."""
+        b = _lib.TraceBatch()
+        b.n_traces = int(traces.n_traces)
+        if device_arrays is not None:
+            b.memory = _lib.OTR_MEM_DEVICE
+            b.trace_offsets = device_arrays['trace_offsets']
+            b.lat = device_arrays['lat']
+            b.lon = device_arrays['lon']
+            b.time = device_arrays['time']
+            b.accuracy = device_arrays.get('accuracy') or None
+            b.mode = device_arrays['mode']
+        else:
+            b.memory = _lib.OTR_MEM_HOST
+            keep = [np.ascontiguousarray(traces.offsets, np.int64), np.ascontiguousarray(traces.lat, np.float64),
+                    np.ascontiguousarray(traces.lon, np.float64), np.ascontiguousarray(traces.time, np.int64),
+                    np.ascontiguousarray(traces.mode, np.uint8)]
+            acc = None if traces.accuracy is None else np.ascontiguousarray(traces.accuracy, np.float32)
+            self._keep = keep + [acc]
+            b.trace_offsets, b.lat, b.lon, b.time, b.mode = [k.ctypes.data for k in keep]
+            b.accuracy = acc.ctypes.data if acc is not None else None
+        b.report_levels = _lib.levels_mask(report_levels)
+        b.transition_levels = _lib.levels_mask(transition_levels)
+        b.threshold_sec = threshold_sec
+        b.quantisation = quantisation
+        b.hist_base_time = hist_base_time
+        b.hist_hours = hist_hours
+        b.flags = (_lib.OTR_BATCH_COPY_OUT if copy_out else 0) | (_lib.OTR_BATCH_TIMING if timing else 0)
+        r = _lib.BatchResult()
+        rc = self._L.otr_match_batch(self._h, ctypes.byref(b), ctypes.byref(r))
+        if rc != 0:
+            raise RuntimeError('otr_match_batch failed (%d): %s' % (rc, _lib.last_error()))
+        return r
+
+    def match_batch_numpy(self, traces, **kw):
+        r = self.match_batch(traces, copy_out=True, **kw)
+        return _lib.result_to_numpy(r)

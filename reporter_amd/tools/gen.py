@@ -1,0 +1,122 @@
+"""ctypes wrappers for libotrgen.so: seeded synthetic graphs and traces.
+
+Workload infrastructure for bench.py and the tests; the product never imports it.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+# named workloads: (graph args, trace args)  — SURVEY.md §8d / BASELINE.md table
+GRAPHS = {
+    # rows, cols, spacing_m, center_lat, center_lon, p_remove, seed, cell_deg
+    'tiny': (24, 24, 60.0, 14.55, 121.03, 0.10, 11, 0.0005),
+    'city': (200, 200, 50.0, 14.55, 121.03, 0.15, 1, 0.0005),
+    'metro': (1024, 1024, 50.0, 14.55, 121.03, 0.15, 2, 0.0005),
+}
+CONFIGS = {
+    # graph, n_traces, points/trace, sample_rate s, sigma m, seed, frac_bicycle, frac_ped, search_radius
+    'C1': ('city', 1000, 300, 1, 5.0, 1, 0.0, 0.0, 50.0),
+    'C2': ('metro', 10000, 100, 15, 10.0, 2, 0.0, 0.0, 50.0),
+    'C4': ('metro', 20000, 60, 60, 50.0, 4, 0.0, 0.0, 200.0),
+}
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, 'libotrgen.so')
+        if not os.path.exists(path):
+            raise RuntimeError('libotrgen.so not built: run python __graft_entry__.py build')
+        L = ctypes.CDLL(path)
+        L.otrgen_graph.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                   ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_uint64,
+                                   ctypes.c_double]
+        L.otrgen_graph.restype = ctypes.c_int
+        P = ctypes.POINTER
+        L.otrgen_traces.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                    ctypes.c_uint64, ctypes.c_double, ctypes.c_double, P(ctypes.c_double),
+                                    P(ctypes.c_double), P(ctypes.c_int64), P(ctypes.c_uint8),
+                                    P(ctypes.c_uint32)]
+        L.otrgen_traces.restype = ctypes.c_int
+        _LIB = L
+    return _LIB
+
+
+def graph_path(name, cache_dir=None):
+    """Return the path of graph `name`, generating it once into cache_dir."""
+    cache_dir = cache_dir or os.environ.get('OTR_CACHE', os.path.join(_HERE, '..', '..', 'build', 'graphs'))
+    os.makedirs(cache_dir, exist_ok=True)
+    path = os.path.abspath(os.path.join(cache_dir, name + '.otrg'))
+    if not os.path.exists(path):
+        args = GRAPHS[name]
+        tmp = path + '.tmp%d' % os.getpid()
+        rc = lib().otrgen_graph(tmp.encode(), *args)
+        if rc != 0:
+            raise RuntimeError('otrgen_graph failed: %d' % rc)
+        os.replace(tmp, path)
+    return path
+
+
+class Traces:
+    """SoA batch of traces: offsets, lat, lon, time, accuracy, mode, uuids."""
+
+    def __init__(self, lat, lon, time, offsets, mode, accuracy=None, truth=None, uuids=None):
+        self.lat, self.lon, self.time, self.offsets, self.mode = lat, lon, time, offsets, mode
+        self.accuracy = accuracy
+        self.truth = truth
+        self.uuids = uuids
+
+    @property
+    def n_traces(self):
+        return len(self.offsets) - 1
+
+    @property
+    def n_probes(self):
+        return int(self.offsets[-1])
+
+    def subset(self, idx):
+        idx = np.asarray(idx, dtype=np.int64)
+        parts = [np.arange(self.offsets[i], self.offsets[i + 1]) for i in idx]
+        sel = np.concatenate(parts) if parts else np.zeros(0, np.int64)
+        lens = np.array([self.offsets[i + 1] - self.offsets[i] for i in idx], dtype=np.int64)
+        off = np.zeros(len(idx) + 1, np.int64)
+        off[1:] = np.cumsum(lens)
+        acc = None if self.accuracy is None else self.accuracy[sel]
+        tr = None if self.truth is None else self.truth[sel]
+        uu = None if self.uuids is None else [self.uuids[i] for i in idx]
+        return Traces(self.lat[sel].copy(), self.lon[sel].copy(), self.time[sel].copy(), off,
+                      self.mode[idx].copy(), acc, tr, uu)
+
+
+def make_traces(graph, n_traces, n_points, sample_rate, sigma, seed, frac_bicycle=0.0, frac_ped=0.0,
+                point_accuracy=None, uuid_base=0):
+    n = n_traces * n_points
+    lat = np.zeros(n, np.float64)
+    lon = np.zeros(n, np.float64)
+    tm = np.zeros(n, np.int64)
+    mode = np.zeros(n_traces, np.uint8)
+    truth = np.zeros(n, np.uint32)
+    P = ctypes.POINTER
+    rc = lib().otrgen_traces(graph.encode(), n_traces, n_points, sample_rate, sigma, seed, frac_bicycle,
+                             frac_ped, lat.ctypes.data_as(P(ctypes.c_double)),
+                             lon.ctypes.data_as(P(ctypes.c_double)), tm.ctypes.data_as(P(ctypes.c_int64)),
+                             mode.ctypes.data_as(P(ctypes.c_uint8)), truth.ctypes.data_as(P(ctypes.c_uint32)))
+    if rc != 0:
+        raise RuntimeError('otrgen_traces failed: %d' % rc)
+    off = np.arange(n_traces + 1, dtype=np.int64) * n_points
+    acc = None
+    if point_accuracy is not None:
+        acc = np.full(n, float(point_accuracy), np.float32)
+    uuids = ['veh%07d' % (uuid_base + i) for i in range(n_traces)]
+    return Traces(lat, lon, tm, off, mode, acc, truth, uuids)
+
+
+def config_traces(name, n_traces=None, graph_cache=None):
+    g, nt, npnt, sr, sig, seed, fb, fp, radius = CONFIGS[name]
+    path = graph_path(g, graph_cache)
+    acc = 50.0 if name == 'C4' else None
+    return path, make_traces(path, n_traces or nt, npnt, sr, sig, seed, fb, fp, acc)

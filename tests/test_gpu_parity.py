@@ -1,0 +1,42 @@
+"""HIP path vs CPU oracle, field by field, through the C-ABI (include/otr.h)."""
+import json
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+from oracle.compare import compare
+from reporter_amd import matcher as M
+from reporter_amd.tools import gen
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    # name: (graph, n_traces, points, sample_rate, sigma, seed, frac_bike, frac_ped, accuracy, meili overrides)
+    'tiny_mixed': ('tiny', 24, 40, 5, 8.0, 7, 0.3, 0.3, None, {}),
+    'city_1hz': ('city', 40, 300, 1, 5.0, 1, 0.0, 0.0, None, {}),
+    'city_15s': ('city', 60, 100, 15, 10.0, 2, 0.0, 0.0, None, {}),
+    'city_sparse_60s': ('city', 30, 60, 60, 50.0, 4, 0.0, 0.0, 50.0,
+                        {'search_radius': 200, 'max_search_radius': 200}),
+    'metro_15s': ('metro', 100, 100, 15, 10.0, 3, 0.0, 0.0, None, {}),
+}
+
+
+@pytest.fixture(scope='module')
+def matcher():
+    return M.Matcher()
+
+
+@pytest.mark.parametrize('name', list(CASES))
+def test_batch_parity(name, graph_dir, matcher):
+    g, nt, npnt, sr, sig, seed, fb, fp, acc, over = CASES[name]
+    path = gen.graph_path(g, graph_dir)
+    M.configure(M.default_config(path, **over))
+    traces = gen.make_traces(path, nt, npnt, sr, sig, seed, fb, fp, acc)
+    got = matcher.match_batch_numpy(traces)
+    prm = po.params(**{k: float(v) for k, v in over.items()})
+    want = po.match_batch(po.Graph(path), traces, prm, threads=8)
+    errors, stats = compare(got, want)
+    assert not errors, errors
+    assert stats['n_seg'] > 0
+    assert got['status'] == 0
