@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""GPS probes matched/s (whole node) on the MI355X hot path — BASELINE.json metric.
+
+One step = one pass of the hot path over one batch resident in HBM:
+  trace SoA → states → candidates → bounded routing → Viterbi → paths → OSMLR
+  segments → report() → simple_reporter hour buckets → [hour][segment][speed-bin]
+  histogram, and for N>1 the RCCL reduce-scatter of that histogram over xGMI.
+
+Workload (N=1): SURVEY.md §8d config C2 — synthetic metro graph (1024x1024 street
+grid, ~1M nodes, ~3.6M directed edges, seed 2) and 10,000 traces x 100 probes at
+15 s sampling with sigma = 10 m noise (seed 2) = 1M probes.  N>1 (config C3 layout):
+N x 10,000 traces generated with one seed, sharded by int(sha1(uuid)[:3], 16) % N
+(simple_reporter.py:116), graph replicated per GPU, weak scaling.
+
+Launch:  python bench.py [--gpus N --steps K --warmup W]
+  N>1:   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+T_BEGIN = 1483228800
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def route_bytes(counters, n_tasks, n_trans):
+    """Algorithmic HBM bytes of one k_route launch:
+    per settled node 8 B (CSR row pair), per relaxed edge 16 B (packed edge record),
+    per task 64 B (task map, step metadata, source candidate), per transition entry
+    28 B (target candidate edge+fraction 12 B, target edge src+len 8 B, cost write 8 B)."""
+    settled, relaxed = counters[3], counters[4]
+    return 8 * settled + 16 * relaxed + 64 * n_tasks + 28 * n_trans
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--traces-per-gpu', type=int, default=10000)
+    ap.add_argument('--cpu-traces', type=int, default=1500, help='bounded oracle sample (0 = skip)')
+    ap.add_argument('--cpu-threads', type=int, default=16)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get('RANK', 0))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    local = int(os.environ.get('LOCAL_RANK', 0))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+
+    from reporter_amd import _lib
+    from reporter_amd import matcher as M
+    from reporter_amd.tools import gen
+    if not os.path.exists(_lib.LIB_PATH):
+        raise SystemExit('libotr.so missing: run python __graft_entry__.py build first')
+
+    gdir = os.path.join(ROOT, 'build', 'graphs')
+    if rank == 0:
+        gpath = gen.graph_path('metro', gdir)
+    barrier()
+    gpath = gen.graph_path('metro', gdir)
+
+    # traces: all ranks generate the same global set, keep their uuid-hash shard
+    n_global = args.traces_per_gpu * world
+    t0 = time.time()
+    allt = gen.make_traces(gpath, n_global, 100, 15, 10.0, 2, t_begin=T_BEGIN, t_spread=1800)
+    if world > 1:
+        shard = np.array([int(hashlib.sha1(u.encode()).hexdigest()[:3], 16) % world for u in allt.uuids])
+        mine = allt.subset(np.flatnonzero(shard == rank))
+    else:
+        mine = allt
+    log('rank %d: %d traces, %d probes (gen %.1fs)' % (rank, mine.n_traces, mine.n_probes, time.time() - t0))
+
+    M.configure(M.default_config(gpath, device=local))
+    n_nodes, n_edges, n_segments = M.graph_info()
+    m = M.Matcher()
+
+    dev = torch.device('cuda', local)
+    t_off = torch.from_numpy(mine.offsets).to(dev)
+    t_lat = torch.from_numpy(mine.lat).to(dev)
+    t_lon = torch.from_numpy(mine.lon).to(dev)
+    t_time = torch.from_numpy(mine.time).to(dev)
+    t_mode = torch.from_numpy(mine.mode).to(dev)
+    darr = {'trace_offsets': t_off.data_ptr(), 'lat': t_lat.data_ptr(), 'lon': t_lon.data_ptr(),
+            'time': t_time.data_ptr(), 'mode': t_mode.data_ptr()}
+    hours = 3  # traces start within 30 min of T_BEGIN and last 25 min
+    hist_len = hours * n_segments * _lib.HIST_BINS
+    hist_len += (-hist_len) % world
+    hist = torch.zeros(hist_len, dtype=torch.int32, device=dev)
+    hist_out = torch.zeros(hist_len // world, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        r = m.match_batch(mine, device_arrays=darr, hist_device=hist.data_ptr(), hist_hours=hours,
+                          hist_base_time=T_BEGIN, copy_out=False, timing=True)
+        if r.status != 0:
+            raise RuntimeError('batch status %d (%d overflow tasks)' % (r.status, r.n_overflow_traces))
+        if world > 1:
+            dist.reduce_scatter_tensor(hist_out, hist, op=dist.ReduceOp.SUM)
+            torch.cuda.current_stream().synchronize()
+        return r
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    t_start = time.perf_counter()
+    route_ms, results = [], []
+    for _ in range(args.steps):
+        r = step()
+        route_ms.append(r.kernel_ms[_lib.STAGES.index('route')])
+        results.append(r)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    probes = torch.tensor([float(mine.n_probes)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(probes, op=dist.ReduceOp.SUM)
+    elapsed = float(el.item())
+    total_probes = float(probes.item())
+    value = total_probes * args.steps / elapsed
+
+    r = results[-1]
+    counters = list(r.counters)
+    stage_ms = {s: round(float(r.kernel_ms[i]), 3) for i, s in enumerate(_lib.STAGES) if r.kernel_ms[i] > 0}
+    route_avg_ms = float(np.mean(route_ms))
+    rbytes = route_bytes(counters, counters[5], counters[6])
+    achieved = rbytes / (route_avg_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_traces > 0:
+        from oracle import pyoracle as po
+        g = po.Graph(gpath)
+        sample = mine.subset(np.arange(min(args.cpu_traces, mine.n_traces)))
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        tc = time.perf_counter()
+        po.match_batch(g, sample, po.params(), threads=threads)
+        dt = time.perf_counter() - tc
+        cpu = {'value': round(sample.n_probes / dt, 1), 'unit': 'probes/s', 'cores': threads, 'kind': 'port',
+               'sample': '%d traces x 100 probes of the same C2 workload through oracle/liboracle.so '
+                         '(scalar C restatement, %d pthreads, %.1f s)' % (sample.n_traces, threads, dt)}
+
+    if rank == 0:
+        line = {
+            'metric': 'GPS probes matched/sec (whole node)',
+            'value': round(value, 1),
+            'unit': 'probes/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(1e3 * elapsed / args.steps, 3),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f64',
+            'data': 'synthetic',
+            'config': {'workload': 'C2: metro street grid (%d nodes, %d directed edges, %d OSMLR segments), '
+                                   '%d traces x 100 probes per GPU @15 s, sigma 10 m' % (
+                                       n_nodes, n_edges, n_segments, args.traces_per_gpu),
+                       'probes_per_step': int(total_probes),
+                       'parallelism': 'uuid-sharded dp%d + RCCL reduce-scatter of [hour][segment][speed] histogram'
+                                      % world if world > 1 else 'single GPU',
+                       'stage_ms': stage_ms},
+            'roofline': {'kernel': 'k_route<512> (K3 bounded one-to-many search + K4 transition)',
+                         'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
+                         'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': None,
+                         'launch_ms': round(route_avg_ms, 3), 'algorithmic_bytes': int(rbytes),
+                         'settled_nodes': int(counters[3]), 'relaxed_edges': int(counters[4]),
+                         'tasks': int(counters[5]), 'transition_entries': int(counters[6])},
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -88,12 +88,18 @@ typedef struct otr_trace_batch {
   int64_t hist_base_time;      /* histogram covers [base, base + hist_hours*quantisation) */
   int32_t hist_hours;
   int32_t flags;               /* OTR_BATCH_* */
+  uint32_t* hist_device;       /* optional caller-owned device histogram (else library-owned) */
 } otr_trace_batch;
 
 #define OTR_BATCH_COPY_OUT 1   /* fill the host arrays of otr_batch_result */
 #define OTR_BATCH_TIMING 2     /* record per-kernel HIP-event timings */
 
 #define OTR_NO_ID 0xFFFFFFFFFFFFFFFFull
+
+/* kernel_ms slots */
+enum { OTR_STAGE_STATES = 0, OTR_STAGE_CANDIDATES, OTR_STAGE_LINK, OTR_STAGE_ROUTE, OTR_STAGE_ROUTE_BIG,
+       OTR_STAGE_VITERBI, OTR_STAGE_PATHS, OTR_STAGE_PATHS_BIG, OTR_STAGE_SEGMENTS, OTR_STAGE_HISTOGRAM,
+       OTR_STAGE_TOTAL };
 #define OTR_HIST_BINS 8        /* speed bins of 20 km/h: [0,20) … [140,∞) */
 
 /* All pointers below are owned by the matcher and stay valid until the next batch
@@ -124,8 +130,10 @@ typedef struct otr_batch_result {
   int64_t hist_len;            /* elements */
   /* algorithmic byte counters, summed over the batch */
   uint64_t counters[8];        /* 0 cells visited, 1 segment tests, 2 candidates, 3 settled nodes,
-                                  4 relaxed edges, 5 route tasks, 6 viterbi cells, 7 output segments */
-  float kernel_ms[16];         /* OTR_BATCH_TIMING: per-stage device time */
+                                  4 relaxed edges (first-tier route launch), 5 route tasks,
+                                  6 transition entries, 7 output segments */
+  uint64_t big_counters[2];    /* settled / relaxed of the large-table retry launch */
+  float kernel_ms[16];         /* OTR_BATCH_TIMING: device time per stage, OTR_STAGE_* */
 } otr_batch_result;
 
 int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result* out);

@@ -18,6 +18,8 @@ OTR_BATCH_TIMING = 2
 OTR_NO_ID = 0xFFFFFFFFFFFFFFFF
 HIST_BINS = 8
 KMAX = 64
+STAGES = ['states', 'candidates', 'link', 'route', 'route_big', 'viterbi', 'paths', 'paths_big', 'segments',
+          'histogram']
 
 # every symbol include/otr.h declares
 EXPORTS = ['otr_configure', 'otr_configure_json', 'otr_matcher_new', 'otr_matcher_free', 'otr_match',
@@ -31,7 +33,8 @@ class TraceBatch(ctypes.Structure):
                 ('time', ctypes.c_void_p), ('accuracy', ctypes.c_void_p), ('mode', ctypes.c_void_p),
                 ('report_levels', ctypes.c_uint32), ('transition_levels', ctypes.c_uint32),
                 ('threshold_sec', ctypes.c_int32), ('quantisation', ctypes.c_int32),
-                ('hist_base_time', ctypes.c_int64), ('hist_hours', ctypes.c_int32), ('flags', ctypes.c_int32)]
+                ('hist_base_time', ctypes.c_int64), ('hist_hours', ctypes.c_int32), ('flags', ctypes.c_int32),
+                ('hist_device', ctypes.c_void_p)]
 
 
 class BatchResult(ctypes.Structure):
@@ -54,7 +57,8 @@ class BatchResult(ctypes.Structure):
                 ('rep_length', P(ctypes.c_int32)), ('rep_queue', P(ctypes.c_int32)),
                 ('shape_used', P(ctypes.c_int32)), ('stats', P(ctypes.c_int32)),
                 ('stats_len', P(ctypes.c_double)), ('d_hist', ctypes.c_void_p), ('hist_len', ctypes.c_int64),
-                ('counters', ctypes.c_uint64 * 8), ('kernel_ms', ctypes.c_float * 16)]
+                ('counters', ctypes.c_uint64 * 8), ('big_counters', ctypes.c_uint64 * 2),
+                ('kernel_ms', ctypes.c_float * 16)]
 
 
 _L = None

@@ -235,9 +235,15 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     ev_init = true;
   }
   const bool timing = (in->flags & OTR_BATCH_TIMING) != 0;
-  int evn = 0;
-  auto mark = [&]() {
-    if (timing && evn < 20) (void)hipEventRecord(ev[evn++], stream);
+  bool used[10] = {false};
+  auto tb = [&](int k) {
+    if (timing) (void)hipEventRecord(ev[2 * k], stream);
+  };
+  auto te = [&](int k) {
+    if (timing) {
+      (void)hipEventRecord(ev[2 * k + 1], stream);
+      used[k] = true;
+    }
   };
   memset(out, 0, sizeof(*out));
   const int32_t T = in->n_traces;
@@ -282,8 +288,8 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     b.acc = in->accuracy;
   }
   out->n_probes = N;
-  unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, 16);
-  HIPCHK(hipMemsetAsync(d_counters, 0, 16 * 8, stream));
+  unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, 32);
+  HIPCHK(hipMemsetAsync(d_counters, 0, 32 * 8, stream));
   size_t scan_bytes = 0;
   auto scan = [&](const int64_t* src, int64_t* dst_np1, int64_t n) -> int {
     // dst[0] = 0, dst[1..n] = inclusive prefix sums
@@ -302,11 +308,12 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     return OTR_OK;
   };
   int rc;
-  mark();  // 0
   // ---- K0: states
   int64_t* state_cnt = need<int64_t>(S_STATE_CNT, T);
   int64_t* trace_state_off = need<int64_t>(S_TRACE_STATE_OFF, T + 1);
+  tb(OTR_STAGE_STATES);
   k_select_states<<<grid_for(T, 256), 256, 0, stream>>>(b, mp, state_cnt, nullptr, nullptr, nullptr);
+  te(OTR_STAGE_STATES);
   if ((rc = scan(state_cnt, trace_state_off, T))) return rc;
   int64_t S = 0;
   if ((rc = read_i64(trace_state_off + T, &S))) return rc;
@@ -315,7 +322,6 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   int32_t* state_trace = need<int32_t>(S_STATE_TRACE, S);
   k_select_states<<<grid_for(T, 256), 256, 0, stream>>>(b, mp, state_cnt, trace_state_off, state_probe,
                                                         state_trace);
-  mark();  // 1
   // ---- K1: candidates
   CandBuf cb;
   cb.edge = need<uint32_t>(S_CAND_EDGE, (size_t)S * OTR_KMAX);
@@ -328,9 +334,10 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   }
   if (S > 0) {
     unsigned gridc = (unsigned)(S < 1048576 ? S : 1048576);
+    tb(OTR_STAGE_CANDIDATES);
     k_candidates<<<gridc, 64, 0, stream>>>(g, b, mp, S, state_probe, state_trace, cb, d_counters);
+    te(OTR_STAGE_CANDIDATES);
   }
-  mark();  // 2
   // ---- K_link + task map
   StepBuf sb;
   sb.prev = need<int64_t>(S_PREV, S);
@@ -341,7 +348,9 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   sb.ntrans = need<int64_t>(S_NTRANS, S);
   int64_t* task_off = need<int64_t>(S_TASK_OFF, S + 1);
   int64_t* trans_off = need<int64_t>(S_TRANS_OFF, S + 1);
+  tb(OTR_STAGE_LINK);
   k_link<<<grid_for(T, 256), 256, 0, stream>>>(b, mp, trace_state_off, state_probe, cb.count, sb);
+  te(OTR_STAGE_LINK);
   if ((rc = scan(sb.ntask, task_off, S))) return rc;
   if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
   int64_t NT = 0, NTR = 0;
@@ -357,7 +366,6 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   }
   if (S > 0) k_taskmap<<<grid_for(S, 256), 256, 0, stream>>>(S, task_off, task_state, task_src);
   if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
-  mark();  // 3
   // ---- K3/K4: routing + transition costs
   RouteArgs ra{};
   ra.task_state = task_state;
@@ -380,7 +388,9 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   ra.overflow_flag = task_ovf;
   if (NT > 0) {
     unsigned gr = (unsigned)(NT < 4194304 ? NT : 4194304);
+    tb(OTR_STAGE_ROUTE);
     k_route<512><<<gr, 64, 0, stream>>>(g, ra, d_counters);
+    te(OTR_STAGE_ROUTE);
     // overflow retry with the large table
     int64_t* list = need<int64_t>(S_LIST, NT);
     unsigned long long* cnt = need<unsigned long long>(S_MISC, 4);
@@ -394,7 +404,9 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.n_tasks = (int64_t)novf;
-      k_route<8192><<<(unsigned)(novf < 65536 ? novf : 65536), 64, 0, stream>>>(g, rb, d_counters);
+      tb(OTR_STAGE_ROUTE_BIG);
+      k_route<8192><<<(unsigned)(novf < 65536 ? novf : 65536), 64, 0, stream>>>(g, rb, d_counters + 16);
+      te(OTR_STAGE_ROUTE_BIG);
       HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
       k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
       HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
@@ -402,7 +414,6 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       out->n_overflow_traces += (int32_t)novf;
     }
   }
-  mark();  // 4
   // ---- K5: Viterbi
   ViterbiArgs va{};
   va.n_traces = T;
@@ -419,8 +430,9 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   va.end_win = need<int32_t>(S_END_WIN, S);
   va.winner = need<int32_t>(S_WINNER, S);
   va.subpath = need<int32_t>(S_SUBPATH, S);
+  tb(OTR_STAGE_VITERBI);
   k_viterbi<<<(unsigned)(T < 1048576 ? T : 1048576), 64, 0, stream>>>(va, d_counters);
-  mark();  // 5
+  te(OTR_STAGE_VITERBI);
   // ---- K6: winner paths
   int64_t* path_off = need<int64_t>(S_PATH_OFF, S);
   int32_t* path_len = need<int32_t>(S_PATH_LEN, S);
@@ -462,8 +474,10 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       pa.capacity = capacity;
       pa.overflow_flag = step_ovf;
       pa.cap_flag = (int32_t*)(cnt + 2);
+      tb(OTR_STAGE_PATHS);
       k_paths<512><<<(unsigned)(nsteps < 4194304 ? nsteps : 4194304), 64, 0, stream>>>(g, pa, nullptr,
                                                                                       (int64_t)nsteps);
+      te(OTR_STAGE_PATHS);
       // large-table retry for table overflows
       int64_t* rl = need<int64_t>(S_TASK_STATE, NT > (int64_t)nsteps ? NT : (int64_t)nsteps);  // reuse
       unsigned long long* c2 = cnt + 3;
@@ -474,8 +488,10 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       HIPCHK(hipStreamSynchronize(stream));
       if (host[2] > 0) {
         HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
+        tb(OTR_STAGE_PATHS_BIG);
         k_paths<8192><<<(unsigned)(host[2] < 65536 ? host[2] : 65536), 64, 0, stream>>>(g, pa, rl,
                                                                                         (int64_t)host[2]);
+        te(OTR_STAGE_PATHS_BIG);
         HIPCHK(hipMemcpyAsync(host, cnt + 1, 16, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
       }
@@ -483,7 +499,6 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       capacity = (int64_t)host[0] + (int64_t)host[0] / 2 + 1024;  // grow and redo
     }
   }
-  mark();  // 6
   // ---- K7: stitching, segments, report()
   int64_t* cap = need<int64_t>(S_CAP, T);
   int64_t* cap_off = need<int64_t>(S_CAP_OFF, T + 1);
@@ -536,8 +551,9 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   sa.threshold = (double)(in->threshold_sec >= 0 ? in->threshold_sec : 15);
   sa.report_levels = in->report_levels;
   sa.transition_levels = in->transition_levels;
+  tb(OTR_STAGE_SEGMENTS);
   k_segments<<<grid_for(T, 64), 64, 0, stream>>>(g, sa, d_counters);
-  mark();  // 7
+  te(OTR_STAGE_SEGMENTS);
   // ---- K8: hour buckets → histogram
   HistArgs ha{};
   ha.b = b;
@@ -555,21 +571,26 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   ha.n_segments = g.n_segments;
   ha.n_rows = d_counters + 8;
   size_t hist_len = (size_t)(in->hist_hours > 0 ? in->hist_hours : 0) * g.n_segments * OTR_HIST_BINS;
-  ha.hist = hist_len ? need<uint32_t>(S_HIST, hist_len) : nullptr;
+  ha.hist = hist_len ? (in->hist_device ? in->hist_device : need<uint32_t>(S_HIST, hist_len)) : nullptr;
   if (hist_len) HIPCHK(hipMemsetAsync(ha.hist, 0, hist_len * 4, stream));
+  tb(OTR_STAGE_HISTOGRAM);
   k_histogram<<<grid_for(T, 256), 256, 0, stream>>>(ha);
-  mark();  // 8
+  te(OTR_STAGE_HISTOGRAM);
   HIPCHK(hipGetLastError());
-  unsigned long long hc[16];
+  unsigned long long hc[32];
   HIPCHK(hipMemcpyAsync(hc, d_counters, sizeof(hc), hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
   for (int k = 0; k < 8; ++k) out->counters[k] = hc[k];
   out->counters[5] = (uint64_t)NT;
+  out->counters[6] = (uint64_t)NTR;
+  out->big_counters[0] = hc[16 + 3];
+  out->big_counters[1] = hc[16 + 4];
   out->n_rows = (int64_t)hc[8];
   out->d_hist = ha.hist;
   out->hist_len = (int64_t)hist_len;
   if (timing)
-    for (int k = 0; k + 1 < evn && k < 16; ++k) (void)hipEventElapsedTime(&out->kernel_ms[k], ev[k], ev[k + 1]);
+    for (int k = 0; k < 10; ++k)
+      if (used[k]) (void)hipEventElapsedTime(&out->kernel_ms[k], ev[2 * k], ev[2 * k + 1]);
   // ---- copy-out (tests / JSON path), compacting the capacity layout
   std::vector<int64_t> route_n(T), seg_n(T), way_n(T), rep_n(T), h_cap_off(T + 1);
   HIPCHK(hipMemcpy(route_n.data(), sa.route_n, 8 * T, hipMemcpyDeviceToHost));

@@ -586,7 +586,6 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
             }
           }
         }
-        cells += (unsigned long long)Kp;
         const bool any = __ballot(lane < K && bi >= 0) != 0ull;
         if (!any) {
           brk = true;
@@ -645,8 +644,8 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
     }
     __syncthreads();
   }
-  for (int off = 32; off > 0; off >>= 1) cells += __shfl_xor(cells, off);
-  if (lane == 0 && counters) atomicAdd(&counters[6], cells);
+  (void)cells;
+  (void)counters;
 }
 
 // ------------------------------------------------------------------------------
@@ -789,17 +788,6 @@ struct SegArgs {
   uint32_t report_levels, transition_levels;
 };
 
-struct TimeCursor {  // time_at() of the oracle with a forward-moving pointer
-  const double* pos;
-  const double* tm;
-  int n, k;
-  __device__ double at(double s) {
-    while (k < n - 2 && s > pos[k + 1]) ++k;
-    if (pos[k + 1] > pos[k]) return tm[k] + (tm[k + 1] - tm[k]) * ((s - pos[k]) / (pos[k + 1] - pos[k]));
-    return tm[k];
-  }
-};
-
 __global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= a.b.n_traces) return;
@@ -843,15 +831,9 @@ __global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) 
       for (int z = 0; z < pl; ++z) s = s + (double)g.edge_len[a.path[a.path_off[sj] + z]];
       pos[q] = s + pj * (double)g.edge_len[ej];
     }
-    // state times (binary64 of the integer epoch seconds)
-    // pass 2: portions → groups, streaming
+    // pass 2: portions → groups, streaming.  time_at() of the oracle with a
+    // forward-moving pointer (queries are non-decreasing route positions).
     const int nst = sb - sa + 1;
-    double* tms = a.pos + eo + 0;  // not used: times read on the fly below
-    (void)tms;
-    // time cursor over (pos, time) of states sa..sb; times materialised in a small ring
-    // (we need random access by k in TimeCursor): reuse `act` tail? keep it simple:
-    // materialise into the per-state scratch after `pos` (pos has eo-so slots; use
-    // the second half of a.act reinterpreted is unsafe) — use a local fetcher instead.
     struct {
       const double* pos;
       const int64_t* act;

@@ -40,7 +40,7 @@ def lib():
         L.otrgen_traces.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                     ctypes.c_uint64, ctypes.c_double, ctypes.c_double, P(ctypes.c_double),
                                     P(ctypes.c_double), P(ctypes.c_int64), P(ctypes.c_uint8),
-                                    P(ctypes.c_uint32)]
+                                    P(ctypes.c_uint32), ctypes.c_int64, ctypes.c_int64]
         L.otrgen_traces.restype = ctypes.c_int
         _LIB = L
     return _LIB
@@ -92,8 +92,11 @@ class Traces:
                       self.mode[idx].copy(), acc, tr, uu)
 
 
+T_BEGIN = 1483228800  # 2017-01-01T00:00:00Z
+
+
 def make_traces(graph, n_traces, n_points, sample_rate, sigma, seed, frac_bicycle=0.0, frac_ped=0.0,
-                point_accuracy=None, uuid_base=0):
+                point_accuracy=None, uuid_base=0, t_begin=T_BEGIN, t_spread=86400 * 7):
     n = n_traces * n_points
     lat = np.zeros(n, np.float64)
     lon = np.zeros(n, np.float64)
@@ -104,7 +107,8 @@ def make_traces(graph, n_traces, n_points, sample_rate, sigma, seed, frac_bicycl
     rc = lib().otrgen_traces(graph.encode(), n_traces, n_points, sample_rate, sigma, seed, frac_bicycle,
                              frac_ped, lat.ctypes.data_as(P(ctypes.c_double)),
                              lon.ctypes.data_as(P(ctypes.c_double)), tm.ctypes.data_as(P(ctypes.c_int64)),
-                             mode.ctypes.data_as(P(ctypes.c_uint8)), truth.ctypes.data_as(P(ctypes.c_uint32)))
+                             mode.ctypes.data_as(P(ctypes.c_uint8)), truth.ctypes.data_as(P(ctypes.c_uint32)),
+                             int(t_begin), int(t_spread))
     if rc != 0:
         raise RuntimeError('otrgen_traces failed: %d' % rc)
     off = np.arange(n_traces + 1, dtype=np.int64) * n_points

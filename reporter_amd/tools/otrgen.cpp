@@ -368,7 +368,8 @@ int otrgen_graph(const char* path, int rows, int cols, double spacing_m, double 
 // out_mode[t] receives 0/1/2.  point_accuracy < 0 means "no accuracy field".
 int otrgen_traces(const char* graph_path, int n_traces, int n_points, int sample_rate, double noise_m,
                   uint64_t seed, double frac_bicycle, double frac_pedestrian, double* out_lat,
-                  double* out_lon, int64_t* out_time, uint8_t* out_mode, uint32_t* out_truth_edge) {
+                  double* out_lon, int64_t* out_time, uint8_t* out_mode, uint32_t* out_truth_edge,
+                  int64_t t_begin, int64_t t_spread) {
   FILE* f = fopen(graph_path, "rb");
   if (!f) return -1;
   otr_graph_header h;
@@ -411,7 +412,7 @@ int otrgen_traces(const char* graph_path, int n_traces, int n_points, int sample
     };
     load_edge(e);
     double along = rng.uni() * cum.back();
-    int64_t t0 = 1483228800ll + (int64_t)rng.below(86400 * 7);
+    int64_t t0 = t_begin + (t_spread > 0 ? (int64_t)rng.below((uint32_t)t_spread) : 0);
     std::vector<double> adj_lon, adj_lat;
     int qlon = 0, qlat = 0;
     int kept = 0;
