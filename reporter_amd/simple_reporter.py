@@ -1,0 +1,178 @@
+"""Batch driver mirroring py/simple_reporter.py's match → bucket → cull stages over the
+batched HIP API.  S3 download/upload (simple_reporter.py:51-129, 247-254) is out of
+scope (network); inputs and outputs are local files.
+
+  shard_key(uuid)                  sha1(uuid)[0:3]                (:116)
+  windows(times, inactivity)       inactivity windows             (:150-160)
+  bucket(first, last, reports, q, mode, source)
+                                   filter + hour buckets → rows   (:176-196)
+  cull(lines, privacy)             privacy cull incl. the trailing-singleton merge (:218-239)
+  match_traces(traces, ...)        windows → otr_match_batch → rows per tile
+  report_tiles(tiles, privacy)     sort + cull                    (:211-245)
+"""
+import hashlib
+import math
+import os
+
+import numpy as np
+
+LEVEL_BITS = 3
+TILE_INDEX_BITS = 22
+SEGMENT_INDEX_BITS = 21
+LEVEL_MASK = (1 << LEVEL_BITS) - 1
+TILE_INDEX_MASK = (1 << TILE_INDEX_BITS) - 1
+SEGMENT_INDEX_MASK = (1 << SEGMENT_INDEX_BITS) - 1
+INVALID_SEGMENT_ID = (SEGMENT_INDEX_MASK << (TILE_INDEX_BITS + LEVEL_BITS)) | \
+    (TILE_INDEX_MASK << LEVEL_BITS) | LEVEL_MASK
+COLUMNS = 'segment_id,next_segment_id,duration,count,length,queue_length,minimum_timestamp,maximum_timestamp,' \
+          'source,vehicle_type'
+
+
+def get_tile_level(segment_id):
+    return segment_id & LEVEL_MASK
+
+
+def get_tile_index(segment_id):
+    return (segment_id >> LEVEL_BITS) & TILE_INDEX_MASK
+
+
+def shard_key(uuid):
+    return hashlib.sha1(uuid.encode() if isinstance(uuid, str) else uuid).hexdigest()[0:3]
+
+
+def shard_of(uuid, n):
+    """GPU (or worker) owning a vehicle: the simple_reporter hash prefix modulo n."""
+    return int(shard_key(uuid), 16) % n
+
+
+def windows(times, inactivity):
+    """[i, j) index ranges split at gaps > inactivity, dropping ranges shorter than 2."""
+    starts = [i for i in range(len(times)) if i == 0 or times[i] - times[i - 1] > inactivity]
+    out = []
+    for k, i in enumerate(starts):
+        j = starts[k + 1] if k + 1 < len(starts) else len(times)
+        if j - i >= 2:
+            out.append((i, j))
+    return out
+
+
+def py2_round_int(x):
+    """int(round(x)) with Python 2 half-away-from-zero on the exact binary value."""
+    f = math.floor(x)
+    return int(f + 1 if x - f >= 0.5 else f) if x >= 0 else -py2_round_int(-x)
+
+
+def _str_num(v):
+    if isinstance(v, float):  # Python 2 str(float): 12 significant digits
+        s = '%.12g' % v
+        if '.' not in s and 'e' not in s and 'n' not in s:
+            s += '.0'
+        return s
+    return str(v)
+
+
+def bucket(first_time, last_time, reports, quantisation, mode, source):
+    """{tile_key: [row lines]} for one window's report() output (simple_reporter.py:176-196).
+    tile_key = '{b*q}_{(b+1)*q-1}/{level}/{tile_index}'."""
+    tiles = {}
+    buckets = (last_time - first_time) // quantisation + 1
+    for r in reports:
+        if not (r['t0'] > 0 and r['t1'] > 0 and r['t1'] - r['t0'] > .5 and r['length'] > 0 and r['queue_length'] >= 0):
+            continue
+        duration = py2_round_int(r['t1'] - r['t0'])
+        start = int(math.floor(r['t0']))
+        end = int(math.ceil(r['t1']))
+        min_b = start // quantisation
+        max_b = end // quantisation
+        if max_b - min_b > buckets:
+            continue
+        for b in range(min_b, max_b + 1):
+            key = '%d_%d/%d/%d' % (b * quantisation, (b + 1) * quantisation - 1, get_tile_level(r['id']),
+                                   get_tile_index(r['id']))
+            row = [str(r['id']), str(r.get('next_id', INVALID_SEGMENT_ID)), str(duration), '1',
+                   _str_num(r['length']), _str_num(r['queue_length']), str(start), str(end), source, mode.upper()]
+            tiles.setdefault(key, []).append(','.join(row) + os.linesep)
+    return tiles
+
+
+def cull(lines, privacy):
+    """Delete (id,next_id) runs seen fewer than `privacy` times, on lexicographically
+    sorted lines.  Reproduces the reference loop exactly, including its quirk: a
+    trailing run of length 1 is judged together with the run before it."""
+    segs = list(lines)
+    start = 0
+    i = 0
+    while i < len(segs):
+        s = segs[start].split(',')
+        e = segs[i].split(',')
+        if s[0] != e[0] or s[1] != e[1] or i == len(segs) - 1:
+            if i == len(segs) - 1:
+                i += 1
+            if i - start < privacy:
+                del segs[start:i]
+                i = start
+            else:
+                start = i
+        i += 1
+    return segs
+
+
+def report_tiles(tiles, privacy):
+    """Sort (string order, :218) and cull each tile; drop empty tiles (:242-244)."""
+    out = {}
+    for key, lines in tiles.items():
+        kept = cull(sorted(lines), privacy)
+        if kept:
+            out[key] = kept
+    return out
+
+
+def match_traces(matcher, traces, mode='auto', report_levels=(0, 1), transition_levels=(0, 1),
+                 quantisation=3600, inactivity=120, source='smpl_rprt', threshold_sec=15):
+    """simple_reporter.match() over a batch: split each trace at inactivity gaps, match
+    all windows in ONE otr_match_batch call, bucket every window's reports."""
+    from .tools.gen import Traces
+    idx_lat, idx_lon, idx_time, offs, modes = [], [], [], [0], []
+    win_src = []
+    for t in range(traces.n_traces):
+        a, b = int(traces.offsets[t]), int(traces.offsets[t + 1])
+        order = np.argsort(traces.time[a:b], kind='stable') + a  # :146 sort by time
+        tm = traces.time[order]
+        for i, j in windows(tm.tolist(), inactivity):
+            sel = order[i:j]
+            idx_lat.append(traces.lat[sel])
+            idx_lon.append(traces.lon[sel])
+            idx_time.append(traces.time[sel])
+            offs.append(offs[-1] + len(sel))
+            modes.append(traces.mode[t])
+            win_src.append(t)
+    if not win_src:
+        return {}
+    batch = Traces(np.concatenate(idx_lat), np.concatenate(idx_lon), np.concatenate(idx_time),
+                   np.asarray(offs, np.int64), np.asarray(modes, np.uint8))
+    r = matcher.match_batch_numpy(batch, report_levels=report_levels, transition_levels=transition_levels,
+                                  threshold_sec=threshold_sec, quantisation=quantisation)
+    tiles = {}
+    for w in range(batch.n_traces):
+        lo, hi = r['trace_rep_off'][w], r['trace_rep_off'][w + 1]
+        reps = []
+        for k in range(lo, hi):
+            d = {'id': int(r['rep_id'][k]), 't0': float(r['rep_t0'][k]), 't1': float(r['rep_t1'][k]),
+                 'length': int(r['rep_length'][k]), 'queue_length': int(r['rep_queue'][k])}
+            if int(r['rep_next'][k]) != 0xFFFFFFFFFFFFFFFF:
+                d['next_id'] = int(r['rep_next'][k])
+            reps.append(d)
+        first, last = int(batch.time[batch.offsets[w]]), int(batch.time[batch.offsets[w + 1] - 1])
+        for key, rows in bucket(first, last, reps, quantisation, mode, source).items():
+            tiles.setdefault(key, []).extend(rows)
+    return tiles
+
+
+def write_tiles(tiles, dest_dir):
+    """Tile files with the reference's CSV header (simple_reporter.py:252)."""
+    for key, lines in tiles.items():
+        path = os.path.join(dest_dir, key)
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, 'w') as f:
+            f.write(COLUMNS + os.linesep)
+            f.write(''.join(lines))

@@ -1,0 +1,115 @@
+"""Hand-built road graphs with known matching answers: straight
+road, turn at a junction, one-way dual carriageway 20 m apart, disconnected roads
+(breakage).  Used by the oracle known-answer tests and the GPU parity tests."""
+import math
+import os
+
+import numpy as np
+
+from reporter_amd.graphfile import write_graph
+from reporter_amd.tools.gen import Traces
+
+LAT0, LON0 = 14.55, 121.03
+M = 20037581.187 / 180.0
+MLON = M * math.cos(math.radians(LAT0))
+
+
+def ll(x_m, y_m):
+    """local metres east/north of (LAT0, LON0) → (lat, lon)"""
+    return (LAT0 + y_m / M, LON0 + x_m / MLON)
+
+
+def osmlr(level, tile, idx):
+    return (idx << 25) | (tile << 3) | level
+
+
+def two_way(edges, a, b, way, **kw):
+    edges.append(dict(src=a, dst=b, way=way, **kw))
+    edges.append(dict(src=b, dst=a, way=way, **kw))
+    return len(edges) - 2, len(edges) - 1
+
+
+def build(path):
+    """Returns (new_id map, dict of named things). Layout (metres):
+       main street y=0: nodes A0..A5 at x=0,100,...,500 (two-way, level 1)
+       side street x=200 going north: B1 (200,100), B2 (200,200)  (two-way, level 2)
+       dual carriageway at y=400 (eastbound, one-way) and y=380 (westbound), x=0..300
+       island road far away at y=2000: I0..I2 (disconnected)"""
+    nodes, names = [], {}
+
+    def node(name, x, y):
+        names[name] = len(nodes)
+        nodes.append(ll(x, y))
+    for k in range(6):
+        node('A%d' % k, 100 * k, 0)
+    node('B1', 200, 100)
+    node('B2', 200, 200)
+    for k in range(4):
+        node('N%d' % k, 100 * k, 400)
+        node('S%d' % k, 100 * k, 380)
+    for k in range(3):
+        node('I%d' % k, 100 * k, 2000)
+    edges = []
+    ids = {}
+    for k in range(5):
+        f, r = two_way(edges, names['A%d' % k], names['A%d' % (k + 1)], 10 + k // 3, level=1, speed=50)
+        ids['A%d>' % k], ids['A%d<' % k] = f, r
+    ids['B0^'], ids['B0v'] = two_way(edges, names['A2'], names['B1'], 20, speed=30)
+    ids['B1^'], ids['B1v'] = two_way(edges, names['B1'], names['B2'], 20, speed=30)
+    for k in range(3):
+        edges.append(dict(src=names['N%d' % k], dst=names['N%d' % (k + 1)], way=30, speed=50, level=1))
+        ids['N%d>' % k] = len(edges) - 1
+        edges.append(dict(src=names['S%d' % (k + 1)], dst=names['S%d' % k], way=31, speed=50, level=1))
+        ids['S%d<' % k] = len(edges) - 1
+    for k in range(2):
+        ids['I%d>' % k], ids['I%d<' % k] = two_way(edges, names['I%d' % k], names['I%d' % (k + 1)], 40)
+    segs = [
+        dict(id=osmlr(1, 100, 1), edges=[ids['A0>']]),
+        dict(id=osmlr(1, 100, 2), edges=[ids['A1>'], ids['A2>']]),
+        dict(id=osmlr(1, 100, 3), edges=[ids['A3>'], ids['A4>']]),
+        dict(id=osmlr(1, 100, 4), edges=[ids['A4<'], ids['A3<'], ids['A2<'], ids['A1<'], ids['A0<']]),
+        dict(id=osmlr(2, 200, 1), edges=[ids['B0^'], ids['B1^']]),
+        dict(id=osmlr(1, 100, 5), edges=[ids['N0>'], ids['N1>'], ids['N2>']]),
+        dict(id=osmlr(1, 100, 6), edges=[ids['S2<'], ids['S1<'], ids['S0<']]),
+        dict(id=osmlr(2, 300, 1), edges=[ids['I0>'], ids['I1>']]),
+    ]
+    new = write_graph(path, nodes, edges, segs)
+    return {k: int(new[v]) for k, v in ids.items()}, {s['id']: i for i, s in enumerate(segs)}, segs
+
+
+def trace(points, t0=1483228800, dt=2):
+    """points: [(x_m, y_m)] every dt seconds."""
+    lat = np.array([ll(x, y)[0] for x, y in points])
+    lon = np.array([ll(x, y)[1] for x, y in points])
+    lat = np.round(lat, 6)
+    lon = np.round(lon, 6)
+    tm = t0 + dt * np.arange(len(points), dtype=np.int64)
+    return lat, lon, tm
+
+
+def batch(traces, modes=None):
+    lats, lons, tms, offs = [], [], [], [0]
+    for la, lo, tm in traces:
+        lats.append(la)
+        lons.append(lo)
+        tms.append(tm)
+        offs.append(offs[-1] + len(la))
+    modes = np.zeros(len(traces), np.uint8) if modes is None else np.asarray(modes, np.uint8)
+    return Traces(np.concatenate(lats), np.concatenate(lons), np.concatenate(tms), np.asarray(offs, np.int64),
+                  modes)
+
+
+def scenarios():
+    """name → list of (x,y) points, driven at 10 m/s, sampled every 2 s (20 m)."""
+    s = {}
+    # straight east along the main street, from x=30 to x=470, 3 m north of the centreline
+    s['straight_east'] = [(30 + 20 * k, 3) for k in range(23)]
+    # east to the junction at x=200, then north up the side street
+    s['turn_north'] = [(40 + 20 * k, -2) for k in range(8)] + [(202, 20 + 20 * k) for k in range(9)]
+    # eastbound on the north carriageway with noise pulling toward the westbound one
+    s['dual_carriageway'] = [(20 + 20 * k, 393 - 2 * (k % 3)) for k in range(14)]
+    # westbound on main street
+    s['straight_west'] = [(480 - 20 * k, -3) for k in range(23)]
+    # jump to a disconnected road → breakage into two sub-paths
+    s['breakage'] = [(30 + 20 * k, 2) for k in range(6)] + [(20 + 20 * k, 2002) for k in range(6)]
+    return s

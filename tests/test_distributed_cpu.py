@@ -1,0 +1,79 @@
+"""N>1 path on CPU: world_size-2 gloo ranks shard traces by uuid hash
+(simple_reporter.py:116), each matches its shard (CPU oracle stands in for the GPU
+here), builds the [hour][segment][speed] histogram, and the cross-rank combine
+(all-reduce-sum then owner slice, the gloo analogue of the RCCL reduce-scatter in
+bench.py) equals the single-process histogram of the whole set."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _workload(graph_dir):
+    from reporter_amd.tools import gen
+    path = gen.graph_path('tiny', graph_dir)
+    tr = gen.make_traces(path, 40, 30, 5, 8.0, 5, t_begin=gen.T_BEGIN, t_spread=1800)
+    return path, tr
+
+
+def _hist_for(path, tr):
+    from oracle import pyoracle as po
+    from oracle.hist import histogram
+    from reporter_amd.graphfile import GraphFile
+    G = GraphFile(path)
+    idx = {int(s): i for i, s in enumerate(G.seg_id)}
+    r = po.match_batch(po.Graph(path), tr, po.params())
+    first = tr.time[tr.offsets[:-1]]
+    last = tr.time[tr.offsets[1:] - 1]
+    return histogram(r, first, last, idx, len(G.seg_id), __import__('reporter_amd.tools.gen').tools.gen.T_BEGIN, 2)
+
+
+def _rank(rank, world, port, graph_dir, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from reporter_amd import simple_reporter as sr
+    path, tr = _workload(graph_dir)
+    mine = np.array([i for i, u in enumerate(tr.uuids) if sr.shard_of(u, world) == rank])
+    h, rows = _hist_for(path, tr.subset(mine))
+    t = torch.from_numpy(h.reshape(-1).copy())
+    pad = (-t.numel()) % world
+    t = torch.cat([t, torch.zeros(pad, dtype=t.dtype)])
+    dist.all_reduce(t)                       # gloo: reduce-scatter = all-reduce + owner slice
+    n = t.numel() // world
+    own = t[rank * n:(rank + 1) * n].clone()
+    gathered = [torch.zeros_like(own) for _ in range(world)]
+    dist.all_gather(gathered, own)
+    cnt = torch.tensor([len(mine)])
+    dist.all_reduce(cnt)
+    if rank == 0:
+        np.save(out, torch.cat(gathered)[:h.size].numpy())
+        np.save(out + '.cnt.npy', cnt.numpy())
+    dist.destroy_process_group()
+
+
+def test_two_rank_shard_and_combine(tmp_path, graph_dir):
+    world = 2
+    out = str(tmp_path / 'hist.npy')
+    mp.spawn(_rank, args=(world, _free_port(), graph_dir, out), nprocs=world, join=True)
+    path, tr = _workload(graph_dir)
+    whole, rows = _hist_for(path, tr)
+    combined = np.load(out)
+    assert int(np.load(out + '.cnt.npy')[0]) == tr.n_traces  # shards partition the traces
+    assert rows > 0 and whole.sum() > 0
+    assert np.array_equal(combined, whole.reshape(-1))

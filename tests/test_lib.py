@@ -1,0 +1,49 @@
+"""The C-ABI library loads and exports every symbol include/otr.h declares (no GPU call)."""
+import ctypes
+import os
+import re
+
+from reporter_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_exports_match_header():
+    hdr = open(os.path.join(ROOT, 'include', 'otr.h')).read()
+    declared = set(re.findall(r'\b(otr_[a-z_]+)\s*\(', hdr))
+    assert declared == set(_lib.EXPORTS)
+    L = _lib.lib()
+    for s in declared:
+        assert hasattr(L, s), s
+
+
+def test_struct_layout():
+    # otr_trace_batch / otr_batch_result sizes must match the C declarations
+    assert ctypes.sizeof(_lib.TraceBatch) == 4 + 4 + 6 * 8 + 4 * 4 + 8 + 4 + 4 + 8
+    assert ctypes.sizeof(_lib.BatchResult) > 0
+
+
+def test_not_configured_errors():
+    from reporter_amd import matcher as M
+    # a bad config fails loudly (no fallback)
+    try:
+        M.configure({'otr': {'graph': '/nonexistent.otrg'}})
+    except RuntimeError as e:
+        assert 'graph' in str(e) or 'open' in str(e)
+    else:
+        raise AssertionError('configure should fail')
+
+
+def test_report_request_validation_without_gpu():
+    """otr_report's 400 paths (reporter_service.py:214-235) run before any device call."""
+    from reporter_amd import matcher as M
+    m = M.Matcher()
+    code, body = m.report_json('{"trace":[]}')
+    assert (code, body) == (400, '{"error":"uuid is required"}')
+    code, body = m.report_json('{"uuid":"a","trace":[{"lat":1,"lon":2,"time":3}]}')
+    assert code == 400 and 'non zero length array' in body
+    code, body = m.report_json('{"uuid":"a","trace":[{"lat":1,"lon":2,"time":3},{"lat":1,"lon":2,"time":4}]}')
+    assert (code, body) == (400, '{"error":"match_options must include report_levels array"}')
+    code, body = m.report_json('{"uuid":"a","match_options":{"report_levels":[0]},'
+                               '"trace":[{"lat":1,"lon":2,"time":3},{"lat":1,"lon":2,"time":4}]}')
+    assert (code, body) == (400, '{"error":"match_options must include transition_levels array"}')
