@@ -35,13 +35,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def route_bytes(counters, n_tasks, n_trans):
-    """Algorithmic HBM bytes of one k_route launch:
-    per settled node 8 B (CSR row pair), per relaxed edge 16 B (packed edge record),
-    per task 64 B (task map, step metadata, source candidate), per transition entry
-    28 B (target candidate edge+fraction 12 B, target edge src+len 8 B, cost write 8 B)."""
-    settled, relaxed = counters[3], counters[4]
-    return 8 * settled + 16 * relaxed + 64 * n_tasks + 28 * n_trans
+def route_bytes(c):
+    """Algorithmic HBM bytes of one k_route<512> launch, from the
+    device work counters: 64 B per task (task record, step metadata, root lookup),
+    32 B per settled node (its adjacency record), 16 B per source candidate
+    (edge, fraction, length), 20 B per target read (edge, fraction, src, length),
+    8 B per transition entry written."""
+    tasks, settled, trans, targets, sources = c[5], c[3], c[6], c[11], c[12]
+    return 64 * tasks + 32 * settled + 16 * sources + 20 * targets + 8 * trans
 
 
 def main():
@@ -145,7 +146,7 @@ def main():
     counters = list(r.counters)
     stage_ms = {s: round(float(r.kernel_ms[i]), 3) for i, s in enumerate(_lib.STAGES) if r.kernel_ms[i] > 0}
     route_avg_ms = float(np.mean(route_ms))
-    rbytes = route_bytes(counters, counters[5], counters[6])
+    rbytes = route_bytes(counters)
     achieved = rbytes / (route_avg_ms * 1e-3) / 1e9
 
     cpu = None
@@ -187,7 +188,9 @@ def main():
                          'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': None,
                          'launch_ms': round(route_avg_ms, 3), 'algorithmic_bytes': int(rbytes),
                          'settled_nodes': int(counters[3]), 'relaxed_edges': int(counters[4]),
-                         'tasks': int(counters[5]), 'transition_entries': int(counters[6])},
+                         'tasks': int(counters[5]), 'transition_entries': int(counters[6]),
+                         'source_candidates': int(counters[12]),
+                         'retry_settled_nodes': int(counters[9])},
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)

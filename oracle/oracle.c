@@ -343,25 +343,26 @@ static void dijkstra(const orc_graph* g, uint32_t start, double d0, double bound
   free(hp.d);
 }
 
-/* route distance from candidate (ei,pi) to (ej,pj) given labels from dst(ei) */
+/* route distance from candidate (ei,pi) to (ej,pj) given labels rooted (label 0)
+ * at dst(ei): (d0 + label(src(ej))) + pj*len(ej), d0 = (1-pi)*len(ei) */
 static double route_from_labels(const orc_graph* g, const nodemap_t* m, uint32_t ei, double pi, uint32_t ej,
                                 double pj) {
   if (ej == ei && pj >= pi) return (pj - pi) * (double)g->edge_len[ei];
   uint32_t s = nm_find(m, g->edge_src[ej]);
   if (s == 0xFFFFFFFFu) return INFINITY;
-  return m->dist[s] + pj * (double)g->edge_len[ej];
+  double d0 = (1.0 - pi) * (double)g->edge_len[ei];
+  return (d0 + m->dist[s]) + pj * (double)g->edge_len[ej];
 }
 
 int orc_route_dist(const orc_graph* g, uint32_t src_edge, double src_p, uint32_t dst_edge, double dst_p,
                    double bound, uint32_t mode_bit, double* out_dist) {
   nodemap_t m;
   nm_init(&m, 1024);
-  double d0 = (1.0 - src_p) * (double)g->edge_len[src_edge];
   double r = INFINITY;
   if (dst_edge == src_edge && dst_p >= src_p) {
     r = (dst_p - src_p) * (double)g->edge_len[src_edge];
-  } else if (d0 <= bound) {
-    dijkstra(g, g->edge_dst[src_edge], d0, bound, mode_bit, &m);
+  } else {
+    dijkstra(g, g->edge_dst[src_edge], 0.0, bound, mode_bit, &m);
     r = route_from_labels(g, &m, src_edge, src_p, dst_edge, dst_p);
   }
   nm_free(&m);
@@ -562,10 +563,10 @@ static void match_trace(job_t* J, int32_t t) {
     double gfl = gcd > P->interpolation_distance ? gcd : P->interpolation_distance;
     double bound = P->max_route_distance_factor * gfl;
     if (bound > P->breakage_distance) bound = P->breakage_distance;
+    uint32_t searched = 0xFFFFFFFFu; /* labels rooted at this node are in nm */
     for (int i = 0; i < Ka; ++i) {
       for (int j = 0; j < Kb; ++j) trans[i * ORC_KMAX + j] = INFINITY;
       if (forced) continue;
-      double d0 = (1.0 - ca[i].p) * (double)g->edge_len[ca[i].e];
       int need = 0;
       for (int j = 0; j < Kb; ++j) {
         if (cb[j].e == ca[i].e && cb[j].p >= ca[i].p) {
@@ -575,8 +576,12 @@ static void match_trace(job_t* J, int32_t t) {
           need = 1;
         }
       }
-      if (!need || !(d0 <= bound)) continue;
-      dijkstra(g, g->edge_dst[ca[i].e], d0, bound, mode_bit, &nm);
+      if (!need) continue;
+      /* one search per root node: labels do not depend on the source edge */
+      if (g->edge_dst[ca[i].e] != searched) {
+        searched = g->edge_dst[ca[i].e];
+        dijkstra(g, searched, 0.0, bound, mode_bit, &nm);
+      }
       for (int j = 0; j < Kb; ++j) {
         if (cb[j].e == ca[i].e && cb[j].p >= ca[i].p) continue;
         double r = route_from_labels(g, &nm, ca[i].e, ca[i].p, cb[j].e, cb[j].p);
@@ -675,9 +680,8 @@ static void match_trace(job_t* J, int32_t t) {
         double gfl = gcd > P->interpolation_distance ? gcd : P->interpolation_distance;
         double bound = P->max_route_distance_factor * gfl;
         if (bound > P->breakage_distance) bound = P->breakage_distance;
-        double d0 = (1.0 - ci->p) * (double)g->edge_len[ci->e];
         uint32_t S = g->edge_dst[ci->e], T = g->edge_src[cj->e];
-        dijkstra(g, S, d0, bound, mode_bit, &nm);
+        dijkstra(g, S, 0.0, bound, mode_bit, &nm);
         VEC(uint32_t) path = {0};
         uint32_t v = T;
         while (v != S) {

@@ -13,6 +13,7 @@
 #define OTR_KMAX 64          // candidate slots per state (lanes of one wave)
 #define OTR_MODES 3          // auto, bicycle, pedestrian
 #define OTR_WAVE 64
+#define OTR_COUNTERS 16      // counter kinds, see otr_batch_result.counters
 
 namespace otr {
 
@@ -55,6 +56,7 @@ struct DevGraph {
   const uint32_t* cell_row;
   const uint32_t* cell_edge;
   const uint4* edge_pack;      // {dst, len bits, attr, 0}: one 16-B load per relaxed edge
+  const uint4* adj;            // 2 x uint4 per node: 4 x {dst | access<<28 | more<<31, len bits}
   uint32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double grid_min_lat, grid_min_lon, grid_cell_deg;
 };
@@ -104,6 +106,16 @@ __device__ inline uint32_t hmix(uint32_t x) {
 }
 
 __device__ inline int lane_id() { return (int)__lane_id(); }
+
+// Blocks are dealt round-robin over the 8 XCDs (b and b+8 share one, MI355X_MICROARCH.md
+// §Workgroup dispatch): give each XCD a contiguous run of logical work items so that
+// neighbouring items (same trace / same step → same graph neighbourhood) share an L2.
+// Speed only; any placement gives the same results.  grid = 8 * per.
+__device__ inline int64_t xcd_remap(int64_t b, int64_t per) { return (b & 7) * per + (b >> 3); }
+
+constexpr int kShards = 64;  // device counters are sharded [kind][64] to avoid one hot address
+constexpr uint32_t kAdjDstMask = 0x0FFFFFFFu;
+constexpr uint32_t kAdjMore = 0x80000000u;
 
 __device__ inline int prefix_count(unsigned long long mask) {
   return __popcll(mask & ((1ull << lane_id()) - 1ull));

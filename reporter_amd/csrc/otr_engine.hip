@@ -117,6 +117,33 @@ int engine_configure(const Config& cfg, std::string* err) {
     gs.allocs.push_back(d);
     HIPCHK(hipMemcpy(d, pack.data(), sizeof(uint4) * pack.size(), hipMemcpyHostToDevice));
     g.edge_pack = (const uint4*)d;
+    // per-node adjacency records: the first 4 out-edges of a node in one 32-B line
+    if (h.n_nodes >= (1u << 28)) {
+      munmap(map, (size_t)st.st_size);
+      if (err) *err = "graph has more than 2^28 nodes";
+      return OTR_BAD_REQUEST;
+    }
+    const uint32_t* row = (const uint32_t*)(base + h.array_offset[OTR_A_NODE_ROW]);
+    std::vector<uint4> adj(2ull * h.n_nodes + 2, make_uint4(0u, 0u, 0u, 0u));
+    for (uint32_t u = 0; u < h.n_nodes; ++u) {
+      uint32_t* w = (uint32_t*)&adj[2ull * u];
+      for (int k = 0; k < 4; ++k) {
+        w[2 * k] = kAdjDstMask;  // empty slot: access bits 0
+        w[2 * k + 1] = 0u;
+      }
+      const uint32_t deg = row[u + 1] - row[u];
+      for (uint32_t k = 0; k < deg && k < 4; ++k) {
+        const uint32_t e = row[u] + k;
+        w[2 * k] = dst[e] | ((attr[e] & OTR_ATTR_ACCESS_MASK) << 28);
+        w[2 * k + 1] = len[e];
+      }
+      if (deg > 4) w[6] |= kAdjMore;
+    }
+    void* da = nullptr;
+    HIPCHK(hipMalloc(&da, sizeof(uint4) * adj.size()));
+    gs.allocs.push_back(da);
+    HIPCHK(hipMemcpy(da, adj.data(), sizeof(uint4) * adj.size(), hipMemcpyHostToDevice));
+    g.adj = (const uint4*)da;
   }
   for (void* p : gs.allocs)
     if (!p) {
@@ -152,7 +179,7 @@ enum Slot {
   S_STATE_CNT, S_TRACE_STATE_OFF, S_STATE_PROBE, S_STATE_TRACE,
   S_CAND_EDGE, S_CAND_P, S_CAND_SQD, S_CAND_COUNT,
   S_PREV, S_G, S_BOUND, S_FORCED, S_NTASK, S_NTRANS, S_TASK_OFF, S_TRANS_OFF,
-  S_TASK_STATE, S_TASK_SRC, S_TASK_OVF, S_TRANS,
+  S_TASK_STATE, S_TASK_MASK, S_TASK_OVF, S_TRANS,
   S_BP, S_BRK, S_END_WIN, S_WINNER, S_SUBPATH,
   S_PATH_OFF, S_PATH_LEN, S_PATH, S_STEP_OVF,
   S_CAP, S_CAP_OFF, S_POS, S_ACT,
@@ -288,8 +315,9 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     b.acc = in->accuracy;
   }
   out->n_probes = N;
-  unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, 32);
-  HIPCHK(hipMemsetAsync(d_counters, 0, 32 * 8, stream));
+  const size_t n_ctr = 2 * (size_t)OTR_COUNTERS * kShards;  // tier-2 kinds land at +6
+  unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, n_ctr);
+  HIPCHK(hipMemsetAsync(d_counters, 0, n_ctr * 8, stream));
   size_t scan_bytes = 0;
   auto scan = [&](const int64_t* src, int64_t* dst_np1, int64_t n) -> int {
     // dst[0] = 0, dst[1..n] = inclusive prefix sums
@@ -333,9 +361,9 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     return OTR_DEVICE_ERROR;
   }
   if (S > 0) {
-    unsigned gridc = (unsigned)(S < 1048576 ? S : 1048576);
     tb(OTR_STAGE_CANDIDATES);
-    k_candidates<<<gridc, 64, 0, stream>>>(g, b, mp, S, state_probe, state_trace, cb, d_counters);
+    k_candidates<<<(unsigned)(8 * ((S + 7) / 8)), 64, 0, stream>>>(g, b, mp, S, state_probe, state_trace, cb,
+                                                                   d_counters);
     te(OTR_STAGE_CANDIDATES);
   }
   // ---- K_link + task map
@@ -351,25 +379,30 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   tb(OTR_STAGE_LINK);
   k_link<<<grid_for(T, 256), 256, 0, stream>>>(b, mp, trace_state_off, state_probe, cb.count, sb);
   te(OTR_STAGE_LINK);
+  if (S > 0)
+    k_tasks<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, nullptr,
+                                                  nullptr, nullptr);
   if ((rc = scan(sb.ntask, task_off, S))) return rc;
   if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
   int64_t NT = 0, NTR = 0;
   if ((rc = read_i64(task_off + S, &NT))) return rc;
   if ((rc = read_i64(trans_off + S, &NTR))) return rc;
   int64_t* task_state = need<int64_t>(S_TASK_STATE, NT);
-  int32_t* task_src = need<int32_t>(S_TASK_SRC, NT);
+  unsigned long long* task_mask = need<unsigned long long>(S_TASK_MASK, NT);
   int32_t* task_ovf = need<int32_t>(S_TASK_OVF, NT);
   double* trans = need<double>(S_TRANS, NTR);
-  if (!task_state || !task_src || !task_ovf || !trans) {
+  if (!task_state || !task_mask || !task_ovf || !trans) {
     if (err) *err = "device allocation failed (transitions)";
     return OTR_DEVICE_ERROR;
   }
-  if (S > 0) k_taskmap<<<grid_for(S, 256), 256, 0, stream>>>(S, task_off, task_state, task_src);
+  if (S > 0)
+    k_tasks<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, task_off,
+                                                  task_state, task_mask);
   if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
   // ---- K3/K4: routing + transition costs
   RouteArgs ra{};
   ra.task_state = task_state;
-  ra.task_src = task_src;
+  ra.task_mask = task_mask;
   ra.task_list = nullptr;
   ra.n_tasks = NT;
   ra.prev = sb.prev;
@@ -387,9 +420,8 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
   ra.overflow_flag = task_ovf;
   if (NT > 0) {
-    unsigned gr = (unsigned)(NT < 4194304 ? NT : 4194304);
     tb(OTR_STAGE_ROUTE);
-    k_route<512><<<gr, 64, 0, stream>>>(g, ra, d_counters);
+    k_route<512><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
     te(OTR_STAGE_ROUTE);
     // overflow retry with the large table
     int64_t* list = need<int64_t>(S_LIST, NT);
@@ -405,7 +437,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       rb.task_list = list;
       rb.n_tasks = (int64_t)novf;
       tb(OTR_STAGE_ROUTE_BIG);
-      k_route<8192><<<(unsigned)(novf < 65536 ? novf : 65536), 64, 0, stream>>>(g, rb, d_counters + 16);
+      k_route<8192><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
       te(OTR_STAGE_ROUTE_BIG);
       HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
       k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
@@ -475,8 +507,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       pa.overflow_flag = step_ovf;
       pa.cap_flag = (int32_t*)(cnt + 2);
       tb(OTR_STAGE_PATHS);
-      k_paths<512><<<(unsigned)(nsteps < 4194304 ? nsteps : 4194304), 64, 0, stream>>>(g, pa, nullptr,
-                                                                                      (int64_t)nsteps);
+      k_paths<512><<<(unsigned)(8 * ((nsteps + 7) / 8)), 64, 0, stream>>>(g, pa, nullptr, (int64_t)nsteps);
       te(OTR_STAGE_PATHS);
       // large-table retry for table overflows
       int64_t* rl = need<int64_t>(S_TASK_STATE, NT > (int64_t)nsteps ? NT : (int64_t)nsteps);  // reuse
@@ -489,8 +520,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       if (host[2] > 0) {
         HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
         tb(OTR_STAGE_PATHS_BIG);
-        k_paths<8192><<<(unsigned)(host[2] < 65536 ? host[2] : 65536), 64, 0, stream>>>(g, pa, rl,
-                                                                                        (int64_t)host[2]);
+        k_paths<8192><<<(unsigned)host[2], 64, 0, stream>>>(g, pa, rl, (int64_t)host[2]);
         te(OTR_STAGE_PATHS_BIG);
         HIPCHK(hipMemcpyAsync(host, cnt + 1, 16, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
@@ -569,7 +599,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   ha.base_time = in->hist_base_time;
   ha.hours = in->hist_hours;
   ha.n_segments = g.n_segments;
-  ha.n_rows = d_counters + 8;
+  ha.n_rows = d_counters + 8 * kShards;
   size_t hist_len = (size_t)(in->hist_hours > 0 ? in->hist_hours : 0) * g.n_segments * OTR_HIST_BINS;
   ha.hist = hist_len ? (in->hist_device ? in->hist_device : need<uint32_t>(S_HIST, hist_len)) : nullptr;
   if (hist_len) HIPCHK(hipMemsetAsync(ha.hist, 0, hist_len * 4, stream));
@@ -577,15 +607,17 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   k_histogram<<<grid_for(T, 256), 256, 0, stream>>>(ha);
   te(OTR_STAGE_HISTOGRAM);
   HIPCHK(hipGetLastError());
-  unsigned long long hc[32];
-  HIPCHK(hipMemcpyAsync(hc, d_counters, sizeof(hc), hipMemcpyDeviceToHost, stream));
+  std::vector<unsigned long long> hc(n_ctr);
+  HIPCHK(hipMemcpyAsync(hc.data(), d_counters, n_ctr * 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
-  for (int k = 0; k < 8; ++k) out->counters[k] = hc[k];
+  for (int k = 0; k < OTR_COUNTERS; ++k) {
+    unsigned long long v = 0;
+    for (int sh = 0; sh < kShards; ++sh) v += hc[(size_t)k * kShards + sh];
+    out->counters[k] = v;
+  }
   out->counters[5] = (uint64_t)NT;
   out->counters[6] = (uint64_t)NTR;
-  out->big_counters[0] = hc[16 + 3];
-  out->big_counters[1] = hc[16 + 4];
-  out->n_rows = (int64_t)hc[8];
+  out->n_rows = (int64_t)out->counters[8];
   out->d_hist = ha.hist;
   out->hist_len = (int64_t)hist_len;
   if (timing)

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(64) void k_candidates(DevGraph g, BatchDev b, ModeP
   __shared__ double s_p[2][2 * OTR_WAVE];
   __shared__ uint32_t s_e[2][2 * OTR_WAVE];
   const int lane = threadIdx.x;
-  for (int64_t s = blockIdx.x; s < n_states; s += gridDim.x) {
+  for (int64_t s = xcd_remap(blockIdx.x, (n_states + 7) / 8); s < n_states; s = n_states) {
     const int64_t probe = state_probe[s];
     const int mode = b.mode[state_trace[s]] < OTR_MODES ? b.mode[state_trace[s]] : 0;
     const MatchParams& P = mp.m[mode];
@@ -196,9 +196,10 @@ __global__ __launch_bounds__(64) void k_candidates(DevGraph g, BatchDev b, ModeP
     // algorithmic-byte counters
     for (int off = 32; off > 0; off >>= 1) tests += __shfl_xor(tests, off);
     if (lane == 0 && counters) {
-      atomicAdd(&counters[0], (unsigned long long)((r1 - r0 + 1) * (c1 - c0 + 1)));
-      atomicAdd(&counters[1], tests);
-      atomicAdd(&counters[2], (unsigned long long)n);
+      const int sh = blockIdx.x & (kShards - 1);
+      atomicAdd(&counters[0 * kShards + sh], (unsigned long long)((r1 - r0 + 1) * (c1 - c0 + 1)));
+      atomicAdd(&counters[1 * kShards + sh], tests);
+      atomicAdd(&counters[2 * kShards + sh], (unsigned long long)n);
     }
     __syncthreads();
   }
@@ -212,7 +213,7 @@ struct StepBuf {
   double* g;          // great-circle distance prev→s
   double* bound;      // route bound
   uint8_t* forced;    // g > breakage_distance
-  int64_t* ntask;     // K[prev] for steps, else 0
+  int64_t* ntask;     // search tasks of the step (k_tasks)
   int64_t* ntrans;    // K[prev]*K[s]
 };
 
@@ -223,7 +224,6 @@ __global__ void k_link(BatchDev b, ModeParams mp, const int64_t* trace_state_off
   const MatchParams& P = mp.m[b.mode[t] < OTR_MODES ? b.mode[t] : 0];
   int64_t last = -1;
   for (int64_t s = trace_state_off[t]; s < trace_state_off[t + 1]; ++s) {
-    st.ntask[s] = 0;
     st.ntrans[s] = 0;
     if (cand_count[s] <= 0) {
       st.prev[s] = -2;
@@ -236,20 +236,49 @@ __global__ void k_link(BatchDev b, ModeParams mp, const int64_t* trace_state_off
       st.g[s] = gcd;
       st.forced[s] = gcd > P.breakage_distance;
       st.bound[s] = route_bound(P, gcd);
-      st.ntask[s] = cand_count[last];
       st.ntrans[s] = (int64_t)cand_count[last] * cand_count[s];
     }
     last = s;
   }
 }
 
-__global__ void k_taskmap(int64_t n_states, const int64_t* task_off, int64_t* task_state, int32_t* task_src) {
-  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// One search task per (step, distinct search root).  Labels are rooted (label 0) at
+// dst(e_i), so every source candidate whose edge ends at the same node shares the
+// search; the task carries the bit mask of those sources.  Pass 1 (task_off == null)
+// counts, pass 2 writes.
+__global__ void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* cand_count,
+                        const uint32_t* cand_edge, const uint32_t* edge_dst, int64_t* ntask,
+                        const int64_t* task_off, int64_t* task_state, unsigned long long* task_mask) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_states) return;
-  for (int64_t k = task_off[s]; k < task_off[s + 1]; ++k) {
-    task_state[k] = s;
-    task_src[k] = (int32_t)(k - task_off[s]);
+  const int64_t sp = prev[s];
+  if (sp < 0 || cand_count[s] <= 0) {
+    if (!task_off) ntask[s] = 0;
+    return;
   }
+  const int Ka = cand_count[sp];
+  uint32_t root[OTR_KMAX];
+  for (int i = 0; i < Ka; ++i) root[i] = edge_dst[cand_edge[sp * OTR_KMAX + i]];
+  int64_t cnt = 0;
+  const int64_t base = task_off ? task_off[s] : 0;
+  for (int i = 0; i < Ka; ++i) {
+    bool rep = true;
+    for (int k = 0; k < i; ++k)
+      if (root[k] == root[i]) {
+        rep = false;
+        break;
+      }
+    if (!rep) continue;
+    if (task_off) {
+      unsigned long long m = 0;
+      for (int k = i; k < Ka; ++k)
+        if (root[k] == root[i]) m |= 1ull << k;
+      task_state[base + cnt] = s;
+      task_mask[base + cnt] = m;
+    }
+    ++cnt;
+  }
+  if (!task_off) ntask[s] = cnt;
 }
 
 // ------------------------------------------------------------------------------
@@ -259,9 +288,10 @@ __global__ void k_taskmap(int64_t n_states, const int64_t* task_off, int64_t* ta
 // label is below (minimum pending label + delta), relaxes its out-edges with LDS
 // 64-bit atomicMin on the binary64 bit pattern (positive doubles order like u64),
 // and re-queues improved nodes.  The fixed point is the minimal left-to-right
-// binary64 path sum — the same value the oracle's binary-heap Dijkstra settles —
-// and a node whose label is below the minimum pending label is final, so the
-// search stops as soon as every target is final or provably beyond the bound.
+// binary64 path sum from the root (label 0) — the value the oracle's binary-heap
+// Dijkstra settles — and a node whose label is below the minimum pending label is
+// final, so the search stops as soon as every target is final or provably beyond
+// the bound.  A node's first four out-edges come from one 32-B adjacency record.
 // ------------------------------------------------------------------------------
 template <int CAP>
 struct SearchLds {
@@ -325,27 +355,52 @@ __device__ inline void search_init(SearchLds<CAP>& L) {
   __syncthreads();
 }
 
-// Target j (lane j < n_tgt) resolved?  tnode==kEmpty: nothing to search for.
+__device__ inline double bits_d(unsigned long long b) { return __longlong_as_double((long long)b); }
+
+// Target (lane) resolved?  tnode == kEmpty: nothing to search for.  A label below the
+// minimum pending label is final; otherwise every later label is >= dmin, so the route
+// (d0 + label) + tpart >= (d0min + dmin) + tpart, which exceeding the bound proves the
+// target unreachable for every source of the task.
 template <int CAP>
-__device__ inline bool target_resolved(const SearchLds<CAP>& L, uint32_t tnode, double tpart, double bound,
-                                       double dmin, bool pend_empty) {
-  if (tnode == kEmpty) return true;
-  if (pend_empty) return true;
+__device__ inline bool target_resolved(const SearchLds<CAP>& L, uint32_t tnode, double tpart, double d0min,
+                                       double bound, double dmin, bool pend_empty) {
+  if (tnode == kEmpty || pend_empty) return true;
   const int sl = lds_find(L, tnode);
-  if (sl >= 0 && __longlong_as_double((long long)L.dist[sl]) < dmin) return true;
-  return dmin + tpart > bound;
+  if (sl >= 0 && bits_d(L.dist[sl]) < dmin) return true;
+  return (d0min + dmin) + tpart > bound;
 }
 
-// Runs the search from `start` (label d0).  Lanes j < n_tgt hold target node tnode
-// and target partial length tpart.  Returns false on LDS-table overflow.
 template <int CAP>
-__device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_bit, uint32_t start, double d0,
-                           double bound, double delta, uint32_t tnode, double tpart, int n_tgt,
+__device__ inline void relax_one(SearchLds<CAP>& L, uint32_t dw, uint32_t lw, double du, double bound,
+                                 uint32_t mode_bit, unsigned long long& relaxed) {
+  if (!(((dw >> 28) & 7u) & mode_bit)) return;
+  ++relaxed;
+  const double nd = du + (double)__uint_as_float(lw);
+  if (nd > bound) return;
+  const int sl = lds_insert(L, dw & kAdjDstMask);
+  if (sl < 0) return;
+  const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
+  const unsigned long long old = atomicMin(&L.dist[sl], nb);
+  if (nb < old) {
+    const uint32_t ok = atomicOr(&L.key[sl], kInq);
+    if (!(ok & kInq)) {
+      const int p = atomicAdd(&L.n_pend, 1);
+      if (p < CAP) L.pend[p] = (uint16_t)sl;
+      else L.overflow = 1;
+    }
+  }
+}
+
+// Runs the search rooted at `start` (label 0).  Lanes j < n_tgt hold target node
+// tnode and target partial length tpart.  Returns false on LDS-table overflow.
+template <int CAP>
+__device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_bit, uint32_t start, double bound,
+                           double delta, uint32_t tnode, double tpart, double d0min, int n_tgt,
                            unsigned long long* settled, unsigned long long* relaxed) {
   const int lane = threadIdx.x;
   if (lane == 0) {
     const int sl = lds_insert(L, start);
-    L.dist[sl] = (unsigned long long)__double_as_longlong(d0);
+    L.dist[sl] = 0ull;  // +0.0
     L.key[sl] |= kInq;
     L.pend[0] = (uint16_t)sl;
     L.n_pend = 1;
@@ -354,19 +409,17 @@ __device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_b
   unsigned long long my_settled = 0, my_relaxed = 0;
   for (;;) {
     const int np = L.n_pend;
-    // minimum pending label (wave reduce)
     double dmin = __builtin_huge_val();
     for (int k = lane; k < np; k += OTR_WAVE) {
-      const double d = __longlong_as_double((long long)L.dist[L.pend[k]]);
+      const double d = bits_d(L.dist[L.pend[k]]);
       dmin = d < dmin ? d : dmin;
     }
     for (int off = 32; off > 0; off >>= 1) {
       const double o = __shfl_xor(dmin, off);
       dmin = o < dmin ? o : dmin;
     }
-    const bool res = lane >= n_tgt || target_resolved(L, tnode, tpart, bound, dmin, np == 0);
+    const bool res = lane >= n_tgt || target_resolved(L, tnode, tpart, d0min, bound, dmin, np == 0);
     if (__ballot(!res) == 0ull || np == 0) break;
-    // split pending into this round's work (label < dmin + delta) and the rest
     const double theta = dmin + delta;
     int kept = 0, nw = 0;
     for (int base = 0; base < np; base += OTR_WAVE) {
@@ -375,7 +428,7 @@ __device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_b
       bool take = false;
       if (k < np) {
         sl = L.pend[k];
-        take = __longlong_as_double((long long)L.dist[sl]) < theta;
+        take = bits_d(L.dist[sl]) < theta;
       }
       const unsigned long long mt = __ballot(take), mk = __ballot(k < np && !take);
       __syncthreads();
@@ -391,33 +444,23 @@ __device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_b
     }
     if (lane == 0) L.n_pend = kept;
     __syncthreads();
-    // relax the work list
     for (int base = 0; base < nw; base += OTR_WAVE) {
       const int k = base + lane;
       if (k < nw) {
         const int ws = L.work[k];
         const uint32_t u = L.key[ws] & ~kInq;
-        const double du = __longlong_as_double((long long)L.dist[ws]);
+        const double du = bits_d(L.dist[ws]);
         ++my_settled;
-        for (uint32_t e = g.node_row[u]; e < g.node_row[u + 1]; ++e) {
-          const uint4 pk = g.edge_pack[e];
-          ++my_relaxed;
-          if (!(pk.z & mode_bit)) continue;
-          const double nd = du + (double)__uint_as_float(pk.y);
-          if (nd > bound) continue;
-          const int sl = lds_insert(L, pk.x);
-          if (sl < 0) break;
-          const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
-          const unsigned long long old = atomicMin(&L.dist[sl], nb);
-          if (nb < old) {
-            const uint32_t ok = atomicOr(&L.key[sl], kInq);
-            if (!(ok & kInq)) {
-              const int p = atomicAdd(&L.n_pend, 1);
-              if (p < CAP) L.pend[p] = (uint16_t)sl;
-              else L.overflow = 1;
-            }
+        const uint4 r0 = g.adj[2 * (size_t)u], r1 = g.adj[2 * (size_t)u + 1];
+        relax_one(L, r0.x, r0.y, du, bound, mode_bit, my_relaxed);
+        relax_one(L, r0.z, r0.w, du, bound, mode_bit, my_relaxed);
+        relax_one(L, r1.x, r1.y, du, bound, mode_bit, my_relaxed);
+        relax_one(L, r1.z, r1.w, du, bound, mode_bit, my_relaxed);
+        if (r1.z & kAdjMore)
+          for (uint32_t e = g.node_row[u] + 4; e < g.node_row[u + 1]; ++e) {
+            const uint4 pk = g.edge_pack[e];
+            relax_one(L, pk.x | ((pk.z & 7u) << 28), pk.y, du, bound, mode_bit, my_relaxed);
           }
-        }
       }
     }
     __syncthreads();
@@ -430,11 +473,12 @@ __device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_b
 }
 
 // ------------------------------------------------------------------------------
-// K3 + K4: one wave per (step, source candidate): search, then transition costs.
+// K3 + K4: one wave per (step, search root): search, then transition costs for
+// every source candidate sharing the root.
 // ------------------------------------------------------------------------------
 struct RouteArgs {
   const int64_t* task_state;
-  const int32_t* task_src;
+  const unsigned long long* task_mask;
   const int64_t* task_list;   // optional indirection (overflow retry), else null
   int64_t n_tasks;
   const int64_t* prev;
@@ -457,67 +501,78 @@ template <int CAP>
 __global__ __launch_bounds__(64) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
   __shared__ SearchLds<CAP> L;
   const int lane = threadIdx.x;
+  const int64_t w = a.task_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (a.n_tasks + 7) / 8);
+  if (w >= a.n_tasks) return;
+  const int64_t task = a.task_list ? a.task_list[w] : w;
+  const int64_t s = a.task_state[task];
+  const unsigned long long mask = a.task_mask[task];
+  const int64_t sp = a.prev[s];
+  const int Kb = a.cand_count[s];
+  const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+  const uint32_t mode_bit = 1u << mode;
+  const double bound = a.bound[s], gcd = a.g[s];
+  const uint32_t root = gr.edge_dst[a.cand_edge[sp * OTR_KMAX + (__ffsll((long long)mask) - 1)]];
+  double* trow = a.trans + a.trans_off[s];
+  // targets: lane j
+  uint32_t ej = 0, tnode = kEmpty;
+  double pj = 0, tpart = 0;
+  bool needed = false;
+  double d0min = __builtin_huge_val();
+  if (lane < Kb) {
+    ej = a.cand_edge[s * OTR_KMAX + lane];
+    pj = a.cand_p[s * OTR_KMAX + lane];
+    tpart = pj * (double)gr.edge_len[ej];
+  }
+  for (unsigned long long m = mask; m; m &= m - 1) {
+    const int i = __ffsll((long long)m) - 1;
+    const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
+    const double pi = a.cand_p[sp * OTR_KMAX + i];
+    const double d0 = (1.0 - pi) * (double)gr.edge_len[ei];
+    d0min = d0 < d0min ? d0 : d0min;
+    if (lane < Kb && !(ej == ei && pj >= pi)) needed = true;
+  }
+  if (needed) tnode = gr.edge_src[ej];
+  if (a.forced[s]) {
+    for (unsigned long long m = mask; m; m &= m - 1)
+      if (lane < Kb) trow[(int64_t)(__ffsll((long long)m) - 1) * Kb + lane] = __builtin_huge_val();
+    return;
+  }
   unsigned long long settled = 0, relaxed = 0;
-  for (int64_t w = blockIdx.x; w < a.n_tasks; w += gridDim.x) {
-    const int64_t task = a.task_list ? a.task_list[w] : w;
-    const int64_t s = a.task_state[task];
-    const int i = a.task_src[task];
-    const int64_t sp = a.prev[s];
-    const int Kb = a.cand_count[s];
-    const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
-    const uint32_t mode_bit = 1u << mode;
-    const double bound = a.bound[s], gcd = a.g[s];
+  bool ok = true;
+  const bool need = __ballot(needed) != 0ull;
+  search_init<CAP>(L);
+  if (need)
+    ok = search_run<CAP>(L, gr, mode_bit, root, bound, a.delta, tnode, tpart, d0min, Kb, &settled, &relaxed);
+  double lab = __builtin_huge_val();
+  if (ok && needed) {
+    const int sl = lds_find(L, tnode);
+    if (sl >= 0) lab = bits_d(L.dist[sl]);
+  }
+  for (unsigned long long m = mask; m; m &= m - 1) {
+    const int i = __ffsll((long long)m) - 1;
     const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
     const double pi = a.cand_p[sp * OTR_KMAX + i];
     const double leni = (double)gr.edge_len[ei];
-    double* row = a.trans + a.trans_off[s] + (int64_t)i * Kb;
-    // targets: lane j
-    uint32_t ej = 0, tnode = kEmpty;
-    double pj = 0, tpart = 0;
-    bool same = false;
-    if (lane < Kb) {
-      ej = a.cand_edge[s * OTR_KMAX + lane];
-      pj = a.cand_p[s * OTR_KMAX + lane];
-      same = (ej == ei && pj >= pi);
-      if (!same) {
-        tnode = gr.edge_src[ej];
-        tpart = pj * (double)gr.edge_len[ej];
-      }
-    }
-    if (a.forced[s]) {
-      if (lane < Kb) row[lane] = __builtin_huge_val();
-      continue;
-    }
-    const double d0 = (1.0 - pi) * leni;
-    const bool need = __ballot(lane < Kb && !same) != 0ull;
-    bool ok = true;
-    search_init<CAP>(L);
-    if (need && d0 <= bound)
-      ok = search_run<CAP>(L, gr, mode_bit, gr.edge_dst[ei], d0, bound, a.delta, tnode, tpart, Kb, &settled,
-                           &relaxed);
-    if (!ok) {
-      if (lane == 0) a.overflow_flag[task] = 1;
-      continue;
-    }
     if (lane < Kb) {
       double r = __builtin_huge_val();
-      if (same) {
-        r = (pj - pi) * leni;
-      } else if (need && d0 <= bound) {
-        const int sl = lds_find(L, tnode);
-        if (sl >= 0) r = __longlong_as_double((long long)L.dist[sl]) + tpart;
-      }
-      row[lane] = r <= bound ? fabs(r - gcd) * a.inv_beta[mode] : __builtin_huge_val();
+      if (ej == ei && pj >= pi) r = (pj - pi) * leni;
+      else if (lab != __builtin_huge_val()) r = ((1.0 - pi) * leni + lab) + tpart;
+      trow[(int64_t)i * Kb + lane] = (ok && r <= bound) ? fabs(r - gcd) * a.inv_beta[mode] : __builtin_huge_val();
     }
-    __syncthreads();
   }
-  for (int off = 32; off > 0; off >>= 1) {
-    settled += __shfl_xor(settled, off);
-    relaxed += __shfl_xor(relaxed, off);
-  }
-  if (lane == 0 && counters) {
-    atomicAdd(&counters[3], settled);
-    atomicAdd(&counters[4], relaxed);
+  if (!ok && lane == 0) a.overflow_flag[task] = 1;
+  if (counters) {
+    for (int off = 32; off > 0; off >>= 1) {
+      settled += __shfl_xor(settled, off);
+      relaxed += __shfl_xor(relaxed, off);
+    }
+    if (lane == 0) {
+      const int sh = blockIdx.x & (kShards - 1);
+      atomicAdd(&counters[3 * kShards + sh], settled);
+      atomicAdd(&counters[4 * kShards + sh], relaxed);
+      atomicAdd(&counters[11 * kShards + sh], (unsigned long long)Kb);
+      atomicAdd(&counters[12 * kShards + sh], (unsigned long long)__popcll(mask));
+    }
   }
 }
 
@@ -650,8 +705,9 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
 
 // ------------------------------------------------------------------------------
 // K6: winner path reconstruction, one wave per step (state s with prev >= 0,
-// not a sub-path start).  Single-target search, then predecessor walk: among the
-// in-edges (u→v) with label(u) + len == label(v) take the smallest edge id.
+// not a sub-path start).  Single-target search from the root dst(e_i), then a
+// predecessor walk: among the in-edges (u→v) with label(u) + len == label(v) take
+// the smallest edge id.
 // ------------------------------------------------------------------------------
 struct PathArgs {
   const int64_t* steps;        // state ids to reconstruct
@@ -683,7 +739,7 @@ __device__ int walk_preds(const SearchLds<CAP>& L, const DevGraph& g, uint32_t m
   while (v != S) {
     const int sv = lds_find(L, v);
     if (sv < 0) return -1;
-    const double dv = __longlong_as_double((long long)L.dist[sv]);
+    const double dv = bits_d(L.dist[sv]);
     uint32_t best = kEmpty;
     for (uint32_t base = g.rev_row[v]; base < g.rev_row[v + 1]; base += OTR_WAVE) {
       const uint32_t r = base + lane;
@@ -692,7 +748,7 @@ __device__ int walk_preds(const SearchLds<CAP>& L, const DevGraph& g, uint32_t m
         const uint32_t ed = g.rev_edge[r];
         if (g.edge_attr[ed] & mode_bit) {
           const int su = lds_find(L, g.edge_src[ed]);
-          if (su >= 0 && __longlong_as_double((long long)L.dist[su]) + (double)g.edge_len[ed] == dv) cand = ed;
+          if (su >= 0 && bits_d(L.dist[su]) + (double)g.edge_len[ed] == dv) cand = ed;
         }
       }
       for (int off = 32; off > 0; off >>= 1) {
@@ -713,46 +769,45 @@ template <int CAP>
 __global__ __launch_bounds__(64) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, int64_t n_list) {
   __shared__ SearchLds<CAP> L;
   const int lane = threadIdx.x;
-  for (int64_t w = blockIdx.x; w < n_list; w += gridDim.x) {
-    const int64_t k = step_list ? step_list[w] : w;
-    const int64_t s = a.steps[k];
-    const int64_t sp = a.prev[s];
-    const int wi = a.winner[sp], wj = a.winner[s];
-    const uint32_t ei = a.cand_edge[sp * OTR_KMAX + wi], ej = a.cand_edge[s * OTR_KMAX + wj];
-    const double pi = a.cand_p[sp * OTR_KMAX + wi], pj = a.cand_p[s * OTR_KMAX + wj];
-    if (ej == ei && pj >= pi) {
-      if (lane == 0) a.path_len[s] = -1;
-      continue;
-    }
-    const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
-    const uint32_t mode_bit = 1u << mode;
-    const double d0 = (1.0 - pi) * (double)gr.edge_len[ei];
-    const uint32_t S = gr.edge_dst[ei], T = gr.edge_src[ej];
-    search_init<CAP>(L);
-    const bool ok = search_run<CAP>(L, gr, mode_bit, S, d0, a.bound[s], a.delta, lane == 0 ? T : kEmpty,
-                                    pj * (double)gr.edge_len[ej], 1, nullptr, nullptr);
-    if (!ok) {
-      if (lane == 0) a.overflow_flag[k] = 1;
-      continue;
-    }
-    const int n = walk_preds<CAP>(L, gr, mode_bit, S, T, nullptr, 0);
-    if (n < 0) {
-      if (lane == 0) a.overflow_flag[k] = 2;
-      continue;
-    }
-    int64_t off = 0;
-    if (lane == 0) off = (int64_t)atomicAdd(a.cursor, (unsigned long long)n);
-    off = __shfl(off, 0);
-    if (off + n > a.capacity) {
-      if (lane == 0) *a.cap_flag = 1;
-      continue;
-    }
-    walk_preds<CAP>(L, gr, mode_bit, S, T, a.path + off, n);
-    if (lane == 0) {
-      a.path_off[s] = off;
-      a.path_len[s] = n;
-    }
-    __syncthreads();
+  const int64_t w = step_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_list + 7) / 8);
+  if (w >= n_list) return;
+  const int64_t k = step_list ? step_list[w] : w;
+  const int64_t s = a.steps[k];
+  const int64_t sp = a.prev[s];
+  const int wi = a.winner[sp], wj = a.winner[s];
+  const uint32_t ei = a.cand_edge[sp * OTR_KMAX + wi], ej = a.cand_edge[s * OTR_KMAX + wj];
+  const double pi = a.cand_p[sp * OTR_KMAX + wi], pj = a.cand_p[s * OTR_KMAX + wj];
+  if (ej == ei && pj >= pi) {
+    if (lane == 0) a.path_len[s] = -1;
+    return;
+  }
+  const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+  const uint32_t mode_bit = 1u << mode;
+  const double d0 = (1.0 - pi) * (double)gr.edge_len[ei];
+  const uint32_t S = gr.edge_dst[ei], T = gr.edge_src[ej];
+  search_init<CAP>(L);
+  const bool ok = search_run<CAP>(L, gr, mode_bit, S, a.bound[s], a.delta, lane == 0 ? T : kEmpty,
+                                  pj * (double)gr.edge_len[ej], d0, 1, nullptr, nullptr);
+  if (!ok) {
+    if (lane == 0) a.overflow_flag[k] = 1;
+    return;
+  }
+  const int n = walk_preds<CAP>(L, gr, mode_bit, S, T, nullptr, 0);
+  if (n < 0) {
+    if (lane == 0) a.overflow_flag[k] = 2;
+    return;
+  }
+  int64_t off = 0;
+  if (lane == 0) off = (int64_t)atomicAdd(a.cursor, (unsigned long long)n);
+  off = __shfl(off, 0);
+  if (off + n > a.capacity) {
+    if (lane == 0) *a.cap_flag = 1;
+    return;
+  }
+  walk_preds<CAP>(L, gr, mode_bit, S, T, a.path + off, n);
+  if (lane == 0) {
+    a.path_off[s] = off;
+    a.path_len[s] = n;
   }
 }
 
@@ -967,7 +1022,7 @@ __global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) 
   a.stats[7 * t + 6] = 0;
   a.stats_len[2 * t] = rs.lengths[0];
   a.stats_len[2 * t + 1] = rs.lengths[1];
-  if (counters) atomicAdd(&counters[7], (unsigned long long)nseg);
+  if (counters) atomicAdd(&counters[7 * kShards + (blockIdx.x & (kShards - 1))], (unsigned long long)nseg);
 }
 
 // ------------------------------------------------------------------------------
@@ -1017,7 +1072,7 @@ __global__ void k_histogram(HistArgs a) {
         atomicAdd(&a.hist[((size_t)h * a.n_segments + seg) * OTR_HIST_BINS + bin], 1u);
     }
   }
-  if (rows) atomicAdd(a.n_rows, rows);
+  if (rows) atomicAdd(&a.n_rows[blockIdx.x & (kShards - 1)], rows);
 }
 
 }  // namespace otr
