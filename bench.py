@@ -53,6 +53,7 @@ def main():
     ap.add_argument('--traces-per-gpu', type=int, default=10000)
     ap.add_argument('--cpu-traces', type=int, default=1500, help='bounded oracle sample (0 = skip)')
     ap.add_argument('--cpu-threads', type=int, default=16)
+    ap.add_argument('--delta', type=float, default=None, help='routing round width (perf knob, metres)')
     args = ap.parse_args()
 
     rank = int(os.environ.get('RANK', 0))
@@ -91,7 +92,10 @@ def main():
         mine = allt
     log('rank %d: %d traces, %d probes (gen %.1fs)' % (rank, mine.n_traces, mine.n_probes, time.time() - t0))
 
-    M.configure(M.default_config(gpath, device=local))
+    cfg = M.default_config(gpath, device=local)
+    if args.delta is not None:
+        cfg['otr']['delta'] = args.delta
+    M.configure(cfg)
     n_nodes, n_edges, n_segments = M.graph_info()
     m = M.Matcher()
 
@@ -190,7 +194,7 @@ def main():
                          'settled_nodes': int(counters[3]), 'relaxed_edges': int(counters[4]),
                          'tasks': int(counters[5]), 'transition_entries': int(counters[6]),
                          'source_candidates': int(counters[12]),
-                         'retry_settled_nodes': int(counters[9])},
+                         'retry_settled_nodes': int(counters[9]), 'search_rounds': int(counters[13])},
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)

@@ -134,7 +134,7 @@ typedef struct otr_batch_result {
                                   4 relaxed edges (first-tier route launch), 5 search tasks,
                                   6 transition entries, 7 output segments, 8 tile rows,
                                   9/10 settled/relaxed of the large-table retry, 11 target reads,
-                                  12 source candidates */
+                                  12 source candidates, 13 search rounds */
   float kernel_ms[16];         /* OTR_BATCH_TIMING: device time per stage, OTR_STAGE_* */
 } otr_batch_result;
 

@@ -92,6 +92,7 @@ int engine_configure(const Config& cfg, std::string* err) {
   DevGraph& g = gs.dg;
   g.node_row = (const uint32_t*)up(OTR_A_NODE_ROW, 4ull * (h.n_nodes + 1));
   g.rev_row = (const uint32_t*)up(OTR_A_REV_ROW, 4ull * (h.n_nodes + 1));
+  g.node_ll = (const int2*)up(OTR_A_NODE_LL, 8ull * h.n_nodes);
   g.rev_edge = (const uint32_t*)up(OTR_A_REV_EDGE, 4ull * h.n_edges);
   g.edge_src = (const uint32_t*)up(OTR_A_EDGE_SRC, 4ull * h.n_edges);
   g.edge_dst = (const uint32_t*)up(OTR_A_EDGE_DST, 4ull * h.n_edges);
@@ -117,27 +118,24 @@ int engine_configure(const Config& cfg, std::string* err) {
     gs.allocs.push_back(d);
     HIPCHK(hipMemcpy(d, pack.data(), sizeof(uint4) * pack.size(), hipMemcpyHostToDevice));
     g.edge_pack = (const uint4*)d;
-    // per-node adjacency records: the first 4 out-edges of a node in one 32-B line
+    // per-node adjacency records: the first 4 out-edges of a node in one 64-B record,
+    // {dst | access<<28 | more<<31, len bits, dst lat_e6, dst lon_e6} per edge
     if (h.n_nodes >= (1u << 28)) {
       munmap(map, (size_t)st.st_size);
       if (err) *err = "graph has more than 2^28 nodes";
       return OTR_BAD_REQUEST;
     }
     const uint32_t* row = (const uint32_t*)(base + h.array_offset[OTR_A_NODE_ROW]);
-    std::vector<uint4> adj(2ull * h.n_nodes + 2, make_uint4(0u, 0u, 0u, 0u));
+    const int32_t* nll = (const int32_t*)(base + h.array_offset[OTR_A_NODE_LL]);
+    std::vector<uint4> adj(4ull * h.n_nodes + 4, make_uint4(kAdjDstMask, 0u, 0u, 0u));
     for (uint32_t u = 0; u < h.n_nodes; ++u) {
-      uint32_t* w = (uint32_t*)&adj[2ull * u];
-      for (int k = 0; k < 4; ++k) {
-        w[2 * k] = kAdjDstMask;  // empty slot: access bits 0
-        w[2 * k + 1] = 0u;
-      }
       const uint32_t deg = row[u + 1] - row[u];
       for (uint32_t k = 0; k < deg && k < 4; ++k) {
         const uint32_t e = row[u] + k;
-        w[2 * k] = dst[e] | ((attr[e] & OTR_ATTR_ACCESS_MASK) << 28);
-        w[2 * k + 1] = len[e];
+        adj[4ull * u + k] = make_uint4(dst[e] | ((attr[e] & OTR_ATTR_ACCESS_MASK) << 28), len[e],
+                                       (uint32_t)nll[2ull * dst[e]], (uint32_t)nll[2ull * dst[e] + 1]);
       }
-      if (deg > 4) w[6] |= kAdjMore;
+      if (deg > 4) adj[4ull * u + 3].x |= kAdjMore;
     }
     void* da = nullptr;
     HIPCHK(hipMalloc(&da, sizeof(uint4) * adj.size()));
@@ -177,7 +175,7 @@ int engine_configure(const Config& cfg, std::string* err) {
 enum Slot {
   S_TRACE_OFF, S_LAT, S_LON, S_TIME, S_ACC, S_MODE,
   S_STATE_CNT, S_TRACE_STATE_OFF, S_STATE_PROBE, S_STATE_TRACE,
-  S_CAND_EDGE, S_CAND_P, S_CAND_SQD, S_CAND_COUNT,
+  S_CAND_EDGE, S_CAND_P, S_CAND_SQD, S_CAND_COUNT, S_CAND_RADIUS,
   S_PREV, S_G, S_BOUND, S_FORCED, S_NTASK, S_NTRANS, S_TASK_OFF, S_TRANS_OFF,
   S_TASK_STATE, S_TASK_MASK, S_TASK_OVF, S_TRANS,
   S_BP, S_BRK, S_END_WIN, S_WINNER, S_SUBPATH,
@@ -356,6 +354,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   cb.p = need<double>(S_CAND_P, (size_t)S * OTR_KMAX);
   cb.sqd = need<double>(S_CAND_SQD, (size_t)S * OTR_KMAX);
   cb.count = need<int32_t>(S_CAND_COUNT, S);
+  cb.radius = need<double>(S_CAND_RADIUS, S);
   if (!cb.edge || !cb.p || !cb.sqd || !cb.count) {
     if (err) *err = "device allocation failed (candidates)";
     return OTR_DEVICE_ERROR;
@@ -416,35 +415,43 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   ra.cand_p = cb.p;
   ra.state_trace = state_trace;
   ra.mode = b.mode;
+  ra.state_probe = state_probe;
+  ra.lat = b.lat;
+  ra.lon = b.lon;
+  ra.radius = cb.radius;
   ra.delta = mp.delta;
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
   ra.overflow_flag = task_ovf;
   if (NT > 0) {
     tb(OTR_STAGE_ROUTE);
-    k_route<512><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
+    k_route<256><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
     te(OTR_STAGE_ROUTE);
-    // overflow retry with the large table
+    // overflow retries with larger LDS tables (same results, fewer resident waves)
     int64_t* list = need<int64_t>(S_LIST, NT);
     unsigned long long* cnt = need<unsigned long long>(S_MISC, 4);
-    HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
-    k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
-    unsigned long long novf = 0;
-    HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipStreamSynchronize(stream));
-    if (novf > 0) {
+    tb(OTR_STAGE_ROUTE_BIG);
+    for (int tier = 0; tier < 2; ++tier) {
+      HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
+      k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
+      unsigned long long novf = 0;
+      HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      if (novf == 0) break;
       HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.n_tasks = (int64_t)novf;
-      tb(OTR_STAGE_ROUTE_BIG);
-      k_route<8192><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
-      te(OTR_STAGE_ROUTE_BIG);
-      HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
-      k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
-      HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipStreamSynchronize(stream));
-      out->n_overflow_traces += (int32_t)novf;
+      if (tier == 0) k_route<1024><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
+      else k_route<4096><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
+      if (tier == 1) {
+        HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
+        k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
+        HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        out->n_overflow_traces += (int32_t)novf;
+      }
     }
+    te(OTR_STAGE_ROUTE_BIG);
   }
   // ---- K5: Viterbi
   ViterbiArgs va{};
@@ -498,6 +505,10 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       pa.cand_p = cb.p;
       pa.state_trace = state_trace;
       pa.mode = b.mode;
+      pa.state_probe = state_probe;
+      pa.lat = b.lat;
+      pa.lon = b.lon;
+      pa.radius = cb.radius;
       pa.delta = mp.delta;
       pa.path_off = path_off;
       pa.path_len = path_len;
@@ -507,24 +518,26 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       pa.overflow_flag = step_ovf;
       pa.cap_flag = (int32_t*)(cnt + 2);
       tb(OTR_STAGE_PATHS);
-      k_paths<512><<<(unsigned)(8 * ((nsteps + 7) / 8)), 64, 0, stream>>>(g, pa, nullptr, (int64_t)nsteps);
+      k_paths<256><<<(unsigned)(8 * ((nsteps + 7) / 8)), 64, 0, stream>>>(g, pa, nullptr, (int64_t)nsteps);
       te(OTR_STAGE_PATHS);
-      // large-table retry for table overflows
+      // large-table retries for table overflows
       int64_t* rl = need<int64_t>(S_TASK_STATE, NT > (int64_t)nsteps ? NT : (int64_t)nsteps);  // reuse
       unsigned long long* c2 = cnt + 3;
-      HIPCHK(hipMemsetAsync(c2, 0, 8, stream));
-      k_collect<<<grid_for(nsteps, 256), 256, 0, stream>>>((int64_t)nsteps, step_ovf, rl, c2);
       unsigned long long host[3] = {0, 0, 0};
-      HIPCHK(hipMemcpyAsync(host, cnt + 1, 24, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipStreamSynchronize(stream));
-      if (host[2] > 0) {
-        HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
-        tb(OTR_STAGE_PATHS_BIG);
-        k_paths<8192><<<(unsigned)host[2], 64, 0, stream>>>(g, pa, rl, (int64_t)host[2]);
-        te(OTR_STAGE_PATHS_BIG);
-        HIPCHK(hipMemcpyAsync(host, cnt + 1, 16, hipMemcpyDeviceToHost, stream));
+      tb(OTR_STAGE_PATHS_BIG);
+      for (int tier = 0; tier < 2; ++tier) {
+        HIPCHK(hipMemsetAsync(c2, 0, 8, stream));
+        k_collect<<<grid_for(nsteps, 256), 256, 0, stream>>>((int64_t)nsteps, step_ovf, rl, c2);
+        HIPCHK(hipMemcpyAsync(host, cnt + 1, 24, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
+        if (host[2] == 0) break;
+        HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
+        if (tier == 0) k_paths<1024><<<(unsigned)host[2], 64, 0, stream>>>(g, pa, rl, (int64_t)host[2]);
+        else k_paths<4096><<<(unsigned)host[2], 64, 0, stream>>>(g, pa, rl, (int64_t)host[2]);
       }
+      te(OTR_STAGE_PATHS_BIG);
+      HIPCHK(hipMemcpyAsync(host, cnt + 1, 16, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
       if ((int32_t)(host[1] & 0xFFFFFFFFu) == 0) break;  // cap flag clear: done
       capacity = (int64_t)host[0] + (int64_t)host[0] / 2 + 1024;  // grow and redo
     }

@@ -63,6 +63,7 @@ struct CandBuf {
   double* p;
   double* sqd;
   int32_t* count;
+  double* radius;   // per state search radius
 };
 
 __device__ inline bool cand_less(double da, uint32_t ea, double db, uint32_t eb) {
@@ -192,7 +193,10 @@ __global__ __launch_bounds__(64) void k_candidates(DevGraph g, BatchDev b, ModeP
       out.p[o + rank] = s_p[buf][idx];
       out.sqd[o + rank] = d;
     }
-    if (lane == 0) out.count[s] = n;
+    if (lane == 0) {
+      out.count[s] = n;
+      out.radius[s] = radius;
+    }
     // algorithmic-byte counters
     for (int off = 32; off > 0; off >>= 1) tests += __shfl_xor(tests, off);
     if (lane == 0 && counters) {
@@ -296,7 +300,8 @@ __global__ void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* ca
 template <int CAP>
 struct SearchLds {
   uint32_t key[CAP];              // node id | INQ bit, 0xFFFFFFFF empty
-  unsigned long long dist[CAP];   // binary64 bits
+  unsigned long long dist[CAP];   // binary64 bits of the label
+  float hv[CAP];                  // A* heuristic of the node
   uint16_t pend[CAP];
   uint16_t work[CAP];
   int n_pend, n_work, n_keys, overflow, all_done;
@@ -305,6 +310,26 @@ struct SearchLds {
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kInq = 0x80000000u;
 constexpr unsigned long long kInfBits = 0x7FF0000000000000ull;
+constexpr double kEps = 1e-6;  // metres; dominates every binary64 rounding of a label sum
+
+// Straight-line lower bound toward the target probe's search disk (P, r), in a
+// fixed metric whose lon scale is the cosine at the most poleward latitude the
+// search can reach, weakened by 1% and 1 m: consistent (h(u) - h(v) <= len(u,v))
+// with margin, so A* ordering never changes a label, only the explored set.
+struct Heur {
+  double plat, plon, mpl, r;
+  __device__ double operator()(int32_t lat_e6, int32_t lon_e6) const {
+    const double dx = (e6(lon_e6) - plon) * mpl, dy = (e6(lat_e6) - plat) * kMetersPerDeg;
+    const double h = (sqrt(dx * dx + dy * dy) - r) * 0.99 - 1.0;
+    return h > 0.0 ? h : 0.0;
+  }
+};
+
+__device__ inline Heur make_heur(double plat, double plon, double r, double bound) {
+  double lat = fabs(plat) + 2.0 * bound / kMetersPerDeg;
+  if (lat > 89.9) lat = 89.9;
+  return Heur{plat, plon, kMetersPerDeg * cos_deg(lat), r};
+}
 
 template <int CAP>
 __device__ inline int lds_find(const SearchLds<CAP>& L, uint32_t node) {
@@ -319,7 +344,7 @@ __device__ inline int lds_find(const SearchLds<CAP>& L, uint32_t node) {
 }
 
 template <int CAP>
-__device__ inline int lds_insert(SearchLds<CAP>& L, uint32_t node) {
+__device__ inline int lds_insert(SearchLds<CAP>& L, uint32_t node, bool* isnew) {
   uint32_t h = hmix(node) & (CAP - 1);
   for (int probe = 0; probe < CAP; ++probe) {
     uint32_t k = L.key[h];
@@ -328,11 +353,15 @@ __device__ inline int lds_insert(SearchLds<CAP>& L, uint32_t node) {
       if (old == kEmpty) {
         const int nk = atomicAdd(&L.n_keys, 1);
         if (nk >= (CAP * 3) / 4) L.overflow = 1;
+        *isnew = true;
         return (int)h;
       }
       k = old;
     }
-    if ((k & ~kInq) == node) return (int)h;
+    if ((k & ~kInq) == node) {
+      *isnew = false;
+      return (int)h;
+    }
     h = (h + 1) & (CAP - 1);
   }
   L.overflow = 1;
@@ -357,28 +386,35 @@ __device__ inline void search_init(SearchLds<CAP>& L) {
 
 __device__ inline double bits_d(unsigned long long b) { return __longlong_as_double((long long)b); }
 
-// Target (lane) resolved?  tnode == kEmpty: nothing to search for.  A label below the
-// minimum pending label is final; otherwise every later label is >= dmin, so the route
-// (d0 + label) + tpart >= (d0min + dmin) + tpart, which exceeding the bound proves the
-// target unreachable for every source of the task.
+// Target (lane) resolved?  tnode == kEmpty: nothing to search for.  With a consistent
+// heuristic every path through a pending node u reaches T with label >=
+// g(u) + h(u) - h(T) >= fmin - h(T); so a label below fmin - h(T) - eps is final, and
+// if even min(label, fmin - h(T) - eps) cannot make (d0 + label) + tpart fit the
+// bound, the target is unreachable for every source of the task.
 template <int CAP>
-__device__ inline bool target_resolved(const SearchLds<CAP>& L, uint32_t tnode, double tpart, double d0min,
-                                       double bound, double dmin, bool pend_empty) {
+__device__ inline bool target_resolved(const SearchLds<CAP>& L, uint32_t tnode, double tpart, double hT,
+                                       double d0min, double bound, double fmin, bool pend_empty) {
   if (tnode == kEmpty || pend_empty) return true;
   const int sl = lds_find(L, tnode);
-  if (sl >= 0 && bits_d(L.dist[sl]) < dmin) return true;
-  return (d0min + dmin) + tpart > bound;
+  const double lab = sl >= 0 ? bits_d(L.dist[sl]) : __builtin_huge_val();
+  const double lb_pend = fmin - hT - kEps;
+  if (lab < lb_pend) return true;
+  const double lb = lab < lb_pend ? lab : lb_pend;
+  return (d0min + lb) + tpart > bound + kEps;
 }
 
 template <int CAP>
-__device__ inline void relax_one(SearchLds<CAP>& L, uint32_t dw, uint32_t lw, double du, double bound,
-                                 uint32_t mode_bit, unsigned long long& relaxed) {
+__device__ inline void relax_one(SearchLds<CAP>& L, const Heur& H, uint32_t dw, uint32_t lw, int32_t vlat,
+                                 int32_t vlon, double du, double bound, uint32_t mode_bit,
+                                 unsigned long long& relaxed) {
   if (!(((dw >> 28) & 7u) & mode_bit)) return;
   ++relaxed;
   const double nd = du + (double)__uint_as_float(lw);
   if (nd > bound) return;
-  const int sl = lds_insert(L, dw & kAdjDstMask);
+  bool isnew = false;
+  const int sl = lds_insert(L, dw & kAdjDstMask, &isnew);
   if (sl < 0) return;
+  if (isnew) L.hv[sl] = (float)H(vlat, vlon);
   const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
   const unsigned long long old = atomicMin(&L.dist[sl], nb);
   if (nb < old) {
@@ -391,36 +427,43 @@ __device__ inline void relax_one(SearchLds<CAP>& L, uint32_t dw, uint32_t lw, do
   }
 }
 
-// Runs the search rooted at `start` (label 0).  Lanes j < n_tgt hold target node
-// tnode and target partial length tpart.  Returns false on LDS-table overflow.
+// Search rooted at `start` (label 0), processed in rounds of f = label + h below
+// (minimum pending f + delta).  Lanes j < n_tgt hold target node tnode, its
+// heuristic hT and the target partial length tpart.  false = LDS-table overflow.
 template <int CAP>
-__device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_bit, uint32_t start, double bound,
-                           double delta, uint32_t tnode, double tpart, double d0min, int n_tgt,
-                           unsigned long long* settled, unsigned long long* relaxed) {
+__device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, const Heur& H, uint32_t mode_bit, uint32_t start,
+                           double bound, double delta, uint32_t tnode, double tpart, double hT, double d0min,
+                           int n_tgt, unsigned long long* settled, unsigned long long* relaxed,
+                           unsigned long long* rounds) {
   const int lane = threadIdx.x;
   if (lane == 0) {
-    const int sl = lds_insert(L, start);
+    bool isnew;
+    const int sl = lds_insert(L, start, &isnew);
+    const int2 sll = g.node_ll[start];
+    L.hv[sl] = (float)H(sll.x, sll.y);
     L.dist[sl] = 0ull;  // +0.0
     L.key[sl] |= kInq;
     L.pend[0] = (uint16_t)sl;
     L.n_pend = 1;
   }
   __syncthreads();
-  unsigned long long my_settled = 0, my_relaxed = 0;
+  unsigned long long my_settled = 0, my_relaxed = 0, my_rounds = 0;
   for (;;) {
     const int np = L.n_pend;
-    double dmin = __builtin_huge_val();
+    double fmin = __builtin_huge_val();
     for (int k = lane; k < np; k += OTR_WAVE) {
-      const double d = bits_d(L.dist[L.pend[k]]);
-      dmin = d < dmin ? d : dmin;
+      const int sl = L.pend[k];
+      const double f = bits_d(L.dist[sl]) + (double)L.hv[sl];
+      fmin = f < fmin ? f : fmin;
     }
     for (int off = 32; off > 0; off >>= 1) {
-      const double o = __shfl_xor(dmin, off);
-      dmin = o < dmin ? o : dmin;
+      const double o = __shfl_xor(fmin, off);
+      fmin = o < fmin ? o : fmin;
     }
-    const bool res = lane >= n_tgt || target_resolved(L, tnode, tpart, d0min, bound, dmin, np == 0);
+    const bool res = lane >= n_tgt || target_resolved(L, tnode, tpart, hT, d0min, bound, fmin, np == 0);
     if (__ballot(!res) == 0ull || np == 0) break;
-    const double theta = dmin + delta;
+    ++my_rounds;
+    const double theta = fmin + delta;
     int kept = 0, nw = 0;
     for (int base = 0; base < np; base += OTR_WAVE) {
       const int k = base + lane;
@@ -428,7 +471,7 @@ __device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_b
       bool take = false;
       if (k < np) {
         sl = L.pend[k];
-        take = bits_d(L.dist[sl]) < theta;
+        take = bits_d(L.dist[sl]) + (double)L.hv[sl] < theta;
       }
       const unsigned long long mt = __ballot(take), mk = __ballot(k < np && !take);
       __syncthreads();
@@ -444,22 +487,23 @@ __device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_b
     }
     if (lane == 0) L.n_pend = kept;
     __syncthreads();
-    for (int base = 0; base < nw; base += OTR_WAVE) {
+    // relax: lane = (work node, adjacency slot), so a round's dependent chain is a
+    // single relaxation; slot 3 of a node with more than 4 out-edges also walks the CSR tail
+    for (int base = 0; base < 4 * nw; base += OTR_WAVE) {
       const int k = base + lane;
-      if (k < nw) {
-        const int ws = L.work[k];
+      if (k < 4 * nw) {
+        const int ws = L.work[k >> 2];
+        const int slot = k & 3;
         const uint32_t u = L.key[ws] & ~kInq;
         const double du = bits_d(L.dist[ws]);
-        ++my_settled;
-        const uint4 r0 = g.adj[2 * (size_t)u], r1 = g.adj[2 * (size_t)u + 1];
-        relax_one(L, r0.x, r0.y, du, bound, mode_bit, my_relaxed);
-        relax_one(L, r0.z, r0.w, du, bound, mode_bit, my_relaxed);
-        relax_one(L, r1.x, r1.y, du, bound, mode_bit, my_relaxed);
-        relax_one(L, r1.z, r1.w, du, bound, mode_bit, my_relaxed);
-        if (r1.z & kAdjMore)
+        if (slot == 0) ++my_settled;
+        const uint4 r = g.adj[4 * (size_t)u + slot];
+        relax_one(L, H, r.x & ~kAdjMore, r.y, (int32_t)r.z, (int32_t)r.w, du, bound, mode_bit, my_relaxed);
+        if (slot == 3 && (r.x & kAdjMore))
           for (uint32_t e = g.node_row[u] + 4; e < g.node_row[u + 1]; ++e) {
             const uint4 pk = g.edge_pack[e];
-            relax_one(L, pk.x | ((pk.z & 7u) << 28), pk.y, du, bound, mode_bit, my_relaxed);
+            const int2 vll = g.node_ll[pk.x];
+            relax_one(L, H, pk.x | ((pk.z & 7u) << 28), pk.y, vll.x, vll.y, du, bound, mode_bit, my_relaxed);
           }
       }
     }
@@ -468,6 +512,7 @@ __device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_b
   }
   if (settled) *settled += my_settled;
   if (relaxed) *relaxed += my_relaxed;
+  if (rounds) *rounds += my_rounds;
   __syncthreads();
   return !L.overflow;
 }
@@ -492,6 +537,10 @@ struct RouteArgs {
   const double* cand_p;
   const int32_t* state_trace;
   const uint8_t* mode;
+  const int64_t* state_probe;
+  const double* lat;
+  const double* lon;
+  const double* radius;       // per state search radius (heuristic disk)
   double delta;
   double inv_beta[OTR_MODES];
   int32_t* overflow_flag;     // per task
@@ -537,12 +586,20 @@ __global__ __launch_bounds__(64) void k_route(DevGraph gr, RouteArgs a, unsigned
       if (lane < Kb) trow[(int64_t)(__ffsll((long long)m) - 1) * Kb + lane] = __builtin_huge_val();
     return;
   }
-  unsigned long long settled = 0, relaxed = 0;
+  unsigned long long settled = 0, relaxed = 0, rounds = 0;
   bool ok = true;
   const bool need = __ballot(needed) != 0ull;
+  const int64_t pb = a.state_probe[s];
+  const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], bound);
+  double hT = 0.0;
+  if (needed) {
+    const int2 tll = gr.node_ll[tnode];
+    hT = H(tll.x, tll.y);
+  }
   search_init<CAP>(L);
   if (need)
-    ok = search_run<CAP>(L, gr, mode_bit, root, bound, a.delta, tnode, tpart, d0min, Kb, &settled, &relaxed);
+    ok = search_run<CAP>(L, gr, H, mode_bit, root, bound, a.delta, tnode, tpart, hT, d0min, Kb, &settled, &relaxed,
+                         &rounds);
   double lab = __builtin_huge_val();
   if (ok && needed) {
     const int sl = lds_find(L, tnode);
@@ -571,6 +628,7 @@ __global__ __launch_bounds__(64) void k_route(DevGraph gr, RouteArgs a, unsigned
       atomicAdd(&counters[3 * kShards + sh], settled);
       atomicAdd(&counters[4 * kShards + sh], relaxed);
       atomicAdd(&counters[11 * kShards + sh], (unsigned long long)Kb);
+      atomicAdd(&counters[13 * kShards + sh], rounds);
       atomicAdd(&counters[12 * kShards + sh], (unsigned long long)__popcll(mask));
     }
   }
@@ -720,6 +778,10 @@ struct PathArgs {
   const double* cand_p;
   const int32_t* state_trace;
   const uint8_t* mode;
+  const int64_t* state_probe;
+  const double* lat;
+  const double* lon;
+  const double* radius;
   double delta;
   int64_t* path_off;           // per state
   int32_t* path_len;           // per state; -1 = same-edge step
@@ -785,9 +847,12 @@ __global__ __launch_bounds__(64) void k_paths(DevGraph gr, PathArgs a, const int
   const uint32_t mode_bit = 1u << mode;
   const double d0 = (1.0 - pi) * (double)gr.edge_len[ei];
   const uint32_t S = gr.edge_dst[ei], T = gr.edge_src[ej];
+  const int64_t pb = a.state_probe[s];
+  const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], a.bound[s]);
+  const int2 tll = gr.node_ll[T];
   search_init<CAP>(L);
-  const bool ok = search_run<CAP>(L, gr, mode_bit, S, a.bound[s], a.delta, lane == 0 ? T : kEmpty,
-                                  pj * (double)gr.edge_len[ej], d0, 1, nullptr, nullptr);
+  const bool ok = search_run<CAP>(L, gr, H, mode_bit, S, a.bound[s], a.delta, lane == 0 ? T : kEmpty,
+                                  pj * (double)gr.edge_len[ej], H(tll.x, tll.y), d0, 1, nullptr, nullptr, nullptr);
   if (!ok) {
     if (lane == 0) a.overflow_flag[k] = 1;
     return;
