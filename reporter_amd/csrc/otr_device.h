@@ -58,6 +58,7 @@ struct DevGraph {
   const uint4* edge_pack;      // {dst, len bits, attr, 0}: one 16-B load per relaxed edge
   const uint4* adj;            // 4 x uint4 per node: {dst | access<<28 | more<<31, len bits, dst lat_e6, dst lon_e6}
   const int2* node_ll;         // (lat_e6, lon_e6)
+  const uint4* radj;           // 4 x uint4 per node: first 4 in-edges {src | access<<28 | more<<31, len bits, edge id, 0}
   uint32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double grid_min_lat, grid_min_lon, grid_cell_deg;
 };

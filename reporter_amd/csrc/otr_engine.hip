@@ -142,6 +142,24 @@ int engine_configure(const Config& cfg, std::string* err) {
     gs.allocs.push_back(da);
     HIPCHK(hipMemcpy(da, adj.data(), sizeof(uint4) * adj.size(), hipMemcpyHostToDevice));
     g.adj = (const uint4*)da;
+    // reverse records for the predecessor walk: the first 4 in-edges of a node
+    const uint32_t* rrow = (const uint32_t*)(base + h.array_offset[OTR_A_REV_ROW]);
+    const uint32_t* redge = (const uint32_t*)(base + h.array_offset[OTR_A_REV_EDGE]);
+    const uint32_t* esrc = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_SRC]);
+    std::vector<uint4> radj(4ull * h.n_nodes + 4, make_uint4(kAdjDstMask, 0u, 0xFFFFFFFFu, 0u));
+    for (uint32_t v = 0; v < h.n_nodes; ++v) {
+      const uint32_t deg = rrow[v + 1] - rrow[v];
+      for (uint32_t k = 0; k < deg && k < 4; ++k) {
+        const uint32_t e = redge[rrow[v] + k];
+        radj[4ull * v + k] = make_uint4(esrc[e] | ((attr[e] & OTR_ATTR_ACCESS_MASK) << 28), len[e], e, 0u);
+      }
+      if (deg > 4) radj[4ull * v + 3].x |= kAdjMore;
+    }
+    void* dr = nullptr;
+    HIPCHK(hipMalloc(&dr, sizeof(uint4) * radj.size()));
+    gs.allocs.push_back(dr);
+    HIPCHK(hipMemcpy(dr, radj.data(), sizeof(uint4) * radj.size(), hipMemcpyHostToDevice));
+    g.radj = (const uint4*)dr;
   }
   for (void* p : gs.allocs)
     if (!p) {
@@ -478,14 +496,15 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   if (S > 0) k_fill_i32<<<grid_for(S, 256), 256, 0, stream>>>(path_len, S, 0);
   {
     int64_t* steps = need<int64_t>(S_LIST, S > NT ? S : NT);
-    unsigned long long* cnt = need<unsigned long long>(S_MISC, 4);
-    HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
+    // misc: [0] step count, [1] cap flag, [2] retry count, [8..8+64) shard cursors
+    unsigned long long* cnt = need<unsigned long long>(S_MISC, 8 + kShards);
+    HIPCHK(hipMemsetAsync(cnt, 0, 8 * (8 + kShards), stream));
     if (S > 0) k_step_list<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, cnt);
     unsigned long long nsteps = 0;
     HIPCHK(hipMemcpyAsync(&nsteps, cnt, 8, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
-    int64_t capacity = (int64_t)nsteps * 24 + 1024;
-    for (int attempt = 0; attempt < 4 && nsteps > 0; ++attempt) {
+    int64_t capacity = kShards * ((int64_t)nsteps * 24 / kShards + 1024);
+    for (int attempt = 0; attempt < 6 && nsteps > 0; ++attempt) {
       uint32_t* path = need<uint32_t>(S_PATH, capacity);
       int32_t* step_ovf = need<int32_t>(S_STEP_OVF, nsteps + 1);
       if (!path || !step_ovf) {
@@ -493,7 +512,8 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
         return OTR_DEVICE_ERROR;
       }
       HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
-      HIPCHK(hipMemsetAsync(cnt + 1, 0, 16, stream));  // cursor, cap flag
+      HIPCHK(hipMemsetAsync(cnt + 1, 0, 16, stream));
+      HIPCHK(hipMemsetAsync(cnt + 8, 0, 8 * kShards, stream));
       PathArgs pa{};
       pa.steps = steps;
       pa.n_steps = (int64_t)nsteps;
@@ -513,33 +533,41 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       pa.path_off = path_off;
       pa.path_len = path_len;
       pa.path = path;
-      pa.cursor = cnt + 1;
+      pa.cursor = cnt + 8;
       pa.capacity = capacity;
       pa.overflow_flag = step_ovf;
-      pa.cap_flag = (int32_t*)(cnt + 2);
+      pa.cap_flag = (int32_t*)(cnt + 1);
       tb(OTR_STAGE_PATHS);
       k_paths<256><<<(unsigned)(8 * ((nsteps + 7) / 8)), 64, 0, stream>>>(g, pa, nullptr, (int64_t)nsteps);
       te(OTR_STAGE_PATHS);
       // large-table retries for table overflows
       int64_t* rl = need<int64_t>(S_TASK_STATE, NT > (int64_t)nsteps ? NT : (int64_t)nsteps);  // reuse
-      unsigned long long* c2 = cnt + 3;
-      unsigned long long host[3] = {0, 0, 0};
+      unsigned long long nretry = 0;
       tb(OTR_STAGE_PATHS_BIG);
-      for (int tier = 0; tier < 2; ++tier) {
-        HIPCHK(hipMemsetAsync(c2, 0, 8, stream));
-        k_collect<<<grid_for(nsteps, 256), 256, 0, stream>>>((int64_t)nsteps, step_ovf, rl, c2);
-        HIPCHK(hipMemcpyAsync(host, cnt + 1, 24, hipMemcpyDeviceToHost, stream));
+      for (int tier = 0; tier < 3; ++tier) {
+        HIPCHK(hipMemsetAsync(cnt + 2, 0, 8, stream));
+        k_collect<<<grid_for(nsteps, 256), 256, 0, stream>>>((int64_t)nsteps, step_ovf, rl, cnt + 2);
+        HIPCHK(hipMemcpyAsync(&nretry, cnt + 2, 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
-        if (host[2] == 0) break;
+        if (nretry == 0) break;
+        if (tier == 2) {
+          out->n_overflow_traces += (int32_t)nretry;
+          break;
+        }
         HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
-        if (tier == 0) k_paths<1024><<<(unsigned)host[2], 64, 0, stream>>>(g, pa, rl, (int64_t)host[2]);
-        else k_paths<4096><<<(unsigned)host[2], 64, 0, stream>>>(g, pa, rl, (int64_t)host[2]);
+        if (tier == 0) k_paths<1024><<<(unsigned)nretry, 64, 0, stream>>>(g, pa, rl, (int64_t)nretry);
+        else k_paths<4096><<<(unsigned)nretry, 64, 0, stream>>>(g, pa, rl, (int64_t)nretry);
       }
       te(OTR_STAGE_PATHS_BIG);
-      HIPCHK(hipMemcpyAsync(host, cnt + 1, 16, hipMemcpyDeviceToHost, stream));
+      unsigned long long capflag = 0;
+      std::vector<unsigned long long> cur(kShards);
+      HIPCHK(hipMemcpyAsync(&capflag, cnt + 1, 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(cur.data(), cnt + 8, 8 * kShards, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
-      if ((int32_t)(host[1] & 0xFFFFFFFFu) == 0) break;  // cap flag clear: done
-      capacity = (int64_t)host[0] + (int64_t)host[0] / 2 + 1024;  // grow and redo
+      if ((capflag & 0xFFFFFFFFu) == 0) break;  // every path fitted its region
+      unsigned long long mx = 0;
+      for (auto c : cur) mx = c > mx ? c : mx;
+      capacity = kShards * ((int64_t)mx + (int64_t)mx / 2 + 1024);  // grow and redo
     }
   }
   // ---- K7: stitching, segments, report()

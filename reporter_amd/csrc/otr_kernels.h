@@ -70,37 +70,155 @@ __device__ inline bool cand_less(double da, uint32_t ea, double db, uint32_t eb)
   return da < db || (da == db && ea < eb);
 }
 
+// Projection of probe (plat, plon) onto edge e's polyline in the probe-local metric;
+// true when the edge is a candidate owned by grid cell (r, c) (the cell holding the
+// snapped point), with squared distance d2 and fraction along the edge.
+__device__ inline bool project_edge(const DevGraph& g, uint32_t e, uint32_t mode_bit, double plat, double plon,
+                                    double mpl, double r2, int64_t r, int64_t c, double* d2_out, double* frac_out,
+                                    unsigned long long* tests) {
+  if (!(g.edge_attr[e] & mode_bit)) return false;
+  double best = __builtin_huge_val();
+  double best_along = 0.0, bqx = 0.0, bqy = 0.0, acc = 0.0;
+  const uint32_t k0 = g.edge_shape[e], k1 = g.edge_shape[e + 1];
+  int2 pa = g.shape_ll[k0];
+  for (uint32_t k = k0; k + 1 < k1; ++k) {
+    const int2 pb = g.shape_ll[k + 1];
+    const double ax = (e6(pa.y) - plon) * mpl;
+    const double ay = (e6(pa.x) - plat) * kMetersPerDeg;
+    const double bx = (e6(pb.y) - plon) * mpl;
+    const double by = (e6(pb.x) - plat) * kMetersPerDeg;
+    const double dx = bx - ax, dy = by - ay;
+    const double l2 = dx * dx + dy * dy;
+    double t = 0.0;
+    if (l2 > 0.0) {
+      t = -(ax * dx + ay * dy) / l2;
+      if (t < 0.0) t = 0.0;
+      if (t > 1.0) t = 1.0;
+    }
+    const double qx = ax + t * dx, qy = ay + t * dy;
+    const double d2 = qx * qx + qy * qy;
+    const double sl = sqrt(l2);
+    if (d2 < best) {
+      best = d2;
+      best_along = acc + t * sl;
+      bqx = qx;
+      bqy = qy;
+    }
+    acc = acc + sl;
+    pa = pb;
+  }
+  *tests += k1 - k0 - 1;
+  if (!(best <= r2)) return false;
+  const double slat = plat + bqy / kMetersPerDeg, slon = plon + bqx / mpl;
+  const int64_t sr = (int64_t)floor((slat - g.grid_min_lat) / g.grid_cell_deg);
+  const int64_t sc = (int64_t)floor((slon - g.grid_min_lon) / g.grid_cell_deg);
+  if (sr != r || sc != c) return false;
+  *d2_out = best;
+  *frac_out = acc > 0.0 ? best_along / acc : 0.0;
+  return true;
+}
+
+constexpr int kWin = 16;  // flattened cell windows up to 16 x 16 cells
+
 __global__ __launch_bounds__(64) void k_candidates(DevGraph g, BatchDev b, ModeParams mp, int64_t n_states,
                                                    const int64_t* state_probe, const int32_t* state_trace,
                                                    CandBuf out, unsigned long long* counters) {
   __shared__ double s_d2[2][2 * OTR_WAVE];
   __shared__ double s_p[2][2 * OTR_WAVE];
   __shared__ uint32_t s_e[2][2 * OTR_WAVE];
+  __shared__ uint32_t s_bnd[kWin][kWin + 1];  // cell_row boundaries of the window, per row
+  __shared__ uint32_t s_pre[kWin + 1];        // entries before each row
   const int lane = threadIdx.x;
-  for (int64_t s = xcd_remap(blockIdx.x, (n_states + 7) / 8); s < n_states; s = n_states) {
-    const int64_t probe = state_probe[s];
-    const int mode = b.mode[state_trace[s]] < OTR_MODES ? b.mode[state_trace[s]] : 0;
-    const MatchParams& P = mp.m[mode];
-    const uint32_t mode_bit = 1u << mode;
-    const int kmax = P.kmax;
-    const double plat = b.lat[probe], plon = b.lon[probe];
-    const double a = (b.acc && b.acc[probe] >= 0.f) ? (double)b.acc[probe] : P.gps_accuracy;
-    double radius = P.search_radius > a ? P.search_radius : a;
-    if (radius > P.max_search_radius) radius = P.max_search_radius;
-    const double mpl = kMetersPerDeg * cos_deg(plat);
-    const double cd = g.grid_cell_deg;
-    const double dlat = radius / kMetersPerDeg, dlon = radius / mpl;
-    int64_t r0 = (int64_t)floor((plat - dlat - OTR_GRID_PAD_DEG - g.grid_min_lat) / cd);
-    int64_t r1 = (int64_t)floor((plat + dlat + OTR_GRID_PAD_DEG - g.grid_min_lat) / cd);
-    int64_t c0 = (int64_t)floor((plon - dlon - OTR_GRID_PAD_DEG - g.grid_min_lon) / cd);
-    int64_t c1 = (int64_t)floor((plon + dlon + OTR_GRID_PAD_DEG - g.grid_min_lon) / cd);
-    if (r0 < 0) r0 = 0;
-    if (c0 < 0) c0 = 0;
-    if (r1 > (int64_t)g.grid_rows - 1) r1 = (int64_t)g.grid_rows - 1;
-    if (c1 > (int64_t)g.grid_cols - 1) c1 = (int64_t)g.grid_cols - 1;
-    const double r2 = radius * radius;
-    int n = 0, buf = 0;
-    unsigned long long tests = 0;
+  const int64_t s = xcd_remap(blockIdx.x, (n_states + 7) / 8);
+  if (s >= n_states) return;
+  const int64_t probe = state_probe[s];
+  const int mode = b.mode[state_trace[s]] < OTR_MODES ? b.mode[state_trace[s]] : 0;
+  const MatchParams& P = mp.m[mode];
+  const uint32_t mode_bit = 1u << mode;
+  const int kmax = P.kmax;
+  const double plat = b.lat[probe], plon = b.lon[probe];
+  const double a = (b.acc && b.acc[probe] >= 0.f) ? (double)b.acc[probe] : P.gps_accuracy;
+  double radius = P.search_radius > a ? P.search_radius : a;
+  if (radius > P.max_search_radius) radius = P.max_search_radius;
+  const double mpl = kMetersPerDeg * cos_deg(plat);
+  const double cd = g.grid_cell_deg;
+  const double dlat = radius / kMetersPerDeg, dlon = radius / mpl;
+  int64_t r0 = (int64_t)floor((plat - dlat - OTR_GRID_PAD_DEG - g.grid_min_lat) / cd);
+  int64_t r1 = (int64_t)floor((plat + dlat + OTR_GRID_PAD_DEG - g.grid_min_lat) / cd);
+  int64_t c0 = (int64_t)floor((plon - dlon - OTR_GRID_PAD_DEG - g.grid_min_lon) / cd);
+  int64_t c1 = (int64_t)floor((plon + dlon + OTR_GRID_PAD_DEG - g.grid_min_lon) / cd);
+  if (r0 < 0) r0 = 0;
+  if (c0 < 0) c0 = 0;
+  if (r1 > (int64_t)g.grid_rows - 1) r1 = (int64_t)g.grid_rows - 1;
+  if (c1 > (int64_t)g.grid_cols - 1) c1 = (int64_t)g.grid_cols - 1;
+  const double r2 = radius * radius;
+  int n = 0, buf = 0;
+  unsigned long long tests = 0;
+  // merge one wave's worth of qualifying candidates into the LDS top-K list
+  auto merge = [&](bool ok, double d2, double frac, uint32_t e) {
+    const unsigned long long mask = __ballot(ok);
+    if (!mask) return;
+    if (ok) {
+      const int pos = n + prefix_count(mask);
+      s_d2[buf][pos] = d2;
+      s_p[buf][pos] = frac;
+      s_e[buf][pos] = e;
+    }
+    n += __popcll(mask);
+    __syncthreads();
+    if (n > kmax) {  // rank-compact to the kmax best (all (d2, edge) keys distinct)
+      for (int idx = lane; idx < n; idx += OTR_WAVE) {
+        const double d = s_d2[buf][idx];
+        const uint32_t ee = s_e[buf][idx];
+        int rank = 0;
+        for (int m = 0; m < n; ++m) rank += cand_less(s_d2[buf][m], s_e[buf][m], d, ee);
+        if (rank < kmax) {
+          s_d2[buf ^ 1][rank] = d;
+          s_p[buf ^ 1][rank] = s_p[buf][idx];
+          s_e[buf ^ 1][rank] = ee;
+        }
+      }
+      __syncthreads();
+      buf ^= 1;
+      n = kmax;
+    }
+  };
+  const int nr = (int)(r1 - r0 + 1), nc = (int)(c1 - c0 + 1);
+  if (nr >= 1 && nc >= 1 && nr <= kWin && nc <= kWin) {
+    // The cells of one grid row are contiguous in cell_edge: flatten the window into
+    // one entry range per row and sweep all rows with full waves.
+    for (int idx = lane; idx < nr * (nc + 1); idx += OTR_WAVE) {
+      const int rr = idx / (nc + 1), cc = idx % (nc + 1);
+      s_bnd[rr][cc] = g.cell_row[(r0 + rr) * (int64_t)g.grid_cols + c0 + cc];
+    }
+    __syncthreads();
+    if (lane == 0) {
+      uint32_t acc = 0;
+      for (int rr = 0; rr < nr; ++rr) {
+        s_pre[rr] = acc;
+        acc += s_bnd[rr][nc] - s_bnd[rr][0];
+      }
+      s_pre[nr] = acc;
+    }
+    __syncthreads();
+    const uint32_t total = s_pre[nr];
+    for (uint32_t base = 0; base < total; base += OTR_WAVE) {
+      const uint32_t k = base + lane;
+      bool ok = false;
+      double d2 = 0, frac = 0;
+      uint32_t e = 0;
+      if (k < total) {
+        int rr = 0;
+        while (rr + 1 < nr && s_pre[rr + 1] <= k) ++rr;
+        const uint32_t q = s_bnd[rr][0] + (k - s_pre[rr]);
+        int cc = 0;
+        while (cc + 1 < nc && s_bnd[rr][cc + 1] <= q) ++cc;
+        e = g.cell_edge[q];
+        ok = project_edge(g, e, mode_bit, plat, plon, mpl, r2, r0 + rr, c0 + cc, &d2, &frac, &tests);
+      }
+      merge(ok, d2, frac, e);
+    }
+  } else {
     for (int64_t r = r0; r <= r1; ++r)
       for (int64_t c = c0; c <= c1; ++c) {
         const uint32_t cell = (uint32_t)(r * g.grid_cols + c);
@@ -108,104 +226,37 @@ __global__ __launch_bounds__(64) void k_candidates(DevGraph g, BatchDev b, ModeP
         for (uint32_t base = beg; base < end; base += OTR_WAVE) {
           const uint32_t q = base + lane;
           bool ok = false;
-          double best = 0, frac = 0;
+          double d2 = 0, frac = 0;
           uint32_t e = 0;
           if (q < end) {
             e = g.cell_edge[q];
-            if (g.edge_attr[e] & mode_bit) {
-              best = __builtin_huge_val();
-              double best_along = 0.0, bqx = 0.0, bqy = 0.0, acc = 0.0;
-              const uint32_t k0 = g.edge_shape[e], k1 = g.edge_shape[e + 1];
-              int2 pa = g.shape_ll[k0];
-              for (uint32_t k = k0; k + 1 < k1; ++k) {
-                const int2 pb = g.shape_ll[k + 1];
-                const double ax = (e6(pa.y) - plon) * mpl;
-                const double ay = (e6(pa.x) - plat) * kMetersPerDeg;
-                const double bx = (e6(pb.y) - plon) * mpl;
-                const double by = (e6(pb.x) - plat) * kMetersPerDeg;
-                const double dx = bx - ax, dy = by - ay;
-                const double l2 = dx * dx + dy * dy;
-                double t = 0.0;
-                if (l2 > 0.0) {
-                  t = -(ax * dx + ay * dy) / l2;
-                  if (t < 0.0) t = 0.0;
-                  if (t > 1.0) t = 1.0;
-                }
-                const double qx = ax + t * dx, qy = ay + t * dy;
-                const double d2 = qx * qx + qy * qy;
-                const double sl = sqrt(l2);
-                if (d2 < best) {
-                  best = d2;
-                  best_along = acc + t * sl;
-                  bqx = qx;
-                  bqy = qy;
-                }
-                acc = acc + sl;
-                pa = pb;
-              }
-              tests += k1 - k0 - 1;
-              if (best <= r2) {
-                const double slat = plat + bqy / kMetersPerDeg, slon = plon + bqx / mpl;
-                const int64_t sr = (int64_t)floor((slat - g.grid_min_lat) / cd);
-                const int64_t sc = (int64_t)floor((slon - g.grid_min_lon) / cd);
-                ok = (sr == r && sc == c);
-                frac = acc > 0.0 ? best_along / acc : 0.0;
-              }
-            }
+            ok = project_edge(g, e, mode_bit, plat, plon, mpl, r2, r, c, &d2, &frac, &tests);
           }
-          const unsigned long long mask = __ballot(ok);
-          if (mask) {
-            if (ok) {
-              const int pos = n + prefix_count(mask);
-              s_d2[buf][pos] = best;
-              s_p[buf][pos] = frac;
-              s_e[buf][pos] = e;
-            }
-            n += __popcll(mask);
-            __syncthreads();
-            if (n > kmax) {  // rank-compact to the kmax best (all (d2,edge) keys distinct)
-              for (int idx = lane; idx < n; idx += OTR_WAVE) {
-                const double d = s_d2[buf][idx];
-                const uint32_t ee = s_e[buf][idx];
-                int rank = 0;
-                for (int m = 0; m < n; ++m) rank += cand_less(s_d2[buf][m], s_e[buf][m], d, ee);
-                if (rank < kmax) {
-                  s_d2[buf ^ 1][rank] = d;
-                  s_p[buf ^ 1][rank] = s_p[buf][idx];
-                  s_e[buf ^ 1][rank] = ee;
-                }
-              }
-              __syncthreads();
-              buf ^= 1;
-              n = kmax;
-            }
-          }
+          merge(ok, d2, frac, e);
         }
       }
-    // final ordering
-    const size_t o = (size_t)s * OTR_KMAX;
-    for (int idx = lane; idx < n; idx += OTR_WAVE) {
-      const double d = s_d2[buf][idx];
-      const uint32_t ee = s_e[buf][idx];
-      int rank = 0;
-      for (int m = 0; m < n; ++m) rank += cand_less(s_d2[buf][m], s_e[buf][m], d, ee);
-      out.edge[o + rank] = ee;
-      out.p[o + rank] = s_p[buf][idx];
-      out.sqd[o + rank] = d;
-    }
-    if (lane == 0) {
-      out.count[s] = n;
-      out.radius[s] = radius;
-    }
-    // algorithmic-byte counters
-    for (int off = 32; off > 0; off >>= 1) tests += __shfl_xor(tests, off);
-    if (lane == 0 && counters) {
-      const int sh = blockIdx.x & (kShards - 1);
-      atomicAdd(&counters[0 * kShards + sh], (unsigned long long)((r1 - r0 + 1) * (c1 - c0 + 1)));
-      atomicAdd(&counters[1 * kShards + sh], tests);
-      atomicAdd(&counters[2 * kShards + sh], (unsigned long long)n);
-    }
-    __syncthreads();
+  }
+  // final ordering
+  const size_t o = (size_t)s * OTR_KMAX;
+  for (int idx = lane; idx < n; idx += OTR_WAVE) {
+    const double d = s_d2[buf][idx];
+    const uint32_t ee = s_e[buf][idx];
+    int rank = 0;
+    for (int m = 0; m < n; ++m) rank += cand_less(s_d2[buf][m], s_e[buf][m], d, ee);
+    out.edge[o + rank] = ee;
+    out.p[o + rank] = s_p[buf][idx];
+    out.sqd[o + rank] = d;
+  }
+  if (lane == 0) {
+    out.count[s] = n;
+    out.radius[s] = radius;
+  }
+  for (int off = 32; off > 0; off >>= 1) tests += __shfl_xor(tests, off);
+  if (lane == 0 && counters) {
+    const int sh = blockIdx.x & (kShards - 1);
+    atomicAdd(&counters[0 * kShards + sh], (unsigned long long)((r1 - r0 + 1) * (c1 - c0 + 1)));
+    atomicAdd(&counters[1 * kShards + sh], tests);
+    atomicAdd(&counters[2 * kShards + sh], (unsigned long long)n);
   }
 }
 
@@ -792,38 +843,59 @@ struct PathArgs {
   int32_t* cap_flag;           // global: path buffer too small
 };
 
+// Predecessor walk from T back to the root S in ONE pass: lanes 0-3 read the four
+// in-edge slots of the node's reverse record (one 64-B line), keep (u→v) with
+// label(u) + len == label(v), and the smallest edge id wins.  Edges land in LDS
+// (reusing the pend/work arrays as CAP u32 slots), reversed into root→T order.
 template <int CAP>
-__device__ int walk_preds(const SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_bit, uint32_t S, uint32_t T,
-                          uint32_t* out, int64_t out_n) {
+__device__ int walk_preds(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_bit, uint32_t S, uint32_t T) {
   const int lane = threadIdx.x;
+  uint32_t* path = reinterpret_cast<uint32_t*>(L.pend);  // pend+work are contiguous: CAP u32
   uint32_t v = T;
   int n = 0;
   while (v != S) {
+    if (n >= CAP) return -1;
     const int sv = lds_find(L, v);
     if (sv < 0) return -1;
     const double dv = bits_d(L.dist[sv]);
-    uint32_t best = kEmpty;
-    for (uint32_t base = g.rev_row[v]; base < g.rev_row[v + 1]; base += OTR_WAVE) {
-      const uint32_t r = base + lane;
-      uint32_t cand = kEmpty;
-      if (r < g.rev_row[v + 1]) {
-        const uint32_t ed = g.rev_edge[r];
-        if (g.edge_attr[ed] & mode_bit) {
-          const int su = lds_find(L, g.edge_src[ed]);
-          if (su >= 0 && bits_d(L.dist[su]) + (double)g.edge_len[ed] == dv) cand = ed;
+    uint32_t best = kEmpty, best_src = kEmpty;
+    if (lane < 4) {
+      const uint4 r = g.radj[4 * (size_t)v + lane];
+      if (((r.x >> 28) & 7u) & mode_bit) {
+        const uint32_t u = r.x & kAdjDstMask;
+        const int su = lds_find(L, u);
+        if (su >= 0 && bits_d(L.dist[su]) + (double)__uint_as_float(r.y) == dv) {
+          best = r.z;
+          best_src = u;
         }
       }
-      for (int off = 32; off > 0; off >>= 1) {
-        const uint32_t o = __shfl_xor(cand, off);
-        cand = o < cand ? o : cand;
-      }
-      best = cand < best ? cand : best;
+      if (lane == 3 && (r.x & kAdjMore))  // in-degree > 4: CSR tail
+        for (uint32_t q = g.rev_row[v] + 4; q < g.rev_row[v + 1]; ++q) {
+          const uint32_t ed = g.rev_edge[q];
+          if (!(g.edge_attr[ed] & mode_bit)) continue;
+          const uint32_t u = g.edge_src[ed];
+          const int su = lds_find(L, u);
+          if (su >= 0 && bits_d(L.dist[su]) + (double)g.edge_len[ed] == dv && ed < best) {
+            best = ed;
+            best_src = u;
+          }
+        }
     }
+    for (int off = 1; off < 4; off <<= 1) {
+      const uint32_t ob = __shfl_xor(best, off), os = __shfl_xor(best_src, off);
+      if (ob < best) {
+        best = ob;
+        best_src = os;
+      }
+    }
+    best = __shfl(best, 0);
+    best_src = __shfl(best_src, 0);
     if (best == kEmpty) return -1;
-    if (out && lane == 0) out[out_n - 1 - n] = best;
+    if (lane == 0) path[n] = best;
     ++n;
-    v = g.edge_src[best];
+    v = best_src;
   }
+  __syncthreads();
   return n;
 }
 
@@ -857,19 +929,25 @@ __global__ __launch_bounds__(64) void k_paths(DevGraph gr, PathArgs a, const int
     if (lane == 0) a.overflow_flag[k] = 1;
     return;
   }
-  const int n = walk_preds<CAP>(L, gr, mode_bit, S, T, nullptr, 0);
+  const int n = walk_preds<CAP>(L, gr, mode_bit, S, T);
   if (n < 0) {
     if (lane == 0) a.overflow_flag[k] = 2;
     return;
   }
+  // bump allocation in one of 64 regions (a single cursor serialises ~1M returning
+  // atomics on one address)
+  const int shard = (int)(blockIdx.x & (kShards - 1));
+  const int64_t region = a.capacity / kShards;
   int64_t off = 0;
-  if (lane == 0) off = (int64_t)atomicAdd(a.cursor, (unsigned long long)n);
+  if (lane == 0) off = (int64_t)atomicAdd(&a.cursor[shard], (unsigned long long)n);
   off = __shfl(off, 0);
-  if (off + n > a.capacity) {
+  if (off + n > region) {
     if (lane == 0) *a.cap_flag = 1;
     return;
   }
-  walk_preds<CAP>(L, gr, mode_bit, S, T, a.path + off, n);
+  off += (int64_t)shard * region;
+  const uint32_t* lp = reinterpret_cast<const uint32_t*>(L.pend);
+  for (int q = lane; q < n; q += OTR_WAVE) a.path[off + q] = lp[n - 1 - q];
   if (lane == 0) {
     a.path_off[s] = off;
     a.path_len[s] = n;
