@@ -54,6 +54,8 @@ def main():
     ap.add_argument('--cpu-traces', type=int, default=1500, help='bounded oracle sample (0 = skip)')
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--delta', type=float, default=None, help='routing round width (perf knob, metres)')
+    ap.add_argument('--streams', type=int, default=2,
+                    help='matchers (one HIP stream + host thread each) sharing the batch')
     args = ap.parse_args()
 
     rank = int(os.environ.get('RANK', 0))
@@ -97,32 +99,44 @@ def main():
         cfg['otr']['delta'] = args.delta
     M.configure(cfg)
     n_nodes, n_edges, n_segments = M.graph_info()
-    m = M.Matcher()
 
+    # one matcher per host thread, each on its own HIP stream, each with a contiguous
+    # slice of this GPU's traces (reporter_service.py:51-52: one matcher per thread)
+    from concurrent.futures import ThreadPoolExecutor
+    ns = max(1, args.streams)
+    cuts = np.linspace(0, mine.n_traces, ns + 1).astype(np.int64)
+    parts = [mine.subset(np.arange(cuts[k], cuts[k + 1])) for k in range(ns)]
+    matchers = [M.Matcher() for _ in range(ns)]
     dev = torch.device('cuda', local)
-    t_off = torch.from_numpy(mine.offsets).to(dev)
-    t_lat = torch.from_numpy(mine.lat).to(dev)
-    t_lon = torch.from_numpy(mine.lon).to(dev)
-    t_time = torch.from_numpy(mine.time).to(dev)
-    t_mode = torch.from_numpy(mine.mode).to(dev)
-    darr = {'trace_offsets': t_off.data_ptr(), 'lat': t_lat.data_ptr(), 'lon': t_lon.data_ptr(),
-            'time': t_time.data_ptr(), 'mode': t_mode.data_ptr()}
     hours = 3  # traces start within 30 min of T_BEGIN and last 25 min
     hist_len = hours * n_segments * _lib.HIST_BINS
     hist_len += (-hist_len) % world
+    keep, darrs, hists = [], [], []
+    for part in parts:
+        t = [torch.from_numpy(x).to(dev) for x in (part.offsets, part.lat, part.lon, part.time, part.mode)]
+        keep.append(t)
+        darrs.append({'trace_offsets': t[0].data_ptr(), 'lat': t[1].data_ptr(), 'lon': t[2].data_ptr(),
+                      'time': t[3].data_ptr(), 'mode': t[4].data_ptr()})
+        hists.append(torch.zeros(hist_len, dtype=torch.int32, device=dev))
     hist = torch.zeros(hist_len, dtype=torch.int32, device=dev)
     hist_out = torch.zeros(hist_len // world, dtype=torch.int32, device=dev)
+    pool = ThreadPoolExecutor(max_workers=ns)
     torch.cuda.synchronize()
 
-    def step():
-        r = m.match_batch(mine, device_arrays=darr, hist_device=hist.data_ptr(), hist_hours=hours,
-                          hist_base_time=T_BEGIN, copy_out=False, timing=True)
+    def run_part(k):
+        r = matchers[k].match_batch(parts[k], device_arrays=darrs[k], hist_device=hists[k].data_ptr(),
+                                    hist_hours=hours, hist_base_time=T_BEGIN, copy_out=False, timing=True)
         if r.status != 0:
             raise RuntimeError('batch status %d (%d overflow tasks)' % (r.status, r.n_overflow_traces))
+        return r
+
+    def step():
+        rs = list(pool.map(run_part, range(ns)))
+        torch.sum(torch.stack(hists), dim=0, out=hist)  # combine the per-stream histograms
         if world > 1:
             dist.reduce_scatter_tensor(hist_out, hist, op=dist.ReduceOp.SUM)
-            torch.cuda.current_stream().synchronize()
-        return r
+        torch.cuda.current_stream().synchronize()
+        return rs
 
     for _ in range(args.warmup):
         step()
@@ -131,9 +145,9 @@ def main():
     t_start = time.perf_counter()
     route_ms, results = [], []
     for _ in range(args.steps):
-        r = step()
-        route_ms.append(r.kernel_ms[_lib.STAGES.index('route')])
-        results.append(r)
+        rs = step()
+        route_ms.extend(r.kernel_ms[_lib.STAGES.index('route')] for r in rs)
+        results.append(rs)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
@@ -146,11 +160,12 @@ def main():
     total_probes = float(probes.item())
     value = total_probes * args.steps / elapsed
 
-    r = results[-1]
-    counters = list(r.counters)
-    stage_ms = {s: round(float(r.kernel_ms[i]), 3) for i, s in enumerate(_lib.STAGES) if r.kernel_ms[i] > 0}
+    rs = results[-1]
+    counters = [sum(int(r.counters[k]) for r in rs) for k in range(len(rs[0].counters))]
+    stage_ms = {s: round(float(np.mean([r.kernel_ms[i] for r in rs])), 3) for i, s in enumerate(_lib.STAGES)
+                if rs[0].kernel_ms[i] > 0}
     route_avg_ms = float(np.mean(route_ms))
-    rbytes = route_bytes(counters)
+    rbytes = route_bytes(counters) / ns  # per launch (each stream launches once per step)
     achieved = rbytes / (route_avg_ms * 1e-3) / 1e9
 
     cpu = None
@@ -186,15 +201,17 @@ def main():
                        'probes_per_step': int(total_probes),
                        'parallelism': 'uuid-sharded dp%d + RCCL reduce-scatter of [hour][segment][speed] histogram'
                                       % world if world > 1 else 'single GPU',
-                       'stage_ms': stage_ms},
-            'roofline': {'kernel': 'k_route<512> (K3 bounded one-to-many search + K4 transition)',
+                       'streams': ns,
+                       'stage_ms_per_stream': stage_ms},
+            'roofline': {'kernel': 'k_route<256> (K3 bounded one-to-many search + K4 transition)',
                          'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': None,
                          'launch_ms': round(route_avg_ms, 3), 'algorithmic_bytes': int(rbytes),
                          'settled_nodes': int(counters[3]), 'relaxed_edges': int(counters[4]),
                          'tasks': int(counters[5]), 'transition_entries': int(counters[6]),
                          'source_candidates': int(counters[12]),
-                         'retry_settled_nodes': int(counters[9]), 'search_rounds': int(counters[13])},
+                         'retry_settled_nodes': int(counters[9]), 'search_rounds': int(counters[13]),
+                         'phase_cycles': [int(x) for x in counters[16:20]] if any(counters[16:20]) else None},
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)

@@ -129,12 +129,13 @@ typedef struct otr_batch_result {
   uint32_t* d_hist;            /* [hist_hours][n_segments][OTR_HIST_BINS] observation counts */
   int64_t hist_len;            /* elements */
   /* algorithmic byte counters, summed over the batch */
-  uint64_t counters[16];       /* algorithmic work counters: 0 cells visited,
+  uint64_t counters[24];       /* algorithmic work counters: 0 cells visited,
                                   1 shape segments tested, 2 candidates, 3 settled nodes and
                                   4 relaxed edges (first-tier route launch), 5 search tasks,
                                   6 transition entries, 7 output segments, 8 tile rows,
                                   9/10 settled/relaxed of the large-table retry, 11 target reads,
-                                  12 source candidates, 13 search rounds */
+                                  12 source candidates, 13 search rounds,
+                                  16-19 diagnostic-build search phase cycles */
   float kernel_ms[16];         /* OTR_BATCH_TIMING: device time per stage, OTR_STAGE_* */
 } otr_batch_result;
 

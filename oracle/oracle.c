@@ -29,6 +29,7 @@ struct orc_graph {
   const int32_t *node_ll, *shape_ll;
   const float* edge_len;
   const uint64_t* seg_id;
+  uint32_t* len_mm; /* routing length, whole millimetres */
 };
 
 orc_graph* orc_graph_load(const char* path) {
@@ -68,11 +69,14 @@ orc_graph* orc_graph_load(const char* path) {
   g->cell_row = (const uint32_t*)A(OTR_A_CELL_ROW);
   g->cell_edge = (const uint32_t*)A(OTR_A_CELL_EDGE);
 #undef A
+  g->len_mm = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)g->h.n_edges + 1));
+  for (uint32_t e = 0; e < g->h.n_edges; ++e) g->len_mm[e] = (uint32_t)llround((double)g->edge_len[e] * 1000.0);
   return g;
 }
 
 void orc_graph_free(orc_graph* g) {
   if (!g) return;
+  free(g->len_mm);
   free(g->blob);
   free(g);
 }
@@ -207,9 +211,10 @@ static int find_candidates(const orc_graph* g, double plat, double plon, double 
 /* ---------------------------------------------------------------------------- */
 /* bounded one-to-many Dijkstra (UPSTREAM meili routing.cc)        */
 /* ---------------------------------------------------------------------------- */
+#define NO_LABEL INT64_MAX
 typedef struct {
   uint32_t* key;  /* node id, UINT32_MAX empty */
-  double* dist;
+  int64_t* dist;  /* label, millimetres */
   uint8_t* done;
   uint32_t cap, n;
 } nodemap_t;
@@ -227,7 +232,7 @@ static void nm_init(nodemap_t* m, uint32_t cap) {
   m->cap = cap;
   m->n = 0;
   m->key = (uint32_t*)malloc(cap * sizeof(uint32_t));
-  m->dist = (double*)malloc(cap * sizeof(double));
+  m->dist = (int64_t*)malloc(cap * sizeof(int64_t));
   m->done = (uint8_t*)malloc(cap);
   memset(m->key, 0xFF, cap * sizeof(uint32_t));
 }
@@ -256,7 +261,7 @@ static uint32_t nm_insert(nodemap_t* m, uint32_t k, int* isnew) {
     s = (s + 1) & (m->cap - 1);
   }
   m->key[s] = k;
-  m->dist[s] = INFINITY;
+  m->dist[s] = NO_LABEL;
   m->done[s] = 0;
   m->n++;
   *isnew = 1;
@@ -276,7 +281,7 @@ static void nm_grow(nodemap_t* m) {
 }
 
 typedef struct {
-  double d;
+  int64_t d;
   uint32_t node;
 } heap_item;
 typedef VEC(heap_item) heap_t;
@@ -309,29 +314,29 @@ static heap_item hpop(heap_t* h) {
   return top;
 }
 
-/* Labels every node reachable from `start` (initial label d0) with the minimal
- * left-to-right binary64 sum of edge lengths, keeping only labels <= bound. */
-static void dijkstra(const orc_graph* g, uint32_t start, double d0, double bound, uint32_t mode_bit,
-                     nodemap_t* m) {
+/* Labels every node reachable from `start` (label 0) with its shortest-path length in
+ * whole millimetres (integer, so exact and order-independent), keeping only labels
+ * <= bound_mm. */
+static void dijkstra(const orc_graph* g, uint32_t start, int64_t bound_mm, uint32_t mode_bit, nodemap_t* m) {
   m->n = 0;
   memset(m->key, 0xFF, m->cap * sizeof(uint32_t));
   heap_t hp = {0};
   int nw;
   uint32_t s = nm_insert(m, start, &nw);
-  m->dist[s] = d0;
-  heap_item it0 = {d0, start};
+  m->dist[s] = 0;
+  heap_item it0 = {0, start};
   hpush(&hp, it0);
   while (hp.n) {
     heap_item it = hpop(&hp);
     uint32_t su = nm_find(m, it.node);
     if (m->done[su] || it.d > m->dist[su]) continue;
     m->done[su] = 1;
-    double du = m->dist[su];
+    int64_t du = m->dist[su];
     uint32_t u = it.node;
     for (uint32_t e = g->node_row[u]; e < g->node_row[u + 1]; ++e) {
       if (!(g->edge_attr[e] & mode_bit)) continue;
-      double nd = du + (double)g->edge_len[e];
-      if (nd > bound) continue;
+      int64_t nd = du + (int64_t)g->len_mm[e];
+      if (nd > bound_mm) continue;
       uint32_t sv = nm_insert(m, g->edge_dst[e], &nw);
       if (nd < m->dist[sv]) {
         m->dist[sv] = nd;
@@ -343,30 +348,35 @@ static void dijkstra(const orc_graph* g, uint32_t start, double d0, double bound
   free(hp.d);
 }
 
-/* route distance from candidate (ei,pi) to (ej,pj) given labels rooted (label 0)
- * at dst(ei): (d0 + label(src(ej))) + pj*len(ej), d0 = (1-pi)*len(ei) */
-static double route_from_labels(const orc_graph* g, const nodemap_t* m, uint32_t ei, double pi, uint32_t ej,
-                                double pj) {
-  if (ej == ei && pj >= pi) return (pj - pi) * (double)g->edge_len[ei];
+/* metres → whole millimetres of the routing bound and the partial edge lengths */
+static int64_t bound_mm_of(double bound) { return (int64_t)floor(bound * 1000.0); }
+static int64_t part_mm(double frac, uint32_t len_mm) { return (int64_t)llround(frac * (double)len_mm); }
+
+/* route length in mm from candidate (ei,pi) to (ej,pj) given labels rooted at dst(ei):
+ * same edge forward: round((pj-pi)*len); else round((1-pi)*len_i) + label(src(ej)) +
+ * round(pj*len_j).  INT64_MAX when src(ej) was not reached. */
+static int64_t route_from_labels(const orc_graph* g, const nodemap_t* m, uint32_t ei, double pi, uint32_t ej,
+                                 double pj) {
+  if (ej == ei && pj >= pi) return part_mm(pj - pi, g->len_mm[ei]);
   uint32_t s = nm_find(m, g->edge_src[ej]);
-  if (s == 0xFFFFFFFFu) return INFINITY;
-  double d0 = (1.0 - pi) * (double)g->edge_len[ei];
-  return (d0 + m->dist[s]) + pj * (double)g->edge_len[ej];
+  if (s == 0xFFFFFFFFu) return NO_LABEL;
+  return part_mm(1.0 - pi, g->len_mm[ei]) + m->dist[s] + part_mm(pj, g->len_mm[ej]);
 }
 
 int orc_route_dist(const orc_graph* g, uint32_t src_edge, double src_p, uint32_t dst_edge, double dst_p,
                    double bound, uint32_t mode_bit, double* out_dist) {
   nodemap_t m;
   nm_init(&m, 1024);
-  double r = INFINITY;
+  int64_t r = NO_LABEL;
+  const int64_t bmm = bound_mm_of(bound);
   if (dst_edge == src_edge && dst_p >= src_p) {
-    r = (dst_p - src_p) * (double)g->edge_len[src_edge];
+    r = part_mm(dst_p - src_p, g->len_mm[src_edge]);
   } else {
-    dijkstra(g, g->edge_dst[src_edge], 0.0, bound, mode_bit, &m);
+    dijkstra(g, g->edge_dst[src_edge], bmm, mode_bit, &m);
     r = route_from_labels(g, &m, src_edge, src_p, dst_edge, dst_p);
   }
   nm_free(&m);
-  *out_dist = r <= bound ? r : INFINITY;
+  *out_dist = r <= bmm ? (double)r / 1000.0 : INFINITY;
   return 0;
 }
 
@@ -465,8 +475,8 @@ typedef struct {
 } trace_out;
 
 typedef struct {
-  uint32_t e, pct_full_end; /* pct_full_end unused marker */
-  double s0, s1;
+  uint32_t e, pad;
+  int64_t s0, s1; /* route positions, whole millimetres */
 } portion_t;
 
 typedef struct {
@@ -484,10 +494,12 @@ typedef struct {
   pthread_mutex_t mu;
 } job_t;
 
-static double time_at(const double* pos, const double* tm, int n, double s) {
+/* time at route position s (mm): linear between the states around it */
+static double time_at(const int64_t* pos, const double* tm, int n, int64_t s) {
   int k = 0;
   while (k < n - 2 && s > pos[k + 1]) ++k;
-  if (pos[k + 1] > pos[k]) return tm[k] + (tm[k + 1] - tm[k]) * ((s - pos[k]) / (pos[k + 1] - pos[k]));
+  if (pos[k + 1] > pos[k])
+    return tm[k] + (tm[k + 1] - tm[k]) * ((double)(s - pos[k]) / (double)(pos[k + 1] - pos[k]));
   return tm[k];
 }
 
@@ -563,6 +575,7 @@ static void match_trace(job_t* J, int32_t t) {
     double gfl = gcd > P->interpolation_distance ? gcd : P->interpolation_distance;
     double bound = P->max_route_distance_factor * gfl;
     if (bound > P->breakage_distance) bound = P->breakage_distance;
+    const int64_t bmm = bound_mm_of(bound);
     uint32_t searched = 0xFFFFFFFFu; /* labels rooted at this node are in nm */
     for (int i = 0; i < Ka; ++i) {
       for (int j = 0; j < Kb; ++j) trans[i * ORC_KMAX + j] = INFINITY;
@@ -570,8 +583,8 @@ static void match_trace(job_t* J, int32_t t) {
       int need = 0;
       for (int j = 0; j < Kb; ++j) {
         if (cb[j].e == ca[i].e && cb[j].p >= ca[i].p) {
-          double r = (cb[j].p - ca[i].p) * (double)g->edge_len[ca[i].e];
-          if (r <= bound) trans[i * ORC_KMAX + j] = fabs(r - gcd) * inv_beta;
+          int64_t r = part_mm(cb[j].p - ca[i].p, g->len_mm[ca[i].e]);
+          if (r <= bmm) trans[i * ORC_KMAX + j] = fabs((double)r / 1000.0 - gcd) * inv_beta;
         } else {
           need = 1;
         }
@@ -580,12 +593,12 @@ static void match_trace(job_t* J, int32_t t) {
       /* one search per root node: labels do not depend on the source edge */
       if (g->edge_dst[ca[i].e] != searched) {
         searched = g->edge_dst[ca[i].e];
-        dijkstra(g, searched, 0.0, bound, mode_bit, &nm);
+        dijkstra(g, searched, bmm, mode_bit, &nm);
       }
       for (int j = 0; j < Kb; ++j) {
         if (cb[j].e == ca[i].e && cb[j].p >= ca[i].p) continue;
-        double r = route_from_labels(g, &nm, ca[i].e, ca[i].p, cb[j].e, cb[j].p);
-        if (r <= bound) trans[i * ORC_KMAX + j] = fabs(r - gcd) * inv_beta;
+        int64_t r = route_from_labels(g, &nm, ca[i].e, ca[i].p, cb[j].e, cb[j].p);
+        if (r <= bmm) trans[i * ORC_KMAX + j] = fabs((double)r / 1000.0 - gcd) * inv_beta;
       }
     }
     int any = 0;
@@ -643,7 +656,7 @@ static void match_trace(job_t* J, int32_t t) {
   /* 4. route stitching + OSMLR segments (§3.7-3.8) */
   {
     VEC(portion_t) por = {0};
-    double* pos = (double*)malloc(sizeof(double) * (na + 1));
+    int64_t* pos = (int64_t*)malloc(sizeof(int64_t) * (na + 1));
     double* stm = (double*)malloc(sizeof(double) * (na + 1));
     int k = 0;
     int first_sub = 1;
@@ -658,8 +671,8 @@ static void match_trace(job_t* J, int32_t t) {
       por.n = 0;
       const cand_t* c = &O->cands.d[(size_t)act[a] * ORC_KMAX + O->winner.d[act[a]]];
       uint32_t cur_e = c->e;
-      double cur_s0 = 0.0;
-      pos[0] = 0.0;
+      int64_t cur_s0 = 0;
+      pos[0] = 0;
       stm[0] = (double)tm[O->state_probe.d[act[a]] - b];
       VPUSH(O->route, cur_e);
       for (int q = a + 1; q <= bidx; ++q) {
@@ -667,13 +680,13 @@ static void match_trace(job_t* J, int32_t t) {
         const cand_t* cj = &O->cands.d[(size_t)act[q] * ORC_KMAX + O->winner.d[act[q]]];
         stm[q - a] = (double)tm[O->state_probe.d[act[q]] - b];
         if (cj->e == ci->e && cj->p >= ci->p) {
-          pos[q - a] = pos[q - a - 1] + (cj->p - ci->p) * (double)g->edge_len[ci->e];
+          pos[q - a] = pos[q - a - 1] + part_mm(cj->p - ci->p, g->len_mm[ci->e]);
           continue;
         }
-        double end_s = pos[q - a - 1] + (1.0 - ci->p) * (double)g->edge_len[ci->e];
+        int64_t end_s = pos[q - a - 1] + part_mm(1.0 - ci->p, g->len_mm[ci->e]);
         portion_t pt = {cur_e, 0, cur_s0, end_s};
         VPUSH(por, pt);
-        double s = end_s;
+        int64_t s = end_s;
         /* path: re-run the bounded search from the winner and walk predecessors */
         int64_t ia = O->state_probe.d[act[q - 1]] - b, ib = O->state_probe.d[act[q]] - b;
         double gcd = gc_dist(lat[ia], lon[ia], lat[ib], lon[ib]);
@@ -681,19 +694,19 @@ static void match_trace(job_t* J, int32_t t) {
         double bound = P->max_route_distance_factor * gfl;
         if (bound > P->breakage_distance) bound = P->breakage_distance;
         uint32_t S = g->edge_dst[ci->e], T = g->edge_src[cj->e];
-        dijkstra(g, S, 0.0, bound, mode_bit, &nm);
+        dijkstra(g, S, bound_mm_of(bound), mode_bit, &nm);
         VEC(uint32_t) path = {0};
         uint32_t v = T;
         while (v != S) {
           uint32_t sv = nm_find(&nm, v);
-          double dv = nm.dist[sv];
+          int64_t dv = nm.dist[sv];
           uint32_t best_e = 0xFFFFFFFFu;
           for (uint32_t r = g->rev_row[v]; r < g->rev_row[v + 1]; ++r) {
             uint32_t ed = g->rev_edge[r];
             if (!(g->edge_attr[ed] & mode_bit)) continue;
             uint32_t su = nm_find(&nm, g->edge_src[ed]);
             if (su == 0xFFFFFFFFu) continue;
-            if (nm.dist[su] + (double)g->edge_len[ed] == dv && ed < best_e) best_e = ed;
+            if (nm.dist[su] + (int64_t)g->len_mm[ed] == dv && ed < best_e) best_e = ed;
           }
           if (best_e == 0xFFFFFFFFu) break; /* unreachable by construction */
           VPUSH(path, best_e);
@@ -701,16 +714,16 @@ static void match_trace(job_t* J, int32_t t) {
         }
         for (size_t z = path.n; z-- > 0;) {
           uint32_t ed = path.d[z];
-          portion_t pp = {ed, 0, s, s + (double)g->edge_len[ed]};
+          portion_t pp = {ed, 0, s, s + (int64_t)g->len_mm[ed]};
           VPUSH(por, pp);
           VPUSH(O->route, ed);
-          s = s + (double)g->edge_len[ed];
+          s = s + (int64_t)g->len_mm[ed];
         }
         free(path.d);
         cur_e = cj->e;
         cur_s0 = s;
         VPUSH(O->route, cur_e);
-        pos[q - a] = s + cj->p * (double)g->edge_len[cj->e];
+        pos[q - a] = s + part_mm(cj->p, g->len_mm[cj->e]);
       }
       portion_t last = {cur_e, 0, cur_s0, pos[bidx - a]};
       VPUSH(por, last);
@@ -739,7 +752,7 @@ static void match_trace(job_t* J, int32_t t) {
           ++r;
         }
         size_t lq = r - 1;
-        double s0 = por.d[q].s0, s1 = por.d[lq].s1;
+        int64_t s0 = por.d[q].s0, s1 = por.d[lq].s1;
         double st = -1.0, et = -1.0;
         int32_t length = -1;
         if (key != OTR_NO_SEGMENT) {
@@ -770,7 +783,7 @@ static void match_trace(job_t* J, int32_t t) {
         VPUSH(O->seg_way_n, nw);
         /* shape indices: last trace index whose route position <= s (§3.8) */
         for (int which = 0; which < 2; ++which) {
-          double sq = which ? s1 : s0;
+          int64_t sq = which ? s1 : s0;
           int64_t best = lo;
           int st_ptr = -1;
           for (int64_t ti = lo; ti <= hi; ++ti) {

@@ -7,7 +7,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libotr.so')
+LIB_PATH = os.environ.get('OTR_LIB') or os.path.join(_HERE, 'libotr.so')
 P = ctypes.POINTER
 
 OTR_OK = 0
@@ -57,7 +57,7 @@ class BatchResult(ctypes.Structure):
                 ('rep_length', P(ctypes.c_int32)), ('rep_queue', P(ctypes.c_int32)),
                 ('shape_used', P(ctypes.c_int32)), ('stats', P(ctypes.c_int32)),
                 ('stats_len', P(ctypes.c_double)), ('d_hist', ctypes.c_void_p), ('hist_len', ctypes.c_int64),
-                ('counters', ctypes.c_uint64 * 16), ('kernel_ms', ctypes.c_float * 16)]
+                ('counters', ctypes.c_uint64 * 24), ('kernel_ms', ctypes.c_float * 16)]
 
 
 _L = None

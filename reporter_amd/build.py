@@ -50,19 +50,22 @@ def _newer(target, sources):
     return all(os.path.getmtime(s) <= t for s in sources)
 
 
-def build_otr(force=False):
+def build_otr(force=False, stamps=False):
+    """stamps=True: diagnostic build with per-phase shader-clock stamps (libotr_stamps.so)."""
     os.makedirs(BUILD, exist_ok=True)
+    suffix = '_stamps' if stamps else ''
+    extra = ['-DOTR_STAMPS'] if stamps else []
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
     headers += [os.path.join(ROOT, 'include', f) for f in os.listdir(os.path.join(ROOT, 'include'))]
     objs = []
     for src in ('otr_engine.hip', 'otr_api.cpp'):
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD, src + '.o')
+        o = os.path.join(BUILD, src + suffix + '.o')
         objs.append(o)
         if force or not _newer(o, [s] + headers):
             lang = [] if src.endswith('.hip') else ['-x', 'hip']
-            _run([HIPCC] + HIP_FLAGS + lang + ['-c', s, '-o', o])
-    lib = os.path.join(PKG, 'libotr.so')
+            _run([HIPCC] + HIP_FLAGS + extra + lang + ['-c', s, '-o', o])
+    lib = os.path.join(PKG, 'libotr%s.so' % suffix)
     if force or not _newer(lib, objs):
         rdir, rname = hip_runtime_dir()
         _run(['g++', '-shared', '-o', lib] + objs +
@@ -93,4 +96,7 @@ def build_all(force=False):
 
 
 if __name__ == '__main__':
-    print(build_all(force='--force' in sys.argv))
+    if '--stamps' in sys.argv:
+        print(build_otr(force='--force' in sys.argv, stamps=True))
+    else:
+        print(build_all(force='--force' in sys.argv))

@@ -13,7 +13,7 @@
 #define OTR_KMAX 64          // candidate slots per state (lanes of one wave)
 #define OTR_MODES 3          // auto, bicycle, pedestrian
 #define OTR_WAVE 64
-#define OTR_COUNTERS 16      // counter kinds, see otr_batch_result.counters
+#define OTR_COUNTERS 24      // counter kinds, see otr_batch_result.counters
 
 namespace otr {
 
@@ -55,10 +55,10 @@ struct DevGraph {
   const uint32_t* seg_len;
   const uint32_t* cell_row;
   const uint32_t* cell_edge;
-  const uint4* edge_pack;      // {dst, len bits, attr, 0}: one 16-B load per relaxed edge
-  const uint4* adj;            // 4 x uint4 per node: {dst | access<<28 | more<<31, len bits, dst lat_e6, dst lon_e6}
+  const uint4* edge_pack;      // {dst, len_mm, attr, 0}: one 16-B load per relaxed edge (CSR tail)
+  const uint4* adj;            // 4 x uint4 per node: {dst | access<<28 | more<<31, len_mm, dst lat_e6, dst lon_e6}
+  const uint32_t* len_mm;      // routing length, whole millimetres
   const int2* node_ll;         // (lat_e6, lon_e6)
-  const uint4* radj;           // 4 x uint4 per node: first 4 in-edges {src | access<<28 | more<<31, len bits, edge id, 0}
   uint32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double grid_min_lat, grid_min_lon, grid_cell_deg;
 };

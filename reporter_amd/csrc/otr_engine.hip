@@ -106,20 +106,27 @@ int engine_configure(const Config& cfg, std::string* err) {
   g.seg_len = (const uint32_t*)up(OTR_A_SEG_LEN, 4ull * h.n_segments);
   g.cell_row = (const uint32_t*)up(OTR_A_CELL_ROW, 4ull * (h.n_cells + 1));
   g.cell_edge = (const uint32_t*)up(OTR_A_CELL_EDGE, 4ull * h.n_cell_entries);
-  // routing view: {dst, len bits, attr, 0} per edge, one dwordx4 per relaxation
+  // routing views.  len_mm = round(len * 1000): the integer routing length the oracle
+  // derives the same way
   {
-    std::vector<uint4> pack(h.n_edges);
     const uint32_t* dst = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_DST]);
-    const uint32_t* len = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_LEN]);
+    const float* lenf = (const float*)(base + h.array_offset[OTR_A_EDGE_LEN]);
     const uint32_t* attr = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_ATTR]);
+    std::vector<uint32_t> len(h.n_edges + 1, 0u);
+    for (uint32_t e = 0; e < h.n_edges; ++e) len[e] = (uint32_t)llround((double)lenf[e] * 1000.0);
+    std::vector<uint4> pack(h.n_edges + 1);
     for (uint32_t e = 0; e < h.n_edges; ++e) pack[e] = make_uint4(dst[e], len[e], attr[e], 0u);
-    void* d = nullptr;
-    HIPCHK(hipMalloc(&d, sizeof(uint4) * (pack.size() + 1)));
-    gs.allocs.push_back(d);
-    HIPCHK(hipMemcpy(d, pack.data(), sizeof(uint4) * pack.size(), hipMemcpyHostToDevice));
-    g.edge_pack = (const uint4*)d;
+    auto upv = [&](const void* src, size_t bytes) -> void* {
+      void* d = nullptr;
+      if (hipMalloc(&d, bytes ? bytes : 16) != hipSuccess) return nullptr;
+      gs.allocs.push_back(d);
+      if (bytes) (void)hipMemcpy(d, src, bytes, hipMemcpyHostToDevice);
+      return d;
+    };
+    g.len_mm = (const uint32_t*)upv(len.data(), 4ull * len.size());
+    g.edge_pack = (const uint4*)upv(pack.data(), sizeof(uint4) * pack.size());
     // per-node adjacency records: the first 4 out-edges of a node in one 64-B record,
-    // {dst | access<<28 | more<<31, len bits, dst lat_e6, dst lon_e6} per edge
+    // {dst | access<<28 | more<<31, len_mm, dst lat_e6, dst lon_e6} per edge
     if (h.n_nodes >= (1u << 28)) {
       munmap(map, (size_t)st.st_size);
       if (err) *err = "graph has more than 2^28 nodes";
@@ -137,29 +144,7 @@ int engine_configure(const Config& cfg, std::string* err) {
       }
       if (deg > 4) adj[4ull * u + 3].x |= kAdjMore;
     }
-    void* da = nullptr;
-    HIPCHK(hipMalloc(&da, sizeof(uint4) * adj.size()));
-    gs.allocs.push_back(da);
-    HIPCHK(hipMemcpy(da, adj.data(), sizeof(uint4) * adj.size(), hipMemcpyHostToDevice));
-    g.adj = (const uint4*)da;
-    // reverse records for the predecessor walk: the first 4 in-edges of a node
-    const uint32_t* rrow = (const uint32_t*)(base + h.array_offset[OTR_A_REV_ROW]);
-    const uint32_t* redge = (const uint32_t*)(base + h.array_offset[OTR_A_REV_EDGE]);
-    const uint32_t* esrc = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_SRC]);
-    std::vector<uint4> radj(4ull * h.n_nodes + 4, make_uint4(kAdjDstMask, 0u, 0xFFFFFFFFu, 0u));
-    for (uint32_t v = 0; v < h.n_nodes; ++v) {
-      const uint32_t deg = rrow[v + 1] - rrow[v];
-      for (uint32_t k = 0; k < deg && k < 4; ++k) {
-        const uint32_t e = redge[rrow[v] + k];
-        radj[4ull * v + k] = make_uint4(esrc[e] | ((attr[e] & OTR_ATTR_ACCESS_MASK) << 28), len[e], e, 0u);
-      }
-      if (deg > 4) radj[4ull * v + 3].x |= kAdjMore;
-    }
-    void* dr = nullptr;
-    HIPCHK(hipMalloc(&dr, sizeof(uint4) * radj.size()));
-    gs.allocs.push_back(dr);
-    HIPCHK(hipMemcpy(dr, radj.data(), sizeof(uint4) * radj.size(), hipMemcpyHostToDevice));
-    g.radj = (const uint4*)dr;
+    g.adj = (const uint4*)upv(adj.data(), sizeof(uint4) * adj.size());
   }
   for (void* p : gs.allocs)
     if (!p) {
@@ -331,7 +316,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     b.acc = in->accuracy;
   }
   out->n_probes = N;
-  const size_t n_ctr = 2 * (size_t)OTR_COUNTERS * kShards;  // tier-2 kinds land at +6
+  const size_t n_ctr = 2 * (size_t)OTR_COUNTERS * kShards;  // tier-2 kinds land at +6, stamps at 16
   unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, n_ctr);
   HIPCHK(hipMemsetAsync(d_counters, 0, n_ctr * 8, stream));
   size_t scan_bytes = 0;
@@ -590,7 +575,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   sa.path_off = path_off;
   sa.path_len = path_len;
   sa.path = (const uint32_t*)need<uint32_t>(S_PATH, 1);
-  sa.pos = need<double>(S_POS, S);
+  sa.pos = need<int64_t>(S_POS, S);
   sa.act = need<int64_t>(S_ACT, S);
   sa.cap_off = cap_off;
   sa.route = need<uint32_t>(S_ROUTE, C);

@@ -339,40 +339,60 @@ __global__ void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* ca
 // ------------------------------------------------------------------------------
 // Bounded one-to-many search, one wave, node labels in an LDS hash table.
 //
-// Distance-bucketed label correcting: each round takes every pending node whose
-// label is below (minimum pending label + delta), relaxes its out-edges with LDS
-// 64-bit atomicMin on the binary64 bit pattern (positive doubles order like u64),
-// and re-queues improved nodes.  The fixed point is the minimal left-to-right
-// binary64 path sum from the root (label 0) — the value the oracle's binary-heap
-// Dijkstra settles — and a node whose label is below the minimum pending label is
-// final, so the search stops as soon as every target is final or provably beyond
-// the bound.  A node's first four out-edges come from one 32-B adjacency record.
+// Labels are whole millimetres (uint32), so every processing order reaches the same
+// fixed point as the oracle's binary-heap Dijkstra, exactly.  Rounds take every
+// pending node whose f = label + h is below (minimum pending f + delta); lane =
+// (node, adjacency slot); relaxation = LDS atomicMin.  With PRED the label word is
+// (label << 32 | edge id) so the minimum also records the smallest-id predecessor
+// edge among those achieving the label (the oracle's predecessor rule).
 // ------------------------------------------------------------------------------
-template <int CAP>
+template <bool PRED>
+struct LabelT {
+  using T = uint32_t;
+  static constexpr T kInf = 0xFFFFFFFFu;
+  __device__ static uint32_t label(T x) { return x; }
+  __device__ static T make(uint32_t l, uint32_t) { return l; }
+};
+template <>
+struct LabelT<true> {
+  using T = unsigned long long;
+  static constexpr T kInf = 0xFFFFFFFFFFFFFFFFull;
+  __device__ static uint32_t label(T x) { return (uint32_t)(x >> 32); }
+  __device__ static T make(uint32_t l, uint32_t e) { return ((unsigned long long)l << 32) | e; }
+};
+
+template <int CAP, bool PRED>
 struct SearchLds {
-  uint32_t key[CAP];              // node id | INQ bit, 0xFFFFFFFF empty
-  unsigned long long dist[CAP];   // binary64 bits of the label
-  float hv[CAP];                  // A* heuristic of the node
+  typename LabelT<PRED>::T lab[CAP];  // label (| pred edge)
+  uint32_t key[CAP];                  // node id | INQ bit, 0xFFFFFFFF empty
+  uint32_t hv[CAP];                   // A* heuristic, mm
   uint16_t pend[CAP];
   uint16_t work[CAP];
-  int n_pend, n_work, n_keys, overflow, all_done;
+  int n_pend, n_keys, overflow;
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kInq = 0x80000000u;
-constexpr unsigned long long kInfBits = 0x7FF0000000000000ull;
-constexpr double kEps = 1e-6;  // metres; dominates every binary64 rounding of a label sum
+constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
 
-// Straight-line lower bound toward the target probe's search disk (P, r), in a
-// fixed metric whose lon scale is the cosine at the most poleward latitude the
-// search can reach, weakened by 1% and 1 m: consistent (h(u) - h(v) <= len(u,v))
-// with margin, so A* ordering never changes a label, only the explored set.
+// Diagnostic build only (-DOTR_STAMPS): shader-clock stamps per search phase, summed
+// into counter kinds 16..19.  The production build compiles them out.
+#ifdef OTR_STAMPS
+#define OTR_STAMP(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define OTR_STAMP(v) const unsigned long long v = 0
+#endif
+
+// Straight-line lower bound (mm) toward the target probe's search disk (P, r), in a
+// fixed metric whose lon scale is the cosine at the most poleward latitude the search
+// can reach, weakened by 1% and 1 m and floored to whole mm: consistent (h(u) - h(v)
+// <= len_mm(u,v) for every edge), so A* ordering never changes a label.
 struct Heur {
   double plat, plon, mpl, r;
-  __device__ double operator()(int32_t lat_e6, int32_t lon_e6) const {
+  __device__ uint32_t operator()(int32_t lat_e6, int32_t lon_e6) const {
     const double dx = (e6(lon_e6) - plon) * mpl, dy = (e6(lat_e6) - plat) * kMetersPerDeg;
     const double h = (sqrt(dx * dx + dy * dy) - r) * 0.99 - 1.0;
-    return h > 0.0 ? h : 0.0;
+    return h > 0.0 ? (uint32_t)floor(h * 1000.0) : 0u;
   }
 };
 
@@ -382,8 +402,12 @@ __device__ inline Heur make_heur(double plat, double plon, double r, double boun
   return Heur{plat, plon, kMetersPerDeg * cos_deg(lat), r};
 }
 
-template <int CAP>
-__device__ inline int lds_find(const SearchLds<CAP>& L, uint32_t node) {
+// routing bound and partial edge lengths in whole mm (shared with the oracle)
+__device__ inline int64_t bound_mm_of(double bound) { return (int64_t)floor(bound * 1000.0); }
+__device__ inline int64_t part_mm(double frac, uint32_t len_mm) { return (int64_t)llround(frac * (double)len_mm); }
+
+template <int CAP, bool PRED>
+__device__ inline int lds_find(const SearchLds<CAP, PRED>& L, uint32_t node) {
   uint32_t h = hmix(node) & (CAP - 1);
   for (int probe = 0; probe < CAP; ++probe) {
     const uint32_t k = L.key[h];
@@ -394,8 +418,8 @@ __device__ inline int lds_find(const SearchLds<CAP>& L, uint32_t node) {
   return -1;
 }
 
-template <int CAP>
-__device__ inline int lds_insert(SearchLds<CAP>& L, uint32_t node, bool* isnew) {
+template <int CAP, bool PRED>
+__device__ inline int lds_insert(SearchLds<CAP, PRED>& L, uint32_t node, bool* isnew) {
   uint32_t h = hmix(node) & (CAP - 1);
   for (int probe = 0; probe < CAP; ++probe) {
     uint32_t k = L.key[h];
@@ -419,56 +443,51 @@ __device__ inline int lds_insert(SearchLds<CAP>& L, uint32_t node, bool* isnew) 
   return -1;
 }
 
-template <int CAP>
-__device__ inline void search_init(SearchLds<CAP>& L) {
+template <int CAP, bool PRED>
+__device__ inline void search_init(SearchLds<CAP, PRED>& L) {
   for (int k = threadIdx.x; k < CAP; k += OTR_WAVE) {
     L.key[k] = kEmpty;
-    L.dist[k] = kInfBits;
+    L.lab[k] = LabelT<PRED>::kInf;
   }
   if (threadIdx.x == 0) {
     L.n_pend = 0;
-    L.n_work = 0;
     L.n_keys = 0;
     L.overflow = 0;
-    L.all_done = 0;
   }
   __syncthreads();
 }
 
-__device__ inline double bits_d(unsigned long long b) { return __longlong_as_double((long long)b); }
-
-// Target (lane) resolved?  tnode == kEmpty: nothing to search for.  With a consistent
-// heuristic every path through a pending node u reaches T with label >=
-// g(u) + h(u) - h(T) >= fmin - h(T); so a label below fmin - h(T) - eps is final, and
-// if even min(label, fmin - h(T) - eps) cannot make (d0 + label) + tpart fit the
-// bound, the target is unreachable for every source of the task.
-template <int CAP>
-__device__ inline bool target_resolved(const SearchLds<CAP>& L, uint32_t tnode, double tpart, double hT,
-                                       double d0min, double bound, double fmin, bool pend_empty) {
-  if (tnode == kEmpty || pend_empty) return true;
-  const int sl = lds_find(L, tnode);
-  const double lab = sl >= 0 ? bits_d(L.dist[sl]) : __builtin_huge_val();
-  const double lb_pend = fmin - hT - kEps;
-  if (lab < lb_pend) return true;
-  const double lb = lab < lb_pend ? lab : lb_pend;
-  return (d0min + lb) + tpart > bound + kEps;
+// Target (lane) resolved?  Every path through a pending node u reaches T with label >=
+// L(u) + h(u) - h(T) >= fmin - h(T), so L(T) + h(T) < fmin makes L(T) final (strictly:
+// then every predecessor on a shortest path has been processed too); if even
+// min(L(T), fmin - h(T)) cannot make d0 + L + tpart fit the bound, T is unreachable for
+// every source of the task.  Integer arithmetic: no rounding margins needed.
+template <int CAP, bool PRED>
+__device__ inline bool target_resolved(const SearchLds<CAP, PRED>& L, int tslot, int64_t tpart, int64_t hT,
+                                       int64_t d0min, int64_t bound_mm, int64_t fmin, bool pend_empty) {
+  if (tslot < 0 || pend_empty) return true;
+  const uint32_t l32 = LabelT<PRED>::label(L.lab[tslot]);
+  const int64_t lab = l32 == kNoLabel ? INT64_MAX / 4 : (int64_t)l32;
+  if (lab + hT < fmin) return true;
+  const int64_t lb = lab < fmin - hT ? lab : fmin - hT;
+  return d0min + lb + tpart > bound_mm;
 }
 
-template <int CAP>
-__device__ inline void relax_one(SearchLds<CAP>& L, const Heur& H, uint32_t dw, uint32_t lw, int32_t vlat,
-                                 int32_t vlon, double du, double bound, uint32_t mode_bit,
+template <int CAP, bool PRED>
+__device__ inline void relax_one(SearchLds<CAP, PRED>& L, const Heur& H, uint32_t dw, uint32_t len_mm, int32_t vlat,
+                                 int32_t vlon, uint32_t du, uint32_t edge, int64_t bound_mm, uint32_t mode_bit,
                                  unsigned long long& relaxed) {
   if (!(((dw >> 28) & 7u) & mode_bit)) return;
   ++relaxed;
-  const double nd = du + (double)__uint_as_float(lw);
-  if (nd > bound) return;
+  const int64_t nd = (int64_t)du + (int64_t)len_mm;
+  if (nd > bound_mm) return;
   bool isnew = false;
   const int sl = lds_insert(L, dw & kAdjDstMask, &isnew);
   if (sl < 0) return;
-  if (isnew) L.hv[sl] = (float)H(vlat, vlon);
-  const unsigned long long nb = (unsigned long long)__double_as_longlong(nd);
-  const unsigned long long old = atomicMin(&L.dist[sl], nb);
-  if (nb < old) {
+  if (isnew) L.hv[sl] = H(vlat, vlon);
+  const typename LabelT<PRED>::T nb = LabelT<PRED>::make((uint32_t)nd, edge);
+  const typename LabelT<PRED>::T old = atomicMin(&L.lab[sl], nb);
+  if (LabelT<PRED>::label(nb) < LabelT<PRED>::label(old)) {
     const uint32_t ok = atomicOr(&L.key[sl], kInq);
     if (!(ok & kInq)) {
       const int p = atomicAdd(&L.n_pend, 1);
@@ -478,43 +497,58 @@ __device__ inline void relax_one(SearchLds<CAP>& L, const Heur& H, uint32_t dw, 
   }
 }
 
-// Search rooted at `start` (label 0), processed in rounds of f = label + h below
-// (minimum pending f + delta).  Lanes j < n_tgt hold target node tnode, its
-// heuristic hT and the target partial length tpart.  false = LDS-table overflow.
-template <int CAP>
-__device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, const Heur& H, uint32_t mode_bit, uint32_t start,
-                           double bound, double delta, uint32_t tnode, double tpart, double hT, double d0min,
-                           int n_tgt, unsigned long long* settled, unsigned long long* relaxed,
-                           unsigned long long* rounds) {
+// Search rooted at `start` (label 0).  Lanes j < n_tgt hold target node tnode, its
+// heuristic hT and the target partial length tpart (mm).  false = LDS-table overflow.
+template <int CAP, bool PRED>
+__device__ bool search_run(SearchLds<CAP, PRED>& L, const DevGraph& g, const Heur& H, uint32_t mode_bit,
+                           uint32_t start, int64_t bound_mm, int64_t delta_mm, uint32_t tnode, int64_t tpart,
+                           int64_t hT, int64_t d0min, int n_tgt, unsigned long long* settled,
+                           unsigned long long* relaxed, unsigned long long* rounds,
+                           unsigned long long* stamps = nullptr) {
   const int lane = threadIdx.x;
   if (lane == 0) {
     bool isnew;
     const int sl = lds_insert(L, start, &isnew);
     const int2 sll = g.node_ll[start];
-    L.hv[sl] = (float)H(sll.x, sll.y);
-    L.dist[sl] = 0ull;  // +0.0
+    L.hv[sl] = H(sll.x, sll.y);
+    L.lab[sl] = LabelT<PRED>::make(0u, kEmpty);
     L.key[sl] |= kInq;
     L.pend[0] = (uint16_t)sl;
     L.n_pend = 1;
   }
   __syncthreads();
+  // targets are pre-inserted (no label) so every round reads their label from a known slot
+  int tslot = -1;
+  if (lane < n_tgt && tnode != kEmpty) {
+    bool isnew;
+    tslot = lds_insert(L, tnode, &isnew);
+    if (tslot >= 0 && isnew) L.hv[tslot] = (uint32_t)hT;
+  }
+  __syncthreads();
   unsigned long long my_settled = 0, my_relaxed = 0, my_rounds = 0;
+  unsigned long long cyc[4] = {0, 0, 0, 0};
   for (;;) {
+    OTR_STAMP(t0);
     const int np = L.n_pend;
-    double fmin = __builtin_huge_val();
+    int64_t fmin = INT64_MAX;
     for (int k = lane; k < np; k += OTR_WAVE) {
       const int sl = L.pend[k];
-      const double f = bits_d(L.dist[sl]) + (double)L.hv[sl];
+      const int64_t f = (int64_t)LabelT<PRED>::label(L.lab[sl]) + (int64_t)L.hv[sl];
       fmin = f < fmin ? f : fmin;
     }
     for (int off = 32; off > 0; off >>= 1) {
-      const double o = __shfl_xor(fmin, off);
+      const int64_t o = __shfl_xor(fmin, off);
       fmin = o < fmin ? o : fmin;
     }
-    const bool res = lane >= n_tgt || target_resolved(L, tnode, tpart, hT, d0min, bound, fmin, np == 0);
-    if (__ballot(!res) == 0ull || np == 0) break;
+    OTR_STAMP(t1);
+    const bool res = lane >= n_tgt || target_resolved(L, tslot, tpart, hT, d0min, bound_mm, fmin, np == 0);
+    const bool done = __ballot(!res) == 0ull || np == 0;
+    OTR_STAMP(t2);
+    cyc[0] += t1 - t0;
+    cyc[1] += t2 - t1;
+    if (done) break;
     ++my_rounds;
-    const double theta = fmin + delta;
+    const int64_t theta = fmin + delta_mm;
     int kept = 0, nw = 0;
     for (int base = 0; base < np; base += OTR_WAVE) {
       const int k = base + lane;
@@ -522,7 +556,7 @@ __device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, const Heur& H, 
       bool take = false;
       if (k < np) {
         sl = L.pend[k];
-        take = bits_d(L.dist[sl]) + (double)L.hv[sl] < theta;
+        take = (int64_t)LabelT<PRED>::label(L.lab[sl]) + (int64_t)L.hv[sl] < theta;
       }
       const unsigned long long mt = __ballot(take), mk = __ballot(k < np && !take);
       __syncthreads();
@@ -538,29 +572,39 @@ __device__ bool search_run(SearchLds<CAP>& L, const DevGraph& g, const Heur& H, 
     }
     if (lane == 0) L.n_pend = kept;
     __syncthreads();
-    // relax: lane = (work node, adjacency slot), so a round's dependent chain is a
-    // single relaxation; slot 3 of a node with more than 4 out-edges also walks the CSR tail
+    OTR_STAMP(t3);
+    cyc[2] += t3 - t2;
+    // relax: lane = (work node, adjacency slot), so a round's dependent chain is a single
+    // relaxation; slot 3 of a node with more than 4 out-edges also walks the CSR tail
     for (int base = 0; base < 4 * nw; base += OTR_WAVE) {
       const int k = base + lane;
       if (k < 4 * nw) {
         const int ws = L.work[k >> 2];
         const int slot = k & 3;
         const uint32_t u = L.key[ws] & ~kInq;
-        const double du = bits_d(L.dist[ws]);
+        const uint32_t du = LabelT<PRED>::label(L.lab[ws]);
         if (slot == 0) ++my_settled;
         const uint4 r = g.adj[4 * (size_t)u + slot];
-        relax_one(L, H, r.x & ~kAdjMore, r.y, (int32_t)r.z, (int32_t)r.w, du, bound, mode_bit, my_relaxed);
+        const uint32_t e0 = PRED ? g.node_row[u] : 0u;  // edge id = CSR row start + slot
+        relax_one(L, H, r.x & ~kAdjMore, r.y, (int32_t)r.z, (int32_t)r.w, du, e0 + slot, bound_mm, mode_bit,
+                  my_relaxed);
         if (slot == 3 && (r.x & kAdjMore))
           for (uint32_t e = g.node_row[u] + 4; e < g.node_row[u + 1]; ++e) {
             const uint4 pk = g.edge_pack[e];
             const int2 vll = g.node_ll[pk.x];
-            relax_one(L, H, pk.x | ((pk.z & 7u) << 28), pk.y, vll.x, vll.y, du, bound, mode_bit, my_relaxed);
+            relax_one(L, H, pk.x | ((pk.z & 7u) << 28), pk.y, vll.x, vll.y, du, e, bound_mm, mode_bit, my_relaxed);
           }
       }
     }
     __syncthreads();
+    OTR_STAMP(t4);
+    cyc[3] += t4 - t3;
     if (L.overflow) break;
   }
+#ifdef OTR_STAMPS
+  if (stamps && lane == 0)
+    for (int q = 0; q < 4; ++q) atomicAdd(&stamps[q * kShards + (blockIdx.x & (kShards - 1))], cyc[q]);
+#endif
   if (settled) *settled += my_settled;
   if (relaxed) *relaxed += my_relaxed;
   if (rounds) *rounds += my_rounds;
@@ -599,7 +643,7 @@ struct RouteArgs {
 
 template <int CAP>
 __global__ __launch_bounds__(64) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
-  __shared__ SearchLds<CAP> L;
+  __shared__ SearchLds<CAP, false> L;
   const int lane = threadIdx.x;
   const int64_t w = a.task_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (a.n_tasks + 7) / 8);
   if (w >= a.n_tasks) return;
@@ -611,23 +655,25 @@ __global__ __launch_bounds__(64) void k_route(DevGraph gr, RouteArgs a, unsigned
   const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
   const uint32_t mode_bit = 1u << mode;
   const double bound = a.bound[s], gcd = a.g[s];
+  const int64_t bmm = bound_mm_of(bound);
   const uint32_t root = gr.edge_dst[a.cand_edge[sp * OTR_KMAX + (__ffsll((long long)mask) - 1)]];
   double* trow = a.trans + a.trans_off[s];
   // targets: lane j
   uint32_t ej = 0, tnode = kEmpty;
-  double pj = 0, tpart = 0;
+  double pj = 0;
+  int64_t tpart = 0;
   bool needed = false;
-  double d0min = __builtin_huge_val();
+  int64_t d0min = INT64_MAX / 4;
   if (lane < Kb) {
     ej = a.cand_edge[s * OTR_KMAX + lane];
     pj = a.cand_p[s * OTR_KMAX + lane];
-    tpart = pj * (double)gr.edge_len[ej];
+    tpart = part_mm(pj, gr.len_mm[ej]);
   }
   for (unsigned long long m = mask; m; m &= m - 1) {
     const int i = __ffsll((long long)m) - 1;
     const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
     const double pi = a.cand_p[sp * OTR_KMAX + i];
-    const double d0 = (1.0 - pi) * (double)gr.edge_len[ei];
+    const int64_t d0 = part_mm(1.0 - pi, gr.len_mm[ei]);
     d0min = d0 < d0min ? d0 : d0min;
     if (lane < Kb && !(ej == ei && pj >= pi)) needed = true;
   }
@@ -642,30 +688,30 @@ __global__ __launch_bounds__(64) void k_route(DevGraph gr, RouteArgs a, unsigned
   const bool need = __ballot(needed) != 0ull;
   const int64_t pb = a.state_probe[s];
   const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], bound);
-  double hT = 0.0;
+  int64_t hT = 0;
   if (needed) {
     const int2 tll = gr.node_ll[tnode];
     hT = H(tll.x, tll.y);
   }
-  search_init<CAP>(L);
+  search_init(L);
   if (need)
-    ok = search_run<CAP>(L, gr, H, mode_bit, root, bound, a.delta, tnode, tpart, hT, d0min, Kb, &settled, &relaxed,
-                         &rounds);
-  double lab = __builtin_huge_val();
+    ok = search_run(L, gr, H, mode_bit, root, bmm, (int64_t)(a.delta * 1000.0), tnode, tpart, hT, d0min, Kb,
+                    &settled, &relaxed, &rounds, counters ? counters + 16 * kShards : nullptr);
+  int64_t lab = -1;
   if (ok && needed) {
     const int sl = lds_find(L, tnode);
-    if (sl >= 0) lab = bits_d(L.dist[sl]);
+    if (sl >= 0 && L.lab[sl] != kNoLabel) lab = (int64_t)L.lab[sl];
   }
   for (unsigned long long m = mask; m; m &= m - 1) {
     const int i = __ffsll((long long)m) - 1;
     const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
     const double pi = a.cand_p[sp * OTR_KMAX + i];
-    const double leni = (double)gr.edge_len[ei];
     if (lane < Kb) {
-      double r = __builtin_huge_val();
-      if (ej == ei && pj >= pi) r = (pj - pi) * leni;
-      else if (lab != __builtin_huge_val()) r = ((1.0 - pi) * leni + lab) + tpart;
-      trow[(int64_t)i * Kb + lane] = (ok && r <= bound) ? fabs(r - gcd) * a.inv_beta[mode] : __builtin_huge_val();
+      int64_t r = -1;
+      if (ej == ei && pj >= pi) r = part_mm(pj - pi, gr.len_mm[ei]);
+      else if (lab >= 0) r = part_mm(1.0 - pi, gr.len_mm[ei]) + lab + tpart;
+      trow[(int64_t)i * Kb + lane] =
+          (ok && r >= 0 && r <= bmm) ? fabs((double)r / 1000.0 - gcd) * a.inv_beta[mode] : __builtin_huge_val();
     }
   }
   if (!ok && lane == 0) a.overflow_flag[task] = 1;
@@ -673,14 +719,15 @@ __global__ __launch_bounds__(64) void k_route(DevGraph gr, RouteArgs a, unsigned
     for (int off = 32; off > 0; off >>= 1) {
       settled += __shfl_xor(settled, off);
       relaxed += __shfl_xor(relaxed, off);
+      rounds = rounds;  // rounds is wave-uniform
     }
     if (lane == 0) {
       const int sh = blockIdx.x & (kShards - 1);
       atomicAdd(&counters[3 * kShards + sh], settled);
       atomicAdd(&counters[4 * kShards + sh], relaxed);
       atomicAdd(&counters[11 * kShards + sh], (unsigned long long)Kb);
-      atomicAdd(&counters[13 * kShards + sh], rounds);
       atomicAdd(&counters[12 * kShards + sh], (unsigned long long)__popcll(mask));
+      atomicAdd(&counters[13 * kShards + sh], rounds);
     }
   }
 }
@@ -814,9 +861,9 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
 
 // ------------------------------------------------------------------------------
 // K6: winner path reconstruction, one wave per step (state s with prev >= 0,
-// not a sub-path start).  Single-target search from the root dst(e_i), then a
-// predecessor walk: among the in-edges (u→v) with label(u) + len == label(v) take
-// the smallest edge id.
+// not a sub-path start).  Single-target search from the root dst(e_i) whose label
+// words carry the smallest-id predecessor edge; the walk from T back to the root
+// follows them (one edge_src load per path edge).
 // ------------------------------------------------------------------------------
 struct PathArgs {
   const int64_t* steps;        // state ids to reconstruct
@@ -843,65 +890,9 @@ struct PathArgs {
   int32_t* cap_flag;           // global: path buffer too small
 };
 
-// Predecessor walk from T back to the root S in ONE pass: lanes 0-3 read the four
-// in-edge slots of the node's reverse record (one 64-B line), keep (u→v) with
-// label(u) + len == label(v), and the smallest edge id wins.  Edges land in LDS
-// (reusing the pend/work arrays as CAP u32 slots), reversed into root→T order.
-template <int CAP>
-__device__ int walk_preds(SearchLds<CAP>& L, const DevGraph& g, uint32_t mode_bit, uint32_t S, uint32_t T) {
-  const int lane = threadIdx.x;
-  uint32_t* path = reinterpret_cast<uint32_t*>(L.pend);  // pend+work are contiguous: CAP u32
-  uint32_t v = T;
-  int n = 0;
-  while (v != S) {
-    if (n >= CAP) return -1;
-    const int sv = lds_find(L, v);
-    if (sv < 0) return -1;
-    const double dv = bits_d(L.dist[sv]);
-    uint32_t best = kEmpty, best_src = kEmpty;
-    if (lane < 4) {
-      const uint4 r = g.radj[4 * (size_t)v + lane];
-      if (((r.x >> 28) & 7u) & mode_bit) {
-        const uint32_t u = r.x & kAdjDstMask;
-        const int su = lds_find(L, u);
-        if (su >= 0 && bits_d(L.dist[su]) + (double)__uint_as_float(r.y) == dv) {
-          best = r.z;
-          best_src = u;
-        }
-      }
-      if (lane == 3 && (r.x & kAdjMore))  // in-degree > 4: CSR tail
-        for (uint32_t q = g.rev_row[v] + 4; q < g.rev_row[v + 1]; ++q) {
-          const uint32_t ed = g.rev_edge[q];
-          if (!(g.edge_attr[ed] & mode_bit)) continue;
-          const uint32_t u = g.edge_src[ed];
-          const int su = lds_find(L, u);
-          if (su >= 0 && bits_d(L.dist[su]) + (double)g.edge_len[ed] == dv && ed < best) {
-            best = ed;
-            best_src = u;
-          }
-        }
-    }
-    for (int off = 1; off < 4; off <<= 1) {
-      const uint32_t ob = __shfl_xor(best, off), os = __shfl_xor(best_src, off);
-      if (ob < best) {
-        best = ob;
-        best_src = os;
-      }
-    }
-    best = __shfl(best, 0);
-    best_src = __shfl(best_src, 0);
-    if (best == kEmpty) return -1;
-    if (lane == 0) path[n] = best;
-    ++n;
-    v = best_src;
-  }
-  __syncthreads();
-  return n;
-}
-
 template <int CAP>
 __global__ __launch_bounds__(64) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, int64_t n_list) {
-  __shared__ SearchLds<CAP> L;
+  __shared__ SearchLds<CAP, true> L;
   const int lane = threadIdx.x;
   const int64_t w = step_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_list + 7) / 8);
   if (w >= n_list) return;
@@ -917,19 +908,37 @@ __global__ __launch_bounds__(64) void k_paths(DevGraph gr, PathArgs a, const int
   }
   const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
   const uint32_t mode_bit = 1u << mode;
-  const double d0 = (1.0 - pi) * (double)gr.edge_len[ei];
+  const int64_t d0 = part_mm(1.0 - pi, gr.len_mm[ei]);
   const uint32_t S = gr.edge_dst[ei], T = gr.edge_src[ej];
   const int64_t pb = a.state_probe[s];
   const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], a.bound[s]);
   const int2 tll = gr.node_ll[T];
-  search_init<CAP>(L);
-  const bool ok = search_run<CAP>(L, gr, H, mode_bit, S, a.bound[s], a.delta, lane == 0 ? T : kEmpty,
-                                  pj * (double)gr.edge_len[ej], H(tll.x, tll.y), d0, 1, nullptr, nullptr, nullptr);
+  search_init(L);
+  const bool ok = search_run(L, gr, H, mode_bit, S, bound_mm_of(a.bound[s]), (int64_t)(a.delta * 1000.0),
+                             lane == 0 ? T : kEmpty, part_mm(pj, gr.len_mm[ej]), (int64_t)H(tll.x, tll.y), d0, 1,
+                             nullptr, nullptr, nullptr);
   if (!ok) {
     if (lane == 0) a.overflow_flag[k] = 1;
     return;
   }
-  const int n = walk_preds<CAP>(L, gr, mode_bit, S, T);
+  // walk predecessor edges T → S (lane 0), staging the edges in LDS
+  uint32_t* lp = reinterpret_cast<uint32_t*>(L.pend);  // pend+work are contiguous: CAP u32
+  int n = 0;
+  if (lane == 0) {
+    uint32_t v = T;
+    while (v != S) {
+      const int sv = lds_find(L, v);
+      const uint32_t e = sv >= 0 ? (uint32_t)(L.lab[sv] & 0xFFFFFFFFull) : kEmpty;
+      if (e == kEmpty || n >= CAP) {
+        n = -1;
+        break;
+      }
+      lp[n++] = e;
+      v = gr.edge_src[e];
+    }
+  }
+  n = __shfl(n, 0);
+  __syncthreads();
   if (n < 0) {
     if (lane == 0) a.overflow_flag[k] = 2;
     return;
@@ -946,7 +955,6 @@ __global__ __launch_bounds__(64) void k_paths(DevGraph gr, PathArgs a, const int
     return;
   }
   off += (int64_t)shard * region;
-  const uint32_t* lp = reinterpret_cast<const uint32_t*>(L.pend);
   for (int q = lane; q < n; q += OTR_WAVE) a.path[off + q] = lp[n - 1 - q];
   if (lane == 0) {
     a.path_off[s] = off;
@@ -971,7 +979,7 @@ struct SegArgs {
   const int64_t* path_off;
   const int32_t* path_len;
   const uint32_t* path;
-  double* pos;                 // scratch per state
+  int64_t* pos;                // scratch per state: route position, mm
   int64_t* act;                // scratch per state: compact active state list
   const int64_t* cap_off;      // per trace capacity offset (route/segments/ways/reports)
   uint32_t* route;  int64_t* route_n;
@@ -999,7 +1007,7 @@ __global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) 
   int64_t* act = a.act + so;
   for (int64_t s = so; s < eo; ++s)
     if (a.cand_count[s] > 0) act[na++] = s;
-  double* pos = a.pos + so;  // indexed by active ordinal
+  int64_t* pos = a.pos + so;  // route position (mm), indexed by active ordinal
   // time stamps of active states are read from the batch (double(time))
   bool first_sub = true;
   int k = 0;
@@ -1015,35 +1023,35 @@ __global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) 
     }
     if (nr) route[nr++] = 0xFFFFFFFFu;
     // pass 1: positions of the sub-path's states
-    pos[sa] = 0.0;
+    pos[sa] = 0;
     for (int q = sa + 1; q <= sb; ++q) {
       const int64_t si = act[q - 1], sj = act[q];
       const uint32_t ei = a.cand_edge[si * OTR_KMAX + a.winner[si]], ej = a.cand_edge[sj * OTR_KMAX + a.winner[sj]];
       const double pi = a.cand_p[si * OTR_KMAX + a.winner[si]], pj = a.cand_p[sj * OTR_KMAX + a.winner[sj]];
       if (ej == ei && pj >= pi) {
-        pos[q] = pos[q - 1] + (pj - pi) * (double)g.edge_len[ei];
+        pos[q] = pos[q - 1] + part_mm(pj - pi, g.len_mm[ei]);
         continue;
       }
-      double s = pos[q - 1] + (1.0 - pi) * (double)g.edge_len[ei];
+      int64_t s = pos[q - 1] + part_mm(1.0 - pi, g.len_mm[ei]);
       const int32_t pl = a.path_len[sj];
-      for (int z = 0; z < pl; ++z) s = s + (double)g.edge_len[a.path[a.path_off[sj] + z]];
-      pos[q] = s + pj * (double)g.edge_len[ej];
+      for (int z = 0; z < pl; ++z) s = s + (int64_t)g.len_mm[a.path[a.path_off[sj] + z]];
+      pos[q] = s + part_mm(pj, g.len_mm[ej]);
     }
     // pass 2: portions → groups, streaming.  time_at() of the oracle with a
     // forward-moving pointer (queries are non-decreasing route positions).
     const int nst = sb - sa + 1;
     struct {
-      const double* pos;
+      const int64_t* pos;
       const int64_t* act;
       const int64_t* probe;
       const int64_t* time;
       int base, n, k;
       __device__ double tm(int q) const { return (double)time[probe[act[base + q]]]; }
-      __device__ double at(double s) {
+      __device__ double at(int64_t s) {
         while (k < n - 2 && s > pos[base + k + 1]) ++k;
-        const double p0 = pos[base + k], p1 = pos[base + k + 1];
+        const int64_t p0 = pos[base + k], p1 = pos[base + k + 1];
         const double t0 = tm(k), t1 = tm(k + 1);
-        if (p1 > p0) return t0 + (t1 - t0) * ((s - p0) / (p1 - p0));
+        if (p1 > p0) return t0 + (t1 - t0) * ((double)(s - p0) / (double)(p1 - p0));
         return t0;
       }
     } tc = {pos, act, a.state_probe, a.b.time, sa, nst, 0};
@@ -1052,7 +1060,7 @@ __global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) 
     const int64_t lo = first_sub ? 0 : a.state_probe[act[sa]] - lo_probe;
     const int64_t hi = (k < na) ? a.state_probe[act[k]] - lo_probe - 1 : n_probe - 1;
     first_sub = false;
-    auto shape_at = [&](double s) -> int32_t {
+    auto shape_at = [&](int64_t s) -> int32_t {
       while (sh_q + 1 < nst && pos[sa + sh_q + 1] <= s) ++sh_q;
       int64_t r = (sh_q + 1 < nst) ? a.state_probe[act[sa + sh_q + 1]] - lo_probe - 1 : hi;
       return (int32_t)(r < lo ? lo : r);
@@ -1061,7 +1069,7 @@ __global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) 
     bool have = false;
     uint32_t gkey = 0, gfirst_e = 0, glast_e = 0, glast_way = 0;
     bool ginternal = false, gfirst_is_route_first = false;
-    double gs0 = 0, gs1 = 0;
+    int64_t gs0 = 0, gs1 = 0;
     int64_t gway_start = 0;
     bool any_portion = false;
     auto finalize = [&](bool is_last_portion) {
@@ -1088,7 +1096,7 @@ __global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) 
       a.seg_way_n[co + nseg] = nway - gway_start;
       ++nseg;
     };
-    auto portion = [&](uint32_t e, double s0, double s1) {
+    auto portion = [&](uint32_t e, int64_t s0, int64_t s1) {
       bool cont = false;
       if (have) {
         if (gkey != OTR_NO_SEGMENT) {
@@ -1122,7 +1130,7 @@ __global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) 
     {
       const int64_t s0i = act[sa];
       uint32_t cur_e = a.cand_edge[s0i * OTR_KMAX + a.winner[s0i]];
-      double cur_s0 = 0.0;
+      int64_t cur_s0 = 0;
       route[nr++] = cur_e;
       for (int q = sa + 1; q <= sb; ++q) {
         const int64_t si = act[q - 1], sj = act[q];
@@ -1130,13 +1138,13 @@ __global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) 
         const uint32_t ej = a.cand_edge[sj * OTR_KMAX + a.winner[sj]];
         const double pi = a.cand_p[si * OTR_KMAX + a.winner[si]], pj = a.cand_p[sj * OTR_KMAX + a.winner[sj]];
         if (ej == ei && pj >= pi) continue;
-        const double end_s = pos[q - 1] + (1.0 - pi) * (double)g.edge_len[ei];
+        const int64_t end_s = pos[q - 1] + part_mm(1.0 - pi, g.len_mm[ei]);
         portion(cur_e, cur_s0, end_s);
-        double s = end_s;
+        int64_t s = end_s;
         const int32_t pl = a.path_len[sj];
         for (int z = 0; z < pl; ++z) {
           const uint32_t ed = a.path[a.path_off[sj] + z];
-          const double s1 = s + (double)g.edge_len[ed];
+          const int64_t s1 = s + (int64_t)g.len_mm[ed];
           portion(ed, s, s1);
           route[nr++] = ed;
           s = s1;
