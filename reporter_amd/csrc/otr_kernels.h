@@ -642,7 +642,7 @@ struct RouteArgs {
 };
 
 template <int CAP>
-__global__ __launch_bounds__(64) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
   __shared__ SearchLds<CAP, false> L;
   const int lane = threadIdx.x;
   const int64_t w = a.task_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (a.n_tasks + 7) / 8);
@@ -891,7 +891,7 @@ struct PathArgs {
 };
 
 template <int CAP>
-__global__ __launch_bounds__(64) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, int64_t n_list) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, int64_t n_list) {
   __shared__ SearchLds<CAP, true> L;
   const int lane = threadIdx.x;
   const int64_t w = step_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_list + 7) / 8);
