@@ -183,7 +183,7 @@ enum Slot {
   S_TASK_STATE, S_TASK_MASK, S_TASK_OVF, S_TRANS,
   S_BP, S_BRK, S_END_WIN, S_WINNER, S_SUBPATH,
   S_PATH_OFF, S_PATH_LEN, S_PATH, S_STEP_OVF,
-  S_CAP, S_CAP_OFF, S_POS, S_ACT,
+  S_CAP, S_CAP_OFF, S_POS, S_ACT, S_ENT, S_SUBA, S_SUBB, S_POR_E, S_POR_S0, S_POR_S1, S_POR_SA, S_GSTART,
   S_ROUTE, S_ROUTE_N, S_SEG_ID, S_SEG_START, S_SEG_END, S_SEG_LEN, S_SEG_QUEUE, S_SEG_INTERNAL,
   S_SEG_BSHAPE, S_SEG_ESHAPE, S_SEG_INDEX, S_SEG_N, S_SEG_WAY_N, S_SEG_WAY, S_WAY_N,
   S_REP_ID, S_REP_NEXT, S_REP_T0, S_REP_T1, S_REP_LEN, S_REP_QUEUE, S_REP_SEG, S_REP_N,
@@ -577,6 +577,14 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   sa.path = (const uint32_t*)need<uint32_t>(S_PATH, 1);
   sa.pos = need<int64_t>(S_POS, S);
   sa.act = need<int64_t>(S_ACT, S);
+  sa.ent = need<int64_t>(S_ENT, S);
+  sa.suba = need<int32_t>(S_SUBA, S);
+  sa.subb = need<int32_t>(S_SUBB, S);
+  sa.por_e = need<uint32_t>(S_POR_E, C);
+  sa.por_s0 = need<int64_t>(S_POR_S0, C);
+  sa.por_s1 = need<int64_t>(S_POR_S1, C);
+  sa.por_sa = need<int32_t>(S_POR_SA, C);
+  sa.gstart = need<int32_t>(S_GSTART, C);
   sa.cap_off = cap_off;
   sa.route = need<uint32_t>(S_ROUTE, C);
   sa.route_n = need<int64_t>(S_ROUTE_N, T);
@@ -608,7 +616,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   sa.report_levels = in->report_levels;
   sa.transition_levels = in->transition_levels;
   tb(OTR_STAGE_SEGMENTS);
-  k_segments<<<grid_for(T, 64), 64, 0, stream>>>(g, sa, d_counters);
+  k_segments<<<(unsigned)(8 * ((T + 7) / 8)), 64, 0, stream>>>(g, sa, d_counters);
   te(OTR_STAGE_SEGMENTS);
   // ---- K8: hour buckets → histogram
   HistArgs ha{};

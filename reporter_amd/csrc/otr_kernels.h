@@ -963,8 +963,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
 }
 
 // ------------------------------------------------------------------------------
-// K7: route stitching, OSMLR traffic segments and report(), one thread per trace.
-// Output slots are at capacity offsets (cap_off), counts in *_n.
+// K7: route stitching, OSMLR traffic segments and report(), one wave per trace.
+//
+// Route positions are integer millimetres, so the oracle's sequential stitching is an
+// exact segmented prefix sum: the wave scans states 64 at a time (positions, the entry
+// position of the current edge, sub-path starts), emits edge portions and route edges
+// at scanned offsets, finds segment groups by comparing each portion with its
+// predecessor, fills every segment lane-parallel (binary searches for times and shape
+// indices), and runs the short report() state machine on lane 0.  Outputs sit at the
+// trace's capacity offset cap_off[t]; counts in *_n.
 // ------------------------------------------------------------------------------
 struct SegArgs {
   BatchDev b;
@@ -979,9 +986,16 @@ struct SegArgs {
   const int64_t* path_off;
   const int32_t* path_len;
   const uint32_t* path;
-  int64_t* pos;                // scratch per state: route position, mm
-  int64_t* act;                // scratch per state: compact active state list
+  // scratch per state (indexed by active ordinal from trace_state_off[t])
+  int64_t* pos;                // route position of the state, mm
+  int64_t* ent;                // position where the state's current edge was entered, mm
+  int64_t* act;                // compact active state list
+  int32_t* suba;               // first active ordinal of the state's sub-path
+  int32_t* subb;               // at a sub-path's first ordinal: its last ordinal
+  // scratch at capacity offsets
+  uint32_t* por_e;  int64_t* por_s0;  int64_t* por_s1;  int32_t* por_sa;  int32_t* gstart;
   const int64_t* cap_off;      // per trace capacity offset (route/segments/ways/reports)
+  int64_t n_traces_pad;
   uint32_t* route;  int64_t* route_n;
   unsigned long long* seg_id;  double* seg_start;  double* seg_end;  int32_t* seg_length;
   int32_t* seg_queue;  uint8_t* seg_internal;  int32_t* seg_bshape;  int32_t* seg_eshape;
@@ -994,186 +1008,302 @@ struct SegArgs {
   uint32_t report_levels, transition_levels;
 };
 
-__global__ void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+template <class T>
+__device__ inline T wave_excl_sum(T v, T* total) {
+  const int lane = threadIdx.x;
+  T x = v;
+  for (int off = 1; off < OTR_WAVE; off <<= 1) {
+    const T u = __shfl_up(x, off);
+    if (lane >= off) x += u;
+  }
+  *total = __shfl(x, OTR_WAVE - 1);
+  return x - v;
+}
+
+// does portion edge e continue the segment group whose last edge is ep?
+__device__ inline bool group_continues(const DevGraph& g, uint32_t ep, uint32_t e) {
+  const uint32_t key = g.edge_seg[ep];
+  if (key != OTR_NO_SEGMENT)
+    return g.edge_seg[e] == key && !(g.edge_attr[ep] & OTR_ATTR_SEG_END) && !(g.edge_attr[e] & OTR_ATTR_SEG_BEGIN);
+  return g.edge_seg[e] == OTR_NO_SEGMENT &&
+         ((g.edge_attr[e] & OTR_ATTR_INTERNAL) != 0) == ((g.edge_attr[ep] & OTR_ATTR_INTERNAL) != 0);
+}
+
+__global__ __launch_bounds__(64) void k_segments(DevGraph g, SegArgs a, unsigned long long* counters) {
+  const int lane = threadIdx.x;
+  const int64_t t = xcd_remap(blockIdx.x, (a.b.n_traces + 7) / 8);
   if (t >= a.b.n_traces) return;
   const int64_t so = a.trace_state_off[t], eo = a.trace_state_off[t + 1];
   const int64_t lo_probe = a.b.trace_off[t], n_probe = a.b.trace_off[t + 1] - lo_probe;
   const int64_t co = a.cap_off[t];
-  uint32_t* route = a.route + co;
-  int64_t nr = 0, nseg = 0, nway = 0;
-  // compact active states
-  int na = 0;
   int64_t* act = a.act + so;
-  for (int64_t s = so; s < eo; ++s)
-    if (a.cand_count[s] > 0) act[na++] = s;
-  int64_t* pos = a.pos + so;  // route position (mm), indexed by active ordinal
-  // time stamps of active states are read from the batch (double(time))
-  bool first_sub = true;
-  int k = 0;
-  while (k < na) {
-    const int sa = k;
-    int e_ = k + 1;
-    while (e_ < na && !a.brk[act[e_]]) ++e_;
-    const int sb = e_ - 1;
-    k = e_;
-    if (sb == sa) {
-      first_sub = false;
-      continue;
-    }
-    if (nr) route[nr++] = 0xFFFFFFFFu;
-    // pass 1: positions of the sub-path's states
-    pos[sa] = 0;
-    for (int q = sa + 1; q <= sb; ++q) {
-      const int64_t si = act[q - 1], sj = act[q];
-      const uint32_t ei = a.cand_edge[si * OTR_KMAX + a.winner[si]], ej = a.cand_edge[sj * OTR_KMAX + a.winner[sj]];
-      const double pi = a.cand_p[si * OTR_KMAX + a.winner[si]], pj = a.cand_p[sj * OTR_KMAX + a.winner[sj]];
-      if (ej == ei && pj >= pi) {
-        pos[q] = pos[q - 1] + part_mm(pj - pi, g.len_mm[ei]);
-        continue;
+  int64_t* pos = a.pos + so;
+  int64_t* ent = a.ent + so;
+  int32_t* suba = a.suba + so;
+  int32_t* subb = a.subb + so;
+  // ---- A1: compact the active states
+  int na = 0;
+  for (int64_t base = so; base < eo; base += OTR_WAVE) {
+    const int64_t s = base + lane;
+    const bool on = s < eo && a.cand_count[s] > 0;
+    const unsigned long long m = __ballot(on);
+    if (on) act[na + prefix_count(m)] = s;
+    na += __popcll(m);
+  }
+  __syncthreads();
+  // ---- A2: positions, portions and route edges, 64 states at a time
+  int64_t c_pos = 0, c_ent = 0, n_por = 0, n_route = 0;
+  int c_sa = 0;
+  bool emitted_any = false;
+  for (int kb = 0; kb < na; kb += OTR_WAVE) {
+    const int k = kb + lane;
+    const bool valid = k < na;
+    int64_t s = 0;
+    bool brk_k = false, last_k = false, same = false, change = false;
+    uint32_t ek = 0, ep = 0;
+    double pk = 0, pp = 0;
+    int pl = 0;
+    int64_t inc = 0;
+    if (valid) {
+      s = act[k];
+      brk_k = a.brk[s] != 0;
+      last_k = (k == na - 1) || a.brk[act[k + 1]] != 0;
+      ek = a.cand_edge[s * OTR_KMAX + a.winner[s]];
+      pk = a.cand_p[s * OTR_KMAX + a.winner[s]];
+      if (!brk_k) {
+        const int64_t sp = act[k - 1];
+        ep = a.cand_edge[sp * OTR_KMAX + a.winner[sp]];
+        pp = a.cand_p[sp * OTR_KMAX + a.winner[sp]];
+        same = ek == ep && pk >= pp;
+        change = !same;
       }
-      int64_t s = pos[q - 1] + part_mm(1.0 - pi, g.len_mm[ei]);
-      const int32_t pl = a.path_len[sj];
-      for (int z = 0; z < pl; ++z) s = s + (int64_t)g.len_mm[a.path[a.path_off[sj] + z]];
-      pos[q] = s + part_mm(pj, g.len_mm[ej]);
+      if (same) inc = part_mm(pk - pp, g.len_mm[ep]);
+      if (change) {
+        pl = a.path_len[s];
+        inc = part_mm(1.0 - pp, g.len_mm[ep]);
+        for (int z = 0; z < pl; ++z) inc += (int64_t)g.len_mm[a.path[a.path_off[s] + z]];
+        inc += part_mm(pk, g.len_mm[ek]);
+      }
     }
-    // pass 2: portions → groups, streaming.  time_at() of the oracle with a
-    // forward-moving pointer (queries are non-decreasing route positions).
-    const int nst = sb - sa + 1;
-    struct {
-      const int64_t* pos;
-      const int64_t* act;
-      const int64_t* probe;
-      const int64_t* time;
-      int base, n, k;
-      __device__ double tm(int q) const { return (double)time[probe[act[base + q]]]; }
-      __device__ double at(int64_t s) {
-        while (k < n - 2 && s > pos[base + k + 1]) ++k;
-        const int64_t p0 = pos[base + k], p1 = pos[base + k + 1];
-        const double t0 = tm(k), t1 = tm(k + 1);
-        if (p1 > p0) return t0 + (t1 - t0) * ((double)(s - p0) / (double)(p1 - p0));
+    // segmented inclusive scan of the position increments (segments start at brk)
+    int64_t v = inc;
+    bool f = brk_k;
+    for (int off = 1; off < OTR_WAVE; off <<= 1) {
+      const int64_t vu = __shfl_up(v, off);
+      const bool fu = __shfl_up((int)f, off) != 0;
+      if (lane >= off) {
+        if (!f) v += vu;
+        f = f || fu;
+      }
+    }
+    if (!f) v += c_pos;
+    const int64_t pos_k = v;
+    // entry position of the current edge: defined at sub-path starts and edge changes
+    int64_t ev = brk_k ? 0 : (change ? pos_k - part_mm(pk, g.len_mm[ek]) : 0);
+    bool eh = brk_k || change;
+    int sv = brk_k ? k : 0;
+    bool sh = brk_k;
+    for (int off = 1; off < OTR_WAVE; off <<= 1) {
+      const int64_t vu = __shfl_up(ev, off);
+      const bool hu = __shfl_up((int)eh, off) != 0;
+      const int su = __shfl_up(sv, off);
+      const bool shu = __shfl_up((int)sh, off) != 0;
+      if (lane >= off) {
+        if (!eh) {
+          ev = vu;
+          eh = hu;
+        }
+        if (!sh) {
+          sv = su;
+          sh = shu;
+        }
+      }
+    }
+    if (!eh) ev = c_ent;
+    if (!sh) sv = c_sa;
+    int64_t ent_prev = __shfl_up(ev, 1), pos_prev = __shfl_up(pos_k, 1);
+    if (lane == 0) {
+      ent_prev = c_ent;
+      pos_prev = c_pos;
+    }
+    if (valid) {
+      pos[k] = pos_k;
+      ent[k] = ev;
+      suba[k] = sv;
+      if (last_k) subb[sv] = k;
+    }
+    // portion and route-edge counts, offsets by wave scans
+    const bool start_emit = valid && brk_k && !last_k;
+    const unsigned long long m_se = __ballot(start_emit);
+    const bool sep = start_emit && (emitted_any || prefix_count(m_se) > 0);
+    const int64_t cnt_por = (change ? 1 + pl : 0) + (valid && last_k && !brk_k ? 1 : 0);
+    const int64_t cnt_route = (sep ? 1 : 0) + (start_emit ? 1 : 0) + (change ? pl + 1 : 0);
+    int64_t tot_por, tot_route;
+    const int64_t por_off = n_por + wave_excl_sum(cnt_por, &tot_por);
+    const int64_t route_off = n_route + wave_excl_sum(cnt_route, &tot_route);
+    if (valid) {
+      int64_t r = co + route_off;
+      if (sep) a.route[r++] = 0xFFFFFFFFu;
+      if (start_emit) a.route[r++] = ek;
+      int64_t q = co + por_off;
+      if (change) {
+        const int64_t s1 = pos_prev + part_mm(1.0 - pp, g.len_mm[ep]);
+        a.por_e[q] = ep;
+        a.por_s0[q] = ent_prev;
+        a.por_s1[q] = s1;
+        a.por_sa[q] = sv;
+        ++q;
+        int64_t x = s1;
+        for (int z = 0; z < pl; ++z) {
+          const uint32_t ed = a.path[a.path_off[s] + z];
+          const int64_t x1 = x + (int64_t)g.len_mm[ed];
+          a.por_e[q] = ed;
+          a.por_s0[q] = x;
+          a.por_s1[q] = x1;
+          a.por_sa[q] = sv;
+          ++q;
+          x = x1;
+          a.route[r++] = ed;
+        }
+        a.route[r++] = ek;
+      }
+      if (last_k && !brk_k) {
+        a.por_e[q] = ek;
+        a.por_s0[q] = ev;
+        a.por_s1[q] = pos_k;
+        a.por_sa[q] = sv;
+      }
+    }
+    n_por += tot_por;
+    n_route += tot_route;
+    emitted_any = emitted_any || m_se != 0ull;
+    c_pos = __shfl(pos_k, OTR_WAVE - 1);
+    c_ent = __shfl(ev, OTR_WAVE - 1);
+    c_sa = __shfl(sv, OTR_WAVE - 1);
+  }
+  __syncthreads();
+  // ---- B1: segment-group starts
+  int ng = 0;
+  for (int64_t qb = 0; qb < n_por; qb += OTR_WAVE) {
+    const int64_t q = qb + lane;
+    bool st = false;
+    if (q < n_por) {
+      const uint32_t e = a.por_e[co + q];
+      st = q == 0 || a.por_sa[co + q - 1] != a.por_sa[co + q] || !group_continues(g, a.por_e[co + q - 1], e);
+    }
+    const unsigned long long m = __ballot(st);
+    if (st) a.gstart[co + ng + prefix_count(m)] = (int32_t)q;
+    ng += __popcll(m);
+  }
+  __syncthreads();
+  // ---- B2: one lane per segment group
+  int64_t n_way = 0;
+  for (int gb = 0; gb < ng; gb += OTR_WAVE) {
+    const int gi = gb + lane;
+    const bool valid = gi < ng;
+    int64_t cnt_w = 0;
+    int32_t first = 0, last = 0;
+    if (valid) {
+      first = a.gstart[co + gi];
+      last = (gi + 1 < ng) ? a.gstart[co + gi + 1] - 1 : (int32_t)n_por - 1;
+      uint32_t lw = 0;
+      for (int32_t z = first; z <= last; ++z) {
+        const uint32_t w = g.edge_way[a.por_e[co + z]];
+        if (z == first || w != lw) ++cnt_w;
+        lw = w;
+      }
+    }
+    int64_t tot_w;
+    const int64_t woff = n_way + wave_excl_sum(cnt_w, &tot_w);
+    if (valid) {
+      const int64_t o = co + gi;
+      const uint32_t e0 = a.por_e[co + first], eL = a.por_e[co + last];
+      const int64_t s0 = a.por_s0[co + first], s1 = a.por_s1[co + last];
+      const int32_t sa = a.por_sa[co + first];
+      const int32_t sb = subb[sa];
+      const bool route_first = first == 0 || a.por_sa[co + first - 1] != sa;
+      const bool is_last = last == (int32_t)n_por - 1 || a.por_sa[co + last + 1] != sa;
+      const uint32_t key = g.edge_seg[e0];
+      const bool internal = (g.edge_attr[e0] & OTR_ATTR_INTERNAL) != 0;
+      // time at route position x: linear between the states around it (oracle time_at)
+      auto time_at = [&](int64_t x) -> double {
+        int32_t lo_i = sa + 1, hi_i = sb + 1;  // first ordinal m in [sa+1, sb] with pos[m] >= x
+        while (lo_i < hi_i) {
+          const int32_t mid = (lo_i + hi_i) >> 1;
+          if (pos[mid] >= x) hi_i = mid;
+          else lo_i = mid + 1;
+        }
+        const int32_t kk = (lo_i > sb ? sb : lo_i) - 1;
+        const double t0 = (double)a.b.time[a.state_probe[act[kk]]];
+        const double t1 = (double)a.b.time[a.state_probe[act[kk + 1]]];
+        const int64_t p0 = pos[kk], p1 = pos[kk + 1];
+        if (p1 > p0) return t0 + (t1 - t0) * ((double)(x - p0) / (double)(p1 - p0));
         return t0;
-      }
-    } tc = {pos, act, a.state_probe, a.b.time, sa, nst, 0};
-    // shape-index cursor: last state q (relative) with pos <= s
-    int sh_q = 0;
-    const int64_t lo = first_sub ? 0 : a.state_probe[act[sa]] - lo_probe;
-    const int64_t hi = (k < na) ? a.state_probe[act[k]] - lo_probe - 1 : n_probe - 1;
-    first_sub = false;
-    auto shape_at = [&](int64_t s) -> int32_t {
-      while (sh_q + 1 < nst && pos[sa + sh_q + 1] <= s) ++sh_q;
-      int64_t r = (sh_q + 1 < nst) ? a.state_probe[act[sa + sh_q + 1]] - lo_probe - 1 : hi;
-      return (int32_t)(r < lo ? lo : r);
-    };
-    // group state
-    bool have = false;
-    uint32_t gkey = 0, gfirst_e = 0, glast_e = 0, glast_way = 0;
-    bool ginternal = false, gfirst_is_route_first = false;
-    int64_t gs0 = 0, gs1 = 0;
-    int64_t gway_start = 0;
-    bool any_portion = false;
-    auto finalize = [&](bool is_last_portion) {
+      };
+      const int64_t lo = sa == 0 ? 0 : a.state_probe[act[sa]] - lo_probe;
+      const int64_t hi = (sb + 1 < na) ? a.state_probe[act[sb + 1]] - lo_probe - 1 : n_probe - 1;
+      auto shape_at = [&](int64_t x) -> int32_t {
+        int32_t lo_i = sa, hi_i = sb + 1;  // last ordinal m in [sa, sb] with pos[m] <= x
+        while (lo_i < hi_i) {
+          const int32_t mid = (lo_i + hi_i) >> 1;
+          if (pos[mid] <= x) lo_i = mid + 1;
+          else hi_i = mid;
+        }
+        const int32_t m = lo_i - 1;
+        const int64_t r = (m < sb) ? a.state_probe[act[m + 1]] - lo_probe - 1 : hi;
+        return (int32_t)(r < lo ? lo : r);
+      };
       double st = -1.0, et = -1.0;
       int32_t length = -1;
-      if (gkey != OTR_NO_SEGMENT) {
-        if (!gfirst_is_route_first && (g.edge_attr[gfirst_e] & OTR_ATTR_SEG_BEGIN)) st = tc.at(gs0);
-        if (!is_last_portion && (g.edge_attr[glast_e] & OTR_ATTR_SEG_END)) et = tc.at(gs1);
-        if (st != -1.0 && et != -1.0) length = (int32_t)g.seg_len[gkey];
-        a.seg_id[co + nseg] = g.seg_id[gkey];
+      if (key != OTR_NO_SEGMENT) {
+        if (!route_first && (g.edge_attr[e0] & OTR_ATTR_SEG_BEGIN)) st = time_at(s0);
+        if (!is_last && (g.edge_attr[eL] & OTR_ATTR_SEG_END)) et = time_at(s1);
+        if (st != -1.0 && et != -1.0) length = (int32_t)g.seg_len[key];
+        a.seg_id[o] = g.seg_id[key];
       } else {
-        if (!gfirst_is_route_first) st = tc.at(gs0);
-        if (!is_last_portion) et = tc.at(gs1);
-        a.seg_id[co + nseg] = OTR_NO_ID_U64;
+        if (!route_first) st = time_at(s0);
+        if (!is_last) et = time_at(s1);
+        a.seg_id[o] = OTR_NO_ID_U64;
       }
-      a.seg_start[co + nseg] = st;
-      a.seg_end[co + nseg] = et;
-      a.seg_length[co + nseg] = length;
-      a.seg_queue[co + nseg] = 0;
-      a.seg_internal[co + nseg] = (gkey == OTR_NO_SEGMENT && ginternal) ? 1 : 0;
-      a.seg_index[co + nseg] = gkey;
-      a.seg_bshape[co + nseg] = shape_at(gs0);
-      a.seg_eshape[co + nseg] = shape_at(gs1);
-      a.seg_way_n[co + nseg] = nway - gway_start;
-      ++nseg;
-    };
-    auto portion = [&](uint32_t e, int64_t s0, int64_t s1) {
-      bool cont = false;
-      if (have) {
-        if (gkey != OTR_NO_SEGMENT) {
-          cont = g.edge_seg[e] == gkey && !(g.edge_attr[glast_e] & OTR_ATTR_SEG_END) &&
-                 !(g.edge_attr[e] & OTR_ATTR_SEG_BEGIN);
-        } else {
-          const bool ie = (g.edge_attr[e] & OTR_ATTR_INTERNAL) != 0;
-          cont = g.edge_seg[e] == OTR_NO_SEGMENT && ie == ginternal;
-        }
-        if (!cont) finalize(false);
+      a.seg_start[o] = st;
+      a.seg_end[o] = et;
+      a.seg_length[o] = length;
+      a.seg_queue[o] = 0;
+      a.seg_internal[o] = (key == OTR_NO_SEGMENT && internal) ? 1 : 0;
+      a.seg_index[o] = key;
+      a.seg_bshape[o] = shape_at(s0);
+      a.seg_eshape[o] = shape_at(s1);
+      a.seg_way_n[o] = cnt_w;
+      int64_t wq = co + woff;
+      uint32_t lw = 0;
+      for (int32_t z = first; z <= last; ++z) {
+        const uint32_t w = g.edge_way[a.por_e[co + z]];
+        if (z == first || w != lw) a.seg_way[wq++] = w;
+        lw = w;
       }
-      if (!cont) {
-        have = true;
-        gkey = g.edge_seg[e];
-        ginternal = (g.edge_attr[e] & OTR_ATTR_INTERNAL) != 0;
-        gfirst_e = e;
-        gfirst_is_route_first = !any_portion;
-        gs0 = s0;
-        gway_start = nway;
-      }
-      const uint32_t w = g.edge_way[e];
-      if (nway == gway_start || w != glast_way) {
-        a.seg_way[co + nway++] = w;
-        glast_way = w;
-      }
-      glast_e = e;
-      gs1 = s1;
-      any_portion = true;
-    };
-    // walk the sub-path again emitting portions
-    {
-      const int64_t s0i = act[sa];
-      uint32_t cur_e = a.cand_edge[s0i * OTR_KMAX + a.winner[s0i]];
-      int64_t cur_s0 = 0;
-      route[nr++] = cur_e;
-      for (int q = sa + 1; q <= sb; ++q) {
-        const int64_t si = act[q - 1], sj = act[q];
-        const uint32_t ei = a.cand_edge[si * OTR_KMAX + a.winner[si]];
-        const uint32_t ej = a.cand_edge[sj * OTR_KMAX + a.winner[sj]];
-        const double pi = a.cand_p[si * OTR_KMAX + a.winner[si]], pj = a.cand_p[sj * OTR_KMAX + a.winner[sj]];
-        if (ej == ei && pj >= pi) continue;
-        const int64_t end_s = pos[q - 1] + part_mm(1.0 - pi, g.len_mm[ei]);
-        portion(cur_e, cur_s0, end_s);
-        int64_t s = end_s;
-        const int32_t pl = a.path_len[sj];
-        for (int z = 0; z < pl; ++z) {
-          const uint32_t ed = a.path[a.path_off[sj] + z];
-          const int64_t s1 = s + (int64_t)g.len_mm[ed];
-          portion(ed, s, s1);
-          route[nr++] = ed;
-          s = s1;
-        }
-        cur_e = ej;
-        cur_s0 = s;
-        route[nr++] = cur_e;
-      }
-      portion(cur_e, cur_s0, pos[sb]);
-      finalize(true);
     }
+    n_way += tot_w;
   }
-  a.route_n[t] = nr;
-  a.seg_n[t] = nseg;
-  a.way_n[t] = nway;
-  // report() over this trace's segments (reporter_service.py:79-179)
-  ReportStats rs;
-  const int64_t end_t = n_probe > 0 ? a.b.time[lo_probe + n_probe - 1] : 0;
-  report_segments((int32_t)nseg, a.seg_id + co, a.seg_start + co, a.seg_end + co, a.seg_internal + co,
-                  a.seg_queue + co, nullptr, a.seg_length + co, a.seg_bshape + co, a.seg_index + co, end_t,
-                  a.threshold, a.report_levels, a.transition_levels, a.rep_id + co, a.rep_next + co,
-                  a.rep_t0 + co, a.rep_t1 + co, a.rep_length + co, a.rep_queue + co, a.rep_seg + co, &rs);
-  a.rep_n[t] = rs.n_rep;
-  a.shape_used[t] = rs.shape_used;
-  for (int q = 0; q < 6; ++q) a.stats[7 * t + q] = rs.counts[q];
-  a.stats[7 * t + 6] = 0;
-  a.stats_len[2 * t] = rs.lengths[0];
-  a.stats_len[2 * t + 1] = rs.lengths[1];
-  if (counters) atomicAdd(&counters[7 * kShards + (blockIdx.x & (kShards - 1))], (unsigned long long)nseg);
+  __syncthreads();
+  if (lane == 0) {
+    a.route_n[t] = n_route;
+    a.seg_n[t] = ng;
+    a.way_n[t] = n_way;
+    // report() over this trace's segments (reporter_service.py:79-179)
+    ReportStats rs;
+    const int64_t end_t = n_probe > 0 ? a.b.time[lo_probe + n_probe - 1] : 0;
+    report_segments((int32_t)ng, a.seg_id + co, a.seg_start + co, a.seg_end + co, a.seg_internal + co,
+                    a.seg_queue + co, nullptr, a.seg_length + co, a.seg_bshape + co, a.seg_index + co, end_t,
+                    a.threshold, a.report_levels, a.transition_levels, a.rep_id + co, a.rep_next + co,
+                    a.rep_t0 + co, a.rep_t1 + co, a.rep_length + co, a.rep_queue + co, a.rep_seg + co, &rs);
+    a.rep_n[t] = rs.n_rep;
+    a.shape_used[t] = rs.shape_used;
+    for (int q = 0; q < 6; ++q) a.stats[7 * t + q] = rs.counts[q];
+    a.stats[7 * t + 6] = 0;
+    a.stats_len[2 * t] = rs.lengths[0];
+    a.stats_len[2 * t + 1] = rs.lengths[1];
+    if (counters) atomicAdd(&counters[7 * kShards + (blockIdx.x & (kShards - 1))], (unsigned long long)ng);
+  }
 }
 
 // ------------------------------------------------------------------------------
