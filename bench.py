@@ -28,6 +28,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+# HBM bytes per k_route<256> launch from the FETCH_SIZE / WRITE_SIZE passes of
+# tools/profile_gpu.sh (separate --pmc runs of this same command; tools/pmc_summary.py)
+PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r01_v6_pmc.json')
 T_BEGIN = 1483228800
 
 
@@ -168,6 +171,12 @@ def main():
     rbytes = route_bytes(counters) / ns  # per launch (each stream launches once per step)
     achieved = rbytes / (route_avg_ms * 1e-3) / 1e9
 
+    traffic = None
+    if os.path.exists(PMC_SUMMARY):
+        k = json.load(open(PMC_SUMMARY))['kernels'].get('k_route<256>', {})
+        if 'fetch_bytes_per_launch' in k and 'write_bytes_per_launch' in k:
+            traffic = int(k['fetch_bytes_per_launch'] + k['write_bytes_per_launch'])
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_traces > 0:
         from oracle import pyoracle as po
@@ -205,13 +214,14 @@ def main():
                        'stage_ms_per_stream': stage_ms},
             'roofline': {'kernel': 'k_route<256> (K3 bounded one-to-many search + K4 transition)',
                          'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
-                         'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': None,
+                         'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': traffic,
+                         'traffic_source': os.path.relpath(PMC_SUMMARY, ROOT) if traffic else None,
                          'launch_ms': round(route_avg_ms, 3), 'algorithmic_bytes': int(rbytes),
                          'settled_nodes': int(counters[3]), 'relaxed_edges': int(counters[4]),
                          'tasks': int(counters[5]), 'transition_entries': int(counters[6]),
                          'source_candidates': int(counters[12]),
                          'retry_settled_nodes': int(counters[9]), 'search_rounds': int(counters[13]),
-                         'phase_cycles': [int(x) for x in counters[16:20]] if any(counters[16:20]) else None},
+                         'phase_cycles': [int(x) for x in counters[16:20]] if 'stamps' in _lib.LIB_PATH else None},
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)
