@@ -29,6 +29,9 @@ void finalize_params(MatchParams* p) {
   p->inv_beta = 1.0 / p->beta;
   if (p->kmax > OTR_KMAX) p->kmax = OTR_KMAX;
   if (p->kmax < 1) p->kmax = 1;
+  // routing labels and A* keys are uint32 millimetres: routes are
+  // bounded by breakage_distance, which is therefore capped at 1000 km
+  if (!(p->breakage_distance <= 1.0e6)) p->breakage_distance = 1.0e6;
 }
 
 ModeParams default_mode_params() {

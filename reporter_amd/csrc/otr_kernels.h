@@ -346,6 +346,27 @@ __global__ void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* ca
 // (label << 32 | edge id) so the minimum also records the smallest-id predecessor
 // edge among those achieving the label (the oracle's predecessor rule).
 // ------------------------------------------------------------------------------
+// One 16-B load whose four words are all materialised here: keeps the compiler from
+// splitting a record load into dependent pieces sunk into the branches that use them.
+__device__ inline uint4 ld16(const uint4* p) {
+  uint4 r = *p;
+  asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w));
+  return r;
+}
+
+// Wave minimum by DPP row shifts and row broadcasts (GFX9), result read from lane 63.
+__device__ inline uint32_t wave_min_u32(uint32_t v) {
+  const int I = -1;
+  auto mn = [](uint32_t a, int b) { return a < (uint32_t)b ? a : (uint32_t)b; };
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 template <bool PRED>
 struct LabelT {
   using T = uint32_t;
@@ -392,7 +413,8 @@ struct Heur {
   __device__ uint32_t operator()(int32_t lat_e6, int32_t lon_e6) const {
     const double dx = (e6(lon_e6) - plon) * mpl, dy = (e6(lat_e6) - plat) * kMetersPerDeg;
     const double h = (sqrt(dx * dx + dy * dy) - r) * 0.99 - 1.0;
-    return h > 0.0 ? (uint32_t)floor(h * 1000.0) : 0u;
+    const double hm = floor(h * 1000.0);
+    return h > 0.0 ? (hm < 2147483647.0 ? (uint32_t)hm : 2147483647u) : 0u;
   }
 };
 
@@ -426,8 +448,7 @@ __device__ inline int lds_insert(SearchLds<CAP, PRED>& L, uint32_t node, bool* i
     if (k == kEmpty) {
       const uint32_t old = atomicCAS(&L.key[h], kEmpty, node);
       if (old == kEmpty) {
-        const int nk = atomicAdd(&L.n_keys, 1);
-        if (nk >= (CAP * 3) / 4) L.overflow = 1;
+        atomicAdd(&L.n_keys, 1);  // load factor checked once per round (search_run)
         *isnew = true;
         return (int)h;
       }
@@ -530,16 +551,13 @@ __device__ bool search_run(SearchLds<CAP, PRED>& L, const DevGraph& g, const Heu
   for (;;) {
     OTR_STAMP(t0);
     const int np = L.n_pend;
-    int64_t fmin = INT64_MAX;
+    uint32_t fm = 0xFFFFFFFFu;
     for (int k = lane; k < np; k += OTR_WAVE) {
       const int sl = L.pend[k];
-      const int64_t f = (int64_t)LabelT<PRED>::label(L.lab[sl]) + (int64_t)L.hv[sl];
-      fmin = f < fmin ? f : fmin;
+      const uint32_t f = LabelT<PRED>::label(L.lab[sl]) + L.hv[sl];  // < 2^32: labels, h < 2^31
+      fm = f < fm ? f : fm;
     }
-    for (int off = 32; off > 0; off >>= 1) {
-      const int64_t o = __shfl_xor(fmin, off);
-      fmin = o < fmin ? o : fmin;
-    }
+    const int64_t fmin = np > 0 ? (int64_t)wave_min_u32(fm) : INT64_MAX;
     OTR_STAMP(t1);
     const bool res = lane >= n_tgt || target_resolved(L, tslot, tpart, hT, d0min, bound_mm, fmin, np == 0);
     const bool done = __ballot(!res) == 0ull || np == 0;
@@ -556,7 +574,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>& L, const DevGraph& g, const Heu
       bool take = false;
       if (k < np) {
         sl = L.pend[k];
-        take = (int64_t)LabelT<PRED>::label(L.lab[sl]) + (int64_t)L.hv[sl] < theta;
+        take = (int64_t)(LabelT<PRED>::label(L.lab[sl]) + L.hv[sl]) < theta;
       }
       const unsigned long long mt = __ballot(take), mk = __ballot(k < np && !take);
       __syncthreads();
@@ -584,13 +602,13 @@ __device__ bool search_run(SearchLds<CAP, PRED>& L, const DevGraph& g, const Heu
         const uint32_t u = L.key[ws] & ~kInq;
         const uint32_t du = LabelT<PRED>::label(L.lab[ws]);
         if (slot == 0) ++my_settled;
-        const uint4 r = g.adj[4 * (size_t)u + slot];
+        const uint4 r = ld16(g.adj + 4 * (size_t)u + slot);
         const uint32_t e0 = PRED ? g.node_row[u] : 0u;  // edge id = CSR row start + slot
         relax_one(L, H, r.x & ~kAdjMore, r.y, (int32_t)r.z, (int32_t)r.w, du, e0 + slot, bound_mm, mode_bit,
                   my_relaxed);
         if (slot == 3 && (r.x & kAdjMore))
           for (uint32_t e = g.node_row[u] + 4; e < g.node_row[u + 1]; ++e) {
-            const uint4 pk = g.edge_pack[e];
+            const uint4 pk = ld16(g.edge_pack + e);
             const int2 vll = g.node_ll[pk.x];
             relax_one(L, H, pk.x | ((pk.z & 7u) << 28), pk.y, vll.x, vll.y, du, e, bound_mm, mode_bit, my_relaxed);
           }
@@ -599,7 +617,10 @@ __device__ bool search_run(SearchLds<CAP, PRED>& L, const DevGraph& g, const Heu
     __syncthreads();
     OTR_STAMP(t4);
     cyc[3] += t4 - t3;
-    if (L.overflow) break;
+    if (L.overflow || L.n_keys > (CAP * 3) / 4) {
+      L.overflow = 1;
+      break;
+    }
   }
 #ifdef OTR_STAMPS
   if (stamps && lane == 0)
