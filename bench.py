@@ -28,9 +28,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-# HBM bytes per k_route<256> launch from the FETCH_SIZE / WRITE_SIZE passes of
+ROUTE_KERNEL = 'k_route<128, 2>'  # first-tier search kernel (rocprofv3 name)
+# HBM bytes per ROUTE_KERNEL launch from the FETCH_SIZE / WRITE_SIZE passes of
 # tools/profile_gpu.sh (separate --pmc runs of this same command; tools/pmc_summary.py)
-PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r01_v6_pmc.json')
+PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r01_v8_pmc.json')
 T_BEGIN = 1483228800
 
 
@@ -39,7 +40,7 @@ def log(*a):
 
 
 def route_bytes(c):
-    """Algorithmic HBM bytes of one k_route<512> launch, from the
+    """Algorithmic HBM bytes of one first-tier k_route launch, from the
     device work counters: 64 B per task (task record, step metadata, root lookup),
     32 B per settled node (its adjacency record), 16 B per source candidate
     (edge, fraction, length), 20 B per target read (edge, fraction, src, length),
@@ -173,7 +174,7 @@ def main():
 
     traffic = None
     if os.path.exists(PMC_SUMMARY):
-        k = json.load(open(PMC_SUMMARY))['kernels'].get('k_route<256>', {})
+        k = json.load(open(PMC_SUMMARY))['kernels'].get(ROUTE_KERNEL, {})
         if 'fetch_bytes_per_launch' in k and 'write_bytes_per_launch' in k:
             traffic = int(k['fetch_bytes_per_launch'] + k['write_bytes_per_launch'])
 
@@ -212,7 +213,7 @@ def main():
                                       % world if world > 1 else 'single GPU',
                        'streams': ns,
                        'stage_ms_per_stream': stage_ms},
-            'roofline': {'kernel': 'k_route<256> (K3 bounded one-to-many search + K4 transition)',
+            'roofline': {'kernel': ROUTE_KERNEL + ' (K3 bounded one-to-many searches, 2 per wave + K4 transition)',
                          'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': traffic,
                          'traffic_source': os.path.relpath(PMC_SUMMARY, ROOT) if traffic else None,
@@ -221,6 +222,8 @@ def main():
                          'tasks': int(counters[5]), 'transition_entries': int(counters[6]),
                          'source_candidates': int(counters[12]),
                          'retry_settled_nodes': int(counters[9]), 'search_rounds': int(counters[13]),
+                         'table_keys': int(counters[14]),
+                         'tasks_keys_gt': {'64': int(counters[22]), '96': int(counters[15]), '128': int(counters[23])},
                          'phase_cycles': [int(x) for x in counters[16:20]] if 'stamps' in _lib.LIB_PATH else None},
             'cpu_baseline': cpu,
         }

@@ -50,11 +50,15 @@ def _newer(target, sources):
     return all(os.path.getmtime(s) <= t for s in sources)
 
 
-def build_otr(force=False, stamps=False):
-    """stamps=True: diagnostic build with per-phase shader-clock stamps (libotr_stamps.so)."""
+def build_otr(force=False, stamps=False, variant=None, defines=()):
+    """stamps=True: diagnostic build with per-phase shader-clock stamps (libotr_stamps.so).
+    variant/defines: an A/B build libotr_<variant>.so with extra -D flags (experiments)."""
     os.makedirs(BUILD, exist_ok=True)
     suffix = '_stamps' if stamps else ''
     extra = ['-DOTR_STAMPS'] if stamps else []
+    if variant:
+        suffix += '_' + variant
+        extra += ['-D' + d for d in defines]
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
     headers += [os.path.join(ROOT, 'include', f) for f in os.listdir(os.path.join(ROOT, 'include'))]
     objs = []
@@ -96,7 +100,11 @@ def build_all(force=False):
 
 
 if __name__ == '__main__':
-    if '--stamps' in sys.argv:
+    if '--variant' in sys.argv:  # --variant NAME DEF1 DEF2 ...
+        i = sys.argv.index('--variant')
+        print(build_otr(force=True, stamps='--stamps' in sys.argv, variant=sys.argv[i + 1],
+                        defines=[d for d in sys.argv[i + 2:] if not d.startswith('--')]))
+    elif '--stamps' in sys.argv:
         print(build_otr(force='--force' in sys.argv, stamps=True))
     else:
         print(build_all(force='--force' in sys.argv))

@@ -430,13 +430,20 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   ra.overflow_flag = task_ovf;
   if (NT > 0) {
     tb(OTR_STAGE_ROUTE);
-    k_route<256><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
+    // two searches per wave (CAP 128 tables); wider steps and overflows retry below
+    static const int route_g = getenv("OTR_ROUTE_G") ? atoi(getenv("OTR_ROUTE_G")) : 2;  // A/B knob
+    if (route_g == 2) {
+      const int64_t units = (NT + 1) / 2;
+      k_route<128, 2><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
+    } else {
+      k_route<256, 1><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
+    }
     te(OTR_STAGE_ROUTE);
     // overflow retries with larger LDS tables (same results, fewer resident waves)
     int64_t* list = need<int64_t>(S_LIST, NT);
     unsigned long long* cnt = need<unsigned long long>(S_MISC, 4);
     tb(OTR_STAGE_ROUTE_BIG);
-    for (int tier = 0; tier < 2; ++tier) {
+    for (int tier = 0; tier < 3; ++tier) {
       HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
       k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
       unsigned long long novf = 0;
@@ -447,9 +454,10 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.n_tasks = (int64_t)novf;
-      if (tier == 0) k_route<1024><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
-      else k_route<4096><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
-      if (tier == 1) {
+      if (tier == 0) k_route<256, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
+      else if (tier == 1) k_route<1024, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
+      else k_route<4096, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
+      if (tier == 2) {
         HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
         k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
         HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));

@@ -367,6 +367,49 @@ __device__ inline uint32_t wave_min_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// 1: the next round's fmin is carried from partition/relax (every relaxation evaluates
+// the heuristic); 0: a pass over the pending list computes it (heuristic on insert only)
+#ifndef OTR_FMIN_CARRY
+#define OTR_FMIN_CARRY 1
+#endif
+
+// G independent searches per wave, GL = 64 / G lanes each (G = 1 or 2).  Per-group
+// ballots, prefix counts, minima and wave-uniform loop bounds.
+template <int G>
+struct Grp {
+  static constexpr int GL = OTR_WAVE / G;
+  __device__ static int g() { return G == 1 ? 0 : (int)threadIdx.x / GL; }
+  __device__ static int gl() { return G == 1 ? (int)threadIdx.x : (int)threadIdx.x % GL; }
+  __device__ static unsigned long long mine(unsigned long long m) {
+    return G == 1 ? m : (m >> (GL * g())) & ((1ull << GL) - 1ull);
+  }
+  __device__ static int prefix(unsigned long long m) { return __popcll(mine(m) & ((1ull << gl()) - 1ull)); }
+  __device__ static int count(unsigned long long m) { return __popcll(mine(m)); }
+  // maximum over groups of a group-uniform value (a wave-uniform loop bound)
+  __device__ static int umax(int v) {
+    if (G == 1) return __builtin_amdgcn_readfirstlane(v);
+    const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 32);
+    return a > b ? a : b;
+  }
+  __device__ static bool all(bool v) {
+    if (G == 1) return __builtin_amdgcn_readfirstlane((int)v) != 0;
+    return __builtin_amdgcn_readlane((int)v, 0) != 0 && __builtin_amdgcn_readlane((int)v, 32) != 0;
+  }
+  __device__ static uint32_t min_u32(uint32_t v) {
+    if (G == 1) return wave_min_u32(v);
+    const int I = -1;
+    auto mn = [](uint32_t a, int b) { return a < (uint32_t)b ? a : (uint32_t)b; };
+    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    return g() ? b : a;
+  }
+};
+
 template <bool PRED>
 struct LabelT {
   using T = uint32_t;
@@ -409,10 +452,13 @@ constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
 // can reach, weakened by 1% and 1 m and floored to whole mm: consistent (h(u) - h(v)
 // <= len_mm(u,v) for every edge), so A* ordering never changes a label.
 struct Heur {
-  double plat, plon, mpl, r;
+  int32_t plat_e6, plon_e6;  // target probe rounded to micro-degrees (any fixed point keeps h consistent)
+  float mx;                  // metres per micro-degree of longitude at the most poleward latitude, rounded down
+  float c;                   // 0.99 r + 1 (m), rounded up
   __device__ uint32_t operator()(int32_t lat_e6, int32_t lon_e6) const {
-    const double dx = (e6(lon_e6) - plon) * mpl, dy = (e6(lat_e6) - plat) * kMetersPerDeg;
-    const double h = (sqrt(dx * dx + dy * dy) - r) * 0.99 - 1.0;
+    const double dx = (double)(lon_e6 - plon_e6) * (double)mx;
+    const double dy = (double)(lat_e6 - plat_e6) * (kMetersPerDeg * 1e-6);
+    const double h = sqrt(dx * dx + dy * dy) * 0.99 - (double)c;
     const double hm = floor(h * 1000.0);
     return h > 0.0 ? (hm < 2147483647.0 ? (uint32_t)hm : 2147483647u) : 0u;
   }
@@ -421,7 +467,13 @@ struct Heur {
 __device__ inline Heur make_heur(double plat, double plon, double r, double bound) {
   double lat = fabs(plat) + 2.0 * bound / kMetersPerDeg;
   if (lat > 89.9) lat = 89.9;
-  return Heur{plat, plon, kMetersPerDeg * cos_deg(lat), r};
+  const double mx = kMetersPerDeg * 1e-6 * cos_deg(lat);
+  float mxf = (float)mx;  // positive: one ulp toward 0 / toward +inf by the bit pattern
+  if ((double)mxf > mx) mxf = __uint_as_float(__float_as_uint(mxf) - 1u);
+  const double c = 0.99 * r + 1.0;
+  float cf = (float)c;
+  if ((double)cf < c) cf = __uint_as_float(__float_as_uint(cf) + 1u);
+  return Heur{(int32_t)llround(plat * 1e6), (int32_t)llround(plon * 1e6), mxf, cf};
 }
 
 // routing bound and partial edge lengths in whole mm (shared with the oracle)
@@ -464,16 +516,19 @@ __device__ inline int lds_insert(SearchLds<CAP, PRED>& L, uint32_t node, bool* i
   return -1;
 }
 
-template <int CAP, bool PRED>
-__device__ inline void search_init(SearchLds<CAP, PRED>& L) {
-  for (int k = threadIdx.x; k < CAP; k += OTR_WAVE) {
-    L.key[k] = kEmpty;
-    L.lab[k] = LabelT<PRED>::kInf;
-  }
-  if (threadIdx.x == 0) {
-    L.n_pend = 0;
-    L.n_keys = 0;
-    L.overflow = 0;
+template <int CAP, bool PRED, int G = 1>
+__device__ inline void search_init(SearchLds<CAP, PRED>* Ls) {
+  for (int q = 0; q < G; ++q) {
+    SearchLds<CAP, PRED>& L = Ls[q];
+    for (int k = threadIdx.x; k < CAP; k += OTR_WAVE) {
+      L.key[k] = kEmpty;
+      L.lab[k] = LabelT<PRED>::kInf;
+    }
+    if (threadIdx.x == 0) {
+      L.n_pend = 0;
+      L.n_keys = 0;
+      L.overflow = 0;
+    }
   }
   __syncthreads();
 }
@@ -484,31 +539,47 @@ __device__ inline void search_init(SearchLds<CAP, PRED>& L) {
 // min(L(T), fmin - h(T)) cannot make d0 + L + tpart fit the bound, T is unreachable for
 // every source of the task.  Integer arithmetic: no rounding margins needed.
 template <int CAP, bool PRED>
-__device__ inline bool target_resolved(const SearchLds<CAP, PRED>& L, int tslot, int64_t tpart, int64_t hT,
-                                       int64_t d0min, int64_t bound_mm, int64_t fmin, bool pend_empty) {
+__device__ inline bool target_resolved(const SearchLds<CAP, PRED>& L, int tslot, uint32_t tpart, uint32_t hT,
+                                       uint32_t d0min, uint32_t bound_mm, uint32_t fmin, bool pend_empty) {
   if (tslot < 0 || pend_empty) return true;
   const uint32_t l32 = LabelT<PRED>::label(L.lab[tslot]);
   const int64_t lab = l32 == kNoLabel ? INT64_MAX / 4 : (int64_t)l32;
-  if (lab + hT < fmin) return true;
-  const int64_t lb = lab < fmin - hT ? lab : fmin - hT;
-  return d0min + lb + tpart > bound_mm;
+  if (lab + (int64_t)hT < (int64_t)fmin) return true;
+  const int64_t rest = (int64_t)fmin - (int64_t)hT;
+  const int64_t lb = lab < rest ? lab : rest;
+  return (int64_t)d0min + lb + (int64_t)tpart > (int64_t)bound_mm;
 }
 
+// Relax edge (u → dw) with u's label du.  Every relaxing lane evaluates the heuristic of
+// the head itself (deterministic, equal to the stored one), so an improvement's key
+// f = label + h is known without reading an hv entry another lane may be writing; the
+// round's minimum over improvements and kept pending nodes is the next round's fmin.
 template <int CAP, bool PRED>
 __device__ inline void relax_one(SearchLds<CAP, PRED>& L, const Heur& H, uint32_t dw, uint32_t len_mm, int32_t vlat,
-                                 int32_t vlon, uint32_t du, uint32_t edge, int64_t bound_mm, uint32_t mode_bit,
-                                 unsigned long long& relaxed) {
+                                 int32_t vlon, uint32_t du, uint32_t edge, uint32_t bound_mm, uint32_t mode_bit,
+                                 uint32_t& relaxed, uint32_t& fnext) {
   if (!(((dw >> 28) & 7u) & mode_bit)) return;
   ++relaxed;
-  const int64_t nd = (int64_t)du + (int64_t)len_mm;
+  const uint64_t nd = (uint64_t)du + len_mm;
   if (nd > bound_mm) return;
+#if OTR_FMIN_CARRY
+  const uint32_t h = H(vlat, vlon);
+#endif
   bool isnew = false;
   const int sl = lds_insert(L, dw & kAdjDstMask, &isnew);
   if (sl < 0) return;
+#if OTR_FMIN_CARRY
+  if (isnew) L.hv[sl] = h;
+#else
   if (isnew) L.hv[sl] = H(vlat, vlon);
+#endif
   const typename LabelT<PRED>::T nb = LabelT<PRED>::make((uint32_t)nd, edge);
   const typename LabelT<PRED>::T old = atomicMin(&L.lab[sl], nb);
   if (LabelT<PRED>::label(nb) < LabelT<PRED>::label(old)) {
+#if OTR_FMIN_CARRY
+    const uint32_t f = (uint32_t)nd + h;
+    fnext = f < fnext ? f : fnext;
+#endif
     const uint32_t ok = atomicOr(&L.key[sl], kInq);
     if (!(ok & kInq)) {
       const int p = atomicAdd(&L.n_pend, 1);
@@ -518,20 +589,27 @@ __device__ inline void relax_one(SearchLds<CAP, PRED>& L, const Heur& H, uint32_
   }
 }
 
-// Search rooted at `start` (label 0).  Lanes j < n_tgt hold target node tnode, its
-// heuristic hT and the target partial length tpart (mm).  false = LDS-table overflow.
-template <int CAP, bool PRED>
-__device__ bool search_run(SearchLds<CAP, PRED>& L, const DevGraph& g, const Heur& H, uint32_t mode_bit,
-                           uint32_t start, int64_t bound_mm, int64_t delta_mm, uint32_t tnode, int64_t tpart,
-                           int64_t hT, int64_t d0min, int n_tgt, unsigned long long* settled,
+// G searches per wave, one per lane group, each in its own table Ls[g]: search g is
+// rooted at `start` (label 0); lanes gl < n_tgt of the group hold a target node tnode, its
+// heuristic hT and partial length tpart (mm).  active = false: the group idles.
+// Returns false (per lane, group-uniform) on an LDS-table overflow.
+template <int CAP, bool PRED, int G = 1>
+__device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const Heur& H, uint32_t mode_bit,
+                           bool active, uint32_t start, uint32_t bound_mm, uint32_t delta_mm, uint32_t tnode,
+                           uint32_t tpart, uint32_t hT, uint32_t d0min, int n_tgt, unsigned long long* settled,
                            unsigned long long* relaxed, unsigned long long* rounds,
                            unsigned long long* stamps = nullptr) {
-  const int lane = threadIdx.x;
-  if (lane == 0) {
+  using Gr = Grp<G>;
+  // load-factor limit (probe chains stay short); small tables run fuller
+  constexpr int kMaxKeys = CAP <= 128 ? (CAP * 7) / 8 : (CAP * 3) / 4;
+  const int gl = Gr::gl();
+  SearchLds<CAP, PRED>& L = Ls[Gr::g()];
+  const int2 sll = g.node_ll[active ? start : 0u];
+  const uint32_t hroot = H(sll.x, sll.y);
+  if (active && gl == 0) {
     bool isnew;
     const int sl = lds_insert(L, start, &isnew);
-    const int2 sll = g.node_ll[start];
-    L.hv[sl] = H(sll.x, sll.y);
+    L.hv[sl] = hroot;
     L.lab[sl] = LabelT<PRED>::make(0u, kEmpty);
     L.key[sl] |= kInq;
     L.pend[0] = (uint16_t)sl;
@@ -540,62 +618,79 @@ __device__ bool search_run(SearchLds<CAP, PRED>& L, const DevGraph& g, const Heu
   __syncthreads();
   // targets are pre-inserted (no label) so every round reads their label from a known slot
   int tslot = -1;
-  if (lane < n_tgt && tnode != kEmpty) {
+  if (active && gl < n_tgt && tnode != kEmpty) {
     bool isnew;
     tslot = lds_insert(L, tnode, &isnew);
     if (tslot >= 0 && isnew) L.hv[tslot] = (uint32_t)hT;
   }
   __syncthreads();
-  unsigned long long my_settled = 0, my_relaxed = 0, my_rounds = 0;
+  uint32_t my_settled = 0, my_relaxed = 0, my_rounds = 0;
   unsigned long long cyc[4] = {0, 0, 0, 0};
+  uint32_t fmin = hroot;  // 0xFFFFFFFF: nothing pending
+  bool done = !active;
   for (;;) {
     OTR_STAMP(t0);
-    const int np = L.n_pend;
-    uint32_t fm = 0xFFFFFFFFu;
-    for (int k = lane; k < np; k += OTR_WAVE) {
-      const int sl = L.pend[k];
-      const uint32_t f = LabelT<PRED>::label(L.lab[sl]) + L.hv[sl];  // < 2^32: labels, h < 2^31
-      fm = f < fm ? f : fm;
+    const int np = done ? 0 : L.n_pend;
+#if !OTR_FMIN_CARRY
+    {  // fmin = minimum key over the pending list
+      uint32_t fm = 0xFFFFFFFFu;
+      const int npx0 = Gr::umax(np);
+      for (int base = 0; base < npx0; base += Gr::GL) {
+        const int k = base + gl;
+        if (k < np) {
+          const int sl = L.pend[k];
+          const uint32_t f = LabelT<PRED>::label(L.lab[sl]) + L.hv[sl];
+          fm = f < fm ? f : fm;
+        }
+      }
+      fmin = Gr::min_u32(fm);
     }
-    const int64_t fmin = np > 0 ? (int64_t)wave_min_u32(fm) : INT64_MAX;
+#endif
     OTR_STAMP(t1);
-    const bool res = lane >= n_tgt || target_resolved(L, tslot, tpart, hT, d0min, bound_mm, fmin, np == 0);
-    const bool done = __ballot(!res) == 0ull || np == 0;
+    const bool res = done || gl >= n_tgt || target_resolved(L, tslot, tpart, hT, d0min, bound_mm, fmin, np == 0);
+    done = done || Gr::mine(__ballot(!res)) == 0ull || np == 0;
     OTR_STAMP(t2);
     cyc[0] += t1 - t0;
     cyc[1] += t2 - t1;
-    if (done) break;
-    ++my_rounds;
-    const int64_t theta = fmin + delta_mm;
+    if (Gr::all(done)) break;
+    if (!done && gl == 0) ++my_rounds;
+    const uint32_t theta = fmin + delta_mm < fmin ? 0xFFFFFFFFu : fmin + delta_mm;  // saturating
+    uint32_t fnext = 0xFFFFFFFFu;
     int kept = 0, nw = 0;
-    for (int base = 0; base < np; base += OTR_WAVE) {
-      const int k = base + lane;
+    const int npx = Gr::umax(np);
+    for (int base = 0; base < npx; base += Gr::GL) {
+      const int k = base + gl;
+      const bool in = k < np;
       uint16_t sl = 0;
+      uint32_t f = 0;
       bool take = false;
-      if (k < np) {
+      if (in) {
         sl = L.pend[k];
-        take = (int64_t)(LabelT<PRED>::label(L.lab[sl]) + L.hv[sl]) < theta;
+        f = LabelT<PRED>::label(L.lab[sl]) + L.hv[sl];  // < 2^32: labels, h < 2^31
+        take = f < theta;
       }
-      const unsigned long long mt = __ballot(take), mk = __ballot(k < np && !take);
+      const unsigned long long mt = __ballot(take), mk = __ballot(in && !take);
       __syncthreads();
       if (take) {
-        L.work[nw + prefix_count(mt)] = sl;
+        L.work[nw + Gr::prefix(mt)] = sl;
         atomicAnd(&L.key[sl], ~kInq);
-      } else if (k < np) {
-        L.pend[kept + prefix_count(mk)] = sl;
+      } else if (in) {
+        L.pend[kept + Gr::prefix(mk)] = sl;
+        fnext = f < fnext ? f : fnext;
       }
-      nw += __popcll(mt);
-      kept += __popcll(mk);
+      nw += Gr::count(mt);
+      kept += Gr::count(mk);
       __syncthreads();
     }
-    if (lane == 0) L.n_pend = kept;
+    if (!done && gl == 0) L.n_pend = kept;
     __syncthreads();
     OTR_STAMP(t3);
     cyc[2] += t3 - t2;
     // relax: lane = (work node, adjacency slot), so a round's dependent chain is a single
     // relaxation; slot 3 of a node with more than 4 out-edges also walks the CSR tail
-    for (int base = 0; base < 4 * nw; base += OTR_WAVE) {
-      const int k = base + lane;
+    const int nwx = Gr::umax(4 * nw);
+    for (int base = 0; base < nwx; base += Gr::GL) {
+      const int k = base + gl;
       if (k < 4 * nw) {
         const int ws = L.work[k >> 2];
         const int slot = k & 3;
@@ -605,25 +700,28 @@ __device__ bool search_run(SearchLds<CAP, PRED>& L, const DevGraph& g, const Heu
         const uint4 r = ld16(g.adj + 4 * (size_t)u + slot);
         const uint32_t e0 = PRED ? g.node_row[u] : 0u;  // edge id = CSR row start + slot
         relax_one(L, H, r.x & ~kAdjMore, r.y, (int32_t)r.z, (int32_t)r.w, du, e0 + slot, bound_mm, mode_bit,
-                  my_relaxed);
+                  my_relaxed, fnext);
         if (slot == 3 && (r.x & kAdjMore))
           for (uint32_t e = g.node_row[u] + 4; e < g.node_row[u + 1]; ++e) {
             const uint4 pk = ld16(g.edge_pack + e);
             const int2 vll = g.node_ll[pk.x];
-            relax_one(L, H, pk.x | ((pk.z & 7u) << 28), pk.y, vll.x, vll.y, du, e, bound_mm, mode_bit, my_relaxed);
+            relax_one(L, H, pk.x | ((pk.z & 7u) << 28), pk.y, vll.x, vll.y, du, e, bound_mm, mode_bit, my_relaxed,
+                      fnext);
           }
       }
     }
     __syncthreads();
     OTR_STAMP(t4);
     cyc[3] += t4 - t3;
-    if (L.overflow || L.n_keys > (CAP * 3) / 4) {
-      L.overflow = 1;
-      break;
-    }
+#if OTR_FMIN_CARRY
+    fmin = Gr::min_u32(fnext);
+#endif
+    if (!done && (L.overflow || L.n_keys > kMaxKeys)) done = true;
+    __syncthreads();
+    if (done && active && gl == 0 && L.n_keys > kMaxKeys) L.overflow = 1;
   }
 #ifdef OTR_STAMPS
-  if (stamps && lane == 0)
+  if (stamps && threadIdx.x == 0)
     for (int q = 0; q < 4; ++q) atomicAdd(&stamps[q * kShards + (blockIdx.x & (kShards - 1))], cyc[q]);
 #endif
   if (settled) *settled += my_settled;
@@ -662,93 +760,129 @@ struct RouteArgs {
   int32_t* overflow_flag;     // per task
 };
 
-template <int CAP>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
-  __shared__ SearchLds<CAP, false> L;
-  const int lane = threadIdx.x;
-  const int64_t w = a.task_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (a.n_tasks + 7) / 8);
-  if (w >= a.n_tasks) return;
-  const int64_t task = a.task_list ? a.task_list[w] : w;
-  const int64_t s = a.task_state[task];
-  const unsigned long long mask = a.task_mask[task];
-  const int64_t sp = a.prev[s];
-  const int Kb = a.cand_count[s];
-  const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
-  const uint32_t mode_bit = 1u << mode;
-  const double bound = a.bound[s], gcd = a.g[s];
-  const int64_t bmm = bound_mm_of(bound);
-  const uint32_t root = gr.edge_dst[a.cand_edge[sp * OTR_KMAX + (__ffsll((long long)mask) - 1)]];
-  double* trow = a.trans + a.trans_off[s];
-  // targets: lane j
-  uint32_t ej = 0, tnode = kEmpty;
-  double pj = 0;
-  int64_t tpart = 0;
-  bool needed = false;
-  int64_t d0min = INT64_MAX / 4;
-  if (lane < Kb) {
-    ej = a.cand_edge[s * OTR_KMAX + lane];
-    pj = a.cand_p[s * OTR_KMAX + lane];
-    tpart = part_mm(pj, gr.len_mm[ej]);
-  }
-  for (unsigned long long m = mask; m; m &= m - 1) {
-    const int i = __ffsll((long long)m) - 1;
-    const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
-    const double pi = a.cand_p[sp * OTR_KMAX + i];
-    const int64_t d0 = part_mm(1.0 - pi, gr.len_mm[ei]);
-    d0min = d0 < d0min ? d0 : d0min;
-    if (lane < Kb && !(ej == ei && pj >= pi)) needed = true;
-  }
-  if (needed) tnode = gr.edge_src[ej];
-  if (a.forced[s]) {
-    for (unsigned long long m = mask; m; m &= m - 1)
-      if (lane < Kb) trow[(int64_t)(__ffsll((long long)m) - 1) * Kb + lane] = __builtin_huge_val();
-    return;
+#ifndef OTR_ROUTE2_WAVES
+#define OTR_ROUTE2_WAVES 8
+#endif
+template <int CAP, int G>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR_ROUTE2_WAVES : 8, G == 2 ? OTR_ROUTE2_WAVES : 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
+  using Gr = Grp<G>;
+  __shared__ SearchLds<CAP, false> Ls[G];
+  const int lane = Gr::gl();
+  const int64_t n_units = (a.n_tasks + G - 1) / G;
+  const int64_t w = a.task_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_units + 7) / 8);
+  if (w >= n_units) return;
+  const int64_t tw = w * G + Gr::g();
+  const bool have = tw < a.n_tasks;
+  const int64_t task = have ? (a.task_list ? a.task_list[tw] : tw) : 0;
+  // ---- search inputs (only these stay live through the search)
+  bool search, fits, forced;
+  uint32_t tnode = kEmpty, tpart = 0, hT = 0, d0min = 0xFFFFFFFFu, root = 0, bmm = 0, mode_bit = 1;
+  int Kb;
+  Heur H;
+  {
+    const int64_t s = a.task_state[task];
+    const unsigned long long mask = have ? a.task_mask[task] : 0ull;
+    const int64_t sp = a.prev[s];
+    Kb = a.cand_count[s];
+    fits = Kb <= Gr::GL;  // targets are lanes of the group: wider steps go to a G = 1 tier
+    const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+    mode_bit = 1u << mode;
+    bmm = (uint32_t)bound_mm_of(a.bound[s]);
+    if (have) root = gr.edge_dst[a.cand_edge[sp * OTR_KMAX + (__ffsll((long long)mask) - 1)]];
+    uint32_t ej = 0;
+    double pj = 0;
+    bool needed = false;
+    if (have && lane < Kb) {
+      ej = a.cand_edge[s * OTR_KMAX + lane];
+      pj = a.cand_p[s * OTR_KMAX + lane];
+      tpart = (uint32_t)part_mm(pj, gr.len_mm[ej]);
+    }
+    for (unsigned long long m = mask; m; m &= m - 1) {
+      const int i = __ffsll((long long)m) - 1;
+      const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
+      const double pi = a.cand_p[sp * OTR_KMAX + i];
+      const uint32_t d0 = (uint32_t)part_mm(1.0 - pi, gr.len_mm[ei]);
+      d0min = d0 < d0min ? d0 : d0min;
+      if (lane < Kb && !(ej == ei && pj >= pi)) needed = true;
+    }
+    forced = have && a.forced[s];
+    const unsigned long long need_mask = __ballot(needed);
+    search = have && fits && !forced && Gr::mine(need_mask) != 0ull;
+    const int64_t pb = a.state_probe[s];
+    H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], a.bound[s]);
+    if (needed) {
+      tnode = gr.edge_src[ej];
+      const int2 tll = gr.node_ll[tnode];
+      hT = H(tll.x, tll.y);
+    }
   }
   unsigned long long settled = 0, relaxed = 0, rounds = 0;
-  bool ok = true;
-  const bool need = __ballot(needed) != 0ull;
-  const int64_t pb = a.state_probe[s];
-  const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], bound);
-  int64_t hT = 0;
-  if (needed) {
-    const int2 tll = gr.node_ll[tnode];
-    hT = H(tll.x, tll.y);
-  }
-  search_init(L);
-  if (need)
-    ok = search_run(L, gr, H, mode_bit, root, bmm, (int64_t)(a.delta * 1000.0), tnode, tpart, hT, d0min, Kb,
-                    &settled, &relaxed, &rounds, counters ? counters + 16 * kShards : nullptr);
+  search_init<CAP, false, G>(Ls);
+  const bool ok = search_run<CAP, false, G>(Ls, gr, H, mode_bit, search, root, bmm, (uint32_t)(a.delta * 1000.0),
+                                            tnode, tpart, hT, d0min, Kb, &settled, &relaxed, &rounds,
+                                            counters ? counters + 16 * kShards : nullptr) && fits;
+  SearchLds<CAP, false>& L = Ls[Gr::g()];
   int64_t lab = -1;
-  if (ok && needed) {
+  if (ok && tnode != kEmpty && !forced) {
     const int sl = lds_find(L, tnode);
     if (sl >= 0 && L.lab[sl] != kNoLabel) lab = (int64_t)L.lab[sl];
   }
-  for (unsigned long long m = mask; m; m &= m - 1) {
-    const int i = __ffsll((long long)m) - 1;
-    const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
-    const double pi = a.cand_p[sp * OTR_KMAX + i];
+  // ---- transition rows: re-read the step (cached) rather than hold it live through the search
+  asm volatile("" ::: "memory");
+  if (have && (ok || forced)) {
+    const int64_t s = a.task_state[task];
+    const unsigned long long mask = a.task_mask[task];
+    const int64_t sp = a.prev[s];
+    const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+    const double gcd = a.g[s], inv_beta = a.inv_beta[mode];
+    double* trow = a.trans + a.trans_off[s];
     if (lane < Kb) {
-      int64_t r = -1;
-      if (ej == ei && pj >= pi) r = part_mm(pj - pi, gr.len_mm[ei]);
-      else if (lab >= 0) r = part_mm(1.0 - pi, gr.len_mm[ei]) + lab + tpart;
-      trow[(int64_t)i * Kb + lane] =
-          (ok && r >= 0 && r <= bmm) ? fabs((double)r / 1000.0 - gcd) * a.inv_beta[mode] : __builtin_huge_val();
+      const uint32_t ej = a.cand_edge[s * OTR_KMAX + lane];
+      const double pj = a.cand_p[s * OTR_KMAX + lane];
+      for (unsigned long long m = mask; m; m &= m - 1) {
+        const int i = __ffsll((long long)m) - 1;
+        const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
+        const double pi = a.cand_p[sp * OTR_KMAX + i];
+        int64_t r = -1;
+        if (forced) r = -1;
+        else if (ej == ei && pj >= pi) r = part_mm(pj - pi, gr.len_mm[ei]);
+        else if (lab >= 0) r = part_mm(1.0 - pi, gr.len_mm[ei]) + lab + tpart;
+        trow[(int64_t)i * Kb + lane] =
+            (r >= 0 && r <= (int64_t)bmm) ? fabs((double)r / 1000.0 - gcd) * inv_beta : __builtin_huge_val();
+      }
     }
   }
-  if (!ok && lane == 0) a.overflow_flag[task] = 1;
+  if (have && !ok && !forced && lane == 0) a.overflow_flag[task] = 1;
   if (counters) {
+    // per-group table statistics; wave totals on lane 0
+    const int nk = have && search ? L.n_keys : 0;
+    unsigned long long kk = lane == 0 ? (unsigned long long)nk : 0ull;
+    unsigned long long c96 = (lane == 0 && nk > 96) ? 1ull : 0ull, c64 = (lane == 0 && nk > 64) ? 1ull : 0ull,
+                       c128 = (lane == 0 && nk > 128) ? 1ull : 0ull;
+    unsigned long long kb = (lane == 0 && have) ? (unsigned long long)Kb : 0ull,
+                       ns = (lane == 0 && have) ? (unsigned long long)__popcll(a.task_mask[task]) : 0ull;
     for (int off = 32; off > 0; off >>= 1) {
       settled += __shfl_xor(settled, off);
       relaxed += __shfl_xor(relaxed, off);
-      rounds = rounds;  // rounds is wave-uniform
+      rounds += __shfl_xor(rounds, off);
+      kk += __shfl_xor(kk, off);
+      c96 += __shfl_xor(c96, off);
+      c64 += __shfl_xor(c64, off);
+      c128 += __shfl_xor(c128, off);
+      kb += __shfl_xor(kb, off);
+      ns += __shfl_xor(ns, off);
     }
-    if (lane == 0) {
+    if (threadIdx.x == 0) {
       const int sh = blockIdx.x & (kShards - 1);
       atomicAdd(&counters[3 * kShards + sh], settled);
       atomicAdd(&counters[4 * kShards + sh], relaxed);
-      atomicAdd(&counters[11 * kShards + sh], (unsigned long long)Kb);
-      atomicAdd(&counters[12 * kShards + sh], (unsigned long long)__popcll(mask));
+      atomicAdd(&counters[11 * kShards + sh], kb);
+      atomicAdd(&counters[12 * kShards + sh], ns);
       atomicAdd(&counters[13 * kShards + sh], rounds);
+      atomicAdd(&counters[14 * kShards + sh], kk);
+      if (c96) atomicAdd(&counters[15 * kShards + sh], c96);
+      if (c64) atomicAdd(&counters[22 * kShards + sh], c64);
+      if (c128) atomicAdd(&counters[23 * kShards + sh], c128);
     }
   }
 }
@@ -934,10 +1068,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
   const int64_t pb = a.state_probe[s];
   const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], a.bound[s]);
   const int2 tll = gr.node_ll[T];
-  search_init(L);
-  const bool ok = search_run(L, gr, H, mode_bit, S, bound_mm_of(a.bound[s]), (int64_t)(a.delta * 1000.0),
-                             lane == 0 ? T : kEmpty, part_mm(pj, gr.len_mm[ej]), (int64_t)H(tll.x, tll.y), d0, 1,
-                             nullptr, nullptr, nullptr);
+  search_init<CAP, true, 1>(&L);
+  const bool ok = search_run<CAP, true, 1>(&L, gr, H, mode_bit, true, S, (uint32_t)bound_mm_of(a.bound[s]),
+                                           (uint32_t)(a.delta * 1000.0), lane == 0 ? T : kEmpty,
+                                           (uint32_t)part_mm(pj, gr.len_mm[ej]), H(tll.x, tll.y), (uint32_t)d0, 1,
+                                           nullptr, nullptr, nullptr);
   if (!ok) {
     if (lane == 0) a.overflow_flag[k] = 1;
     return;
