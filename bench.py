@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-ROUTE_KERNEL = 'k_route<128, 2>'  # first-tier search kernel (rocprofv3 name)
+ROUTE_KERNEL = 'k_route<160, 2>'  # first-tier search kernel (rocprofv3 name)
 # HBM bytes per ROUTE_KERNEL launch from the FETCH_SIZE / WRITE_SIZE passes of
 # tools/profile_gpu.sh (separate --pmc runs of this same command; tools/pmc_summary.py)
 PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r01_v8_pmc.json')
@@ -212,7 +212,10 @@ def main():
                        'parallelism': 'uuid-sharded dp%d + RCCL reduce-scatter of [hour][segment][speed] histogram'
                                       % world if world > 1 else 'single GPU',
                        'streams': ns,
-                       'stage_ms_per_stream': stage_ms},
+                       'stage_ms_per_stream': stage_ms,
+                       'work': {'states': int(sum(r.n_states for r in rs)), 'grid_cells': int(counters[0]),
+                                'shape_segments_tested': int(counters[1]), 'candidates': int(counters[2]),
+                                'output_segments': int(counters[7])}},
             'roofline': {'kernel': ROUTE_KERNEL + ' (K3 bounded one-to-many searches, 2 per wave + K4 transition)',
                          'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': traffic,

@@ -239,16 +239,31 @@ __global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
   if (i < n) p[i] = v;
 }
 
+// Append `value` to an unordered list, one global atomic per block (a single counter
+// takes ~3 ns per same-address atomic: per-wave appends of ~1M items cost ~0.5 ms).
+__device__ inline void block_append(bool hit, int64_t value, int64_t* list, unsigned long long* count) {
+  __shared__ unsigned int s_n;
+  __shared__ unsigned long long s_base;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  unsigned int my = 0;
+  if (hit) my = atomicAdd(&s_n, 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) s_base = s_n ? atomicAdd(count, (unsigned long long)s_n) : 0ull;
+  __syncthreads();
+  if (hit) list[s_base + my] = value;
+}
+
 __global__ void k_collect(int64_t n, const int32_t* flag, int64_t* list, unsigned long long* count) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && flag[i]) list[atomicAdd(count, 1ull)] = i;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  block_append(i < n && flag[i], i, list, count);
 }
 
 // states that need a path: a step inside a sub-path
 __global__ void k_step_list(int64_t n_states, const int64_t* prev, const uint8_t* brk, const int32_t* cand_count,
                             int64_t* list, unsigned long long* count) {
-  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < n_states && cand_count[s] > 0 && prev[s] >= 0 && !brk[s]) list[atomicAdd(count, 1ull)] = s;
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  block_append(s < n_states && cand_count[s] > 0 && prev[s] >= 0 && !brk[s], s, list, count);
 }
 
 static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
@@ -430,11 +445,11 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   ra.overflow_flag = task_ovf;
   if (NT > 0) {
     tb(OTR_STAGE_ROUTE);
-    // two searches per wave (CAP 128 tables); wider steps and overflows retry below
+    // two searches per wave (CAP 160 tables); wider steps and overflows retry below
     static const int route_g = getenv("OTR_ROUTE_G") ? atoi(getenv("OTR_ROUTE_G")) : 2;  // A/B knob
     if (route_g == 2) {
       const int64_t units = (NT + 1) / 2;
-      k_route<128, 2><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
+      k_route<160, 2><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
     } else {
       k_route<256, 1><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
     }
@@ -445,7 +460,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     tb(OTR_STAGE_ROUTE_BIG);
     for (int tier = 0; tier < 3; ++tier) {
       HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
-      k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
+      k_collect<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, list, cnt);
       unsigned long long novf = 0;
       HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
@@ -459,7 +474,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       else k_route<4096, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
       if (tier == 2) {
         HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
-        k_collect<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_ovf, list, cnt);
+        k_collect<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, list, cnt);
         HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
         out->n_overflow_traces += (int32_t)novf;
@@ -495,7 +510,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     // misc: [0] step count, [1] cap flag, [2] retry count, [8..8+64) shard cursors
     unsigned long long* cnt = need<unsigned long long>(S_MISC, 8 + kShards);
     HIPCHK(hipMemsetAsync(cnt, 0, 8 * (8 + kShards), stream));
-    if (S > 0) k_step_list<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, cnt);
+    if (S > 0) k_step_list<<<grid_for(S, 1024), 1024, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, cnt);
     unsigned long long nsteps = 0;
     HIPCHK(hipMemcpyAsync(&nsteps, cnt, 8, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
@@ -542,7 +557,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       tb(OTR_STAGE_PATHS_BIG);
       for (int tier = 0; tier < 3; ++tier) {
         HIPCHK(hipMemsetAsync(cnt + 2, 0, 8, stream));
-        k_collect<<<grid_for(nsteps, 256), 256, 0, stream>>>((int64_t)nsteps, step_ovf, rl, cnt + 2);
+        k_collect<<<grid_for(nsteps, 1024), 1024, 0, stream>>>((int64_t)nsteps, step_ovf, rl, cnt + 2);
         HIPCHK(hipMemcpyAsync(&nretry, cnt + 2, 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
         if (nretry == 0) break;

@@ -14,6 +14,8 @@
 // Every decision-path expression mirrors oracle/oracle.c operation for operation
 // (DESIGN.md §3); the tests compare the two bit for bit.
 #pragma once
+#include <type_traits>
+
 #include "otr_device.h"
 #include "otr_report.h"
 
@@ -430,8 +432,9 @@ struct SearchLds {
   typename LabelT<PRED>::T lab[CAP];  // label (| pred edge)
   uint32_t key[CAP];                  // node id | INQ bit, 0xFFFFFFFF empty
   uint32_t hv[CAP];                   // A* heuristic, mm
-  uint16_t pend[CAP];
-  uint16_t work[CAP];
+  using Idx = typename std::conditional<(CAP <= 256 && !PRED), uint8_t, uint16_t>::type;
+  Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
+  Idx work[CAP];
   int n_pend, n_keys, overflow;
 };
 
@@ -480,21 +483,27 @@ __device__ inline Heur make_heur(double plat, double plon, double r, double boun
 __device__ inline int64_t bound_mm_of(double bound) { return (int64_t)floor(bound * 1000.0); }
 __device__ inline int64_t part_mm(double frac, uint32_t len_mm) { return (int64_t)llround(frac * (double)len_mm); }
 
+// home slot: multiply-shift of the mixed id, so CAP need not be a power of two
+template <int CAP>
+__device__ inline uint32_t hslot(uint32_t node) {
+  return (uint32_t)(((unsigned long long)hmix(node) * (unsigned long long)CAP) >> 32);
+}
+
 template <int CAP, bool PRED>
 __device__ inline int lds_find(const SearchLds<CAP, PRED>& L, uint32_t node) {
-  uint32_t h = hmix(node) & (CAP - 1);
+  uint32_t h = hslot<CAP>(node);
   for (int probe = 0; probe < CAP; ++probe) {
     const uint32_t k = L.key[h];
     if (k == kEmpty) return -1;
     if ((k & ~kInq) == node) return (int)h;
-    h = (h + 1) & (CAP - 1);
+    h = h + 1 == (uint32_t)CAP ? 0u : h + 1;
   }
   return -1;
 }
 
 template <int CAP, bool PRED>
 __device__ inline int lds_insert(SearchLds<CAP, PRED>& L, uint32_t node, bool* isnew) {
-  uint32_t h = hmix(node) & (CAP - 1);
+  uint32_t h = hslot<CAP>(node);
   for (int probe = 0; probe < CAP; ++probe) {
     uint32_t k = L.key[h];
     if (k == kEmpty) {
@@ -510,7 +519,7 @@ __device__ inline int lds_insert(SearchLds<CAP, PRED>& L, uint32_t node, bool* i
       *isnew = false;
       return (int)h;
     }
-    h = (h + 1) & (CAP - 1);
+    h = h + 1 == (uint32_t)CAP ? 0u : h + 1;
   }
   L.overflow = 1;
   return -1;
@@ -583,7 +592,7 @@ __device__ inline void relax_one(SearchLds<CAP, PRED>& L, const Heur& H, uint32_
     const uint32_t ok = atomicOr(&L.key[sl], kInq);
     if (!(ok & kInq)) {
       const int p = atomicAdd(&L.n_pend, 1);
-      if (p < CAP) L.pend[p] = (uint16_t)sl;
+      if (p < CAP) L.pend[p] = (typename SearchLds<CAP, PRED>::Idx)sl;
       else L.overflow = 1;
     }
   }
@@ -612,7 +621,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
     L.hv[sl] = hroot;
     L.lab[sl] = LabelT<PRED>::make(0u, kEmpty);
     L.key[sl] |= kInq;
-    L.pend[0] = (uint16_t)sl;
+    L.pend[0] = (typename SearchLds<CAP, PRED>::Idx)sl;
     L.n_pend = 1;
   }
   __syncthreads();
@@ -661,7 +670,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
     for (int base = 0; base < npx; base += Gr::GL) {
       const int k = base + gl;
       const bool in = k < np;
-      uint16_t sl = 0;
+      int sl = 0;
       uint32_t f = 0;
       bool take = false;
       if (in) {
@@ -672,10 +681,10 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
       const unsigned long long mt = __ballot(take), mk = __ballot(in && !take);
       __syncthreads();
       if (take) {
-        L.work[nw + Gr::prefix(mt)] = sl;
+        L.work[nw + Gr::prefix(mt)] = (typename SearchLds<CAP, PRED>::Idx)sl;
         atomicAnd(&L.key[sl], ~kInq);
       } else if (in) {
-        L.pend[kept + Gr::prefix(mk)] = sl;
+        L.pend[kept + Gr::prefix(mk)] = (typename SearchLds<CAP, PRED>::Idx)sl;
         fnext = f < fnext ? f : fnext;
       }
       nw += Gr::count(mt);
@@ -940,15 +949,25 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
       if (!brk) {
         double best = __builtin_huge_val();
         if (lane < K) {
+          // 16 independent transition loads in flight per chunk, then the min-plus scan in
+          // ascending i (strict <: lowest index among equal minima)
           const double* tr = a.trans + a.trans_off[s];
-          for (int i = 0; i < Kp; ++i) {
-            const double ti = tr[(int64_t)i * K + lane];
-            const double ci = s_cost[i];
-            if (ti == __builtin_huge_val() || ci == __builtin_huge_val()) continue;
-            const double c = ci + ti;
-            if (c < best) {
-              best = c;
-              bi = i;
+          for (int i0 = 0; i0 < Kp; i0 += 16) {
+            double tv[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+              tv[u] = i0 + u < Kp ? tr[(int64_t)(i0 + u) * K + lane] : __builtin_huge_val();
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const double ti = tv[u];
+              if (ti == __builtin_huge_val()) continue;
+              const double ci = s_cost[i0 + u];
+              if (ci == __builtin_huge_val()) continue;
+              const double c = ci + ti;
+              if (c < best) {
+                best = c;
+                bi = i0 + u;
+              }
             }
           }
         }
