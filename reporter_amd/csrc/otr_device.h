@@ -55,6 +55,7 @@ struct DevGraph {
   const uint32_t* seg_len;
   const uint32_t* cell_row;
   const uint32_t* cell_edge;
+  const uint4* cell_rec;       // per cell entry {edge, shape begin, shape end, attr}: one 16-B load
   const uint4* edge_pack;      // {dst, len_mm, attr, 0}: one 16-B load per relaxed edge (CSR tail)
   const uint4* adj;            // 4 x uint4 per node: {dst | access<<28 | more<<31, len_mm, dst lat_e6, dst lon_e6}
   const uint32_t* len_mm;      // routing length, whole millimetres
@@ -114,6 +115,14 @@ __device__ inline int lane_id() { return (int)__lane_id(); }
 // neighbouring items (same trace / same step → same graph neighbourhood) share an L2.
 // Speed only; any placement gives the same results.  grid = 8 * per.
 __device__ inline int64_t xcd_remap(int64_t b, int64_t per) { return (b & 7) * per + (b >> 3); }
+
+// One 16-B load whose four words are all materialised here: keeps the compiler from
+// splitting a record load into dependent pieces sunk into the branches that use them.
+__device__ inline uint4 ld16(const uint4* p) {
+  uint4 r = *p;
+  asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w));
+  return r;
+}
 
 constexpr int kShards = 64;  // device counters are sharded [kind][64] to avoid one hot address
 constexpr uint32_t kAdjDstMask = 0x0FFFFFFFu;

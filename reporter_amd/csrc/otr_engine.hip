@@ -148,6 +148,15 @@ int engine_configure(const Config& cfg, std::string* err) {
       if (deg > 4) adj[4ull * u + 3].x |= kAdjMore;
     }
     g.adj = (const uint4*)upv(adj.data(), sizeof(uint4) * adj.size());
+    // candidate-search view: each grid-cell entry carries its edge's shape range and attributes
+    const uint32_t* cedge = (const uint32_t*)(base + h.array_offset[OTR_A_CELL_EDGE]);
+    const uint32_t* eshape = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_SHAPE]);
+    std::vector<uint4> crec(h.n_cell_entries + 1, make_uint4(0u, 0u, 0u, 0u));
+    for (uint64_t q = 0; q < h.n_cell_entries; ++q) {
+      const uint32_t e = cedge[q];
+      crec[q] = make_uint4(e, eshape[e], eshape[e + 1], attr[e]);
+    }
+    g.cell_rec = (const uint4*)upv(crec.data(), sizeof(uint4) * crec.size());
   }
   for (void* p : gs.allocs)
     if (!p) {

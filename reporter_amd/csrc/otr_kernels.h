@@ -75,13 +75,15 @@ __device__ inline bool cand_less(double da, uint32_t ea, double db, uint32_t eb)
 // Projection of probe (plat, plon) onto edge e's polyline in the probe-local metric;
 // true when the edge is a candidate owned by grid cell (r, c) (the cell holding the
 // snapped point), with squared distance d2 and fraction along the edge.
-__device__ inline bool project_edge(const DevGraph& g, uint32_t e, uint32_t mode_bit, double plat, double plon,
-                                    double mpl, double r2, int64_t r, int64_t c, double* d2_out, double* frac_out,
-                                    unsigned long long* tests) {
-  if (!(g.edge_attr[e] & mode_bit)) return false;
+// rec = the cell entry's {edge, first shape point, end shape point, attr} (DevGraph::cell_rec).
+// Returns the grid cell (sr, sc) of the snapped point through *sr/*sc.
+__device__ inline bool project_edge(const DevGraph& g, uint4 rec, uint32_t mode_bit, double plat, double plon,
+                                    double mpl, double r2, int64_t* sr_out, int64_t* sc_out, double* d2_out,
+                                    double* frac_out, unsigned long long* tests) {
+  if (!(rec.w & mode_bit)) return false;
   double best = __builtin_huge_val();
   double best_along = 0.0, bqx = 0.0, bqy = 0.0, acc = 0.0;
-  const uint32_t k0 = g.edge_shape[e], k1 = g.edge_shape[e + 1];
+  const uint32_t k0 = rec.y, k1 = rec.z;
   int2 pa = g.shape_ll[k0];
   for (uint32_t k = k0; k + 1 < k1; ++k) {
     const int2 pb = g.shape_ll[k + 1];
@@ -112,9 +114,8 @@ __device__ inline bool project_edge(const DevGraph& g, uint32_t e, uint32_t mode
   *tests += k1 - k0 - 1;
   if (!(best <= r2)) return false;
   const double slat = plat + bqy / kMetersPerDeg, slon = plon + bqx / mpl;
-  const int64_t sr = (int64_t)floor((slat - g.grid_min_lat) / g.grid_cell_deg);
-  const int64_t sc = (int64_t)floor((slon - g.grid_min_lon) / g.grid_cell_deg);
-  if (sr != r || sc != c) return false;
+  *sr_out = (int64_t)floor((slat - g.grid_min_lat) / g.grid_cell_deg);
+  *sc_out = (int64_t)floor((slon - g.grid_min_lon) / g.grid_cell_deg);
   *d2_out = best;
   *frac_out = acc > 0.0 ? best_along / acc : 0.0;
   return true;
@@ -122,12 +123,12 @@ __device__ inline bool project_edge(const DevGraph& g, uint32_t e, uint32_t mode
 
 constexpr int kWin = 16;  // flattened cell windows up to 16 x 16 cells
 
-__global__ __launch_bounds__(64) void k_candidates(DevGraph g, BatchDev b, ModeParams mp, int64_t n_states,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_candidates(DevGraph g, BatchDev b, ModeParams mp, int64_t n_states,
                                                    const int64_t* state_probe, const int32_t* state_trace,
                                                    CandBuf out, unsigned long long* counters) {
-  __shared__ double s_d2[2][2 * OTR_WAVE];
-  __shared__ double s_p[2][2 * OTR_WAVE];
-  __shared__ uint32_t s_e[2][2 * OTR_WAVE];
+  __shared__ double s_d2[2 * OTR_WAVE];  // candidate list (≤ kmax + 64 entries), one buffer:
+  __shared__ double s_p[2 * OTR_WAVE];   // compaction stages each lane's ≤ 2 entries in registers
+  __shared__ uint32_t s_e[2 * OTR_WAVE];
   __shared__ uint32_t s_bnd[kWin][kWin + 1];  // cell_row boundaries of the window, per row
   __shared__ uint32_t s_pre[kWin + 1];        // entries before each row
   const int lane = threadIdx.x;
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(64) void k_candidates(DevGraph g, BatchDev b, ModeP
   if (r1 > (int64_t)g.grid_rows - 1) r1 = (int64_t)g.grid_rows - 1;
   if (c1 > (int64_t)g.grid_cols - 1) c1 = (int64_t)g.grid_cols - 1;
   const double r2 = radius * radius;
-  int n = 0, buf = 0;
+  int n = 0;
   unsigned long long tests = 0;
   // merge one wave's worth of qualifying candidates into the LDS top-K list
   auto merge = [&](bool ok, double d2, double frac, uint32_t e) {
@@ -162,26 +163,38 @@ __global__ __launch_bounds__(64) void k_candidates(DevGraph g, BatchDev b, ModeP
     if (!mask) return;
     if (ok) {
       const int pos = n + prefix_count(mask);
-      s_d2[buf][pos] = d2;
-      s_p[buf][pos] = frac;
-      s_e[buf][pos] = e;
+      s_d2[pos] = d2;
+      s_p[pos] = frac;
+      s_e[pos] = e;
     }
     n += __popcll(mask);
     __syncthreads();
     if (n > kmax) {  // rank-compact to the kmax best (all (d2, edge) keys distinct)
-      for (int idx = lane; idx < n; idx += OTR_WAVE) {
-        const double d = s_d2[buf][idx];
-        const uint32_t ee = s_e[buf][idx];
-        int rank = 0;
-        for (int m = 0; m < n; ++m) rank += cand_less(s_d2[buf][m], s_e[buf][m], d, ee);
-        if (rank < kmax) {
-          s_d2[buf ^ 1][rank] = d;
-          s_p[buf ^ 1][rank] = s_p[buf][idx];
-          s_e[buf ^ 1][rank] = ee;
+      double dv[2], pv[2];
+      uint32_t ev[2];
+      int rk[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int idx = lane + h * OTR_WAVE;
+        rk[h] = OTR_KMAX * 2;
+        if (idx < n) {
+          dv[h] = s_d2[idx];
+          pv[h] = s_p[idx];
+          ev[h] = s_e[idx];
+          int rank = 0;
+          for (int m = 0; m < n; ++m) rank += cand_less(s_d2[m], s_e[m], dv[h], ev[h]);
+          rk[h] = rank;
         }
       }
       __syncthreads();
-      buf ^= 1;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (rk[h] < kmax) {
+          s_d2[rk[h]] = dv[h];
+          s_p[rk[h]] = pv[h];
+          s_e[rk[h]] = ev[h];
+        }
+      __syncthreads();
       n = kmax;
     }
   };
@@ -208,17 +221,21 @@ __global__ __launch_bounds__(64) void k_candidates(DevGraph g, BatchDev b, ModeP
       const uint32_t k = base + lane;
       bool ok = false;
       double d2 = 0, frac = 0;
-      uint32_t e = 0;
+      uint4 rec = make_uint4(0u, 0u, 0u, 0u);
       if (k < total) {
         int rr = 0;
         while (rr + 1 < nr && s_pre[rr + 1] <= k) ++rr;
         const uint32_t q = s_bnd[rr][0] + (k - s_pre[rr]);
-        int cc = 0;
-        while (cc + 1 < nc && s_bnd[rr][cc + 1] <= q) ++cc;
-        e = g.cell_edge[q];
-        ok = project_edge(g, e, mode_bit, plat, plon, mpl, r2, r0 + rr, c0 + cc, &d2, &frac, &tests);
+        rec = ld16(g.cell_rec + q);
+        int64_t sr, sc;
+        ok = project_edge(g, rec, mode_bit, plat, plon, mpl, r2, &sr, &sc, &d2, &frac, &tests);
+        // owned by the cell holding the snapped point: entry q lies in that cell's range
+        if (ok) {
+          const int64_t wr = sr - r0, wc = sc - c0;
+          ok = wr >= 0 && wr < nr && wc >= 0 && wc < nc && s_bnd[wr][wc] <= q && q < s_bnd[wr][wc + 1];
+        }
       }
-      merge(ok, d2, frac, e);
+      merge(ok, d2, frac, rec.x);
     }
   } else {
     for (int64_t r = r0; r <= r1; ++r)
@@ -229,24 +246,26 @@ __global__ __launch_bounds__(64) void k_candidates(DevGraph g, BatchDev b, ModeP
           const uint32_t q = base + lane;
           bool ok = false;
           double d2 = 0, frac = 0;
-          uint32_t e = 0;
+          uint4 rec = make_uint4(0u, 0u, 0u, 0u);
           if (q < end) {
-            e = g.cell_edge[q];
-            ok = project_edge(g, e, mode_bit, plat, plon, mpl, r2, r, c, &d2, &frac, &tests);
+            rec = ld16(g.cell_rec + q);
+            int64_t sr, sc;
+            ok = project_edge(g, rec, mode_bit, plat, plon, mpl, r2, &sr, &sc, &d2, &frac, &tests) && sr == r &&
+                 sc == c;
           }
-          merge(ok, d2, frac, e);
+          merge(ok, d2, frac, rec.x);
         }
       }
   }
   // final ordering
   const size_t o = (size_t)s * OTR_KMAX;
   for (int idx = lane; idx < n; idx += OTR_WAVE) {
-    const double d = s_d2[buf][idx];
-    const uint32_t ee = s_e[buf][idx];
+    const double d = s_d2[idx];
+    const uint32_t ee = s_e[idx];
     int rank = 0;
-    for (int m = 0; m < n; ++m) rank += cand_less(s_d2[buf][m], s_e[buf][m], d, ee);
+    for (int m = 0; m < n; ++m) rank += cand_less(s_d2[m], s_e[m], d, ee);
     out.edge[o + rank] = ee;
-    out.p[o + rank] = s_p[buf][idx];
+    out.p[o + rank] = s_p[idx];
     out.sqd[o + rank] = d;
   }
   if (lane == 0) {
@@ -348,14 +367,6 @@ __global__ void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* ca
 // (label << 32 | edge id) so the minimum also records the smallest-id predecessor
 // edge among those achieving the label (the oracle's predecessor rule).
 // ------------------------------------------------------------------------------
-// One 16-B load whose four words are all materialised here: keeps the compiler from
-// splitting a record load into dependent pieces sunk into the branches that use them.
-__device__ inline uint4 ld16(const uint4* p) {
-  uint4 r = *p;
-  asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w));
-  return r;
-}
-
 // Wave minimum by DPP row shifts and row broadcasts (GFX9), result read from lane 63.
 __device__ inline uint32_t wave_min_u32(uint32_t v) {
   const int I = -1;
@@ -505,15 +516,12 @@ template <int CAP, bool PRED>
 __device__ inline int lds_insert(SearchLds<CAP, PRED>& L, uint32_t node, bool* isnew) {
   uint32_t h = hslot<CAP>(node);
   for (int probe = 0; probe < CAP; ++probe) {
-    uint32_t k = L.key[h];
+    // CAS first: one LDS round trip both claims an empty slot and reads an occupied one
+    const uint32_t k = atomicCAS(&L.key[h], kEmpty, node);
     if (k == kEmpty) {
-      const uint32_t old = atomicCAS(&L.key[h], kEmpty, node);
-      if (old == kEmpty) {
-        atomicAdd(&L.n_keys, 1);  // load factor checked once per round (search_run)
-        *isnew = true;
-        return (int)h;
-      }
-      k = old;
+      atomicAdd(&L.n_keys, 1);  // load factor checked once per round (search_run)
+      *isnew = true;
+      return (int)h;
     }
     if ((k & ~kInq) == node) {
       *isnew = false;
