@@ -367,6 +367,17 @@ __global__ void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* ca
 // (label << 32 | edge id) so the minimum also records the smallest-id predecessor
 // edge among those achieving the label (the oracle's predecessor rule).
 // ------------------------------------------------------------------------------
+// Wave sum (mod 2^32) by DPP row shifts and row broadcasts, result read from lane 63.
+__device__ inline uint32_t wave_sum_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // Wave minimum by DPP row shifts and row broadcasts (GFX9), result read from lane 63.
 __device__ inline uint32_t wave_min_u32(uint32_t v) {
   const int I = -1;
@@ -379,12 +390,6 @@ __device__ inline uint32_t wave_min_u32(uint32_t v) {
   v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
-
-// 1: the next round's fmin is carried from partition/relax (every relaxation evaluates
-// the heuristic); 0: a pass over the pending list computes it (heuristic on insert only)
-#ifndef OTR_FMIN_CARRY
-#define OTR_FMIN_CARRY 1
-#endif
 
 // G independent searches per wave, GL = 64 / G lanes each (G = 1 or 2).  Per-group
 // ballots, prefix counts, minima and wave-uniform loop bounds.
@@ -444,8 +449,9 @@ struct SearchLds {
   uint32_t key[CAP];                  // node id | INQ bit, 0xFFFFFFFF empty
   uint32_t hv[CAP];                   // A* heuristic, mm
   using Idx = typename std::conditional<(CAP <= 256 && !PRED), uint8_t, uint16_t>::type;
+  static constexpr int WCAP = CAP <= 160 ? 48 : CAP / 4;  // nodes settled per round (at most)
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
-  Idx work[CAP];
+  uint2 work[WCAP];                   // this round's settled nodes: {node, label}
   int n_pend, n_keys, overflow;
 };
 
@@ -572,38 +578,27 @@ __device__ inline bool target_resolved(const SearchLds<CAP, PRED>& L, int tslot,
 // f = label + h is known without reading an hv entry another lane may be writing; the
 // round's minimum over improvements and kept pending nodes is the next round's fmin.
 template <int CAP, bool PRED>
-__device__ inline void relax_one(SearchLds<CAP, PRED>& L, const Heur& H, uint32_t dw, uint32_t len_mm, int32_t vlat,
-                                 int32_t vlon, uint32_t du, uint32_t edge, uint32_t bound_mm, uint32_t mode_bit,
-                                 uint32_t& relaxed, uint32_t& fnext) {
-  if (!(((dw >> 28) & 7u) & mode_bit)) return;
+__device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, uint32_t dw, uint32_t len_mm, int32_t vlat,
+                                int32_t vlon, uint32_t du, uint32_t edge, uint32_t bound_mm, uint32_t mode_bit,
+                                uint32_t& relaxed, uint32_t& fnext) {
+  if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
   const uint64_t nd = (uint64_t)du + len_mm;
-  if (nd > bound_mm) return;
-#if OTR_FMIN_CARRY
+  if (nd > bound_mm) return -1;
   const uint32_t h = H(vlat, vlon);
-#endif
   bool isnew = false;
   const int sl = lds_insert(L, dw & kAdjDstMask, &isnew);
-  if (sl < 0) return;
-#if OTR_FMIN_CARRY
+  if (sl < 0) return -1;
   if (isnew) L.hv[sl] = h;
-#else
-  if (isnew) L.hv[sl] = H(vlat, vlon);
-#endif
   const typename LabelT<PRED>::T nb = LabelT<PRED>::make((uint32_t)nd, edge);
   const typename LabelT<PRED>::T old = atomicMin(&L.lab[sl], nb);
   if (LabelT<PRED>::label(nb) < LabelT<PRED>::label(old)) {
-#if OTR_FMIN_CARRY
     const uint32_t f = (uint32_t)nd + h;
     fnext = f < fnext ? f : fnext;
-#endif
     const uint32_t ok = atomicOr(&L.key[sl], kInq);
-    if (!(ok & kInq)) {
-      const int p = atomicAdd(&L.n_pend, 1);
-      if (p < CAP) L.pend[p] = (typename SearchLds<CAP, PRED>::Idx)sl;
-      else L.overflow = 1;
-    }
+    if (!(ok & kInq)) return sl;  // newly pending: the caller appends it
   }
+  return -1;
 }
 
 // G searches per wave, one per lane group, each in its own table Ls[g]: search g is
@@ -623,14 +618,15 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
   SearchLds<CAP, PRED>& L = Ls[Gr::g()];
   const int2 sll = g.node_ll[active ? start : 0u];
   const uint32_t hroot = H(sll.x, sll.y);
+  using Idx = typename SearchLds<CAP, PRED>::Idx;
+  constexpr int WCAP = SearchLds<CAP, PRED>::WCAP;
   if (active && gl == 0) {
     bool isnew;
     const int sl = lds_insert(L, start, &isnew);
     L.hv[sl] = hroot;
     L.lab[sl] = LabelT<PRED>::make(0u, kEmpty);
     L.key[sl] |= kInq;
-    L.pend[0] = (typename SearchLds<CAP, PRED>::Idx)sl;
-    L.n_pend = 1;
+    L.pend[0] = (Idx)sl;
   }
   __syncthreads();
   // targets are pre-inserted (no label) so every round reads their label from a known slot
@@ -645,24 +641,10 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
   unsigned long long cyc[4] = {0, 0, 0, 0};
   uint32_t fmin = hroot;  // 0xFFFFFFFF: nothing pending
   bool done = !active;
+  int npend = active ? 1 : 0;  // pending-list length (group-uniform register)
   for (;;) {
     OTR_STAMP(t0);
-    const int np = done ? 0 : L.n_pend;
-#if !OTR_FMIN_CARRY
-    {  // fmin = minimum key over the pending list
-      uint32_t fm = 0xFFFFFFFFu;
-      const int npx0 = Gr::umax(np);
-      for (int base = 0; base < npx0; base += Gr::GL) {
-        const int k = base + gl;
-        if (k < np) {
-          const int sl = L.pend[k];
-          const uint32_t f = LabelT<PRED>::label(L.lab[sl]) + L.hv[sl];
-          fm = f < fm ? f : fm;
-        }
-      }
-      fmin = Gr::min_u32(fm);
-    }
-#endif
+    const int np = done ? 0 : npend;
     OTR_STAMP(t1);
     const bool res = done || gl >= n_tgt || target_resolved(L, tslot, tpart, hT, d0min, bound_mm, fmin, np == 0);
     done = done || Gr::mine(__ballot(!res)) == 0ull || np == 0;
@@ -679,60 +661,90 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
       const int k = base + gl;
       const bool in = k < np;
       int sl = 0;
-      uint32_t f = 0;
+      uint32_t f = 0, lb = 0, node = 0;
       bool take = false;
       if (in) {
         sl = L.pend[k];
-        f = LabelT<PRED>::label(L.lab[sl]) + L.hv[sl];  // < 2^32: labels, h < 2^31
+        lb = LabelT<PRED>::label(L.lab[sl]);
+        node = L.key[sl] & ~kInq;
+        f = lb + L.hv[sl];  // < 2^32: labels, h < 2^31
         take = f < theta;
       }
+      // at most WCAP settles per round; the rest stay pending (order only, never labels)
+      take = take && nw + Gr::prefix(__ballot(take)) < WCAP;
       const unsigned long long mt = __ballot(take), mk = __ballot(in && !take);
       __syncthreads();
       if (take) {
-        L.work[nw + Gr::prefix(mt)] = (typename SearchLds<CAP, PRED>::Idx)sl;
+        L.work[nw + Gr::prefix(mt)] = make_uint2(node, lb);
         atomicAnd(&L.key[sl], ~kInq);
       } else if (in) {
-        L.pend[kept + Gr::prefix(mk)] = (typename SearchLds<CAP, PRED>::Idx)sl;
+        L.pend[kept + Gr::prefix(mk)] = (Idx)sl;
         fnext = f < fnext ? f : fnext;
       }
       nw += Gr::count(mt);
       kept += Gr::count(mk);
       __syncthreads();
     }
-    if (!done && gl == 0) L.n_pend = kept;
-    __syncthreads();
+    npend = kept;
     OTR_STAMP(t3);
     cyc[2] += t3 - t2;
     // relax: lane = (work node, adjacency slot), so a round's dependent chain is a single
     // relaxation; slot 3 of a node with more than 4 out-edges also walks the CSR tail
     const int nwx = Gr::umax(4 * nw);
+    bool tail = false;
     for (int base = 0; base < nwx; base += Gr::GL) {
       const int k = base + gl;
+      int psl = -1;
       if (k < 4 * nw) {
-        const int ws = L.work[k >> 2];
+        const uint2 wk = L.work[k >> 2];
         const int slot = k & 3;
-        const uint32_t u = L.key[ws] & ~kInq;
-        const uint32_t du = LabelT<PRED>::label(L.lab[ws]);
         if (slot == 0) ++my_settled;
-        const uint4 r = ld16(g.adj + 4 * (size_t)u + slot);
-        const uint32_t e0 = PRED ? g.node_row[u] : 0u;  // edge id = CSR row start + slot
-        relax_one(L, H, r.x & ~kAdjMore, r.y, (int32_t)r.z, (int32_t)r.w, du, e0 + slot, bound_mm, mode_bit,
-                  my_relaxed, fnext);
-        if (slot == 3 && (r.x & kAdjMore))
-          for (uint32_t e = g.node_row[u] + 4; e < g.node_row[u + 1]; ++e) {
-            const uint4 pk = ld16(g.edge_pack + e);
-            const int2 vll = g.node_ll[pk.x];
-            relax_one(L, H, pk.x | ((pk.z & 7u) << 28), pk.y, vll.x, vll.y, du, e, bound_mm, mode_bit, my_relaxed,
-                      fnext);
-          }
+        const uint4 r = ld16(g.adj + 4 * (size_t)wk.x + slot);
+        const uint32_t e0 = PRED ? g.node_row[wk.x] : 0u;  // edge id = CSR row start + slot
+        psl = relax_one(L, H, r.x & ~kAdjMore, r.y, (int32_t)r.z, (int32_t)r.w, wk.y, e0 + slot, bound_mm,
+                        mode_bit, my_relaxed, fnext);
+        tail = tail || (slot == 3 && (r.x & kAdjMore));
       }
+      // append newly pending nodes by ballot (no shared counter)
+      const unsigned long long mp = __ballot(psl >= 0);
+      if (psl >= 0) {
+        const int p = npend + Gr::prefix(mp);
+        if (p < CAP) L.pend[p] = (Idx)psl;
+        else L.overflow = 1;
+      }
+      npend += Gr::count(mp);
+    }
+    if (__ballot(tail) != 0ull) {
+      // rare: slot 3 of a node with more than 4 out-edges walks the CSR tail; appends
+      // through the shared counter
+      if (gl == 0) L.n_pend = npend;
+      __syncthreads();
+      for (int base = 0; base < nwx; base += Gr::GL) {
+        const int k = base + gl;
+        if (k < 4 * nw && (k & 3) == 3) {
+          const uint2 wk = L.work[k >> 2];
+          if (g.adj[4 * (size_t)wk.x + 3].x & kAdjMore)
+            for (uint32_t e = g.node_row[wk.x] + 4; e < g.node_row[wk.x + 1]; ++e) {
+              const uint4 pk = ld16(g.edge_pack + e);
+              const int2 vll = g.node_ll[pk.x];
+              const int psl = relax_one(L, H, pk.x | ((pk.z & 7u) << 28), pk.y, vll.x, vll.y, wk.y, e, bound_mm,
+                                        mode_bit, my_relaxed, fnext);
+              if (psl >= 0) {
+                const int p = atomicAdd(&L.n_pend, 1);
+                if (p < CAP) L.pend[p] = (Idx)psl;
+                else L.overflow = 1;
+              }
+            }
+        }
+      }
+      __syncthreads();
+      npend = L.n_pend;
+      if (npend > CAP) npend = CAP;
     }
     __syncthreads();
     OTR_STAMP(t4);
     cyc[3] += t4 - t3;
-#if OTR_FMIN_CARRY
     fmin = Gr::min_u32(fnext);
-#endif
     if (!done && (L.overflow || L.n_keys > kMaxKeys)) done = true;
     __syncthreads();
     if (done && active && gl == 0 && L.n_keys > kMaxKeys) L.overflow = 1;
@@ -871,23 +883,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   }
   if (have && !ok && !forced && lane == 0) a.overflow_flag[task] = 1;
   if (counters) {
-    // per-group table statistics; wave totals on lane 0
+    // wave totals: lane sums by DPP, per-group values read from each group's lane 0
+    settled = wave_sum_u32((uint32_t)settled);
+    relaxed = wave_sum_u32((uint32_t)relaxed);
+    rounds = wave_sum_u32((uint32_t)rounds);
     const int nk = have && search ? L.n_keys : 0;
-    unsigned long long kk = lane == 0 ? (unsigned long long)nk : 0ull;
-    unsigned long long c96 = (lane == 0 && nk > 96) ? 1ull : 0ull, c64 = (lane == 0 && nk > 64) ? 1ull : 0ull,
-                       c128 = (lane == 0 && nk > 128) ? 1ull : 0ull;
-    unsigned long long kb = (lane == 0 && have) ? (unsigned long long)Kb : 0ull,
-                       ns = (lane == 0 && have) ? (unsigned long long)__popcll(a.task_mask[task]) : 0ull;
-    for (int off = 32; off > 0; off >>= 1) {
-      settled += __shfl_xor(settled, off);
-      relaxed += __shfl_xor(relaxed, off);
-      rounds += __shfl_xor(rounds, off);
-      kk += __shfl_xor(kk, off);
-      c96 += __shfl_xor(c96, off);
-      c64 += __shfl_xor(c64, off);
-      c128 += __shfl_xor(c128, off);
-      kb += __shfl_xor(kb, off);
-      ns += __shfl_xor(ns, off);
+    const int nsrc = have ? __popcll(a.task_mask[task]) : 0;
+    unsigned long long kk = 0, c96 = 0, c64 = 0, c128 = 0, kb = 0, ns = 0;
+    for (int q = 0; q < G; ++q) {
+      const int nkq = __builtin_amdgcn_readlane(nk, q * Gr::GL);
+      kk += (unsigned long long)nkq;
+      c96 += nkq > 96;
+      c64 += nkq > 64;
+      c128 += nkq > 128;
+      kb += (unsigned long long)__builtin_amdgcn_readlane(have ? Kb : 0, q * Gr::GL);
+      ns += (unsigned long long)__builtin_amdgcn_readlane(nsrc, q * Gr::GL);
     }
     if (threadIdx.x == 0) {
       const int sh = blockIdx.x & (kShards - 1);
