@@ -116,7 +116,15 @@ int engine_configure(const Config& cfg, std::string* err) {
     const float* lenf = (const float*)(base + h.array_offset[OTR_A_EDGE_LEN]);
     const uint32_t* attr = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_ATTR]);
     std::vector<uint32_t> len(h.n_edges + 1, 0u);
-    for (uint32_t e = 0; e < h.n_edges; ++e) len[e] = (uint32_t)llround((double)lenf[e] * 1000.0);
+    for (uint32_t e = 0; e < h.n_edges; ++e) {
+      const double mm = (double)lenf[e] * 1000.0;
+      if (!(mm >= 0.0 && mm < 2.0e9)) {  // uint32 label arithmetic
+        munmap(map, (size_t)st.st_size);
+        if (err) *err = "graph edge length outside [0, 2000 km)";
+        return OTR_BAD_REQUEST;
+      }
+      len[e] = (uint32_t)llround(mm);
+    }
     std::vector<uint4> pack(h.n_edges + 1);
     for (uint32_t e = 0; e < h.n_edges; ++e) pack[e] = make_uint4(dst[e], len[e], attr[e], 0u);
     auto upv = [&](const void* src, size_t bytes) -> void* {

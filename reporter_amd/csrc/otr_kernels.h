@@ -500,10 +500,11 @@ __device__ inline Heur make_heur(double plat, double plon, double r, double boun
 __device__ inline int64_t bound_mm_of(double bound) { return (int64_t)floor(bound * 1000.0); }
 __device__ inline int64_t part_mm(double frac, uint32_t len_mm) { return (int64_t)llround(frac * (double)len_mm); }
 
-// home slot: multiply-shift of the mixed id, so CAP need not be a power of two
+// home slot: Fibonacci hashing (the ids of one search are spatially clustered, nearly
+// consecutive) scaled to CAP by a high multiply, so CAP need not be a power of two
 template <int CAP>
 __device__ inline uint32_t hslot(uint32_t node) {
-  return (uint32_t)(((unsigned long long)hmix(node) * (unsigned long long)CAP) >> 32);
+  return __umulhi(node * 0x9E3779B1u, (uint32_t)CAP);
 }
 
 template <int CAP, bool PRED>
@@ -583,7 +584,7 @@ __device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, uint32_t
                                 uint32_t& relaxed, uint32_t& fnext) {
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
-  const uint64_t nd = (uint64_t)du + len_mm;
+  const uint32_t nd = du + len_mm;  // du <= bound < 2^31, len_mm < 2^31: no wrap
   if (nd > bound_mm) return -1;
   const uint32_t h = H(vlat, vlon);
   bool isnew = false;
@@ -593,7 +594,7 @@ __device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, uint32_t
   const typename LabelT<PRED>::T nb = LabelT<PRED>::make((uint32_t)nd, edge);
   const typename LabelT<PRED>::T old = atomicMin(&L.lab[sl], nb);
   if (LabelT<PRED>::label(nb) < LabelT<PRED>::label(old)) {
-    const uint32_t f = (uint32_t)nd + h;
+    const uint32_t f = nd + h;
     fnext = f < fnext ? f : fnext;
     const uint32_t ok = atomicOr(&L.key[sl], kInq);
     if (!(ok & kInq)) return sl;  // newly pending: the caller appends it
