@@ -93,9 +93,21 @@ def build_oracle(force=False):
     return os.path.join(ROOT, 'oracle', 'liboracle.so')
 
 
+def build_calib(force=False):
+    """tools/calib_fetch: known-byte access shapes for calibrating FETCH_SIZE/WRITE_SIZE
+    (profiling infrastructure, run by tools/profile_gpu.sh)."""
+    src = os.path.join(PKG, 'tools', 'calib_fetch.hip')
+    exe = os.path.join(PKG, 'tools', 'calib_fetch')
+    if force or not _newer(exe, [src]):
+        rdir, rname = hip_runtime_dir()
+        _run([HIPCC] + HIP_FLAGS + ['-o', exe, src, '-Wl,-rpath,' + rdir])
+    return exe
+
+
 def build_all(force=False):
     build_gen(force)
     build_oracle(force)
+    build_calib(force)
     return build_otr(force)
 
 
