@@ -64,6 +64,24 @@ int otr_report_segments(const char* match_json, size_t match_len, const char* tr
                         int threshold_sec, const int32_t* report_levels, int n_report_levels,
                         const int32_t* transition_levels, int n_transition_levels, char** out, size_t* out_len);
 
+/* n POST /report bodies at once (the reference serves one per HTTP request,
+ * reporter_service.py:209-245; a batching caller such as BatchingProcessor.java:58-141
+ * holds many).  Bodies are scanned on host threads, grouped by the options that must
+ * be uniform within a device batch (report/transition levels, match_options
+ * overrides) and matched in shared device batches.  codes[i] / outs[i] / out_lens[i]
+ * are exactly what otr_report returns for bodies[i] (release each outs[i] with
+ * otr_free).  Returns OTR_OK once every item has its code. */
+int otr_report_batch(otr_matcher* m, int32_t n, const char* const* bodies, const size_t* lens, int threshold_sec,
+                     int32_t* codes, char** outs, size_t* out_lens);
+
+/* Process-wide request coalescing (SURVEY §8b threading row): while enabled,
+ * otr_report calls from any number of threads are handed to one dispatcher thread
+ * that runs them as shared device batches of up to max_traces, waiting at most
+ * max_wait_us after the first queued request.  Each caller still blocks until its
+ * own response is ready and receives exactly what the uncoalesced call returns.
+ * max_traces <= 0 drains the queue and stops the dispatcher. */
+int otr_coalesce(int32_t max_traces, int32_t max_wait_us);
+
 void otr_free(char* p);
 const char* otr_last_error(void);
 
@@ -93,6 +111,7 @@ typedef struct otr_trace_batch {
 
 #define OTR_BATCH_COPY_OUT 1   /* fill the host arrays of otr_batch_result */
 #define OTR_BATCH_TIMING 2     /* record per-kernel HIP-event timings */
+#define OTR_BATCH_COPY_REPORTS 4  /* host copies of segments, reports, stats only (the JSON path) */
 
 #define OTR_NO_ID 0xFFFFFFFFFFFFFFFFull
 
@@ -137,6 +156,8 @@ typedef struct otr_batch_result {
                                   12 source candidates, 13 search rounds,
                                   16-19 diagnostic-build search phase cycles */
   float kernel_ms[16];         /* OTR_BATCH_TIMING: device time per stage, OTR_STAGE_* */
+  int32_t* trace_status;       /* host, per trace (with COPY_OUT / COPY_REPORTS): OTR_OK, or
+                                  OTR_MATCH_ERROR when its search outgrew the largest LDS table */
 } otr_batch_result;
 
 int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result* out);

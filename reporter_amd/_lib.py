@@ -15,6 +15,7 @@ OTR_MEM_HOST = 0
 OTR_MEM_DEVICE = 1
 OTR_BATCH_COPY_OUT = 1
 OTR_BATCH_TIMING = 2
+OTR_BATCH_COPY_REPORTS = 4
 OTR_NO_ID = 0xFFFFFFFFFFFFFFFF
 HIST_BINS = 8
 KMAX = 64
@@ -24,7 +25,7 @@ STAGES = ['states', 'candidates', 'link', 'route', 'route_big', 'viterbi', 'path
 # every symbol include/otr.h declares
 EXPORTS = ['otr_configure', 'otr_configure_json', 'otr_matcher_new', 'otr_matcher_free', 'otr_match',
            'otr_report', 'otr_report_segments', 'otr_free', 'otr_last_error', 'otr_match_batch',
-           'otr_graph_info', 'otr_matcher_stream', 'otr_device']
+           'otr_graph_info', 'otr_matcher_stream', 'otr_device', 'otr_report_batch', 'otr_coalesce']
 
 
 class TraceBatch(ctypes.Structure):
@@ -57,7 +58,8 @@ class BatchResult(ctypes.Structure):
                 ('rep_length', P(ctypes.c_int32)), ('rep_queue', P(ctypes.c_int32)),
                 ('shape_used', P(ctypes.c_int32)), ('stats', P(ctypes.c_int32)),
                 ('stats_len', P(ctypes.c_double)), ('d_hist', ctypes.c_void_p), ('hist_len', ctypes.c_int64),
-                ('counters', ctypes.c_uint64 * 24), ('kernel_ms', ctypes.c_float * 16)]
+                ('counters', ctypes.c_uint64 * 24), ('kernel_ms', ctypes.c_float * 16),
+                ('trace_status', P(ctypes.c_int32))]
 
 
 _L = None
@@ -94,6 +96,9 @@ def lib():
     L.otr_graph_info.argtypes = [P(ctypes.c_int64), P(ctypes.c_int64), P(ctypes.c_int64)]
     L.otr_matcher_stream.argtypes = [ctypes.c_void_p]
     L.otr_matcher_stream.restype = ctypes.c_void_p
+    L.otr_report_batch.argtypes = [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_char_p), P(ctypes.c_size_t),
+                                   ctypes.c_int, P(ctypes.c_int32), P(ctypes.c_void_p), P(ctypes.c_size_t)]
+    L.otr_coalesce.argtypes = [ctypes.c_int32, ctypes.c_int32]
     _L = L
     return L
 

@@ -62,7 +62,7 @@ def build_otr(force=False, stamps=False, variant=None, defines=()):
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
     headers += [os.path.join(ROOT, 'include', f) for f in os.listdir(os.path.join(ROOT, 'include'))]
     objs = []
-    for src in ('otr_engine.hip', 'otr_api.cpp'):
+    for src in ('otr_engine.hip', 'otr_api.cpp', 'otr_service.cpp'):
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, src + suffix + '.o')
         objs.append(o)

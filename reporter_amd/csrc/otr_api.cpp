@@ -12,7 +12,9 @@
 #include "../../include/otr.h"
 #include "otr_engine.h"
 #include "otr_json.h"
+#include "otr_format.h"
 #include "otr_report.h"
+#include "otr_service.h"
 
 using otrjson::Value;
 
@@ -38,12 +40,6 @@ int fail(int code, const std::string& msg, char** out, size_t* out_len) {
   std::string body = "{\"error\":\"" + msg + "\"}";  // reporter_service.py:214-245 builds it the same way
   if (out) dup_out(body, out, out_len);
   return code;
-}
-
-int mode_index(const std::string& m) {
-  if (m == "bicycle") return 1;
-  if (m == "pedestrian" || m == "foot") return 2;
-  return 0;  // auto and the other motor modes share auto access
 }
 
 void apply_options(otr::MatchParams* p, const Value* o) {
@@ -96,158 +92,28 @@ int parse_config(const Value& root, otr::Config* cfg, std::string* err) {
   return OTR_OK;
 }
 
-uint32_t levels_mask(const Value* arr) {
-  uint32_t m = 0;
-  if (!arr) return 0;
-  for (auto& v : arr->arr)
-    if (v->kind == Value::Number) {
-      int64_t l = v->as_int();
-      if (l >= 0 && l < 32) m |= 1u << l;
-    }
-  return m;
-}
-
 int threshold_default(int t) {
   if (t >= 0) return t;
   const char* e = getenv("THRESHOLD_SEC");  // reporter_service.py:55-58
   return (e && *e) ? atoi(e) : 15;
 }
 
-struct SingleTrace {
-  std::vector<int64_t> off{0, 0};
-  std::vector<double> lat, lon;
-  std::vector<int64_t> time;
-  std::vector<float> acc;
-  uint8_t mode = 0;
-  bool any_acc = false;
-};
-
-// trace JSON (Batch.java:56-65, simple_reporter.py:164) → SoA; options into mp
-int load_trace(const Value& tr, SingleTrace* st, otr::ModeParams* mp, std::string* err) {
-  const Value* pts = tr.get("trace");
-  if (!pts || pts->kind != Value::Array) {
-    *err = "trace must be a non zero length array of object each of which must have at least lat, lon and time";
-    return OTR_BAD_REQUEST;
+// one request through the shared JSON path (coalesced across threads when enabled)
+int run_item(otr_matcher* m, const char* json, size_t len, int threshold, bool report, char** out,
+             size_t* out_len) {
+  otrsvc::Item it;
+  it.body = json;
+  it.len = json ? len : 0;
+  it.threshold = threshold;
+  it.report = report;
+  if (report && otrsvc::coalesce_enabled()) otrsvc::coalesce_submit(m->m, &it);
+  else otrsvc::process(m->m, {&it});
+  if (it.code != 200 && it.code != OTR_OK) {
+    const size_t a = it.out.find(":\""), b = it.out.rfind('"');
+    g_last_error = (a != std::string::npos && b > a + 2) ? it.out.substr(a + 2, b - a - 2) : it.out;
   }
-  for (auto& p : pts->arr) {
-    const Value* la = p->get("lat");
-    const Value* lo = p->get("lon");
-    const Value* tm = p->get("time");
-    if (!la || !lo || !tm || la->kind != Value::Number || lo->kind != Value::Number || tm->kind != Value::Number) {
-      *err = "trace must be a non zero length array of object each of which must have at least lat, lon and time";
-      return OTR_BAD_REQUEST;
-    }
-    st->lat.push_back(la->as_double());
-    st->lon.push_back(lo->as_double());
-    st->time.push_back(tm->is_int ? tm->i : (int64_t)std::floor(tm->num));
-    const Value* a = p->get("accuracy");
-    if (a && a->kind == Value::Number) {
-      st->acc.push_back((float)a->as_double());
-      st->any_acc = true;
-    } else {
-      st->acc.push_back(-1.f);
-    }
-  }
-  st->off[1] = (int64_t)st->lat.size();
-  *mp = otr::graph_state().defaults;
-  const Value* mo = tr.get("match_options");
-  std::string mode = "auto";
-  if (mo) {
-    const Value* m = mo->get("mode");
-    if (m && m->kind == Value::String) mode = m->str;
-  }
-  st->mode = (uint8_t)mode_index(mode);
-  otr::MatchParams& P = mp->m[st->mode];
-  apply_options(&P, mo);
-  otr::finalize_params(&P);
-  return OTR_OK;
-}
-
-void put_segments(std::string& o, const otr_batch_result& r) {
-  o += "[";
-  for (int64_t k = 0; k < r.n_seg; ++k) {
-    if (k) o += ",";
-    o += "{";
-    if (r.seg_id[k] != OTR_NO_ID) o += "\"segment_id\":" + std::to_string((unsigned long long)r.seg_id[k]) + ",";
-    o += "\"way_ids\":[";
-    for (int64_t w = r.seg_way_off[k]; w < r.seg_way_off[k + 1]; ++w) {
-      if (w != r.seg_way_off[k]) o += ",";
-      o += std::to_string(r.seg_way[w]);
-    }
-    o += "],\"start_time\":";
-    if (r.seg_start[k] == -1.0) o += "-1"; else otrjson::put_double(o, r.seg_start[k]);
-    o += ",\"end_time\":";
-    if (r.seg_end[k] == -1.0) o += "-1"; else otrjson::put_double(o, r.seg_end[k]);
-    o += ",\"queue_length\":" + std::to_string(r.seg_queue[k]);
-    o += ",\"length\":" + std::to_string(r.seg_length[k]);
-    o += std::string(",\"internal\":") + (r.seg_internal[k] ? "true" : "false");
-    o += ",\"begin_shape_index\":" + std::to_string(r.seg_begin_shape[k]);
-    o += ",\"end_shape_index\":" + std::to_string(r.seg_end_shape[k]);
-    o += "}";
-  }
-  o += "]";
-}
-
-void put_stats(std::string& o, const int32_t* c, const double* len, const int32_t* len_set) {
-  auto L = [&](int i) {
-    if (len_set[i]) otrjson::put_double(o, len[i]);
-    else o += "0";
-  };
-  o += "\"stats\":{\"successful_matches\":{\"count\":" + std::to_string(c[0]) + ",\"length\":";
-  L(0);
-  o += "},\"unreported_matches\":{\"count\":" + std::to_string(c[1]) + ",\"length\":";
-  L(1);
-  o += "},\"match_errors\":{\"discontinuities\":" + std::to_string(c[2]) + ",\"invalid_speeds\":" +
-       std::to_string(c[3]) + ",\"invalid_times\":" + std::to_string(c[4]) + "},\"unassociated_segments\":" +
-       std::to_string(c[5]) + "}";
-}
-
-void put_reports(std::string& o, int64_t n, const unsigned long long* id, const unsigned long long* nx,
-                 const double* t0, const double* t1, const int32_t* len, const int32_t* q) {
-  o += "\"datastore\":{\"mode\":\"auto\",\"reports\":[";
-  for (int64_t k = 0; k < n; ++k) {
-    if (k) o += ",";
-    o += "{\"id\":" + std::to_string(id[k]) + ",\"t0\":";
-    otrjson::put_double(o, t0[k]);
-    o += ",\"t1\":";
-    otrjson::put_double(o, t1[k]);
-    o += ",\"length\":" + std::to_string(len[k]) + ",\"queue_length\":" + std::to_string(q[k]);
-    if (nx[k] != OTR_NO_ID) o += ",\"next_id\":" + std::to_string(nx[k]);
-    o += "}";
-  }
-  o += "]}";
-}
-
-int run_single(otr_matcher* m, const Value& tr, uint32_t rl, uint32_t tl, int threshold, otr_batch_result* res,
-               std::string* err) {
-  SingleTrace st;
-  otr::ModeParams mp;
-  int rc = load_trace(tr, &st, &mp, err);
-  if (rc) return rc;
-  otr_trace_batch b{};
-  b.n_traces = 1;
-  b.memory = OTR_MEM_HOST;
-  b.trace_offsets = st.off.data();
-  b.lat = st.lat.data();
-  b.lon = st.lon.data();
-  b.time = st.time.data();
-  b.accuracy = st.any_acc ? st.acc.data() : nullptr;
-  b.mode = &st.mode;
-  b.report_levels = rl;
-  b.transition_levels = tl;
-  b.threshold_sec = threshold;
-  b.quantisation = 3600;
-  b.flags = OTR_BATCH_COPY_OUT;
-  if (st.lat.empty()) {
-    memset(res, 0, sizeof(*res));
-    return OTR_OK;
-  }
-  rc = m->m.run(&b, mp, res, err);
-  if (rc == OTR_OK && res->status != OTR_OK) {
-    *err = "route search exceeded the device table";
-    return OTR_MATCH_ERROR;
-  }
-  return rc;
+  dup_out(it.out, out, out_len);
+  return it.code;
 }
 
 }  // namespace
@@ -309,66 +175,42 @@ int otr_graph_info(int64_t* n_nodes, int64_t* n_edges, int64_t* n_segments) {
 // SegmentMatcher.Match(json) -> str: reporter_service.py:240, simple_reporter.py:166
 int otr_match(otr_matcher* m, const char* json, size_t len, char** out, size_t* out_len) {
   if (!m) return fail(OTR_MATCH_ERROR, "null matcher", out, out_len);
-  std::string perr;
-  otrjson::Parser ps(json, len);
-  otrjson::Ptr tr = ps.parse(&perr);
-  if (!tr || tr->kind != Value::Object) return fail(OTR_MATCH_ERROR, perr, out, out_len);
-  otr_batch_result res;
-  std::string err;
-  int rc = run_single(m, *tr, 0, 0, 15, &res, &err);
-  if (rc != OTR_OK) return fail(rc == OTR_BAD_REQUEST ? OTR_MATCH_ERROR : rc, err, out, out_len);
-  std::string o = "{\"segments\":";
-  put_segments(o, res);
-  o += "}";
-  dup_out(o, out, out_len);
-  return OTR_OK;
+  return run_item(m, json, len, 15, false, out, out_len);
 }
 
 // POST /report: Batch.java:68 → reporter_service.py handle_request 209-245
 int otr_report(otr_matcher* m, const char* json, size_t len, int threshold_sec, char** out, size_t* out_len) {
-  std::string perr;
   if (!json || len == 0) return fail(OTR_BAD_REQUEST, "No json provided", out, out_len);
-  otrjson::Parser ps(json, len);
-  otrjson::Ptr tr = ps.parse(&perr);
-  if (!tr || tr->kind != Value::Object) return fail(OTR_BAD_REQUEST, perr, out, out_len);
-  const Value* uuid = tr->get("uuid");  // :217-219
-  if (!uuid || uuid->kind == Value::Null) return fail(OTR_BAD_REQUEST, "uuid is required", out, out_len);
-  const Value* pts = tr->get("trace");  // :222-225
-  if (!pts || pts->kind != Value::Array || pts->arr.size() < 2)
-    return fail(OTR_BAD_REQUEST,
-                "trace must be a non zero length array of object each of which must have at least lat, lon and time",
-                out, out_len);
-  const Value* mo = tr->get("match_options");  // :228-235
-  const Value* rl = mo ? mo->get("report_levels") : nullptr;
-  if (!rl || rl->kind != Value::Array)
-    return fail(OTR_BAD_REQUEST, "match_options must include report_levels array", out, out_len);
-  const Value* tl = mo->get("transition_levels");
-  if (!tl || tl->kind != Value::Array)
-    return fail(OTR_BAD_REQUEST, "match_options must include transition_levels array", out, out_len);
   if (!m) return fail(OTR_MATCH_ERROR, "null matcher", out, out_len);
-  const int thr = threshold_default(threshold_sec);
-  otr_batch_result res;
-  std::string err;
-  int rc = run_single(m, *tr, levels_mask(rl), levels_mask(tl), thr, &res, &err);
-  if (rc != OTR_OK) return fail(OTR_MATCH_ERROR, err, out, out_len);  // :244-245
-  // report() output, reporter_service.py:164-179 (computed on device by k_segments)
-  std::string o = "{";
-  int32_t length_set[2] = {0, 0};
-  const int32_t* c = res.stats;
-  // a length is "set" iff the matching counter is non-zero (report() assigns it then)
-  length_set[0] = c[0] > 0;
-  length_set[1] = c[1] > 0;
-  put_stats(o, c, res.stats_len, length_set);
-  if (res.shape_used && res.shape_used[0] >= 0) o += ",\"shape_used\":" + std::to_string(res.shape_used[0]);
-  o += ",\"segment_matcher\":{\"segments\":";
-  put_segments(o, res);
-  o += ",\"mode\":\"auto\"},";
-  put_reports(o, res.n_rep, (const unsigned long long*)res.rep_id, (const unsigned long long*)res.rep_next,
-              res.rep_t0, res.rep_t1, res.rep_length, res.rep_queue);
-  o += "}";
-  dup_out(o, out, out_len);
-  return 200;
+  return run_item(m, json, len, threshold_default(threshold_sec), true, out, out_len);
 }
+
+// n POST /report bodies in shared device batches (Batch.java:68 × n)
+int otr_report_batch(otr_matcher* m, int32_t n, const char* const* bodies, const size_t* lens, int threshold_sec,
+                     int32_t* codes, char** outs, size_t* out_lens) {
+  if (!m || n < 0 || (n > 0 && (!bodies || !lens || !codes || !outs))) {
+    g_last_error = "null argument";
+    return OTR_BAD_REQUEST;
+  }
+  std::vector<otrsvc::Item> items(n);
+  std::vector<otrsvc::Item*> ptrs(n);
+  const int thr = threshold_default(threshold_sec);
+  for (int32_t i = 0; i < n; ++i) {
+    items[i].body = bodies[i];
+    items[i].len = bodies[i] ? lens[i] : 0;
+    items[i].threshold = thr;
+    items[i].report = true;
+    ptrs[i] = &items[i];
+  }
+  otrsvc::process(m->m, ptrs);
+  for (int32_t i = 0; i < n; ++i) {
+    codes[i] = items[i].code;
+    dup_out(items[i].out, &outs[i], out_lens ? &out_lens[i] : nullptr);
+  }
+  return OTR_OK;
+}
+
+int otr_coalesce(int32_t max_traces, int32_t max_wait_us) { return otrsvc::coalesce_configure(max_traces, max_wait_us); }
 
 // report() alone: reporter_service.py:79-179 (as simple_reporter.py:168 calls it)
 int otr_report_segments(const char* match_json, size_t match_len, const char* trace_json, size_t trace_len,
@@ -421,7 +263,7 @@ int otr_report_segments(const char* match_json, size_t match_len, const char* tr
                        len.data(), bs.data(), nullptr, end_time, (double)threshold_default(threshold_sec), rmask,
                        tmask, rid.data(), rnx.data(), t0.data(), t1.data(), rl.data(), rq.data(), nullptr, &rs);
   std::string o = "{";
-  put_stats(o, rs.counts, rs.lengths, rs.length_set);
+  otrfmt::put_stats(o, rs.counts, rs.lengths, rs.length_set);
   if (rs.shape_used >= 0) o += ",\"shape_used\":" + std::to_string(rs.shape_used);
   // segment_matcher echoes the match with mode forced to auto (reporter_service.py:96,167)
   Value echo = *mj;
@@ -443,7 +285,7 @@ int otr_report_segments(const char* match_json, size_t match_len, const char* tr
   o += ",\"segment_matcher\":";
   otrjson::put_value(o, echo);
   o += ",";
-  put_reports(o, rs.n_rep, rid.data(), rnx.data(), t0.data(), t1.data(), rl.data(), rq.data());
+  otrfmt::put_reports(o, 0, rs.n_rep, rid.data(), rnx.data(), t0.data(), t1.data(), rl.data(), rq.data());
   o += "}";
   dup_out(o, out, out_len);
   return OTR_OK;

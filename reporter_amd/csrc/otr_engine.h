@@ -48,7 +48,7 @@ struct Matcher {
   std::vector<int64_t> h_trace_state_off, h_state_probe, h_trace_route_off, h_trace_seg_off, h_seg_way_off,
       h_trace_rep_off;
   std::vector<int32_t> h_cand_count, h_winner, h_subpath, h_seg_length, h_seg_queue, h_seg_bshape, h_seg_eshape,
-      h_rep_length, h_rep_queue, h_shape_used, h_stats;
+      h_rep_length, h_rep_queue, h_shape_used, h_stats, h_trace_status;
   std::vector<uint32_t> h_cand_edge, h_route_edge, h_seg_way;
   std::vector<double> h_cand_p, h_cand_sqd, h_seg_start, h_seg_end, h_rep_t0, h_rep_t1, h_stats_len;
   std::vector<unsigned long long> h_seg_id, h_rep_id, h_rep_next;

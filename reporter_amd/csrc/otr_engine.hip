@@ -351,6 +351,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     b.acc = in->accuracy;
   }
   out->n_probes = N;
+  h_trace_status.assign(T, OTR_OK);
   const size_t n_ctr = 2 * (size_t)OTR_COUNTERS * kShards;  // tier-2 kinds land at +6, stamps at 16
   unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, n_ctr);
   HIPCHK(hipMemsetAsync(d_counters, 0, n_ctr * 8, stream));
@@ -495,6 +496,16 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
         HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
         out->n_overflow_traces += (int32_t)novf;
+        // rare: name the traces (task → state → trace) for per-trace status
+        std::vector<int64_t> tl(novf);
+        if (novf) HIPCHK(hipMemcpy(tl.data(), list, 8 * novf, hipMemcpyDeviceToHost));
+        for (int64_t task : tl) {
+          int64_t s = 0;
+          int32_t t = 0;
+          HIPCHK(hipMemcpy(&s, task_state + task, 8, hipMemcpyDeviceToHost));
+          HIPCHK(hipMemcpy(&t, state_trace + s, 4, hipMemcpyDeviceToHost));
+          if (t >= 0 && t < T) h_trace_status[t] = OTR_MATCH_ERROR;
+        }
       }
     }
     te(OTR_STAGE_ROUTE_BIG);
@@ -580,6 +591,15 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
         if (nretry == 0) break;
         if (tier == 2) {
           out->n_overflow_traces += (int32_t)nretry;
+          std::vector<int64_t> il(nretry);
+          HIPCHK(hipMemcpy(il.data(), rl, 8 * nretry, hipMemcpyDeviceToHost));
+          for (int64_t i : il) {
+            int64_t s = 0;
+            int32_t t = 0;
+            HIPCHK(hipMemcpy(&s, steps + i, 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(&t, state_trace + s, 4, hipMemcpyDeviceToHost));
+            if (t >= 0 && t < T) h_trace_status[t] = OTR_MATCH_ERROR;
+          }
           break;
         }
         HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
@@ -716,21 +736,25 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   out->n_seg = nseg;
   out->n_rep = nrep;
   out->status = out->n_overflow_traces ? OTR_MATCH_ERROR : OTR_OK;
-  if (!(in->flags & OTR_BATCH_COPY_OUT)) return OTR_OK;
+  const bool full = (in->flags & OTR_BATCH_COPY_OUT) != 0;
+  if (!full && !(in->flags & OTR_BATCH_COPY_REPORTS)) return OTR_OK;
+  out->trace_status = h_trace_status.data();
   HIPCHK(hipMemcpy(h_cap_off.data(), cap_off, 8 * (T + 1), hipMemcpyDeviceToHost));
   auto dl = [&](auto& vec, const void* src, size_t n) -> int {
     vec.resize(n ? n : 1);
     if (n) HIPCHK(hipMemcpy(vec.data(), src, n * sizeof(vec[0]), hipMemcpyDeviceToHost));
     return OTR_OK;
   };
-  if ((rc = dl(h_trace_state_off, trace_state_off, T + 1))) return rc;
-  if ((rc = dl(h_state_probe, state_probe, S))) return rc;
-  if ((rc = dl(h_cand_count, cb.count, S))) return rc;
-  if ((rc = dl(h_cand_edge, cb.edge, (size_t)S * OTR_KMAX))) return rc;
-  if ((rc = dl(h_cand_p, cb.p, (size_t)S * OTR_KMAX))) return rc;
-  if ((rc = dl(h_cand_sqd, cb.sqd, (size_t)S * OTR_KMAX))) return rc;
-  if ((rc = dl(h_winner, va.winner, S))) return rc;
-  if ((rc = dl(h_subpath, va.subpath, S))) return rc;
+  if (full) {
+    if ((rc = dl(h_trace_state_off, trace_state_off, T + 1))) return rc;
+    if ((rc = dl(h_state_probe, state_probe, S))) return rc;
+    if ((rc = dl(h_cand_count, cb.count, S))) return rc;
+    if ((rc = dl(h_cand_edge, cb.edge, (size_t)S * OTR_KMAX))) return rc;
+    if ((rc = dl(h_cand_p, cb.p, (size_t)S * OTR_KMAX))) return rc;
+    if ((rc = dl(h_cand_sqd, cb.sqd, (size_t)S * OTR_KMAX))) return rc;
+    if ((rc = dl(h_winner, va.winner, S))) return rc;
+    if ((rc = dl(h_subpath, va.subpath, S))) return rc;
+  }
   if ((rc = dl(h_shape_used, sa.shape_used, T))) return rc;
   if ((rc = dl(h_stats, sa.stats, 7 * (size_t)T))) return rc;
   if ((rc = dl(h_stats_len, sa.stats_len, 2 * (size_t)T))) return rc;
@@ -741,7 +765,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   std::vector<int32_t> c_sl, c_sq, c_sb, c_sx, c_rl, c_rq;
   std::vector<uint8_t> c_si;
   std::vector<int64_t> c_swn;
-  if ((rc = dl(c_route, sa.route, C))) return rc;
+  if (full && (rc = dl(c_route, sa.route, C))) return rc;
   if ((rc = dl(c_way, sa.seg_way, C))) return rc;
   if ((rc = dl(c_seg_id, sa.seg_id, C))) return rc;
   if ((rc = dl(c_ss, sa.seg_start, C))) return rc;
@@ -768,7 +792,8 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   h_rep_queue.clear();
   for (int t = 0; t < T; ++t) {
     const int64_t co = h_cap_off[t];
-    for (int64_t k = 0; k < route_n[t]; ++k) h_route_edge.push_back(c_route[co + k]);
+    if (full)
+      for (int64_t k = 0; k < route_n[t]; ++k) h_route_edge.push_back(c_route[co + k]);
     int64_t wk = co;
     for (int64_t k = 0; k < seg_n[t]; ++k) {
       h_seg_id.push_back(c_seg_id[co + k]);
@@ -796,16 +821,18 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     h_trace_rep_off[t + 1] = (int64_t)h_rep_id.size();
   }
   auto P = [](auto& v) { return v.empty() ? nullptr : v.data(); };
-  out->trace_state_off = P(h_trace_state_off);
-  out->state_probe = P(h_state_probe);
-  out->cand_count = P(h_cand_count);
-  out->cand_edge = P(h_cand_edge);
-  out->cand_p = P(h_cand_p);
-  out->cand_sqd = P(h_cand_sqd);
-  out->winner = P(h_winner);
-  out->subpath = P(h_subpath);
-  out->trace_route_off = P(h_trace_route_off);
-  out->route_edge = P(h_route_edge);
+  if (full) {
+    out->trace_state_off = P(h_trace_state_off);
+    out->state_probe = P(h_state_probe);
+    out->cand_count = P(h_cand_count);
+    out->cand_edge = P(h_cand_edge);
+    out->cand_p = P(h_cand_p);
+    out->cand_sqd = P(h_cand_sqd);
+    out->winner = P(h_winner);
+    out->subpath = P(h_subpath);
+    out->trace_route_off = P(h_trace_route_off);
+    out->route_edge = P(h_route_edge);
+  }
   out->trace_seg_off = P(h_trace_seg_off);
   out->seg_id = (uint64_t*)P(h_seg_id);
   out->seg_start = P(h_seg_start);

@@ -12,6 +12,8 @@
 #include <string>
 #include <vector>
 
+#include "otr_request.h"
+
 namespace otrjson {
 
 struct Value;
@@ -207,17 +209,8 @@ class Parser {
 };
 
 // shortest round-tripping repr of a double, Python-style ("1000.0", "1e-05")
-inline void put_double(std::string& o, double v) {
-  if (std::isnan(v)) { o += "NaN"; return; }
-  if (std::isinf(v)) { o += v > 0 ? "Infinity" : "-Infinity"; return; }
-  char buf[40];
-  for (int prec = 1; prec <= 17; ++prec) {
-    snprintf(buf, sizeof buf, "%.*g", prec, v);
-    if (strtod(buf, nullptr) == v) break;
-  }
-  o += buf;
-  if (!strpbrk(buf, ".eEn")) o += ".0";
-}
+// repr() digits and layout, as json.dumps prints floats (reporter_service.py:243)
+inline void put_double(std::string& o, double v) { otrreq::put_repr(o, v); }
 
 inline void put_string(std::string& o, const std::string& s) {
   o.push_back('"');

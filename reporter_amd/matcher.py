@@ -40,6 +40,14 @@ def configure(config):
         raise RuntimeError('otr_configure failed (%d): %s' % (rc, _lib.last_error()))
 
 
+def coalesce(max_traces, max_wait_us=2000):
+    """Coalesce concurrent report_json calls of all threads into shared device batches
+    (otr_coalesce); max_traces <= 0 stops it."""
+    rc = _lib.lib().otr_coalesce(int(max_traces), int(max_wait_us))
+    if rc != 0:
+        raise RuntimeError('otr_coalesce failed (%d): %s' % (rc, _lib.last_error()))
+
+
 def graph_info():
     a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     rc = _lib.lib().otr_graph_info(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
@@ -86,6 +94,24 @@ class Matcher:
         out, n = ctypes.c_void_p(), ctypes.c_size_t()
         rc = self._L.otr_report(self._h, s, len(s), threshold_sec, ctypes.byref(out), ctypes.byref(n))
         return rc, _lib.take_string(out, n)
+
+    def report_json_batch(self, bodies, threshold_sec=-1):
+        """Many POST /report bodies in shared device batches (otr_report_batch):
+        [(http_code, body)], item i exactly as report_json(bodies[i])."""
+        enc = [b.encode() if isinstance(b, str) else bytes(b) for b in bodies]
+        n = len(enc)
+        arr = (ctypes.c_char_p * max(n, 1))(*enc)
+        lens = (ctypes.c_size_t * max(n, 1))(*[len(b) for b in enc])
+        codes = (ctypes.c_int32 * max(n, 1))()
+        outs = (ctypes.c_void_p * max(n, 1))()
+        olens = (ctypes.c_size_t * max(n, 1))()
+        rc = self._L.otr_report_batch(self._h, n, arr, lens, threshold_sec, codes, outs, olens)
+        if rc != 0:
+            raise RuntimeError('otr_report_batch failed (%d): %s' % (rc, _lib.last_error()))
+        res = []
+        for i in range(n):
+            res.append((codes[i], _lib.take_string(ctypes.c_void_p(outs[i]), ctypes.c_size_t(olens[i]))))
+        return res
 
     # --- batched API ----------------------------------------------------------------
     def match_batch(self, traces, report_levels=(0, 1), transition_levels=(0, 1), threshold_sec=15,

@@ -6,8 +6,11 @@
   handle_request(body) -> (code, body)
         reporter_service.py:209-245 — validation + Match + report() in one C-ABI call
         (otr_report), the call that replaces Batch.java:68's HTTP POST.
-  serve(address)
-        optional HTTP front (POST/GET /report) for callers that still speak HTTP.
+  handle_requests(bodies) -> [(code, body)]
+        many bodies in shared device batches (otr_report_batch).
+  serve(address, config, coalesce_traces)
+        optional HTTP front (POST/GET /report) for callers that still speak HTTP;
+        concurrent requests coalesce into shared device batches (otr_coalesce).
 """
 import ctypes
 import json
@@ -57,11 +60,20 @@ def handle_request(body, threshold_sec=None):
     return _matcher().report_json(body, t)
 
 
-def serve(address, config):
-    """Minimal threaded HTTP front: POST /report or GET /report?json=... ."""
+def handle_requests(bodies, threshold_sec=None):
+    """[(code, body)] for many POST /report bodies, matched in shared device batches."""
+    t = _threshold() if threshold_sec is None else threshold_sec
+    return _matcher().report_json_batch(bodies, t)
+
+
+def serve(address, config, coalesce_traces=0, coalesce_wait_us=2000):
+    """coalesce_traces > 0: concurrent requests of the server threads share device
+    batches (otr_coalesce) instead of one device batch per request."""
     from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
     from urllib.parse import parse_qs, urlsplit
     _m.configure(config)
+    if coalesce_traces > 0:
+        _m.coalesce(coalesce_traces, coalesce_wait_us)
 
     class H(BaseHTTPRequestHandler):
         def _do(self, post):

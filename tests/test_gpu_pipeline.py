@@ -129,3 +129,58 @@ def test_simple_reporter_end_to_end(city):
     assert tiles == wt and len(tiles) > 0
     culled = sr.report_tiles(tiles, 2)
     assert sum(len(v) for v in culled.values()) <= sum(len(v) for v in tiles.values())
+
+
+def _mixed_bodies(city):
+    """Bodies a batching caller would hold: several option groups, modes and invalid
+    requests interleaved."""
+    tr = gen.make_traces(city, 36, 60, 5, 8.0, 21, 0.2, 0.1)
+    bodies = []
+    for t in range(tr.n_traces):
+        mode = ['auto', 'bicycle', 'pedestrian'][int(tr.mode[t])]
+        if t % 9 == 4:
+            bodies.append(_trace_json(tr, t, report_levels=(0,), transition_levels=(0, 1, 2), mode=mode))
+        elif t % 9 == 7:
+            bodies.append(_trace_json(tr, t, mode=mode, extra={'sigma_z': 6.5, 'search_radius': 40}))
+        else:
+            bodies.append(_trace_json(tr, t, mode=mode))
+        if t % 10 == 3:
+            bodies.append('{"uuid":"x","trace":[{"lat":1,"lon":2,"time":3}]}')
+        if t % 10 == 6:
+            bodies.append(_trace_json(tr, t).replace('"time"', '"tim"', 1))
+    return bodies
+
+
+def test_report_batch_equals_single(city):
+    """otr_report_batch: the same bytes as otr_report, body by body, across option groups."""
+    m = M.Matcher()
+    bodies = _mixed_bodies(city)
+    single = [m.report_json(b) for b in bodies]
+    batch = m.report_json_batch(bodies)
+    assert batch == single
+    codes = [c for c, _ in batch]
+    assert codes.count(200) >= 30 and 400 in codes and 500 in codes
+
+
+def test_coalesced_threads_equal_single(city):
+    """otr_coalesce: concurrent otr_report calls from many threads share device batches
+    and each caller receives exactly its uncoalesced response."""
+    import threading
+    bodies = _mixed_bodies(city)
+    m = M.Matcher()
+    want = [m.report_json(b) for b in bodies]
+    got = [None] * len(bodies)
+    M.coalesce(16, 20000)
+    try:
+        def worker(k):
+            mk = M.Matcher()
+            for i in range(k, len(bodies), 6):
+                got[i] = mk.report_json(bodies[i])
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(6)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(120)
+    finally:
+        M.coalesce(0)
+    assert got == want
