@@ -112,6 +112,23 @@ typedef struct otr_trace_batch {
 #define OTR_BATCH_COPY_OUT 1   /* fill the host arrays of otr_batch_result */
 #define OTR_BATCH_TIMING 2     /* record per-kernel HIP-event timings */
 #define OTR_BATCH_COPY_REPORTS 4  /* host copies of segments, reports, stats only (the JSON path) */
+#define OTR_BATCH_TILE_ROWS 8  /* also emit simple_reporter tile rows on device (d_rows / n_rows) */
+
+/* One simple_reporter tile line (simple_reporter.py:188-195) in binary form: the line
+ * "id,next_id,duration,1,length,queue_length,start,end,source,MODE" of the file
+ * "{b*q}_{(b+1)*q-1}/{level}/{tile_index}" (q = quantisation). */
+typedef struct otr_tile_row {
+  uint64_t file;       /* bucket b << 25 | level << 22 | tile index (get_tile_level/_index, :45-49) */
+  uint64_t id;         /* segment id */
+  uint64_t next_id;    /* next segment id, or INVALID_SEGMENT_ID 0x3fffffffffff (:43,193) */
+  int64_t start;       /* floor(t0) */
+  int64_t end;         /* ceil(t1) */
+  int32_t duration;    /* int(round(t1 - t0)), Python 2 rounding (:179) */
+  int32_t length;
+  int32_t queue_length;
+  int32_t pad;
+} otr_tile_row;
+#define OTR_INVALID_SEGMENT_ID 0x3fffffffffffull
 
 #define OTR_NO_ID 0xFFFFFFFFFFFFFFFFull
 
@@ -158,9 +175,26 @@ typedef struct otr_batch_result {
   float kernel_ms[16];         /* OTR_BATCH_TIMING: device time per stage, OTR_STAGE_* */
   int32_t* trace_status;       /* host, per trace (with COPY_OUT / COPY_REPORTS): OTR_OK, or
                                   OTR_MATCH_ERROR when its search outgrew the largest LDS table */
+  otr_tile_row* d_rows;        /* OTR_BATCH_TILE_ROWS: n_rows tile rows in HBM (matcher-owned),
+                                  trace by trace in report order */
 } otr_batch_result;
 
 int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result* out);
+
+/* simple_reporter's tile stage (simple_reporter.py:211-239) on device: sort the rows
+ * by file, then in the line order of segments.sort() (:218, string order of the whole
+ * line), and delete the (id, next_id) runs seen fewer than `privacy` times with the
+ * reference loop's exact rule (:221-239, including its trailing-singleton quirk).
+ * rows: n rows in host (OTR_MEM_HOST) or device (OTR_MEM_DEVICE) memory, e.g. the
+ * d_rows of a batch or rows received from other GPUs.  *out: the kept rows, sorted,
+ * in host memory owned by the matcher (valid until its next call). */
+int otr_tiles_cull(otr_matcher* m, const otr_tile_row* rows, int64_t n, int32_t memory, int32_t privacy,
+                   const otr_tile_row** out, int64_t* n_out);
+
+/* The CSV lines of n (host) rows in order, "id,next,duration,1,length,queue,start,end,
+ * source,MODE\n" each (simple_reporter.py:188-195; mode is upper-cased as :195 does). */
+int otr_tiles_format(const otr_tile_row* rows, int64_t n, const char* source, const char* mode, char** out,
+                     size_t* out_len);
 
 /* graph facts for callers sizing histograms */
 int otr_graph_info(int64_t* n_nodes, int64_t* n_edges, int64_t* n_segments);

@@ -16,6 +16,7 @@ OTR_MEM_DEVICE = 1
 OTR_BATCH_COPY_OUT = 1
 OTR_BATCH_TIMING = 2
 OTR_BATCH_COPY_REPORTS = 4
+OTR_BATCH_TILE_ROWS = 8
 OTR_NO_ID = 0xFFFFFFFFFFFFFFFF
 HIST_BINS = 8
 KMAX = 64
@@ -25,7 +26,8 @@ STAGES = ['states', 'candidates', 'link', 'route', 'route_big', 'viterbi', 'path
 # every symbol include/otr.h declares
 EXPORTS = ['otr_configure', 'otr_configure_json', 'otr_matcher_new', 'otr_matcher_free', 'otr_match',
            'otr_report', 'otr_report_segments', 'otr_free', 'otr_last_error', 'otr_match_batch',
-           'otr_graph_info', 'otr_matcher_stream', 'otr_device', 'otr_report_batch', 'otr_coalesce']
+           'otr_graph_info', 'otr_matcher_stream', 'otr_device', 'otr_report_batch', 'otr_coalesce',
+           'otr_tiles_cull', 'otr_tiles_format']
 
 
 class TraceBatch(ctypes.Structure):
@@ -59,7 +61,12 @@ class BatchResult(ctypes.Structure):
                 ('shape_used', P(ctypes.c_int32)), ('stats', P(ctypes.c_int32)),
                 ('stats_len', P(ctypes.c_double)), ('d_hist', ctypes.c_void_p), ('hist_len', ctypes.c_int64),
                 ('counters', ctypes.c_uint64 * 24), ('kernel_ms', ctypes.c_float * 16),
-                ('trace_status', P(ctypes.c_int32))]
+                ('trace_status', P(ctypes.c_int32)), ('d_rows', ctypes.c_void_p)]
+
+
+# otr_tile_row (include/otr.h), 56 bytes
+TILE_ROW = np.dtype([('file', '<u8'), ('id', '<u8'), ('next_id', '<u8'), ('start', '<i8'), ('end', '<i8'),
+                     ('duration', '<i4'), ('length', '<i4'), ('queue_length', '<i4'), ('pad', '<i4')])
 
 
 _L = None
@@ -99,6 +106,10 @@ def lib():
     L.otr_report_batch.argtypes = [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_char_p), P(ctypes.c_size_t),
                                    ctypes.c_int, P(ctypes.c_int32), P(ctypes.c_void_p), P(ctypes.c_size_t)]
     L.otr_coalesce.argtypes = [ctypes.c_int32, ctypes.c_int32]
+    L.otr_tiles_cull.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                 P(ctypes.c_void_p), P(ctypes.c_int64)]
+    L.otr_tiles_format.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_char_p,
+                                   P(ctypes.c_void_p), P(ctypes.c_size_t)]
     _L = L
     return L
 

@@ -53,12 +53,15 @@ struct Matcher {
   std::vector<double> h_cand_p, h_cand_sqd, h_seg_start, h_seg_end, h_rep_t0, h_rep_t1, h_stats_len;
   std::vector<unsigned long long> h_seg_id, h_rep_id, h_rep_next;
   std::vector<uint8_t> h_seg_internal;
+  std::vector<otr_tile_row> h_tile_rows;
   hipEvent_t ev[20];
   bool ev_init = false;
 
   template <class T>
   T* need(int slot, size_t n);
   int run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err);
+  int tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int privacy, const otr_tile_row** out,
+                 int64_t* n_out, std::string* err);
   ~Matcher();
 };
 

@@ -208,6 +208,10 @@ enum Slot {
   S_SEG_BSHAPE, S_SEG_ESHAPE, S_SEG_INDEX, S_SEG_N, S_SEG_WAY_N, S_SEG_WAY, S_WAY_N,
   S_REP_ID, S_REP_NEXT, S_REP_T0, S_REP_T1, S_REP_LEN, S_REP_QUEUE, S_REP_SEG, S_REP_N,
   S_SHAPE_USED, S_STATS, S_STATS_LEN, S_HIST, S_COUNTERS, S_SCAN_TMP, S_LIST, S_MISC,
+  S_ROW_CNT, S_ROW_OFF, S_ROWS, S_ROWS_IN, S_ROWS_OUT, S_ROWS_KEPT, S_IDX_A, S_IDX_B, S_KEY_A, S_KEY_B, S_POS_SCAN, S_KEEP, S_FILE_HEAD, S_FILE_START, S_NFILES, S_SORT_TMP,
+  S_C_ROUTE_OFF, S_C_SEG_OFF, S_C_WAY_OFF, S_C_REP_OFF, S_C_ARGS, S_C_ROUTE, S_C_SEG_ID, S_C_SEG_START,
+  S_C_SEG_END, S_C_SEG_LEN, S_C_SEG_QUEUE, S_C_SEG_INTERNAL, S_C_SEG_BSHAPE, S_C_SEG_ESHAPE, S_C_SEG_WAY_N,
+  S_C_SEG_WAY, S_C_SEG_WAY_OFF, S_C_REP_ID, S_C_REP_NEXT, S_C_REP_T0, S_C_REP_T1, S_C_REP_LEN, S_C_REP_QUEUE,
   S_NUM
 };
 
@@ -703,6 +707,31 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   tb(OTR_STAGE_HISTOGRAM);
   k_histogram<<<grid_for(T, 256), 256, 0, stream>>>(ha);
   te(OTR_STAGE_HISTOGRAM);
+  // ---- K9: simple_reporter tile rows (optional)
+  if (in->flags & OTR_BATCH_TILE_ROWS) {
+    TileArgs ta{};
+    ta.b = b;
+    ta.cap_off = cap_off;
+    ta.rep_n = sa.rep_n;
+    ta.rep_id = sa.rep_id;
+    ta.rep_next = sa.rep_next;
+    ta.rep_t0 = sa.rep_t0;
+    ta.rep_t1 = sa.rep_t1;
+    ta.rep_length = sa.rep_length;
+    ta.rep_queue = sa.rep_queue;
+    ta.quantisation = ha.quantisation;
+    ta.row_cnt = need<int64_t>(S_ROW_CNT, T);
+    k_tile_rows<<<grid_for(T, 256), 256, 0, stream>>>(ta);
+    int64_t* row_off = need<int64_t>(S_ROW_OFF, T + 1);
+    if ((rc = scan(ta.row_cnt, row_off, T))) return rc;
+    int64_t R = 0;
+    if ((rc = read_i64(row_off + T, &R))) return rc;
+    ta.row_off = row_off;
+    ta.rows = need<otr_tile_row>(S_ROWS, R > 0 ? R : 1);
+    if (R > 0) k_tile_rows<<<grid_for(T, 256), 256, 0, stream>>>(ta);
+    out->d_rows = ta.rows;
+    out->n_rows = R;
+  }
   HIPCHK(hipGetLastError());
   std::vector<unsigned long long> hc(n_ctr);
   HIPCHK(hipMemcpyAsync(hc.data(), d_counters, n_ctr * 8, hipMemcpyDeviceToHost, stream));
@@ -714,7 +743,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   }
   out->counters[5] = (uint64_t)NT;
   out->counters[6] = (uint64_t)NTR;
-  out->n_rows = (int64_t)out->counters[8];
+  if (!(in->flags & OTR_BATCH_TILE_ROWS)) out->n_rows = (int64_t)out->counters[8];
   out->d_hist = ha.hist;
   out->hist_len = (int64_t)hist_len;
   if (timing)
@@ -739,10 +768,9 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   const bool full = (in->flags & OTR_BATCH_COPY_OUT) != 0;
   if (!full && !(in->flags & OTR_BATCH_COPY_REPORTS)) return OTR_OK;
   out->trace_status = h_trace_status.data();
-  HIPCHK(hipMemcpy(h_cap_off.data(), cap_off, 8 * (T + 1), hipMemcpyDeviceToHost));
   auto dl = [&](auto& vec, const void* src, size_t n) -> int {
     vec.resize(n ? n : 1);
-    if (n) HIPCHK(hipMemcpy(vec.data(), src, n * sizeof(vec[0]), hipMemcpyDeviceToHost));
+    if (n) HIPCHK(hipMemcpyAsync(vec.data(), src, n * sizeof(vec[0]), hipMemcpyDeviceToHost, stream));
     return OTR_OK;
   };
   if (full) {
@@ -758,67 +786,67 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   if ((rc = dl(h_shape_used, sa.shape_used, T))) return rc;
   if ((rc = dl(h_stats, sa.stats, 7 * (size_t)T))) return rc;
   if ((rc = dl(h_stats_len, sa.stats_len, 2 * (size_t)T))) return rc;
-  // capacity-layout arrays
-  std::vector<uint32_t> c_route, c_way, c_seg_index;
-  std::vector<unsigned long long> c_seg_id, c_rep_id, c_rep_next;
-  std::vector<double> c_ss, c_se, c_t0, c_t1;
-  std::vector<int32_t> c_sl, c_sq, c_sb, c_sx, c_rl, c_rq;
-  std::vector<uint8_t> c_si;
-  std::vector<int64_t> c_swn;
-  if (full && (rc = dl(c_route, sa.route, C))) return rc;
-  if ((rc = dl(c_way, sa.seg_way, C))) return rc;
-  if ((rc = dl(c_seg_id, sa.seg_id, C))) return rc;
-  if ((rc = dl(c_ss, sa.seg_start, C))) return rc;
-  if ((rc = dl(c_se, sa.seg_end, C))) return rc;
-  if ((rc = dl(c_sl, sa.seg_length, C))) return rc;
-  if ((rc = dl(c_sq, sa.seg_queue, C))) return rc;
-  if ((rc = dl(c_si, sa.seg_internal, C))) return rc;
-  if ((rc = dl(c_sb, sa.seg_bshape, C))) return rc;
-  if ((rc = dl(c_sx, sa.seg_eshape, C))) return rc;
-  if ((rc = dl(c_swn, sa.seg_way_n, C))) return rc;
-  if ((rc = dl(c_rep_id, sa.rep_id, C))) return rc;
-  if ((rc = dl(c_rep_next, sa.rep_next, C))) return rc;
-  if ((rc = dl(c_t0, sa.rep_t0, C))) return rc;
-  if ((rc = dl(c_t1, sa.rep_t1, C))) return rc;
-  if ((rc = dl(c_rl, sa.rep_length, C))) return rc;
-  if ((rc = dl(c_rq, sa.rep_queue, C))) return rc;
+  // dense layout on device (k_compact), then only the used entries cross PCIe
+  int64_t nway = 0;
+  for (int t = 0; t < T; ++t) nway += way_n[t];
+  CompactArgs ca{};
+  ca.n_traces = T;
+  ca.cap_off = cap_off;
+  int64_t* route_off = need<int64_t>(S_C_ROUTE_OFF, T + 1);
+  int64_t* seg_off = need<int64_t>(S_C_SEG_OFF, T + 1);
+  int64_t* way_off = need<int64_t>(S_C_WAY_OFF, T + 1);
+  int64_t* rep_off = need<int64_t>(S_C_REP_OFF, T + 1);
+  if ((rc = scan(sa.seg_n, seg_off, T)) || (rc = scan(sa.way_n, way_off, T)) || (rc = scan(sa.rep_n, rep_off, T)))
+    return rc;
+  if (full && (rc = scan(sa.route_n, route_off, T))) return rc;
+  ca.route_off = full ? route_off : nullptr;
+  ca.seg_off = seg_off;
+  ca.way_off = way_off;
+  ca.rep_off = rep_off;
+  SegArgs* d_sa = need<SegArgs>(S_C_ARGS, 1);
+  HIPCHK(hipMemcpyAsync(d_sa, &sa, sizeof(SegArgs), hipMemcpyHostToDevice, stream));
+  ca.s = d_sa;
+  auto n1 = [](int64_t n) { return (size_t)(n > 0 ? n : 1); };
+  ca.route = need<uint32_t>(S_C_ROUTE, n1(nroute));
+  ca.seg_id = need<unsigned long long>(S_C_SEG_ID, n1(nseg));
+  ca.seg_start = need<double>(S_C_SEG_START, n1(nseg));
+  ca.seg_end = need<double>(S_C_SEG_END, n1(nseg));
+  ca.seg_length = need<int32_t>(S_C_SEG_LEN, n1(nseg));
+  ca.seg_queue = need<int32_t>(S_C_SEG_QUEUE, n1(nseg));
+  ca.seg_internal = need<uint8_t>(S_C_SEG_INTERNAL, n1(nseg));
+  ca.seg_bshape = need<int32_t>(S_C_SEG_BSHAPE, n1(nseg));
+  ca.seg_eshape = need<int32_t>(S_C_SEG_ESHAPE, n1(nseg));
+  ca.seg_way_n = need<int64_t>(S_C_SEG_WAY_N, n1(nseg));
+  ca.seg_way = need<uint32_t>(S_C_SEG_WAY, n1(nway));
+  ca.rep_id = need<unsigned long long>(S_C_REP_ID, n1(nrep));
+  ca.rep_next = need<unsigned long long>(S_C_REP_NEXT, n1(nrep));
+  ca.rep_t0 = need<double>(S_C_REP_T0, n1(nrep));
+  ca.rep_t1 = need<double>(S_C_REP_T1, n1(nrep));
+  ca.rep_length = need<int32_t>(S_C_REP_LEN, n1(nrep));
+  ca.rep_queue = need<int32_t>(S_C_REP_QUEUE, n1(nrep));
+  k_compact<<<(unsigned)T, 64, 0, stream>>>(ca);
+  int64_t* seg_way_off = need<int64_t>(S_C_SEG_WAY_OFF, (size_t)nseg + 1);
+  if ((rc = scan(ca.seg_way_n, seg_way_off, nseg))) return rc;
+  HIPCHK(hipGetLastError());
+  if (full && (rc = dl(h_route_edge, ca.route, nroute))) return rc;
+  if (!full) h_route_edge.clear();
+  if ((rc = dl(h_seg_id, ca.seg_id, nseg)) || (rc = dl(h_seg_start, ca.seg_start, nseg)) ||
+      (rc = dl(h_seg_end, ca.seg_end, nseg)) || (rc = dl(h_seg_length, ca.seg_length, nseg)) ||
+      (rc = dl(h_seg_queue, ca.seg_queue, nseg)) || (rc = dl(h_seg_internal, ca.seg_internal, nseg)) ||
+      (rc = dl(h_seg_bshape, ca.seg_bshape, nseg)) || (rc = dl(h_seg_eshape, ca.seg_eshape, nseg)) ||
+      (rc = dl(h_seg_way_off, seg_way_off, (size_t)nseg + 1)) || (rc = dl(h_seg_way, ca.seg_way, nway)) ||
+      (rc = dl(h_rep_id, ca.rep_id, nrep)) || (rc = dl(h_rep_next, ca.rep_next, nrep)) ||
+      (rc = dl(h_rep_t0, ca.rep_t0, nrep)) || (rc = dl(h_rep_t1, ca.rep_t1, nrep)) ||
+      (rc = dl(h_rep_length, ca.rep_length, nrep)) || (rc = dl(h_rep_queue, ca.rep_queue, nrep)))
+    return rc;
+  HIPCHK(hipStreamSynchronize(stream));
   h_trace_route_off.assign(T + 1, 0);
   h_trace_seg_off.assign(T + 1, 0);
   h_trace_rep_off.assign(T + 1, 0);
-  h_route_edge.clear();
-  h_seg_id.clear(); h_seg_start.clear(); h_seg_end.clear(); h_seg_length.clear(); h_seg_queue.clear();
-  h_seg_internal.clear(); h_seg_bshape.clear(); h_seg_eshape.clear(); h_seg_way_off.assign(1, 0); h_seg_way.clear();
-  h_rep_id.clear(); h_rep_next.clear(); h_rep_t0.clear(); h_rep_t1.clear(); h_rep_length.clear();
-  h_rep_queue.clear();
   for (int t = 0; t < T; ++t) {
-    const int64_t co = h_cap_off[t];
-    if (full)
-      for (int64_t k = 0; k < route_n[t]; ++k) h_route_edge.push_back(c_route[co + k]);
-    int64_t wk = co;
-    for (int64_t k = 0; k < seg_n[t]; ++k) {
-      h_seg_id.push_back(c_seg_id[co + k]);
-      h_seg_start.push_back(c_ss[co + k]);
-      h_seg_end.push_back(c_se[co + k]);
-      h_seg_length.push_back(c_sl[co + k]);
-      h_seg_queue.push_back(c_sq[co + k]);
-      h_seg_internal.push_back(c_si[co + k]);
-      h_seg_bshape.push_back(c_sb[co + k]);
-      h_seg_eshape.push_back(c_sx[co + k]);
-      for (int64_t w = 0; w < c_swn[co + k]; ++w) h_seg_way.push_back(c_way[wk + w]);
-      wk += c_swn[co + k];
-      h_seg_way_off.push_back((int64_t)h_seg_way.size());
-    }
-    for (int64_t k = 0; k < rep_n[t]; ++k) {
-      h_rep_id.push_back(c_rep_id[co + k]);
-      h_rep_next.push_back(c_rep_next[co + k]);
-      h_rep_t0.push_back(c_t0[co + k]);
-      h_rep_t1.push_back(c_t1[co + k]);
-      h_rep_length.push_back(c_rl[co + k]);
-      h_rep_queue.push_back(c_rq[co + k]);
-    }
-    h_trace_route_off[t + 1] = (int64_t)h_route_edge.size();
-    h_trace_seg_off[t + 1] = (int64_t)h_seg_id.size();
-    h_trace_rep_off[t + 1] = (int64_t)h_rep_id.size();
+    h_trace_route_off[t + 1] = h_trace_route_off[t] + route_n[t];
+    h_trace_seg_off[t + 1] = h_trace_seg_off[t] + seg_n[t];
+    h_trace_rep_off[t + 1] = h_trace_rep_off[t] + rep_n[t];
   }
   auto P = [](auto& v) { return v.empty() ? nullptr : v.data(); };
   if (full) {
@@ -854,6 +882,89 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   out->shape_used = P(h_shape_used);
   out->stats = P(h_stats);
   out->stats_len = P(h_stats_len);
+  return OTR_OK;
+}
+
+// Tile stage: sort rows into simple_reporter's line order per file, then cull
+// (K10).  Result rows are copied to host (matcher-owned).
+int Matcher::tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int privacy,
+                        const otr_tile_row** out, int64_t* n_out, std::string* err) {
+  GraphState& gs = graph_state();
+  HIPCHK(hipSetDevice(gs.device));
+  if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  *n_out = 0;
+  *out = nullptr;
+  h_tile_rows.clear();
+  if (n <= 0) return OTR_OK;
+  if (n >= (int64_t)INT32_MAX) {
+    if (err) *err = "too many tile rows for one call";
+    return OTR_BAD_REQUEST;
+  }
+  // staging: in (copy of the caller's rows), sorted, kept; permutation + radix keys
+  otr_tile_row* d_in = need<otr_tile_row>(S_ROWS_IN, n);
+  otr_tile_row* d = need<otr_tile_row>(S_ROWS_OUT, n);
+  otr_tile_row* d_kept = need<otr_tile_row>(S_ROWS_KEPT, n);
+  int32_t* perm_a = need<int32_t>(S_IDX_A, n);
+  int32_t* perm_b = need<int32_t>(S_IDX_B, n);
+  unsigned long long* key_a = need<unsigned long long>(S_KEY_A, n);
+  unsigned long long* key_b = need<unsigned long long>(S_KEY_B, n);
+  int64_t* head = need<int64_t>(S_FILE_HEAD, n);
+  int64_t* keep = need<int64_t>(S_KEEP, n);
+  int64_t* pos = need<int64_t>(S_POS_SCAN, n);
+  int64_t* fstart = need<int64_t>(S_FILE_START, n);
+  if (!d_in || !d || !d_kept || !perm_a || !perm_b || !key_a || !key_b || !head || !keep || !pos || !fstart) {
+    if (err) *err = "device allocation failed (tiles)";
+    return OTR_DEVICE_ERROR;
+  }
+  HIPCHK(hipMemcpyAsync(d_in, rows, sizeof(otr_tile_row) * n,
+                        memory == OTR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, stream));
+  const int ni = (int)n;
+  size_t tb_sort = 0, tb_scan = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, key_a, key_b, perm_a, perm_b, ni, 0, 64, stream));
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb_scan, head, pos, ni, stream));
+  void* tmp = need<char>(S_SORT_TMP, std::max(tb_sort, tb_scan));
+  if (!tmp) {
+    if (err) *err = "device allocation failed (tiles)";
+    return OTR_DEVICE_ERROR;
+  }
+  // LSD over the line's fields: stable radix passes, least significant field first
+  k_iota_i32<<<grid_for(n, 256), 256, 0, stream>>>(perm_a, n);
+  for (int f = TF_COUNT - 1; f >= 0; --f) {
+    k_line_key<<<grid_for(n, 256), 256, 0, stream>>>(d_in, perm_a, n, f, key_a);
+    size_t tb = tb_sort;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key_a, key_b, perm_a, perm_b, ni, 0, f == TF_FILE ? 64 : 63,
+                                              stream));
+    std::swap(perm_a, perm_b);
+  }
+  k_gather_rows<<<grid_for(n, 256), 256, 0, stream>>>(d_in, perm_a, n, d);
+  // file starts: inclusive scan of head flags, scatter indices
+  k_file_heads<<<grid_for(n, 256), 256, 0, stream>>>(d, n, head);
+  size_t tb = tb_scan;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, head, pos, ni, stream));
+  k_scatter_index<<<grid_for(n, 256), 256, 0, stream>>>(head, pos, n, fstart);
+  int64_t nf = 0;
+  HIPCHK(hipMemcpyAsync(&nf, pos + (n - 1), 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  if (nf < 1 || nf > n) {
+    if (err) *err = "tile file split failed";
+    return OTR_DEVICE_ERROR;
+  }
+  k_cull_files<<<grid_for(nf, 64), 64, 0, stream>>>(d, n, fstart, nf, privacy, keep);
+  tb = tb_scan;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, keep, pos, ni, stream));
+  k_scatter_flagged<otr_tile_row><<<grid_for(n, 256), 256, 0, stream>>>(d, keep, pos, n, d_kept);
+  int64_t nk = 0;
+  HIPCHK(hipMemcpyAsync(&nk, pos + (n - 1), 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  if (nk < 0 || nk > n) {
+    if (err) *err = "tile cull compaction failed";
+    return OTR_DEVICE_ERROR;
+  }
+  h_tile_rows.resize(nk > 0 ? nk : 1);
+  if (nk > 0) HIPCHK(hipMemcpy(h_tile_rows.data(), d_kept, sizeof(otr_tile_row) * nk, hipMemcpyDeviceToHost));
+  HIPCHK(hipGetLastError());
+  *out = h_tile_rows.data();
+  *n_out = nk;
   return OTR_OK;
 }
 

@@ -1501,6 +1501,68 @@ __global__ __launch_bounds__(64) void k_segments(DevGraph g, SegArgs a, unsigned
 }
 
 // ------------------------------------------------------------------------------
+// Copy-out compaction: K7 writes each trace's route / segments / ways / reports at its
+// capacity offset; one wave per trace moves them to dense arrays (offsets = scans of
+// the per-trace counts) so only used entries cross PCIe.
+// ------------------------------------------------------------------------------
+struct CompactArgs {
+  int32_t n_traces;
+  const int64_t* cap_off;
+  const int64_t* route_off;  // null: skip the route edges
+  const int64_t* seg_off;
+  const int64_t* way_off;
+  const int64_t* rep_off;
+  const SegArgs* s;          // capacity-layout arrays (device copy of the K7 arguments)
+  uint32_t* route;
+  unsigned long long* seg_id;  double* seg_start;  double* seg_end;  int32_t* seg_length;
+  int32_t* seg_queue;  uint8_t* seg_internal;  int32_t* seg_bshape;  int32_t* seg_eshape;
+  int64_t* seg_way_n;  uint32_t* seg_way;
+  unsigned long long* rep_id;  unsigned long long* rep_next;  double* rep_t0;  double* rep_t1;
+  int32_t* rep_length;  int32_t* rep_queue;
+};
+
+__global__ __launch_bounds__(64) void k_compact(CompactArgs a) {
+  const int t = blockIdx.x;
+  if (t >= a.n_traces) return;
+  const SegArgs& s = *a.s;
+  const int64_t co = a.cap_off[t];
+  const int lane = threadIdx.x;
+  if (a.route_off) {
+    const int64_t o = a.route_off[t], n = a.route_off[t + 1] - o;
+    for (int64_t k = lane; k < n; k += 64) a.route[o + k] = s.route[co + k];
+  }
+  {
+    const int64_t o = a.seg_off[t], n = a.seg_off[t + 1] - o;
+    for (int64_t k = lane; k < n; k += 64) {
+      a.seg_id[o + k] = s.seg_id[co + k];
+      a.seg_start[o + k] = s.seg_start[co + k];
+      a.seg_end[o + k] = s.seg_end[co + k];
+      a.seg_length[o + k] = s.seg_length[co + k];
+      a.seg_queue[o + k] = s.seg_queue[co + k];
+      a.seg_internal[o + k] = s.seg_internal[co + k];
+      a.seg_bshape[o + k] = s.seg_bshape[co + k];
+      a.seg_eshape[o + k] = s.seg_eshape[co + k];
+      a.seg_way_n[o + k] = s.seg_way_n[co + k];
+    }
+  }
+  {
+    const int64_t o = a.way_off[t], n = a.way_off[t + 1] - o;
+    for (int64_t k = lane; k < n; k += 64) a.seg_way[o + k] = s.seg_way[co + k];
+  }
+  {
+    const int64_t o = a.rep_off[t], n = a.rep_off[t + 1] - o;
+    for (int64_t k = lane; k < n; k += 64) {
+      a.rep_id[o + k] = s.rep_id[co + k];
+      a.rep_next[o + k] = s.rep_next[co + k];
+      a.rep_t0[o + k] = s.rep_t0[co + k];
+      a.rep_t1[o + k] = s.rep_t1[co + k];
+      a.rep_length[o + k] = s.rep_length[co + k];
+      a.rep_queue[o + k] = s.rep_queue[co + k];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------
 // K8: simple_reporter filter + hour bucketing (simple_reporter.py:176-196) into a
 // dense [hour][segment][speed bin] count histogram; one thread per trace.
 // ------------------------------------------------------------------------------
@@ -1548,6 +1610,192 @@ __global__ void k_histogram(HistArgs a) {
     }
   }
   if (rows) atomicAdd(&a.n_rows[blockIdx.x & (kShards - 1)], rows);
+}
+
+// ------------------------------------------------------------------------------
+// K9: simple_reporter tile rows (simple_reporter.py:176-196), one thread per trace:
+// pass 1 (rows == nullptr) counts each trace's rows, pass 2 writes them at row_off.
+// ------------------------------------------------------------------------------
+struct TileArgs {
+  BatchDev b;
+  const int64_t* cap_off;
+  const int64_t* rep_n;
+  const unsigned long long* rep_id;
+  const unsigned long long* rep_next;
+  const double* rep_t0;
+  const double* rep_t1;
+  const int32_t* rep_length;
+  const int32_t* rep_queue;
+  int64_t quantisation;
+  int64_t* row_cnt;        // pass 1 output
+  const int64_t* row_off;  // pass 2 input (exclusive offsets)
+  otr_tile_row* rows;      // pass 2 output
+};
+
+__global__ void k_tile_rows(TileArgs a) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.b.n_traces) return;
+  const int64_t lo = a.b.trace_off[t], hi = a.b.trace_off[t + 1];
+  int64_t k = a.rows ? a.row_off[t] : 0;
+  const int64_t k0 = k;
+  if (hi > lo) {
+    const int64_t first = a.b.time[lo], last = a.b.time[hi - 1];
+    const int64_t co = a.cap_off[t];
+    for (int64_t r = 0; r < a.rep_n[t]; ++r) {
+      const double t0 = a.rep_t0[co + r], t1 = a.rep_t1[co + r];
+      const int32_t len = a.rep_length[co + r], qu = a.rep_queue[co + r];
+      if (!bucket_keep(t0, t1, len, qu)) continue;
+      const BucketSpan sp = bucket_span(t0, t1, first, last, a.quantisation);
+      if (!sp.ok) continue;
+      const unsigned long long id = a.rep_id[co + r], nx = a.rep_next[co + r];
+      for (int64_t bk = sp.min_bucket; bk <= sp.max_bucket; ++bk, ++k) {
+        if (!a.rows) continue;
+        otr_tile_row row;
+        row.file = ((unsigned long long)bk << 25) | ((id & 7ull) << 22) | ((id >> 3) & 0x3FFFFFull);
+        row.id = id;
+        row.next_id = nx == OTR_NO_ID ? OTR_INVALID_SEGMENT_ID : nx;
+        row.start = sp.start;
+        row.end = sp.end;
+        row.duration = (int32_t)sp.duration;
+        row.length = len;
+        row.queue_length = qu;
+        row.pad = 0;
+        a.rows[k] = row;
+      }
+    }
+  }
+  if (!a.rows) a.row_cnt[t] = k - k0;
+}
+
+// Line order of simple_reporter.py:218 (segments.sort() over whole text lines).  Every
+// field before the constant tail is a non-negative decimal integer followed by ',',
+// and ',' sorts below every digit, so the string order is the field-by-field
+// lexicographic order of the digit strings (a proper prefix sorts first).
+__host__ __device__ inline int dec_digits(unsigned long long v) {
+  int n = 1;
+  while (v >= 10ull) {
+    v /= 10ull;
+    ++n;
+  }
+  return n;
+}
+__host__ __device__ inline int dec_cmp(unsigned long long a, unsigned long long b) {
+  if (a == b) return 0;
+  const int na = dec_digits(a), nb = dec_digits(b);
+  unsigned long long pa = a, pb = b;
+  for (int k = nb; k < na; ++k) pa /= 10ull;  // leading min(na, nb) digits
+  for (int k = na; k < nb; ++k) pb /= 10ull;
+  if (pa != pb) return pa < pb ? -1 : 1;
+  return na < nb ? -1 : 1;
+}
+struct TileLineLess {
+  __host__ __device__ bool operator()(const otr_tile_row& x, const otr_tile_row& y) const {
+    if (x.file != y.file) return x.file < y.file;  // files are independent: any fixed order
+    int c = dec_cmp(x.id, y.id);
+    if (!c) c = dec_cmp(x.next_id, y.next_id);
+    if (!c) c = dec_cmp((unsigned long long)x.duration, (unsigned long long)y.duration);
+    if (!c) c = dec_cmp((unsigned long long)x.length, (unsigned long long)y.length);
+    if (!c) c = dec_cmp((unsigned long long)x.queue_length, (unsigned long long)y.queue_length);
+    if (!c) c = dec_cmp((unsigned long long)x.start, (unsigned long long)y.start);
+    if (!c) c = dec_cmp((unsigned long long)x.end, (unsigned long long)y.end);
+    return c < 0;
+  }
+};
+
+// Radix keys for the line order: a non-negative integer's decimal string, left-aligned
+// in 18 base-11 digits (digit d → d + 1, padding → 0), is an integer whose numeric
+// order is the string order of the decimal strings (a proper prefix sorts first).
+// 11^18 < 2^63.  Fields are stable-sorted least significant first (LSD over fields).
+__host__ __device__ inline unsigned long long dec_key(unsigned long long v) {
+  const int n = dec_digits(v);
+  unsigned long long p = 1;
+  for (int k = 1; k < n; ++k) p *= 10ull;
+  unsigned long long key = 0;
+  for (int k = 0; k < 18; ++k) {
+    unsigned long long d = 0;
+    if (k < n) {
+      d = (v / p) % 10ull + 1ull;
+      p /= 10ull;
+    }
+    key = key * 11ull + d;
+  }
+  return key;
+}
+enum TileField { TF_FILE = 0, TF_ID, TF_NEXT, TF_DURATION, TF_LENGTH, TF_QUEUE, TF_START, TF_END, TF_COUNT };
+__global__ void k_line_key(const otr_tile_row* rows, const int32_t* perm, int64_t n, int field,
+                           unsigned long long* key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const otr_tile_row& r = rows[perm[i]];
+  unsigned long long v;
+  switch (field) {
+    case TF_FILE: key[i] = r.file; return;
+    case TF_ID: v = r.id; break;
+    case TF_NEXT: v = r.next_id; break;
+    case TF_DURATION: v = (unsigned long long)(uint32_t)r.duration; break;
+    case TF_LENGTH: v = (unsigned long long)(uint32_t)r.length; break;
+    case TF_QUEUE: v = (unsigned long long)(uint32_t)r.queue_length; break;
+    case TF_START: v = (unsigned long long)r.start; break;
+    default: v = (unsigned long long)r.end; break;
+  }
+  key[i] = dec_key(v);
+}
+__global__ void k_iota_i32(int32_t* v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = (int32_t)i;
+}
+__global__ void k_gather_rows(const otr_tile_row* in, const int32_t* idx, int64_t n, otr_tile_row* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[idx[i]];
+}
+// stream compaction by an inclusive scan of 0/1 flags: out[pos[i] - 1] = in[i]
+template <class T>
+__global__ void k_scatter_flagged(const T* in, const int64_t* flag, const int64_t* pos, int64_t n, T* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && flag[i]) out[pos[i] - 1] = in[i];
+}
+__global__ void k_scatter_index(const int64_t* flag, const int64_t* pos, int64_t n, int64_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && flag[i]) out[pos[i] - 1] = i;
+}
+
+// K10: privacy cull (simple_reporter.py:221-239), one thread per file over its sorted
+// rows.  Runs of equal (id, next_id) are kept iff at least `privacy` long — except that
+// a trailing run of length 1 is judged together with the run before it (the loop
+// reaches the last line while its range still starts at the previous run).
+__global__ void k_file_heads(const otr_tile_row* r, int64_t n, int64_t* head) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) head[i] = (i == 0 || r[i].file != r[i - 1].file) ? 1 : 0;
+}
+
+__global__ void k_cull_files(const otr_tile_row* r, int64_t n, const int64_t* file_start, int64_t n_files,
+                             int32_t privacy, int64_t* keep) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n_files) return;
+  const int64_t s = file_start[f], e = f + 1 < n_files ? file_start[f + 1] : n;
+  int64_t ps = -1, pl = 0;  // previous run, not yet judged
+  for (int64_t i = s; i < e;) {
+    int64_t j = i + 1;
+    while (j < e && r[j].id == r[i].id && r[j].next_id == r[i].next_id) ++j;
+    const int64_t len = j - i;
+    if (j == e && len == 1 && ps >= 0) {  // trailing singleton: judged with the run before
+      const int64_t k = pl + 1 >= privacy;
+      for (int64_t x = ps; x < e; ++x) keep[x] = k;
+      ps = -1;
+      break;
+    }
+    if (ps >= 0) {
+      const int64_t k = pl >= privacy;
+      for (int64_t x = ps; x < ps + pl; ++x) keep[x] = k;
+    }
+    ps = i;
+    pl = len;
+    i = j;
+  }
+  if (ps >= 0) {
+    const int64_t k = pl >= privacy;
+    for (int64_t x = ps; x < ps + pl; ++x) keep[x] = k;
+  }
 }
 
 }  // namespace otr

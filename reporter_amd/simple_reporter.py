@@ -176,3 +176,119 @@ def write_tiles(tiles, dest_dir):
         with open(path, 'w') as f:
             f.write(COLUMNS + os.linesep)
             f.write(''.join(lines))
+
+
+# ---------------------------------------------------------------------------------
+# Device tile stage: rows (K9) → sort + cull (K10) → CSV lines, and the multi-GPU
+# exchange that routes every row to the GPU owning its (hour, tile) file.
+# ---------------------------------------------------------------------------------
+def file_key(file, quantisation=3600):
+    """'{b*q}_{(b+1)*q-1}/{level}/{tile_index}' of an otr_tile_row.file (simple_reporter.py:189)."""
+    b, level, tile = int(file) >> 25, (int(file) >> 22) & LEVEL_MASK, int(file) & TILE_INDEX_MASK
+    return '%d_%d/%d/%d' % (b * quantisation, (b + 1) * quantisation - 1, level, tile)
+
+
+def file_owner(files, world):
+    """Rank owning each (hour, tile) file: a fixed mix of bucket and tile, modulo world
+    (numpy or torch int64 arrays)."""
+    return ((files >> 25) * 40503 + (files & 0x1FFFFFF)) % world
+
+
+def cull_rows(matcher, rows, privacy, device_ptr=None, n=None):
+    """otr_tiles_cull: host numpy TILE_ROW rows, or (device_ptr, n) rows in HBM →
+    kept rows (numpy, sorted in simple_reporter's line order per file)."""
+    import ctypes
+    from . import _lib
+    L = _lib.lib()
+    out, nout = ctypes.c_void_p(), ctypes.c_int64()
+    if device_ptr is not None:
+        rc = L.otr_tiles_cull(matcher._h, device_ptr, int(n), _lib.OTR_MEM_DEVICE, int(privacy), ctypes.byref(out),
+                              ctypes.byref(nout))
+    else:
+        rows = np.ascontiguousarray(rows, dtype=_lib.TILE_ROW)
+        rc = L.otr_tiles_cull(matcher._h, rows.ctypes.data if len(rows) else None, len(rows), _lib.OTR_MEM_HOST,
+                              int(privacy), ctypes.byref(out), ctypes.byref(nout))
+    if rc != 0:
+        raise RuntimeError('otr_tiles_cull failed (%d): %s' % (rc, _lib.last_error()))
+    k = nout.value
+    if k == 0:
+        return np.zeros(0, _lib.TILE_ROW)
+    buf = (ctypes.c_char * (k * _lib.TILE_ROW.itemsize)).from_address(out.value)
+    return np.frombuffer(bytes(buf), dtype=_lib.TILE_ROW)
+
+
+def rows_to_tiles(rows, quantisation=3600, mode='auto', source='smpl_rprt'):
+    """{tile_key: [lines]} from sorted rows (otr_tiles_format writes the lines)."""
+    import ctypes
+    from . import _lib
+    rows = np.ascontiguousarray(rows, dtype=_lib.TILE_ROW)
+    if len(rows) == 0:
+        return {}
+    out, n = ctypes.c_void_p(), ctypes.c_size_t()
+    rc = _lib.lib().otr_tiles_format(rows.ctypes.data, len(rows), source.encode(), mode.encode(), ctypes.byref(out),
+                                     ctypes.byref(n))
+    if rc != 0:
+        raise RuntimeError('otr_tiles_format failed: %s' % _lib.last_error())
+    lines = _lib.take_string(out, n).splitlines(True)
+    tiles = {}
+    cuts = np.flatnonzero(np.diff(rows['file'].astype(np.int64))) + 1
+    for a, b in zip(np.concatenate([[0], cuts]), np.concatenate([cuts, [len(rows)]])):
+        tiles[file_key(rows['file'][a], quantisation)] = lines[a:b]
+    return tiles
+
+
+def _window_batch(traces, inactivity):
+    from .tools.gen import Traces
+    idx_lat, idx_lon, idx_time, offs, modes = [], [], [], [0], []
+    for t in range(traces.n_traces):
+        a, b = int(traces.offsets[t]), int(traces.offsets[t + 1])
+        order = np.argsort(traces.time[a:b], kind='stable') + a  # :146 sort by time
+        tm = traces.time[order]
+        for i, j in windows(tm.tolist(), inactivity):
+            sel = order[i:j]
+            idx_lat.append(traces.lat[sel])
+            idx_lon.append(traces.lon[sel])
+            idx_time.append(traces.time[sel])
+            offs.append(offs[-1] + len(sel))
+            modes.append(traces.mode[t])
+    if len(offs) == 1:
+        return None
+    return Traces(np.concatenate(idx_lat), np.concatenate(idx_lon), np.concatenate(idx_time),
+                  np.asarray(offs, np.int64), np.asarray(modes, np.uint8))
+
+
+def report_tiles_device(matcher, traces, privacy, mode='auto', report_levels=(0, 1), transition_levels=(0, 1),
+                        quantisation=3600, inactivity=120, source='smpl_rprt', threshold_sec=15):
+    """simple_reporter match() + report() with the tile stage on device: windows → one
+    batch emitting tile rows in HBM (K9) → sort + cull in HBM (K10) → CSV lines.
+    Equals report_tiles(match_traces(...), privacy)."""
+    from . import _lib
+    batch = _window_batch(traces, inactivity)
+    if batch is None:
+        return {}
+    r = matcher.match_batch(batch, report_levels=report_levels, transition_levels=transition_levels,
+                            threshold_sec=threshold_sec, quantisation=quantisation, copy_out=False, tile_rows=True)
+    kept = cull_rows(matcher, None, privacy, device_ptr=r.d_rows, n=r.n_rows)
+    return rows_to_tiles(kept, quantisation, mode, source)
+
+
+def exchange_rows(rows, world, group=None):
+    """Route every row to the rank owning its file (all-to-all, one exchange step):
+    rows is a uint8 tensor of n*56 bytes (device for RCCL, host for gloo); returns the
+    rows this rank owns (uint8 tensor).  Owners then cull complete files locally."""
+    import torch
+    import torch.distributed as dist
+    from . import _lib
+    w = _lib.TILE_ROW.itemsize
+    r8 = rows.view(-1, w)
+    files = r8[:, 0:8].contiguous().view(torch.int64).reshape(-1)
+    owner = file_owner(files, world)
+    order = torch.argsort(owner, stable=True)
+    send = r8[order].contiguous().reshape(-1)
+    counts = torch.bincount(owner, minlength=world).to(torch.int64)
+    recv = torch.empty_like(counts)
+    dist.all_to_all_single(recv, counts, group=group)
+    out = torch.empty(int(recv.sum().item()) * w, dtype=torch.uint8, device=rows.device)
+    dist.all_to_all_single(out, send, output_split_sizes=[int(x) * w for x in recv.tolist()],
+                           input_split_sizes=[int(x) * w for x in counts.tolist()], group=group)
+    return out

@@ -1,0 +1,124 @@
+"""Tile stage on CPU: the oracle restatement pinned to the reference's cull goldens and to
+the product's bucketing mirror, the C-ABI line writer, and the 2-rank gloo exchange
+that routes rows to their file's owner (simple_reporter.py:176-239)."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import tiles as ot
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.abspath(__file__))
+CULL = json.load(open(os.path.join(HERE, 'golden', 'cull_cases.json')))['cases']
+
+
+@pytest.mark.parametrize('i', range(len(CULL)))
+def test_oracle_cull_matches_reference_goldens(i):
+    c = CULL[i]
+    assert ot.sort_and_cull(sorted(c['lines']), c['privacy']) == c['expected']
+
+
+def _oracle_workload(graph_dir, n=30, seed=5):
+    from oracle import pyoracle as po
+    from reporter_amd.tools import gen
+    path = gen.graph_path('tiny', graph_dir)
+    tr = gen.make_traces(path, n, 40, 5, 8.0, seed, t_begin=gen.T_BEGIN, t_spread=7200)
+    res = po.match_batch(po.Graph(path), tr, po.params())
+    first = tr.time[tr.offsets[:-1]]
+    last = tr.time[tr.offsets[1:] - 1]
+    return tr, res, first, last
+
+
+def _reports(res, t):
+    reps = []
+    for k in range(res['trace_rep_off'][t], res['trace_rep_off'][t + 1]):
+        d = {'id': int(res['rep_id'][k]), 't0': float(res['rep_t0'][k]), 't1': float(res['rep_t1'][k]),
+             'length': int(res['rep_length'][k]), 'queue_length': int(res['rep_queue'][k])}
+        if int(res['rep_next'][k]) != ot.NO_ID:
+            d['next_id'] = int(res['rep_next'][k])
+        reps.append(d)
+    return reps
+
+
+def test_oracle_rows_match_bucketing_mirror(graph_dir):
+    from reporter_amd import simple_reporter as sr
+    tr, res, first, last = _oracle_workload(graph_dir)
+    rows = ot.rows_from_reports(res, first, last)
+    want = {}
+    for t in range(tr.n_traces):
+        for k, v in sr.bucket(int(first[t]), int(last[t]), _reports(res, t), 3600, 'auto', 'smpl_rprt').items():
+            want.setdefault(k, []).extend(v)
+    got = {}
+    for r, line in zip(rows, ot.lines_of(rows)):
+        got.setdefault(ot.file_name(r['file']), []).append(line)
+    assert got == want and len(rows) > 0
+
+
+def test_format_lines_match_oracle(graph_dir):
+    from reporter_amd import simple_reporter as sr
+    tr, res, first, last = _oracle_workload(graph_dir)
+    rows = ot.rows_from_reports(res, first, last)
+    rows = rows[np.argsort(rows['file'], kind='stable')]  # rows_to_tiles expects rows grouped by file
+    tiles = sr.rows_to_tiles(rows, 3600, 'auto', 'smpl_rprt')
+    want = {}
+    for r, line in zip(rows, ot.lines_of(rows)):
+        want.setdefault(ot.file_name(r['file']), []).append(line)
+    assert tiles == want
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, graph_dir, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from reporter_amd import simple_reporter as sr
+    tr, res, first, last = _oracle_workload(graph_dir)
+    # each rank holds the rows of its uuid shard (simple_reporter.py:116)
+    mine = [t for t in range(tr.n_traces) if sr.shard_of(tr.uuids[t], world) == rank]
+    rows = ot.rows_from_reports(res, first, last)
+    per_trace = np.concatenate([[0], np.cumsum([len(ot.rows_from_reports(
+        {k: (v[t:t + 2] if k == 'trace_rep_off' else v) for k, v in res.items()}, first[t:t + 1], last[t:t + 1]))
+        for t in range(tr.n_traces)])])
+    sel = np.concatenate([np.arange(per_trace[t], per_trace[t + 1]) for t in mine]) if mine else np.zeros(0, int)
+    local = rows[sel.astype(np.int64)]
+    got = sr.exchange_rows(torch.from_numpy(local.view(np.uint8).copy()), world)
+    owned = got.numpy().view(ot.TILE_ROW)
+    # every received row belongs here, and owners hold complete files
+    assert np.all(sr.file_owner(owned['file'].astype(np.int64), world) == rank)
+    q.put((rank, ot.tiles(owned, 2), len(owned)))
+    dist.destroy_process_group()
+
+
+def test_two_rank_row_exchange(graph_dir):
+    tr, res, first, last = _oracle_workload(graph_dir)
+    want = ot.tiles(ot.rows_from_reports(res, first, last), 2)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank, args=(r, 2, port, graph_dir, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    outs = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    merged = {}
+    for _, t, _ in outs:
+        assert not (set(t) & set(merged))  # a file lives on exactly one owner
+        merged.update(t)
+    assert merged == want and len(want) > 0
+    assert all(n > 0 for _, _, n in outs)
