@@ -60,6 +60,9 @@ def main():
     ap.add_argument('--delta', type=float, default=None, help='routing round width (perf knob, metres)')
     ap.add_argument('--streams', type=int, default=1,
                     help='matchers (one HIP stream + host thread each) sharing the batch')
+    ap.add_argument('--tiles', type=int, default=0,
+                    help='privacy > 0: the step also runs the device tile stage (K9 rows, K10 sort + cull, '
+                         'simple_reporter.py:176-239) on each matcher (not part of the headline config)')
     args = ap.parse_args()
 
     rank = int(os.environ.get('RANK', 0))
@@ -125,13 +128,20 @@ def main():
     hist = torch.zeros(hist_len, dtype=torch.int32, device=dev)
     hist_out = torch.zeros(hist_len // world, dtype=torch.int32, device=dev)
     pool = ThreadPoolExecutor(max_workers=ns)
+    from reporter_amd import simple_reporter as sr
+    tile_stats = []
     torch.cuda.synchronize()
 
     def run_part(k):
         r = matchers[k].match_batch(parts[k], device_arrays=darrs[k], hist_device=hists[k].data_ptr(),
-                                    hist_hours=hours, hist_base_time=T_BEGIN, copy_out=False, timing=True)
+                                    hist_hours=hours, hist_base_time=T_BEGIN, copy_out=False, timing=True,
+                                    tile_rows=args.tiles > 0)
         if r.status != 0:
             raise RuntimeError('batch status %d (%d overflow tasks)' % (r.status, r.n_overflow_traces))
+        if args.tiles > 0:
+            tc = time.perf_counter()
+            kept = sr.cull_rows(matchers[k], None, args.tiles, device_ptr=r.d_rows, n=r.n_rows)
+            tile_stats.append((int(r.n_rows), len(kept), time.perf_counter() - tc))
         return r
 
     def step():
@@ -213,6 +223,8 @@ def main():
                                       % world if world > 1 else 'single GPU',
                        'streams': ns,
                        'stage_ms_per_stream': stage_ms,
+                       'tile_stage': ({'privacy': args.tiles, 'rows': tile_stats[-1][0], 'kept': tile_stats[-1][1],
+                                       'ms': round(1e3 * tile_stats[-1][2], 3)} if tile_stats else None),
                        'work': {'states': int(sum(r.n_states for r in rs)), 'grid_cells': int(counters[0]),
                                 'shape_segments_tested': int(counters[1]), 'candidates': int(counters[2]),
                                 'output_segments': int(counters[7])}},

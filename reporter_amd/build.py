@@ -104,11 +104,24 @@ def build_calib(force=False):
     return exe
 
 
+def build_loadgen(force=False):
+    """tools/loadgen: concurrent otr_report callers with/without the coalescer (bench tool)."""
+    src = os.path.join(PKG, 'tools', 'loadgen.cpp')
+    exe = os.path.join(PKG, 'tools', 'loadgen')
+    lib = os.path.join(PKG, 'libotr.so')
+    if force or not _newer(exe, [src, lib, os.path.join(ROOT, 'include', 'otr.h')]):
+        _run(['g++', '-O2', '-std=c++17', '-o', exe, src, '-L' + PKG, '-l:libotr.so', '-Wl,-rpath,' + PKG,
+              '-lpthread'])
+    return exe
+
+
 def build_all(force=False):
     build_gen(force)
     build_oracle(force)
     build_calib(force)
-    return build_otr(force)
+    lib = build_otr(force)
+    build_loadgen(force)
+    return lib
 
 
 if __name__ == '__main__':

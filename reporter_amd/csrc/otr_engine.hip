@@ -208,7 +208,7 @@ enum Slot {
   S_SEG_BSHAPE, S_SEG_ESHAPE, S_SEG_INDEX, S_SEG_N, S_SEG_WAY_N, S_SEG_WAY, S_WAY_N,
   S_REP_ID, S_REP_NEXT, S_REP_T0, S_REP_T1, S_REP_LEN, S_REP_QUEUE, S_REP_SEG, S_REP_N,
   S_SHAPE_USED, S_STATS, S_STATS_LEN, S_HIST, S_COUNTERS, S_SCAN_TMP, S_LIST, S_MISC,
-  S_ROW_CNT, S_ROW_OFF, S_ROWS, S_ROWS_IN, S_ROWS_OUT, S_ROWS_KEPT, S_IDX_A, S_IDX_B, S_KEY_A, S_KEY_B, S_POS_SCAN, S_KEEP, S_FILE_HEAD, S_FILE_START, S_NFILES, S_SORT_TMP,
+  S_ROW_CNT, S_ROW_OFF, S_ROWS, S_ROWS_IN, S_ROWS_OUT, S_ROWS_KEPT, S_IDX_A, S_IDX_B, S_KEY_A, S_KEY_B, S_POS_SCAN, S_RUN_KEEP, S_KEEP, S_FILE_HEAD, S_FILE_START, S_NFILES, S_SORT_TMP,
   S_C_ROUTE_OFF, S_C_SEG_OFF, S_C_WAY_OFF, S_C_REP_OFF, S_C_ARGS, S_C_ROUTE, S_C_SEG_ID, S_C_SEG_START,
   S_C_SEG_END, S_C_SEG_LEN, S_C_SEG_QUEUE, S_C_SEG_INTERNAL, S_C_SEG_BSHAPE, S_C_SEG_ESHAPE, S_C_SEG_WAY_N,
   S_C_SEG_WAY, S_C_SEG_WAY_OFF, S_C_REP_ID, S_C_REP_NEXT, S_C_REP_T0, S_C_REP_T1, S_C_REP_LEN, S_C_REP_QUEUE,
@@ -937,21 +937,28 @@ int Matcher::tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int pri
     std::swap(perm_a, perm_b);
   }
   k_gather_rows<<<grid_for(n, 256), 256, 0, stream>>>(d_in, perm_a, n, d);
-  // file starts: inclusive scan of head flags, scatter indices
-  k_file_heads<<<grid_for(n, 256), 256, 0, stream>>>(d, n, head);
+  // runs of equal (file, id, next_id): heads → scan → run starts; per-run decision
+  k_run_heads<<<grid_for(n, 256), 256, 0, stream>>>(d, n, head);
   size_t tb = tb_scan;
   HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, head, pos, ni, stream));
   k_scatter_index<<<grid_for(n, 256), 256, 0, stream>>>(head, pos, n, fstart);
-  int64_t nf = 0;
-  HIPCHK(hipMemcpyAsync(&nf, pos + (n - 1), 8, hipMemcpyDeviceToHost, stream));
+  int64_t nr = 0;
+  HIPCHK(hipMemcpyAsync(&nr, pos + (n - 1), 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
-  if (nf < 1 || nf > n) {
-    if (err) *err = "tile file split failed";
+  if (nr < 1 || nr > n) {
+    if (err) *err = "tile run split failed";
     return OTR_DEVICE_ERROR;
   }
-  k_cull_files<<<grid_for(nf, 64), 64, 0, stream>>>(d, n, fstart, nf, privacy, keep);
+  uint8_t* run_keep = need<uint8_t>(S_RUN_KEEP, nr);
+  if (!run_keep) {
+    if (err) *err = "device allocation failed (tiles)";
+    return OTR_DEVICE_ERROR;
+  }
+  k_cull_runs<<<grid_for(nr, 256), 256, 0, stream>>>(d, n, fstart, nr, privacy, run_keep);
+  k_row_keep<<<grid_for(n, 256), 256, 0, stream>>>(pos, run_keep, n, keep);
   tb = tb_scan;
-  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, keep, pos, ni, stream));
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, keep, head, ni, stream));  // head: reused as positions
+  std::swap(pos, head);
   k_scatter_flagged<otr_tile_row><<<grid_for(n, 256), 256, 0, stream>>>(d, keep, pos, n, d_kept);
   int64_t nk = 0;
   HIPCHK(hipMemcpyAsync(&nk, pos + (n - 1), 8, hipMemcpyDeviceToHost, stream));

@@ -1763,39 +1763,39 @@ __global__ void k_scatter_index(const int64_t* flag, const int64_t* pos, int64_t
 // rows.  Runs of equal (id, next_id) are kept iff at least `privacy` long — except that
 // a trailing run of length 1 is judged together with the run before it (the loop
 // reaches the last line while its range still starts at the previous run).
-__global__ void k_file_heads(const otr_tile_row* r, int64_t n, int64_t* head) {
+// Run-parallel form: rows → runs of equal (file, id, next_id) (head flags, scan,
+// scatter of run starts); one thread per run decides from its own length and its
+// neighbours' whether it is kept; rows inherit their run's decision.
+__global__ void k_run_heads(const otr_tile_row* r, int64_t n, int64_t* head) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) head[i] = (i == 0 || r[i].file != r[i - 1].file) ? 1 : 0;
+  if (i < n)
+    head[i] = (i == 0 || r[i].file != r[i - 1].file || r[i].id != r[i - 1].id || r[i].next_id != r[i - 1].next_id)
+                  ? 1 : 0;
 }
 
-__global__ void k_cull_files(const otr_tile_row* r, int64_t n, const int64_t* file_start, int64_t n_files,
-                             int32_t privacy, int64_t* keep) {
-  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n_files) return;
-  const int64_t s = file_start[f], e = f + 1 < n_files ? file_start[f + 1] : n;
-  int64_t ps = -1, pl = 0;  // previous run, not yet judged
-  for (int64_t i = s; i < e;) {
-    int64_t j = i + 1;
-    while (j < e && r[j].id == r[i].id && r[j].next_id == r[i].next_id) ++j;
-    const int64_t len = j - i;
-    if (j == e && len == 1 && ps >= 0) {  // trailing singleton: judged with the run before
-      const int64_t k = pl + 1 >= privacy;
-      for (int64_t x = ps; x < e; ++x) keep[x] = k;
-      ps = -1;
-      break;
-    }
-    if (ps >= 0) {
-      const int64_t k = pl >= privacy;
-      for (int64_t x = ps; x < ps + pl; ++x) keep[x] = k;
-    }
-    ps = i;
-    pl = len;
-    i = j;
+__global__ void k_cull_runs(const otr_tile_row* r, int64_t n, const int64_t* run_start, int64_t n_runs,
+                            int32_t privacy, uint8_t* run_keep) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_runs) return;
+  auto len = [&](int64_t q) { return (q + 1 < n_runs ? run_start[q + 1] : n) - run_start[q]; };
+  auto same_file = [&](int64_t p, int64_t q) { return r[run_start[p]].file == r[run_start[q]].file; };
+  const bool last = k + 1 == n_runs || !same_file(k, k + 1);
+  const int64_t L = len(k);
+  bool keep;
+  if (last) {
+    // the final run of a file: a singleton after another run is judged with it
+    keep = (L == 1 && k > 0 && same_file(k - 1, k)) ? len(k - 1) + 1 >= privacy : L >= privacy;
+  } else {
+    const bool next_last = k + 2 == n_runs || !same_file(k + 1, k + 2);
+    keep = (next_last && len(k + 1) == 1) ? L + 1 >= privacy : L >= privacy;
   }
-  if (ps >= 0) {
-    const int64_t k = pl >= privacy;
-    for (int64_t x = ps; x < ps + pl; ++x) keep[x] = k;
-  }
+  run_keep[k] = keep ? 1 : 0;
+}
+
+// row keep flag from its run (run index = inclusive scan of run heads - 1)
+__global__ void k_row_keep(const int64_t* run_pos, const uint8_t* run_keep, int64_t n, int64_t* keep) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) keep[i] = run_keep[run_pos[i] - 1];
 }
 
 }  // namespace otr
