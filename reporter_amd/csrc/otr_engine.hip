@@ -422,8 +422,8 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   k_link<<<grid_for(T, 256), 256, 0, stream>>>(b, mp, trace_state_off, state_probe, cb.count, sb);
   te(OTR_STAGE_LINK);
   if (S > 0)
-    k_tasks<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, nullptr,
-                                                  nullptr, nullptr);
+    k_tasks<<<grid_for(S, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, nullptr,
+                                                nullptr, nullptr);
   if ((rc = scan(sb.ntask, task_off, S))) return rc;
   if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
   int64_t NT = 0, NTR = 0;
@@ -438,8 +438,8 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     return OTR_DEVICE_ERROR;
   }
   if (S > 0)
-    k_tasks<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, task_off,
-                                                  task_state, task_mask);
+    k_tasks<<<grid_for(S, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, task_off,
+                                                task_state, task_mask);
   if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
   // ---- K3/K4: routing + transition costs
   RouteArgs ra{};

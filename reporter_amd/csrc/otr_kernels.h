@@ -322,39 +322,36 @@ __global__ void k_link(BatchDev b, ModeParams mp, const int64_t* trace_state_off
 // dst(e_i), so every source candidate whose edge ends at the same node shares the
 // search; the task carries the bit mask of those sources.  Pass 1 (task_off == null)
 // counts, pass 2 writes.
-__global__ void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* cand_count,
-                        const uint32_t* cand_edge, const uint32_t* edge_dst, int64_t* ntask,
-                        const int64_t* task_off, int64_t* task_state, unsigned long long* task_mask) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* cand_count,
+                                               const uint32_t* cand_edge, const uint32_t* edge_dst, int64_t* ntask,
+                                               const int64_t* task_off, int64_t* task_state,
+                                               unsigned long long* task_mask) {
+  // one wave per state, lane i = source candidate i of the previous state
+  const int64_t s = (int64_t)blockIdx.x * (blockDim.x / OTR_WAVE) + threadIdx.x / OTR_WAVE;
+  const int lane = threadIdx.x % OTR_WAVE;
   if (s >= n_states) return;
   const int64_t sp = prev[s];
   if (sp < 0 || cand_count[s] <= 0) {
-    if (!task_off) ntask[s] = 0;
+    if (!task_off && lane == 0) ntask[s] = 0;
     return;
   }
   const int Ka = cand_count[sp];
-  uint32_t root[OTR_KMAX];
-  for (int i = 0; i < Ka; ++i) root[i] = edge_dst[cand_edge[sp * OTR_KMAX + i]];
-  int64_t cnt = 0;
-  const int64_t base = task_off ? task_off[s] : 0;
-  for (int i = 0; i < Ka; ++i) {
-    bool rep = true;
-    for (int k = 0; k < i; ++k)
-      if (root[k] == root[i]) {
-        rep = false;
-        break;
-      }
-    if (!rep) continue;
-    if (task_off) {
-      unsigned long long m = 0;
-      for (int k = i; k < Ka; ++k)
-        if (root[k] == root[i]) m |= 1ull << k;
-      task_state[base + cnt] = s;
-      task_mask[base + cnt] = m;
-    }
-    ++cnt;
+  const uint32_t root = lane < Ka ? edge_dst[cand_edge[sp * OTR_KMAX + lane]] : 0xFFFFFFFFu;
+  // sources sharing my root, then: am I the lowest of them (the task's representative)?
+  unsigned long long same = 0;
+  for (int k = 0; k < Ka; ++k)
+    if ((uint32_t)__shfl((int)root, k) == root) same |= 1ull << k;
+  const bool rep = lane < Ka && (__ffsll((long long)same) - 1) == lane;
+  const unsigned long long reps = __ballot(rep);
+  if (!task_off) {
+    if (lane == 0) ntask[s] = __popcll(reps);
+    return;
   }
-  if (!task_off) ntask[s] = cnt;
+  if (rep) {
+    const int64_t o = task_off[s] + __popcll(reps & ((1ull << lane) - 1ull));
+    task_state[o] = s;
+    task_mask[o] = same;
+  }
 }
 
 // ------------------------------------------------------------------------------
@@ -467,33 +464,49 @@ constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
 #define OTR_STAMP(v) const unsigned long long v = 0
 #endif
 
-// Straight-line lower bound (mm) toward the target probe's search disk (P, r), in a
-// fixed metric whose lon scale is the cosine at the most poleward latitude the search
-// can reach, weakened by 1% and 1 m and floored to whole mm: consistent (h(u) - h(v)
-// <= len_mm(u,v) for every edge), so A* ordering never changes a label.
+// Straight-line lower bound (mm) toward the target probe's search disk (P, r) for the
+// A* order, in f32: h = trunc(990 * |v - P| - 1000 * (0.99 r + 1)) in a fixed metric
+// whose lon scale is the cosine at the most poleward latitude the search can reach
+// (both scales rounded down).  The ideal value satisfies h(u) - h(T) <= 0.99 * dist(u, T);
+// f32 evaluation moves each h by at most ~5e-7 * |v - P| + 1 mm, so the finality and
+// unreachability tests (target_resolved) carry a margin covering twice that over the
+// whole search region: labels never depend on h, whatever the edge lengths
+// (DESIGN.md §3.4).  Coordinates differ by < 2^24 micro-degrees within a search, so
+// the integer differences convert exactly.
 struct Heur {
   int32_t plat_e6, plon_e6;  // target probe rounded to micro-degrees (any fixed point keeps h consistent)
-  float mx;                  // metres per micro-degree of longitude at the most poleward latitude, rounded down
-  float c;                   // 0.99 r + 1 (m), rounded up
+  float mx, my;              // metres per micro-degree (lon at the most poleward latitude, lat), rounded down
+  float c;                   // 1000 * (0.99 r + 1), mm, rounded up
+  uint32_t margin;           // mm added to h(T) in the finality / unreachability tests
   __device__ uint32_t operator()(int32_t lat_e6, int32_t lon_e6) const {
-    const double dx = (double)(lon_e6 - plon_e6) * (double)mx;
-    const double dy = (double)(lat_e6 - plat_e6) * (kMetersPerDeg * 1e-6);
-    const double h = sqrt(dx * dx + dy * dy) * 0.99 - (double)c;
-    const double hm = floor(h * 1000.0);
-    return h > 0.0 ? (hm < 2147483647.0 ? (uint32_t)hm : 2147483647u) : 0u;
+    const float dx = (float)(lon_e6 - plon_e6) * mx;
+    const float dy = (float)(lat_e6 - plat_e6) * my;
+    const float d = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+    const float h = d * 990.0f - c;
+    return h > 0.0f ? (h < 2147483520.0f ? (uint32_t)h : 2147483520u) : 0u;
   }
 };
+
+__device__ inline float f32_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = __uint_as_float(__float_as_uint(f) - 1u);  // positive x: one ulp toward 0
+  return f;
+}
 
 __device__ inline Heur make_heur(double plat, double plon, double r, double bound) {
   double lat = fabs(plat) + 2.0 * bound / kMetersPerDeg;
   if (lat > 89.9) lat = 89.9;
-  const double mx = kMetersPerDeg * 1e-6 * cos_deg(lat);
-  float mxf = (float)mx;  // positive: one ulp toward 0 / toward +inf by the bit pattern
-  if ((double)mxf > mx) mxf = __uint_as_float(__float_as_uint(mxf) - 1u);
-  const double c = 0.99 * r + 1.0;
+  const float mx = f32_down(kMetersPerDeg * 1e-6 * cos_deg(lat));
+  const float my = f32_down(kMetersPerDeg * 1e-6);
+  const double c = 1000.0 * (0.99 * r + 1.0);
   float cf = (float)c;
   if ((double)cf < c) cf = __uint_as_float(__float_as_uint(cf) + 1u);
-  return Heur{(int32_t)llround(plat * 1e6), (int32_t)llround(plon * 1e6), mxf, cf};
+  // every node a search touches lies within ~2 * bound + r of P: relative error 1e-5
+  // (>> the f32 error of ~5e-7) over that distance, twice, plus the truncations
+  const double reach_mm = 1000.0 * (2.0 * bound + r);
+  const double m = 2e-5 * reach_mm + 8.0;
+  const uint32_t margin = m < 1e9 ? (uint32_t)m + 1u : 1000000000u;
+  return Heur{(int32_t)llround(plat * 1e6), (int32_t)llround(plon * 1e6), mx, my, cf, margin};
 }
 
 // routing bound and partial edge lengths in whole mm (shared with the oracle)
@@ -641,13 +654,14 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
   uint32_t my_settled = 0, my_relaxed = 0, my_rounds = 0;
   unsigned long long cyc[4] = {0, 0, 0, 0};
   uint32_t fmin = hroot;  // 0xFFFFFFFF: nothing pending
+  const uint32_t hTm = hT + H.margin;  // h(T) with the evaluation margin (see Heur)
   bool done = !active;
   int npend = active ? 1 : 0;  // pending-list length (group-uniform register)
   for (;;) {
     OTR_STAMP(t0);
     const int np = done ? 0 : npend;
     OTR_STAMP(t1);
-    const bool res = done || gl >= n_tgt || target_resolved(L, tslot, tpart, hT, d0min, bound_mm, fmin, np == 0);
+    const bool res = done || gl >= n_tgt || target_resolved(L, tslot, tpart, hTm, d0min, bound_mm, fmin, np == 0);
     done = done || Gr::mine(__ballot(!res)) == 0ull || np == 0;
     OTR_STAMP(t2);
     cyc[0] += t1 - t0;
