@@ -581,19 +581,22 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       pa.overflow_flag = step_ovf;
       pa.cap_flag = (int32_t*)(cnt + 1);
       tb(OTR_STAGE_PATHS);
-      k_paths<256><<<(unsigned)(8 * ((nsteps + 7) / 8)), 64, 0, stream>>>(g, pa, nullptr, (int64_t)nsteps);
+      {
+        const int64_t units = ((int64_t)nsteps + 1) / 2;  // two searches per wave
+        k_paths<160, 2><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, pa, nullptr, (int64_t)nsteps);
+      }
       te(OTR_STAGE_PATHS);
       // large-table retries for table overflows
       int64_t* rl = need<int64_t>(S_TASK_STATE, NT > (int64_t)nsteps ? NT : (int64_t)nsteps);  // reuse
       unsigned long long nretry = 0;
       tb(OTR_STAGE_PATHS_BIG);
-      for (int tier = 0; tier < 3; ++tier) {
+      for (int tier = 0; tier < 4; ++tier) {
         HIPCHK(hipMemsetAsync(cnt + 2, 0, 8, stream));
         k_collect<<<grid_for(nsteps, 1024), 1024, 0, stream>>>((int64_t)nsteps, step_ovf, rl, cnt + 2);
         HIPCHK(hipMemcpyAsync(&nretry, cnt + 2, 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
         if (nretry == 0) break;
-        if (tier == 2) {
+        if (tier == 3) {
           out->n_overflow_traces += (int32_t)nretry;
           std::vector<int64_t> il(nretry);
           HIPCHK(hipMemcpy(il.data(), rl, 8 * nretry, hipMemcpyDeviceToHost));
@@ -607,8 +610,9 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
           break;
         }
         HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
-        if (tier == 0) k_paths<1024><<<(unsigned)nretry, 64, 0, stream>>>(g, pa, rl, (int64_t)nretry);
-        else k_paths<4096><<<(unsigned)nretry, 64, 0, stream>>>(g, pa, rl, (int64_t)nretry);
+        if (tier == 0) k_paths<512, 1><<<(unsigned)nretry, 64, 0, stream>>>(g, pa, rl, (int64_t)nretry);
+        else if (tier == 1) k_paths<1024, 1><<<(unsigned)nretry, 64, 0, stream>>>(g, pa, rl, (int64_t)nretry);
+        else k_paths<4096, 1><<<(unsigned)nretry, 64, 0, stream>>>(g, pa, rl, (int64_t)nretry);
       }
       te(OTR_STAGE_PATHS_BIG);
       unsigned long long capflag = 0;

@@ -962,8 +962,16 @@ __device__ inline void argmin_lane(double c, int j, double* oc, int* oj) {
   *oj = j;
 }
 
+// Back-pointers, break flags and sub-path-end winners of a trace's states are also kept
+// in LDS (traces of up to kVitLds states, K <= 32) so the serial backtrack reads LDS
+// instead of a chain of dependent global loads; other traces use the global copies.
+constexpr int kVitLds = 128;
+
 __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long long* counters) {
   __shared__ double s_cost[OTR_KMAX];
+  __shared__ int8_t s_bp[kVitLds][32];
+  __shared__ int8_t s_brk[kVitLds];  // 1 break, 0 no break, -1 no candidates
+  __shared__ int8_t s_win[kVitLds];  // end_win of the states that end a sub-path
   const int lane = threadIdx.x;
   unsigned long long cells = 0;
   for (int t = blockIdx.x; t < a.n_traces; t += gridDim.x) {
@@ -971,9 +979,12 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
     const int64_t so = a.trace_state_off[t], eo = a.trace_state_off[t + 1];
     int64_t prev_s = -1;
     int Kp = 0;
+    bool lds_ok = eo - so <= kVitLds;  // wave-uniform: every state cached (and K <= 32, below)
     for (int64_t s = so; s < eo; ++s) {
       const int K = a.cand_count[s];
+      if (lds_ok && lane == 0) s_brk[s - so] = -1;
       if (K <= 0) continue;
+      lds_ok = lds_ok && K <= 32;
       double emis = 0.0;
       if (lane < K) emis = a.cand_sqd[s * OTR_KMAX + lane] * inv2s2;
       double cost = __builtin_huge_val();
@@ -1018,12 +1029,17 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
           int mj;
           argmin_lane(lane < Kp ? s_cost[lane] : __builtin_huge_val(), lane < Kp ? lane : OTR_KMAX, &mc, &mj);
           if (lane == 0) a.end_win[prev_s] = mj;
+          if (lds_ok && lane == 0) s_win[prev_s - so] = (int8_t)mj;
         }
         cost = emis;
         bi = -1;
       }
       if (lane < K) a.bp[s * OTR_KMAX + lane] = (int8_t)bi;
       if (lane == 0) a.brk[s] = brk ? 1 : 0;
+      if (lds_ok) {
+        if (lane < K) s_bp[s - so][lane] = (int8_t)bi;
+        if (lane == 0) s_brk[s - so] = brk ? 1 : 0;
+      }
       __syncthreads();
       if (lane < K) s_cost[lane] = cost;
       __syncthreads();
@@ -1035,10 +1051,32 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
       int mj;
       argmin_lane(lane < Kp ? s_cost[lane] : __builtin_huge_val(), lane < Kp ? lane : OTR_KMAX, &mc, &mj);
       if (lane == 0) a.end_win[prev_s] = mj;
+      if (lds_ok && lane == 0) s_win[prev_s - so] = (int8_t)mj;
     }
     __syncthreads();
     // backtrack (lane 0), then sub-path ordinals
-    if (lane == 0) {
+    if (lds_ok && lane == 0) {
+      int cur = -1;
+      bool next_brk = true;  // "state after this one starts a sub-path" (true past the end)
+      for (int64_t s = eo - 1; s >= so; --s) {
+        const int k = (int)(s - so);
+        const int b = s_brk[k];
+        if (b < 0) {
+          a.winner[s] = -1;
+          continue;
+        }
+        if (next_brk) cur = s_win[k];
+        a.winner[s] = cur;
+        if (!b) cur = s_bp[k][cur];
+        next_brk = b != 0;
+      }
+      int sp = -1;
+      for (int64_t s = so; s < eo; ++s) {
+        const int b = s_brk[s - so];
+        sp += b > 0 ? 1 : 0;
+        a.subpath[s] = b < 0 ? -1 : sp;
+      }
+    } else if (lane == 0) {
       int cur = -1;
       bool next_brk = true;  // "state after this one starts a sub-path" (true past the end)
       for (int64_t s = eo - 1; s >= so; --s) {
@@ -1097,42 +1135,57 @@ struct PathArgs {
   int32_t* cap_flag;           // global: path buffer too small
 };
 
-template <int CAP>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, int64_t n_list) {
-  __shared__ SearchLds<CAP, true> L;
-  const int lane = threadIdx.x;
-  const int64_t w = step_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_list + 7) / 8);
-  if (w >= n_list) return;
-  const int64_t k = step_list ? step_list[w] : w;
-  const int64_t s = a.steps[k];
-  const int64_t sp = a.prev[s];
-  const int wi = a.winner[sp], wj = a.winner[s];
-  const uint32_t ei = a.cand_edge[sp * OTR_KMAX + wi], ej = a.cand_edge[s * OTR_KMAX + wj];
-  const double pi = a.cand_p[sp * OTR_KMAX + wi], pj = a.cand_p[s * OTR_KMAX + wj];
-  if (ej == ei && pj >= pi) {
-    if (lane == 0) a.path_len[s] = -1;
-    return;
+// G searches per wave (G = 2 for the first tier, lanes split 32/32), each a
+// single-target search from the winner's root with predecessor labels.
+template <int CAP, int G>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 : 8, 8))) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, int64_t n_list) {
+  using Gr = Grp<G>;
+  __shared__ SearchLds<CAP, true> Ls[G];
+  const int gl = Gr::gl();
+  const int64_t n_units = (n_list + G - 1) / G;
+  const int64_t w = step_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_units + 7) / 8);
+  if (w >= n_units) return;
+  const int64_t iw = w * G + Gr::g();
+  const bool have = iw < n_list;
+  const int64_t k = have ? (step_list ? step_list[iw] : iw) : 0;
+  const int64_t s = have ? a.steps[k] : 0;
+  const int64_t sp = have ? a.prev[s] : 0;
+  bool active = false;
+  uint32_t S = 0, T = kEmpty, bmm = 0, tpart = 0, hT = 0, d0 = 0, mode_bit = 1;
+  Heur H{};
+  if (have) {
+    const int wi = a.winner[sp], wj = a.winner[s];
+    const uint32_t ei = a.cand_edge[sp * OTR_KMAX + wi], ej = a.cand_edge[s * OTR_KMAX + wj];
+    const double pi = a.cand_p[sp * OTR_KMAX + wi], pj = a.cand_p[s * OTR_KMAX + wj];
+    if (ej == ei && pj >= pi) {
+      if (gl == 0) a.path_len[s] = -1;
+    } else {
+      active = true;
+      const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+      mode_bit = 1u << mode;
+      d0 = (uint32_t)part_mm(1.0 - pi, gr.len_mm[ei]);
+      S = gr.edge_dst[ei];
+      T = gr.edge_src[ej];
+      const int64_t pb = a.state_probe[s];
+      H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], a.bound[s]);
+      const int2 tll = gr.node_ll[T];
+      hT = H(tll.x, tll.y);
+      tpart = (uint32_t)part_mm(pj, gr.len_mm[ej]);
+      bmm = (uint32_t)bound_mm_of(a.bound[s]);
+    }
   }
-  const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
-  const uint32_t mode_bit = 1u << mode;
-  const int64_t d0 = part_mm(1.0 - pi, gr.len_mm[ei]);
-  const uint32_t S = gr.edge_dst[ei], T = gr.edge_src[ej];
-  const int64_t pb = a.state_probe[s];
-  const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], a.bound[s]);
-  const int2 tll = gr.node_ll[T];
-  search_init<CAP, true, 1>(&L);
-  const bool ok = search_run<CAP, true, 1>(&L, gr, H, mode_bit, true, S, (uint32_t)bound_mm_of(a.bound[s]),
-                                           (uint32_t)(a.delta * 1000.0), lane == 0 ? T : kEmpty,
-                                           (uint32_t)part_mm(pj, gr.len_mm[ej]), H(tll.x, tll.y), (uint32_t)d0, 1,
-                                           nullptr, nullptr, nullptr);
-  if (!ok) {
-    if (lane == 0) a.overflow_flag[k] = 1;
-    return;
+  search_init<CAP, true, G>(Ls);
+  const bool ok = search_run<CAP, true, G>(Ls, gr, H, mode_bit, active, S, bmm, (uint32_t)(a.delta * 1000.0),
+                                           gl == 0 ? T : kEmpty, tpart, hT, d0, 1, nullptr, nullptr, nullptr);
+  SearchLds<CAP, true>& L = Ls[Gr::g()];
+  if (active && !ok) {
+    if (gl == 0) a.overflow_flag[k] = 1;
+    active = false;
   }
-  // walk predecessor edges T → S (lane 0), staging the edges in LDS
-  uint32_t* lp = reinterpret_cast<uint32_t*>(L.pend);  // pend+work are contiguous: CAP u32
+  // walk predecessor edges T → S (the group's lane 0), staging the edges in LDS
+  uint32_t* lp = reinterpret_cast<uint32_t*>(L.pend);  // pend+work are contiguous: >= CAP u32
   int n = 0;
-  if (lane == 0) {
+  if (active && gl == 0) {
     uint32_t v = T;
     while (v != S) {
       const int sv = lds_find(L, v);
@@ -1145,26 +1198,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
       v = gr.edge_src[e];
     }
   }
-  n = __shfl(n, 0);
+  n = __shfl(n, Gr::g() * Gr::GL);
   __syncthreads();
-  if (n < 0) {
-    if (lane == 0) a.overflow_flag[k] = 2;
-    return;
+  if (active && n < 0) {
+    if (gl == 0) a.overflow_flag[k] = 2;
+    active = false;
   }
   // bump allocation in one of 64 regions (a single cursor serialises ~1M returning
   // atomics on one address)
-  const int shard = (int)(blockIdx.x & (kShards - 1));
+  const int shard = (int)((blockIdx.x * G + Gr::g()) & (kShards - 1));
   const int64_t region = a.capacity / kShards;
   int64_t off = 0;
-  if (lane == 0) off = (int64_t)atomicAdd(&a.cursor[shard], (unsigned long long)n);
-  off = __shfl(off, 0);
-  if (off + n > region) {
-    if (lane == 0) *a.cap_flag = 1;
-    return;
+  if (active && gl == 0) off = (int64_t)atomicAdd(&a.cursor[shard], (unsigned long long)n);
+  off = __shfl(off, Gr::g() * Gr::GL);
+  if (active && off + n > region) {
+    if (gl == 0) *a.cap_flag = 1;
+    active = false;
   }
+  if (!active) return;
   off += (int64_t)shard * region;
-  for (int q = lane; q < n; q += OTR_WAVE) a.path[off + q] = lp[n - 1 - q];
-  if (lane == 0) {
+  for (int q = gl; q < n; q += Gr::GL) a.path[off + q] = lp[n - 1 - q];
+  if (gl == 0) {
     a.path_off[s] = off;
     a.path_len[s] = n;
   }
