@@ -107,6 +107,8 @@ typedef struct otr_trace_batch {
   int32_t hist_hours;
   int32_t flags;               /* OTR_BATCH_* */
   uint32_t* hist_device;       /* optional caller-owned device histogram (else library-owned) */
+  int32_t tile_rules;          /* OTR_TILE_RULES_* for OTR_BATCH_TILE_ROWS */
+  int32_t reserved;
 } otr_trace_batch;
 
 #define OTR_BATCH_COPY_OUT 1   /* fill the host arrays of otr_batch_result */
@@ -129,6 +131,17 @@ typedef struct otr_tile_row {
   int32_t pad;
 } otr_tile_row;
 #define OTR_INVALID_SEGMENT_ID 0x3fffffffffffull
+
+/* Which reference path the tile rows follow.
+ * OTR_TILE_RULES_SIMPLE: simple_reporter.py:176-196 (t1 - t0 > .5, floor/ceil hour buckets,
+ *   bucket-span limit), files sorted as text lines (:218).
+ * OTR_TILE_RULES_STREAM: the Java streaming path — Segment.valid (Segment.java:38-40) as
+ *   BatchingProcessor.forward applies it (:119-126), TimeQuantisedTile.getTiles buckets
+ *   (TimeQuantisedTile.java:26-35), files sorted by Segment.compareTo (numeric id,
+ *   next_id; stable: arrival order within a pair) and written by
+ *   Segment.appendToStringBuffer (Segment.java:59-74) as AnonymisingProcessor.store does. */
+#define OTR_TILE_RULES_SIMPLE 0
+#define OTR_TILE_RULES_STREAM 1
 
 #define OTR_NO_ID 0xFFFFFFFFFFFFFFFFull
 
@@ -185,16 +198,20 @@ int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result*
  * by file, then in the line order of segments.sort() (:218, string order of the whole
  * line), and delete the (id, next_id) runs seen fewer than `privacy` times with the
  * reference loop's exact rule (:221-239, including its trailing-singleton quirk).
+ * With rules = OTR_TILE_RULES_STREAM the order is Segment.compareTo's instead and the
+ * cull is AnonymisingProcessor.clean (AnonymisingProcessor.java:155-175, same rule).
  * rows: n rows in host (OTR_MEM_HOST) or device (OTR_MEM_DEVICE) memory, e.g. the
  * d_rows of a batch or rows received from other GPUs.  *out: the kept rows, sorted,
  * in host memory owned by the matcher (valid until its next call). */
 int otr_tiles_cull(otr_matcher* m, const otr_tile_row* rows, int64_t n, int32_t memory, int32_t privacy,
-                   const otr_tile_row** out, int64_t* n_out);
+                   int32_t rules, const otr_tile_row** out, int64_t* n_out);
 
-/* The CSV lines of n (host) rows in order, "id,next,duration,1,length,queue,start,end,
- * source,MODE\n" each (simple_reporter.py:188-195; mode is upper-cased as :195 does). */
-int otr_tiles_format(const otr_tile_row* rows, int64_t n, const char* source, const char* mode, char** out,
-                     size_t* out_len);
+/* The CSV lines of n (host) rows in order.  OTR_TILE_RULES_SIMPLE: "id,next,duration,1,
+ * length,queue,start,end,source,MODE\n" each (simple_reporter.py:188-195).
+ * OTR_TILE_RULES_STREAM: "\nid,[next],duration,1,length,queue,start,end,source,MODE"
+ * each, next empty when invalid (Segment.java:59-74).  mode is upper-cased as both do. */
+int otr_tiles_format(const otr_tile_row* rows, int64_t n, const char* source, const char* mode, int32_t rules,
+                     char** out, size_t* out_len);
 
 /* graph facts for callers sizing histograms */
 int otr_graph_info(int64_t* n_nodes, int64_t* n_edges, int64_t* n_segments);

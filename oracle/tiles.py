@@ -6,6 +6,10 @@ rows_from_reports: simple_reporter.py:176-196 (filter, duration/start/end, hour
 lines_of: simple_reporter.py:188-195 row text.
 sort_and_cull: simple_reporter.py:216-239 — whole-line string sort and the reference's
     cull loop, restated line for line (pinned by tests/golden/cull_cases.json).
+stream_rows_from_reports / stream_tiles: the Java streaming path — BatchingProcessor.java:
+    108-141 (Segment.valid), TimeQuantisedTile.java:26-35, Collections.sort by
+    Segment.compareTo (Segment.java:50-53, stable), AnonymisingProcessor.clean (:155-175,
+    the same loop), Segment.appendToStringBuffer (Segment.java:59-74).
 """
 import math
 
@@ -86,4 +90,68 @@ def tiles(rows, privacy, q=3600, source='smpl_rprt', mode='auto'):
         kept = sort_and_cull(v, privacy)
         if kept:                                    # :242-244
             out[k] = kept
+    return out
+
+
+def _java_round(x):
+    """Math.round(double): closest long, ties toward positive infinity."""
+    f = math.floor(x)
+    return int(f + 1 if x - f >= 0.5 else f)
+
+
+def stream_rows_from_reports(res, q=3600):
+    out = []
+    off = res['trace_rep_off']
+    for t in range(len(off) - 1):
+        for k in range(off[t], off[t + 1]):
+            t0, t1 = float(res['rep_t0'][k]), float(res['rep_t1'][k])
+            ln, qu = int(res['rep_length'][k]), int(res['rep_queue'][k])
+            if not (t0 > 0 and t1 > 0 and t1 > t0 and ln > 0 and qu >= 0):   # Segment.valid
+                continue
+            sid = int(res['rep_id'][k])
+            nx = int(res['rep_next'][k])
+            nx = INVALID_SEGMENT_ID if nx == NO_ID else nx                    # Segment.java:26
+            for b in range(int(t0) // q, int(t1) // q + 1):                   # getTiles: (long) casts
+                f = (b << 25) | ((sid & 7) << 22) | ((sid >> 3) & 0x3FFFFF)
+                out.append((f, sid, nx, int(math.floor(t0)), int(math.ceil(t1)), _java_round(t1 - t0), ln, qu, 0))
+    return np.array(out, dtype=TILE_ROW) if out else np.zeros(0, TILE_ROW)
+
+
+def java_clean(rows, privacy):
+    """AnonymisingProcessor.clean over rows already in Segment.compareTo order."""
+    segs = list(rows)
+    start = 0
+    i = 0
+    while i < len(segs):
+        s, e = segs[start], segs[i]
+        if s['id'] != e['id'] or s['next_id'] != e['next_id'] or i == len(segs) - 1:
+            if i == len(segs) - 1:
+                i += 1
+            if i - start < privacy:
+                del segs[start:i]
+                i = start
+            else:
+                start = i
+        i += 1
+    return segs
+
+
+def java_line(r, source, mode):
+    nx = '' if int(r['next_id']) == INVALID_SEGMENT_ID else str(int(r['next_id']))
+    return '\n%d,%s,%d,1,%d,%d,%d,%d,%s,%s' % (int(r['id']), nx, int(r['duration']), int(r['length']),
+                                              int(r['queue_length']), int(r['start']), int(r['end']), source,
+                                              mode.upper())
+
+
+def stream_tiles(rows, privacy, q=3600, source='reporter', mode='auto'):
+    """{file name: lines} of the streaming path for rows in arrival order."""
+    by_file = {}
+    for r in rows:
+        by_file.setdefault(file_name(r['file'], q), []).append(r)
+    out = {}
+    for k, v in by_file.items():
+        v = sorted(v, key=lambda r: (int(r['id']), int(r['next_id'])))  # stable, as Collections.sort
+        kept = java_clean(v, privacy)
+        if kept:
+            out[k] = [java_line(r, source, mode) for r in kept]
     return out

@@ -17,6 +17,8 @@ OTR_BATCH_COPY_OUT = 1
 OTR_BATCH_TIMING = 2
 OTR_BATCH_COPY_REPORTS = 4
 OTR_BATCH_TILE_ROWS = 8
+OTR_TILE_RULES_SIMPLE = 0
+OTR_TILE_RULES_STREAM = 1
 OTR_NO_ID = 0xFFFFFFFFFFFFFFFF
 HIST_BINS = 8
 KMAX = 64
@@ -37,7 +39,7 @@ class TraceBatch(ctypes.Structure):
                 ('report_levels', ctypes.c_uint32), ('transition_levels', ctypes.c_uint32),
                 ('threshold_sec', ctypes.c_int32), ('quantisation', ctypes.c_int32),
                 ('hist_base_time', ctypes.c_int64), ('hist_hours', ctypes.c_int32), ('flags', ctypes.c_int32),
-                ('hist_device', ctypes.c_void_p)]
+                ('hist_device', ctypes.c_void_p), ('tile_rules', ctypes.c_int32), ('reserved', ctypes.c_int32)]
 
 
 class BatchResult(ctypes.Structure):
@@ -107,9 +109,9 @@ def lib():
                                    ctypes.c_int, P(ctypes.c_int32), P(ctypes.c_void_p), P(ctypes.c_size_t)]
     L.otr_coalesce.argtypes = [ctypes.c_int32, ctypes.c_int32]
     L.otr_tiles_cull.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
-                                 P(ctypes.c_void_p), P(ctypes.c_int64)]
+                                 ctypes.c_int32, P(ctypes.c_void_p), P(ctypes.c_int64)]
     L.otr_tiles_format.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_char_p,
-                                   P(ctypes.c_void_p), P(ctypes.c_size_t)]
+                                   ctypes.c_int32, P(ctypes.c_void_p), P(ctypes.c_size_t)]
     _L = L
     return L
 

@@ -305,37 +305,40 @@ int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result*
 
 // simple_reporter.py:211-239 (sort + privacy cull) on device
 int otr_tiles_cull(otr_matcher* m, const otr_tile_row* rows, int64_t n, int32_t memory, int32_t privacy,
-                   const otr_tile_row** out, int64_t* n_out) {
+                   int32_t rules, const otr_tile_row** out, int64_t* n_out) {
   if (!m || !out || !n_out || (n > 0 && !rows)) {
     g_last_error = "null argument";
     return OTR_BAD_REQUEST;
   }
   std::string err;
-  const int rc = m->m.tiles_cull(rows, n, memory, privacy, out, n_out, &err);
+  const int rc = m->m.tiles_cull(rows, n, memory, privacy, rules, out, n_out, &err);
   if (rc != OTR_OK) g_last_error = err;
   return rc;
 }
 
 // simple_reporter.py:188-195: ','.join([id, next, duration, '1', length, queue, start, end,
 // source, mode.upper()]) + os.linesep
-int otr_tiles_format(const otr_tile_row* rows, int64_t n, const char* source, const char* mode, char** out,
-                     size_t* out_len) {
+// Segment.appendToStringBuffer (Segment.java:59-74) for OTR_TILE_RULES_STREAM
+int otr_tiles_format(const otr_tile_row* rows, int64_t n, const char* source, const char* mode, int32_t rules,
+                     char** out, size_t* out_len) {
   if ((n > 0 && !rows) || !out) {
     g_last_error = "null argument";
     return OTR_BAD_REQUEST;
   }
+  const bool stream = rules == OTR_TILE_RULES_STREAM;
   std::string tail = ",";
   tail += source ? source : "";
   tail += ",";
   for (const char* c = mode ? mode : ""; *c; ++c) tail.push_back((*c >= 'a' && *c <= 'z') ? (char)(*c - 32) : *c);
-  tail += "\n";
+  if (!stream) tail += "\n";
   std::string o;
   o.reserve((size_t)(n > 0 ? n : 0) * (72 + tail.size()));
   for (int64_t k = 0; k < n; ++k) {
     const otr_tile_row& r = rows[k];
+    if (stream) o.push_back('\n');
     otrfmt::put_u64(o, r.id);
     o.push_back(',');
-    otrfmt::put_u64(o, r.next_id);
+    if (!stream || r.next_id != OTR_INVALID_SEGMENT_ID) otrfmt::put_u64(o, r.next_id);
     o.push_back(',');
     otrfmt::put_i64(o, r.duration);
     o += ",1,";

@@ -60,7 +60,7 @@ struct Matcher {
   template <class T>
   T* need(int slot, size_t n);
   int run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err);
-  int tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int privacy, const otr_tile_row** out,
+  int tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int privacy, int rules, const otr_tile_row** out,
                  int64_t* n_out, std::string* err);
   ~Matcher();
 };

@@ -724,6 +724,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     ta.rep_length = sa.rep_length;
     ta.rep_queue = sa.rep_queue;
     ta.quantisation = ha.quantisation;
+    ta.rules = in->tile_rules;
     ta.row_cnt = need<int64_t>(S_ROW_CNT, T);
     k_tile_rows<<<grid_for(T, 256), 256, 0, stream>>>(ta);
     int64_t* row_off = need<int64_t>(S_ROW_OFF, T + 1);
@@ -891,7 +892,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
 
 // Tile stage: sort rows into simple_reporter's line order per file, then cull
 // (K10).  Result rows are copied to host (matcher-owned).
-int Matcher::tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int privacy,
+int Matcher::tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int privacy, int rules,
                         const otr_tile_row** out, int64_t* n_out, std::string* err) {
   GraphState& gs = graph_state();
   HIPCHK(hipSetDevice(gs.device));
@@ -931,13 +932,16 @@ int Matcher::tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int pri
     if (err) *err = "device allocation failed (tiles)";
     return OTR_DEVICE_ERROR;
   }
-  // LSD over the line's fields: stable radix passes, least significant field first
+  // LSD over the sort fields: stable radix passes, least significant field first (the
+  // identity start keeps arrival order within equal keys)
   k_iota_i32<<<grid_for(n, 256), 256, 0, stream>>>(perm_a, n);
-  for (int f = TF_COUNT - 1; f >= 0; --f) {
-    k_line_key<<<grid_for(n, 256), 256, 0, stream>>>(d_in, perm_a, n, f, key_a);
+  const bool pair_order = rules == OTR_TILE_RULES_STREAM;
+  for (int f = pair_order ? TF_NEXT : TF_COUNT - 1; f >= 0; --f) {
+    if (pair_order) k_pair_key<<<grid_for(n, 256), 256, 0, stream>>>(d_in, perm_a, n, f, key_a);
+    else k_line_key<<<grid_for(n, 256), 256, 0, stream>>>(d_in, perm_a, n, f, key_a);
     size_t tb = tb_sort;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key_a, key_b, perm_a, perm_b, ni, 0, f == TF_FILE ? 64 : 63,
-                                              stream));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key_a, key_b, perm_a, perm_b, ni, 0,
+                                              (f == TF_FILE || pair_order) ? 64 : 63, stream));
     std::swap(perm_a, perm_b);
   }
   k_gather_rows<<<grid_for(n, 256), 256, 0, stream>>>(d_in, perm_a, n, d);

@@ -84,9 +84,16 @@ __device__ inline bool project_edge(const DevGraph& g, uint4 rec, uint32_t mode_
   double best = __builtin_huge_val();
   double best_along = 0.0, bqx = 0.0, bqy = 0.0, acc = 0.0;
   const uint32_t k0 = rec.y, k1 = rec.z;
-  int2 pa = g.shape_ll[k0];
+  // the first kPre points are loaded together (one memory round trip instead of one per
+  // point); longer polylines continue point by point
+  constexpr uint32_t kPre = 4;
+  int2 pre[kPre];
+#pragma unroll
+  for (uint32_t i = 0; i < kPre; ++i) pre[i] = k0 + i < k1 ? g.shape_ll[k0 + i] : make_int2(0, 0);
+  int2 pa = pre[0];
   for (uint32_t k = k0; k + 1 < k1; ++k) {
-    const int2 pb = g.shape_ll[k + 1];
+    const uint32_t i = k + 1 - k0;
+    const int2 pb = i < kPre ? (i == 1 ? pre[1] : (i == 2 ? pre[2] : pre[3])) : g.shape_ll[k + 1];
     const double ax = (e6(pa.y) - plon) * mpl;
     const double ay = (e6(pa.x) - plat) * kMetersPerDeg;
     const double bx = (e6(pb.y) - plon) * mpl;
@@ -1695,6 +1702,7 @@ struct TileArgs {
   const int32_t* rep_length;
   const int32_t* rep_queue;
   int64_t quantisation;
+  int32_t rules;           // OTR_TILE_RULES_*: simple_reporter.py or the Java streaming path
   int64_t* row_cnt;        // pass 1 output
   const int64_t* row_off;  // pass 2 input (exclusive offsets)
   otr_tile_row* rows;      // pass 2 output
@@ -1712,9 +1720,22 @@ __global__ void k_tile_rows(TileArgs a) {
     for (int64_t r = 0; r < a.rep_n[t]; ++r) {
       const double t0 = a.rep_t0[co + r], t1 = a.rep_t1[co + r];
       const int32_t len = a.rep_length[co + r], qu = a.rep_queue[co + r];
-      if (!bucket_keep(t0, t1, len, qu)) continue;
-      const BucketSpan sp = bucket_span(t0, t1, first, last, a.quantisation);
-      if (!sp.ok) continue;
+      BucketSpan sp;
+      if (a.rules == OTR_TILE_RULES_STREAM) {
+        // BatchingProcessor.java:119-126 (Segment.valid, Segment.java:38-40) and
+        // TimeQuantisedTile.getTiles (TimeQuantisedTile.java:26-35): buckets from the
+        // truncated times, no span limit; duration Math.round (ties up), Segment.java:65-71
+        if (!(t0 > 0 && t1 > 0 && t1 > t0 && len > 0 && qu >= 0)) continue;
+        sp.duration = py2_round_int(t1 - t0);
+        sp.start = (int64_t)floor(t0);
+        sp.end = (int64_t)ceil(t1);
+        sp.min_bucket = (int64_t)t0 / a.quantisation;
+        sp.max_bucket = (int64_t)t1 / a.quantisation;
+      } else {
+        if (!bucket_keep(t0, t1, len, qu)) continue;
+        sp = bucket_span(t0, t1, first, last, a.quantisation);
+        if (!sp.ok) continue;
+      }
       const unsigned long long id = a.rep_id[co + r], nx = a.rep_next[co + r];
       for (int64_t bk = sp.min_bucket; bk <= sp.max_bucket; ++bk, ++k) {
         if (!a.rows) continue;
@@ -1790,6 +1811,15 @@ __host__ __device__ inline unsigned long long dec_key(unsigned long long v) {
   return key;
 }
 enum TileField { TF_FILE = 0, TF_ID, TF_NEXT, TF_DURATION, TF_LENGTH, TF_QUEUE, TF_START, TF_END, TF_COUNT };
+// Segment.compareTo (Segment.java:50-53): numeric (id, next_id), stable
+// (Collections.sort keeps arrival order within equal keys)
+__global__ void k_pair_key(const otr_tile_row* rows, const int32_t* perm, int64_t n, int field,
+                           unsigned long long* key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const otr_tile_row& r = rows[perm[i]];
+  key[i] = field == TF_FILE ? r.file : (field == TF_ID ? r.id : r.next_id);
+}
 __global__ void k_line_key(const otr_tile_row* rows, const int32_t* perm, int64_t n, int field,
                            unsigned long long* key) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

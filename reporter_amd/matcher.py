@@ -116,7 +116,7 @@ class Matcher:
     # --- batched API ----------------------------------------------------------------
     def match_batch(self, traces, report_levels=(0, 1), transition_levels=(0, 1), threshold_sec=15,
                     quantisation=3600, hist_base_time=0, hist_hours=0, copy_out=True, timing=False,
-                    device_arrays=None, hist_device=None, tile_rows=False):
+                    device_arrays=None, hist_device=None, tile_rows=False, tile_rules=0):
         """Match a gen.Traces-like SoA batch.  With device_arrays (dict of device
         pointers: trace_offsets, lat, lon, time, accuracy, mode) the inputs are
         already resident in HBM."""
@@ -146,6 +146,7 @@ class Matcher:
         b.hist_base_time = hist_base_time
         b.hist_hours = hist_hours
         b.hist_device = hist_device
+        b.tile_rules = int(tile_rules)
         b.flags = (_lib.OTR_BATCH_COPY_OUT if copy_out else 0) | (_lib.OTR_BATCH_TIMING if timing else 0) | \
             (_lib.OTR_BATCH_TILE_ROWS if tile_rows else 0)
         r = _lib.BatchResult()

@@ -194,20 +194,21 @@ def file_owner(files, world):
     return ((files >> 25) * 40503 + (files & 0x1FFFFFF)) % world
 
 
-def cull_rows(matcher, rows, privacy, device_ptr=None, n=None):
+def cull_rows(matcher, rows, privacy, device_ptr=None, n=None, rules=0):
     """otr_tiles_cull: host numpy TILE_ROW rows, or (device_ptr, n) rows in HBM →
-    kept rows (numpy, sorted in simple_reporter's line order per file)."""
+    kept rows (numpy, sorted per file in simple_reporter's line order, or with
+    rules=OTR_TILE_RULES_STREAM in Segment.compareTo order)."""
     import ctypes
     from . import _lib
     L = _lib.lib()
     out, nout = ctypes.c_void_p(), ctypes.c_int64()
     if device_ptr is not None:
-        rc = L.otr_tiles_cull(matcher._h, device_ptr, int(n), _lib.OTR_MEM_DEVICE, int(privacy), ctypes.byref(out),
-                              ctypes.byref(nout))
+        rc = L.otr_tiles_cull(matcher._h, device_ptr, int(n), _lib.OTR_MEM_DEVICE, int(privacy), int(rules),
+                              ctypes.byref(out), ctypes.byref(nout))
     else:
         rows = np.ascontiguousarray(rows, dtype=_lib.TILE_ROW)
         rc = L.otr_tiles_cull(matcher._h, rows.ctypes.data if len(rows) else None, len(rows), _lib.OTR_MEM_HOST,
-                              int(privacy), ctypes.byref(out), ctypes.byref(nout))
+                              int(privacy), int(rules), ctypes.byref(out), ctypes.byref(nout))
     if rc != 0:
         raise RuntimeError('otr_tiles_cull failed (%d): %s' % (rc, _lib.last_error()))
     k = nout.value
@@ -217,19 +218,24 @@ def cull_rows(matcher, rows, privacy, device_ptr=None, n=None):
     return np.frombuffer(bytes(buf), dtype=_lib.TILE_ROW)
 
 
-def rows_to_tiles(rows, quantisation=3600, mode='auto', source='smpl_rprt'):
-    """{tile_key: [lines]} from sorted rows (otr_tiles_format writes the lines)."""
+def rows_to_tiles(rows, quantisation=3600, mode='auto', source='smpl_rprt', rules=0):
+    """{tile_key: [lines]} from rows grouped by file (otr_tiles_format writes the lines;
+    with rules=OTR_TILE_RULES_STREAM each line is '\n' + fields as Segment.java:59-74)."""
     import ctypes
     from . import _lib
     rows = np.ascontiguousarray(rows, dtype=_lib.TILE_ROW)
     if len(rows) == 0:
         return {}
     out, n = ctypes.c_void_p(), ctypes.c_size_t()
-    rc = _lib.lib().otr_tiles_format(rows.ctypes.data, len(rows), source.encode(), mode.encode(), ctypes.byref(out),
-                                     ctypes.byref(n))
+    rc = _lib.lib().otr_tiles_format(rows.ctypes.data, len(rows), source.encode(), mode.encode(), int(rules),
+                                     ctypes.byref(out), ctypes.byref(n))
     if rc != 0:
         raise RuntimeError('otr_tiles_format failed: %s' % _lib.last_error())
-    lines = _lib.take_string(out, n).splitlines(True)
+    text = _lib.take_string(out, n)
+    if rules == _lib.OTR_TILE_RULES_STREAM:
+        lines = ['\n' + l for l in text.split('\n')[1:]]
+    else:
+        lines = text.splitlines(True)
     tiles = {}
     cuts = np.flatnonzero(np.diff(rows['file'].astype(np.int64))) + 1
     for a, b in zip(np.concatenate([[0], cuts]), np.concatenate([cuts, [len(rows)]])):
@@ -270,6 +276,21 @@ def report_tiles_device(matcher, traces, privacy, mode='auto', report_levels=(0,
                             threshold_sec=threshold_sec, quantisation=quantisation, copy_out=False, tile_rows=True)
     kept = cull_rows(matcher, None, privacy, device_ptr=r.d_rows, n=r.n_rows)
     return rows_to_tiles(kept, quantisation, mode, source)
+
+
+def stream_tiles_device(matcher, traces, privacy, mode='auto', report_levels=(0, 1), transition_levels=(0, 1),
+                        quantisation=3600, source='reporter', threshold_sec=15):
+    """The Java streaming path's output stage on device: report() reports → Segment
+    (BatchingProcessor.java:108-141) → TimeQuantisedTile buckets → Collections.sort +
+    clean (AnonymisingProcessor.java:155-175, 223-266) → Segment lines.  Returns
+    {"{start}_{start+q-1}/{level}/{tile}": [lines]} (AnonymisingProcessor.store names the
+    file under that directory source.UUID, :185-188)."""
+    from . import _lib
+    r = matcher.match_batch(traces, report_levels=report_levels, transition_levels=transition_levels,
+                            threshold_sec=threshold_sec, quantisation=quantisation, copy_out=False, tile_rows=True,
+                            tile_rules=_lib.OTR_TILE_RULES_STREAM)
+    kept = cull_rows(matcher, None, privacy, device_ptr=r.d_rows, n=r.n_rows, rules=_lib.OTR_TILE_RULES_STREAM)
+    return rows_to_tiles(kept, quantisation, mode, source, rules=_lib.OTR_TILE_RULES_STREAM)
 
 
 def exchange_rows(rows, world, group=None):

@@ -100,3 +100,30 @@ def test_report_tiles_device_equals_host_path(city):
     want = sr.report_tiles(sr.match_traces(m, tr), 2)
     got = sr.report_tiles_device(m, tr, 2)
     assert got == want and len(got) > 0
+
+
+@pytest.fixture(scope='module')
+def stream_workload(city):
+    tr = gen.make_traces(city, 120, 120, 10, 8.0, 33, t_begin=gen.T_BEGIN, t_spread=3 * 3600)
+    want = po.match_batch(po.Graph(city), tr, po.params(), threads=8)
+    return tr, ot.stream_rows_from_reports(want)
+
+
+def test_stream_rows_equal_restatement(stream_workload):
+    import torch
+    tr, want = stream_workload
+    m = M.Matcher()
+    r = m.match_batch(tr, copy_out=False, tile_rows=True, tile_rules=_lib.OTR_TILE_RULES_STREAM)
+    w = _lib.TILE_ROW.itemsize
+    got = torch.as_tensor(_DevArr(r.d_rows, int(r.n_rows) * w), device='cuda').clone().cpu().numpy()
+    got = got.view(_lib.TILE_ROW)
+    assert len(got) == len(want) > 100
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize('privacy', [1, 2, 3])
+def test_stream_cull_equals_restatement(stream_workload, privacy):
+    tr, want_rows = stream_workload
+    m = M.Matcher()
+    got = sr.stream_tiles_device(m, tr, privacy, source='reporter')
+    assert got == ot.stream_tiles(want_rows, privacy, source='reporter')

@@ -19,7 +19,7 @@ def test_exports_match_header():
 
 def test_struct_layout():
     # otr_trace_batch / otr_batch_result sizes must match the C declarations
-    assert ctypes.sizeof(_lib.TraceBatch) == 4 + 4 + 6 * 8 + 4 * 4 + 8 + 4 + 4 + 8
+    assert ctypes.sizeof(_lib.TraceBatch) == 4 + 4 + 6 * 8 + 4 * 4 + 8 + 4 + 4 + 8 + 4 + 4
     assert ctypes.sizeof(_lib.BatchResult) > 0
 
 

@@ -122,3 +122,40 @@ def test_two_rank_row_exchange(graph_dir):
         merged.update(t)
     assert merged == want and len(want) > 0
     assert all(n > 0 for _, _, n in outs)
+
+
+def test_java_clean_matches_python_cull_on_numeric_order():
+    """AnonymisingProcessor.clean and simple_reporter's loop are the same rule: on rows
+    whose ids have equal digit counts (string order == numeric order) they agree."""
+    rng = np.random.default_rng(3)
+    for trial in range(200):
+        n = int(rng.integers(1, 14))
+        rows = np.zeros(n, ot.TILE_ROW)
+        rows['id'] = 8 * rng.integers(100, 104, n) + 2
+        rows['next_id'] = 8 * rng.integers(100, 102, n)
+        rows['duration'] = rng.integers(10, 20, n)
+        rows['start'] = 1483228800 + rng.integers(0, 9, n)
+        rows['end'] = rows['start'] + rows['duration']
+        rows['length'] = 50
+        order = np.lexsort((np.arange(n), rows['next_id'], rows['id']))
+        for p in (1, 2, 3):
+            kept = ot.java_clean(rows[order], p)
+            pairs = [(int(r['id']), int(r['next_id'])) for r in kept]
+            lines = ot.sort_and_cull(ot.lines_of(rows), p)
+            want = [(int(l.split(',')[0]), int(l.split(',')[1])) for l in lines]
+            assert pairs == want
+
+
+def test_stream_format_matches_oracle(graph_dir):
+    from reporter_amd import _lib
+    from reporter_amd import simple_reporter as sr
+    tr, res, first, last = _oracle_workload(graph_dir)
+    rows = ot.stream_rows_from_reports(res)
+    rows = rows[np.argsort(rows['file'], kind='stable')]
+    got = sr.rows_to_tiles(rows, 3600, 'auto', 'reporter', rules=_lib.OTR_TILE_RULES_STREAM)
+    want = {}
+    for r in rows:
+        want.setdefault(ot.file_name(r['file']), []).append(ot.java_line(r, 'reporter', 'auto'))
+    assert got == want and len(rows) > 0
+    # INVALID next ids print as an empty field (Segment.java:62-64)
+    assert any(l.split(',')[1] == '' for v in got.values() for l in v)
