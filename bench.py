@@ -58,7 +58,7 @@ def main():
     ap.add_argument('--cpu-traces', type=int, default=1500, help='bounded oracle sample (0 = skip)')
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--delta', type=float, default=None, help='routing round width (perf knob, metres)')
-    ap.add_argument('--streams', type=int, default=1,
+    ap.add_argument('--streams', type=int, default=2,
                     help='matchers (one HIP stream + host thread each) sharing the batch')
     ap.add_argument('--tiles', type=int, default=0,
                     help='privacy > 0: the step also runs the device tile stage (K9 rows, K10 sort + cull, '
