@@ -208,7 +208,7 @@ enum Slot {
   S_SEG_BSHAPE, S_SEG_ESHAPE, S_SEG_INDEX, S_SEG_N, S_SEG_WAY_N, S_SEG_WAY, S_WAY_N,
   S_REP_ID, S_REP_NEXT, S_REP_T0, S_REP_T1, S_REP_LEN, S_REP_QUEUE, S_REP_SEG, S_REP_N,
   S_SHAPE_USED, S_STATS, S_STATS_LEN, S_HIST, S_COUNTERS, S_SCAN_TMP, S_LIST, S_MISC,
-  S_ROW_CNT, S_ROW_OFF, S_ROWS, S_ROWS_IN, S_ROWS_OUT, S_ROWS_KEPT, S_IDX_A, S_IDX_B, S_KEY_A, S_KEY_B, S_POS_SCAN, S_RUN_KEEP, S_KEEP, S_FILE_HEAD, S_FILE_START, S_NFILES, S_SORT_TMP,
+  S_HEUR, S_CPREP, S_ROW_CNT, S_ROW_OFF, S_ROWS, S_ROWS_IN, S_ROWS_OUT, S_ROWS_KEPT, S_IDX_A, S_IDX_B, S_KEY_A, S_KEY_B, S_POS_SCAN, S_RUN_KEEP, S_KEEP, S_FILE_HEAD, S_FILE_START, S_NFILES, S_SORT_TMP,
   S_C_ROUTE_OFF, S_C_SEG_OFF, S_C_WAY_OFF, S_C_REP_OFF, S_C_ARGS, S_C_ROUTE, S_C_SEG_ID, S_C_SEG_START,
   S_C_SEG_END, S_C_SEG_LEN, S_C_SEG_QUEUE, S_C_SEG_INTERNAL, S_C_SEG_BSHAPE, S_C_SEG_ESHAPE, S_C_SEG_WAY_N,
   S_C_SEG_WAY, S_C_SEG_WAY_OFF, S_C_REP_ID, S_C_REP_NEXT, S_C_REP_T0, S_C_REP_T1, S_C_REP_LEN, S_C_REP_QUEUE,
@@ -462,6 +462,27 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   ra.lat = b.lat;
   ra.lon = b.lon;
   ra.radius = cb.radius;
+  // K2b: per-state search inputs
+  PrepArgs pr{};
+  pr.n_states = S;
+  pr.prev = sb.prev;
+  pr.bound = sb.bound;
+  pr.cand_count = cb.count;
+  pr.cand_edge = cb.edge;
+  pr.cand_p = cb.p;
+  pr.state_probe = state_probe;
+  pr.lat = b.lat;
+  pr.lon = b.lon;
+  pr.radius = cb.radius;
+  pr.heur = need<Heur>(S_HEUR, S);
+  pr.cprep = need<uint4>(S_CPREP, (size_t)S * OTR_KMAX);
+  if (!pr.heur || !pr.cprep) {
+    if (err) *err = "device allocation failed (prep)";
+    return OTR_DEVICE_ERROR;
+  }
+  if (S > 0) k_prep<<<grid_for(S, 4), 256, 0, stream>>>(g, pr);
+  ra.heur = pr.heur;
+  ra.cprep = pr.cprep;
   ra.delta = mp.delta;
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
   ra.overflow_flag = task_ovf;
@@ -572,6 +593,8 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       pa.lat = b.lat;
       pa.lon = b.lon;
       pa.radius = cb.radius;
+      pa.heur = ra.heur;
+      pa.cprep = ra.cprep;
       pa.delta = mp.delta;
       pa.path_off = path_off;
       pa.path_len = path_len;

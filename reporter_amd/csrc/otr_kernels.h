@@ -783,6 +783,47 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
 }
 
 // ------------------------------------------------------------------------------
+// K2b: per-state search inputs, computed once per state instead of once per search
+// task (a step has ~9 tasks): the A* heuristic of the step ending at the state, and per
+// candidate j {entry part mm, source node, h(source node), exit part mm}.
+// ------------------------------------------------------------------------------
+struct PrepArgs {
+  int64_t n_states;
+  const int64_t* prev;
+  const double* bound;
+  const int32_t* cand_count;
+  const uint32_t* cand_edge;
+  const double* cand_p;
+  const int64_t* state_probe;
+  const double* lat;
+  const double* lon;
+  const double* radius;
+  Heur* heur;     // [S]
+  uint4* cprep;   // [S][OTR_KMAX]: {part(p), src(e), h(src(e)), part(1 - p)}
+};
+
+__global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
+  const int64_t s = (int64_t)blockIdx.x * (blockDim.x / OTR_WAVE) + threadIdx.x / OTR_WAVE;
+  const int lane = threadIdx.x % OTR_WAVE;
+  if (s >= a.n_states) return;
+  const int K = a.cand_count[s];
+  if (K <= 0) return;
+  const int64_t pb = a.state_probe[s];
+  const double bound = a.prev[s] >= 0 ? a.bound[s] : 0.0;  // set by k_link for steps only
+  const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], bound);
+  if (lane == 0) a.heur[s] = H;
+  if (lane < K) {
+    const uint32_t e = a.cand_edge[s * OTR_KMAX + lane];
+    const double p = a.cand_p[s * OTR_KMAX + lane];
+    const uint32_t len = g.len_mm[e];
+    const uint32_t tn = g.edge_src[e];
+    const int2 ll = g.node_ll[tn];
+    a.cprep[s * OTR_KMAX + lane] =
+        make_uint4((uint32_t)part_mm(p, len), tn, H(ll.x, ll.y), (uint32_t)part_mm(1.0 - p, len));
+  }
+}
+
+// ------------------------------------------------------------------------------
 // K3 + K4: one wave per (step, search root): search, then transition costs for
 // every source candidate sharing the root.
 // ------------------------------------------------------------------------------
@@ -806,6 +847,8 @@ struct RouteArgs {
   const double* lat;
   const double* lon;
   const double* radius;       // per state search radius (heuristic disk)
+  const Heur* heur;           // per state (k_prep)
+  const uint4* cprep;         // per state candidate (k_prep)
   double delta;
   double inv_beta[OTR_MODES];
   int32_t* overflow_flag;     // per task
@@ -843,28 +886,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
     uint32_t ej = 0;
     double pj = 0;
     bool needed = false;
+    uint4 cq = make_uint4(0u, 0u, 0u, 0u);
     if (have && lane < Kb) {
       ej = a.cand_edge[s * OTR_KMAX + lane];
       pj = a.cand_p[s * OTR_KMAX + lane];
-      tpart = (uint32_t)part_mm(pj, gr.len_mm[ej]);
+      cq = a.cprep[s * OTR_KMAX + lane];
+      tpart = cq.x;
     }
     for (unsigned long long m = mask; m; m &= m - 1) {
       const int i = __ffsll((long long)m) - 1;
       const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
       const double pi = a.cand_p[sp * OTR_KMAX + i];
-      const uint32_t d0 = (uint32_t)part_mm(1.0 - pi, gr.len_mm[ei]);
+      const uint32_t d0 = a.cprep[sp * OTR_KMAX + i].w;
       d0min = d0 < d0min ? d0 : d0min;
       if (lane < Kb && !(ej == ei && pj >= pi)) needed = true;
     }
     forced = have && a.forced[s];
     const unsigned long long need_mask = __ballot(needed);
     search = have && fits && !forced && Gr::mine(need_mask) != 0ull;
-    const int64_t pb = a.state_probe[s];
-    H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], a.bound[s]);
+    H = a.heur[s];
     if (needed) {
-      tnode = gr.edge_src[ej];
-      const int2 tll = gr.node_ll[tnode];
-      hT = H(tll.x, tll.y);
+      tnode = cq.y;
+      hT = cq.z;
     }
   }
   unsigned long long settled = 0, relaxed = 0, rounds = 0;
@@ -897,7 +940,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
         int64_t r = -1;
         if (forced) r = -1;
         else if (ej == ei && pj >= pi) r = part_mm(pj - pi, gr.len_mm[ei]);
-        else if (lab >= 0) r = part_mm(1.0 - pi, gr.len_mm[ei]) + lab + tpart;
+        else if (lab >= 0) r = (int64_t)a.cprep[sp * OTR_KMAX + i].w + lab + tpart;
         trow[(int64_t)i * Kb + lane] =
             (r >= 0 && r <= (int64_t)bmm) ? fabs((double)r / 1000.0 - gcd) * inv_beta : __builtin_huge_val();
       }
@@ -1132,6 +1175,8 @@ struct PathArgs {
   const double* lat;
   const double* lon;
   const double* radius;
+  const Heur* heur;            // per state (k_prep)
+  const uint4* cprep;          // per state candidate (k_prep)
   double delta;
   int64_t* path_off;           // per state
   int32_t* path_len;           // per state; -1 = same-edge step
@@ -1170,14 +1215,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
       active = true;
       const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
       mode_bit = 1u << mode;
-      d0 = (uint32_t)part_mm(1.0 - pi, gr.len_mm[ei]);
+      const uint4 cs = a.cprep[sp * OTR_KMAX + wi], ct = a.cprep[s * OTR_KMAX + wj];
+      d0 = cs.w;
       S = gr.edge_dst[ei];
-      T = gr.edge_src[ej];
-      const int64_t pb = a.state_probe[s];
-      H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], a.bound[s]);
-      const int2 tll = gr.node_ll[T];
-      hT = H(tll.x, tll.y);
-      tpart = (uint32_t)part_mm(pj, gr.len_mm[ej]);
+      T = ct.y;
+      H = a.heur[s];
+      hT = ct.z;
+      tpart = ct.x;
       bmm = (uint32_t)bound_mm_of(a.bound[s]);
     }
   }
