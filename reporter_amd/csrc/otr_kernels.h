@@ -141,6 +141,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
   const int lane = threadIdx.x;
   const int64_t s = xcd_remap(blockIdx.x, (n_states + 7) / 8);
   if (s >= n_states) return;
+#ifdef OTR_STAMPS_CAND
+  const unsigned long long cs0 = __builtin_amdgcn_s_memtime();
+  unsigned long long cs1 = cs0, cs2 = cs0;
+#endif
   const int64_t probe = state_probe[s];
   const int mode = b.mode[state_trace[s]] < OTR_MODES ? b.mode[state_trace[s]] : 0;
   const MatchParams& P = mp.m[mode];
@@ -223,6 +227,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
       s_pre[nr] = acc;
     }
     __syncthreads();
+#ifdef OTR_STAMPS_CAND
+    cs1 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t total = s_pre[nr];
     for (uint32_t base = 0; base < total; base += OTR_WAVE) {
       const uint32_t k = base + lane;
@@ -244,6 +251,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
       }
       merge(ok, d2, frac, rec.x);
     }
+#ifdef OTR_STAMPS_CAND
+    cs2 = __builtin_amdgcn_s_memtime();
+#endif
   } else {
     for (int64_t r = r0; r <= r1; ++r)
       for (int64_t c = c0; c <= c1; ++c) {
@@ -280,6 +290,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
     out.radius[s] = radius;
   }
   for (int off = 32; off > 0; off >>= 1) tests += __shfl_xor(tests, off);
+#ifdef OTR_STAMPS_CAND
+  if (lane == 0 && counters) {
+    const unsigned long long cs3 = __builtin_amdgcn_s_memtime();
+    const int sh = blockIdx.x & (kShards - 1);
+    atomicAdd(&counters[16 * kShards + sh], cs1 - cs0);
+    atomicAdd(&counters[17 * kShards + sh], cs2 - cs1);
+    atomicAdd(&counters[18 * kShards + sh], cs3 - cs2);
+  }
+#endif
   if (lane == 0 && counters) {
     const int sh = blockIdx.x & (kShards - 1);
     atomicAdd(&counters[0 * kShards + sh], (unsigned long long)((r1 - r0 + 1) * (c1 - c0 + 1)));
