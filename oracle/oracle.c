@@ -70,7 +70,12 @@ orc_graph* orc_graph_load(const char* path) {
   g->cell_edge = (const uint32_t*)A(OTR_A_CELL_EDGE);
 #undef A
   g->len_mm = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)g->h.n_edges + 1));
-  for (uint32_t e = 0; e < g->h.n_edges; ++e) g->len_mm[e] = (uint32_t)llround((double)g->edge_len[e] * 1000.0);
+  /* routing length in whole mm, at least 1 mm: with no zero-length edges every tight
+   * in-edge strictly decreases the label, so predecessor walks always end */
+  for (uint32_t e = 0; e < g->h.n_edges; ++e) {
+    const long long mm = llround((double)g->edge_len[e] * 1000.0);
+    g->len_mm[e] = (uint32_t)(mm < 1 ? 1 : mm);
+  }
   return g;
 }
 
@@ -697,7 +702,7 @@ static void match_trace(job_t* J, int32_t t) {
         dijkstra(g, S, bound_mm_of(bound), mode_bit, &nm);
         VEC(uint32_t) path = {0};
         uint32_t v = T;
-        while (v != S) {
+        while (v != S && path.n <= g->h.n_nodes) {
           uint32_t sv = nm_find(&nm, v);
           int64_t dv = nm.dist[sv];
           uint32_t best_e = 0xFFFFFFFFu;

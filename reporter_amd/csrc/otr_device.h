@@ -62,6 +62,8 @@ struct DevGraph {
   const int2* node_ll;         // (lat_e6, lon_e6)
   uint32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double grid_min_lat, grid_min_lon, grid_cell_deg;
+  float h_scale;               // min over edges of len_mm / straight-line mm (<= 1): keeps the A*
+                               // heuristic consistent for graphs whose lengths undercut geometry
 };
 
 // cos of an angle in degrees, |deg| <= 90: Taylor series to x^22 (Horner).

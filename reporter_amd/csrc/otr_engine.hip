@@ -123,7 +123,7 @@ int engine_configure(const Config& cfg, std::string* err) {
         if (err) *err = "graph edge length outside [0, 2000 km)";
         return OTR_BAD_REQUEST;
       }
-      len[e] = (uint32_t)llround(mm);
+      len[e] = (uint32_t)std::max(1LL, (long long)llround(mm));  // >= 1 mm
     }
     std::vector<uint4> pack(h.n_edges + 1);
     for (uint32_t e = 0; e < h.n_edges; ++e) pack[e] = make_uint4(dst[e], len[e], attr[e], 0u);
@@ -156,6 +156,28 @@ int engine_configure(const Config& cfg, std::string* err) {
       if (deg > 4) adj[4ull * u + 3].x |= kAdjMore;
     }
     g.adj = (const uint4*)upv(adj.data(), sizeof(uint4) * adj.size());
+    // heuristic scale: every edge must satisfy len_mm >= scale * (straight-line mm in any
+    // search's metric); the upper bound of that metric distance uses the edge's own
+    // more equatorward cosine.  Generated graphs give 1; lengths rounded
+    // below geometry (e.g. whole metres) lower it; a zero-length edge between distinct
+    // points makes it 0, i.e. plain Dijkstra order.
+    double scale = 1.0;
+    for (uint32_t u = 0; u < h.n_nodes; ++u)
+      for (uint32_t e = row[u]; e < row[u + 1]; ++e) {
+        const uint32_t v = dst[e];
+        const double la1 = nll[2ull * u] * 1e-6, lo1 = nll[2ull * u + 1] * 1e-6;
+        const double la2 = nll[2ull * v] * 1e-6, lo2 = nll[2ull * v + 1] * 1e-6;
+        const double cmax = cos_deg(fmin(fabs(la1), fabs(la2)));
+        const double x = (lo1 - lo2) * kMetersPerDeg * cmax, y = (la1 - la2) * kMetersPerDeg;
+        const double d_mm = sqrt(x * x + y * y) * 1000.0 * (1.0 + 1e-9) + 1e-6;
+        if (d_mm > 1e-3 && (double)len[e] < scale * d_mm) scale = (double)len[e] / d_mm;
+      }
+    float hs = (float)scale;
+    if ((double)hs > scale) hs = nextafterf(hs, 0.0f);
+    g.h_scale = hs > 0.0f ? hs : 0.0f;
+#ifdef OTR_FORCE_H_SCALE1
+    g.h_scale = 1.0f;  // experiment only: the unscaled heuristic
+#endif
     // candidate-search view: each grid-cell entry carries its edge's shape range and attributes
     const uint32_t* cedge = (const uint32_t*)(base + h.array_offset[OTR_A_CELL_EDGE]);
     const uint32_t* eshape = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_SHAPE]);

@@ -491,7 +491,8 @@ constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
 #endif
 
 // Straight-line lower bound (mm) toward the target probe's search disk (P, r) for the
-// A* order, in f32: h = trunc(990 * |v - P| - 1000 * (0.99 r + 1)) in a fixed metric
+// A* order, in f32: h = trunc(990 s |v - P| - 1000 (0.99 r + 1)) in a fixed metric, with
+// s = DevGraph::h_scale (1 unless the graph's lengths undercut its geometry),
 // whose lon scale is the cosine at the most poleward latitude the search can reach
 // (both scales rounded down).  The ideal value satisfies h(u) - h(T) <= 0.99 * dist(u, T);
 // f32 evaluation moves each h by at most ~5e-7 * |v - P| + 1 mm, so the finality and
@@ -502,13 +503,14 @@ constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
 struct Heur {
   int32_t plat_e6, plon_e6;  // target probe rounded to micro-degrees (any fixed point keeps h consistent)
   float mx, my;              // metres per micro-degree (lon at the most poleward latitude, lat), rounded down
+  float k;                   // 990 * DevGraph::h_scale (mm per metre), rounded down
   float c;                   // 1000 * (0.99 r + 1), mm, rounded up
   uint32_t margin;           // mm added to h(T) in the finality / unreachability tests
   __device__ uint32_t operator()(int32_t lat_e6, int32_t lon_e6) const {
     const float dx = (float)(lon_e6 - plon_e6) * mx;
     const float dy = (float)(lat_e6 - plat_e6) * my;
     const float d = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-    const float h = d * 990.0f - c;
+    const float h = d * k - c;
     return h > 0.0f ? (h < 2147483520.0f ? (uint32_t)h : 2147483520u) : 0u;
   }
 };
@@ -519,7 +521,7 @@ __device__ inline float f32_down(double x) {
   return f;
 }
 
-__device__ inline Heur make_heur(double plat, double plon, double r, double bound) {
+__device__ inline Heur make_heur(double plat, double plon, double r, double bound, float h_scale) {
   double lat = fabs(plat) + 2.0 * bound / kMetersPerDeg;
   if (lat > 89.9) lat = 89.9;
   const float mx = f32_down(kMetersPerDeg * 1e-6 * cos_deg(lat));
@@ -532,7 +534,8 @@ __device__ inline Heur make_heur(double plat, double plon, double r, double boun
   const double reach_mm = 1000.0 * (2.0 * bound + r);
   const double m = 2e-5 * reach_mm + 8.0;
   const uint32_t margin = m < 1e9 ? (uint32_t)m + 1u : 1000000000u;
-  return Heur{(int32_t)llround(plat * 1e6), (int32_t)llround(plon * 1e6), mx, my, cf, margin};
+  const float k = f32_down(990.0 * (double)h_scale);
+  return Heur{(int32_t)llround(plat * 1e6), (int32_t)llround(plon * 1e6), mx, my, k, cf, margin};
 }
 
 // routing bound and partial edge lengths in whole mm (shared with the oracle)
@@ -829,7 +832,7 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
   if (K <= 0) return;
   const int64_t pb = a.state_probe[s];
   const double bound = a.prev[s] >= 0 ? a.bound[s] : 0.0;  // set by k_link for steps only
-  const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], bound);
+  const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], bound, g.h_scale);
   if (lane == 0) a.heur[s] = H;
   if (lane < K) {
     const uint32_t e = a.cand_edge[s * OTR_KMAX + lane];

@@ -57,7 +57,8 @@ def write_graph(path, node_ll, edges, segments=(), cell_deg=0.0005):
 
     node_ll:  [(lat, lon)] in degrees (stored as micro-degrees)
     edges:    [dict(src, dst, shape=[(lat,lon),...] (interior points, optional),
-                    speed=50, access=7, level=2, internal=False, way=1)]
+                    speed=50, access=7, level=2, internal=False, way=1,
+                    length=metres (optional; default: the polyline's length, at least 0.5 m))]
     segments: [dict(id=osmlr_id, edges=[edge indices in order])]  (length = sum of edge lengths)
     Edge ids in the file follow the CSR order (sorted by src, dst, input order);
     returns the permutation new_id_of[input_index].
@@ -97,7 +98,7 @@ def write_graph(path, node_ll, edges, segments=(), cell_deg=0.0005):
                 x = (lo1 - lo2) * M * _cos_deg(0.5 * (la1 + la2))
                 y = (la1 - la2) * M
                 L += math.sqrt(x * x + y * y)
-        elen[nid] = max(L, 0.5)
+        elen[nid] = e['length'] if 'length' in e else max(L, 0.5)
         a = (e.get('access', 7) & 7) | (int(e.get('speed', 50)) << 3) | (int(e.get('level', 2)) << 11)
         if e.get('internal'):
             a |= ATTR_INTERNAL

@@ -113,3 +113,47 @@ def scenarios():
     # jump to a disconnected road → breakage into two sub-paths
     s['breakage'] = [(30 + 20 * k, 2) for k in range(6)] + [(20 + 20 * k, 2002) for k in range(6)]
     return s
+
+
+def build_short_lengths(path, seed=5, n=14, spacing=40.0):
+    """A street grid whose stored edge lengths undercut the geometry (as whole-metre
+    rounding does: 0.6-1.0 x the straight-line length, some 0 m) and with clusters of
+    nearly coincident nodes (a few cm apart): the graphs a tile flattener can produce.
+    Routing must still equal plain Dijkstra (oracle)."""
+    rng = np.random.default_rng(seed)
+    nodes, edges, segs = [], [], []
+    idx = {}
+    for r in range(n):
+        for c in range(n):
+            idx[(r, c)] = len(nodes)
+            nodes.append(ll(c * spacing + rng.uniform(-3, 3), r * spacing + rng.uniform(-3, 3)))
+
+    def dist(a, b):
+        (la1, lo1), (la2, lo2) = nodes[a], nodes[b]
+        x = (lo1 - lo2) * M * math.cos(math.radians(0.5 * (la1 + la2)))
+        y = (la1 - la2) * M
+        return math.hypot(x, y)
+
+    way = 1
+    for r in range(n):
+        for c in range(n):
+            for dr, dc in ((0, 1), (1, 0)):
+                if r + dr >= n or c + dc >= n:
+                    continue
+                a, b = idx[(r, c)], idx[(r + dr, c + dc)]
+                # split the street at a node a few cm past its start (near-coincident pair)
+                la, lo = nodes[a]
+                lb, lob = nodes[b]
+                f = rng.uniform(0.0003, 0.002)
+                m = len(nodes)
+                nodes.append((la + f * (lb - la), lo + f * (lob - lo)))
+                for u, v in ((a, m), (m, b)):
+                    d = dist(u, v)
+                    k = rng.random()
+                    length = 0.0 if k < 0.05 else (math.floor(d) if k < 0.6 else d * rng.uniform(0.6, 1.0))
+                    for s_, t_ in ((u, v), (v, u)):
+                        edges.append(dict(src=s_, dst=t_, way=way, level=2, speed=30, length=float(length)))
+                segs.append(dict(id=osmlr(2, 500, len(segs) + 1), edges=[len(edges) - 4, len(edges) - 2]))
+                way += 1
+    write_graph(path, nodes, edges, segs)
+    return path

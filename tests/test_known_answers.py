@@ -94,3 +94,29 @@ def test_known_answers_gpu_parity(kat):
     want = po.match_batch(po.Graph(path), b, po.params())
     errors, stats = compare(got, want)
     assert not errors, errors
+
+
+def test_short_length_graph_oracle_sanity(graph_dir):
+    """The oracle matches traces on a graph whose lengths undercut its geometry."""
+    path = K.build_short_lengths(os.path.join(graph_dir, 'short_len.otrg'))
+    from reporter_amd.tools import gen
+    tr = gen.make_traces(path, 12, 40, 3, 4.0, 17)
+    r = po.match_batch(po.Graph(path), tr, po.params())
+    assert r['trace_seg_off'][-1] > 0
+
+
+@pytest.mark.gpu
+def test_short_length_graph_gpu_parity(graph_dir):
+    """A* order on the GPU keeps exact labels when stored lengths are below the straight
+    line (DevGraph::h_scale) and nodes nearly coincide: bit-exact with the oracle."""
+    from oracle.compare import compare
+    from reporter_amd import matcher as M
+    from reporter_amd.tools import gen
+    path = K.build_short_lengths(os.path.join(graph_dir, 'short_len.otrg'))
+    M.configure(M.default_config(path))
+    tr = gen.make_traces(path, 40, 60, 3, 6.0, 18)
+    got = M.Matcher().match_batch_numpy(tr)
+    want = po.match_batch(po.Graph(path), tr, po.params())
+    errors, stats = compare(got, want)
+    assert not errors, errors
+    assert stats['n_seg'] > 0
