@@ -19,6 +19,11 @@ CASES = {
     'city_sparse_60s': ('city', 30, 60, 60, 50.0, 4, 0.0, 0.0, 50.0,
                         {'search_radius': 200, 'max_search_radius': 200}),
     'metro_15s': ('metro', 100, 100, 15, 10.0, 3, 0.0, 0.0, None, {}),
+    # C4 on the metro graph: 60 s sampling, 50 m accuracy, 200 m search radius
+    'metro_sparse_60s': ('metro', 40, 60, 60, 50.0, 4, 0.0, 0.0, 50.0,
+                         {'search_radius': 200, 'max_search_radius': 200}),
+    # C5's mode mix (60 % auto / 25 % bicycle / 15 % pedestrian) on the metro graph
+    'metro_mixed_modes': ('metro', 120, 100, 15, 10.0, 5, 0.25, 0.15, None, {}),
 }
 
 
