@@ -60,6 +60,10 @@ def main():
     ap.add_argument('--delta', type=float, default=None, help='routing round width (perf knob, metres)')
     ap.add_argument('--streams', type=int, default=2,
                     help='matchers (one HIP stream + host thread each) sharing the batch')
+    ap.add_argument('--workload', choices=['c2', 'c4', 'c5mix'], default='c2',
+                    help='c2 (default, the headline): 100 probes @15 s, sigma 10 m; c4: 60 probes @60 s, '
+                         'sigma 50 m, accuracy 50 m, search radius 200 m; c5mix: C2 with the C5 mode mix '
+                         '(60%% auto / 25%% bicycle / 15%% pedestrian) on the metro graph')
     ap.add_argument('--tiles', type=int, default=0,
                     help='privacy > 0: the step also runs the device tile stage (K9 rows, K10 sort + cull, '
                          'simple_reporter.py:176-239) on each matcher (not part of the headline config)')
@@ -93,7 +97,12 @@ def main():
     # traces: all ranks generate the same global set, keep their uuid-hash shard
     n_global = args.traces_per_gpu * world
     t0 = time.time()
-    allt = gen.make_traces(gpath, n_global, 100, 15, 10.0, 2, t_begin=T_BEGIN, t_spread=1800)
+    W = {'c2': dict(points=100, rate=15, sigma=10.0, seed=2, bike=0.0, ped=0.0, acc=None, meili={}),
+         'c4': dict(points=60, rate=60, sigma=50.0, seed=4, bike=0.0, ped=0.0, acc=50.0,
+                    meili={'search_radius': 200, 'max_search_radius': 200}),
+         'c5mix': dict(points=100, rate=15, sigma=10.0, seed=5, bike=0.25, ped=0.15, acc=None, meili={})}[args.workload]
+    allt = gen.make_traces(gpath, n_global, W['points'], W['rate'], W['sigma'], W['seed'], W['bike'], W['ped'],
+                           W['acc'], t_begin=T_BEGIN, t_spread=1800)
     if world > 1:
         shard = np.array([int(hashlib.sha1(u.encode()).hexdigest()[:3], 16) % world for u in allt.uuids])
         mine = allt.subset(np.flatnonzero(shard == rank))
@@ -101,7 +110,7 @@ def main():
         mine = allt
     log('rank %d: %d traces, %d probes (gen %.1fs)' % (rank, mine.n_traces, mine.n_probes, time.time() - t0))
 
-    cfg = M.default_config(gpath, device=local)
+    cfg = M.default_config(gpath, device=local, **W['meili'])
     if args.delta is not None:
         cfg['otr']['delta'] = args.delta
     M.configure(cfg)
@@ -121,9 +130,13 @@ def main():
     keep, darrs, hists = [], [], []
     for part in parts:
         t = [torch.from_numpy(x).to(dev) for x in (part.offsets, part.lat, part.lon, part.time, part.mode)]
+        da = {'trace_offsets': t[0].data_ptr(), 'lat': t[1].data_ptr(), 'lon': t[2].data_ptr(),
+              'time': t[3].data_ptr(), 'mode': t[4].data_ptr()}
+        if part.accuracy is not None:
+            t.append(torch.from_numpy(np.ascontiguousarray(part.accuracy, np.float32)).to(dev))
+            da['accuracy'] = t[-1].data_ptr()
         keep.append(t)
-        darrs.append({'trace_offsets': t[0].data_ptr(), 'lat': t[1].data_ptr(), 'lon': t[2].data_ptr(),
-                      'time': t[3].data_ptr(), 'mode': t[4].data_ptr()})
+        darrs.append(da)
         hists.append(torch.zeros(hist_len, dtype=torch.int32, device=dev))
     hist = torch.zeros(hist_len, dtype=torch.int32, device=dev)
     hist_out = torch.zeros(hist_len // world, dtype=torch.int32, device=dev)
@@ -195,11 +208,12 @@ def main():
         sample = mine.subset(np.arange(min(args.cpu_traces, mine.n_traces)))
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         tc = time.perf_counter()
-        po.match_batch(g, sample, po.params(), threads=threads)
+        po.match_batch(g, sample, po.params(**{k: float(v) for k, v in W['meili'].items()}), threads=threads)
         dt = time.perf_counter() - tc
         cpu = {'value': round(sample.n_probes / dt, 1), 'unit': 'probes/s', 'cores': threads, 'kind': 'port',
-               'sample': '%d traces x 100 probes of the same C2 workload through oracle/liboracle.so '
-                         '(scalar C restatement, %d pthreads, %.1f s)' % (sample.n_traces, threads, dt)}
+               'sample': '%d traces x %d probes of the same %s workload through oracle/liboracle.so '
+                         '(scalar C restatement, %d pthreads, %.1f s)' % (sample.n_traces, W['points'],
+                                                                          args.workload.upper(), threads, dt)}
 
     if rank == 0:
         line = {
@@ -215,9 +229,12 @@ def main():
             'vs_baseline': None,
             'dtype': 'f64',
             'data': 'synthetic',
-            'config': {'workload': 'C2: metro street grid (%d nodes, %d directed edges, %d OSMLR segments), '
-                                   '%d traces x 100 probes per GPU @15 s, sigma 10 m' % (
-                                       n_nodes, n_edges, n_segments, args.traces_per_gpu),
+            'config': {'workload': '%s: metro street grid (%d nodes, %d directed edges, %d OSMLR segments), '
+                                   '%d traces x %d probes per GPU @%d s, sigma %g m%s' % (
+                                       args.workload.upper(), n_nodes, n_edges, n_segments, args.traces_per_gpu,
+                                       W['points'], W['rate'], W['sigma'],
+                                       {'c2': '', 'c4': ', accuracy 50 m, search radius 200 m',
+                                        'c5mix': ', modes 60% auto / 25% bicycle / 15% pedestrian'}[args.workload]),
                        'probes_per_step': int(total_probes),
                        'parallelism': 'uuid-sharded dp%d + RCCL reduce-scatter of [hour][segment][speed] histogram'
                                       % world if world > 1 else 'single GPU',
