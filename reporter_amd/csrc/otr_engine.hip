@@ -302,6 +302,16 @@ __global__ void k_collect(int64_t n, const int32_t* flag, int64_t* list, unsigne
   block_append(i < n && flag[i], i, list, count);
 }
 
+// retry tiers: take the flagged tasks (flag == want, or any flag when want == 0) and
+// clear their flags; tasks flagged for a later tier keep theirs
+__global__ void k_collect_tier(int64_t n, int32_t* flag, int want, int64_t* list, unsigned long long* count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int f = i < n ? flag[i] : 0;
+  const bool sel = f != 0 && (want == 0 || f == want);
+  if (sel) flag[i] = 0;
+  block_append(sel, i, list, count);
+}
+
 // states that need a path: a step inside a sub-path
 __global__ void k_step_list(int64_t n_states, const int64_t* prev, const uint8_t* brk, const int32_t* cand_count,
                             int64_t* list, unsigned long long* count) {
@@ -523,14 +533,15 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     int64_t* list = need<int64_t>(S_LIST, NT);
     unsigned long long* cnt = need<unsigned long long>(S_MISC, 4);
     tb(OTR_STAGE_ROUTE_BIG);
+    // first-tier overflows flagged 2 (long bounds) skip the 256-slot tier
     for (int tier = 0; tier < 3; ++tier) {
       HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
-      k_collect<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, list, cnt);
+      k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, tier == 0 ? 1 : 0, list, cnt);
       unsigned long long novf = 0;
       HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
-      if (novf == 0) break;
-      HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
+      if (novf == 0 && tier > 0) break;
+      if (novf == 0) continue;
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.n_tasks = (int64_t)novf;

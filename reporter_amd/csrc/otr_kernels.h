@@ -968,7 +968,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
       }
     }
   }
-  if (have && !ok && !forced && lane == 0) a.overflow_flag[task] = 1;
+  // overflow: retry with a bigger table; a first-tier search with a long bound (> 1.9 km)
+  // that outgrew 160 slots goes straight to the 1024-slot tier (flag 2)
+  if (have && !ok && !forced && lane == 0) a.overflow_flag[task] = (G == 2 && bmm > 1900000u) ? 2 : 1;
   if (counters) {
     // wave totals: lane sums by DPP, per-group values read from each group's lane 0
     settled = wave_sum_u32((uint32_t)settled);
