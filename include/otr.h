@@ -213,6 +213,70 @@ int otr_tiles_cull(otr_matcher* m, const otr_tile_row* rows, int64_t n, int32_t 
 int otr_tiles_format(const otr_tile_row* rows, int64_t n, const char* source, const char* mode, int32_t rules,
                      char** out, size_t* out_len);
 
+/* ---- ingest: probe text → windowed traces in HBM (§8 f rank 4) -------------------------
+ * OTR_INGEST_SHARD: the "uuid,time,lat,lon,acc" lines simple_reporter.match() reads
+ *   (simple_reporter.py:140-160): line.strip().split(',') into exactly 5 fields,
+ *   float() coordinates, int() time and accuracy.
+ * OTR_INGEST_RAW: the raw feed simple_reporter.download() reads (:99-111) followed by the
+ *   shard round trip into match(): fields by index after splitting on `separator`, the
+ *   bbox filter (applied before time and accuracy are parsed, as :103-105), the fast
+ *   "%Y-%m-%d %H:%M:%S" time (:106-107) or epoch seconds, accuracy min(ceil(x), 1000)
+ *   (:110), and coordinates as match() re-reads them from the Python 2 str() text
+ *   (12 significant digits, :111).
+ * OTR_INGEST_JAVA_SV: Formatter.formatSV (Formatter.java:103-114): float32 coordinates,
+ *   (int)ceil accuracy, Long.parseLong or "yyyy-MM-dd HH:mm:ss" time.
+ * Then, for every rule: points grouped by uuid, sorted by time (stable), split at gaps
+ *   > inactivity seconds, windows of fewer than 2 points dropped (:146-160).  Traces come
+ *   out in order of the first appearance of their uuid, then by time. */
+#define OTR_INGEST_SHARD 0
+#define OTR_INGEST_RAW 1
+#define OTR_INGEST_JAVA_SV 2
+#define OTR_TIME_EPOCH 0
+#define OTR_TIME_YMDHMS 1
+/* bad_reason: why the first rejected line (bad_line) was rejected */
+#define OTR_INGEST_E_FIELDS 1     /* wrong field count / index out of range (ValueError, IndexError) */
+#define OTR_INGEST_E_FLOAT 2      /* coordinate not a finite decimal number */
+#define OTR_INGEST_E_INT 3        /* time or accuracy not an integer (int()) */
+#define OTR_INGEST_E_TIME 4       /* date fields out of range (datetime.date) */
+#define OTR_INGEST_E_UUID 5       /* uuid holds the shard separator ',' */
+#define OTR_INGEST_E_PRECISION 6  /* > 19 significant digits whose rounding needs big-number arithmetic */
+#define OTR_INGEST_E_COLLISION 7  /* two uuids share a 64-bit hash (never seen; refused rather than merged) */
+#define OTR_INGEST_E_ACCURACY 8   /* accuracy not finite or beyond ±2^24 */
+
+typedef struct otr_ingest_format {
+  int32_t rules;          /* OTR_INGEST_* */
+  int32_t separator;      /* field separator byte: ',' (SHARD, fixed), '|' (raw feed) */
+  int32_t uuid_index, time_index, lat_index, lon_index, accuracy_index;  /* RAW / JAVA_SV */
+  int32_t time_format;    /* OTR_TIME_* (RAW / JAVA_SV) */
+  int32_t inactivity;     /* seconds (--inactivity, 120) */
+  int32_t mode;           /* 0 auto, 1 bicycle, 2 pedestrian: the batch's mode (--mode) */
+  int32_t use_bbox;       /* RAW: apply bbox */
+  int32_t reserved;
+  double bbox[4];         /* min lat, min lon, max lat, max lon (--bbox) */
+} otr_ingest_format;
+
+typedef struct otr_ingest_result {
+  int64_t n_lines;        /* lines in the text */
+  int64_t n_kept;         /* lines inside the bbox */
+  int64_t n_probes;       /* probes in windows of >= 2 points */
+  int32_t n_traces;       /* windows */
+  int32_t n_uuids;
+  int64_t bad_line;       /* first rejected line (0-based), -1 if none */
+  int32_t bad_reason;     /* OTR_INGEST_E_* */
+  int32_t reserved;
+  otr_trace_batch batch;  /* memory = OTR_MEM_DEVICE: offsets, lat, lon, time, accuracy, mode in HBM
+                             (matcher-owned, valid until its next otr_ingest); levels/flags zero */
+  const int64_t* d_trace_uuid_off;  /* per trace: byte offset of its uuid in the text */
+  const int32_t* d_trace_uuid_len;
+} otr_ingest_result;
+
+/* Parse `len` bytes of probe lines (host or device memory) into traces in HBM.  Returns
+ * OTR_OK, or OTR_BAD_REQUEST with bad_line / bad_reason set where the reference raises
+ * (the whole text is refused, as the reference loses the file).  The batch can be
+ * passed straight to otr_match_batch after setting its levels, threshold and flags. */
+int otr_ingest(otr_matcher* m, const char* text, int64_t len, int32_t memory, const otr_ingest_format* fmt,
+               otr_ingest_result* out);
+
 /* graph facts for callers sizing histograms */
 int otr_graph_info(int64_t* n_nodes, int64_t* n_edges, int64_t* n_segments);
 

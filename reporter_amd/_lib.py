@@ -19,6 +19,13 @@ OTR_BATCH_COPY_REPORTS = 4
 OTR_BATCH_TILE_ROWS = 8
 OTR_TILE_RULES_SIMPLE = 0
 OTR_TILE_RULES_STREAM = 1
+OTR_INGEST_SHARD = 0
+OTR_INGEST_RAW = 1
+OTR_INGEST_JAVA_SV = 2
+OTR_TIME_EPOCH = 0
+OTR_TIME_YMDHMS = 1
+INGEST_REASONS = {1: 'fields', 2: 'float', 3: 'int', 4: 'time', 5: 'uuid', 6: 'precision', 7: 'collision',
+                  8: 'accuracy'}
 OTR_NO_ID = 0xFFFFFFFFFFFFFFFF
 HIST_BINS = 8
 KMAX = 64
@@ -29,7 +36,7 @@ STAGES = ['states', 'candidates', 'link', 'route', 'route_big', 'viterbi', 'path
 EXPORTS = ['otr_configure', 'otr_configure_json', 'otr_matcher_new', 'otr_matcher_free', 'otr_match',
            'otr_report', 'otr_report_segments', 'otr_free', 'otr_last_error', 'otr_match_batch',
            'otr_graph_info', 'otr_matcher_stream', 'otr_device', 'otr_report_batch', 'otr_coalesce',
-           'otr_tiles_cull', 'otr_tiles_format']
+           'otr_tiles_cull', 'otr_tiles_format', 'otr_ingest']
 
 
 class TraceBatch(ctypes.Structure):
@@ -40,6 +47,21 @@ class TraceBatch(ctypes.Structure):
                 ('threshold_sec', ctypes.c_int32), ('quantisation', ctypes.c_int32),
                 ('hist_base_time', ctypes.c_int64), ('hist_hours', ctypes.c_int32), ('flags', ctypes.c_int32),
                 ('hist_device', ctypes.c_void_p), ('tile_rules', ctypes.c_int32), ('reserved', ctypes.c_int32)]
+
+
+class IngestFormat(ctypes.Structure):
+    _fields_ = [('rules', ctypes.c_int32), ('separator', ctypes.c_int32), ('uuid_index', ctypes.c_int32),
+                ('time_index', ctypes.c_int32), ('lat_index', ctypes.c_int32), ('lon_index', ctypes.c_int32),
+                ('accuracy_index', ctypes.c_int32), ('time_format', ctypes.c_int32), ('inactivity', ctypes.c_int32),
+                ('mode', ctypes.c_int32), ('use_bbox', ctypes.c_int32), ('reserved', ctypes.c_int32),
+                ('bbox', ctypes.c_double * 4)]
+
+
+class IngestResult(ctypes.Structure):
+    _fields_ = [('n_lines', ctypes.c_int64), ('n_kept', ctypes.c_int64), ('n_probes', ctypes.c_int64),
+                ('n_traces', ctypes.c_int32), ('n_uuids', ctypes.c_int32), ('bad_line', ctypes.c_int64),
+                ('bad_reason', ctypes.c_int32), ('reserved', ctypes.c_int32), ('batch', TraceBatch),
+                ('d_trace_uuid_off', ctypes.c_void_p), ('d_trace_uuid_len', ctypes.c_void_p)]
 
 
 class BatchResult(ctypes.Structure):
@@ -112,6 +134,8 @@ def lib():
                                  ctypes.c_int32, P(ctypes.c_void_p), P(ctypes.c_int64)]
     L.otr_tiles_format.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_char_p,
                                    ctypes.c_int32, P(ctypes.c_void_p), P(ctypes.c_size_t)]
+    L.otr_ingest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, P(IngestFormat),
+                             P(IngestResult)]
     _L = L
     return L
 

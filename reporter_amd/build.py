@@ -115,8 +115,20 @@ def build_loadgen(force=False):
     return exe
 
 
+def build_parsecheck(force=False):
+    """tools/libparsecheck.so: host build of the ingest number parsers (CPU tests only)."""
+    src = os.path.join(PKG, 'tools', 'parsecheck.cpp')
+    lib = os.path.join(PKG, 'tools', 'libparsecheck.so')
+    deps = [src] + [os.path.join(CSRC, f) for f in ('otr_ingest.h', 'otr_pow5.h')]
+    if force or not _newer(lib, deps):
+        _run([HIPCC, '-x', 'hip', '--cuda-host-only', '-O2', '-std=c++17', '-fPIC', '-shared',
+              '-I' + os.path.join(ROOT, 'include'), '-o', lib, src])
+    return lib
+
+
 def build_all(force=False):
     build_gen(force)
+    build_parsecheck(force)
     build_oracle(force)
     build_calib(force)
     lib = build_otr(force)

@@ -316,6 +316,19 @@ int otr_tiles_cull(otr_matcher* m, const otr_tile_row* rows, int64_t n, int32_t 
   return rc;
 }
 
+// simple_reporter.py:140-160 (shard lines), :99-111 (raw feed), Formatter.java:103-114
+int otr_ingest(otr_matcher* m, const char* text, int64_t len, int32_t memory, const otr_ingest_format* fmt,
+               otr_ingest_result* out) {
+  if (!m || !fmt || !out || (len > 0 && !text)) {
+    g_last_error = "null argument";
+    return OTR_BAD_REQUEST;
+  }
+  std::string err;
+  const int rc = m->m.ingest(text, len, memory, fmt, out, &err);
+  if (rc != OTR_OK) g_last_error = err;
+  return rc;
+}
+
 // simple_reporter.py:188-195: ','.join([id, next, duration, '1', length, queue, start, end,
 // source, mode.upper()]) + os.linesep
 // Segment.appendToStringBuffer (Segment.java:59-74) for OTR_TILE_RULES_STREAM

@@ -62,6 +62,8 @@ struct Matcher {
   int run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err);
   int tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int privacy, int rules, const otr_tile_row** out,
                  int64_t* n_out, std::string* err);
+  int ingest(const char* text, int64_t len, int memory, const otr_ingest_format* fmt, otr_ingest_result* out,
+             std::string* err);
   ~Matcher();
 };
 

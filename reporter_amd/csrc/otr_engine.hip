@@ -12,6 +12,7 @@
 
 #include "otr_engine.h"
 #include "otr_kernels.h"
+#include "otr_ingest.h"
 
 namespace otr {
 
@@ -234,6 +235,10 @@ enum Slot {
   S_C_ROUTE_OFF, S_C_SEG_OFF, S_C_WAY_OFF, S_C_REP_OFF, S_C_ARGS, S_C_ROUTE, S_C_SEG_ID, S_C_SEG_START,
   S_C_SEG_END, S_C_SEG_LEN, S_C_SEG_QUEUE, S_C_SEG_INTERNAL, S_C_SEG_BSHAPE, S_C_SEG_ESHAPE, S_C_SEG_WAY_N,
   S_C_SEG_WAY, S_C_SEG_WAY_OFF, S_C_REP_ID, S_C_REP_NEXT, S_C_REP_T0, S_C_REP_T1, S_C_REP_LEN, S_C_REP_QUEUE,
+  S_IN_TEXT, S_IN_CNT, S_IN_CSCAN, S_IN_NL, S_IN_HASH, S_IN_UOFF, S_IN_ULEN, S_IN_TIME, S_IN_LAT, S_IN_LON,
+  S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
+  S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
+  S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
   S_NUM
 };
 
@@ -1036,6 +1041,225 @@ int Matcher::tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int pri
   HIPCHK(hipGetLastError());
   *out = h_tile_rows.data();
   *n_out = nk;
+  return OTR_OK;
+}
+
+// ---- K11 ingest (include/otr.h otr_ingest) ----------------------------------------------
+int Matcher::ingest(const char* text, int64_t len, int memory, const otr_ingest_format* fmt, otr_ingest_result* out,
+                    std::string* err) {
+  GraphState& gs = graph_state();
+  HIPCHK(hipSetDevice(gs.device));
+  if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  memset(out, 0, sizeof(*out));
+  out->bad_line = -1;
+  if (fmt->rules < OTR_INGEST_SHARD || fmt->rules > OTR_INGEST_JAVA_SV || fmt->mode < 0 || fmt->mode > 2 ||
+      fmt->inactivity < 0 || (fmt->rules != OTR_INGEST_SHARD && (fmt->separator < 1 || fmt->separator > 255))) {
+    if (err) *err = "bad ingest format";
+    return OTR_BAD_REQUEST;
+  }
+  for (int k : {fmt->uuid_index, fmt->time_index, fmt->lat_index, fmt->lon_index, fmt->accuracy_index})
+    if (fmt->rules != OTR_INGEST_SHARD && (k < 0 || k > 4096)) {
+      if (err) *err = "bad ingest field index";
+      return OTR_BAD_REQUEST;
+    }
+  out->batch.memory = OTR_MEM_DEVICE;
+  if (len <= 0) return OTR_OK;
+  if (len >= ((int64_t)1 << 40)) {
+    if (err) *err = "ingest text too large";
+    return OTR_BAD_REQUEST;
+  }
+  auto fail = [&](const char* what) {
+    if (err) *err = what;
+    return OTR_DEVICE_ERROR;
+  };
+  // text in HBM, zero-padded to whole 16-byte chunks
+  const int64_t n_chunks = (len + 15) / 16;
+  uint8_t* d_text = need<uint8_t>(S_IN_TEXT, 16 * n_chunks);
+  int64_t* cnt = need<int64_t>(S_IN_CNT, n_chunks);
+  int64_t* cscan = need<int64_t>(S_IN_CSCAN, n_chunks);
+  unsigned long long* bad = need<unsigned long long>(S_IN_BAD, 1);
+  if (!d_text || !cnt || !cscan || !bad) return fail("device allocation failed (ingest)");
+  HIPCHK(hipMemsetAsync(d_text + 16 * (n_chunks - 1), 0, 16, stream));
+  HIPCHK(hipMemcpyAsync(d_text, text, len, memory == OTR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                        stream));
+  HIPCHK(hipMemsetAsync(bad, 0xFF, 8, stream));
+  size_t tb_scan = 0;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb_scan, cnt, cscan, (int)std::min<int64_t>(n_chunks, INT32_MAX),
+                                          stream));
+  if (n_chunks >= INT32_MAX) return fail("ingest text too large");
+  void* tmp = need<char>(S_IN_TMP, tb_scan);
+  if (!tmp) return fail("device allocation failed (ingest)");
+  k_nl_count<<<grid_for(n_chunks, 256), 256, 0, stream>>>(reinterpret_cast<const uint4*>(d_text), n_chunks, cnt);
+  size_t tb = tb_scan;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, cnt, cscan, (int)n_chunks, stream));
+  int64_t n_nl = 0;
+  uint8_t last = 0;
+  HIPCHK(hipMemcpyAsync(&n_nl, cscan + (n_chunks - 1), 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(&last, d_text + (len - 1), 1, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  // Python's file iteration: a final fragment without '\n' is a line too
+  const int64_t n_lines = n_nl + (last != '\n' ? 1 : 0);
+  out->n_lines = n_lines;
+  if (n_lines >= INT32_MAX) {
+    if (err) *err = "too many lines for one ingest";
+    return OTR_BAD_REQUEST;
+  }
+  const int64_t nL = std::max<int64_t>(n_lines, 1);
+  int64_t* nl = need<int64_t>(S_IN_NL, std::max<int64_t>(n_nl, 1));
+  IngestLines L{};
+  L.text = d_text;
+  L.len = len;
+  L.nl = nl;
+  L.n_nl = n_nl;
+  L.n_lines = n_lines;
+  L.hash = need<uint64_t>(S_IN_HASH, nL);
+  L.uoff = need<int64_t>(S_IN_UOFF, nL);
+  L.ulen = need<int32_t>(S_IN_ULEN, nL);
+  L.time = need<int64_t>(S_IN_TIME, nL);
+  L.lat = need<double>(S_IN_LAT, nL);
+  L.lon = need<double>(S_IN_LON, nL);
+  L.acc = need<float>(S_IN_ACC, nL);
+  L.keep = need<int64_t>(S_IN_KEEP, nL);
+  L.bad = bad;
+  int64_t* kpos = need<int64_t>(S_IN_KPOS, nL);
+  int32_t* kidx = need<int32_t>(S_IN_KIDX, nL);
+  if (!nl || !L.hash || !L.uoff || !L.ulen || !L.time || !L.lat || !L.lon || !L.acc || !L.keep || !kpos || !kidx)
+    return fail("device allocation failed (ingest)");
+  if (n_nl) k_nl_write<<<grid_for(n_chunks, 256), 256, 0, stream>>>(reinterpret_cast<const uint4*>(d_text), n_chunks,
+                                                                    cscan, nl);
+  IngestFmt f{};
+  f.rules = fmt->rules;
+  f.sep = fmt->separator;
+  f.tfmt = fmt->time_format;
+  f.use_bbox = fmt->use_bbox;
+  f.idx[0] = fmt->uuid_index;
+  f.idx[1] = fmt->time_index;
+  f.idx[2] = fmt->lat_index;
+  f.idx[3] = fmt->lon_index;
+  f.idx[4] = fmt->accuracy_index;
+  for (int k = 0; k < 4; ++k) f.bbox[k] = fmt->bbox[k];
+  k_ingest_parse<<<grid_for(n_lines, 256), 256, 0, stream>>>(L, f);
+  unsigned long long hbad = ~0ull;
+  HIPCHK(hipMemcpyAsync(&hbad, bad, 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  if (hbad != ~0ull) {
+    out->bad_line = (int64_t)(hbad >> 8);
+    out->bad_reason = (int32_t)(hbad & 0xFF);
+    if (err) *err = "malformed probe line " + std::to_string(out->bad_line);
+    return OTR_BAD_REQUEST;
+  }
+  // kept lines (bbox), in line order
+  const int nI = (int)n_lines;
+  size_t tb_sort = 0;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb_scan, L.keep, kpos, nI, stream));
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                            (const int32_t*)nullptr, (int32_t*)nullptr, nI, 0, 64, stream));
+  tmp = need<char>(S_IN_TMP, std::max(tb_scan, tb_sort));
+  if (!tmp) return fail("device allocation failed (ingest)");
+  tb = tb_scan;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, L.keep, kpos, nI, stream));
+  k_scatter_index32<<<grid_for(n_lines, 256), 256, 0, stream>>>(L.keep, kpos, n_lines, kidx);
+  int64_t M = 0;
+  HIPCHK(hipMemcpyAsync(&M, kpos + (n_lines - 1), 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  out->n_kept = M;
+  if (M == 0) return OTR_OK;
+  const int nM = (int)M;
+  uint64_t* key_a = need<uint64_t>(S_IN_KEY_A, M);
+  uint64_t* key_b = need<uint64_t>(S_IN_KEY_B, M);
+  int32_t* val_a = need<int32_t>(S_IN_VAL_A, M);
+  int32_t* val_b = need<int32_t>(S_IN_VAL_B, M);
+  int64_t* head = need<int64_t>(S_IN_HEAD, M);
+  int64_t* gid = need<int64_t>(S_IN_GID, M);
+  int32_t* gfirst = need<int32_t>(S_IN_GFIRST, M);
+  uint32_t* gkey = need<uint32_t>(S_IN_GKEY, nL);
+  if (!key_a || !key_b || !val_a || !val_b || !head || !gid || !gfirst || !gkey)
+    return fail("device allocation failed (ingest)");
+  // 1. group by uuid: sort (hash, line) — the stable sort keeps line order within a hash
+  k_gather_by<uint64_t><<<grid_for(M, 256), 256, 0, stream>>>(L.hash, kidx, M, key_a);
+  tb = tb_sort;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key_a, key_b, kidx, val_b, nM, 0, 64, stream));
+  k_group_heads<<<grid_for(M, 256), 256, 0, stream>>>(key_b, val_b, M, L.uoff, L.ulen, d_text, head, bad);
+  tb = tb_scan;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, head, gid, nM, stream));
+  k_group_first<<<grid_for(M, 256), 256, 0, stream>>>(head, gid, val_b, M, gfirst);
+  k_group_key<<<grid_for(M, 256), 256, 0, stream>>>(gid, val_b, M, gfirst, gkey);
+  int64_t n_uuid = 0;
+  HIPCHK(hipMemcpyAsync(&n_uuid, gid + (M - 1), 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(&hbad, bad, 8, hipMemcpyDeviceToHost, stream));
+  // 2. final order (first appearance of the uuid, time, line): stable LSD passes
+  int64_t* tkey_a = reinterpret_cast<int64_t*>(key_a);
+  int64_t* tkey_b = reinterpret_cast<int64_t*>(key_b);
+  k_gather_by<int64_t><<<grid_for(M, 256), 256, 0, stream>>>(L.time, kidx, M, tkey_a);
+  tb = tb_sort;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, tkey_a, tkey_b, kidx, val_a, nM, 0, 64, stream));
+  uint32_t* gk_a = reinterpret_cast<uint32_t*>(key_a);
+  uint32_t* gk_b = reinterpret_cast<uint32_t*>(key_b);
+  k_gather_by<uint32_t><<<grid_for(M, 256), 256, 0, stream>>>(gkey, val_a, M, gk_a);
+  int end_bit = 1;
+  while (end_bit < 32 && ((int64_t)1 << end_bit) < n_lines) ++end_bit;
+  tb = tb_sort;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, gk_a, gk_b, val_a, val_b, nM, 0, end_bit, stream));
+  const int32_t* perm = val_b;
+  // 3. windows
+  k_win_heads<<<grid_for(M, 256), 256, 0, stream>>>(perm, M, gkey, L.time, fmt->inactivity, head);
+  tb = tb_scan;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, head, gid, nM, stream));  // gid: window ids now
+  int64_t n_win = 0;
+  HIPCHK(hipMemcpyAsync(&n_win, gid + (M - 1), 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  if (hbad != ~0ull) {
+    out->bad_line = (int64_t)(hbad >> 8);
+    out->bad_reason = (int32_t)(hbad & 0xFF);
+    if (err) *err = "uuid hash collision at line " + std::to_string(out->bad_line);
+    return OTR_BAD_REQUEST;
+  }
+  out->n_uuids = (int32_t)n_uuid;
+  int64_t* ws = need<int64_t>(S_IN_WS, n_win);
+  int64_t* klen = need<int64_t>(S_IN_KLEN, n_win);
+  int64_t* kflag = need<int64_t>(S_IN_KFLAG, n_win);
+  int64_t* poff = need<int64_t>(S_IN_POFF, n_win);
+  int64_t* tpos = need<int64_t>(S_IN_TPOS, n_win);
+  if (!ws || !klen || !kflag || !poff || !tpos) return fail("device allocation failed (ingest)");
+  k_scatter_index<<<grid_for(M, 256), 256, 0, stream>>>(head, gid, M, ws);
+  k_win_len<<<grid_for(n_win, 256), 256, 0, stream>>>(ws, n_win, M, klen, kflag);
+  tb = tb_scan;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, klen, poff, (int)n_win, stream));
+  tb = tb_scan;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, kflag, tpos, (int)n_win, stream));
+  int64_t n_tr = 0, n_pr = 0;
+  HIPCHK(hipMemcpyAsync(&n_tr, tpos + (n_win - 1), 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(&n_pr, poff + (n_win - 1), 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  out->n_traces = (int32_t)n_tr;
+  out->n_probes = n_pr;
+  if (n_tr == 0) return OTR_OK;
+  IngestOut o{};
+  o.trace_off = need<int64_t>(S_IN_T_OFF, n_tr + 1);
+  o.lat = need<double>(S_IN_T_LAT, n_pr);
+  o.lon = need<double>(S_IN_T_LON, n_pr);
+  o.time = need<int64_t>(S_IN_T_TIME, n_pr);
+  o.acc = need<float>(S_IN_T_ACC, n_pr);
+  o.mode = need<uint8_t>(S_IN_T_MODE, n_tr);
+  o.uoff = need<int64_t>(S_IN_T_UOFF, n_tr);
+  o.ulen = need<int32_t>(S_IN_T_ULEN, n_tr);
+  if (!o.trace_off || !o.lat || !o.lon || !o.time || !o.acc || !o.mode || !o.uoff || !o.ulen)
+    return fail("device allocation failed (ingest)");
+  k_win_emit<<<grid_for(M, 256), 256, 0, stream>>>(perm, M, gid, ws, klen, poff, tpos, (int32_t)n_tr, L,
+                                                   (uint8_t)fmt->mode, o);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(stream));
+  otr_trace_batch& b = out->batch;
+  b.n_traces = (int32_t)n_tr;
+  b.memory = OTR_MEM_DEVICE;
+  b.trace_offsets = o.trace_off;
+  b.lat = o.lat;
+  b.lon = o.lon;
+  b.time = o.time;
+  b.accuracy = o.acc;
+  b.mode = o.mode;
+  out->d_trace_uuid_off = o.uoff;
+  out->d_trace_uuid_len = o.ulen;
   return OTR_OK;
 }
 

@@ -56,6 +56,19 @@ def graph_info():
     return a.value, b.value, c.value
 
 
+class IngestedBatch:
+    """The traces otr_ingest left in HBM, in the shape match_batch takes."""
+
+    def __init__(self, r):
+        b = r.batch
+        self.n_traces = int(r.n_traces)
+        self.n_probes = int(r.n_probes)
+        self.arrays = {'trace_offsets': b.trace_offsets, 'lat': b.lat, 'lon': b.lon, 'time': b.time,
+                       'accuracy': b.accuracy, 'mode': b.mode}
+        self.uuid_off = r.d_trace_uuid_off
+        self.uuid_len = r.d_trace_uuid_len
+
+
 class Matcher:
     def __init__(self):
         self._L = _lib.lib()
@@ -154,6 +167,42 @@ class Matcher:
         if rc != 0:
             raise RuntimeError('otr_match_batch failed (%d): %s' % (rc, _lib.last_error()))
         return r
+
+    def ingest(self, text, rules=0, separator='|', uuid_index=1, time_index=0, lat_index=9, lon_index=10,
+               accuracy_index=5, time_format=None, inactivity=120, mode='auto', bbox=None, device_ptr=None,
+               nbytes=None):
+        """Probe text → windowed traces in HBM (include/otr.h otr_ingest).  text: bytes
+        (host), or device_ptr + nbytes for text already in HBM.  Defaults: the raw-feed
+        valuer and time pattern of simple_reporter.py:352-353.  Returns (IngestResult,
+        batch) where batch is a device-array handle for match_batch(batch, device_arrays=
+        batch.arrays).  Raises ValueError with the line number where the reference raises."""
+        f = _lib.IngestFormat()
+        f.rules = int(rules)
+        f.separator = ord(separator) if isinstance(separator, str) else int(separator)
+        f.uuid_index, f.time_index, f.lat_index, f.lon_index, f.accuracy_index = (
+            uuid_index, time_index, lat_index, lon_index, accuracy_index)
+        if time_format is None:
+            time_format = _lib.OTR_TIME_EPOCH if rules == _lib.OTR_INGEST_SHARD else _lib.OTR_TIME_YMDHMS
+        f.time_format = int(time_format)
+        f.inactivity = int(inactivity)
+        f.mode = {'auto': 0, 'bicycle': 1, 'pedestrian': 2}[mode] if isinstance(mode, str) else int(mode)
+        if bbox is not None:
+            f.use_bbox = 1
+            for k in range(4):
+                f.bbox[k] = float(bbox[k])
+        r = _lib.IngestResult()
+        if device_ptr is not None:
+            rc = self._L.otr_ingest(self._h, ctypes.c_void_p(device_ptr), int(nbytes), _lib.OTR_MEM_DEVICE,
+                                    ctypes.byref(f), ctypes.byref(r))
+        else:
+            self._keep = [text]
+            rc = self._L.otr_ingest(self._h, ctypes.c_char_p(text), len(text), _lib.OTR_MEM_HOST, ctypes.byref(f),
+                                    ctypes.byref(r))
+        if rc != 0:
+            if r.bad_line >= 0:
+                raise ValueError('line %d: %s' % (r.bad_line, _lib.INGEST_REASONS.get(r.bad_reason, r.bad_reason)))
+            raise RuntimeError('otr_ingest failed (%d): %s' % (rc, _lib.last_error()))
+        return r, IngestedBatch(r)
 
     def match_batch_numpy(self, traces, **kw):
         r = self.match_batch(traces, copy_out=True, **kw)

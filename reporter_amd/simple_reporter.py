@@ -9,6 +9,8 @@ scope (network); inputs and outputs are local files.
   cull(lines, privacy)             privacy cull incl. the trailing-singleton merge (:218-239)
   match_traces(traces, ...)        windows → otr_match_batch → rows per tile
   report_tiles(tiles, privacy)     sort + cull                    (:211-245)
+  text_tiles_device(m, text, p)    shard / raw probe text → tiles, every stage in HBM
+                                   (K11 ingest :99-111,136-160 → K1-K10)
 """
 import hashlib
 import math
@@ -275,6 +277,22 @@ def report_tiles_device(matcher, traces, privacy, mode='auto', report_levels=(0,
     r = matcher.match_batch(batch, report_levels=report_levels, transition_levels=transition_levels,
                             threshold_sec=threshold_sec, quantisation=quantisation, copy_out=False, tile_rows=True)
     kept = cull_rows(matcher, None, privacy, device_ptr=r.d_rows, n=r.n_rows)
+    return rows_to_tiles(kept, quantisation, mode, source)
+
+
+def text_tiles_device(matcher, text, privacy, rules=0, mode='auto', report_levels=(0, 1), transition_levels=(0, 1),
+                      quantisation=3600, inactivity=120, source='smpl_rprt', threshold_sec=15, **fmt):
+    """simple_reporter from probe text to tiles with every stage in HBM: the shard lines
+    match() reads (rules OTR_INGEST_SHARD, :136-160) or the raw feed download() reads
+    (OTR_INGEST_RAW, :99-111; fmt: separator, field indices, bbox) → K11 ingest → K1-K8
+    → K9 tile rows → K10 sort + cull → CSV lines."""
+    r, batch = matcher.ingest(text, rules=rules, inactivity=inactivity, mode=mode, **fmt)
+    if r.n_traces == 0:
+        return {}
+    res = matcher.match_batch(batch, report_levels=report_levels, transition_levels=transition_levels,
+                              threshold_sec=threshold_sec, quantisation=quantisation, copy_out=False,
+                              tile_rows=True, device_arrays=batch.arrays)
+    kept = cull_rows(matcher, None, privacy, device_ptr=res.d_rows, n=res.n_rows)
     return rows_to_tiles(kept, quantisation, mode, source)
 
 

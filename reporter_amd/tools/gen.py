@@ -124,3 +124,57 @@ def config_traces(name, n_traces=None, graph_cache=None):
     path = graph_path(g, graph_cache)
     acc = 50.0 if name == 'C4' else None
     return path, make_traces(path, n_traces or nt, npnt, sr, sig, seed, fb, fp, acc)
+
+
+def _coord_text(x, style, rng):
+    if style == 0:
+        return repr(float(x))                      # shortest round trip (≤ 17 digits)
+    if style == 1:
+        return '%.6f' % x                          # a fixed-point feed (Point.java:49 prints ≤ 6)
+    if style == 2:
+        return '%.*f' % (int(rng.integers(0, 15)), x)
+    return '%.15e' % x                             # exponent form
+
+
+def probe_text(traces, kind='shard', seed=0, shuffle=0.3, styles=(0, 1, 2, 3), split_gap=None, crlf=False,
+               uuids=None):
+    """Probe lines for the ingest path (bench/test workload): kind 'shard' =
+    "uuid,time,lat,lon,acc" (simple_reporter match() input), 'raw' = the '|' feed of the
+    default valuer (c[0] time string, c[1] uuid, c[5] accuracy, c[9] lat, c[10] lon).
+    A fraction `shuffle` of lines is moved to random positions (files are appended by
+    competing processes); split_gap inserts a pause longer than the inactivity window
+    into each trace.  Returns bytes."""
+    import datetime
+    rng = np.random.default_rng(seed)
+    lines = []
+    nl = '\r\n' if crlf else '\n'
+    for t in range(traces.n_traces):
+        u = uuids[t] if uuids is not None else 'veh%07d' % t
+        a, b = int(traces.offsets[t]), int(traces.offsets[t + 1])
+        shift = 0
+        for k in range(a, b):
+            if split_gap and k == (a + b) // 2:
+                shift = split_gap
+            tm = int(traces.time[k]) + shift
+            acc = 5 + int(rng.integers(0, 20))
+            st = styles[int(rng.integers(0, len(styles)))]
+            la = _coord_text(traces.lat[k], st, rng)
+            lo = _coord_text(traces.lon[k], st, rng)
+            if kind == 'shard':
+                lines.append('%s,%d,%s,%s,%d%s' % (u, tm, la, lo, acc, nl))
+            else:
+                ts = datetime.datetime.fromtimestamp(tm, datetime.timezone.utc).strftime('%Y-%m-%d %H:%M:%S')
+                accs = '%.1f' % (acc - rng.random())
+                lines.append('%s|%s|x|y|z|%s|a|b|c|%s|%s%s' % (ts, u, accs, la, lo, nl))
+    n = len(lines)
+    m = int(n * shuffle)
+    if m:
+        src = rng.choice(n, m, replace=False)
+        moved = [lines[i] for i in src]
+        keep = np.ones(n, bool)
+        keep[src] = False
+        rest = [lines[i] for i in np.flatnonzero(keep)]
+        for ln in moved:
+            rest.insert(int(rng.integers(0, len(rest) + 1)), ln)
+        lines = rest
+    return ''.join(lines).encode()

@@ -47,3 +47,29 @@ def test_report_request_validation_without_gpu():
     code, body = m.report_json('{"uuid":"a","match_options":{"report_levels":[0]},'
                                '"trace":[{"lat":1,"lon":2,"time":3},{"lat":1,"lon":2,"time":4}]}')
     assert (code, body) == (400, '{"error":"match_options must include transition_levels array"}')
+
+
+def test_struct_layouts_against_c_header(tmp_path):
+    """ctypes mirrors of the header structs have the C compiler's sizes and offsets."""
+    import shutil
+    import subprocess
+    if not shutil.which('gcc'):
+        import pytest
+        pytest.skip('no C compiler')
+    structs = {'otr_trace_batch': _lib.TraceBatch, 'otr_ingest_format': _lib.IngestFormat,
+               'otr_ingest_result': _lib.IngestResult, 'otr_batch_result': _lib.BatchResult}
+    prog = ['#include <stdio.h>', '#include <stddef.h>', '#include "otr.h"', 'int main(void) {']
+    for cname, cls in structs.items():
+        prog.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f in cls._fields_:
+            prog.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, f[0], cname, f[0]))
+    prog.append('return 0; }')
+    src = tmp_path / 'layout.c'
+    src.write_text('\n'.join(prog))
+    exe = tmp_path / 'layout'
+    subprocess.check_call(['gcc', '-I' + os.path.join(ROOT, 'include'), str(src), '-o', str(exe)])
+    got = dict(line.split() for line in subprocess.check_output([str(exe)], text=True).splitlines())
+    for cname, cls in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(cls), cname
+        for f in cls._fields_:
+            assert int(got['%s.%s' % (cname, f[0])]) == getattr(cls, f[0]).offset, (cname, f[0])
