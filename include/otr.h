@@ -263,6 +263,8 @@ typedef struct otr_ingest_result {
   int32_t n_uuids;
   int64_t bad_line;       /* first rejected line (0-based), -1 if none */
   int32_t bad_reason;     /* OTR_INGEST_E_* */
+  float parse_ms;         /* device time of the line parse kernel (HIP events on the matcher's stream) */
+  float total_ms;         /* device time from the first kernel to the last (host syncs between included) */
   int32_t reserved;
   otr_trace_batch batch;  /* memory = OTR_MEM_DEVICE: offsets, lat, lon, time, accuracy, mode in HBM
                              (matcher-owned, valid until its next otr_ingest); levels/flags zero */

@@ -60,7 +60,8 @@ class IngestFormat(ctypes.Structure):
 class IngestResult(ctypes.Structure):
     _fields_ = [('n_lines', ctypes.c_int64), ('n_kept', ctypes.c_int64), ('n_probes', ctypes.c_int64),
                 ('n_traces', ctypes.c_int32), ('n_uuids', ctypes.c_int32), ('bad_line', ctypes.c_int64),
-                ('bad_reason', ctypes.c_int32), ('reserved', ctypes.c_int32), ('batch', TraceBatch),
+                ('bad_reason', ctypes.c_int32), ('parse_ms', ctypes.c_float), ('total_ms', ctypes.c_float),
+                ('reserved', ctypes.c_int32), ('batch', TraceBatch),
                 ('d_trace_uuid_off', ctypes.c_void_p), ('d_trace_uuid_len', ctypes.c_void_p)]
 
 

@@ -54,7 +54,7 @@ struct Matcher {
   std::vector<unsigned long long> h_seg_id, h_rep_id, h_rep_next;
   std::vector<uint8_t> h_seg_internal;
   std::vector<otr_tile_row> h_tile_rows;
-  hipEvent_t ev[20];
+  hipEvent_t ev[24];  // 0..19 batch stages, 20..23 ingest
   bool ev_init = false;
 
   template <class T>

@@ -1083,6 +1083,11 @@ int Matcher::ingest(const char* text, int64_t len, int memory, const otr_ingest_
   HIPCHK(hipMemcpyAsync(d_text, text, len, memory == OTR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                         stream));
   HIPCHK(hipMemsetAsync(bad, 0xFF, 8, stream));
+  if (!ev_init) {
+    for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+    ev_init = true;
+  }
+  HIPCHK(hipEventRecord(ev[20], stream));
   size_t tb_scan = 0;
   HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb_scan, cnt, cscan, (int)std::min<int64_t>(n_chunks, INT32_MAX),
                                           stream));
@@ -1138,7 +1143,9 @@ int Matcher::ingest(const char* text, int64_t len, int memory, const otr_ingest_
   f.idx[3] = fmt->lon_index;
   f.idx[4] = fmt->accuracy_index;
   for (int k = 0; k < 4; ++k) f.bbox[k] = fmt->bbox[k];
+  HIPCHK(hipEventRecord(ev[21], stream));
   k_ingest_parse<<<grid_for(n_lines, 256), 256, 0, stream>>>(L, f);
+  HIPCHK(hipEventRecord(ev[22], stream));
   unsigned long long hbad = ~0ull;
   HIPCHK(hipMemcpyAsync(&hbad, bad, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
@@ -1248,7 +1255,10 @@ int Matcher::ingest(const char* text, int64_t len, int memory, const otr_ingest_
   k_win_emit<<<grid_for(M, 256), 256, 0, stream>>>(perm, M, gid, ws, klen, poff, tpos, (int32_t)n_tr, L,
                                                    (uint8_t)fmt->mode, o);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ev[23], stream));
   HIPCHK(hipStreamSynchronize(stream));
+  HIPCHK(hipEventElapsedTime(&out->parse_ms, ev[21], ev[22]));
+  HIPCHK(hipEventElapsedTime(&out->total_ms, ev[20], ev[23]));
   otr_trace_batch& b = out->batch;
   b.n_traces = (int32_t)n_tr;
   b.memory = OTR_MEM_DEVICE;
