@@ -55,7 +55,7 @@ def main():
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--traces-per-gpu', type=int, default=10000)
-    ap.add_argument('--cpu-traces', type=int, default=1500, help='bounded oracle sample (0 = skip)')
+    ap.add_argument('--cpu-traces', type=int, default=6000, help='bounded oracle sample (0 = skip)')
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--delta', type=float, default=None, help='routing round width (perf knob, metres)')
     ap.add_argument('--streams', type=int, default=2,

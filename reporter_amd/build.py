@@ -132,6 +132,8 @@ def build_all(force=False):
     build_oracle(force)
     build_calib(force)
     lib = build_otr(force)
+    # test build: every first-tier search is sent down the retry tiers (tests/test_gpu_tiers.py)
+    build_otr(force, variant='tiercheck', defines=['OTR_FORCE_RETRY'])
     build_loadgen(force)
     return lib
 

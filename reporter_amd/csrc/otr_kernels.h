@@ -934,9 +934,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   }
   unsigned long long settled = 0, relaxed = 0, rounds = 0;
   search_init<CAP, false, G>(Ls);
-  const bool ok = search_run<CAP, false, G>(Ls, gr, H, mode_bit, search, root, bmm, (uint32_t)(a.delta * 1000.0),
-                                            tnode, tpart, hT, d0min, Kb, &settled, &relaxed, &rounds,
-                                            counters ? counters + 16 * kShards : nullptr) && fits;
+  bool ok = search_run<CAP, false, G>(Ls, gr, H, mode_bit, search, root, bmm, (uint32_t)(a.delta * 1000.0),
+                                      tnode, tpart, hT, d0min, Kb, &settled, &relaxed, &rounds,
+                                      counters ? counters + 16 * kShards : nullptr) && fits;
+#ifdef OTR_FORCE_RETRY
+  if (G == 2) ok = false;  // test build: every first-tier task takes the retry tiers
+#endif
   SearchLds<CAP, false>& L = Ls[Gr::g()];
   int64_t lab = -1;
   if (ok && tnode != kEmpty && !forced) {

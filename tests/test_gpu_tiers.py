@@ -1,0 +1,47 @@
+"""Retry tiers give the first tier's results: a test build of the library
+(libotr_tiercheck.so, -DOTR_FORCE_RETRY) sends EVERY first-tier search down the
+256/1024/4096-slot retry kernels, and must still match the oracle field by field.
+Runs in a child process (one library per process)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r'''
+import sys
+sys.path.insert(0, %r)
+from oracle import pyoracle as po
+from oracle.compare import compare
+from reporter_amd import matcher as M
+from reporter_amd.tools import gen
+for g, nt, npnt, sr, sig, seed, acc, over in [('city', 40, 100, 15, 10.0, 2, None, {}),
+                                             ('metro', 30, 60, 60, 50.0, 4, 50.0,
+                                              {'search_radius': 200, 'max_search_radius': 200})]:
+    path = gen.graph_path(g, %r)
+    M.configure(M.default_config(path, **over))
+    tr = gen.make_traces(path, nt, npnt, sr, sig, seed, 0.0, 0.0, acc)
+    m = M.Matcher()  # owns the host result arrays
+    r = m.match_batch(tr, copy_out=True)
+    assert r.status == 0, r.status
+    c = [int(r.counters[k]) for k in range(24)]
+    assert c[9] > 0, c  # the retry tiers settled nodes (and wrote every transition row)
+    from reporter_amd import _lib
+    got = _lib.result_to_numpy(r)
+    want = po.match_batch(po.Graph(path), tr, po.params(**{k: float(v) for k, v in over.items()}), threads=8)
+    errors, stats = compare(got, want)
+    assert not errors, errors
+print('tiers ok')
+'''
+
+
+def test_retry_tiers_equal_first_tier(graph_dir):
+    lib = os.path.join(ROOT, 'reporter_amd', 'libotr_tiercheck.so')
+    assert os.path.exists(lib), 'build first: python -m reporter_amd.build'
+    env = dict(os.environ, OTR_LIB=lib)
+    p = subprocess.run([sys.executable, '-c', CHILD % (ROOT, graph_dir)], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0 and 'tiers ok' in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
