@@ -256,7 +256,7 @@ def main():
                          'retry_settled_nodes': int(counters[9]), 'search_rounds': int(counters[13]),
                          'table_keys': int(counters[14]),
                          'tasks_keys_gt': {'64': int(counters[22]), '96': int(counters[15]), '128': int(counters[23])},
-                         'phase_cycles': [int(x) for x in counters[16:20]] if ('stamps' in _lib.LIB_PATH or 'cstamp' in _lib.LIB_PATH) else None},
+                         'phase_cycles': [int(x) for x in counters[16:22]] if ('stamps' in _lib.LIB_PATH or 'cstamp' in _lib.LIB_PATH) else None},
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)

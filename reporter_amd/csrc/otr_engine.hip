@@ -235,7 +235,7 @@ enum Slot {
   S_C_ROUTE_OFF, S_C_SEG_OFF, S_C_WAY_OFF, S_C_REP_OFF, S_C_ARGS, S_C_ROUTE, S_C_SEG_ID, S_C_SEG_START,
   S_C_SEG_END, S_C_SEG_LEN, S_C_SEG_QUEUE, S_C_SEG_INTERNAL, S_C_SEG_BSHAPE, S_C_SEG_ESHAPE, S_C_SEG_WAY_N,
   S_C_SEG_WAY, S_C_SEG_WAY_OFF, S_C_REP_ID, S_C_REP_NEXT, S_C_REP_T0, S_C_REP_T1, S_C_REP_LEN, S_C_REP_QUEUE,
-  S_IN_TEXT, S_IN_CNT, S_IN_CSCAN, S_IN_NL, S_IN_HASH, S_IN_UOFF, S_IN_ULEN, S_IN_TIME, S_IN_LAT, S_IN_LON,
+  S_TASK_REC, S_IN_TEXT, S_IN_CNT, S_IN_CSCAN, S_IN_NL, S_IN_HASH, S_IN_UOFF, S_IN_ULEN, S_IN_TIME, S_IN_LAT, S_IN_LON,
   S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
@@ -518,8 +518,17 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     return OTR_DEVICE_ERROR;
   }
   if (S > 0) k_prep<<<grid_for(S, 4), 256, 0, stream>>>(g, pr);
+  uint4* task_rec = need<uint4>(S_TASK_REC, 2 * (size_t)std::max<int64_t>(NT, 1));
+  if (!task_rec) {
+    if (err) *err = "device allocation failed (task records)";
+    return OTR_DEVICE_ERROR;
+  }
+  if (NT > 0)
+    k_task_rec<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_state, task_mask, sb.prev, sb.bound, sb.forced, cb.count,
+                                                      cb.edge, g.edge_dst, state_trace, b.mode, pr.cprep, task_rec);
   ra.heur = pr.heur;
   ra.cprep = pr.cprep;
+  ra.rec = task_rec;
   ra.delta = mp.delta;
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
   ra.overflow_flag = task_ovf;

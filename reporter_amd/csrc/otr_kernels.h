@@ -871,10 +871,38 @@ struct RouteArgs {
   const double* radius;       // per state search radius (heuristic disk)
   const Heur* heur;           // per state (k_prep)
   const uint4* cprep;         // per state candidate (k_prep)
+  const uint4* rec;           // per task, 2 x uint4 (k_task_rec)
   double delta;
   double inv_beta[OTR_MODES];
   int32_t* overflow_flag;     // per task
 };
+
+// K2c: one record per search task with everything its setup and its transition rows
+// need that sits behind a chain of dependent loads (task → state → previous state →
+// first source edge → root node; mode through the trace): the search kernels read two
+// 16-B words instead of walking that chain twice (before and after the search).
+//   rec[2t]   = {s, sp, root, bound_mm}
+//   rec[2t+1] = {d0min, Kb | mode << 8 | forced << 10, mask lo, mask hi}
+__global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const unsigned long long* task_mask,
+                           const int64_t* prev, const double* bound, const uint8_t* forced, const int32_t* cand_count,
+                           const uint32_t* cand_edge, const uint32_t* edge_dst, const int32_t* state_trace,
+                           const uint8_t* mode, const uint4* cprep, uint4* rec) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tasks) return;
+  const int64_t s = task_state[t];
+  const unsigned long long mask = task_mask[t];
+  const int64_t sp = prev[s];
+  const int md = mode[state_trace[s]] < OTR_MODES ? mode[state_trace[s]] : 0;
+  const uint32_t root = edge_dst[cand_edge[sp * OTR_KMAX + (__ffsll((long long)mask) - 1)]];
+  uint32_t d0min = 0xFFFFFFFFu;
+  for (unsigned long long m = mask; m; m &= m - 1) {
+    const uint32_t d0 = cprep[sp * OTR_KMAX + (__ffsll((long long)m) - 1)].w;
+    d0min = d0 < d0min ? d0 : d0min;
+  }
+  const uint32_t meta = (uint32_t)cand_count[s] | ((uint32_t)md << 8) | ((forced[s] ? 1u : 0u) << 10);
+  rec[2 * t] = make_uint4((uint32_t)s, (uint32_t)sp, root, (uint32_t)bound_mm_of(bound[s]));
+  rec[2 * t + 1] = make_uint4(d0min, meta, (uint32_t)mask, (uint32_t)(mask >> 32));
+}
 
 #ifndef OTR_ROUTE2_WAVES
 #define OTR_ROUTE2_WAVES 8
@@ -890,21 +918,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   const int64_t tw = w * G + Gr::g();
   const bool have = tw < a.n_tasks;
   const int64_t task = have ? (a.task_list ? a.task_list[tw] : tw) : 0;
+  OTR_STAMP(ts_in);
   // ---- search inputs (only these stay live through the search)
   bool search, fits, forced;
   uint32_t tnode = kEmpty, tpart = 0, hT = 0, d0min = 0xFFFFFFFFu, root = 0, bmm = 0, mode_bit = 1;
   int Kb;
   Heur H;
   {
-    const int64_t s = a.task_state[task];
-    const unsigned long long mask = have ? a.task_mask[task] : 0ull;
-    const int64_t sp = a.prev[s];
-    Kb = a.cand_count[s];
+    const uint4 r0 = have ? a.rec[2 * task] : make_uint4(0u, 0u, 0u, 0u);
+    const uint4 r1 = have ? a.rec[2 * task + 1] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+    const int64_t s = r0.x;
+    const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
+    const int64_t sp = r0.y;
+    Kb = (int)(r1.y & 0xFFu);
     fits = Kb <= Gr::GL;  // targets are lanes of the group: wider steps go to a G = 1 tier
-    const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
-    mode_bit = 1u << mode;
-    bmm = (uint32_t)bound_mm_of(a.bound[s]);
-    if (have) root = gr.edge_dst[a.cand_edge[sp * OTR_KMAX + (__ffsll((long long)mask) - 1)]];
+    mode_bit = 1u << ((r1.y >> 8) & 3u);
+    bmm = r0.w;
+    root = r0.z;
+    d0min = r1.x;
     uint32_t ej = 0;
     double pj = 0;
     bool needed = false;
@@ -919,11 +950,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
       const int i = __ffsll((long long)m) - 1;
       const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
       const double pi = a.cand_p[sp * OTR_KMAX + i];
-      const uint32_t d0 = a.cprep[sp * OTR_KMAX + i].w;
-      d0min = d0 < d0min ? d0 : d0min;
       if (lane < Kb && !(ej == ei && pj >= pi)) needed = true;
     }
-    forced = have && a.forced[s];
+    forced = have && ((r1.y >> 10) & 1u);
     const unsigned long long need_mask = __ballot(needed);
     search = have && fits && !forced && Gr::mine(need_mask) != 0ull;
     H = a.heur[s];
@@ -933,6 +962,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
     }
   }
   unsigned long long settled = 0, relaxed = 0, rounds = 0;
+  OTR_STAMP(ts_set);
   search_init<CAP, false, G>(Ls);
   bool ok = search_run<CAP, false, G>(Ls, gr, H, mode_bit, search, root, bmm, (uint32_t)(a.delta * 1000.0),
                                       tnode, tpart, hT, d0min, Kb, &settled, &relaxed, &rounds,
@@ -940,6 +970,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
 #ifdef OTR_FORCE_RETRY
   if (G == 2) ok = false;  // test build: every first-tier task takes the retry tiers
 #endif
+  OTR_STAMP(ts_srch);
   SearchLds<CAP, false>& L = Ls[Gr::g()];
   int64_t lab = -1;
   if (ok && tnode != kEmpty && !forced) {
@@ -949,10 +980,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   // ---- transition rows: re-read the step (cached) rather than hold it live through the search
   asm volatile("" ::: "memory");
   if (have && (ok || forced)) {
-    const int64_t s = a.task_state[task];
-    const unsigned long long mask = a.task_mask[task];
-    const int64_t sp = a.prev[s];
-    const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+    const uint4 r0 = a.rec[2 * task], r1 = a.rec[2 * task + 1];
+    const int64_t s = r0.x;
+    const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
+    const int64_t sp = r0.y;
+    const int mode = (int)((r1.y >> 8) & 3u);
     const double gcd = a.g[s], inv_beta = a.inv_beta[mode];
     double* trow = a.trans + a.trans_off[s];
     if (lane < Kb) {
@@ -974,6 +1006,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   // overflow: retry with a bigger table; a first-tier search with a long bound (> 1.9 km)
   // that outgrew 160 slots goes straight to the 1024-slot tier (flag 2)
   if (have && !ok && !forced && lane == 0) a.overflow_flag[task] = (G == 2 && bmm > 1900000u) ? 2 : 1;
+#ifdef OTR_STAMPS
+  if (G == 2 && counters && threadIdx.x == 0) {  // task setup and transition rows, wave cycles
+    OTR_STAMP(ts_out);
+    const int sh = blockIdx.x & (kShards - 1);
+    atomicAdd(&counters[20 * kShards + sh], ts_set - ts_in);
+    atomicAdd(&counters[21 * kShards + sh], ts_out - ts_srch);
+  }
+#endif
   if (counters) {
     // wave totals: lane sums by DPP, per-group values read from each group's lane 0
     settled = wave_sum_u32((uint32_t)settled);
