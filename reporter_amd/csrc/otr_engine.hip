@@ -326,6 +326,30 @@ __global__ void k_step_list(int64_t n_states, const int64_t* prev, const uint8_t
 
 static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 
+// Retry tiers of the route search after the first (160-slot, 2 per wave) tier, as
+// capacity * 10 + searches per wave.  512x2 (two 512-slot searches per wave) takes the
+// long-bound overflows: C4 route 117 -> 112 ms against a 1024-slot G = 1 tier.  The last tier is always the 4096-slot one (its
+// overflows are per-trace errors).  OTR_TIERS overrides the list for A/B runs, e.g.
+// "256,512x2,1024,4096".
+static std::vector<int> route_tiers() {
+  std::vector<int> t;
+  const char* env = getenv("OTR_TIERS");
+  std::string spec = env ? env : "256,512x2,1024,4096";
+  size_t i = 0;
+  while (i < spec.size()) {
+    size_t j = spec.find(',', i);
+    if (j == std::string::npos) j = spec.size();
+    const std::string item = spec.substr(i, j - i);
+    const int cap = atoi(item.c_str());
+    const int gw = item.find('x') != std::string::npos ? atoi(item.c_str() + item.find('x') + 1) : 1;
+    const int code = cap * 10 + gw;
+    if (code == 2561 || code == 5121 || code == 10241 || code == 3842 || code == 5122) t.push_back(code);
+    i = j + 1;
+  }
+  t.push_back(40961);
+  return t;
+}
+
 int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err) {
   GraphState& gs = graph_state();
   if (!gs.ready) {
@@ -532,6 +556,10 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   ra.delta = mp.delta;
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
   ra.overflow_flag = task_ovf;
+  // bounds > 1.9 km skip the first tier (most outgrow 160 slots: C4 route 24 -> 15 ms)
+  static const uint32_t direct_bmm =
+      getenv("OTR_DIRECT_BMM") ? (uint32_t)strtoul(getenv("OTR_DIRECT_BMM"), nullptr, 10) : 1900000u;  // A/B knob
+  ra.direct_bmm = direct_bmm;
   if (NT > 0) {
     tb(OTR_STAGE_ROUTE);
     // two searches per wave (CAP 160 tables); wider steps and overflows retry below
@@ -547,8 +575,11 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     int64_t* list = need<int64_t>(S_LIST, NT);
     unsigned long long* cnt = need<unsigned long long>(S_MISC, 4);
     tb(OTR_STAGE_ROUTE_BIG);
-    // first-tier overflows flagged 2 (long bounds) skip the 256-slot tier
-    for (int tier = 0; tier < 3; ++tier) {
+    // first-tier overflows flagged 2 (long bounds) skip the 256-slot tier;
+    // OTR_TIERS (A/B knob) lists the retry kernels, e.g. "256,512x2,1024,4096"
+    static const std::vector<int> tiers = route_tiers();
+    const int ntier = (int)tiers.size();
+    for (int tier = 0; tier < ntier; ++tier) {
       HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
       k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, tier == 0 ? 1 : 0, list, cnt);
       unsigned long long novf = 0;
@@ -559,10 +590,16 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.n_tasks = (int64_t)novf;
-      if (tier == 0) k_route<256, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
-      else if (tier == 1) k_route<1024, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
-      else k_route<4096, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, d_counters + 6 * kShards);
-      if (tier == 2) {
+      unsigned long long* rc = d_counters + 6 * kShards;
+      switch (tiers[tier]) {
+        case 2561: k_route<256, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
+        case 5121: k_route<512, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
+        case 10241: k_route<1024, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
+        case 3842: k_route<384, 2><<<(unsigned)((novf + 1) / 2), 64, 0, stream>>>(g, rb, rc); break;
+        case 5122: k_route<512, 2><<<(unsigned)((novf + 1) / 2), 64, 0, stream>>>(g, rb, rc); break;
+        default: k_route<4096, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
+      }
+      if (tier == ntier - 1) {
         HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
         k_collect<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, list, cnt);
         HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));

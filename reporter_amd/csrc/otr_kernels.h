@@ -875,6 +875,7 @@ struct RouteArgs {
   double delta;
   double inv_beta[OTR_MODES];
   int32_t* overflow_flag;     // per task
+  uint32_t direct_bmm;        // first tier: bounds above this go straight to the retry tiers
 };
 
 // K2c: one record per search task with everything its setup and its transition rows
@@ -932,6 +933,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
     const int64_t sp = r0.y;
     Kb = (int)(r1.y & 0xFFu);
     fits = Kb <= Gr::GL;  // targets are lanes of the group: wider steps go to a G = 1 tier
+    if (G == 2 && !a.task_list && r0.w > a.direct_bmm) fits = false;
     mode_bit = 1u << ((r1.y >> 8) & 3u);
     bmm = r0.w;
     root = r0.z;
@@ -968,7 +970,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
                                       tnode, tpart, hT, d0min, Kb, &settled, &relaxed, &rounds,
                                       counters ? counters + 16 * kShards : nullptr) && fits;
 #ifdef OTR_FORCE_RETRY
-  if (G == 2) ok = false;  // test build: every first-tier task takes the retry tiers
+  if (G == 2 && !a.task_list) ok = false;  // test build: every first-tier task takes the retry tiers
 #endif
   OTR_STAMP(ts_srch);
   SearchLds<CAP, false>& L = Ls[Gr::g()];

@@ -1,6 +1,9 @@
 """Retry tiers give the first tier's results: a test build of the library
 (libotr_tiercheck.so, -DOTR_FORCE_RETRY) sends EVERY first-tier search down the
-256/1024/4096-slot retry kernels, and must still match the oracle field by field.
+retry kernels, and must still match the oracle field by field.  Parametrised over
+the retry-tier list (OTR_TIERS): the default 256 → 512x2 → 1024 → 4096 chain, a chain
+that starts with two-searches-per-wave 384-slot tables, and direct 1024/4096; with
+OTR_DIRECT_BMM=0 every search skips the first tier on its own.
 Runs in a child process (one library per process)."""
 import os
 import subprocess
@@ -38,10 +41,17 @@ print('tiers ok')
 '''
 
 
-def test_retry_tiers_equal_first_tier(graph_dir):
+@pytest.mark.parametrize('tiers,direct', [(None, None), ('384x2,512', None), ('1024', '0')])
+def test_retry_tiers_equal_first_tier(graph_dir, tiers, direct):
     lib = os.path.join(ROOT, 'reporter_amd', 'libotr_tiercheck.so')
     assert os.path.exists(lib), 'build first: python -m reporter_amd.build'
     env = dict(os.environ, OTR_LIB=lib)
+    env.pop('OTR_TIERS', None)
+    env.pop('OTR_DIRECT_BMM', None)
+    if tiers:
+        env['OTR_TIERS'] = tiers
+    if direct is not None:
+        env['OTR_DIRECT_BMM'] = direct
     p = subprocess.run([sys.executable, '-c', CHILD % (ROOT, graph_dir)], env=env, capture_output=True, text=True,
                        timeout=240)
     assert p.returncode == 0 and 'tiers ok' in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
