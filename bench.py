@@ -74,13 +74,25 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', 0))
     import torch
     import torch.distributed as dist
+    # OTR_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on one GPU
+    # (RCCL refuses two ranks per device); the histogram exchange is then an all-reduce
+    # whose owner slice equals the reduce-scatter output
+    backend = os.environ.get('OTR_BENCH_BACKEND', 'nccl')
+    if backend != 'nccl':
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            if backend == 'nccl':
+                dist.barrier(device_ids=[local])
+            else:
+                dist.barrier()
 
     from reporter_amd import _lib
     from reporter_amd import matcher as M
@@ -160,8 +172,12 @@ def main():
     def step():
         rs = list(pool.map(run_part, range(ns)))
         torch.sum(torch.stack(hists), dim=0, out=hist)  # combine the per-stream histograms
-        if world > 1:
+        if world > 1 and backend == 'nccl':
             dist.reduce_scatter_tensor(hist_out, hist, op=dist.ReduceOp.SUM)
+        elif world > 1:
+            hc = hist.cpu()
+            dist.all_reduce(hc, op=dist.ReduceOp.SUM)
+            hist_out.copy_(hc[rank * hist_out.numel():(rank + 1) * hist_out.numel()])
         torch.cuda.current_stream().synchronize()
         return rs
 
@@ -181,6 +197,8 @@ def main():
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     probes = torch.tensor([float(mine.n_probes)], dtype=torch.float64, device=dev)
     if world > 1:
+        if backend != 'nccl':
+            el, probes = el.cpu(), probes.cpu()
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(probes, op=dist.ReduceOp.SUM)
     elapsed = float(el.item())
@@ -236,7 +254,7 @@ def main():
                                        {'c2': '', 'c4': ', accuracy 50 m, search radius 200 m',
                                         'c5mix': ', modes 60% auto / 25% bicycle / 15% pedestrian'}[args.workload]),
                        'probes_per_step': int(total_probes),
-                       'parallelism': 'uuid-sharded dp%d + RCCL reduce-scatter of [hour][segment][speed] histogram'
+                       'parallelism': ('uuid-sharded dp%d + ' + ('RCCL reduce-scatter' if backend == 'nccl' else 'gloo all-reduce (rehearsal)') + ' of [hour][segment][speed] histogram')
                                       % world if world > 1 else 'single GPU',
                        'streams': ns,
                        'stage_ms_per_stream': stage_ms,
