@@ -86,14 +86,27 @@ __device__ inline bool project_edge(const DevGraph& g, uint4 rec, uint32_t mode_
   const uint32_t k0 = rec.y, k1 = rec.z;
   // the first kPre points are loaded together (one memory round trip instead of one per
   // point); longer polylines continue point by point
+  // Named registers rotated through the loop, loads at clamped (always valid) indices:
+  // an indexed array, or `q < k1 ? shape_ll[q] : 0`, was compiled into a select between
+  // the global address and a stack slot (flat loads + 24 B of scratch stores per lane and
+  // sweep iteration: 1.4 GB of WRITE_SIZE per C2 launch).
   constexpr uint32_t kPre = 4;
-  int2 pre[kPre];
-#pragma unroll
-  for (uint32_t i = 0; i < kPre; ++i) pre[i] = k0 + i < k1 ? g.shape_ll[k0 + i] : make_int2(0, 0);
-  int2 pa = pre[0];
+  const uint32_t qmax = k0 < k1 ? k1 - 1 : 0u;
+  const int2 pre0 = g.shape_ll[k0 < qmax ? k0 : qmax];
+  int2 q1 = g.shape_ll[k0 + 1 < qmax ? k0 + 1 : qmax];
+  int2 q2 = g.shape_ll[k0 + 2 < qmax ? k0 + 2 : qmax];
+  int2 q3 = g.shape_ll[k0 + 3 < qmax ? k0 + 3 : qmax];
+  int2 pa = pre0;
   for (uint32_t k = k0; k + 1 < k1; ++k) {
     const uint32_t i = k + 1 - k0;
-    const int2 pb = i < kPre ? (i == 1 ? pre[1] : (i == 2 ? pre[2] : pre[3])) : g.shape_ll[k + 1];
+    int2 pb;
+    if (i < kPre) {
+      pb = q1;
+      q1 = q2;
+      q2 = q3;
+    } else {
+      pb = g.shape_ll[k + 1];
+    }
     const double ax = (e6(pa.y) - plon) * mpl;
     const double ay = (e6(pa.x) - plat) * kMetersPerDeg;
     const double bx = (e6(pb.y) - plon) * mpl;
