@@ -44,9 +44,9 @@ def route_bytes(c):
     device work counters: 64 B per task (task record, step metadata, root lookup),
     32 B per settled node (its adjacency record), 16 B per source candidate
     (edge, fraction, length), 20 B per target read (edge, fraction, src, length),
-    8 B per transition entry written."""
+    4 B per transition entry written (route length in mm, u32; v26 — 8 B fp64 costs before)."""
     tasks, settled, trans, targets, sources = c[5], c[3], c[6], c[11], c[12]
-    return 64 * tasks + 32 * settled + 16 * sources + 20 * targets + 8 * trans
+    return 64 * tasks + 32 * settled + 16 * sources + 20 * targets + 4 * trans
 
 
 def main():

@@ -493,7 +493,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   int64_t* task_state = need<int64_t>(S_TASK_STATE, NT);
   unsigned long long* task_mask = need<unsigned long long>(S_TASK_MASK, NT);
   int32_t* task_ovf = need<int32_t>(S_TASK_OVF, NT);
-  double* trans = need<double>(S_TRANS, NTR);
+  uint32_t* trans = need<uint32_t>(S_TRANS, NTR);
   if (!task_state || !task_mask || !task_ovf || !trans) {
     if (err) *err = "device allocation failed (transitions)";
     return OTR_DEVICE_ERROR;
@@ -628,8 +628,10 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   va.prev = sb.prev;
   va.trans_off = trans_off;
   va.trans = trans;
+  va.g = sb.g;
   va.mode = b.mode;
   for (int m = 0; m < OTR_MODES; ++m) va.inv2s2[m] = mp.m[m].inv2s2;
+  for (int m = 0; m < OTR_MODES; ++m) va.inv_beta[m] = mp.m[m].inv_beta;
   va.bp = need<int8_t>(S_BP, (size_t)S * OTR_KMAX);
   va.brk = need<uint8_t>(S_BRK, S);
   va.end_win = need<int32_t>(S_END_WIN, S);

@@ -494,6 +494,7 @@ struct SearchLds {
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kInq = 0x80000000u;
 constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
+constexpr uint32_t kNoRoute = 0xFFFFFFFFu;  // transition array: no valid route within the bound
 
 // Diagnostic build only (-DOTR_STAMPS): shader-clock stamps per search phase, summed
 // into counter kinds 16..19.  The production build compiles them out.
@@ -872,7 +873,7 @@ struct RouteArgs {
   const double* bound;
   const uint8_t* forced;
   const int64_t* trans_off;
-  double* trans;
+  uint32_t* trans;            // route length (mm) per transition, kNoRoute when invalid
   const int32_t* cand_count;
   const uint32_t* cand_edge;
   const double* cand_p;
@@ -999,9 +1000,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
     const int64_t s = r0.x;
     const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
     const int64_t sp = r0.y;
-    const int mode = (int)((r1.y >> 8) & 3u);
-    const double gcd = a.g[s], inv_beta = a.inv_beta[mode];
-    double* trow = a.trans + a.trans_off[s];
+    uint32_t* trow = a.trans + a.trans_off[s];
     if (lane < Kb) {
       const uint32_t ej = a.cand_edge[s * OTR_KMAX + lane];
       const double pj = a.cand_p[s * OTR_KMAX + lane];
@@ -1013,8 +1012,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
         if (forced) r = -1;
         else if (ej == ei && pj >= pi) r = part_mm(pj - pi, gr.len_mm[ei]);
         else if (lab >= 0) r = (int64_t)a.cprep[sp * OTR_KMAX + i].w + lab + tpart;
-        trow[(int64_t)i * Kb + lane] =
-            (r >= 0 && r <= (int64_t)bmm) ? fabs((double)r / 1000.0 - gcd) * inv_beta : __builtin_huge_val();
+        trow[(int64_t)i * Kb + lane] = (r >= 0 && r <= (int64_t)bmm) ? (uint32_t)r : kNoRoute;
       }
     }
   }
@@ -1071,9 +1069,11 @@ struct ViterbiArgs {
   const double* cand_sqd;
   const int64_t* prev;
   const int64_t* trans_off;
-  const double* trans;
+  const uint32_t* trans;   // route mm per transition (k_route), kNoRoute when invalid
+  const double* g;         // great-circle distance of the step ending at the state
   const uint8_t* mode;
   double inv2s2[OTR_MODES];
+  double inv_beta[OTR_MODES];
   int8_t* bp;          // [n_states][OTR_KMAX]
   uint8_t* brk;        // sub-path starts here
   int32_t* end_win;    // winner of a state that ends a sub-path
@@ -1107,7 +1107,8 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
   const int lane = threadIdx.x;
   unsigned long long cells = 0;
   for (int t = blockIdx.x; t < a.n_traces; t += gridDim.x) {
-    const double inv2s2 = a.inv2s2[a.mode[t] < OTR_MODES ? a.mode[t] : 0];
+    const int md = a.mode[t] < OTR_MODES ? a.mode[t] : 0;
+    const double inv2s2 = a.inv2s2[md], inv_beta = a.inv_beta[md];
     const int64_t so = a.trace_state_off[t], eo = a.trace_state_off[t + 1];
     int64_t prev_s = -1;
     int Kp = 0;
@@ -1126,17 +1127,19 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
         double best = __builtin_huge_val();
         if (lane < K) {
           // 16 independent transition loads in flight per chunk, then the min-plus scan in
-          // ascending i (strict <: lowest index among equal minima)
-          const double* tr = a.trans + a.trans_off[s];
+          // ascending i (strict <: lowest index among equal minima).  The array holds route
+          // lengths (u32 mm, half the bytes of a cost); the transition cost |route - g| / beta
+          // (K4) is evaluated here, with the same operations k_route used to apply.
+          const uint32_t* tr = a.trans + a.trans_off[s];
+          const double gcd = a.g[s];
           for (int i0 = 0; i0 < Kp; i0 += 16) {
-            double tv[16];
+            uint32_t tv[16];
 #pragma unroll
-            for (int u = 0; u < 16; ++u)
-              tv[u] = i0 + u < Kp ? tr[(int64_t)(i0 + u) * K + lane] : __builtin_huge_val();
+            for (int u = 0; u < 16; ++u) tv[u] = i0 + u < Kp ? tr[(int64_t)(i0 + u) * K + lane] : kNoRoute;
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-              const double ti = tv[u];
-              if (ti == __builtin_huge_val()) continue;
+              if (tv[u] == kNoRoute) continue;
+              const double ti = fabs((double)tv[u] / 1000.0 - gcd) * inv_beta;
               const double ci = s_cost[i0 + u];
               if (ci == __builtin_huge_val()) continue;
               const double c = ci + ti;
