@@ -480,7 +480,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   int64_t* task_off = need<int64_t>(S_TASK_OFF, S + 1);
   int64_t* trans_off = need<int64_t>(S_TRANS_OFF, S + 1);
   tb(OTR_STAGE_LINK);
-  k_link<<<grid_for(T, 256), 256, 0, stream>>>(b, mp, trace_state_off, state_probe, cb.count, sb);
+  k_link<<<grid_for(T, 4), 256, 0, stream>>>(b, mp, trace_state_off, state_probe, cb.count, sb);
   te(OTR_STAGE_LINK);
   if (S > 0)
     k_tasks<<<grid_for(S, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, nullptr,

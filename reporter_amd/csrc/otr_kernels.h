@@ -332,28 +332,41 @@ struct StepBuf {
   int64_t* ntrans;    // K[prev]*K[s]
 };
 
-__global__ void k_link(BatchDev b, ModeParams mp, const int64_t* trace_state_off, const int64_t* state_probe,
-                       const int32_t* cand_count, StepBuf st) {
-  int t = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per trace, lane = state within a chunk of 64: the previous active state is
+// the highest active lane below (ballot), or the last active state of earlier chunks —
+// the trace's serial chain becomes one step per 64 states.
+__global__ __launch_bounds__(256) void k_link(BatchDev b, ModeParams mp, const int64_t* trace_state_off,
+                                              const int64_t* state_probe, const int32_t* cand_count, StepBuf st) {
+  const int64_t t = (int64_t)blockIdx.x * (blockDim.x / OTR_WAVE) + threadIdx.x / OTR_WAVE;
+  const int lane = threadIdx.x % OTR_WAVE;
   if (t >= b.n_traces) return;
   const MatchParams& P = mp.m[b.mode[t] < OTR_MODES ? b.mode[t] : 0];
-  int64_t last = -1;
-  for (int64_t s = trace_state_off[t]; s < trace_state_off[t + 1]; ++s) {
-    st.ntrans[s] = 0;
-    if (cand_count[s] <= 0) {
-      st.prev[s] = -2;
-      continue;
+  const int64_t so = trace_state_off[t], eo = trace_state_off[t + 1];
+  int64_t last = -1;  // wave-uniform: last active state of the chunks before
+  for (int64_t base = so; base < eo; base += OTR_WAVE) {
+    const int64_t s = base + lane;
+    const bool in = s < eo;
+    const int K = in ? cand_count[s] : 0;
+    const unsigned long long am = __ballot(K > 0);
+    const unsigned long long below = am & ((1ull << lane) - 1ull);
+    const int64_t pv = below ? base + (63 - __clzll((long long)below)) : last;
+    if (in) {
+      st.ntrans[s] = 0;
+      if (K <= 0) {
+        st.prev[s] = -2;
+      } else {
+        st.prev[s] = pv;
+        if (pv >= 0) {
+          const int64_t ia = state_probe[pv], ib = state_probe[s];
+          const double gcd = gc_dist(b.lat[ia], b.lon[ia], b.lat[ib], b.lon[ib]);
+          st.g[s] = gcd;
+          st.forced[s] = gcd > P.breakage_distance;
+          st.bound[s] = route_bound(P, gcd);
+          st.ntrans[s] = (int64_t)cand_count[pv] * K;
+        }
+      }
     }
-    st.prev[s] = last;
-    if (last >= 0) {
-      const int64_t ia = state_probe[last], ib = state_probe[s];
-      const double gcd = gc_dist(b.lat[ia], b.lon[ia], b.lat[ib], b.lon[ib]);
-      st.g[s] = gcd;
-      st.forced[s] = gcd > P.breakage_distance;
-      st.bound[s] = route_bound(P, gcd);
-      st.ntrans[s] = (int64_t)cand_count[last] * cand_count[s];
-    }
-    last = s;
+    if (am) last = base + (63 - __clzll((long long)am));
   }
 }
 
