@@ -55,7 +55,7 @@ struct DevGraph {
   const uint32_t* seg_len;
   const uint32_t* cell_row;
   const uint32_t* cell_edge;
-  const uint4* cell_rec;       // per cell entry {edge, shape begin, shape end, attr}: one 16-B load
+  const uint4* cell_rec;       // per cell entry 3 x 16 B: {edge, shape begin, shape end, attr}, shape points 0-1, 2-3
   const uint4* edge_pack;      // {dst, len_mm, attr, 0}: one 16-B load per relaxed edge (CSR tail)
   const uint4* adj;            // 4 x uint4 per node: {dst | access<<28 | more<<31, len_mm, dst lat_e6, dst lon_e6}
   const uint32_t* len_mm;      // routing length, whole millimetres

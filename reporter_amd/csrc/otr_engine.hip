@@ -182,10 +182,19 @@ int engine_configure(const Config& cfg, std::string* err) {
     // candidate-search view: each grid-cell entry carries its edge's shape range and attributes
     const uint32_t* cedge = (const uint32_t*)(base + h.array_offset[OTR_A_CELL_EDGE]);
     const uint32_t* eshape = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_SHAPE]);
-    std::vector<uint4> crec(h.n_cell_entries + 1, make_uint4(0u, 0u, 0u, 0u));
+    // 48 B per entry: {edge, shape begin, shape end, attr} + the first four shape points
+    const int32_t* sll = (const int32_t*)(base + h.array_offset[OTR_A_SHAPE_LL]);
+    std::vector<uint4> crec(3 * ((size_t)h.n_cell_entries + 1), make_uint4(0u, 0u, 0u, 0u));
     for (uint64_t q = 0; q < h.n_cell_entries; ++q) {
-      const uint32_t e = cedge[q];
-      crec[q] = make_uint4(e, eshape[e], eshape[e + 1], attr[e]);
+      const uint32_t e = cedge[q], k0 = eshape[e], k1 = eshape[e + 1];
+      crec[3 * q] = make_uint4(e, k0, k1, attr[e]);
+      uint32_t pt[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+      for (uint32_t i = 0; i < 4 && k0 + i < k1; ++i) {
+        pt[2 * i] = (uint32_t)sll[2ull * (k0 + i)];
+        pt[2 * i + 1] = (uint32_t)sll[2ull * (k0 + i) + 1];
+      }
+      crec[3 * q + 1] = make_uint4(pt[0], pt[1], pt[2], pt[3]);
+      crec[3 * q + 2] = make_uint4(pt[4], pt[5], pt[6], pt[7]);
     }
     g.cell_rec = (const uint4*)upv(crec.data(), sizeof(uint4) * crec.size());
   }

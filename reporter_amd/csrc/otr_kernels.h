@@ -75,27 +75,24 @@ __device__ inline bool cand_less(double da, uint32_t ea, double db, uint32_t eb)
 // Projection of probe (plat, plon) onto edge e's polyline in the probe-local metric;
 // true when the edge is a candidate owned by grid cell (r, c) (the cell holding the
 // snapped point), with squared distance d2 and fraction along the edge.
-// rec = the cell entry's {edge, first shape point, end shape point, attr} (DevGraph::cell_rec).
+// rec = the cell entry's {edge, first shape point, end shape point, attr}, pts01/pts23 its
+// first four shape points (DevGraph::cell_rec, 48 B per entry).
 // Returns the grid cell (sr, sc) of the snapped point through *sr/*sc.
-__device__ inline bool project_edge(const DevGraph& g, uint4 rec, uint32_t mode_bit, double plat, double plon,
-                                    double mpl, double r2, int64_t* sr_out, int64_t* sc_out, double* d2_out,
-                                    double* frac_out, unsigned long long* tests) {
+__device__ inline bool project_edge(const DevGraph& g, uint4 rec, uint4 pts01, uint4 pts23, uint32_t mode_bit,
+                                    double plat, double plon, double mpl, double r2, int64_t* sr_out, int64_t* sc_out,
+                                    double* d2_out, double* frac_out, unsigned long long* tests) {
   if (!(rec.w & mode_bit)) return false;
   double best = __builtin_huge_val();
   double best_along = 0.0, bqx = 0.0, bqy = 0.0, acc = 0.0;
   const uint32_t k0 = rec.y, k1 = rec.z;
-  // the first kPre points are loaded together (one memory round trip instead of one per
-  // point); longer polylines continue point by point
-  // Named registers rotated through the loop, loads at clamped (always valid) indices:
-  // an indexed array, or `q < k1 ? shape_ll[q] : 0`, was compiled into a select between
-  // the global address and a stack slot (flat loads + 24 B of scratch stores per lane and
-  // sweep iteration: 1.4 GB of WRITE_SIZE per C2 launch).
+  // the first kPre shape points travel in the cell record itself (DevGraph::cell_rec:
+  // no dependent shape load for edges of up to 4 points — every edge of the synthetic
+  // graphs); longer polylines continue point by point from shape_ll
   constexpr uint32_t kPre = 4;
-  const uint32_t qmax = k0 < k1 ? k1 - 1 : 0u;
-  const int2 pre0 = g.shape_ll[k0 < qmax ? k0 : qmax];
-  int2 q1 = g.shape_ll[k0 + 1 < qmax ? k0 + 1 : qmax];
-  int2 q2 = g.shape_ll[k0 + 2 < qmax ? k0 + 2 : qmax];
-  int2 q3 = g.shape_ll[k0 + 3 < qmax ? k0 + 3 : qmax];
+  const int2 pre0 = make_int2((int)pts01.x, (int)pts01.y);
+  int2 q1 = make_int2((int)pts01.z, (int)pts01.w);
+  int2 q2 = make_int2((int)pts23.x, (int)pts23.y);
+  int2 q3 = make_int2((int)pts23.z, (int)pts23.w);
   int2 pa = pre0;
   for (uint32_t k = k0; k + 1 < k1; ++k) {
     const uint32_t i = k + 1 - k0;
@@ -253,9 +250,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
         int rr = 0;
         while (rr + 1 < nr && s_pre[rr + 1] <= k) ++rr;
         const uint32_t q = s_bnd[rr][0] + (k - s_pre[rr]);
-        rec = ld16(g.cell_rec + q);
+        rec = ld16(g.cell_rec + 3 * (size_t)q);
+        const uint4 p01 = ld16(g.cell_rec + 3 * (size_t)q + 1), p23 = ld16(g.cell_rec + 3 * (size_t)q + 2);
         int64_t sr, sc;
-        ok = project_edge(g, rec, mode_bit, plat, plon, mpl, r2, &sr, &sc, &d2, &frac, &tests);
+        ok = project_edge(g, rec, p01, p23, mode_bit, plat, plon, mpl, r2, &sr, &sc, &d2, &frac, &tests);
         // owned by the cell holding the snapped point: entry q lies in that cell's range
         if (ok) {
           const int64_t wr = sr - r0, wc = sc - c0;
@@ -278,9 +276,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
           double d2 = 0, frac = 0;
           uint4 rec = make_uint4(0u, 0u, 0u, 0u);
           if (q < end) {
-            rec = ld16(g.cell_rec + q);
+            rec = ld16(g.cell_rec + 3 * (size_t)q);
+            const uint4 p01 = ld16(g.cell_rec + 3 * (size_t)q + 1), p23 = ld16(g.cell_rec + 3 * (size_t)q + 2);
             int64_t sr, sc;
-            ok = project_edge(g, rec, mode_bit, plat, plon, mpl, r2, &sr, &sc, &d2, &frac, &tests) && sr == r &&
+            ok = project_edge(g, rec, p01, p23, mode_bit, plat, plon, mpl, r2, &sr, &sc, &d2, &frac, &tests) &&
+                 sr == r &&
                  sc == c;
           }
           merge(ok, d2, frac, rec.x);
