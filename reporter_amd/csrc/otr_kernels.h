@@ -1094,6 +1094,15 @@ struct ViterbiArgs {
   int32_t* subpath;
 };
 
+// x / 1000.0 for integral x in [0, 2^32), correctly rounded without a division: product
+// with RN(1/1000), exact residual by fma, one fma correction.  Equal to the IEEE quotient
+// for every such x (exhaustive check: tests/div1000_check.c, tests/test_div1000.py).
+__device__ inline double div1000(double x) {
+  const double q0 = x * 0.001;
+  const double e = __builtin_fma(-q0, 1000.0, x);
+  return __builtin_fma(e, 0.001, q0);
+}
+
 __device__ inline void argmin_lane(double c, int j, double* oc, int* oj) {
   for (int off = 32; off > 0; off >>= 1) {
     const double c2 = __shfl_xor(c, off);
@@ -1152,7 +1161,7 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
               if (tv[u] == kNoRoute) continue;
-              const double ti = fabs((double)tv[u] / 1000.0 - gcd) * inv_beta;
+              const double ti = fabs(div1000((double)tv[u]) - gcd) * inv_beta;
               const double ci = s_cost[i0 + u];
               if (ci == __builtin_huge_val()) continue;
               const double c = ci + ti;
