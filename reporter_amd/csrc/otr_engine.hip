@@ -344,7 +344,7 @@ static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + b
 static std::vector<int> route_tiers() {
   std::vector<int> t;
   const char* env = getenv("OTR_TIERS");
-  std::string spec = env ? env : "256,512x2,1024,2048";
+  std::string spec = env ? env : "256,448x2,1024,2048";
   size_t i = 0;
   while (i < spec.size()) {
     size_t j = spec.find(',', i);
@@ -353,7 +353,7 @@ static std::vector<int> route_tiers() {
     const int cap = atoi(item.c_str());
     const int gw = item.find('x') != std::string::npos ? atoi(item.c_str() + item.find('x') + 1) : 1;
     const int code = cap * 10 + gw;
-    if (code == 2561 || code == 5121 || code == 10241 || code == 20481 || code == 3842 || code == 5122) t.push_back(code);
+    if (code == 2561 || code == 5121 || code == 10241 || code == 20481 || code == 3842 || code == 4482 || code == 5122) t.push_back(code);
     i = j + 1;
   }
   t.push_back(40961);
@@ -607,6 +607,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
         case 10241: k_route<1024, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
         case 20481: k_route<2048, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
         case 3842: k_route<384, 2><<<(unsigned)((novf + 1) / 2), 64, 0, stream>>>(g, rb, rc); break;
+        case 4482: k_route<448, 2><<<(unsigned)((novf + 1) / 2), 64, 0, stream>>>(g, rb, rc); break;
         case 5122: k_route<512, 2><<<(unsigned)((novf + 1) / 2), 64, 0, stream>>>(g, rb, rc); break;
         default: k_route<4096, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
       }

@@ -1,7 +1,7 @@
 """Retry tiers give the first tier's results: a test build of the library
 (libotr_tiercheck.so, -DOTR_FORCE_RETRY) sends EVERY first-tier search down the
 retry kernels, and must still match the oracle field by field.  Parametrised over
-the retry-tier list (OTR_TIERS): the default 256 → 512x2 → 1024 → 2048 → 4096 chain, a chain
+the retry-tier list (OTR_TIERS): the default 256 → 448x2 → 1024 → 2048 → 4096 chain, a chain
 that starts with two-searches-per-wave 384-slot tables, and direct 1024/4096; with
 OTR_DIRECT_BMM=0 every search skips the first tier on its own.
 Runs in a child process (one library per process)."""
@@ -41,7 +41,7 @@ print('tiers ok')
 '''
 
 
-@pytest.mark.parametrize('tiers,direct', [(None, None), ('384x2,512', None), ('1024', '0')])
+@pytest.mark.parametrize('tiers,direct', [(None, None), ('384x2,512', None), ('512x2,2048', None), ('1024', '0')])
 def test_retry_tiers_equal_first_tier(graph_dir, tiers, direct):
     lib = os.path.join(ROOT, 'reporter_amd', 'libotr_tiercheck.so')
     assert os.path.exists(lib), 'build first: python -m reporter_amd.build'
