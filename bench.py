@@ -31,7 +31,7 @@ PEAK_HBM_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 ROUTE_KERNEL = 'k_route<160, 2>'  # first-tier search kernel (rocprofv3 name)
 # HBM bytes per ROUTE_KERNEL launch from the FETCH_SIZE / WRITE_SIZE passes of
 # tools/profile_gpu.sh (separate --pmc runs of this same command; tools/pmc_summary.py)
-PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r01_v28_pmc.json')
+PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r01_v31_pmc.json')
 T_BEGIN = 1483228800
 
 
