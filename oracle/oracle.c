@@ -30,7 +30,24 @@ struct orc_graph {
   const float* edge_len;
   const uint64_t* seg_id;
   uint32_t* len_mm; /* routing length, whole millimetres */
+  int16_t *h_begin, *h_end; /* headings of the first / last shape segment, degrees (§3.5) */
 };
+
+static double cos_deg(double deg);
+
+/* heading (integer degrees clockwise from north, 0..359) of the shape segment a → b in
+ * the local equirectangular metric; -1 for a zero-length segment */
+static int seg_heading(const int32_t* a, const int32_t* b) {
+  const double la1 = (double)a[0] * 1e-6, lo1 = (double)a[1] * 1e-6;
+  const double la2 = (double)b[0] * 1e-6, lo2 = (double)b[1] * 1e-6;
+  const double m = 20037581.187 / 180.0; /* metres per degree, Batch.java:36 */
+  const double x = (lo2 - lo1) * m * cos_deg(0.5 * (la1 + la2));
+  const double y = (la2 - la1) * m;
+  if (x == 0.0 && y == 0.0) return -1;
+  double deg = atan2(x, y) * (180.0 / 3.14159265358979323846);
+  if (deg < 0.0) deg = deg + 360.0;
+  return (int)(llround(deg) % 360);
+}
 
 orc_graph* orc_graph_load(const char* path) {
   FILE* f = fopen(path, "rb");
@@ -76,12 +93,24 @@ orc_graph* orc_graph_load(const char* path) {
     const long long mm = llround((double)g->edge_len[e] * 1000.0);
     g->len_mm[e] = (uint32_t)(mm < 1 ? 1 : mm);
   }
+  g->h_begin = (int16_t*)malloc(sizeof(int16_t) * ((size_t)g->h.n_edges + 1));
+  g->h_end = (int16_t*)malloc(sizeof(int16_t) * ((size_t)g->h.n_edges + 1));
+  for (uint32_t e = 0; e < g->h.n_edges; ++e) {
+    const uint32_t k0 = g->edge_shape[e], k1 = g->edge_shape[e + 1];
+    int hb = -1, he = -1;
+    for (uint32_t k = k0; k + 1 < k1 && hb < 0; ++k) hb = seg_heading(g->shape_ll + 2 * k, g->shape_ll + 2 * k + 2);
+    for (uint32_t k = k1 - 1; k > k0 && he < 0; --k) he = seg_heading(g->shape_ll + 2 * k - 2, g->shape_ll + 2 * k);
+    g->h_begin[e] = (int16_t)(hb < 0 ? 0 : hb);
+    g->h_end[e] = (int16_t)(he < 0 ? 0 : he);
+  }
   return g;
 }
 
 void orc_graph_free(orc_graph* g) {
   if (!g) return;
   free(g->len_mm);
+  free(g->h_begin);
+  free(g->h_end);
   free(g->blob);
   free(g);
 }
@@ -214,12 +243,28 @@ static int find_candidates(const orc_graph* g, double plat, double plon, double 
 }
 
 /* ---------------------------------------------------------------------------- */
-/* bounded one-to-many Dijkstra (UPSTREAM meili routing.cc)        */
+/* bounded one-to-many routing (UPSTREAM meili routing.cc)     */
 /* ---------------------------------------------------------------------------- */
-#define NO_LABEL INT64_MAX
+/* Route labels are lexicographic keys (d, t, c): d = length in whole mm, t = route time
+ * in 0.1 s (only while the step's time bound is active, else 0; saturating at
+ * ORC_TCAP), c = accumulated turn cost in mm (only when the mode's turn_penalty_factor
+ * is > 0, else 0; saturating at ORC_TCCAP).  Every component is an exact integer, so
+ * the labels are the unique lexicographic shortest-path values whatever the order of
+ * processing (the GPU's label-correcting search reaches the same fixed point). */
 typedef struct {
-  uint32_t* key;  /* node id, UINT32_MAX empty */
-  int64_t* dist;  /* label, millimetres */
+  int64_t d, t, c;
+} rkey;
+
+static int rk_lt(rkey a, rkey b) {
+  if (a.d != b.d) return a.d < b.d;
+  if (a.t != b.t) return a.t < b.t;
+  return a.c < b.c;
+}
+static int rk_eq(rkey a, rkey b) { return a.d == b.d && a.t == b.t && a.c == b.c; }
+
+typedef struct {
+  uint32_t* key;  /* node or edge id, UINT32_MAX empty */
+  rkey* lab;
   uint8_t* done;
   uint32_t cap, n;
 } nodemap_t;
@@ -237,13 +282,13 @@ static void nm_init(nodemap_t* m, uint32_t cap) {
   m->cap = cap;
   m->n = 0;
   m->key = (uint32_t*)malloc(cap * sizeof(uint32_t));
-  m->dist = (int64_t*)malloc(cap * sizeof(int64_t));
+  m->lab = (rkey*)malloc(cap * sizeof(rkey));
   m->done = (uint8_t*)malloc(cap);
   memset(m->key, 0xFF, cap * sizeof(uint32_t));
 }
 static void nm_free(nodemap_t* m) {
   free(m->key);
-  free(m->dist);
+  free(m->lab);
   free(m->done);
 }
 static uint32_t nm_find(const nodemap_t* m, uint32_t k) {
@@ -266,7 +311,9 @@ static uint32_t nm_insert(nodemap_t* m, uint32_t k, int* isnew) {
     s = (s + 1) & (m->cap - 1);
   }
   m->key[s] = k;
-  m->dist[s] = NO_LABEL;
+  m->lab[s].d = INT64_MAX;
+  m->lab[s].t = 0;
+  m->lab[s].c = 0;
   m->done[s] = 0;
   m->n++;
   *isnew = 1;
@@ -279,23 +326,24 @@ static void nm_grow(nodemap_t* m) {
     if (o.key[i] != 0xFFFFFFFFu) {
       int nw;
       uint32_t s = nm_insert(m, o.key[i], &nw);
-      m->dist[s] = o.dist[i];
+      m->lab[s] = o.lab[i];
       m->done[s] = o.done[i];
     }
   nm_free(&o);
 }
 
 typedef struct {
-  int64_t d;
-  uint32_t node;
+  rkey k;
+  uint32_t id;
 } heap_item;
 typedef VEC(heap_item) heap_t;
+static int hi_lt(const heap_item* a, const heap_item* b) { return rk_lt(a->k, b->k); }
 static void hpush(heap_t* h, heap_item x) {
   VPUSH(*h, x);
   size_t i = h->n - 1;
   while (i > 0) {
     size_t p = (i - 1) / 2;
-    if (h->d[p].d <= h->d[i].d) break;
+    if (!hi_lt(&h->d[i], &h->d[p])) break;
     heap_item t = h->d[p];
     h->d[p] = h->d[i];
     h->d[i] = t;
@@ -308,8 +356,8 @@ static heap_item hpop(heap_t* h) {
   size_t i = 0;
   for (;;) {
     size_t l = 2 * i + 1, r = l + 1, m = i;
-    if (l < h->n && h->d[l].d < h->d[m].d) m = l;
-    if (r < h->n && h->d[r].d < h->d[m].d) m = r;
+    if (l < h->n && hi_lt(&h->d[l], &h->d[m])) m = l;
+    if (r < h->n && hi_lt(&h->d[r], &h->d[m])) m = r;
     if (m == i) break;
     heap_item t = h->d[m];
     h->d[m] = h->d[i];
@@ -319,33 +367,117 @@ static heap_item hpop(heap_t* h) {
   return top;
 }
 
-/* Labels every node reachable from `start` (label 0) with its shortest-path length in
- * whole millimetres (integer, so exact and order-independent), keeping only labels
- * <= bound_mm. */
-static void dijkstra(const orc_graph* g, uint32_t start, int64_t bound_mm, uint32_t mode_bit, nodemap_t* m) {
+/* metres → whole millimetres of the routing bound and the partial edge lengths; the
+ * same for route times (0.1 s) of partial edges */
+static int64_t bound_mm_of(double bound) { return (int64_t)floor(bound * 1000.0); }
+static int64_t part_mm(double frac, uint32_t len_mm) { return (int64_t)llround(frac * (double)len_mm); }
+
+/* per-mode routing data */
+typedef struct {
+  uint32_t* time_ds; /* [E] route time of each edge at the mode's speed, 0.1 s */
+  int32_t turn[181]; /* turn cost by turn degree (0 = U-turn, 180 = straight), mm */
+  int turn_on;
+  uint32_t mode_bit;
+} mode_data;
+
+/* e^(-1/45) by its Taylor series; the turn table multiplies it up (deterministic, no libm) */
+void orc_turn_table(const orc_params* p, int32_t* tab) {
+  const double x = -1.0 / 45.0;
+  double r = 1.0, term = 1.0;
+  for (int k = 1; k <= 20; ++k) {
+    term = term * x / (double)k;
+    r = r + term;
+  }
+  double f = 1.0;
+  for (int i = 0; i <= 180; ++i) {
+    const double v = 1000.0 * p->turn_penalty_factor * f; /* turn_penalty_factor * exp(-i/45) m */
+    tab[i] = p->turn_penalty_factor > 0.0 ? (int32_t)llround(v) : 0;
+    f = f * r;
+  }
+}
+
+/* route time of one edge at the mode's speed: 0.1 s units, len_mm * 0.036 / kph */
+static uint32_t edge_time_ds(const orc_graph* g, const orc_params* p, uint32_t e) {
+  double kph = (double)OTR_ATTR_SPEED(g->edge_attr[e]);
+  if (!(kph > 0.0)) kph = 30.0; /* unknown speed */
+  if (p->speed_kph > 0.0 && p->speed_kph < kph) kph = p->speed_kph;
+  const double v = (double)g->len_mm[e] * 0.036 / kph;
+  return v < 2.0e9 ? (uint32_t)llround(v) : 2000000000u;
+}
+
+static void mode_data_init(const orc_graph* g, const orc_params* p, int mode, mode_data* md) {
+  md->time_ds = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)g->h.n_edges + 1));
+  for (uint32_t e = 0; e < g->h.n_edges; ++e) md->time_ds[e] = edge_time_ds(g, p, e);
+  orc_turn_table(p, md->turn);
+  md->turn_on = p->turn_penalty_factor > 0.0;
+  md->mode_bit = 1u << mode;
+}
+
+/* turn degree at a node from in-edge a to out-edge b: the angle between the heading
+ * back along a and the heading out along b, folded to 0..180 (0 = U-turn) */
+static int turn_degree(const orc_graph* g, uint32_t a, uint32_t b) {
+  const int back = (g->h_end[a] + 180) % 360;
+  const int td = (g->h_begin[b] - back + 360) % 360;
+  return td <= 180 ? td : 360 - td;
+}
+
+/* One step's routing context */
+typedef struct {
+  const orc_graph* g;
+  const mode_data* md;
+  int time_on;      /* the step's time bound is active: t components are tracked */
+  int64_t bt;       /* the time bound, 0.1 s */
+  int64_t bmm;      /* the distance bound, mm */
+} rctx;
+
+static rkey step_key(const rctx* X, rkey L, uint32_t e, int turn_from /* in-edge or -1 */) {
+  rkey k;
+  k.d = L.d + (int64_t)X->g->len_mm[e];
+  k.t = 0;
+  if (X->time_on) {
+    k.t = L.t + (int64_t)X->md->time_ds[e];
+    if (k.t > ORC_TCAP) k.t = ORC_TCAP;
+  }
+  k.c = 0;
+  if (X->md->turn_on && turn_from >= 0) {
+    k.c = L.c + X->md->turn[turn_degree(X->g, (uint32_t)turn_from, e)];
+    if (k.c > ORC_TCCAP) k.c = ORC_TCCAP;
+  }
+  return k;
+}
+
+/* Label-setting search (binary heap) over lexicographic keys, labels with d <= bmm.
+ * Node mode (turn costs off): states are nodes, rooted at node `root` with label 0.
+ * Edge mode (turn costs on): states are edges (arrived at dst(e) through e), rooted at
+ * edge `root` with label 0; moving from a to b adds turn(a, b). */
+static void search(const rctx* X, uint32_t root, nodemap_t* m) {
+  const orc_graph* g = X->g;
+  const int edge_mode = X->md->turn_on;
   m->n = 0;
   memset(m->key, 0xFF, m->cap * sizeof(uint32_t));
   heap_t hp = {0};
   int nw;
-  uint32_t s = nm_insert(m, start, &nw);
-  m->dist[s] = 0;
-  heap_item it0 = {0, start};
+  uint32_t s = nm_insert(m, root, &nw);
+  const rkey zero = {0, 0, 0};
+  m->lab[s] = zero;
+  heap_item it0 = {zero, root};
   hpush(&hp, it0);
   while (hp.n) {
     heap_item it = hpop(&hp);
-    uint32_t su = nm_find(m, it.node);
-    if (m->done[su] || it.d > m->dist[su]) continue;
+    uint32_t su = nm_find(m, it.id);
+    if (m->done[su] || !rk_eq(it.k, m->lab[su])) continue;
     m->done[su] = 1;
-    int64_t du = m->dist[su];
-    uint32_t u = it.node;
+    const rkey L = m->lab[su];
+    const uint32_t u = edge_mode ? g->edge_dst[it.id] : it.id;
     for (uint32_t e = g->node_row[u]; e < g->node_row[u + 1]; ++e) {
-      if (!(g->edge_attr[e] & mode_bit)) continue;
-      int64_t nd = du + (int64_t)g->len_mm[e];
-      if (nd > bound_mm) continue;
-      uint32_t sv = nm_insert(m, g->edge_dst[e], &nw);
-      if (nd < m->dist[sv]) {
-        m->dist[sv] = nd;
-        heap_item x = {nd, g->edge_dst[e]};
+      if (!(g->edge_attr[e] & X->md->mode_bit)) continue;
+      const rkey k = step_key(X, L, e, edge_mode ? (int)it.id : -1);
+      if (k.d > X->bmm) continue;
+      const uint32_t id = edge_mode ? e : g->edge_dst[e];
+      uint32_t sv = nm_insert(m, id, &nw);
+      if (rk_lt(k, m->lab[sv])) {
+        m->lab[sv] = k;
+        heap_item x = {k, id};
         hpush(&hp, x);
       }
     }
@@ -353,36 +485,196 @@ static void dijkstra(const orc_graph* g, uint32_t start, int64_t bound_mm, uint3
   free(hp.d);
 }
 
-/* metres → whole millimetres of the routing bound and the partial edge lengths */
-static int64_t bound_mm_of(double bound) { return (int64_t)floor(bound * 1000.0); }
-static int64_t part_mm(double frac, uint32_t len_mm) { return (int64_t)llround(frac * (double)len_mm); }
-
-/* route length in mm from candidate (ei,pi) to (ej,pj) given labels rooted at dst(ei):
- * same edge forward: round((pj-pi)*len); else round((1-pi)*len_i) + label(src(ej)) +
- * round(pj*len_j).  INT64_MAX when src(ej) was not reached. */
-static int64_t route_from_labels(const orc_graph* g, const nodemap_t* m, uint32_t ei, double pi, uint32_t ej,
-                                 double pj) {
-  if (ej == ei && pj >= pi) return part_mm(pj - pi, g->len_mm[ei]);
-  uint32_t s = nm_find(m, g->edge_src[ej]);
-  if (s == 0xFFFFFFFFu) return NO_LABEL;
-  return part_mm(1.0 - pi, g->len_mm[ei]) + m->dist[s] + part_mm(pj, g->len_mm[ej]);
+/* Best label at the start node v = src(ej) of a target edge, with the turn into ej:
+ * node mode: v's own label; edge mode: the lexicographic minimum over the labelled
+ * in-edges a of v (and the root edge when it ends at v) of (d, t, c + turn(a, ej)),
+ * smallest edge id among equals (*via).  Returns 0 when v was not reached. */
+static int target_key(const rctx* X, const nodemap_t* m, uint32_t root, uint32_t ej, rkey* out, uint32_t* via) {
+  const orc_graph* g = X->g;
+  const uint32_t v = g->edge_src[ej];
+  if (!X->md->turn_on) {
+    if (v == root) {
+      const rkey z = {0, 0, 0};
+      *out = z;
+      return 1;
+    }
+    uint32_t s = nm_find(m, v);
+    if (s == 0xFFFFFFFFu) return 0;
+    *out = m->lab[s];
+    return 1;
+  }
+  int found = 0;
+  rkey best = {0, 0, 0};
+  uint32_t bid = 0xFFFFFFFFu;
+  for (uint32_t r = g->rev_row[v]; r < g->rev_row[v + 1]; ++r) {
+    const uint32_t a = g->rev_edge[r];
+    const uint32_t s = nm_find(m, a);
+    if (s == 0xFFFFFFFFu) continue;
+    rkey k = m->lab[s];
+    k.c = k.c + X->md->turn[turn_degree(g, a, ej)];
+    if (k.c > ORC_TCCAP) k.c = ORC_TCCAP;
+    if (!found || rk_lt(k, best) || (rk_eq(k, best) && a < bid)) {
+      best = k;
+      bid = a;
+      found = 1;
+    }
+  }
+  if (found) {
+    *out = best;
+    *via = bid;
+  }
+  return found;
 }
 
-int orc_route_dist(const orc_graph* g, uint32_t src_edge, double src_p, uint32_t dst_edge, double dst_p,
-                   double bound, uint32_t mode_bit, double* out_dist) {
+/* route of a transition: same edge forward: the part between the two
+ * fractions; else exit part + label + entry part.  Returns 1 when valid (within the
+ * distance bound and, when active, the time bound). */
+static int route_of(const rctx* X, const nodemap_t* m, uint32_t root, uint32_t ei, double pi, uint32_t ej, double pj,
+                    rkey* out) {
+  const orc_graph* g = X->g;
+  rkey r;
+  if (ej == ei && pj >= pi) {
+    r.d = part_mm(pj - pi, g->len_mm[ei]);
+    r.t = X->time_on ? part_mm(pj - pi, X->md->time_ds[ei]) : 0;
+    r.c = 0;
+  } else {
+    rkey L;
+    uint32_t via;
+    if (!target_key(X, m, root, ej, &L, &via)) return 0;
+    r.d = part_mm(1.0 - pi, g->len_mm[ei]) + L.d + part_mm(pj, g->len_mm[ej]);
+    r.t = X->time_on ? part_mm(1.0 - pi, X->md->time_ds[ei]) + L.t + part_mm(pj, X->md->time_ds[ej]) : 0;
+    r.c = L.c;
+  }
+  *out = r;
+  return r.d <= X->bmm && (!X->time_on || r.t <= X->bt);
+}
+
+/* the step's routing context: distance bound from the great-circle distance, time
+ * bound max_route_time_factor * (time difference), 0.1 s */
+static void step_ctx(rctx* X, const orc_graph* g, const mode_data* md, const orc_params* P, double gcd,
+                     int64_t dt) {
+  X->g = g;
+  X->md = md;
+  const double gfl = gcd > P->interpolation_distance ? gcd : P->interpolation_distance;
+  double bound = P->max_route_distance_factor * gfl;
+  if (bound > P->breakage_distance) bound = P->breakage_distance;
+  X->bmm = bound_mm_of(bound);
+  X->time_on = 0;
+  X->bt = 0;
+  if (P->max_route_time_factor > 0.0 && dt > 0) {
+    const double b = floor(P->max_route_time_factor * (double)dt * 10.0);
+    if (b <= (double)ORC_TB_MAX) {
+      X->time_on = 1;
+      X->bt = (int64_t)b;
+    }
+  }
+}
+
+/* the search root of a source candidate: its edge's end node, or the edge itself when
+ * turn costs make the search edge-based */
+static uint32_t root_of(const rctx* X, uint32_t ei) { return X->md->turn_on ? ei : X->g->edge_dst[ei]; }
+
+/* winner path: edges strictly between ei and ej, walking back from ej
+ * through the smallest-id in-edge (in-state) whose label plus the step is exactly the
+ * label reached.  Appends to *path in travel order. */
+typedef VEC(uint32_t) u32vec;
+static int walk_path(const rctx* X, const nodemap_t* m, uint32_t ei, uint32_t ej, u32vec* path) {
+  const orc_graph* g = X->g;
+  u32vec rev = {0};
+  int ok = 1;
+  if (!X->md->turn_on) {
+    const uint32_t S = g->edge_dst[ei];
+    uint32_t v = g->edge_src[ej];
+    while (v != S && rev.n <= g->h.n_nodes) {
+      const uint32_t sv = nm_find(m, v);
+      if (sv == 0xFFFFFFFFu) {
+        ok = 0;
+        break;
+      }
+      const rkey Lv = m->lab[sv];
+      uint32_t best_e = 0xFFFFFFFFu;
+      for (uint32_t r = g->rev_row[v]; r < g->rev_row[v + 1]; ++r) {
+        const uint32_t ed = g->rev_edge[r];
+        if (!(g->edge_attr[ed] & X->md->mode_bit)) continue;
+        const uint32_t u = g->edge_src[ed];
+        rkey Lu;
+        if (u == S) {
+          const rkey z = {0, 0, 0};
+          Lu = z;
+        } else {
+          const uint32_t su = nm_find(m, u);
+          if (su == 0xFFFFFFFFu) continue;
+          Lu = m->lab[su];
+        }
+        if (rk_eq(step_key(X, Lu, ed, -1), Lv) && ed < best_e) best_e = ed;
+      }
+      if (best_e == 0xFFFFFFFFu) {
+        ok = 0;
+        break;
+      }
+      VPUSH(rev, best_e);
+      v = g->edge_src[best_e];
+    }
+  } else {
+    rkey L;
+    uint32_t a;
+    if (!target_key(X, m, ei, ej, &L, &a)) ok = 0;
+    while (ok && a != ei && rev.n <= g->h.n_edges) {
+      VPUSH(rev, a);
+      const uint32_t sa = nm_find(m, a);
+      const rkey La = m->lab[sa];
+      const uint32_t v = g->edge_src[a];
+      uint32_t best = 0xFFFFFFFFu;
+      for (uint32_t r = g->rev_row[v]; r < g->rev_row[v + 1]; ++r) {
+        const uint32_t p = g->rev_edge[r];
+        const uint32_t sp = nm_find(m, p);
+        if (sp == 0xFFFFFFFFu) continue;
+        if (rk_eq(step_key(X, m->lab[sp], a, (int)p), La) && p < best) best = p;
+      }
+      if (best == 0xFFFFFFFFu) {
+        ok = 0;
+        break;
+      }
+      a = best;
+    }
+  }
+  for (size_t z = rev.n; ok && z-- > 0;) VPUSH(*path, rev.d[z]);
+  free(rev.d);
+  return ok;
+}
+
+int orc_edge_info(const orc_graph* g, const orc_params* p, uint32_t edge, int32_t* h_begin, int32_t* h_end,
+                  int64_t* time_ds) {
+  if (edge >= g->h.n_edges) return 0;
+  *h_begin = g->h_begin[edge];
+  *h_end = g->h_end[edge];
+  *time_ds = edge_time_ds(g, p, edge);
+  return 1;
+}
+
+int orc_route(const orc_graph* g, const orc_params* p, int mode, uint32_t src_edge, double src_p, uint32_t dst_edge,
+              double dst_p, double bound, int64_t dt_sec, double* out_dist, int64_t* out_time_ds,
+              int64_t* out_turn_mm) {
+  mode_data md;
+  mode_data_init(g, p, mode, &md);
+  rctx X;
+  /* bound given directly: a great-circle distance whose bound it is */
+  orc_params q = *p;
+  q.max_route_distance_factor = 1.0;
+  q.interpolation_distance = 0.0;
+  q.breakage_distance = bound;
+  step_ctx(&X, g, &md, &q, bound, dt_sec);
   nodemap_t m;
   nm_init(&m, 1024);
-  int64_t r = NO_LABEL;
-  const int64_t bmm = bound_mm_of(bound);
-  if (dst_edge == src_edge && dst_p >= src_p) {
-    r = part_mm(dst_p - src_p, g->len_mm[src_edge]);
-  } else {
-    dijkstra(g, g->edge_dst[src_edge], bmm, mode_bit, &m);
-    r = route_from_labels(g, &m, src_edge, src_p, dst_edge, dst_p);
-  }
+  if (!(dst_edge == src_edge && dst_p >= src_p)) search(&X, root_of(&X, src_edge), &m);
+  rkey r;
+  const int ok = route_of(&X, &m, root_of(&X, src_edge), src_edge, src_p, dst_edge, dst_p, &r);
   nm_free(&m);
-  *out_dist = r <= bmm ? (double)r / 1000.0 : INFINITY;
-  return 0;
+  free(md.time_ds);
+  *out_dist = ok ? (double)r.d / 1000.0 : INFINITY;
+  *out_time_ds = ok ? r.t : -1;
+  *out_turn_mm = ok ? r.c : -1;
+  return ok;
 }
 
 /* ---------------------------------------------------------------------------- */
@@ -486,7 +778,8 @@ typedef struct {
 
 typedef struct {
   const orc_graph* g;
-  const orc_params* p;
+  const orc_params* p;   /* ORC_MODES parameter sets */
+  const mode_data* md;   /* ORC_MODES routing data */
   const int64_t* trace_off;
   const double *lat, *lon;
   const int64_t* time;
@@ -508,15 +801,35 @@ static double time_at(const int64_t* pos, const double* tm, int n, int64_t s) {
   return tm[k];
 }
 
+/* queue_length (README.md:283,295: "the distance from the end of the segment where the
+ * speed drops below the threshold"): the state-to-state piece holding the
+ * segment's exit position s1 and the slow pieces right before it, clipped to [s0, s1];
+ * a piece is slow when its mean speed (route mm over the state times) is below
+ * queue_kph.  Whole metres, half up. */
+static int piece_slow(const int64_t* pos, const double* tm, int k, double kph) {
+  return (double)(pos[k + 1] - pos[k]) * 0.0036 < kph * (tm[k + 1] - tm[k]);
+}
+static int32_t queue_at(const int64_t* pos, const double* tm, int n, int64_t s0, int64_t s1, double kph) {
+  if (n < 2) return 0;
+  int k = 0;
+  while (k < n - 2 && s1 > pos[k + 1]) ++k;
+  if (!piece_slow(pos, tm, k, kph)) return 0;
+  while (k > 0 && pos[k] > s0 && piece_slow(pos, tm, k - 1, kph)) --k;
+  const int64_t q0 = pos[k] > s0 ? pos[k] : s0;
+  return (int32_t)((s1 - q0 + 500) / 1000);
+}
+
 static void match_trace(job_t* J, int32_t t) {
   const orc_graph* g = J->g;
-  const orc_params* P = J->p;
+  const int mode = J->mode[t] < ORC_MODES ? J->mode[t] : 0;
+  const orc_params* P = &J->p[mode];
+  const mode_data* MD = &J->md[mode];
   trace_out* O = &J->outs[t];
   memset(O, 0, sizeof(*O));
   const int64_t b = J->trace_off[t], n = J->trace_off[t + 1] - b;
   const double *lat = J->lat + b, *lon = J->lon + b;
   const int64_t* tm = J->time + b;
-  const uint32_t mode_bit = 1u << J->mode[t];
+  const uint32_t mode_bit = MD->mode_bit;
   const int kmax = P->max_candidates < ORC_KMAX ? P->max_candidates : ORC_KMAX;
   const double inv2s2 = 1.0 / (P->sigma_z * P->sigma_z * 2.0);
   const double inv_beta = 1.0 / P->beta;
@@ -577,33 +890,26 @@ static void match_trace(job_t* J, int32_t t) {
     const cand_t* cb = &O->cands.d[(size_t)sb * ORC_KMAX];
     double gcd = gc_dist(lat[ia], lon[ia], lat[ib], lon[ib]);
     int forced = gcd > P->breakage_distance;
-    double gfl = gcd > P->interpolation_distance ? gcd : P->interpolation_distance;
-    double bound = P->max_route_distance_factor * gfl;
-    if (bound > P->breakage_distance) bound = P->breakage_distance;
-    const int64_t bmm = bound_mm_of(bound);
-    uint32_t searched = 0xFFFFFFFFu; /* labels rooted at this node are in nm */
+    rctx X;
+    step_ctx(&X, g, MD, P, gcd, tm[ib] - tm[ia]);
+    uint32_t searched = 0xFFFFFFFFu; /* labels rooted here are in nm */
     for (int i = 0; i < Ka; ++i) {
       for (int j = 0; j < Kb; ++j) trans[i * ORC_KMAX + j] = INFINITY;
       if (forced) continue;
       int need = 0;
-      for (int j = 0; j < Kb; ++j) {
-        if (cb[j].e == ca[i].e && cb[j].p >= ca[i].p) {
-          int64_t r = part_mm(cb[j].p - ca[i].p, g->len_mm[ca[i].e]);
-          if (r <= bmm) trans[i * ORC_KMAX + j] = fabs((double)r / 1000.0 - gcd) * inv_beta;
-        } else {
-          need = 1;
-        }
-      }
-      if (!need) continue;
-      /* one search per root node: labels do not depend on the source edge */
-      if (g->edge_dst[ca[i].e] != searched) {
-        searched = g->edge_dst[ca[i].e];
-        dijkstra(g, searched, bmm, mode_bit, &nm);
+      for (int j = 0; j < Kb; ++j)
+        if (!(cb[j].e == ca[i].e && cb[j].p >= ca[i].p)) need = 1;
+      /* one search per root (node, or edge with turn costs): labels do not depend on
+       * the source's fraction along its edge */
+      const uint32_t root = root_of(&X, ca[i].e);
+      if (need && root != searched) {
+        searched = root;
+        search(&X, root, &nm);
       }
       for (int j = 0; j < Kb; ++j) {
-        if (cb[j].e == ca[i].e && cb[j].p >= ca[i].p) continue;
-        int64_t r = route_from_labels(g, &nm, ca[i].e, ca[i].p, cb[j].e, cb[j].p);
-        if (r <= bmm) trans[i * ORC_KMAX + j] = fabs((double)r / 1000.0 - gcd) * inv_beta;
+        rkey r;
+        if (route_of(&X, &nm, root, ca[i].e, ca[i].p, cb[j].e, cb[j].p, &r))
+          trans[i * ORC_KMAX + j] = ((double)r.c / 1000.0 + fabs((double)r.d / 1000.0 - gcd)) * inv_beta;
       }
     }
     int any = 0;
@@ -695,29 +1001,12 @@ static void match_trace(job_t* J, int32_t t) {
         /* path: re-run the bounded search from the winner and walk predecessors */
         int64_t ia = O->state_probe.d[act[q - 1]] - b, ib = O->state_probe.d[act[q]] - b;
         double gcd = gc_dist(lat[ia], lon[ia], lat[ib], lon[ib]);
-        double gfl = gcd > P->interpolation_distance ? gcd : P->interpolation_distance;
-        double bound = P->max_route_distance_factor * gfl;
-        if (bound > P->breakage_distance) bound = P->breakage_distance;
-        uint32_t S = g->edge_dst[ci->e], T = g->edge_src[cj->e];
-        dijkstra(g, S, bound_mm_of(bound), mode_bit, &nm);
-        VEC(uint32_t) path = {0};
-        uint32_t v = T;
-        while (v != S && path.n <= g->h.n_nodes) {
-          uint32_t sv = nm_find(&nm, v);
-          int64_t dv = nm.dist[sv];
-          uint32_t best_e = 0xFFFFFFFFu;
-          for (uint32_t r = g->rev_row[v]; r < g->rev_row[v + 1]; ++r) {
-            uint32_t ed = g->rev_edge[r];
-            if (!(g->edge_attr[ed] & mode_bit)) continue;
-            uint32_t su = nm_find(&nm, g->edge_src[ed]);
-            if (su == 0xFFFFFFFFu) continue;
-            if (nm.dist[su] + (int64_t)g->len_mm[ed] == dv && ed < best_e) best_e = ed;
-          }
-          if (best_e == 0xFFFFFFFFu) break; /* unreachable by construction */
-          VPUSH(path, best_e);
-          v = g->edge_src[best_e];
-        }
-        for (size_t z = path.n; z-- > 0;) {
+        rctx X;
+        step_ctx(&X, g, MD, P, gcd, tm[ib] - tm[ia]);
+        search(&X, root_of(&X, ci->e), &nm);
+        u32vec path = {0};
+        walk_path(&X, &nm, ci->e, cj->e, &path); /* the winner's route is valid by construction */
+        for (size_t z = 0; z < path.n; ++z) {
           uint32_t ed = path.d[z];
           portion_t pp = {ed, 0, s, s + (int64_t)g->len_mm[ed]};
           VPUSH(por, pp);
@@ -773,7 +1062,7 @@ static void match_trace(job_t* J, int32_t t) {
         VPUSH(O->seg_start, st);
         VPUSH(O->seg_end, et);
         VPUSH(O->seg_length, length);
-        VPUSH(O->seg_queue, 0);
+        VPUSH(O->seg_queue, et != -1.0 ? queue_at(pos, stm, nst, s0, s1, P->queue_kph) : 0);
         VPUSH(O->seg_internal, (uint8_t)(key == OTR_NO_SEGMENT && internal));
         int64_t nw = 0;
         uint32_t lastw = 0;
@@ -882,6 +1171,16 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, int32_t n_traces, c
   J.rl = report_levels_mask;
   J.tl = transition_levels_mask;
   J.n_traces = n_traces;
+  /* per-mode route times and turn tables (only for the modes present) */
+  mode_data md[ORC_MODES];
+  memset(md, 0, sizeof(md));
+  for (int m = 0; m < ORC_MODES; ++m) {
+    int used = 0;
+    for (int32_t t = 0; t < n_traces && !used; ++t) used = (mode[t] < ORC_MODES ? mode[t] : 0) == m;
+    if (used) mode_data_init(g, &p[m], m, &md[m]);
+    else md[m].mode_bit = 1u << m;
+  }
+  J.md = md;
   J.outs = (trace_out*)calloc((size_t)n_traces + 1, sizeof(trace_out));
   pthread_mutex_init(&J.mu, NULL);
   if (n_threads < 1) n_threads = 1;
@@ -890,6 +1189,7 @@ int orc_match_batch(const orc_graph* g, const orc_params* p, int32_t n_traces, c
   for (int i = 0; i < n_threads; ++i) pthread_join(th[i], NULL);
   free(th);
   pthread_mutex_destroy(&J.mu);
+  for (int m = 0; m < ORC_MODES; ++m) free(md[m].time_ds);
   trace_out* T = J.outs;
   out->n_traces = n_traces;
   out->trace_state_off = (int64_t*)malloc(sizeof(int64_t) * (n_traces + 1));

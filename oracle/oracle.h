@@ -31,20 +31,33 @@ extern "C" {
 #define ORC_INVALID_SEGMENT_ID 0x3fffffffffffull /* simple_reporter.py:43 */
 #define ORC_NO_ID 0xFFFFFFFFFFFFFFFFull
 
+/* Matching parameters of ONE travel mode (meili.default merged with meili.<mode>, then
+ * the request's match_options).  orc_match_batch takes an array of three: auto,
+ * bicycle, pedestrian (the trace's mode selects one). */
 typedef struct orc_params {
   double sigma_z;                    /* 4.07  Dockerfile:14 */
   double beta;                       /* 3     Dockerfile:15 */
   double max_route_distance_factor;  /* 5     Dockerfile:16 */
-  double max_route_time_factor;      /* 2     Dockerfile:17 (not applied) */
-  double breakage_distance;          /* 2000  generate_test_trace.py:48 */
+  double max_route_time_factor;      /* 2     Dockerfile:17,48 */
+  double breakage_distance;          /* 2000  generate_test_trace.py:48 (<= ORC_MAX_BREAKAGE) */
   double interpolation_distance;     /* 10 */
   double search_radius;              /* 50    generate_test_trace.py:51 */
   double max_search_radius;          /* 100 */
   double gps_accuracy;               /* 5 */
-  double turn_penalty_factor;        /* 0     generate_test_trace.py:47 */
+  double turn_penalty_factor;        /* per mode: auto 200, bicycle 140, pedestrian 100; requests
+                                        of generate_test_trace.py:47 send 0 */
+  double speed_kph;                  /* mode speed cap for route times, 0 = edge speed (auto);
+                                        bicycle 18, pedestrian 5.1 */
+  double queue_kph;                  /* queue_length speed threshold (README.md:283,295; §3.8) */
   int32_t max_candidates;            /* <= ORC_KMAX */
   int32_t threshold_sec;             /* 15    reporter_service.py:55 */
 } orc_params;
+
+#define ORC_MODES 3
+#define ORC_MAX_BREAKAGE 30000.0     /* metres: route labels pack d in 25 bits of mm */
+#define ORC_TCAP 131071              /* route-time labels saturate here (0.1 s, 17 bits) */
+#define ORC_TB_MAX 131070            /* time bounds above this are not applied */
+#define ORC_TCCAP 4194303            /* turn-cost labels saturate here (mm, 22 bits) */
 
 typedef struct orc_graph orc_graph;
 
@@ -98,7 +111,8 @@ typedef struct orc_result {
 } orc_result;
 
 /* lat/lon/time/accuracy are per probe, trace_off has n_traces+1 entries,
- * accuracy < 0 means "not given"; mode[t]: 0 auto, 1 bicycle, 2 pedestrian. */
+ * accuracy < 0 means "not given"; mode[t]: 0 auto, 1 bicycle, 2 pedestrian.
+ * p points to ORC_MODES parameter sets (one per mode). */
 int orc_match_batch(const orc_graph* g, const orc_params* p, int32_t n_traces, const int64_t* trace_off,
                     const double* lat, const double* lon, const int64_t* time, const float* accuracy,
                     const uint8_t* mode, uint32_t report_levels_mask, uint32_t transition_levels_mask,
@@ -121,9 +135,20 @@ int orc_report(int32_t n, const uint8_t* has_id, const uint64_t* seg_id, const d
                uint32_t report_levels_mask, uint32_t transition_levels_mask, uint64_t* rep_id, uint64_t* rep_next,
                double* rep_t0, double* rep_t1, int32_t* rep_length, int32_t* rep_queue, orc_report_out* out);
 
-/* per-trace routing query used by the transition-parity tests */
-int orc_route_dist(const orc_graph* g, uint32_t src_edge, double src_p, uint32_t dst_edge, double dst_p,
-                   double bound, uint32_t mode_bit, double* out_dist);
+/* One transition's route from candidate (src_edge, src_p) to (dst_edge, dst_p) under
+ * the mode's parameters p: distance bound `bound` metres, time
+ * bound from the probes' time difference dt_sec (<= 0: none).  Returns 1 and the route
+ * length (m), time (0.1 s) and turn cost (mm) when valid, 0 when no valid route. */
+int orc_route(const orc_graph* g, const orc_params* p, int mode, uint32_t src_edge, double src_p, uint32_t dst_edge,
+              double dst_p, double bound, int64_t dt_sec, double* out_dist, int64_t* out_time_ds,
+              int64_t* out_turn_mm);
+
+/* graph-derived per-edge data the routing semantics use (for tests): heading of the
+ * first / last shape segment (integer degrees clockwise from north), route time
+ * (0.1 s) under the mode's speed, and the mode's turn cost table (mm, 181 entries). */
+int orc_edge_info(const orc_graph* g, const orc_params* p, uint32_t edge, int32_t* h_begin, int32_t* h_end,
+                  int64_t* time_ds);
+void orc_turn_table(const orc_params* p, int32_t* table181);
 
 #ifdef __cplusplus
 }

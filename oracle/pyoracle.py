@@ -20,19 +20,39 @@ class Params(ctypes.Structure):
                 ('breakage_distance', ctypes.c_double), ('interpolation_distance', ctypes.c_double),
                 ('search_radius', ctypes.c_double), ('max_search_radius', ctypes.c_double),
                 ('gps_accuracy', ctypes.c_double), ('turn_penalty_factor', ctypes.c_double),
+                ('speed_kph', ctypes.c_double), ('queue_kph', ctypes.c_double),
                 ('max_candidates', ctypes.c_int32), ('threshold_sec', ctypes.c_int32)]
 
 
+MODES = ('auto', 'bicycle', 'pedestrian')
+# Restated valhalla_build_config meili section (UPSTREAM 2.3.x) with the
+# reference deployment's overrides (Dockerfile:14-17,42-49: sigma_z 4.07, beta 3,
+# max_route_distance_factor 5, max_route_time_factor 2), plus this build's per-mode route
+# speeds and queue thresholds.
 DEFAULTS = dict(sigma_z=4.07, beta=3.0, max_route_distance_factor=5.0, max_route_time_factor=2.0,
                 breakage_distance=2000.0, interpolation_distance=10.0, search_radius=50.0,
-                max_search_radius=100.0, gps_accuracy=5.0, turn_penalty_factor=0.0, max_candidates=32,
-                threshold_sec=15)
+                max_search_radius=100.0, gps_accuracy=5.0, turn_penalty_factor=0.0, speed_kph=0.0,
+                queue_kph=10.0, max_candidates=32, threshold_sec=15)
+MODE_DEFAULTS = {'auto': dict(turn_penalty_factor=200.0, search_radius=50.0),
+                 'bicycle': dict(turn_penalty_factor=140.0, speed_kph=18.0, queue_kph=5.0),
+                 'pedestrian': dict(turn_penalty_factor=100.0, search_radius=50.0, speed_kph=5.1, queue_kph=2.0)}
 
 
-def params(**kw):
-    d = dict(DEFAULTS)
-    d.update(kw)
-    return Params(**d)
+def params(modes=None, **kw):
+    """Per-mode parameter array (ORC_MODES): DEFAULTS, then MODE_DEFAULTS[mode], then
+    modes[mode] (config sections), then kw applied to every mode — as a request's
+    match_options override the configured values (reporter_amd.matcher.default_config
+    builds the same configuration for the engine)."""
+    arr = (Params * 3)()
+    for i, m in enumerate(MODES):
+        d = dict(DEFAULTS)
+        d.update(MODE_DEFAULTS[m])
+        d.update((modes or {}).get(m, {}))
+        d.update(kw)
+        d['max_candidates'] = int(d['max_candidates'])
+        d['threshold_sec'] = int(d['threshold_sec'])
+        arr[i] = Params(**{k: d[k] for k, _ in Params._fields_})
+    return arr
 
 
 class Result(ctypes.Structure):
@@ -85,8 +105,13 @@ def lib():
                                  ctypes.c_uint32, ctypes.c_uint32, P(ctypes.c_uint64), P(ctypes.c_uint64),
                                  P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_int32),
                                  P(ReportOut)]
-        L.orc_route_dist.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_double, ctypes.c_uint32,
-                                     ctypes.c_double, ctypes.c_double, ctypes.c_uint32, P(ctypes.c_double)]
+        L.orc_route.argtypes = [ctypes.c_void_p, P(Params), ctypes.c_int, ctypes.c_uint32, ctypes.c_double,
+                                ctypes.c_uint32, ctypes.c_double, ctypes.c_double, ctypes.c_int64,
+                                P(ctypes.c_double), P(ctypes.c_int64), P(ctypes.c_int64)]
+        L.orc_route.restype = ctypes.c_int
+        L.orc_edge_info.argtypes = [ctypes.c_void_p, P(Params), ctypes.c_uint32, P(ctypes.c_int32),
+                                    P(ctypes.c_int32), P(ctypes.c_int64)]
+        L.orc_turn_table.argtypes = [P(Params), P(ctypes.c_int32)]
         _L = L
     return _L
 
@@ -112,10 +137,26 @@ class Graph:
             lib().orc_graph_free(self.h)
             self.h = None
 
-    def route_dist(self, se, sp, de, dp, bound, mode_bit=1):
-        out = ctypes.c_double()
-        lib().orc_route_dist(self.h, se, sp, de, dp, bound, mode_bit, ctypes.byref(out))
-        return out.value
+    def route(self, se, sp, de, dp, bound, dt_sec=0, prm=None, mode=0):
+        """(length m, time 0.1 s, turn cost mm) of one transition's route, or None."""
+        prm = prm if prm is not None else params()
+        d, t, c = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+        ok = lib().orc_route(self.h, ctypes.byref(prm[mode]), mode, se, sp, de, dp, bound, int(dt_sec),
+                             ctypes.byref(d), ctypes.byref(t), ctypes.byref(c))
+        return (d.value, t.value, c.value) if ok else None
+
+    def edge_info(self, e, prm=None, mode=0):
+        """(begin heading, end heading, route time 0.1 s) of edge e."""
+        prm = prm if prm is not None else params()
+        hb, he, t = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        lib().orc_edge_info(self.h, ctypes.byref(prm[mode]), e, ctypes.byref(hb), ctypes.byref(he), ctypes.byref(t))
+        return hb.value, he.value, t.value
+
+
+def turn_table(prm, mode=0):
+    tab = (ctypes.c_int32 * 181)()
+    lib().orc_turn_table(ctypes.byref(prm[mode]), tab)
+    return list(tab)
 
 
 def levels_mask(levels):
@@ -131,7 +172,7 @@ def match_batch(graph, traces, prm=None, report_levels=(0, 1), transition_levels
     prm = prm or params()
     r = Result()
     acc = traces.accuracy
-    lib().orc_match_batch(graph.h, ctypes.byref(prm), traces.n_traces, _ptr(traces.offsets, ctypes.c_int64),
+    lib().orc_match_batch(graph.h, prm, traces.n_traces, _ptr(traces.offsets, ctypes.c_int64),
                           _ptr(traces.lat, ctypes.c_double), _ptr(traces.lon, ctypes.c_double),
                           _ptr(traces.time, ctypes.c_int64), _ptr(acc, ctypes.c_float),
                           _ptr(traces.mode, ctypes.c_uint8), levels_mask(report_levels),

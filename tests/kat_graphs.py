@@ -157,3 +157,39 @@ def build_short_lengths(path, seed=5, n=14, spacing=40.0):
                 way += 1
     write_graph(path, nodes, edges, segs)
     return path
+
+
+def build_slow(path):
+    """Time-bound graph: a two-way road T0..T5 at x = 0..500 m (y = 0),
+    50 km/h except the block T2-T3 (x = 200..300 m), which is 5 km/h both ways."""
+    nodes = [ll(100 * k, 0) for k in range(6)]
+    edges, ids = [], {}
+    for k in range(5):
+        sp = 5 if k == 2 else 50
+        ids['T%d>' % k], ids['T%d<' % k] = two_way(edges, k, k + 1, 50 + k, level=1, speed=sp)
+    segs = [dict(id=osmlr(1, 400, 1), edges=[ids['T%d>' % k] for k in range(5)])]
+    new = write_graph(path, nodes, edges, segs)
+    return {k: int(new[v]) for k, v in ids.items()}
+
+
+def slow_scenarios():
+    """Eastbound at 12.5 m/s, a probe every 4 s (50 m), 3 m north of the centreline."""
+    return {'through_slow_block': [(20 + 50 * k, 3) for k in range(10)]}
+
+
+def turn_scenarios():
+    """On the 'kat' graph: east along the main street, the last probe 48 m east of the side
+    street (x = 200, going north) and 50 m north of the main street: nearer the side street
+    (emission) but straight ahead costs one straight pass instead of a left turn."""
+    return {'straight_or_left': [(50, 0), (150, 0), (248, 50)],
+            # east to x = 290, turning at the node x = 300, back west to x = 60
+            'u_turn': [(30 + 20 * k, -3) for k in range(14)] + [(280 - 20 * k, -3) for k in range(12)]}
+
+
+def queue_scenario():
+    """East on the main street at 10 m/s (a probe every 2 s) to x = 190, then 1 m/s from
+    x = 201 to 319: states every 10 m in the slow part, so the slow pieces start at the
+    state at x = 201 and segment A1-A3 (x = 100..300) ends 99 m later."""
+    pts = [(30 + 20 * k, 3) for k in range(9)]        # x = 30..190, t = 0..16 s
+    pts += [(201 + 2 * m, 3) for m in range(60)]      # x = 201..319, t = 18..136 s
+    return pts

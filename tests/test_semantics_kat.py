@@ -1,0 +1,184 @@
+"""Hand-derived known answers for the route-time bound (max_route_time_factor), turn
+costs (turn_penalty_factor), U-turns and queue_length — the semantics of DESIGN.md
+§3.4-3.8 — on the CPU oracle, plus GPU parity on the same inputs (-m gpu).
+
+References: max_route_time_factor = 2 (Dockerfile:17,48); per-mode turn_penalty_factor
+(valhalla_build_config meili section); queue_length README.md:283,295."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+from oracle.compare import compare
+from tests import kat_graphs as K
+
+
+@pytest.fixture(scope='module')
+def kat(graph_dir):
+    path = os.path.join(graph_dir, 'kat.otrg')
+    ids, segidx, segs = K.build(path)
+    return path, ids, segs
+
+
+@pytest.fixture(scope='module')
+def slow(graph_dir):
+    path = os.path.join(graph_dir, 'kat_slow.otrg')
+    return path, K.build_slow(path)
+
+
+def _match(path, pts, dt, **kw):
+    b = K.batch([K.trace(pts, dt=dt)])
+    return b, po.match_batch(po.Graph(path), b, po.params(**kw))
+
+
+# ---- graph-derived data ---------------------------------------------------------------
+def test_turn_table_values():
+    tab = po.turn_table(po.params())  # auto: turn_penalty_factor 200
+    for td in (0, 45, 90, 135, 180):
+        want = 1000.0 * 200.0 * math.exp(-td / 45.0)
+        assert abs(tab[td] - want) <= 1.0, (td, tab[td], want)
+    assert tab[0] == 200000 and tab[90] == 27067 and tab[180] == 3663
+    assert po.turn_table(po.params(turn_penalty_factor=0)) == [0] * 181
+
+
+def test_headings_and_edge_times(kat, slow):
+    path, ids, _ = kat
+    g = po.Graph(path)
+    assert g.edge_info(ids['A0>'])[:2] == (90, 90)
+    assert g.edge_info(ids['A0<'])[:2] == (270, 270)
+    assert g.edge_info(ids['B0^'])[:2] == (0, 0)
+    assert g.edge_info(ids['B0v'])[:2] == (180, 180)
+    spath, sid = slow
+    gs = po.Graph(spath)
+    # 100 m at 50 km/h = 7.2 s; at 5 km/h = 72 s (0.1 s units)
+    assert gs.edge_info(sid['T0>'])[2] == 72
+    assert gs.edge_info(sid['T2>'])[2] == 720
+    # bicycle: capped at 18 km/h -> 20 s; pedestrian 5.1 km/h -> 70.6 s
+    assert gs.edge_info(sid['T0>'], mode=1)[2] == 200
+    assert gs.edge_info(sid['T0>'], mode=2)[2] == 706
+
+
+# ---- time bound ------------------------------------------------------------------------
+def test_route_time_bound_by_hand(slow):
+    path, sid = slow
+    g = po.Graph(path)
+    prm = po.params(turn_penalty_factor=0)
+    # T1> at 0.5 -> T3> at 0.5: 50 + 100 + 50 m; 3.6 s + 72 s + 3.6 s = 79.2 s
+    r = g.route(sid['T1>'], 0.5, sid['T3>'], 0.5, 1000.0, dt_sec=40, prm=prm)
+    assert r is not None and abs(r[0] - 200.0) < 0.1 and r[1] == 792  # lengths from micro-degree nodes
+    assert g.route(sid['T1>'], 0.5, sid['T3>'], 0.5, 1000.0, dt_sec=39, prm=prm) is None  # 780 < 792
+    assert g.route(sid['T1>'], 0.5, sid['T3>'], 0.5, 1000.0, dt_sec=0, prm=prm) is not None  # no bound
+    r = g.route(sid['T1>'], 0.5, sid['T3>'], 0.5, 1000.0, dt_sec=10,
+                prm=po.params(turn_penalty_factor=0, max_route_time_factor=0))
+    assert r is not None and r[1] == 0  # factor 0: no time bound (times not tracked)
+    # same edge forward: part of the edge's time
+    r = g.route(sid['T2>'], 0.25, sid['T2>'], 0.75, 1000.0, dt_sec=100, prm=prm)
+    assert r is not None and r[1] == 360
+    assert g.route(sid['T2>'], 0.25, sid['T2>'], 0.75, 1000.0, dt_sec=17, prm=prm) is None  # 340 < 360
+
+
+def test_slow_block_breaks_trace(slow):
+    """Probes 4 s apart cross a 5 km/h block at 12.5 m/s.  Crossing the block takes 72 s,
+    more than any step's bound (2 x 4 s), so no route may use it: the probes on the block
+    snap to its end nodes (within the 50 m radius) and the trace breaks exactly once
+    between them; the slow edge never appears in the route.  With
+    max_route_time_factor = 0 the trace is one sub-path through the block."""
+    path, sid = slow
+    pts = K.slow_scenarios()['through_slow_block']
+    b, r = _match(path, pts, 4, turn_penalty_factor=0)
+    assert r['subpath'].tolist() == [0, 0, 0, 0, 0, 1, 1, 1, 1, 1]
+    assert [int(e) for e in r['route_edge']] == [sid['T0>'], sid['T1>'], 0xFFFFFFFF, sid['T3>'], sid['T4>']]
+    b, r0 = _match(path, pts, 4, turn_penalty_factor=0, max_route_time_factor=0)
+    assert r0['subpath'].max() == 0
+    assert [int(e) for e in r0['route_edge']] == [sid['T%d>' % k] for k in range(5)]
+
+
+# ---- turn costs ------------------------------------------------------------------------
+def test_turn_penalty_prefers_straight(kat):
+    """Without turn costs the last probe matches the side street (nearer, left turn);
+    with the auto default (200) going straight on costs 3.7 m instead of 27.1 m and wins."""
+    path, ids, segs = kat
+    pts = K.turn_scenarios()['straight_or_left']
+    b, r0 = _match(path, pts, 10, turn_penalty_factor=0)
+    last = int(r0['trace_state_off'][1]) - 1
+    assert int(r0['cand_edge'][last][r0['winner'][last]]) == ids['B0^']
+    b, r = _match(path, pts, 10)
+    assert int(r['cand_edge'][last][r['winner'][last]]) == ids['A2>']
+    assert [int(e) for e in r['route_edge']][-2:] == [ids['A1>'], ids['A2>']]
+
+
+def test_turn_costs_in_route(kat):
+    """turn(A1>, A2>) is straight (180 degrees): 3663 mm at 200; a left turn A1> -> B0^ at
+    node A2 is 90 degrees: 27067 mm; a U-turn (0 degrees) 200000 mm."""
+    path, ids, _ = kat
+    g = po.Graph(path)
+    prm = po.params()
+    r = g.route(ids['A1>'], 0.5, ids['A2>'], 0.5, 1000.0, dt_sec=100, prm=prm)
+    assert r[2] == 3663
+    r = g.route(ids['A1>'], 0.5, ids['B0^'], 0.5, 1000.0, dt_sec=100, prm=prm)
+    assert r[2] == 27067
+    r = g.route(ids['A1>'], 0.5, ids['A1<'], 0.5, 1000.0, dt_sec=100, prm=prm)
+    assert abs(r[0] - 100.0) < 0.1 and r[2] == 200000  # U-turn at A2
+    # straight over two nodes: A0> -> A2> passes A1 and A2 (2 x straight)
+    r = g.route(ids['A0>'], 0.5, ids['A2>'], 0.5, 1000.0, dt_sec=100, prm=prm)
+    assert r[2] == 2 * 3663
+    assert g.route(ids['A1>'], 0.5, ids['B0^'], 0.5, 1000.0, dt_sec=100, prm=po.params(turn_penalty_factor=0))[2] == 0
+
+
+@pytest.mark.parametrize('tpf', [0, 200])
+def test_u_turn_route(kat, tpf):
+    """East to x = 290, then back west from x = 280 (2 s later: 30 m of route in 2.2 s at
+    50 km/h, inside the 4 s bound): the route U-turns at node A3 (x = 300)."""
+    path, ids, segs = kat
+    pts = K.turn_scenarios()['u_turn']
+    b, r = _match(path, pts, 2, turn_penalty_factor=tpf)
+    rt = [int(e) for e in r['route_edge']]
+    assert 0xFFFFFFFF not in rt
+    assert rt == [ids['A0>'], ids['A1>'], ids['A2>'], ids['A2<'], ids['A1<'], ids['A0<']]
+
+
+# ---- queue_length ----------------------------------------------------------------------
+def test_queue_length_on_deceleration(kat):
+    path, ids, segs = kat
+    b, r = _match(path, K.queue_scenario(), 2)
+    sid = [int(x) for x in r['seg_id']]
+    k = sid.index(segs[1]['id'])  # A1-A3, complete
+    assert r['seg_length'][k] == 200
+    assert r['seg_queue'][k] == 99
+    # the first segment (entered mid-edge, exit at x = 100 at 10 m/s) has no queue
+    assert r['seg_queue'][0] == 0
+    # report() carries it into datastore reports
+    rk = [int(x) for x in r['rep_id']].index(segs[1]['id'])
+    assert r['rep_queue'][rk] == 99
+    # a higher threshold (20 km/h) makes the piece x = 190 -> 201 (11 m in 2 s, 19.8 km/h)
+    # slow too, but not the one before it (20 m in 2 s, 36 km/h): 300 - 190 = 110 m
+    b, r2 = _match(path, K.queue_scenario(), 2, queue_kph=20.0)
+    assert r2['seg_queue'][k] == 110
+
+
+# ---- GPU parity on the same inputs -----------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize('opts', [{}, {'turn_penalty_factor': 0}, {'max_route_time_factor': 0}])
+def test_semantics_gpu_parity(kat, slow, opts):
+    from reporter_amd import matcher as M
+    path, ids, segs = kat
+    M.configure(M.default_config(path, **opts))
+    m = M.Matcher()
+    sc = dict(K.turn_scenarios())
+    sc['queue'] = K.queue_scenario()
+    trs = [K.trace(p, dt=2 if n != 'straight_or_left' else 10) for n, p in sc.items()]
+    trs += [K.trace(p) for p in K.scenarios().values()]
+    b = K.batch(trs)
+    got = m.match_batch_numpy(b)
+    want = po.match_batch(po.Graph(path), b, po.params(**opts))
+    errors, stats = compare(got, want)
+    assert not errors, errors
+    spath, sid = slow
+    M.configure(M.default_config(spath, **opts))
+    b = K.batch([K.trace(p, dt=4) for p in K.slow_scenarios().values()])
+    got = M.Matcher().match_batch_numpy(b)
+    want = po.match_batch(po.Graph(spath), b, po.params(**opts))
+    errors, stats = compare(got, want)
+    assert not errors, errors
