@@ -109,10 +109,16 @@ def main():
     # traces: all ranks generate the same global set, keep their uuid-hash shard
     n_global = args.traces_per_gpu * world
     t0 = time.time()
-    W = {'c2': dict(points=100, rate=15, sigma=10.0, seed=2, bike=0.0, ped=0.0, acc=None, meili={}),
+    # match_options as generate_test_trace.py:44-52 sends them (turn_penalty_factor 0,
+    # gps_accuracy = the 95th percentile of the noise); max_route_time_factor stays the
+    # deployed 2 (Dockerfile:17)
+    gtt = {'turn_penalty_factor': 0, 'beta': 3, 'sigma_z': 4.07, 'breakage_distance': 2000}
+    W = {'c2': dict(points=100, rate=15, sigma=10.0, seed=2, bike=0.0, ped=0.0, acc=None,
+                    meili=dict(gtt, search_radius=50, gps_accuracy=16.45)),
          'c4': dict(points=60, rate=60, sigma=50.0, seed=4, bike=0.0, ped=0.0, acc=50.0,
-                    meili={'search_radius': 200, 'max_search_radius': 200}),
-         'c5mix': dict(points=100, rate=15, sigma=10.0, seed=5, bike=0.25, ped=0.15, acc=None, meili={})}[args.workload]
+                    meili=dict(gtt, search_radius=200, max_search_radius=200, gps_accuracy=82.24)),
+         'c5mix': dict(points=100, rate=15, sigma=10.0, seed=5, bike=0.25, ped=0.15, acc=None,
+                       meili=dict(gtt, search_radius=50, gps_accuracy=16.45))}[args.workload]
     allt = gen.make_traces(gpath, n_global, W['points'], W['rate'], W['sigma'], W['seed'], W['bike'], W['ped'],
                            W['acc'], t_begin=T_BEGIN, t_spread=1800)
     if world > 1:

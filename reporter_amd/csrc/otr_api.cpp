@@ -56,6 +56,8 @@ void apply_options(otr::MatchParams* p, const Value* o) {
   num("search_radius", &p->search_radius);
   num("max_search_radius", &p->max_search_radius);
   num("gps_accuracy", &p->gps_accuracy);
+  num("max_route_time_factor", &p->max_route_time_factor);
+  num("turn_penalty_factor", &p->turn_penalty_factor);
   const Value* k = o->get("max_candidates");
   if (k && k->kind == Value::Number) p->kmax = (int32_t)k->as_int();
 }
@@ -78,6 +80,19 @@ int parse_config(const Value& root, otr::Config* cfg, std::string* err) {
     if (dv && dv->kind == Value::Number) cfg->device = (int)dv->as_int();
     const Value* dl = o->get("delta");
     if (dl && dl->kind == Value::Number) cfg->mp.delta = dl->as_double();
+    // per-mode route speeds and queue thresholds: a number for
+    // every mode or {"auto": .., "bicycle": .., "pedestrian": ..}
+    const char* names[OTR_MODES] = {"auto", "bicycle", "pedestrian"};
+    auto per_mode = [&](const char* key, double otr::MatchParams::*f) {
+      const Value* v = o->get(key);
+      if (!v) return;
+      for (int m = 0; m < OTR_MODES; ++m) {
+        const Value* x = v->kind == Value::Object ? v->get(names[m]) : v;
+        if (x && x->kind == Value::Number) cfg->mp.m[m].*f = x->as_double();
+      }
+    };
+    per_mode("speed_kph", &otr::MatchParams::speed_kph);
+    per_mode("queue_kph", &otr::MatchParams::queue_kph);
   }
   if (cfg->graph_path.empty()) {
     const Value* mj = root.get("mjolnir");

@@ -28,6 +28,10 @@ struct MatchParams {          // one per travel mode (meili.default + meili.<mod
   double search_radius;
   double max_search_radius;
   double gps_accuracy;
+  double max_route_time_factor;  // Dockerfile:17,48 (2): route time <= factor * dt
+  double turn_penalty_factor;    // per mode, valhalla_build_config: auto 200, bicycle 140, pedestrian 100
+  double speed_kph;           // mode speed cap for route times (0 = edge speed); fixed at configure
+  double queue_kph;           // queue_length speed threshold (README.md:283,295)
   double inv2s2;              // 1 / (sigma_z * sigma_z * 2)
   double inv_beta;            // 1 / beta
   int32_t kmax;               // max_candidates <= OTR_KMAX
@@ -38,6 +42,27 @@ struct ModeParams {
   MatchParams m[OTR_MODES];
   double delta;               // distance-bucket width of the routing search (metres)
 };
+
+// Route-label limits shared with the oracle (oracle/oracle.h ORC_*)
+constexpr double kMaxBreakage = 30000.0;  // metres: d fits 25 bits of mm in 64-bit labels
+constexpr uint32_t kTCap = 131071;        // route time saturates here (0.1 s, 17 bits)
+constexpr int64_t kTbMax = 131070;        // larger time bounds are not applied
+constexpr uint32_t kTcCap = 4194303;      // turn cost saturates here (mm, 22 bits)
+
+// the step's time bound in 0.1 s from the states' time difference, -1 = none (oracle step_ctx)
+__host__ __device__ inline int32_t time_bound_ds(const MatchParams& p, int64_t dt) {
+  if (!(p.max_route_time_factor > 0.0) || dt <= 0) return -1;
+  const double b = floor(p.max_route_time_factor * (double)dt * 10.0);
+  return b <= (double)kTbMax ? (int32_t)b : -1;
+}
+
+// turn degree from in-edge a (end heading ha) into out-edge b (begin heading hb): the
+// angle between the heading back along a and out along b, 0 (U-turn) .. 180 (straight)
+__host__ __device__ inline int turn_degree(int ha_end, int hb_begin) {
+  const int back = (ha_end + 180) % 360;
+  const int td = (hb_begin - back + 360) % 360;
+  return td <= 180 ? td : 360 - td;
+}
 
 struct DevGraph {
   const uint32_t* node_row;
@@ -60,8 +85,13 @@ struct DevGraph {
   const uint4* adj;            // 4 x uint4 per node: {dst | access<<28 | more<<31, len_mm, dst lat_e6, dst lon_e6}
   const uint32_t* len_mm;      // routing length, whole millimetres
   const int2* node_ll;         // (lat_e6, lon_e6)
+  const uint32_t* adj_t;       // [mode][4 per node like adj]: route time of the slot's edge, 0.1 s
+  const uint32_t* edge_t;      // [mode][edge]: route time, 0.1 s
+  uint32_t adj_t_stride, edge_t_stride;  // elements per mode
+  const short2* edge_head;     // per edge {begin heading, end heading}, integer degrees
   uint32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double grid_min_lat, grid_min_lon, grid_cell_deg;
+  __device__ const uint32_t* et(int mode) const { return edge_t + (size_t)mode * edge_t_stride; }
   float h_scale;               // min over edges of len_mm / straight-line mm (<= 1): keeps the A*
                                // heuristic consistent for graphs whose lengths undercut geometry
 };

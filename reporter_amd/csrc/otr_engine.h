@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -20,8 +21,11 @@ struct Config {
 
 ModeParams default_mode_params();
 void finalize_params(MatchParams* p);
+const char* check_params(const MatchParams& p);  // nullptr when the engine can honour p
 
-// The configured graph, resident in HBM (one replica per process/GPU).
+// The configured graph, resident in HBM (one replica per process/GPU).  A reconfigure
+// builds the new replica aside and swaps it in under the exclusive lock; batches hold
+// the shared lock for their whole run, so no kernel ever sees a freed array.
 struct GraphState {
   bool ready = false;
   int device = 0;
@@ -31,6 +35,7 @@ struct GraphState {
   uint64_t n_nodes = 0, n_edges = 0, n_segments = 0;
   // host copy of the few arrays the JSON path needs
   std::vector<unsigned long long> seg_id;
+  std::shared_mutex mu;
 };
 
 GraphState& graph_state();
@@ -41,9 +46,24 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
+// one tier of global-memory search slabs (otr_general.h), owned by a matcher
+struct GSlab {
+  uint32_t* key = nullptr;
+  unsigned long long* lab = nullptr;
+  uint32_t* qmark = nullptr;
+  uint32_t* fr = nullptr;
+  uint32_t* touched = nullptr;
+};
+
+// turn cost table (mm) of a turn_penalty_factor: factor * exp(-deg / 45) for deg 0..180
+// (oracle orc_turn_table: the same operations)
+void turn_table(double factor, int32_t* tab181);
+
 struct Matcher {
   hipStream_t stream = nullptr;
   std::vector<DevBuf> bufs;
+  GSlab gslab[2];
+  std::vector<int32_t> h_turn;
   // host result storage (OTR_BATCH_COPY_OUT)
   std::vector<int64_t> h_trace_state_off, h_state_probe, h_trace_route_off, h_trace_seg_off, h_seg_way_off,
       h_trace_rep_off;

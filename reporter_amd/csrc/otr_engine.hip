@@ -12,6 +12,7 @@
 
 #include "otr_engine.h"
 #include "otr_kernels.h"
+#include "otr_general.h"
 #include "otr_ingest.h"
 
 namespace otr {
@@ -30,9 +31,22 @@ void finalize_params(MatchParams* p) {
   p->inv_beta = 1.0 / p->beta;
   if (p->kmax > OTR_KMAX) p->kmax = OTR_KMAX;
   if (p->kmax < 1) p->kmax = 1;
-  // routing labels and A* keys are uint32 millimetres: routes are
-  // bounded by breakage_distance, which is therefore capped at 1000 km
-  if (!(p->breakage_distance <= 1.0e6)) p->breakage_distance = 1.0e6;
+}
+
+// values the engine cannot honour are refused by name (400), never silently changed
+const char* check_params(const MatchParams& p) {
+  if (!(p.breakage_distance >= 0.0 && p.breakage_distance <= kMaxBreakage))
+    return "breakage_distance must be within [0, 30000] m";
+  if (!(p.max_route_distance_factor >= 0.0) || !(p.max_route_distance_factor < 1e6))
+    return "max_route_distance_factor must be >= 0";
+  if (!(p.max_route_time_factor >= 0.0) || !(p.max_route_time_factor < 1e6)) return "max_route_time_factor must be >= 0";
+  if (!(p.turn_penalty_factor >= 0.0) || !(p.turn_penalty_factor <= 1e6)) return "turn_penalty_factor must be within [0, 1e6]";
+  if (!(p.sigma_z > 0.0)) return "sigma_z must be > 0";
+  if (!(p.beta > 0.0)) return "beta must be > 0";
+  if (!(p.search_radius >= 0.0) || !(p.max_search_radius >= 0.0)) return "search_radius must be >= 0";
+  if (!(p.interpolation_distance >= 0.0)) return "interpolation_distance must be >= 0";
+  if (!(p.speed_kph >= 0.0) || !(p.queue_kph >= 0.0)) return "speed_kph and queue_kph must be >= 0";
+  return nullptr;
 }
 
 ModeParams default_mode_params() {
@@ -42,16 +56,65 @@ ModeParams default_mode_params() {
     p.sigma_z = 4.07;                   // Dockerfile:14
     p.beta = 3.0;                       // Dockerfile:15
     p.max_route_distance_factor = 5.0;  // Dockerfile:16
+    p.max_route_time_factor = 2.0;      // Dockerfile:17,48 (MATCHER_TIME_FACTOR)
     p.breakage_distance = 2000.0;
     p.interpolation_distance = 10.0;
     p.search_radius = 50.0;
     p.max_search_radius = 100.0;
     p.gps_accuracy = 5.0;
     p.kmax = 32;
-    finalize_params(&p);
+    p.queue_kph = 10.0;
   }
+  // valhalla_build_config per-mode meili sections; mode speeds and queue
+  // thresholds of DESIGN.md §3.5/3.8
+  mp.m[0].turn_penalty_factor = 200.0;
+  mp.m[1].turn_penalty_factor = 140.0;
+  mp.m[1].speed_kph = 18.0;
+  mp.m[1].queue_kph = 5.0;
+  mp.m[2].turn_penalty_factor = 100.0;
+  mp.m[2].speed_kph = 5.1;
+  mp.m[2].queue_kph = 2.0;
+  for (int m = 0; m < OTR_MODES; ++m) finalize_params(&mp.m[m]);
   mp.delta = 60.0;  // round width (m): search order only; C2 39.3M -> 39.7M, C4 4.35M -> ~4.4M single stream vs 100
   return mp;
+}
+
+// route time of an edge at the mode's speed, 0.1 s (oracle edge_time_ds)
+static uint32_t edge_time_ds(uint32_t attr, uint32_t len_mm, double speed_cap) {
+  double kph = (double)OTR_ATTR_SPEED(attr);
+  if (!(kph > 0.0)) kph = 30.0;  // unknown speed
+  if (speed_cap > 0.0 && speed_cap < kph) kph = speed_cap;
+  const double v = (double)len_mm * 0.036 / kph;
+  return v < 2.0e9 ? (uint32_t)llround(v) : 2000000000u;
+}
+
+// heading of the shape segment a -> b, integer degrees clockwise from north, -1 when
+// degenerate (oracle seg_heading)
+static int seg_heading(const int32_t* a, const int32_t* b) {
+  const double la1 = (double)a[0] * 1e-6, lo1 = (double)a[1] * 1e-6;
+  const double la2 = (double)b[0] * 1e-6, lo2 = (double)b[1] * 1e-6;
+  const double m = 20037581.187 / 180.0;  // metres per degree, Batch.java:36
+  const double x = (lo2 - lo1) * m * cos_deg(0.5 * (la1 + la2));
+  const double y = (la2 - la1) * m;
+  if (x == 0.0 && y == 0.0) return -1;
+  double deg = atan2(x, y) * (180.0 / 3.14159265358979323846);
+  if (deg < 0.0) deg = deg + 360.0;
+  return (int)(llround(deg) % 360);
+}
+
+void turn_table(double factor, int32_t* tab) {
+  const double x = -1.0 / 45.0;  // e^(-1/45) by its Taylor series, then powers
+  double r = 1.0, term = 1.0;
+  for (int k = 1; k <= 20; ++k) {
+    term = term * x / (double)k;
+    r = r + term;
+  }
+  double f = 1.0;
+  for (int i = 0; i <= 180; ++i) {
+    const double v = 1000.0 * factor * f;
+    tab[i] = factor > 0.0 ? (int32_t)llround(v) : 0;
+    f = f * r;
+  }
 }
 
 GraphState& graph_state() {
@@ -59,8 +122,30 @@ GraphState& graph_state() {
   return gs;
 }
 
+namespace {
+struct Mapped {
+  void* p = MAP_FAILED;
+  size_t n = 0;
+  ~Mapped() {
+    if (p != MAP_FAILED) munmap(p, n);
+  }
+};
+struct Staged {  // a graph replica being built; freed unless adopted
+  std::vector<void*> allocs;
+  bool adopted = false;
+  ~Staged() {
+    if (!adopted)
+      for (void* q : allocs) (void)hipFree(q);
+  }
+};
+}  // namespace
+
 int engine_configure(const Config& cfg, std::string* err) {
-  GraphState& gs = graph_state();
+  for (int m = 0; m < OTR_MODES; ++m)
+    if (const char* bad = check_params(cfg.mp.m[m])) {
+      if (err) *err = std::string("config: ") + bad;
+      return OTR_BAD_REQUEST;
+    }
   int fd = open(cfg.graph_path.c_str(), O_RDONLY);
   if (fd < 0) {
     if (err) *err = "cannot open graph file " + cfg.graph_path + ": " + strerror(errno);
@@ -68,32 +153,139 @@ int engine_configure(const Config& cfg, std::string* err) {
   }
   struct stat st;
   fstat(fd, &st);
-  void* map = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+  Mapped mf;
+  mf.n = (size_t)st.st_size;
+  mf.p = mf.n >= sizeof(otr_graph_header) ? mmap(nullptr, mf.n, PROT_READ, MAP_PRIVATE, fd, 0) : MAP_FAILED;
   close(fd);
-  if (map == MAP_FAILED) {
-    if (err) *err = "cannot map graph file";
+  if (mf.p == MAP_FAILED) {
+    if (err) *err = "cannot map graph file " + cfg.graph_path;
     return OTR_BAD_REQUEST;
   }
-  const char* base = (const char*)map;
+  const char* base = (const char*)mf.p;
   otr_graph_header h;
   memcpy(&h, base, sizeof(h));
   if (memcmp(h.magic, OTR_GRAPH_MAGIC, 8) != 0 || h.version != OTR_GRAPH_VERSION ||
       h.array_offset[OTR_A_END] > (uint64_t)st.st_size) {
-    munmap(map, (size_t)st.st_size);
     if (err) *err = "not an OTR graph file: " + cfg.graph_path;
     return OTR_BAD_REQUEST;
   }
+  if (h.n_nodes >= (1u << 28)) {  // adj packs dst in 28 bits
+    if (err) *err = "graph has more than 2^28 nodes";
+    return OTR_BAD_REQUEST;
+  }
+  const uint32_t* dst = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_DST]);
+  const float* lenf = (const float*)(base + h.array_offset[OTR_A_EDGE_LEN]);
+  const uint32_t* attr = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_ATTR]);
+  const uint32_t* row = (const uint32_t*)(base + h.array_offset[OTR_A_NODE_ROW]);
+  const int32_t* nll = (const int32_t*)(base + h.array_offset[OTR_A_NODE_LL]);
+  const uint32_t* eshape = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_SHAPE]);
+  const int32_t* sll = (const int32_t*)(base + h.array_offset[OTR_A_SHAPE_LL]);
+  // ---- host-side validation and derived views (nothing on the device is touched yet)
+  // len_mm = round(len * 1000), >= 1 mm: the integer routing length the oracle derives
+  // the same way
+  std::vector<uint32_t> len(h.n_edges + 1, 0u);
+  for (uint32_t e = 0; e < h.n_edges; ++e) {
+    const double mm = (double)lenf[e] * 1000.0;
+    if (!(mm >= 0.0 && mm < 2.0e9)) {  // uint32 label arithmetic
+      if (err) *err = "graph edge length outside [0, 2000 km)";
+      return OTR_BAD_REQUEST;
+    }
+    len[e] = (uint32_t)std::max(1LL, (long long)llround(mm));
+  }
+  for (uint32_t u = 0; u < h.n_nodes; ++u)
+    if (row[u + 1] < row[u] || row[u + 1] > h.n_edges) {
+      if (err) *err = "graph CSR rows are not monotone";
+      return OTR_BAD_REQUEST;
+    }
+  for (uint32_t e = 0; e < h.n_edges; ++e)
+    if (dst[e] >= h.n_nodes || eshape[e + 1] < eshape[e] + 2 || eshape[e + 1] > h.n_shape) {
+      if (err) *err = "graph edge " + std::to_string(e) + " has a bad end node or shape range";
+      return OTR_BAD_REQUEST;
+    }
+  std::vector<uint4> pack(h.n_edges + 1);
+  for (uint32_t e = 0; e < h.n_edges; ++e) pack[e] = make_uint4(dst[e], len[e], attr[e], 0u);
+  // per-node adjacency records: the first 4 out-edges of a node in one 64-B record,
+  // {dst | access<<28 | more<<31, len_mm, dst lat_e6, dst lon_e6} per edge
+  std::vector<uint4> adj(4ull * h.n_nodes + 4, make_uint4(kAdjDstMask, 0u, 0u, 0u));
+  for (uint32_t u = 0; u < h.n_nodes; ++u) {
+    const uint32_t deg = row[u + 1] - row[u];
+    for (uint32_t k = 0; k < deg && k < 4; ++k) {
+      const uint32_t e = row[u] + k;
+      adj[4ull * u + k] = make_uint4(dst[e] | ((attr[e] & OTR_ATTR_ACCESS_MASK) << 28), len[e],
+                                     (uint32_t)nll[2ull * dst[e]], (uint32_t)nll[2ull * dst[e] + 1]);
+    }
+    if (deg > 4) adj[4ull * u + 3].x |= kAdjMore;
+  }
+  // route times per mode (0.1 s) per edge and per adjacency slot
+  std::vector<uint32_t> et[OTR_MODES], at[OTR_MODES];
+  for (int m = 0; m < OTR_MODES; ++m) {
+    et[m].assign(h.n_edges + 1, 0u);
+    for (uint32_t e = 0; e < h.n_edges; ++e) et[m][e] = edge_time_ds(attr[e], len[e], cfg.mp.m[m].speed_kph);
+    at[m].assign(4ull * h.n_nodes + 4, 0u);
+    for (uint32_t u = 0; u < h.n_nodes; ++u)
+      for (uint32_t k = 0; k < 4 && row[u] + k < row[u + 1]; ++k) at[m][4ull * u + k] = et[m][row[u] + k];
+  }
+  // edge headings: first / last non-degenerate shape segment (oracle orc_graph_load)
+  std::vector<short2> head(h.n_edges + 1, make_short2(0, 0));
+  for (uint32_t e = 0; e < h.n_edges; ++e) {
+    const uint32_t k0 = eshape[e], k1 = eshape[e + 1];
+    int hb = -1, he = -1;
+    for (uint32_t k = k0; k + 1 < k1 && hb < 0; ++k) hb = seg_heading(sll + 2ull * k, sll + 2ull * k + 2);
+    for (uint32_t k = k1 - 1; k > k0 && he < 0; --k) he = seg_heading(sll + 2ull * k - 2, sll + 2ull * k);
+    head[e] = make_short2((short)(hb < 0 ? 0 : hb), (short)(he < 0 ? 0 : he));
+  }
+  // heuristic scale: every edge must satisfy len_mm >= scale * (straight-line mm in any
+  // search's metric); the upper bound of that metric distance uses the edge's own
+  // more equatorward cosine.  Generated graphs give 1; lengths rounded
+  // below geometry (e.g. whole metres) lower it; a zero-length edge between distinct
+  // points makes it 0, i.e. plain Dijkstra order.
+  double scale = 1.0;
+  for (uint32_t u = 0; u < h.n_nodes; ++u)
+    for (uint32_t e = row[u]; e < row[u + 1]; ++e) {
+      const uint32_t v = dst[e];
+      const double la1 = nll[2ull * u] * 1e-6, lo1 = nll[2ull * u + 1] * 1e-6;
+      const double la2 = nll[2ull * v] * 1e-6, lo2 = nll[2ull * v + 1] * 1e-6;
+      const double cmax = cos_deg(fmin(fabs(la1), fabs(la2)));
+      const double x = (lo1 - lo2) * kMetersPerDeg * cmax, y = (la1 - la2) * kMetersPerDeg;
+      const double d_mm = sqrt(x * x + y * y) * 1000.0 * (1.0 + 1e-9) + 1e-6;
+      if (d_mm > 1e-3 && (double)len[e] < scale * d_mm) scale = (double)len[e] / d_mm;
+    }
+  // candidate-search view: each grid-cell entry carries its edge's shape range and
+  // attributes, 48 B per entry: {edge, shape begin, shape end, attr} + the first four shape points
+  const uint32_t* cedge = (const uint32_t*)(base + h.array_offset[OTR_A_CELL_EDGE]);
+  std::vector<uint4> crec(3 * ((size_t)h.n_cell_entries + 1), make_uint4(0u, 0u, 0u, 0u));
+  for (uint64_t q = 0; q < h.n_cell_entries; ++q) {
+    const uint32_t e = cedge[q];
+    if (e >= h.n_edges) {
+      if (err) *err = "graph cell index names a missing edge";
+      return OTR_BAD_REQUEST;
+    }
+    const uint32_t k0 = eshape[e], k1 = eshape[e + 1];
+    crec[3 * q] = make_uint4(e, k0, k1, attr[e]);
+    uint32_t pt[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    for (uint32_t i = 0; i < 4 && k0 + i < k1; ++i) {
+      pt[2 * i] = (uint32_t)sll[2ull * (k0 + i)];
+      pt[2 * i + 1] = (uint32_t)sll[2ull * (k0 + i) + 1];
+    }
+    crec[3 * q + 1] = make_uint4(pt[0], pt[1], pt[2], pt[3]);
+    crec[3 * q + 2] = make_uint4(pt[4], pt[5], pt[6], pt[7]);
+  }
+  // ---- upload into a staged replica
   HIPCHK(hipSetDevice(cfg.device));
-  for (void* p : gs.allocs) (void)hipFree(p);
-  gs.allocs.clear();
-  auto up = [&](int a, size_t bytes) -> void* {
+  Staged sg;
+  bool alloc_ok = true;
+  auto upv = [&](const void* src, size_t bytes) -> void* {
     void* d = nullptr;
-    if (hipMalloc(&d, bytes ? bytes : 16) != hipSuccess) return nullptr;
-    if (bytes) (void)hipMemcpy(d, base + h.array_offset[a], bytes, hipMemcpyHostToDevice);
-    gs.allocs.push_back(d);
+    if (hipMalloc(&d, bytes ? bytes : 16) != hipSuccess) {
+      alloc_ok = false;
+      return nullptr;
+    }
+    sg.allocs.push_back(d);
+    if (bytes && hipMemcpy(d, src, bytes, hipMemcpyHostToDevice) != hipSuccess) alloc_ok = false;
     return d;
   };
-  DevGraph& g = gs.dg;
+  auto up = [&](int a, size_t bytes) -> void* { return upv(base + h.array_offset[a], bytes); };
+  DevGraph g{};
   g.node_row = (const uint32_t*)up(OTR_A_NODE_ROW, 4ull * (h.n_nodes + 1));
   g.rev_row = (const uint32_t*)up(OTR_A_REV_ROW, 4ull * (h.n_nodes + 1));
   g.node_ll = (const int2*)up(OTR_A_NODE_LL, 8ull * h.n_nodes);
@@ -110,100 +302,32 @@ int engine_configure(const Config& cfg, std::string* err) {
   g.seg_len = (const uint32_t*)up(OTR_A_SEG_LEN, 4ull * h.n_segments);
   g.cell_row = (const uint32_t*)up(OTR_A_CELL_ROW, 4ull * (h.n_cells + 1));
   g.cell_edge = (const uint32_t*)up(OTR_A_CELL_EDGE, 4ull * h.n_cell_entries);
-  // routing views.  len_mm = round(len * 1000): the integer routing length the oracle
-  // derives the same way
+  g.len_mm = (const uint32_t*)upv(len.data(), 4ull * len.size());
+  g.edge_pack = (const uint4*)upv(pack.data(), sizeof(uint4) * pack.size());
+  g.adj = (const uint4*)upv(adj.data(), sizeof(uint4) * adj.size());
   {
-    const uint32_t* dst = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_DST]);
-    const float* lenf = (const float*)(base + h.array_offset[OTR_A_EDGE_LEN]);
-    const uint32_t* attr = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_ATTR]);
-    std::vector<uint32_t> len(h.n_edges + 1, 0u);
-    for (uint32_t e = 0; e < h.n_edges; ++e) {
-      const double mm = (double)lenf[e] * 1000.0;
-      if (!(mm >= 0.0 && mm < 2.0e9)) {  // uint32 label arithmetic
-        munmap(map, (size_t)st.st_size);
-        if (err) *err = "graph edge length outside [0, 2000 km)";
-        return OTR_BAD_REQUEST;
-      }
-      len[e] = (uint32_t)std::max(1LL, (long long)llround(mm));  // >= 1 mm
+    std::vector<uint32_t> all_et, all_at;
+    for (int m = 0; m < OTR_MODES; ++m) {
+      all_et.insert(all_et.end(), et[m].begin(), et[m].end());
+      all_at.insert(all_at.end(), at[m].begin(), at[m].end());
     }
-    std::vector<uint4> pack(h.n_edges + 1);
-    for (uint32_t e = 0; e < h.n_edges; ++e) pack[e] = make_uint4(dst[e], len[e], attr[e], 0u);
-    auto upv = [&](const void* src, size_t bytes) -> void* {
-      void* d = nullptr;
-      if (hipMalloc(&d, bytes ? bytes : 16) != hipSuccess) return nullptr;
-      gs.allocs.push_back(d);
-      if (bytes) (void)hipMemcpy(d, src, bytes, hipMemcpyHostToDevice);
-      return d;
-    };
-    g.len_mm = (const uint32_t*)upv(len.data(), 4ull * len.size());
-    g.edge_pack = (const uint4*)upv(pack.data(), sizeof(uint4) * pack.size());
-    // per-node adjacency records: the first 4 out-edges of a node in one 64-B record,
-    // {dst | access<<28 | more<<31, len_mm, dst lat_e6, dst lon_e6} per edge
-    if (h.n_nodes >= (1u << 28)) {
-      munmap(map, (size_t)st.st_size);
-      if (err) *err = "graph has more than 2^28 nodes";
-      return OTR_BAD_REQUEST;
-    }
-    const uint32_t* row = (const uint32_t*)(base + h.array_offset[OTR_A_NODE_ROW]);
-    const int32_t* nll = (const int32_t*)(base + h.array_offset[OTR_A_NODE_LL]);
-    std::vector<uint4> adj(4ull * h.n_nodes + 4, make_uint4(kAdjDstMask, 0u, 0u, 0u));
-    for (uint32_t u = 0; u < h.n_nodes; ++u) {
-      const uint32_t deg = row[u + 1] - row[u];
-      for (uint32_t k = 0; k < deg && k < 4; ++k) {
-        const uint32_t e = row[u] + k;
-        adj[4ull * u + k] = make_uint4(dst[e] | ((attr[e] & OTR_ATTR_ACCESS_MASK) << 28), len[e],
-                                       (uint32_t)nll[2ull * dst[e]], (uint32_t)nll[2ull * dst[e] + 1]);
-      }
-      if (deg > 4) adj[4ull * u + 3].x |= kAdjMore;
-    }
-    g.adj = (const uint4*)upv(adj.data(), sizeof(uint4) * adj.size());
-    // heuristic scale: every edge must satisfy len_mm >= scale * (straight-line mm in any
-    // search's metric); the upper bound of that metric distance uses the edge's own
-    // more equatorward cosine.  Generated graphs give 1; lengths rounded
-    // below geometry (e.g. whole metres) lower it; a zero-length edge between distinct
-    // points makes it 0, i.e. plain Dijkstra order.
-    double scale = 1.0;
-    for (uint32_t u = 0; u < h.n_nodes; ++u)
-      for (uint32_t e = row[u]; e < row[u + 1]; ++e) {
-        const uint32_t v = dst[e];
-        const double la1 = nll[2ull * u] * 1e-6, lo1 = nll[2ull * u + 1] * 1e-6;
-        const double la2 = nll[2ull * v] * 1e-6, lo2 = nll[2ull * v + 1] * 1e-6;
-        const double cmax = cos_deg(fmin(fabs(la1), fabs(la2)));
-        const double x = (lo1 - lo2) * kMetersPerDeg * cmax, y = (la1 - la2) * kMetersPerDeg;
-        const double d_mm = sqrt(x * x + y * y) * 1000.0 * (1.0 + 1e-9) + 1e-6;
-        if (d_mm > 1e-3 && (double)len[e] < scale * d_mm) scale = (double)len[e] / d_mm;
-      }
-    float hs = (float)scale;
-    if ((double)hs > scale) hs = nextafterf(hs, 0.0f);
-    g.h_scale = hs > 0.0f ? hs : 0.0f;
-#ifdef OTR_FORCE_H_SCALE1
-    g.h_scale = 1.0f;  // experiment only: the unscaled heuristic
-#endif
-    // candidate-search view: each grid-cell entry carries its edge's shape range and attributes
-    const uint32_t* cedge = (const uint32_t*)(base + h.array_offset[OTR_A_CELL_EDGE]);
-    const uint32_t* eshape = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_SHAPE]);
-    // 48 B per entry: {edge, shape begin, shape end, attr} + the first four shape points
-    const int32_t* sll = (const int32_t*)(base + h.array_offset[OTR_A_SHAPE_LL]);
-    std::vector<uint4> crec(3 * ((size_t)h.n_cell_entries + 1), make_uint4(0u, 0u, 0u, 0u));
-    for (uint64_t q = 0; q < h.n_cell_entries; ++q) {
-      const uint32_t e = cedge[q], k0 = eshape[e], k1 = eshape[e + 1];
-      crec[3 * q] = make_uint4(e, k0, k1, attr[e]);
-      uint32_t pt[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-      for (uint32_t i = 0; i < 4 && k0 + i < k1; ++i) {
-        pt[2 * i] = (uint32_t)sll[2ull * (k0 + i)];
-        pt[2 * i + 1] = (uint32_t)sll[2ull * (k0 + i) + 1];
-      }
-      crec[3 * q + 1] = make_uint4(pt[0], pt[1], pt[2], pt[3]);
-      crec[3 * q + 2] = make_uint4(pt[4], pt[5], pt[6], pt[7]);
-    }
-    g.cell_rec = (const uint4*)upv(crec.data(), sizeof(uint4) * crec.size());
+    g.edge_t = (const uint32_t*)upv(all_et.data(), 4ull * all_et.size());
+    g.adj_t = (const uint32_t*)upv(all_at.data(), 4ull * all_at.size());
+    g.edge_t_stride = (uint32_t)et[0].size();
+    g.adj_t_stride = (uint32_t)at[0].size();
   }
-  for (void* p : gs.allocs)
-    if (!p) {
-      munmap(map, (size_t)st.st_size);
-      if (err) *err = "device allocation for the graph failed";
-      return OTR_DEVICE_ERROR;
-    }
+  g.edge_head = (const short2*)upv(head.data(), sizeof(short2) * head.size());
+  g.cell_rec = (const uint4*)upv(crec.data(), sizeof(uint4) * crec.size());
+  if (!alloc_ok) {
+    if (err) *err = "device allocation for the graph failed";
+    return OTR_DEVICE_ERROR;  // the previous graph (if any) stays configured
+  }
+  float hs = (float)scale;
+  if ((double)hs > scale) hs = nextafterf(hs, 0.0f);
+  g.h_scale = hs > 0.0f ? hs : 0.0f;
+#ifdef OTR_FORCE_H_SCALE1
+  g.h_scale = 1.0f;  // experiment only: the unscaled heuristic
+#endif
   g.n_nodes = h.n_nodes;
   g.n_edges = h.n_edges;
   g.n_segments = h.n_segments;
@@ -212,15 +336,26 @@ int engine_configure(const Config& cfg, std::string* err) {
   g.grid_min_lat = h.grid_min_lat;
   g.grid_min_lon = h.grid_min_lon;
   g.grid_cell_deg = h.grid_cell_deg;
-  gs.n_nodes = h.n_nodes;
-  gs.n_edges = h.n_edges;
-  gs.n_segments = h.n_segments;
-  gs.seg_id.assign((const unsigned long long*)(base + h.array_offset[OTR_A_SEG_ID]),
-                   (const unsigned long long*)(base + h.array_offset[OTR_A_SEG_ID]) + h.n_segments);
-  munmap(map, (size_t)st.st_size);
-  gs.defaults = cfg.mp;
-  gs.device = cfg.device;
-  gs.ready = true;
+  std::vector<unsigned long long> sid((const unsigned long long*)(base + h.array_offset[OTR_A_SEG_ID]),
+                                      (const unsigned long long*)(base + h.array_offset[OTR_A_SEG_ID]) + h.n_segments);
+  // ---- swap in: batches in flight hold the shared lock, so the old arrays are unused
+  GraphState& gs = graph_state();
+  std::vector<void*> old;
+  {
+    std::unique_lock<std::shared_mutex> lk(gs.mu);
+    old.swap(gs.allocs);
+    gs.allocs = sg.allocs;
+    sg.adopted = true;
+    gs.dg = g;
+    gs.n_nodes = h.n_nodes;
+    gs.n_edges = h.n_edges;
+    gs.n_segments = h.n_segments;
+    gs.seg_id.swap(sid);
+    gs.defaults = cfg.mp;
+    gs.device = cfg.device;
+    gs.ready = true;
+  }
+  for (void* q : old) (void)hipFree(q);
   return OTR_OK;
 }
 
@@ -244,7 +379,7 @@ enum Slot {
   S_C_ROUTE_OFF, S_C_SEG_OFF, S_C_WAY_OFF, S_C_REP_OFF, S_C_ARGS, S_C_ROUTE, S_C_SEG_ID, S_C_SEG_START,
   S_C_SEG_END, S_C_SEG_LEN, S_C_SEG_QUEUE, S_C_SEG_INTERNAL, S_C_SEG_BSHAPE, S_C_SEG_ESHAPE, S_C_SEG_WAY_N,
   S_C_SEG_WAY, S_C_SEG_WAY_OFF, S_C_REP_ID, S_C_REP_NEXT, S_C_REP_T0, S_C_REP_T1, S_C_REP_LEN, S_C_REP_QUEUE,
-  S_TASK_REC, S_IN_TEXT, S_IN_CNT, S_IN_CSCAN, S_IN_NL, S_IN_HASH, S_IN_UOFF, S_IN_ULEN, S_IN_TIME, S_IN_LAT, S_IN_LON,
+  S_TASK_REC, S_BT, S_CPREP_T, S_TRANS_TC, S_TURN, S_LIST2, S_GFLAG, S_IN_TEXT, S_IN_CNT, S_IN_CSCAN, S_IN_NL, S_IN_HASH, S_IN_UOFF, S_IN_ULEN, S_IN_TIME, S_IN_LAT, S_IN_LON,
   S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
@@ -272,6 +407,9 @@ T* Matcher::need(int slot, size_t n) {
 Matcher::~Matcher() {
   for (auto& b : bufs)
     if (b.p) (void)hipFree(b.p);
+  for (auto& sl : gslab)
+    for (void* q : {(void*)sl.key, (void*)sl.lab, (void*)sl.qmark, (void*)sl.fr, (void*)sl.touched})
+      if (q) (void)hipFree(q);
   if (ev_init)
     for (auto& e : ev) (void)hipEventDestroy(e);
   if (stream) (void)hipStreamDestroy(stream);
@@ -316,12 +454,23 @@ __global__ void k_collect(int64_t n, const int32_t* flag, int64_t* list, unsigne
   block_append(i < n && flag[i], i, list, count);
 }
 
-// retry tiers: take the flagged tasks (flag == want, or any flag when want == 0) and
-// clear their flags; tasks flagged for a later tier keep theirs
-__global__ void k_collect_tier(int64_t n, int32_t* flag, int want, int64_t* list, unsigned long long* count) {
+// retry tiers: take the tasks whose flag is in the bit set `want` (bit f = flag value f)
+// and clear their flags; tasks flagged for a later tier keep theirs.  The list length
+// stays on the device: the next kernel reads it there.
+__global__ void k_collect_tier(int64_t n, int32_t* flag, uint32_t want, int64_t* list, unsigned long long* count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int f = i < n ? flag[i] : 0;
-  const bool sel = f != 0 && (want == 0 || f == want);
+  const bool sel = f != 0 && ((want >> f) & 1u);
+  if (sel) flag[i] = 0;
+  block_append(sel, i, list, count);
+}
+
+// the same over a device-counted list (steps of the path stage): entries list_in[0..*n_in)
+__global__ void k_collect_tier_list(const unsigned long long* n_in, int32_t* flag, uint32_t want, int64_t* list,
+                                    unsigned long long* count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int f = i < (int64_t)*n_in ? flag[i] : 0;
+  const bool sel = f != 0 && ((want >> f) & 1u);
   if (sel) flag[i] = 0;
   block_append(sel, i, list, count);
 }
@@ -362,6 +511,7 @@ static std::vector<int> route_tiers() {
 
 int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err) {
   GraphState& gs = graph_state();
+  std::shared_lock<std::shared_mutex> graph_lock(gs.mu);  // a reconfigure waits for this batch
   if (!gs.ready) {
     if (err) *err = "otr_configure has not been called";
     return OTR_NOT_CONFIGURED;
@@ -480,11 +630,15 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     te(OTR_STAGE_CANDIDATES);
   }
   // ---- K_link + task map
+  uint32_t turn_modes = 0;  // modes whose searches carry turn costs (edge-based, k_general)
+  for (int m = 0; m < OTR_MODES; ++m)
+    if (mp.m[m].turn_penalty_factor > 0.0) turn_modes |= 1u << m;
   StepBuf sb;
   sb.prev = need<int64_t>(S_PREV, S);
   sb.g = need<double>(S_G, S);
   sb.bound = need<double>(S_BOUND, S);
   sb.forced = need<uint8_t>(S_FORCED, S);
+  sb.bt = need<int32_t>(S_BT, S);
   sb.ntask = need<int64_t>(S_NTASK, S);
   sb.ntrans = need<int64_t>(S_NTRANS, S);
   int64_t* task_off = need<int64_t>(S_TASK_OFF, S + 1);
@@ -494,24 +648,31 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   te(OTR_STAGE_LINK);
   if (S > 0)
     k_tasks<<<grid_for(S, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, nullptr,
-                                                nullptr, nullptr);
+                                                nullptr, nullptr, state_trace, b.mode, turn_modes);
   if ((rc = scan(sb.ntask, task_off, S))) return rc;
   if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
   int64_t NT = 0, NTR = 0;
-  if ((rc = read_i64(task_off + S, &NT))) return rc;
-  if ((rc = read_i64(trans_off + S, &NTR))) return rc;
+  HIPCHK(hipMemcpyAsync(&NT, task_off + S, 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(&NTR, trans_off + S, 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
   int64_t* task_state = need<int64_t>(S_TASK_STATE, NT);
   unsigned long long* task_mask = need<unsigned long long>(S_TASK_MASK, NT);
   int32_t* task_ovf = need<int32_t>(S_TASK_OVF, NT);
   uint32_t* trans = need<uint32_t>(S_TRANS, NTR);
-  if (!task_state || !task_mask || !task_ovf || !trans) {
+  uint32_t* trans_tc = need<uint32_t>(S_TRANS_TC, NTR);
+  if (!task_state || !task_mask || !task_ovf || !trans || !trans_tc) {
     if (err) *err = "device allocation failed (transitions)";
     return OTR_DEVICE_ERROR;
   }
   if (S > 0)
     k_tasks<<<grid_for(S, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, task_off,
-                                                task_state, task_mask);
+                                                task_state, task_mask, state_trace, b.mode, turn_modes);
   if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
+  // turn cost tables of this batch's parameters (oracle orc_turn_table)
+  int32_t* d_turn = need<int32_t>(S_TURN, 181 * OTR_MODES);
+  h_turn.resize(181 * OTR_MODES);
+  for (int m = 0; m < OTR_MODES; ++m) turn_table(mp.m[m].turn_penalty_factor, h_turn.data() + 181 * m);
+  HIPCHK(hipMemcpyAsync(d_turn, h_turn.data(), 4 * 181 * OTR_MODES, hipMemcpyHostToDevice, stream));
   // ---- K3/K4: routing + transition costs
   RouteArgs ra{};
   ra.task_state = task_state;
@@ -533,6 +694,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   ra.lat = b.lat;
   ra.lon = b.lon;
   ra.radius = cb.radius;
+  ra.bt = sb.bt;
   // K2b: per-state search inputs
   PrepArgs pr{};
   pr.n_states = S;
@@ -545,9 +707,12 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   pr.lat = b.lat;
   pr.lon = b.lon;
   pr.radius = cb.radius;
+  pr.state_trace = state_trace;
+  pr.mode = b.mode;
   pr.heur = need<Heur>(S_HEUR, S);
   pr.cprep = need<uint4>(S_CPREP, (size_t)S * OTR_KMAX);
-  if (!pr.heur || !pr.cprep) {
+  pr.cprep_t = need<uint2>(S_CPREP_T, (size_t)S * OTR_KMAX);
+  if (!pr.heur || !pr.cprep || !pr.cprep_t) {
     if (err) *err = "device allocation failed (prep)";
     return OTR_DEVICE_ERROR;
   }
@@ -559,9 +724,11 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   }
   if (NT > 0)
     k_task_rec<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_state, task_mask, sb.prev, sb.bound, sb.forced, cb.count,
-                                                      cb.edge, g.edge_dst, state_trace, b.mode, pr.cprep, task_rec);
+                                                      cb.edge, g.edge_dst, state_trace, b.mode, pr.cprep, sb.bt,
+                                                      turn_modes, task_rec);
   ra.heur = pr.heur;
   ra.cprep = pr.cprep;
+  ra.cprep_t = pr.cprep_t;
   ra.rec = task_rec;
   ra.delta = mp.delta;
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
@@ -570,6 +737,60 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   static const uint32_t direct_bmm =
       getenv("OTR_DIRECT_BMM") ? (uint32_t)strtoul(getenv("OTR_DIRECT_BMM"), nullptr, 10) : 1900000u;  // A/B knob
   ra.direct_bmm = direct_bmm;
+  // device-side counters of the retry lists: [0..7] route tiers, [8] general tier 1,
+  // [9] general tier 2, [10] route tasks left unrouted, [11] steps, [12..15] path tiers,
+  // [16] path general 1, [17] path general 2, [18] paths left, [19] general overflow
+  // count, [20] cap flag, [32..96) path bump cursors
+  unsigned long long* cnt = need<unsigned long long>(S_MISC, 32 + kShards);
+  HIPCHK(hipMemsetAsync(cnt, 0, 8 * (32 + kShards), stream));
+  int64_t* list = need<int64_t>(S_LIST, std::max<int64_t>(NT, S));
+  int64_t* fail_tasks = need<int64_t>(S_GFLAG, std::max<int64_t>(NT, 1));
+  // general (global-memory) search slabs: allocated on first use, cleared once
+  auto slabs = [&](int tier, GSlabs* out) -> int {
+    GSlab& sl = gslab[tier];
+    const uint32_t cap = tier == 0 ? (1u << 15) : (1u << 20);
+    const uint32_t n = tier == 0 ? 1024u : 8u;
+    if (!sl.key) {
+      const size_t c = (size_t)cap * n;
+      HIPCHK(hipMalloc(&sl.key, 4 * c));
+      HIPCHK(hipMalloc(&sl.lab, 8 * c));
+      HIPCHK(hipMalloc(&sl.qmark, 4 * c));
+      HIPCHK(hipMalloc(&sl.fr, 8 * c));
+      HIPCHK(hipMalloc(&sl.touched, 4 * c));
+      HIPCHK(hipMemsetAsync(sl.key, 0xFF, 4 * c, stream));
+      HIPCHK(hipMemsetAsync(sl.lab, 0xFF, 8 * c, stream));
+      HIPCHK(hipMemsetAsync(sl.qmark, 0, 4 * c, stream));
+    }
+    out->key = sl.key;
+    out->lab = sl.lab;
+    out->qmark = sl.qmark;
+    out->fr = sl.fr;
+    out->touched = sl.touched;
+    out->cap = cap;
+    out->n = n;
+    return OTR_OK;
+  };
+  GenArgs ga{};
+  ga.prev = sb.prev;
+  ga.g = sb.g;
+  ga.bt = sb.bt;
+  ga.bound = sb.bound;
+  ga.cand_count = cb.count;
+  ga.cand_edge = cb.edge;
+  ga.cand_p = cb.p;
+  ga.cprep = pr.cprep;
+  ga.cprep_t = pr.cprep_t;
+  ga.state_trace = state_trace;
+  ga.mode_of_trace = b.mode;
+  ga.turn_modes = turn_modes;
+  ga.turn = d_turn;
+  ga.task_state = task_state;
+  ga.task_mask = task_mask;
+  ga.trans_off = trans_off;
+  ga.trans = trans;
+  ga.trans_tc = trans_tc;
+  ga.counters = d_counters;
+  ga.n_overflow = cnt + 19;
   if (NT > 0) {
     tb(OTR_STAGE_ROUTE);
     // two searches per wave (CAP 160 tables); wider steps and overflows retry below
@@ -581,54 +802,48 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       k_route<256, 1><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
     }
     te(OTR_STAGE_ROUTE);
-    // overflow retries with larger LDS tables (same results, fewer resident waves)
-    int64_t* list = need<int64_t>(S_LIST, NT);
-    unsigned long long* cnt = need<unsigned long long>(S_MISC, 4);
+    // overflow retries with larger LDS tables (same results, fewer resident waves): each
+    // tier takes its list on the device and runs a fixed grid over it — no host round
+    // trip between tiers.  First-tier overflows flagged 2 (long bounds)
+    // skip the 256-slot tier; OTR_TIERS (A/B knob) lists the retry kernels.
     tb(OTR_STAGE_ROUTE_BIG);
-    // first-tier overflows flagged 2 (long bounds) skip the 256-slot tier;
-    // OTR_TIERS (A/B knob) lists the retry kernels, e.g. "256,512x2,1024,4096"
     static const std::vector<int> tiers = route_tiers();
     const int ntier = (int)tiers.size();
+    const unsigned tgrid = 2048;
     for (int tier = 0; tier < ntier; ++tier) {
-      HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
-      k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, tier == 0 ? 1 : 0, list, cnt);
-      unsigned long long novf = 0;
-      HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipStreamSynchronize(stream));
-      if (novf == 0 && tier > 0) break;
-      if (novf == 0) continue;
+      unsigned long long* c = cnt + tier;
+      k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, tier == 0 ? 0x2u : 0x6u, list + 0, c);
       RouteArgs rb = ra;
       rb.task_list = list;
-      rb.n_tasks = (int64_t)novf;
-      unsigned long long* rc = d_counters + 6 * kShards;
+      rb.list_count = c;
+      unsigned long long* rcn = d_counters + 6 * kShards;
       switch (tiers[tier]) {
-        case 2561: k_route<256, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
-        case 5121: k_route<512, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
-        case 10241: k_route<1024, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
-        case 20481: k_route<2048, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
-        case 3842: k_route<384, 2><<<(unsigned)((novf + 1) / 2), 64, 0, stream>>>(g, rb, rc); break;
-        case 4482: k_route<448, 2><<<(unsigned)((novf + 1) / 2), 64, 0, stream>>>(g, rb, rc); break;
-        case 5122: k_route<512, 2><<<(unsigned)((novf + 1) / 2), 64, 0, stream>>>(g, rb, rc); break;
-        default: k_route<4096, 1><<<(unsigned)novf, 64, 0, stream>>>(g, rb, rc); break;
-      }
-      if (tier == ntier - 1) {
-        HIPCHK(hipMemsetAsync(cnt, 0, 32, stream));
-        k_collect<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, list, cnt);
-        HIPCHK(hipMemcpyAsync(&novf, cnt, 8, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipStreamSynchronize(stream));
-        out->n_overflow_traces += (int32_t)novf;
-        // rare: name the traces (task → state → trace) for per-trace status
-        std::vector<int64_t> tl(novf);
-        if (novf) HIPCHK(hipMemcpy(tl.data(), list, 8 * novf, hipMemcpyDeviceToHost));
-        for (int64_t task : tl) {
-          int64_t s = 0;
-          int32_t t = 0;
-          HIPCHK(hipMemcpy(&s, task_state + task, 8, hipMemcpyDeviceToHost));
-          HIPCHK(hipMemcpy(&t, state_trace + s, 4, hipMemcpyDeviceToHost));
-          if (t >= 0 && t < T) h_trace_status[t] = OTR_MATCH_ERROR;
-        }
+        case 2561: k_route<256, 1><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 5121: k_route<512, 1><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 10241: k_route<1024, 1><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 20481: k_route<2048, 1><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 3842: k_route<384, 2><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 4482: k_route<448, 2><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 5122: k_route<512, 2><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        default: k_route<4096, 1><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
       }
     }
+    // everything left — turn-cost (edge-based) tasks, tasks whose labels need 64 bits,
+    // overflows of the largest LDS table — runs in the global-memory search: first on
+    // 32K-slot slabs, then what outgrew those on 1M-slot slabs
+    for (int gt = 0; gt < 2; ++gt) {
+      unsigned long long* c = cnt + 8 + gt;
+      k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, gt == 0 ? 0xEu : 0x2u, list, c);
+      GSlabs gs2;
+      if ((rc = slabs(gt, &gs2))) return rc;
+      ga.mode = 0;
+      ga.list = list;
+      ga.list_count = c;
+      ga.flag = task_ovf;
+      k_general<<<gs2.n, kGenThreads, 0, stream>>>(g, ga, gs2);
+    }
+    // tasks still flagged (beyond a 1M-state slab): their traces get OTR_MATCH_ERROR
+    k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, 0xEu, fail_tasks, cnt + 10);
     te(OTR_STAGE_ROUTE_BIG);
   }
   // ---- K5: Viterbi
@@ -640,6 +855,8 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   va.prev = sb.prev;
   va.trans_off = trans_off;
   va.trans = trans;
+  va.trans_tc = trans_tc;
+  va.turn_modes = turn_modes;
   va.g = sb.g;
   va.mode = b.mode;
   for (int m = 0; m < OTR_MODES; ++m) va.inv2s2[m] = mp.m[m].inv2s2;
@@ -652,33 +869,29 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   tb(OTR_STAGE_VITERBI);
   k_viterbi<<<(unsigned)(T < 1048576 ? T : 1048576), 64, 0, stream>>>(va, d_counters);
   te(OTR_STAGE_VITERBI);
-  // ---- K6: winner paths
+  // ---- K6: winner paths (step list, tiers and general fallback counted on the device)
   int64_t* path_off = need<int64_t>(S_PATH_OFF, S);
   int32_t* path_len = need<int32_t>(S_PATH_LEN, S);
   if (S > 0) k_fill_i32<<<grid_for(S, 256), 256, 0, stream>>>(path_len, S, 0);
   {
-    int64_t* steps = need<int64_t>(S_LIST, S > NT ? S : NT);
-    // misc: [0] step count, [1] cap flag, [2] retry count, [8..8+64) shard cursors
-    unsigned long long* cnt = need<unsigned long long>(S_MISC, 8 + kShards);
-    HIPCHK(hipMemsetAsync(cnt, 0, 8 * (8 + kShards), stream));
-    if (S > 0) k_step_list<<<grid_for(S, 1024), 1024, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, cnt);
-    unsigned long long nsteps = 0;
-    HIPCHK(hipMemcpyAsync(&nsteps, cnt, 8, hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipStreamSynchronize(stream));
-    int64_t capacity = kShards * ((int64_t)nsteps * 24 / kShards + 1024);
-    for (int attempt = 0; attempt < 6 && nsteps > 0; ++attempt) {
+    int64_t* steps = need<int64_t>(S_LIST2, std::max<int64_t>(S, 1));
+    unsigned long long* nsteps_d = cnt + 11;
+    if (S > 0) k_step_list<<<grid_for(S, 1024), 1024, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, nsteps_d);
+    int32_t* step_ovf = need<int32_t>(S_STEP_OVF, S + 1);
+    int64_t capacity = kShards * ((int64_t)S * 24 / kShards + 1024);
+    for (int attempt = 0; attempt < 8 && S > 0; ++attempt) {
       uint32_t* path = need<uint32_t>(S_PATH, capacity);
-      int32_t* step_ovf = need<int32_t>(S_STEP_OVF, nsteps + 1);
       if (!path || !step_ovf) {
         if (err) *err = "device allocation failed (paths)";
         return OTR_DEVICE_ERROR;
       }
-      HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
-      HIPCHK(hipMemsetAsync(cnt + 1, 0, 16, stream));
-      HIPCHK(hipMemsetAsync(cnt + 8, 0, 8 * kShards, stream));
+      HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (S + 1), stream));
+      HIPCHK(hipMemsetAsync(cnt + 12, 0, 8 * 9, stream));  // path tier counts, cap flag
+      HIPCHK(hipMemsetAsync(cnt + 32, 0, 8 * kShards, stream));
       PathArgs pa{};
       pa.steps = steps;
-      pa.n_steps = (int64_t)nsteps;
+      pa.n_steps = S;
+      pa.n_steps_dev = nsteps_d;
       pa.prev = sb.prev;
       pa.bound = sb.bound;
       pa.brk = va.brk;
@@ -693,53 +906,59 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       pa.radius = cb.radius;
       pa.heur = ra.heur;
       pa.cprep = ra.cprep;
+      pa.bt = sb.bt;
+      pa.turn_modes = turn_modes;
       pa.delta = mp.delta;
       pa.path_off = path_off;
       pa.path_len = path_len;
       pa.path = path;
-      pa.cursor = cnt + 8;
+      pa.cursor = cnt + 32;
       pa.capacity = capacity;
       pa.overflow_flag = step_ovf;
-      pa.cap_flag = (int32_t*)(cnt + 1);
+      pa.cap_flag = (int32_t*)(cnt + 20);
       tb(OTR_STAGE_PATHS);
       {
-        const int64_t units = ((int64_t)nsteps + 1) / 2;  // two searches per wave
-        k_paths<160, 2><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, pa, nullptr, (int64_t)nsteps);
+        const int64_t units = (S + 1) / 2;  // upper bound: two searches per wave
+        k_paths<160, 2><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, pa, nullptr, nullptr);
       }
       te(OTR_STAGE_PATHS);
-      // large-table retries for table overflows
-      int64_t* rl = need<int64_t>(S_TASK_STATE, NT > (int64_t)nsteps ? NT : (int64_t)nsteps);  // reuse
-      unsigned long long nretry = 0;
       tb(OTR_STAGE_PATHS_BIG);
-      for (int tier = 0; tier < 4; ++tier) {
-        HIPCHK(hipMemsetAsync(cnt + 2, 0, 8, stream));
-        k_collect<<<grid_for(nsteps, 1024), 1024, 0, stream>>>((int64_t)nsteps, step_ovf, rl, cnt + 2);
-        HIPCHK(hipMemcpyAsync(&nretry, cnt + 2, 8, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipStreamSynchronize(stream));
-        if (nretry == 0) break;
-        if (tier == 3) {
-          out->n_overflow_traces += (int32_t)nretry;
-          std::vector<int64_t> il(nretry);
-          HIPCHK(hipMemcpy(il.data(), rl, 8 * nretry, hipMemcpyDeviceToHost));
-          for (int64_t i : il) {
-            int64_t s = 0;
-            int32_t t = 0;
-            HIPCHK(hipMemcpy(&s, steps + i, 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(&t, state_trace + s, 4, hipMemcpyDeviceToHost));
-            if (t >= 0 && t < T) h_trace_status[t] = OTR_MATCH_ERROR;
-          }
-          break;
-        }
-        HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (nsteps + 1), stream));
-        if (tier == 0) k_paths<512, 1><<<(unsigned)nretry, 64, 0, stream>>>(g, pa, rl, (int64_t)nretry);
-        else if (tier == 1) k_paths<1024, 1><<<(unsigned)nretry, 64, 0, stream>>>(g, pa, rl, (int64_t)nretry);
-        else k_paths<4096, 1><<<(unsigned)nretry, 64, 0, stream>>>(g, pa, rl, (int64_t)nretry);
+      // large-table retries for table overflows (flag 1), on device-side lists
+      for (int tier = 0; tier < 3; ++tier) {
+        unsigned long long* c = cnt + 12 + tier;
+        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0x2u, list, c);
+        if (tier == 0) k_paths<512, 1><<<2048, 64, 0, stream>>>(g, pa, list, c);
+        else if (tier == 1) k_paths<1024, 1><<<2048, 64, 0, stream>>>(g, pa, list, c);
+        else k_paths<4096, 1><<<1024, 64, 0, stream>>>(g, pa, list, c);
       }
+      // turn-cost winners, 64-bit labels and the largest-table overflows: k_general
+      ga.steps = steps;
+      ga.winner = va.winner;
+      ga.path_off = path_off;
+      ga.path_len = path_len;
+      ga.path = path;
+      ga.cursor = cnt + 32;
+      ga.capacity = capacity;
+      ga.cap_flag = (int32_t*)(cnt + 20);
+      for (int gt = 0; gt < 2; ++gt) {
+        unsigned long long* c = cnt + 16 + gt;
+        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, gt == 0 ? 0xAu : 0x2u, list,
+                                                                     c);
+        GSlabs gs2;
+        if ((rc = slabs(gt, &gs2))) return rc;
+        ga.mode = 1;
+        ga.list = list;
+        ga.list_count = c;
+        ga.flag = step_ovf;
+        k_general<<<gs2.n, kGenThreads, 0, stream>>>(g, ga, gs2);
+      }
+      // steps still flagged (beyond a 1M-state slab): named after the final sync
+      k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0xAu, list, cnt + 18);
       te(OTR_STAGE_PATHS_BIG);
       unsigned long long capflag = 0;
       std::vector<unsigned long long> cur(kShards);
-      HIPCHK(hipMemcpyAsync(&capflag, cnt + 1, 8, hipMemcpyDeviceToHost, stream));
-      HIPCHK(hipMemcpyAsync(cur.data(), cnt + 8, 8 * kShards, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(&capflag, cnt + 20, 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(cur.data(), cnt + 32, 8 * kShards, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
       if ((capflag & 0xFFFFFFFFu) == 0) break;  // every path fitted its region
       unsigned long long mx = 0;
@@ -807,6 +1026,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   sa.threshold = (double)(in->threshold_sec >= 0 ? in->threshold_sec : 15);
   sa.report_levels = in->report_levels;
   sa.transition_levels = in->transition_levels;
+  for (int m = 0; m < OTR_MODES; ++m) sa.queue_kph[m] = mp.m[m].queue_kph;
   tb(OTR_STAGE_SEGMENTS);
   k_segments<<<(unsigned)(8 * ((T + 7) / 8)), 64, 0, stream>>>(g, sa, d_counters);
   te(OTR_STAGE_SEGMENTS);
@@ -860,8 +1080,31 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   }
   HIPCHK(hipGetLastError());
   std::vector<unsigned long long> hc(n_ctr);
+  unsigned long long h_fail[2] = {0ull, 0ull};  // route tasks / paths beyond every search tier
   HIPCHK(hipMemcpyAsync(hc.data(), d_counters, n_ctr * 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(&h_fail[0], cnt + 10, 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(&h_fail[1], cnt + 18, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
+  if (h_fail[0] + h_fail[1] > 0) {
+    // beyond a 1M-state slab (never seen): name the traces (task/step -> state -> trace)
+    for (int which = 0; which < 2; ++which) {
+      const unsigned long long nf = h_fail[which];
+      if (!nf) continue;
+      std::vector<int64_t> idx(nf), st(nf);
+      HIPCHK(hipMemcpy(idx.data(), which == 0 ? fail_tasks : list, 8 * nf, hipMemcpyDeviceToHost));
+      const int64_t* src = which == 0 ? task_state : need<int64_t>(S_LIST2, 1);
+      for (unsigned long long k = 0; k < nf; ++k) {
+        int64_t sidx = 0;
+        int32_t t = 0;
+        HIPCHK(hipMemcpy(&sidx, src + idx[k], 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&t, state_trace + sidx, 4, hipMemcpyDeviceToHost));
+        if (t >= 0 && t < T && h_trace_status[t] == OTR_OK) {
+          h_trace_status[t] = OTR_MATCH_ERROR;
+          ++out->n_overflow_traces;
+        }
+      }
+    }
+  }
   for (int k = 0; k < OTR_COUNTERS; ++k) {
     unsigned long long v = 0;
     for (int sh = 0; sh < kShards; ++sh) v += hc[(size_t)k * kShards + sh];

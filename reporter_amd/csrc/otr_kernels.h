@@ -328,6 +328,7 @@ struct StepBuf {
   double* g;          // great-circle distance prev→s
   double* bound;      // route bound
   uint8_t* forced;    // g > breakage_distance
+  int32_t* bt;        // time bound of the step, 0.1 s (max_route_time_factor * dt), -1 none
   int64_t* ntask;     // search tasks of the step (k_tasks)
   int64_t* ntrans;    // K[prev]*K[s]
 };
@@ -352,6 +353,7 @@ __global__ __launch_bounds__(256) void k_link(BatchDev b, ModeParams mp, const i
     const int64_t pv = below ? base + (63 - __clzll((long long)below)) : last;
     if (in) {
       st.ntrans[s] = 0;
+      st.bt[s] = -1;
       if (K <= 0) {
         st.prev[s] = -2;
       } else {
@@ -362,6 +364,7 @@ __global__ __launch_bounds__(256) void k_link(BatchDev b, ModeParams mp, const i
           st.g[s] = gcd;
           st.forced[s] = gcd > P.breakage_distance;
           st.bound[s] = route_bound(P, gcd);
+          st.bt[s] = time_bound_ds(P, b.time[ib] - b.time[ia]);
           st.ntrans[s] = (int64_t)cand_count[pv] * K;
         }
       }
@@ -377,7 +380,8 @@ __global__ __launch_bounds__(256) void k_link(BatchDev b, ModeParams mp, const i
 __global__ __launch_bounds__(256) void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* cand_count,
                                                const uint32_t* cand_edge, const uint32_t* edge_dst, int64_t* ntask,
                                                const int64_t* task_off, int64_t* task_state,
-                                               unsigned long long* task_mask) {
+                                               unsigned long long* task_mask, const int32_t* state_trace,
+                                               const uint8_t* mode, uint32_t turn_modes) {
   // one wave per state, lane i = source candidate i of the previous state
   const int64_t s = (int64_t)blockIdx.x * (blockDim.x / OTR_WAVE) + threadIdx.x / OTR_WAVE;
   const int lane = threadIdx.x % OTR_WAVE;
@@ -388,7 +392,11 @@ __global__ __launch_bounds__(256) void k_tasks(int64_t n_states, const int64_t* 
     return;
   }
   const int Ka = cand_count[sp];
-  const uint32_t root = lane < Ka ? edge_dst[cand_edge[sp * OTR_KMAX + lane]] : 0xFFFFFFFFu;
+  // with turn costs the search is edge-based: sources share it only on the same edge
+  const int md = mode[state_trace[s]] < OTR_MODES ? mode[state_trace[s]] : 0;
+  const bool by_edge = (turn_modes >> md) & 1u;
+  const uint32_t ce = lane < Ka ? cand_edge[sp * OTR_KMAX + lane] : 0xFFFFFFFFu;
+  const uint32_t root = lane < Ka ? (by_edge ? ce : edge_dst[ce]) : 0xFFFFFFFFu;
   // sources sharing my root, then: am I the lowest of them (the task's representative)?
   unsigned long long same = 0;
   for (int k = 0; k < Ka; ++k)
@@ -626,41 +634,68 @@ __device__ inline void search_init(SearchLds<CAP, PRED>* Ls) {
   __syncthreads();
 }
 
-// Target (lane) resolved?  Every path through a pending node u reaches T with label >=
-// L(u) + h(u) - h(T) >= fmin - h(T), so L(T) + h(T) < fmin makes L(T) final (strictly:
-// then every predecessor on a shortest path has been processed too); if even
-// min(L(T), fmin - h(T)) cannot make d0 + L + tpart fit the bound, T is unreachable for
-// every source of the task.  Integer arithmetic: no rounding margins needed.
+// Route-label packing of the LDS search: a node label is the 32-bit
+// word (length mm << sh) | time, time in 0.1 s saturating at tcap = 2^sh - 1 >= bound + 1
+// (sh = 0: no time bound, the word is the length).  The word order is the
+// lexicographic (length, time) order, so one atomicMin keeps the exact minimum.
+struct Pack {
+  uint32_t sh;
+  __device__ uint32_t tcap() const { return (1u << sh) - 1u; }
+  __device__ uint32_t d(uint32_t w) const { return w >> sh; }
+  __device__ uint32_t t(uint32_t w) const { return w & tcap(); }
+};
+// the step's shift: the smallest sh with 2^sh - 1 >= bt + 1; 0 without a time bound
+__host__ __device__ inline uint32_t pack_shift(int32_t bt) {
+  if (bt < 0) return 0u;
+  uint32_t sh = 0;
+  while (((1u << sh) - 1u) < (uint32_t)bt + 1u) ++sh;
+  return sh;
+}
+// the largest packed word of the step stays below kNoLabel
+__host__ __device__ inline bool pack_fits(uint32_t bmm, uint32_t sh) {
+  return (((uint64_t)bmm << sh) | ((1ull << sh) - 1ull)) < 0xFFFFFFFFull;
+}
+
+// Target (lane) resolved?  Every path through a pending node u reaches T with length >=
+// L(u) + h(u) - h(T) >= fmin - h(T), so L(T) + h(T) < fmin makes T's label final (its
+// length is strictly shorter than any path not yet found, so its time is final too);
+// if even min(L(T), fmin - h(T)) cannot make d0 + L + tpart fit the bound, T is
+// unreachable for every source of the task.  Integer arithmetic: no rounding margins needed.
 template <int CAP, bool PRED>
-__device__ inline bool target_resolved(const SearchLds<CAP, PRED>& L, int tslot, uint32_t tpart, uint32_t hT,
-                                       uint32_t d0min, uint32_t bound_mm, uint32_t fmin, bool pend_empty) {
+__device__ inline bool target_resolved(const SearchLds<CAP, PRED>& L, const Pack& K, int tslot, uint32_t tpart,
+                                       uint32_t hT, uint32_t d0min, uint32_t bound_mm, uint32_t fmin,
+                                       bool pend_empty) {
   if (tslot < 0 || pend_empty) return true;
   const uint32_t l32 = LabelT<PRED>::label(L.lab[tslot]);
-  const int64_t lab = l32 == kNoLabel ? INT64_MAX / 4 : (int64_t)l32;
+  const int64_t lab = l32 == kNoLabel ? INT64_MAX / 4 : (int64_t)K.d(l32);
   if (lab + (int64_t)hT < (int64_t)fmin) return true;
   const int64_t rest = (int64_t)fmin - (int64_t)hT;
   const int64_t lb = lab < rest ? lab : rest;
   return (int64_t)d0min + lb + (int64_t)tpart > (int64_t)bound_mm;
 }
 
-// Relax edge (u → dw) with u's label du.  Every relaxing lane evaluates the heuristic of
-// the head itself (deterministic, equal to the stored one), so an improvement's key
-// f = label + h is known without reading an hv entry another lane may be writing; the
-// round's minimum over improvements and kept pending nodes is the next round's fmin.
+// Relax edge (u → dw) with u's packed label pu.  Every relaxing lane evaluates the
+// heuristic of the head itself (deterministic, equal to the stored one), so an
+// improvement's key f = length + h is known without reading an hv entry another lane may
+// be writing; the round's minimum over improvements and kept pending nodes is the next
+// round's fmin.  A label improves when its packed word does (a shorter length, or the
+// same length sooner): the node is then pending again.
 template <int CAP, bool PRED>
-__device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, uint32_t dw, uint32_t len_mm, int32_t vlat,
-                                int32_t vlon, uint32_t du, uint32_t edge, uint32_t bound_mm, uint32_t mode_bit,
-                                uint32_t& relaxed, uint32_t& fnext) {
+__device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, const Pack& K, uint32_t dw, uint32_t len_mm,
+                                uint32_t time_ds, int32_t vlat, int32_t vlon, uint32_t pu, uint32_t edge,
+                                uint32_t bound_mm, uint32_t mode_bit, uint32_t& relaxed, uint32_t& fnext) {
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
-  const uint32_t nd = du + len_mm;  // du <= bound < 2^31, len_mm < 2^31: no wrap
+  const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
   if (nd > bound_mm) return -1;
+  const uint32_t tt = K.t(pu) + time_ds;  // both < 2^31
+  const uint32_t nw = (nd << K.sh) | (tt < K.tcap() ? tt : K.tcap());
   const uint32_t h = H(vlat, vlon);
   bool isnew = false;
   const int sl = lds_insert(L, dw & kAdjDstMask, &isnew);
   if (sl < 0) return -1;
   if (isnew) L.hv[sl] = h;
-  const typename LabelT<PRED>::T nb = LabelT<PRED>::make((uint32_t)nd, edge);
+  const typename LabelT<PRED>::T nb = LabelT<PRED>::make(nw, edge);
   const typename LabelT<PRED>::T old = atomicMin(&L.lab[sl], nb);
   if (LabelT<PRED>::label(nb) < LabelT<PRED>::label(old)) {
     const uint32_t f = nd + h;
@@ -673,10 +708,12 @@ __device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, uint32_t
 
 // G searches per wave, one per lane group, each in its own table Ls[g]: search g is
 // rooted at `start` (label 0); lanes gl < n_tgt of the group hold a target node tnode, its
-// heuristic hT and partial length tpart (mm).  active = false: the group idles.
+// heuristic hT and partial length tpart (mm).  active = false: the group idles.  K packs
+// the labels (route time tracked when K.sh > 0, from adj_t / edge_t: the mode's times).
 // Returns false (per lane, group-uniform) on an LDS-table overflow.
 template <int CAP, bool PRED, int G = 1>
-__device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const Heur& H, uint32_t mode_bit,
+__device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const Heur& H, const Pack& K,
+                           uint32_t mode_bit,
                            bool active, uint32_t start, uint32_t bound_mm, uint32_t delta_mm, uint32_t tnode,
                            uint32_t tpart, uint32_t hT, uint32_t d0min, int n_tgt, unsigned long long* settled,
                            unsigned long long* relaxed, unsigned long long* rounds,
@@ -693,6 +730,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
   const uint32_t hroot = H(sll.x, sll.y);
   using Idx = typename SearchLds<CAP, PRED>::Idx;
   constexpr int WCAP = SearchLds<CAP, PRED>::WCAP;
+  const bool timed = K.sh != 0u;  // group-uniform
   if (active && gl == 0) {
     bool isnew;
     const int sl = lds_insert(L, start, &isnew);
@@ -720,7 +758,8 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
     OTR_STAMP(t0);
     const int np = done ? 0 : npend;
     OTR_STAMP(t1);
-    const bool res = done || gl >= n_tgt || target_resolved(L, tslot, tpart, hTm, d0min, bound_mm, fmin, np == 0);
+    const bool res =
+        done || gl >= n_tgt || target_resolved(L, K, tslot, tpart, hTm, d0min, bound_mm, fmin, np == 0);
     done = done || Gr::mine(__ballot(!res)) == 0ull || np == 0;
     OTR_STAMP(t2);
     cyc[0] += t1 - t0;
@@ -741,7 +780,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
         sl = L.pend[k];
         lb = LabelT<PRED>::label(L.lab[sl]);
         node = L.key[sl] & ~kInq;
-        f = lb + L.hv[sl];  // < 2^32: labels, h < 2^31
+        f = K.d(lb) + L.hv[sl];  // < 2^32: labels, h < 2^31
         take = f < theta;
       }
       // at most WCAP settles per round; the rest stay pending (order only, never labels)
@@ -774,8 +813,11 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
         const int slot = k & 3;
         if (slot == 0) ++my_settled;
         const uint4 r = ld16(g.adj + 4 * (size_t)wk.x + slot);
+        // the mode's route times (DevGraph::adj_t, one block per mode)
+        const uint32_t tt =
+            timed ? g.adj_t[(size_t)__builtin_ctz(mode_bit) * g.adj_t_stride + 4 * (size_t)wk.x + slot] : 0u;
         const uint32_t e0 = PRED ? g.node_row[wk.x] : 0u;  // edge id = CSR row start + slot
-        psl = relax_one(L, H, r.x & ~kAdjMore, r.y, (int32_t)r.z, (int32_t)r.w, wk.y, e0 + slot, bound_mm,
+        psl = relax_one(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.y, e0 + slot, bound_mm,
                         mode_bit, my_relaxed, fnext);
         tail = tail || (slot == 3 && (r.x & kAdjMore));
       }
@@ -801,8 +843,9 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
             for (uint32_t e = g.node_row[wk.x] + 4; e < g.node_row[wk.x + 1]; ++e) {
               const uint4 pk = ld16(g.edge_pack + e);
               const int2 vll = g.node_ll[pk.x];
-              const int psl = relax_one(L, H, pk.x | ((pk.z & 7u) << 28), pk.y, vll.x, vll.y, wk.y, e, bound_mm,
-                                        mode_bit, my_relaxed, fnext);
+              const uint32_t tt = timed ? g.et(__builtin_ctz(mode_bit))[e] : 0u;
+              const int psl = relax_one(L, H, K, pk.x | ((pk.z & 7u) << 28), pk.y, tt, vll.x, vll.y, wk.y, e,
+                                        bound_mm, mode_bit, my_relaxed, fnext);
               if (psl >= 0) {
                 const int p = atomicAdd(&L.n_pend, 1);
                 if (p < CAP) L.pend[p] = (Idx)psl;
@@ -850,8 +893,11 @@ struct PrepArgs {
   const double* lat;
   const double* lon;
   const double* radius;
+  const int32_t* state_trace;
+  const uint8_t* mode;
   Heur* heur;     // [S]
   uint4* cprep;   // [S][OTR_KMAX]: {part(p), src(e), h(src(e)), part(1 - p)}
+  uint2* cprep_t; // [S][OTR_KMAX]: {part_t(p), part_t(1 - p)}: the same parts of the edge's route time
 };
 
 __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
@@ -865,6 +911,7 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
   const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], bound, g.h_scale);
   if (lane == 0) a.heur[s] = H;
   if (lane < K) {
+    const int md = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
     const uint32_t e = a.cand_edge[s * OTR_KMAX + lane];
     const double p = a.cand_p[s * OTR_KMAX + lane];
     const uint32_t len = g.len_mm[e];
@@ -872,6 +919,8 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
     const int2 ll = g.node_ll[tn];
     a.cprep[s * OTR_KMAX + lane] =
         make_uint4((uint32_t)part_mm(p, len), tn, H(ll.x, ll.y), (uint32_t)part_mm(1.0 - p, len));
+    const uint32_t et = g.et(md)[e];
+    a.cprep_t[s * OTR_KMAX + lane] = make_uint2((uint32_t)part_mm(p, et), (uint32_t)part_mm(1.0 - p, et));
   }
 }
 
@@ -901,10 +950,13 @@ struct RouteArgs {
   const double* radius;       // per state search radius (heuristic disk)
   const Heur* heur;           // per state (k_prep)
   const uint4* cprep;         // per state candidate (k_prep)
+  const uint2* cprep_t;       // per state candidate: route-time parts (k_prep)
+  const int32_t* bt;          // per state: the step's time bound (0.1 s), -1 none
   const uint4* rec;           // per task, 2 x uint4 (k_task_rec)
+  const unsigned long long* list_count;  // retry tiers: length of task_list, on the device
   double delta;
   double inv_beta[OTR_MODES];
-  int32_t* overflow_flag;     // per task
+  int32_t* overflow_flag;     // per task: 1/2 retry in a larger LDS table, 3 the global-memory search
   uint32_t direct_bmm;        // first tier: bounds above this go straight to the retry tiers
 };
 
@@ -913,11 +965,14 @@ struct RouteArgs {
 // first source edge → root node; mode through the trace): the search kernels read two
 // 16-B words instead of walking that chain twice (before and after the search).
 //   rec[2t]   = {s, sp, root, bound_mm}
-//   rec[2t+1] = {d0min, Kb | mode << 8 | forced << 10, mask lo, mask hi}
+//   rec[2t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16, mask lo, mask hi}
+// general: the task runs in the global-memory search (turn costs: edge-based labels; or
+// a bound whose packed labels would not fit 32 bits).
 __global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const unsigned long long* task_mask,
                            const int64_t* prev, const double* bound, const uint8_t* forced, const int32_t* cand_count,
                            const uint32_t* cand_edge, const uint32_t* edge_dst, const int32_t* state_trace,
-                           const uint8_t* mode, const uint4* cprep, uint4* rec) {
+                           const uint8_t* mode, const uint4* cprep, const int32_t* bt, uint32_t turn_modes,
+                           uint4* rec) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tasks) return;
   const int64_t s = task_state[t];
@@ -930,8 +985,12 @@ __global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const uns
     const uint32_t d0 = cprep[sp * OTR_KMAX + (__ffsll((long long)m) - 1)].w;
     d0min = d0 < d0min ? d0 : d0min;
   }
-  const uint32_t meta = (uint32_t)cand_count[s] | ((uint32_t)md << 8) | ((forced[s] ? 1u : 0u) << 10);
-  rec[2 * t] = make_uint4((uint32_t)s, (uint32_t)sp, root, (uint32_t)bound_mm_of(bound[s]));
+  const uint32_t bmm = (uint32_t)bound_mm_of(bound[s]);
+  const uint32_t sh = pack_shift(bt[s]);
+  const bool general = ((turn_modes >> md) & 1u) || !pack_fits(bmm, sh);
+  const uint32_t meta = (uint32_t)cand_count[s] | ((uint32_t)md << 8) | ((forced[s] ? 1u : 0u) << 10) | (sh << 11) |
+                        ((general ? 1u : 0u) << 16);
+  rec[2 * t] = make_uint4((uint32_t)s, (uint32_t)sp, root, bmm);
   rec[2 * t + 1] = make_uint4(d0min, meta, (uint32_t)mask, (uint32_t)(mask >> 32));
 }
 
@@ -943,17 +1002,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   using Gr = Grp<G>;
   __shared__ SearchLds<CAP, false> Ls[G];
   const int lane = Gr::gl();
-  const int64_t n_units = (a.n_tasks + G - 1) / G;
-  const int64_t w = a.task_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_units + 7) / 8);
-  if (w >= n_units) return;
+  // first tier: one unit per block over all tasks (XCD-mapped); retry tiers: a fixed
+  // grid strides over the device-side task list (its length never crosses to the host)
+  const int64_t n_tasks = a.task_list ? (int64_t)*a.list_count : a.n_tasks;
+  const int64_t n_units = (n_tasks + G - 1) / G;
+  const int64_t w0 = a.task_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_units + 7) / 8);
+  const int64_t wstep = a.task_list ? (int64_t)gridDim.x : n_units;
+  for (int64_t w = w0; w < n_units; w += wstep) {
   const int64_t tw = w * G + Gr::g();
-  const bool have = tw < a.n_tasks;
+  const bool have = tw < n_tasks;
   const int64_t task = have ? (a.task_list ? a.task_list[tw] : tw) : 0;
   OTR_STAMP(ts_in);
   // ---- search inputs (only these stay live through the search)
   bool search, fits, forced;
   uint32_t tnode = kEmpty, tpart = 0, hT = 0, d0min = 0xFFFFFFFFu, root = 0, bmm = 0, mode_bit = 1;
   int Kb;
+  Pack K;
   Heur H;
   {
     const uint4 r0 = have ? a.rec[2 * task] : make_uint4(0u, 0u, 0u, 0u);
@@ -962,7 +1026,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
     const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
     const int64_t sp = r0.y;
     Kb = (int)(r1.y & 0xFFu);
-    fits = Kb <= Gr::GL;  // targets are lanes of the group: wider steps go to a G = 1 tier
+    K.sh = (r1.y >> 11) & 31u;
+    const bool general = (r1.y >> 16) & 1u;  // re-read after the search
+    fits = Kb <= Gr::GL && !general;  // targets are lanes of the group: wider steps go to a G = 1 tier
     if (G == 2 && !a.task_list && r0.w > a.direct_bmm) fits = false;
     mode_bit = 1u << ((r1.y >> 8) & 3u);
     bmm = r0.w;
@@ -996,9 +1062,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   unsigned long long settled = 0, relaxed = 0, rounds = 0;
   OTR_STAMP(ts_set);
   search_init<CAP, false, G>(Ls);
-  bool ok = search_run<CAP, false, G>(Ls, gr, H, mode_bit, search, root, bmm, (uint32_t)(a.delta * 1000.0),
-                                      tnode, tpart, hT, d0min, Kb, &settled, &relaxed, &rounds,
-                                      counters ? counters + 16 * kShards : nullptr) && fits;
+  bool ok = search_run<CAP, false, G>(Ls, gr, H, K, mode_bit, search, root, bmm,
+                                      (uint32_t)(a.delta * 1000.0), tnode, tpart, hT, d0min, Kb, &settled, &relaxed,
+                                      &rounds, counters ? counters + 16 * kShards : nullptr) &&
+            fits;
 #ifdef OTR_FORCE_RETRY
   if (G == 2 && !a.task_list) ok = false;  // test build: every first-tier task takes the retry tiers
 #endif
@@ -1016,25 +1083,39 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
     const int64_t s = r0.x;
     const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
     const int64_t sp = r0.y;
+    const int32_t bt = a.bt[s];
+    const int md = (int)((r1.y >> 8) & 3u);
     uint32_t* trow = a.trans + a.trans_off[s];
     if (lane < Kb) {
       const uint32_t ej = a.cand_edge[s * OTR_KMAX + lane];
       const double pj = a.cand_p[s * OTR_KMAX + lane];
+      const uint32_t tpt = bt >= 0 ? a.cprep_t[s * OTR_KMAX + lane].x : 0u;
       for (unsigned long long m = mask; m; m &= m - 1) {
         const int i = __ffsll((long long)m) - 1;
         const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
         const double pi = a.cand_p[sp * OTR_KMAX + i];
-        int64_t r = -1;
-        if (forced) r = -1;
-        else if (ej == ei && pj >= pi) r = part_mm(pj - pi, gr.len_mm[ei]);
-        else if (lab >= 0) r = (int64_t)a.cprep[sp * OTR_KMAX + i].w + lab + tpart;
-        trow[(int64_t)i * Kb + lane] = (r >= 0 && r <= (int64_t)bmm) ? (uint32_t)r : kNoRoute;
+        int64_t r = -1, rt = 0;
+        if (forced) {
+          r = -1;
+        } else if (ej == ei && pj >= pi) {
+          r = part_mm(pj - pi, gr.len_mm[ei]);
+          if (bt >= 0) rt = part_mm(pj - pi, gr.et(md)[ei]);
+        } else if (lab >= 0) {
+          r = (int64_t)a.cprep[sp * OTR_KMAX + i].w + K.d((uint32_t)lab) + tpart;
+          if (bt >= 0) rt = (int64_t)a.cprep_t[sp * OTR_KMAX + i].y + K.t((uint32_t)lab) + tpt;
+        }
+        const bool valid = r >= 0 && r <= (int64_t)bmm && (bt < 0 || rt <= (int64_t)bt);
+        trow[(int64_t)i * Kb + lane] = valid ? (uint32_t)r : kNoRoute;
       }
     }
   }
-  // overflow: retry with a bigger table; a first-tier search with a long bound (> 1.9 km)
-  // that outgrew 160 slots goes straight to the 1024-slot tier (flag 2)
-  if (have && !ok && !forced && lane == 0) a.overflow_flag[task] = (G == 2 && bmm > 1900000u) ? 2 : 1;
+  // general: the global-memory search (flag 3); overflow: retry with a bigger table; a
+  // first-tier search with a long bound (> 1.9 km) that outgrew 160 slots goes straight
+  // to the 1024-slot tier (flag 2)
+  if (have && !ok && !forced && lane == 0) {
+    const bool general = (a.rec[2 * task + 1].y >> 16) & 1u;
+    a.overflow_flag[task] = general ? 3 : ((G == 2 && !a.task_list && bmm > 1900000u) ? 2 : 1);
+  }
 #ifdef OTR_STAMPS
   if (G == 2 && counters && threadIdx.x == 0) {  // task setup and transition rows, wave cycles
     OTR_STAMP(ts_out);
@@ -1073,6 +1154,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
       if (c128) atomicAdd(&counters[23 * kShards + sh], c128);
     }
   }
+  __syncthreads();
+  }
 }
 
 // ------------------------------------------------------------------------------
@@ -1086,6 +1169,8 @@ struct ViterbiArgs {
   const int64_t* prev;
   const int64_t* trans_off;
   const uint32_t* trans;   // route mm per transition (k_route), kNoRoute when invalid
+  const uint32_t* trans_tc;  // turn cost mm per transition (modes with turn costs only)
+  uint32_t turn_modes;     // bit m: mode m has turn costs
   const double* g;         // great-circle distance of the step ending at the state
   const uint8_t* mode;
   double inv2s2[OTR_MODES];
@@ -1134,6 +1219,7 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
   for (int t = blockIdx.x; t < a.n_traces; t += gridDim.x) {
     const int md = a.mode[t] < OTR_MODES ? a.mode[t] : 0;
     const double inv2s2 = a.inv2s2[md], inv_beta = a.inv_beta[md];
+    const bool turns = (a.turn_modes >> md) & 1u;  // wave-uniform
     const int64_t so = a.trace_state_off[t], eo = a.trace_state_off[t + 1];
     int64_t prev_s = -1;
     int Kp = 0;
@@ -1156,15 +1242,19 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
           // lengths (u32 mm, half the bytes of a cost); the transition cost |route - g| / beta
           // (K4) is evaluated here, with the same operations k_route used to apply.
           const uint32_t* tr = a.trans + a.trans_off[s];
+          const uint32_t* tcr = a.trans_tc + a.trans_off[s];
           const double gcd = a.g[s];
           for (int i0 = 0; i0 < Kp; i0 += 16) {
-            uint32_t tv[16];
+            uint32_t tv[16], tc[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) tv[u] = i0 + u < Kp ? tr[(int64_t)(i0 + u) * K + lane] : kNoRoute;
 #pragma unroll
+            for (int u = 0; u < 16; ++u) tc[u] = (turns && i0 + u < Kp) ? tcr[(int64_t)(i0 + u) * K + lane] : 0u;
+#pragma unroll
             for (int u = 0; u < 16; ++u) {
               if (tv[u] == kNoRoute) continue;
-              const double ti = fabs(div1000((double)tv[u]) - gcd) * inv_beta;
+              // (turn_cost + |route - gc|) / beta; 0 + x == x exactly when there are no turn costs
+              const double ti = (div1000((double)tc[u]) + fabs(div1000((double)tv[u]) - gcd)) * inv_beta;
               const double ci = s_cost[i0 + u];
               if (ci == __builtin_huge_val()) continue;
               const double c = ci + ti;
@@ -1287,26 +1377,34 @@ struct PathArgs {
   const double* radius;
   const Heur* heur;            // per state (k_prep)
   const uint4* cprep;          // per state candidate (k_prep)
+  const int32_t* bt;           // per state: the step's time bound (0.1 s), -1 none
+  uint32_t turn_modes;         // bit m: mode m has turn costs (its paths run in k_general)
+  const unsigned long long* n_steps_dev;  // number of steps, on the device
   double delta;
   int64_t* path_off;           // per state
   int32_t* path_len;           // per state; -1 = same-edge step
   uint32_t* path;              // bump-allocated edge list
   unsigned long long* cursor;
   int64_t capacity;
-  int32_t* overflow_flag;      // per step index (table overflow)
+  int32_t* overflow_flag;      // per step index: 1 table overflow, 3 global-memory search
   int32_t* cap_flag;           // global: path buffer too small
 };
 
 // G searches per wave (G = 2 for the first tier, lanes split 32/32), each a
-// single-target search from the winner's root with predecessor labels.
+// single-target search from the winner's root with predecessor labels.  First tier:
+// step_list == null, the step count is read on the device (n_steps_dev), one unit per
+// block; retry tiers: a fixed grid strides over step_list[0 .. *list_count).
 template <int CAP, int G>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 : 8, 8))) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, int64_t n_list) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 : 8, 8))) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, const unsigned long long* list_count) {
   using Gr = Grp<G>;
   __shared__ SearchLds<CAP, true> Ls[G];
   const int gl = Gr::gl();
+  const int64_t n_list = (int64_t)(step_list ? *list_count : *a.n_steps_dev);
   const int64_t n_units = (n_list + G - 1) / G;
-  const int64_t w = step_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_units + 7) / 8);
-  if (w >= n_units) return;
+  // first tier: grid = 8 x (upper bound of units / 8), XCD-mapped, one unit per block
+  const int64_t w0 = step_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x / 8);
+  const int64_t wstep = step_list ? (int64_t)gridDim.x : ((int64_t)gridDim.x + n_units);
+  for (int64_t w = w0; w < n_units; w += wstep) {
   const int64_t iw = w * G + Gr::g();
   const bool have = iw < n_list;
   const int64_t k = have ? (step_list ? step_list[iw] : iw) : 0;
@@ -1314,16 +1412,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
   const int64_t sp = have ? a.prev[s] : 0;
   bool active = false;
   uint32_t S = 0, T = kEmpty, bmm = 0, tpart = 0, hT = 0, d0 = 0, mode_bit = 1;
+  int mode = 0;
+  Pack K;
+  K.sh = 0;
   Heur H{};
   if (have) {
     const int wi = a.winner[sp], wj = a.winner[s];
     const uint32_t ei = a.cand_edge[sp * OTR_KMAX + wi], ej = a.cand_edge[s * OTR_KMAX + wj];
     const double pi = a.cand_p[sp * OTR_KMAX + wi], pj = a.cand_p[s * OTR_KMAX + wj];
+    mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+    bmm = (uint32_t)bound_mm_of(a.bound[s]);
+    K.sh = pack_shift(a.bt[s]);
     if (ej == ei && pj >= pi) {
       if (gl == 0) a.path_len[s] = -1;
+    } else if (((a.turn_modes >> mode) & 1u) || !pack_fits(bmm, K.sh)) {
+      if (gl == 0) a.overflow_flag[k] = 3;  // edge-based / 64-bit labels: k_general
     } else {
       active = true;
-      const int mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
       mode_bit = 1u << mode;
       const uint4 cs = a.cprep[sp * OTR_KMAX + wi], ct = a.cprep[s * OTR_KMAX + wj];
       d0 = cs.w;
@@ -1332,12 +1437,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
       H = a.heur[s];
       hT = ct.z;
       tpart = ct.x;
-      bmm = (uint32_t)bound_mm_of(a.bound[s]);
     }
   }
   search_init<CAP, true, G>(Ls);
-  const bool ok = search_run<CAP, true, G>(Ls, gr, H, mode_bit, active, S, bmm, (uint32_t)(a.delta * 1000.0),
-                                           gl == 0 ? T : kEmpty, tpart, hT, d0, 1, nullptr, nullptr, nullptr);
+  const bool ok = search_run<CAP, true, G>(Ls, gr, H, K, mode_bit, active, S, bmm,
+                                           (uint32_t)(a.delta * 1000.0), gl == 0 ? T : kEmpty, tpart, hT, d0, 1,
+                                           nullptr, nullptr, nullptr);
   SearchLds<CAP, true>& L = Ls[Gr::g()];
   if (active && !ok) {
     if (gl == 0) a.overflow_flag[k] = 1;
@@ -1362,7 +1467,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
   n = __shfl(n, Gr::g() * Gr::GL);
   __syncthreads();
   if (active && n < 0) {
-    if (gl == 0) a.overflow_flag[k] = 2;
+    if (gl == 0) a.overflow_flag[k] = 1;
     active = false;
   }
   // bump allocation in one of 64 regions (a single cursor serialises ~1M returning
@@ -1376,12 +1481,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
     if (gl == 0) *a.cap_flag = 1;
     active = false;
   }
-  if (!active) return;
-  off += (int64_t)shard * region;
-  for (int q = gl; q < n; q += Gr::GL) a.path[off + q] = lp[n - 1 - q];
-  if (gl == 0) {
-    a.path_off[s] = off;
-    a.path_len[s] = n;
+  if (active) {
+    off += (int64_t)shard * region;
+    for (int q = gl; q < n; q += Gr::GL) a.path[off + q] = lp[n - 1 - q];
+    if (gl == 0) {
+      a.path_off[s] = off;
+      a.path_len[s] = n;
+    }
+  }
+  __syncthreads();
   }
 }
 
@@ -1429,6 +1537,7 @@ struct SegArgs {
   int32_t* shape_used;  int32_t* stats;  double* stats_len;
   double threshold;
   uint32_t report_levels, transition_levels;
+  double queue_kph[OTR_MODES];  // queue_length speed threshold per mode
 };
 
 template <class T>
@@ -1459,6 +1568,7 @@ __global__ __launch_bounds__(64) void k_segments(DevGraph g, SegArgs a, unsigned
   const int64_t so = a.trace_state_off[t], eo = a.trace_state_off[t + 1];
   const int64_t lo_probe = a.b.trace_off[t], n_probe = a.b.trace_off[t + 1] - lo_probe;
   const int64_t co = a.cap_off[t];
+  const double qkph = a.queue_kph[a.b.mode[t] < OTR_MODES ? a.b.mode[t] : 0];
   int64_t* act = a.act + so;
   int64_t* pos = a.pos + so;
   int64_t* ent = a.ent + so;
@@ -1688,10 +1798,29 @@ __global__ __launch_bounds__(64) void k_segments(DevGraph g, SegArgs a, unsigned
         if (!is_last) et = time_at(s1);
         a.seg_id[o] = OTR_NO_ID_U64;
       }
+      // queue_length (README.md:283,295; oracle queue_at): the piece between the states
+      // around the exit s1 and the slow pieces right before it, clipped to [s0, s1]
+      int32_t queue = 0;
+      if (et != -1.0) {
+        auto tm_of = [&](int32_t m) { return (double)a.b.time[a.state_probe[act[m]]]; };
+        auto slow = [&](int32_t m) { return (double)(pos[m + 1] - pos[m]) * 0.0036 < qkph * (tm_of(m + 1) - tm_of(m)); };
+        int32_t lo_i = sa + 1, hi_i = sb + 1;  // first ordinal m in [sa+1, sb] with pos[m] >= s1
+        while (lo_i < hi_i) {
+          const int32_t mid = (lo_i + hi_i) >> 1;
+          if (pos[mid] >= s1) hi_i = mid;
+          else lo_i = mid + 1;
+        }
+        int32_t kq = (lo_i > sb ? sb : lo_i) - 1;
+        if (slow(kq)) {
+          while (kq > sa && pos[kq] > s0 && slow(kq - 1)) --kq;
+          const int64_t q0 = pos[kq] > s0 ? pos[kq] : s0;
+          queue = (int32_t)((s1 - q0 + 500) / 1000);
+        }
+      }
       a.seg_start[o] = st;
       a.seg_end[o] = et;
       a.seg_length[o] = length;
-      a.seg_queue[o] = 0;
+      a.seg_queue[o] = queue;
       a.seg_internal[o] = (key == OTR_NO_SEGMENT && internal) ? 1 : 0;
       a.seg_index[o] = key;
       a.seg_bshape[o] = shape_at(s0);

@@ -33,11 +33,14 @@ enum Override {
   OV_MAX_SEARCH_RADIUS,
   OV_GPS_ACCURACY,
   OV_MAX_CANDIDATES,
+  OV_TIME_FACTOR,
+  OV_TURN_PENALTY,
   OV_COUNT
 };
 static const char* const kOverrideNames[OV_COUNT] = {
     "sigma_z",         "beta",          "max_route_distance_factor", "breakage_distance", "interpolation_distance",
-    "search_radius",   "max_search_radius", "gps_accuracy",          "max_candidates"};
+    "search_radius",   "max_search_radius", "gps_accuracy",          "max_candidates",
+    "max_route_time_factor", "turn_penalty_factor"};
 
 struct Request {
   int code = 0;  // 0 = valid; else 400 (request) or 500 (what Match() would raise on)

@@ -28,7 +28,8 @@ bool service_timing() {
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-double g_t_soa = 0, g_t_run = 0, g_t_fmt = 0;
+// per calling thread: concurrent process() calls (coalescer off) never share them
+thread_local double g_t_soa = 0, g_t_run = 0, g_t_fmt = 0;
 
 int host_threads() {
   static const int n = [] {
@@ -93,7 +94,8 @@ otr::ModeParams group_params(const otrreq::Request& r) {
   otr::MatchParams& p = mp.m[r.mode < OTR_MODES ? r.mode : 0];
   double* dst[otrreq::OV_COUNT] = {&p.sigma_z,          &p.beta,          &p.max_route_distance_factor,
                                    &p.breakage_distance, &p.interpolation_distance, &p.search_radius,
-                                   &p.max_search_radius, &p.gps_accuracy, nullptr};
+                                   &p.max_search_radius, &p.gps_accuracy, nullptr,
+                                   &p.max_route_time_factor, &p.turn_penalty_factor};
   for (int o = 0; o < otrreq::OV_COUNT; ++o) {
     if (!(r.ov_mask & (1u << o))) continue;
     if (o == otrreq::OV_MAX_CANDIDATES) p.kmax = (int32_t)(int64_t)r.ov[o];
@@ -214,6 +216,14 @@ void process(otr::Matcher& m, const std::vector<Item*>& items) {
     } else {
       otrreq::Scanner sc(it->body, it->len);
       sc.request(&r, !it->report);
+    }
+    if (r.code == 0 && r.ov_mask && configured) {
+      // match_options values the engine cannot honour are refused by name, never ignored
+      const otr::ModeParams mp = group_params(r);
+      if (const char* bad = otr::check_params(mp.m[r.mode < OTR_MODES ? r.mode : 0])) {
+        r.code = 400;
+        r.err = std::string("match_options: ") + bad;
+      }
     }
     if (r.code) {
       error_body(it, it->report ? r.code : OTR_MATCH_ERROR, r.err);

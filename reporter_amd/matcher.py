@@ -18,14 +18,31 @@ P = ctypes.POINTER
 MODES = {'auto': 0, 'bicycle': 1, 'pedestrian': 2}
 
 
-def default_config(graph_path, device=0, **meili_default):
-    """Valhalla-style config dict (meili values Dockerfile:14-17,42-49)."""
+OTR_KEYS = ('speed_kph', 'queue_kph', 'delta')  # engine keys, not meili's
+
+
+def default_config(graph_path, device=0, **options):
+    """Valhalla-style config dict of the reference deployment: valhalla_build_config's meili
+    section (per-mode turn_penalty_factor auto 200 / bicycle 140 / pedestrian 100) with the
+    Dockerfile's overrides (sigma_z 4.07, beta 3, max_route_distance_factor 5,
+    max_route_time_factor 2; Dockerfile:14-17,42-49).  `options` apply to every mode, as a
+    request's match_options override the configured values (generate_test_trace.py:44-52
+    sends turn_penalty_factor 0, for example); speed_kph / queue_kph go to the otr section."""
     d = {'sigma_z': 4.07, 'beta': 3, 'max_route_distance_factor': 5, 'max_route_time_factor': 2,
          'breakage_distance': 2000, 'interpolation_distance': 10, 'search_radius': 50,
          'max_search_radius': 100, 'gps_accuracy': 5.0, 'turn_penalty_factor': 0, 'max_candidates': 32}
-    d.update(meili_default)
-    return {'meili': {'default': d, 'auto': {}, 'bicycle': {}, 'pedestrian': {}},
-            'otr': {'graph': os.path.abspath(graph_path), 'device': device}}
+    modes = {'auto': {'turn_penalty_factor': 200, 'search_radius': 50},
+             'bicycle': {'turn_penalty_factor': 140},
+             'pedestrian': {'turn_penalty_factor': 100, 'search_radius': 50}}
+    otr = {'graph': os.path.abspath(graph_path), 'device': device}
+    for k, v in options.items():
+        if k in OTR_KEYS:
+            otr[k] = v
+        else:
+            d[k] = v
+            for m in modes.values():
+                m[k] = v
+    return {'meili': dict(default=d, **modes), 'otr': otr}
 
 
 def configure(config):

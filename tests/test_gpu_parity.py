@@ -32,9 +32,18 @@ def matcher():
     return M.Matcher()
 
 
+# 'deployed': the reference deployment's config (Dockerfile meili overrides, per-mode turn
+# penalties auto 200 / bicycle 140 / pedestrian 100, max_route_time_factor 2) — what a
+# Batch.java request (mode + levels only, Batch.java:56-65) is matched with;
+# 'gtt': the match_options generate_test_trace.py:44-52 sends (turn_penalty_factor 0)
+CONFIGS = {'deployed': {}, 'gtt': {'turn_penalty_factor': 0}}
+
+
+@pytest.mark.parametrize('cfg', list(CONFIGS))
 @pytest.mark.parametrize('name', list(CASES))
-def test_batch_parity(name, graph_dir, matcher):
+def test_batch_parity(name, cfg, graph_dir, matcher):
     g, nt, npnt, sr, sig, seed, fb, fp, acc, over = CASES[name]
+    over = dict(over, **CONFIGS[cfg])
     path = gen.graph_path(g, graph_dir)
     M.configure(M.default_config(path, **over))
     traces = gen.make_traces(path, nt, npnt, sr, sig, seed, fb, fp, acc)
