@@ -7,10 +7,22 @@ One step = one pass of the hot path over one batch resident in HBM:
   histogram, and for N>1 the RCCL reduce-scatter of that histogram over xGMI.
 
 Workload (N=1): SURVEY.md §8d config C2 — synthetic metro graph (1024x1024 street
-grid, ~1M nodes, ~3.6M directed edges, seed 2) and 10,000 traces x 100 probes at
-15 s sampling with sigma = 10 m noise (seed 2) = 1M probes.  N>1 (config C3 layout):
-N x 10,000 traces generated with one seed, sharded by int(sha1(uuid)[:3], 16) % N
-(simple_reporter.py:116), graph replicated per GPU, weak scaling.
+grid, ~1M nodes, ~3.5M directed edges, seed 2) and 10,000 traces x 100 probes at
+15 s sampling with sigma = 10 m noise (seed 2) = 1M probes, matched with the match_options
+generate_test_trace.py:44-52 sends (turn_penalty_factor 0) under the deployed
+max_route_time_factor 2 (Dockerfile:17).  N>1 (config C3 layout): N x 10,000 traces
+generated with one seed, sharded by int(sha1(uuid)[:3], 16) % N (simple_reporter.py:116),
+graph replicated per GPU, weak scaling.
+
+Besides the timed device-resident line the bench reports, for rank 0 at N=1:
+  * roofline: the dominant route-search kernel of the workload (largest device time):
+    SURVEY §8(d) algorithmic bytes (K3: 24 B per settled node + 16 B per relaxed edge;
+    K4: 8 B per transition entry) ÷ its HIP-event time on the matcher's stream;
+  * parity: the oracle sample matched on the CPU compared bit-exactly with the GPU
+    output for the same traces of this batch (the line fails on a mismatch);
+  * cpu_baseline: that oracle sample's rate on the host cores the process may use;
+  * end_to_end: the SoA input in pinned host memory → H2D → match → reports and the
+    histogram back on the host (SURVEY §8(d)'s drop-in definition; PCIe included).
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
   N>1:   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -28,25 +40,38 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-ROUTE_KERNEL = 'k_route<160, 2>'  # first-tier search kernel (rocprofv3 name)
-# HBM bytes per ROUTE_KERNEL launch from the FETCH_SIZE / WRITE_SIZE passes of
-# tools/profile_gpu.sh (separate --pmc runs of this same command; tools/pmc_summary.py)
-PMC_SUMMARY = os.path.join(ROOT, 'profiles', 'r01_v31_pmc.json')
 T_BEGIN = 1483228800
+# HBM bytes per launch of the dominant kernel from separate FETCH_SIZE / WRITE_SIZE
+# --pmc passes of this command (tools/profile_gpu.sh, tools/pmc_summary.py), when the
+# committed summary holds the kernel
+PMC_SUMMARY = os.environ.get('OTR_PMC_SUMMARY', os.path.join(ROOT, 'profiles', 'r02_pmc.json'))
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def route_bytes(c):
-    """Algorithmic HBM bytes of one first-tier k_route launch, from the
-    device work counters: 64 B per task (task record, step metadata, root lookup),
-    32 B per settled node (its adjacency record), 16 B per source candidate
-    (edge, fraction, length), 20 B per target read (edge, fraction, src, length),
-    4 B per transition entry written (route length in mm, u32; v26 — 8 B fp64 costs before)."""
-    tasks, settled, trans, targets, sources = c[5], c[3], c[6], c[11], c[12]
-    return 64 * tasks + 32 * settled + 16 * sources + 20 * targets + 4 * trans
+def kernel_name(code):
+    """rocprofv3 name of a route kernel (otr_batch_result.route_tier_code)."""
+    if code < 0:
+        return 'k_general'
+    cap, g = code // 10, code % 10
+    return 'k_route<%d, %d, %s>' % (cap, g, 'false' if code == 1602 or code == 2561 else 'true')
+
+
+def route_bytes(work):
+    """SURVEY.md §8(d) algorithmic bytes of one route-search launch: K3 per source search
+    16 B per settled node (row pointer + coordinates) + 8 B per settled node (its label)
+    + 16 B per relaxed edge (dst, length, access, osmlr); K4 8 B per transition entry."""
+    searches, settled, relaxed, trans = work
+    return 24 * settled + 16 * relaxed + 8 * trans
+
+
+def usable_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def main():
@@ -54,16 +79,19 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--traces-per-gpu', type=int, default=10000)
-    ap.add_argument('--cpu-traces', type=int, default=6000, help='bounded oracle sample (0 = skip)')
-    ap.add_argument('--cpu-threads', type=int, default=16)
+    ap.add_argument('--traces-per-gpu', type=int, default=None,
+                    help='default: 10,000 (c2, c5mix), 20,000 (c4: BASELINE C4); c3: every owned uuid')
+    ap.add_argument('--cpu-traces', type=int, default=None,
+                    help='bounded oracle sample for the CPU baseline and the parity check (0 = skip)')
     ap.add_argument('--delta', type=float, default=None, help='routing round width (perf knob, metres)')
     ap.add_argument('--streams', type=int, default=2,
                     help='matchers (one HIP stream + host thread each) sharing the batch')
-    ap.add_argument('--workload', choices=['c2', 'c4', 'c5mix'], default='c2',
-                    help='c2 (default, the headline): 100 probes @15 s, sigma 10 m; c4: 60 probes @60 s, '
-                         'sigma 50 m, accuracy 50 m, search radius 200 m; c5mix: C2 with the C5 mode mix '
+    ap.add_argument('--workload', choices=['c2', 'c3', 'c4', 'c5mix'], default='c2',
+                    help='c2 (default, the headline): 100 probes @15 s, sigma 10 m; c3: the C3 shard of '
+                         '1M veh%%07d uuids x 100 probes this GPU owns; c4: 60 probes @60 s, sigma 50 m, '
+                         'accuracy 50 m, search radius 200 m; c5mix: C2 with the C5 mode mix '
                          '(60%% auto / 25%% bicycle / 15%% pedestrian) on the metro graph')
+    ap.add_argument('--e2e-steps', type=int, default=3, help='host-to-host drop-in steps (0 = skip)')
     ap.add_argument('--tiles', type=int, default=0,
                     help='privacy > 0: the step also runs the device tile stage (K9 rows, K10 sort + cull, '
                          'simple_reporter.py:176-239) on each matcher (not part of the headline config)')
@@ -106,26 +134,43 @@ def main():
     barrier()
     gpath = gen.graph_path('metro', gdir)
 
-    # traces: all ranks generate the same global set, keep their uuid-hash shard
-    n_global = args.traces_per_gpu * world
-    t0 = time.time()
     # match_options as generate_test_trace.py:44-52 sends them (turn_penalty_factor 0,
     # gps_accuracy = the 95th percentile of the noise); max_route_time_factor stays the
     # deployed 2 (Dockerfile:17)
     gtt = {'turn_penalty_factor': 0, 'beta': 3, 'sigma_z': 4.07, 'breakage_distance': 2000}
-    W = {'c2': dict(points=100, rate=15, sigma=10.0, seed=2, bike=0.0, ped=0.0, acc=None,
+    W = {'c2': dict(points=100, rate=15, sigma=10.0, seed=2, bike=0.0, ped=0.0, acc=None, traces=10000,
                     meili=dict(gtt, search_radius=50, gps_accuracy=16.45)),
-         'c4': dict(points=60, rate=60, sigma=50.0, seed=4, bike=0.0, ped=0.0, acc=50.0,
+         'c3': dict(points=100, rate=15, sigma=10.0, seed=3, bike=0.0, ped=0.0, acc=None, traces=None,
+                    meili=dict(gtt, search_radius=50, gps_accuracy=16.45)),
+         'c4': dict(points=60, rate=60, sigma=50.0, seed=4, bike=0.0, ped=0.0, acc=50.0, traces=20000,
                     meili=dict(gtt, search_radius=200, max_search_radius=200, gps_accuracy=82.24)),
-         'c5mix': dict(points=100, rate=15, sigma=10.0, seed=5, bike=0.25, ped=0.15, acc=None,
+         'c5mix': dict(points=100, rate=15, sigma=10.0, seed=5, bike=0.25, ped=0.15, acc=None, traces=10000,
                        meili=dict(gtt, search_radius=50, gps_accuracy=16.45))}[args.workload]
-    allt = gen.make_traces(gpath, n_global, W['points'], W['rate'], W['sigma'], W['seed'], W['bike'], W['ped'],
-                           W['acc'], t_begin=T_BEGIN, t_spread=1800)
-    if world > 1:
-        shard = np.array([int(hashlib.sha1(u.encode()).hexdigest()[:3], 16) % world for u in allt.uuids])
-        mine = allt.subset(np.flatnonzero(shard == rank))
+
+    t0 = time.time()
+    if args.workload == 'c3':
+        # C3: 1,000,000 uuids "veh%07d" x 100 probes, sharded by
+        # int(sha1(uuid)[:3], 16) % N (simple_reporter.py:116); each rank generates only the
+        # uuids it owns (a uuid's trace is seeded by its number, so shards are independent).
+        # --traces-per-gpu bounds the uuids per rank (a one-GPU rehearsal).
+        n_uuid = 1000000
+        owner = np.array([int(hashlib.sha1(('veh%07d' % u).encode()).hexdigest()[:3], 16) % world
+                          for u in range(n_uuid)])
+        mine_ids = np.flatnonzero(owner == rank)
+        if args.traces_per_gpu:
+            mine_ids = mine_ids[:args.traces_per_gpu]
+        mine = gen.make_traces_ids(gpath, mine_ids, W['points'], W['rate'], W['sigma'], W['seed'],
+                                   t_begin=T_BEGIN, t_spread=1800)
     else:
-        mine = allt
+        n_per = args.traces_per_gpu or W['traces']
+        n_global = n_per * world
+        allt = gen.make_traces(gpath, n_global, W['points'], W['rate'], W['sigma'], W['seed'], W['bike'],
+                               W['ped'], W['acc'], t_begin=T_BEGIN, t_spread=1800)
+        if world > 1:
+            shard = np.array([int(hashlib.sha1(u.encode()).hexdigest()[:3], 16) % world for u in allt.uuids])
+            mine = allt.subset(np.flatnonzero(shard == rank))
+        else:
+            mine = allt
     log('rank %d: %d traces, %d probes (gen %.1fs)' % (rank, mine.n_traces, mine.n_probes, time.time() - t0))
 
     cfg = M.default_config(gpath, device=local, **W['meili'])
@@ -142,7 +187,7 @@ def main():
     parts = [mine.subset(np.arange(cuts[k], cuts[k + 1])) for k in range(ns)]
     matchers = [M.Matcher() for _ in range(ns)]
     dev = torch.device('cuda', local)
-    hours = 3  # traces start within 30 min of T_BEGIN and last 25 min
+    hours = 3  # traces start within 30 min of T_BEGIN and last <= 100 min
     hist_len = hours * n_segments * _lib.HIST_BINS
     hist_len += (-hist_len) % world
     keep, darrs, hists = [], [], []
@@ -168,7 +213,8 @@ def main():
                                     hist_hours=hours, hist_base_time=T_BEGIN, copy_out=False, timing=True,
                                     tile_rows=args.tiles > 0)
         if r.status != 0:
-            raise RuntimeError('batch status %d (%d overflow tasks)' % (r.status, r.n_overflow_traces))
+            raise RuntimeError('batch status %d (%d traces beyond every search tier)' % (r.status,
+                                                                                          r.n_overflow_traces))
         if args.tiles > 0:
             tc = time.perf_counter()
             kept = sr.cull_rows(matchers[k], None, args.tiles, device_ptr=r.d_rows, n=r.n_rows)
@@ -192,11 +238,9 @@ def main():
     torch.cuda.synchronize()
     barrier()
     t_start = time.perf_counter()
-    route_ms, results = [], []
+    results = []
     for _ in range(args.steps):
-        rs = step()
-        route_ms.extend(r.kernel_ms[_lib.STAGES.index('route')] for r in rs)
-        results.append(rs)
+        results.append(step())
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
@@ -211,33 +255,100 @@ def main():
     total_probes = float(probes.item())
     value = total_probes * args.steps / elapsed
 
+    # ---- per-kernel work and device time over the timed steps (every stream, every step)
     rs = results[-1]
     counters = [sum(int(r.counters[k]) for r in rs) for k in range(len(rs[0].counters))]
     stage_ms = {s: round(float(np.mean([r.kernel_ms[i] for r in rs])), 3) for i, s in enumerate(_lib.STAGES)
                 if rs[0].kernel_ms[i] > 0}
-    route_avg_ms = float(np.mean(route_ms))
-    rbytes = route_bytes(counters) / ns  # per launch (each stream launches once per step)
-    achieved = rbytes / (route_avg_ms * 1e-3) / 1e9
-
-    traffic = None
+    tiers = {}
+    for step_rs in results:
+        for r in step_rs:
+            for t in range(8):
+                code = int(r.route_tier_code[t])
+                if code == 0:
+                    continue
+                d = tiers.setdefault(t, {'code': code, 'launches': 0, 'ms': 0.0, 'work': np.zeros(4, np.int64)})
+                d['launches'] += 1
+                d['ms'] += float(r.route_tier_ms[t])
+                d['work'] += np.array([int(x) for x in r.route_tier_work[t]], np.int64)
+    dom_t = max(tiers, key=lambda t: tiers[t]['ms'])
+    dom = tiers[dom_t]
+    launch_ms = dom['ms'] / dom['launches']
+    dom_bytes = route_bytes(dom['work'] / dom['launches'])
+    achieved = dom_bytes / (launch_ms * 1e-3) / 1e9
+    tier_table = {kernel_name(d['code']): {'ms_per_launch': round(d['ms'] / d['launches'], 3),
+                                          'searches_per_launch': int(d['work'][0] // d['launches']),
+                                          'settled_per_launch': int(d['work'][1] // d['launches']),
+                                          'relaxed_per_launch': int(d['work'][2] // d['launches']),
+                                          'transitions_per_launch': int(d['work'][3] // d['launches']),
+                                          'gbs': round(route_bytes(d['work'] / d['launches']) /
+                                                       (max(d['ms'], 1e-9) / d['launches'] * 1e-3) / 1e9, 1)}
+                  for t, d in sorted(tiers.items())}
+    traffic, traffic_src = None, None
     if os.path.exists(PMC_SUMMARY):
-        k = json.load(open(PMC_SUMMARY))['kernels'].get(ROUTE_KERNEL, {})
+        k = json.load(open(PMC_SUMMARY)).get('kernels', {}).get(kernel_name(dom['code']), {})
         if 'fetch_bytes_per_launch' in k and 'write_bytes_per_launch' in k:
             traffic = int(k['fetch_bytes_per_launch'] + k['write_bytes_per_launch'])
+            traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
 
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_traces > 0:
+    # ---- rank 0, N = 1: oracle sample (CPU baseline) and its bit-exact comparison
+    cpu, parity = None, None
+    n_cpu = args.cpu_traces if args.cpu_traces is not None else {'c2': 6000, 'c5mix': 6000, 'c4': 600,
+                                                                 'c3': 6000}[args.workload]
+    if rank == 0 and world == 1 and n_cpu > 0:
         from oracle import pyoracle as po
+        from oracle.compare import compare, subset
         g = po.Graph(gpath)
-        sample = mine.subset(np.arange(min(args.cpu_traces, mine.n_traces)))
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        idx = np.arange(min(n_cpu, mine.n_traces))
+        sample = mine.subset(idx)
+        threads = usable_cores()
         tc = time.perf_counter()
-        po.match_batch(g, sample, po.params(**{k: float(v) for k, v in W['meili'].items()}), threads=threads)
+        want = po.match_batch(g, sample, po.params(**W['meili']), threads=threads)
         dt = time.perf_counter() - tc
         cpu = {'value': round(sample.n_probes / dt, 1), 'unit': 'probes/s', 'cores': threads, 'kind': 'port',
                'sample': '%d traces x %d probes of the same %s workload through oracle/liboracle.so '
-                         '(scalar C restatement, %d pthreads, %.1f s)' % (sample.n_traces, W['points'],
-                                                                          args.workload.upper(), threads, dt)}
+                         '(scalar C restatement, %d pthreads = the cores this process may use; os.cpu_count() '
+                         '= %d; %.1f s)' % (sample.n_traces, W['points'], args.workload.upper(), threads,
+                                            os.cpu_count() or 0, dt)}
+        # the GPU output of the same traces: this batch (copy-out run, untimed), sliced
+        got_full = _lib.result_to_numpy(M.Matcher().match_batch(mine, copy_out=True))
+        errors, stats = compare(subset(got_full, idx, mine.offsets), want)
+        parity = {'traces': int(sample.n_traces), 'probes': int(sample.n_probes), 'ok': not errors,
+                  'segments': stats.get('n_seg'), 'reports': stats.get('n_rep'), 'errors': errors[:3],
+                  'floats_bitexact': all(v for k, v in stats.items() if k.endswith('_bitexact'))}
+
+    # ---- rank 0, N = 1: the drop-in path host → host (PCIe included; never `value`)
+    e2e = None
+    if rank == 0 and world == 1 and args.e2e_steps > 0:
+        m = matchers[0]
+        pin = {}
+        for name, arr in (('offsets', mine.offsets), ('lat', mine.lat), ('lon', mine.lon), ('time', mine.time),
+                          ('mode', mine.mode)):
+            pin[name] = torch.from_numpy(np.ascontiguousarray(arr)).pin_memory()
+        if mine.accuracy is not None:
+            pin['accuracy'] = torch.from_numpy(np.ascontiguousarray(mine.accuracy, np.float32)).pin_memory()
+        hist_host = torch.zeros(hist_len, dtype=torch.int32).pin_memory()
+        harr = {'trace_offsets': pin['offsets'].data_ptr(), 'lat': pin['lat'].data_ptr(),
+                'lon': pin['lon'].data_ptr(), 'time': pin['time'].data_ptr(), 'mode': pin['mode'].data_ptr(),
+                'accuracy': pin['accuracy'].data_ptr() if 'accuracy' in pin else None}
+
+        def e2e_step():
+            r = m.match_batch(mine, host_arrays=harr, hist_device=hists[0].data_ptr(), hist_hours=hours,
+                              hist_base_time=T_BEGIN, copy_out=False, copy_reports=True)
+            hist_host.copy_(hists[0], non_blocking=False)
+            return r
+
+        e2e_step()
+        torch.cuda.synchronize()
+        te0 = time.perf_counter()
+        for _ in range(args.e2e_steps):
+            r = e2e_step()
+        torch.cuda.synchronize()
+        tel = time.perf_counter() - te0
+        e2e = {'value': round(mine.n_probes * args.e2e_steps / tel, 1), 'unit': 'probes/s',
+               'ms_per_step': round(1e3 * tel / args.e2e_steps, 3), 'streams': 1, 'reports': int(r.n_rep),
+               'what': 'SoA input in pinned host memory -> H2D -> match -> reports (dense, host) and the '
+                       '[hour][segment][speed] histogram (host); SURVEY 8(d) drop-in definition'}
 
     if rank == 0:
         line = {
@@ -254,36 +365,45 @@ def main():
             'dtype': 'f64',
             'data': 'synthetic',
             'config': {'workload': '%s: metro street grid (%d nodes, %d directed edges, %d OSMLR segments), '
-                                   '%d traces x %d probes per GPU @%d s, sigma %g m%s' % (
-                                       args.workload.upper(), n_nodes, n_edges, n_segments, args.traces_per_gpu,
+                                   '%d traces x %d probes per GPU @%d s, sigma %g m%s; generate_test_trace '
+                                   'match_options, max_route_time_factor 2' % (
+                                       args.workload.upper(), n_nodes, n_edges, n_segments, mine.n_traces,
                                        W['points'], W['rate'], W['sigma'],
-                                       {'c2': '', 'c4': ', accuracy 50 m, search radius 200 m',
-                                        'c5mix': ', modes 60% auto / 25% bicycle / 15% pedestrian'}[args.workload]),
+                                       {'c2': '', 'c3': ', C3 uuid shard (1M veh%07d uuids, sha1[:3] % N)',
+                                        'c4': ', accuracy 50 m, search radius 200 m',
+                                        'c5mix': ', modes 60% auto / 25% bicycle / 15% pedestrian'}[
+                                           args.workload]),
                        'probes_per_step': int(total_probes),
-                       'parallelism': ('uuid-sharded dp%d + ' + ('RCCL reduce-scatter' if backend == 'nccl' else 'gloo all-reduce (rehearsal)') + ' of [hour][segment][speed] histogram')
-                                      % world if world > 1 else 'single GPU',
+                       'parallelism': ('uuid-sharded dp%d + ' + ('RCCL reduce-scatter' if backend == 'nccl'
+                                                                 else 'gloo all-reduce (rehearsal)') +
+                                       ' of [hour][segment][speed] histogram') % world if world > 1 else
+                       'single GPU',
                        'streams': ns,
                        'stage_ms_per_stream': stage_ms,
+                       'route_kernels': tier_table,
                        'tile_stage': ({'privacy': args.tiles, 'rows': tile_stats[-1][0], 'kept': tile_stats[-1][1],
                                        'ms': round(1e3 * tile_stats[-1][2], 3)} if tile_stats else None),
                        'work': {'states': int(sum(r.n_states for r in rs)), 'grid_cells': int(counters[0]),
                                 'shape_segments_tested': int(counters[1]), 'candidates': int(counters[2]),
                                 'output_segments': int(counters[7])}},
-            'roofline': {'kernel': ROUTE_KERNEL + ' (K3 bounded one-to-many searches, 2 per wave + K4 transition)',
+            'roofline': {'kernel': kernel_name(dom['code']) + ' (dominant route-search kernel of this workload)',
                          'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': traffic,
-                         'traffic_source': os.path.relpath(PMC_SUMMARY, ROOT) if traffic else None,
-                         'launch_ms': round(route_avg_ms, 3), 'algorithmic_bytes': int(rbytes),
-                         'settled_nodes': int(counters[3]), 'relaxed_edges': int(counters[4]),
-                         'tasks': int(counters[5]), 'transition_entries': int(counters[6]),
-                         'source_candidates': int(counters[12]),
-                         'retry_settled_nodes': int(counters[9]), 'search_rounds': int(counters[13]),
-                         'table_keys': int(counters[14]),
-                         'tasks_keys_gt': {'64': int(counters[22]), '96': int(counters[15]), '128': int(counters[23])},
-                         'phase_cycles': [int(x) for x in counters[16:22]] if ('stamps' in _lib.LIB_PATH or 'cstamp' in _lib.LIB_PATH) else None},
+                         'traffic_source': traffic_src, 'launch_ms': round(launch_ms, 3),
+                         'algorithmic_bytes': int(dom_bytes),
+                         'bytes_formula': 'SURVEY 8(d): 24 B x settled + 16 B x relaxed + 8 B x transitions',
+                         'searches': int(dom['work'][0] // dom['launches']),
+                         'settled_nodes': int(dom['work'][1] // dom['launches']),
+                         'relaxed_edges': int(dom['work'][2] // dom['launches']),
+                         'transition_entries': int(dom['work'][3] // dom['launches']),
+                         'search_rounds': int(counters[13]), 'table_keys': int(counters[14])},
             'cpu_baseline': cpu,
+            'parity': parity,
+            'end_to_end': e2e,
         }
         print(json.dumps(line), flush=True)
+        if parity is not None and not parity['ok']:
+            raise SystemExit('bench: GPU output differs from the oracle sample: %s' % parity['errors'])
     if world > 1:
         dist.destroy_process_group()
 

@@ -190,6 +190,14 @@ typedef struct otr_batch_result {
                                   OTR_MATCH_ERROR when its search outgrew the largest LDS table */
   otr_tile_row* d_rows;        /* OTR_BATCH_TILE_ROWS: n_rows tile rows in HBM (matcher-owned),
                                   trace by trace in report order */
+  /* per route-search kernel: slot 0 the first tier (k_route<160,2>), 1..5 the LDS retry
+   * tiers in order, 6 / 7 the global-memory search (32K / 1M-state slabs).  code: CAP*10+G
+   * of an LDS tier, -1 / -2 the global tiers, 0 unused.  work: searches, settled nodes
+   * (expanded states), relaxed edges, transition entries written.  ms (OTR_BATCH_TIMING):
+   * HIP-event time of the kernel on the matcher's stream. */
+  int32_t route_tier_code[8];
+  float route_tier_ms[8];
+  uint64_t route_tier_work[8][4];
 } otr_batch_result;
 
 int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result* out);
@@ -278,6 +286,21 @@ typedef struct otr_ingest_result {
  * passed straight to otr_match_batch after setting its levels, threshold and flags. */
 int otr_ingest(otr_matcher* m, const char* text, int64_t len, int32_t memory, const otr_ingest_format* fmt,
                otr_ingest_result* out);
+
+/* report() (reporter_service.py:79-179) over n segment lists at once, evaluated by the
+ * device code of the segment scan K7 (otr_report.h compiled for gfx950, one thread per
+ * list) — what pins the device tail against the reference's own report() outputs.  Host
+ * arrays; list c holds segments seg_off[c] .. seg_off[c+1]-1 (seg_id OTR_NO_ID: no id;
+ * has_length 0: no length) and its reports go to rep_* from index seg_off[c]; per list:
+ * n_rep, shape_used (-1 absent), counts[6] (successful, unreported, discontinuities,
+ * invalid_speeds, invalid_times, unassociated), lengths[2], length_set[2]. */
+int otr_report_lists_device(int32_t n, const int64_t* seg_off, const uint64_t* seg_id, const double* start,
+                            const double* end, const uint8_t* internal, const int32_t* queue,
+                            const uint8_t* has_length, const int32_t* length, const int32_t* begin_shape,
+                            const int64_t* end_time, const double* threshold, const uint32_t* report_levels,
+                            const uint32_t* transition_levels, uint64_t* rep_id, uint64_t* rep_next, double* rep_t0,
+                            double* rep_t1, int32_t* rep_length, int32_t* rep_queue, int32_t* n_rep,
+                            int32_t* shape_used, int32_t* counts, double* lengths, int32_t* length_set);
 
 /* graph facts for callers sizing histograms */
 int otr_graph_info(int64_t* n_nodes, int64_t* n_edges, int64_t* n_segments);

@@ -36,7 +36,7 @@ STAGES = ['states', 'candidates', 'link', 'route', 'route_big', 'viterbi', 'path
 EXPORTS = ['otr_configure', 'otr_configure_json', 'otr_matcher_new', 'otr_matcher_free', 'otr_match',
            'otr_report', 'otr_report_segments', 'otr_free', 'otr_last_error', 'otr_match_batch',
            'otr_graph_info', 'otr_matcher_stream', 'otr_device', 'otr_report_batch', 'otr_coalesce',
-           'otr_tiles_cull', 'otr_tiles_format', 'otr_ingest']
+           'otr_tiles_cull', 'otr_tiles_format', 'otr_ingest', 'otr_report_lists_device']
 
 
 class TraceBatch(ctypes.Structure):
@@ -86,7 +86,9 @@ class BatchResult(ctypes.Structure):
                 ('shape_used', P(ctypes.c_int32)), ('stats', P(ctypes.c_int32)),
                 ('stats_len', P(ctypes.c_double)), ('d_hist', ctypes.c_void_p), ('hist_len', ctypes.c_int64),
                 ('counters', ctypes.c_uint64 * 24), ('kernel_ms', ctypes.c_float * 16),
-                ('trace_status', P(ctypes.c_int32)), ('d_rows', ctypes.c_void_p)]
+                ('trace_status', P(ctypes.c_int32)), ('d_rows', ctypes.c_void_p),
+                ('route_tier_code', ctypes.c_int32 * 8), ('route_tier_ms', ctypes.c_float * 8),
+                ('route_tier_work', (ctypes.c_uint64 * 4) * 8)]
 
 
 # otr_tile_row (include/otr.h), 56 bytes

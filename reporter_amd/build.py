@@ -61,14 +61,17 @@ def build_otr(force=False, stamps=False, variant=None, defines=()):
         extra += ['-D' + d for d in defines]
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
     headers += [os.path.join(ROOT, 'include', f) for f in os.listdir(os.path.join(ROOT, 'include'))]
-    objs = []
+    objs, jobs = [], []
     for src in ('otr_engine.hip', 'otr_api.cpp', 'otr_service.cpp'):
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, src + suffix + '.o')
         objs.append(o)
         if force or not _newer(o, [s] + headers):
             lang = [] if src.endswith('.hip') else ['-x', 'hip']
-            _run([HIPCC] + HIP_FLAGS + extra + lang + ['-c', s, '-o', o])
+            jobs.append([HIPCC] + HIP_FLAGS + extra + lang + ['-c', s, '-o', o])
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=3) as ex:
+        list(ex.map(_run, jobs))
     lib = os.path.join(PKG, 'libotr%s.so' % suffix)
     if force or not _newer(lib, objs):
         rdir, rname = hip_runtime_dir()
@@ -127,13 +130,22 @@ def build_parsecheck(force=False):
 
 
 def build_all(force=False):
+    """Everything, the three libotr builds in parallel (each compiles its HIP sources for
+    gfx950).  force=True recompiles every object (what the driver's build() does)."""
+    from concurrent.futures import ThreadPoolExecutor
     build_gen(force)
     build_parsecheck(force)
     build_oracle(force)
     build_calib(force)
-    lib = build_otr(force)
-    # test build: every first-tier search is sent down the retry tiers (tests/test_gpu_tiers.py)
-    build_otr(force, variant='tiercheck', defines=['OTR_FORCE_RETRY'])
+    with ThreadPoolExecutor(max_workers=3) as ex:
+        futs = [ex.submit(build_otr, force),
+                # test build: every first-tier search goes down the retry tiers (tests/test_gpu_tiers.py)
+                ex.submit(build_otr, force, False, 'tiercheck', ['OTR_FORCE_RETRY']),
+                # test build: every search in the global-memory kernel (tests/test_gpu_tiers.py)
+                ex.submit(build_otr, force, False, 'generalcheck', ['OTR_FORCE_GENERAL'])]
+        lib = futs[0].result()
+        for f in futs[1:]:
+            f.result()
     build_loadgen(force)
     return lib
 

@@ -306,6 +306,51 @@ int otr_report_segments(const char* match_json, size_t match_len, const char* tr
   return OTR_OK;
 }
 
+// report() on the device over many segment lists (the K7 tail; tests)
+int otr_report_lists_device(int32_t n, const int64_t* seg_off, const uint64_t* seg_id, const double* start,
+                            const double* end, const uint8_t* internal, const int32_t* queue,
+                            const uint8_t* has_length, const int32_t* length, const int32_t* begin_shape,
+                            const int64_t* end_time, const double* threshold, const uint32_t* report_levels,
+                            const uint32_t* transition_levels, uint64_t* rep_id, uint64_t* rep_next, double* rep_t0,
+                            double* rep_t1, int32_t* rep_length, int32_t* rep_queue, int32_t* n_rep,
+                            int32_t* shape_used, int32_t* counts, double* lengths, int32_t* length_set) {
+  if (n < 0 || (n > 0 && (!seg_off || !end_time || !threshold || !report_levels || !transition_levels || !n_rep ||
+                          !shape_used || !counts || !lengths || !length_set))) {
+    g_last_error = "null argument";
+    return OTR_BAD_REQUEST;
+  }
+  otr::ReportLists h{};
+  h.n = n;
+  h.seg_off = seg_off;
+  h.seg_id = (const unsigned long long*)seg_id;
+  h.start = start;
+  h.end = end;
+  h.internal = internal;
+  h.queue = queue;
+  h.has_length = has_length;
+  h.length = length;
+  h.begin_shape = begin_shape;
+  h.end_time = end_time;
+  h.threshold = threshold;
+  h.rl = report_levels;
+  h.tl = transition_levels;
+  h.rep_id = (unsigned long long*)rep_id;
+  h.rep_next = (unsigned long long*)rep_next;
+  h.rep_t0 = rep_t0;
+  h.rep_t1 = rep_t1;
+  h.rep_length = rep_length;
+  h.rep_queue = rep_queue;
+  h.n_rep = n_rep;
+  h.shape_used = shape_used;
+  h.counts = counts;
+  h.lengths = lengths;
+  h.length_set = length_set;
+  std::string err;
+  const int rc = otr::report_lists_device(h, &err);
+  if (rc != OTR_OK) g_last_error = err;
+  return rc;
+}
+
 // batched throughput API (new)
 int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result* out) {
   if (!m || !in || !out) {

@@ -41,6 +41,27 @@ struct GraphState {
 GraphState& graph_state();
 int engine_configure(const Config& cfg, std::string* err);
 
+struct ReportLists {
+  int32_t n;
+  const int64_t* seg_off;
+  const unsigned long long* seg_id;
+  const double *start, *end;
+  const uint8_t* internal;
+  const int32_t* queue;
+  const uint8_t* has_length;
+  const int32_t *length, *begin_shape;
+  const int64_t* end_time;
+  const double* threshold;
+  const uint32_t *rl, *tl;
+  unsigned long long *rep_id, *rep_next;
+  double *rep_t0, *rep_t1;
+  int32_t *rep_length, *rep_queue, *n_rep, *shape_used, *counts;
+  double* lengths;
+  int32_t* length_set;
+};
+
+int report_lists_device(const ReportLists& h, std::string* err);
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -74,7 +95,7 @@ struct Matcher {
   std::vector<unsigned long long> h_seg_id, h_rep_id, h_rep_next;
   std::vector<uint8_t> h_seg_internal;
   std::vector<otr_tile_row> h_tile_rows;
-  hipEvent_t ev[24];  // 0..19 batch stages, 20..23 ingest
+  hipEvent_t ev[40];  // 0..19 batch stages, 20..23 ingest, 24..39 route tiers
   bool ev_init = false;
 
   template <class T>

@@ -505,6 +505,7 @@ static std::vector<int> route_tiers() {
     if (code == 2561 || code == 5121 || code == 10241 || code == 20481 || code == 3842 || code == 4482 || code == 5122) t.push_back(code);
     i = j + 1;
   }
+  if (t.size() > 4) t.resize(4);  // at most 5 retry tiers (otr_batch_result route_tier_*)
   t.push_back(40961);
   return t;
 }
@@ -577,7 +578,10 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   }
   out->n_probes = N;
   h_trace_status.assign(T, OTR_OK);
-  const size_t n_ctr = 2 * (size_t)OTR_COUNTERS * kShards;  // tier-2 kinds land at +6, stamps at 16
+  // counter banks of OTR_COUNTERS kinds x kShards: 0 the batch (and the first route
+  // tier), 2..6 the LDS retry tiers, 8..9 the global-memory tiers
+  const size_t bank = (size_t)OTR_COUNTERS * kShards;
+  const size_t n_ctr = 10 * bank;
   unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, n_ctr);
   HIPCHK(hipMemsetAsync(d_counters, 0, n_ctr * 8, stream));
   size_t scan_bytes = 0;
@@ -797,9 +801,11 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     static const int route_g = getenv("OTR_ROUTE_G") ? atoi(getenv("OTR_ROUTE_G")) : 2;  // A/B knob
     if (route_g == 2) {
       const int64_t units = (NT + 1) / 2;
-      k_route<160, 2><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
+      k_route<160, 2, false><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
+      out->route_tier_code[0] = 1602;
     } else {
-      k_route<256, 1><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
+      k_route<256, 1, false><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
+      out->route_tier_code[0] = 2561;
     }
     te(OTR_STAGE_ROUTE);
     // overflow retries with larger LDS tables (same results, fewer resident waves): each
@@ -809,24 +815,29 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     tb(OTR_STAGE_ROUTE_BIG);
     static const std::vector<int> tiers = route_tiers();
     const int ntier = (int)tiers.size();
-    const unsigned tgrid = 2048;
+    // persistent grids: twice the resident waves of the widest tier (256 CUs x 4 SIMDs x
+    // 8 waves), so no tier is starved; blocks past the list length exit at once
+    const unsigned tgrid = 16384;
     for (int tier = 0; tier < ntier; ++tier) {
       unsigned long long* c = cnt + tier;
       k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, tier == 0 ? 0x2u : 0x6u, list + 0, c);
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.list_count = c;
-      unsigned long long* rcn = d_counters + 6 * kShards;
+      unsigned long long* rcn = d_counters + (2 + tier) * bank;
+      out->route_tier_code[1 + tier] = tiers[tier];
+      if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier)], stream);
       switch (tiers[tier]) {
-        case 2561: k_route<256, 1><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 5121: k_route<512, 1><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 10241: k_route<1024, 1><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 20481: k_route<2048, 1><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 3842: k_route<384, 2><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 4482: k_route<448, 2><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 5122: k_route<512, 2><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        default: k_route<4096, 1><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 2561: k_route<256, 1, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 5121: k_route<512, 1, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 10241: k_route<1024, 1, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 20481: k_route<2048, 1, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 3842: k_route<384, 2, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 4482: k_route<448, 2, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 5122: k_route<512, 2, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        default: k_route<4096, 1, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
       }
+      if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier) + 1], stream);
     }
     // everything left — turn-cost (edge-based) tasks, tasks whose labels need 64 bits,
     // overflows of the largest LDS table — runs in the global-memory search: first on
@@ -840,7 +851,11 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       ga.list = list;
       ga.list_count = c;
       ga.flag = task_ovf;
+      ga.counters = d_counters + (8 + gt) * bank;
+      out->route_tier_code[6 + gt] = -1 - gt;
+      if (timing) (void)hipEventRecord(ev[24 + 2 * (6 + gt)], stream);
       k_general<<<gs2.n, kGenThreads, 0, stream>>>(g, ga, gs2);
+      if (timing) (void)hipEventRecord(ev[24 + 2 * (6 + gt) + 1], stream);
     }
     // tasks still flagged (beyond a 1M-state slab): their traces get OTR_MATCH_ERROR
     k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, 0xEu, fail_tasks, cnt + 10);
@@ -927,9 +942,9 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       for (int tier = 0; tier < 3; ++tier) {
         unsigned long long* c = cnt + 12 + tier;
         k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0x2u, list, c);
-        if (tier == 0) k_paths<512, 1><<<2048, 64, 0, stream>>>(g, pa, list, c);
-        else if (tier == 1) k_paths<1024, 1><<<2048, 64, 0, stream>>>(g, pa, list, c);
-        else k_paths<4096, 1><<<1024, 64, 0, stream>>>(g, pa, list, c);
+        if (tier == 0) k_paths<512, 1><<<16384, 64, 0, stream>>>(g, pa, list, c);
+        else if (tier == 1) k_paths<1024, 1><<<8192, 64, 0, stream>>>(g, pa, list, c);
+        else k_paths<4096, 1><<<4096, 64, 0, stream>>>(g, pa, list, c);
       }
       // turn-cost winners, 64-bit labels and the largest-table overflows: k_general
       ga.steps = steps;
@@ -950,6 +965,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
         ga.list = list;
         ga.list_count = c;
         ga.flag = step_ovf;
+        ga.counters = nullptr;
         k_general<<<gs2.n, kGenThreads, 0, stream>>>(g, ga, gs2);
       }
       // steps still flagged (beyond a 1M-state slab): named after the final sync
@@ -1105,19 +1121,37 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       }
     }
   }
-  for (int k = 0; k < OTR_COUNTERS; ++k) {
+  auto ctr = [&](int b, int k) {
     unsigned long long v = 0;
-    for (int sh = 0; sh < kShards; ++sh) v += hc[(size_t)k * kShards + sh];
-    out->counters[k] = v;
+    for (int sh = 0; sh < kShards; ++sh) v += hc[(size_t)b * bank + (size_t)k * kShards + sh];
+    return v;
+  };
+  for (int k = 0; k < OTR_COUNTERS; ++k) out->counters[k] = ctr(0, k);
+  // per route kernel: searches, settled, relaxed, transition entries (banks 0, 2..6, 8..9)
+  for (int t = 0; t < 8; ++t) {
+    const int b = t == 0 ? 0 : (t < 6 ? 1 + t : 2 + t);
+    out->route_tier_work[t][0] = ctr(b, 6);
+    out->route_tier_work[t][1] = ctr(b, 3);
+    out->route_tier_work[t][2] = ctr(b, 4);
+    out->route_tier_work[t][3] = ctr(b, 5);
+    if (t >= 1 && t < 6) {  // the LDS retry tiers together (counters 9 / 10)
+      out->counters[9] += ctr(b, 3);
+      out->counters[10] += ctr(b, 4);
+    }
   }
   out->counters[5] = (uint64_t)NT;
   out->counters[6] = (uint64_t)NTR;
   if (!(in->flags & OTR_BATCH_TILE_ROWS)) out->n_rows = (int64_t)out->counters[8];
   out->d_hist = ha.hist;
   out->hist_len = (int64_t)hist_len;
-  if (timing)
+  if (timing) {
     for (int k = 0; k < 10; ++k)
       if (used[k]) (void)hipEventElapsedTime(&out->kernel_ms[k], ev[2 * k], ev[2 * k + 1]);
+    out->route_tier_ms[0] = out->kernel_ms[OTR_STAGE_ROUTE];
+    for (int t = 1; t < 8; ++t)
+      if (out->route_tier_code[t] != 0)
+        (void)hipEventElapsedTime(&out->route_tier_ms[t], ev[24 + 2 * t], ev[24 + 2 * t + 1]);
+  }
   // ---- copy-out (tests / JSON path), compacting the capacity layout
   std::vector<int64_t> route_n(T), seg_n(T), way_n(T), rep_n(T), h_cap_off(T + 1);
   HIPCHK(hipMemcpy(route_n.data(), sa.route_n, 8 * T, hipMemcpyDeviceToHost));
@@ -1251,6 +1285,99 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   out->shape_used = P(h_shape_used);
   out->stats = P(h_stats);
   out->stats_len = P(h_stats_len);
+  return OTR_OK;
+}
+
+// report() over many segment lists on the device (include/otr.h otr_report_lists_device):
+// one thread per list runs the report_segments K7 runs.
+__global__ void k_report_lists(ReportLists a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.n) return;
+  const int64_t o = a.seg_off[c];
+  ReportStats rs;
+  report_segments((int32_t)(a.seg_off[c + 1] - o), a.seg_id + o, a.start + o, a.end + o, a.internal + o, a.queue + o,
+                  a.has_length + o, a.length + o, a.begin_shape + o, nullptr, a.end_time[c], a.threshold[c], a.rl[c],
+                  a.tl[c], a.rep_id + o, a.rep_next + o, a.rep_t0 + o, a.rep_t1 + o, a.rep_length + o, a.rep_queue + o,
+                  nullptr, &rs);
+  a.n_rep[c] = rs.n_rep;
+  a.shape_used[c] = rs.shape_used;
+  for (int k = 0; k < 6; ++k) a.counts[6 * c + k] = rs.counts[k];
+  for (int k = 0; k < 2; ++k) {
+    a.lengths[2 * c + k] = rs.lengths[k];
+    a.length_set[2 * c + k] = rs.length_set[k];
+  }
+}
+
+int report_lists_device(const ReportLists& h, std::string* err) {
+  GraphState& gs = graph_state();
+  HIPCHK(hipSetDevice(gs.device));
+  const int32_t n = h.n;
+  if (n <= 0) return OTR_OK;
+  const int64_t S = h.seg_off[n];
+  std::vector<void*> mem;
+  bool ok = true;
+  auto put = [&](const void* src, size_t bytes) -> void* {
+    void* d = nullptr;
+    if (hipMalloc(&d, bytes ? bytes : 16) != hipSuccess) ok = false;
+    mem.push_back(d);
+    if (ok && bytes && src && hipMemcpy(d, src, bytes, hipMemcpyHostToDevice) != hipSuccess) ok = false;
+    return d;
+  };
+  ReportLists d = h;
+  d.seg_off = (const int64_t*)put(h.seg_off, 8ull * (n + 1));
+  d.seg_id = (const unsigned long long*)put(h.seg_id, 8ull * S);
+  d.start = (const double*)put(h.start, 8ull * S);
+  d.end = (const double*)put(h.end, 8ull * S);
+  d.internal = (const uint8_t*)put(h.internal, (size_t)S);
+  d.queue = (const int32_t*)put(h.queue, 4ull * S);
+  d.has_length = (const uint8_t*)put(h.has_length, (size_t)S);
+  d.length = (const int32_t*)put(h.length, 4ull * S);
+  d.begin_shape = (const int32_t*)put(h.begin_shape, 4ull * S);
+  d.end_time = (const int64_t*)put(h.end_time, 8ull * n);
+  d.threshold = (const double*)put(h.threshold, 8ull * n);
+  d.rl = (const uint32_t*)put(h.rl, 4ull * n);
+  d.tl = (const uint32_t*)put(h.tl, 4ull * n);
+  d.rep_id = (unsigned long long*)put(nullptr, 8ull * S);
+  d.rep_next = (unsigned long long*)put(nullptr, 8ull * S);
+  d.rep_t0 = (double*)put(nullptr, 8ull * S);
+  d.rep_t1 = (double*)put(nullptr, 8ull * S);
+  d.rep_length = (int32_t*)put(nullptr, 4ull * S);
+  d.rep_queue = (int32_t*)put(nullptr, 4ull * S);
+  d.n_rep = (int32_t*)put(nullptr, 4ull * n);
+  d.shape_used = (int32_t*)put(nullptr, 4ull * n);
+  d.counts = (int32_t*)put(nullptr, 24ull * n);
+  d.lengths = (double*)put(nullptr, 16ull * n);
+  d.length_set = (int32_t*)put(nullptr, 8ull * n);
+  auto release = [&] {
+    for (void* q : mem)
+      if (q) (void)hipFree(q);
+  };
+  if (!ok) {
+    release();
+    if (err) *err = "device allocation failed (report lists)";
+    return OTR_DEVICE_ERROR;
+  }
+  k_report_lists<<<grid_for(n, 128), 128>>>(d);
+  hipError_t e = hipDeviceSynchronize();
+  auto get = [&](void* dst, const void* src, size_t bytes) {
+    if (e == hipSuccess && bytes) e = hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+  };
+  get(h.rep_id, d.rep_id, 8ull * S);
+  get(h.rep_next, d.rep_next, 8ull * S);
+  get(h.rep_t0, d.rep_t0, 8ull * S);
+  get(h.rep_t1, d.rep_t1, 8ull * S);
+  get(h.rep_length, d.rep_length, 4ull * S);
+  get(h.rep_queue, d.rep_queue, 4ull * S);
+  get(h.n_rep, d.n_rep, 4ull * n);
+  get(h.shape_used, d.shape_used, 4ull * n);
+  get(h.counts, d.counts, 24ull * n);
+  get(h.lengths, d.lengths, 16ull * n);
+  get(h.length_set, d.length_set, 8ull * n);
+  release();
+  if (e != hipSuccess) {
+    if (err) *err = std::string("HIP error: ") + hipGetErrorString(e);
+    return OTR_DEVICE_ERROR;
+  }
   return OTR_OK;
 }
 

@@ -133,7 +133,7 @@ struct GTask {
 // false (workgroup-uniform) on slab overflow.
 __device__ bool g_search(const DevGraph& G, const GTask& T, uint32_t* key, unsigned long long* lab, uint32_t* qmark,
                          uint32_t* fr, uint32_t* touched, uint32_t cap, uint32_t* s_n, uint32_t* s_touched,
-                         uint32_t* s_ovf, unsigned long long* relaxed_out) {
+                         uint32_t* s_ovf, unsigned long long* work) {
   const int tid = threadIdx.x;
   const uint32_t maxk = cap - cap / 8u;
   unsigned long long my_relaxed = 0;
@@ -211,6 +211,7 @@ __device__ bool g_search(const DevGraph& G, const GTask& T, uint32_t* key, unsig
   __syncthreads();
   uint32_t round = 0;
   int cur = 0;
+  unsigned long long expanded = 0;  // states expanded (uniform): the search's "settled" count
   for (;;) {
     const uint32_t n = s_n[cur];
     if (n == 0 || *s_ovf) break;
@@ -219,6 +220,7 @@ __device__ bool g_search(const DevGraph& G, const GTask& T, uint32_t* key, unsig
     if (tid == 0) s_n[nxt] = 0;
     __syncthreads();
     const uint32_t nn = n < cap ? n : cap;
+    expanded += nn;
     for (uint32_t i = tid; i < nn; i += kGenThreads) {
       const uint32_t sl = ld_u32(&fr[(size_t)cur * cap + i]);
       const uint32_t a = ld_u32(&key[sl]);
@@ -231,7 +233,11 @@ __device__ bool g_search(const DevGraph& G, const GTask& T, uint32_t* key, unsig
     cur = nxt;
   }
   __syncthreads();
-  if (relaxed_out) atomicAdd(relaxed_out, my_relaxed);
+  if (work) {  // this tier's counter bank (kinds 3 settled, 4 relaxed)
+    const int sh = blockIdx.x & (kShards - 1);
+    atomicAdd(&work[4 * kShards + sh], my_relaxed);
+    if (tid == 0) atomicAdd(&work[3 * kShards + sh], expanded);
+  }
   return *s_ovf == 0;
 }
 
@@ -322,10 +328,14 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
       const int64_t sp = a.prev[s];
       const int i0 = __ffsll((long long)mask) - 1;
       const GTask T = g_task(G, a, s, sp, a.cand_edge[sp * OTR_KMAX + i0]);
-      const bool ok = g_search(G, T, key, lab, qmark, fr, touched, cap, s_n, &s_touched, &s_ovf,
-                               a.counters ? a.counters + 10 * kShards + (blockIdx.x & (kShards - 1)) : nullptr);
+      const bool ok = g_search(G, T, key, lab, qmark, fr, touched, cap, s_n, &s_touched, &s_ovf, a.counters);
       if (ok) {
         const int Kb = a.cand_count[s];
+        if (a.counters && tid == 0) {  // kinds 5 transition entries, 6 searches
+          const int sh = blockIdx.x & (kShards - 1);
+          atomicAdd(&a.counters[5 * kShards + sh], (unsigned long long)Kb * (unsigned long long)__popcll(mask));
+          atomicAdd(&a.counters[6 * kShards + sh], 1ull);
+        }
         uint32_t* trow = a.trans + a.trans_off[s];
         uint32_t* crow = a.trans_tc + a.trans_off[s];
         for (int j = tid; j < Kb; j += kGenThreads) {

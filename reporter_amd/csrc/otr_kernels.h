@@ -987,7 +987,11 @@ __global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const uns
   }
   const uint32_t bmm = (uint32_t)bound_mm_of(bound[s]);
   const uint32_t sh = pack_shift(bt[s]);
+#ifdef OTR_FORCE_GENERAL
+  const bool general = true;  // test build: every search in k_general (tests/test_gpu_tiers.py)
+#else
   const bool general = ((turn_modes >> md) & 1u) || !pack_fits(bmm, sh);
+#endif
   const uint32_t meta = (uint32_t)cand_count[s] | ((uint32_t)md << 8) | ((forced[s] ? 1u : 0u) << 10) | (sh << 11) |
                         ((general ? 1u : 0u) << 16);
   rec[2 * t] = make_uint4((uint32_t)s, (uint32_t)sp, root, bmm);
@@ -997,21 +1001,21 @@ __global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const uns
 #ifndef OTR_ROUTE2_WAVES
 #define OTR_ROUTE2_WAVES 8
 #endif
-template <int CAP, int G>
+// LIST = false: the first tier, one unit per block over all tasks (XCD-mapped); LIST =
+// true: a retry tier, a fixed grid striding over the device-side task list (its length
+// never crosses to the host)
+template <int CAP, int G, bool LIST>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR_ROUTE2_WAVES : 8, G == 2 ? OTR_ROUTE2_WAVES : 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
   using Gr = Grp<G>;
   __shared__ SearchLds<CAP, false> Ls[G];
   const int lane = Gr::gl();
-  // first tier: one unit per block over all tasks (XCD-mapped); retry tiers: a fixed
-  // grid strides over the device-side task list (its length never crosses to the host)
-  const int64_t n_tasks = a.task_list ? (int64_t)*a.list_count : a.n_tasks;
+  const int64_t n_tasks = LIST ? (int64_t)*a.list_count : a.n_tasks;
   const int64_t n_units = (n_tasks + G - 1) / G;
-  const int64_t w0 = a.task_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_units + 7) / 8);
-  const int64_t wstep = a.task_list ? (int64_t)gridDim.x : n_units;
-  for (int64_t w = w0; w < n_units; w += wstep) {
+  const int64_t w0 = LIST ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_units + 7) / 8);
+  for (int64_t w = w0; w < n_units; w += (LIST ? (int64_t)gridDim.x : n_units)) {
   const int64_t tw = w * G + Gr::g();
   const bool have = tw < n_tasks;
-  const int64_t task = have ? (a.task_list ? a.task_list[tw] : tw) : 0;
+  const int64_t task = have ? (LIST ? a.task_list[tw] : tw) : 0;
   OTR_STAMP(ts_in);
   // ---- search inputs (only these stay live through the search)
   bool search, fits, forced;
@@ -1029,7 +1033,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
     K.sh = (r1.y >> 11) & 31u;
     const bool general = (r1.y >> 16) & 1u;  // re-read after the search
     fits = Kb <= Gr::GL && !general;  // targets are lanes of the group: wider steps go to a G = 1 tier
-    if (G == 2 && !a.task_list && r0.w > a.direct_bmm) fits = false;
+    if (G == 2 && !LIST && r0.w > a.direct_bmm) fits = false;
     mode_bit = 1u << ((r1.y >> 8) & 3u);
     bmm = r0.w;
     root = r0.z;
@@ -1067,7 +1071,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
                                       &rounds, counters ? counters + 16 * kShards : nullptr) &&
             fits;
 #ifdef OTR_FORCE_RETRY
-  if (G == 2 && !a.task_list) ok = false;  // test build: every first-tier task takes the retry tiers
+  if (G == 2 && !LIST) ok = false;  // test build: every first-tier task takes the retry tiers
 #endif
   OTR_STAMP(ts_srch);
   SearchLds<CAP, false>& L = Ls[Gr::g()];
@@ -1114,7 +1118,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   // to the 1024-slot tier (flag 2)
   if (have && !ok && !forced && lane == 0) {
     const bool general = (a.rec[2 * task + 1].y >> 16) & 1u;
-    a.overflow_flag[task] = general ? 3 : ((G == 2 && !a.task_list && bmm > 1900000u) ? 2 : 1);
+    a.overflow_flag[task] = general ? 3 : ((G == 2 && !LIST && bmm > 1900000u) ? 2 : 1);
   }
 #ifdef OTR_STAMPS
   if (G == 2 && counters && threadIdx.x == 0) {  // task setup and transition rows, wave cycles
@@ -1131,20 +1135,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
     rounds = wave_sum_u32((uint32_t)rounds);
     const int nk = have && search ? L.n_keys : 0;
     const int nsrc = have ? __popcll(a.task_mask[task]) : 0;
-    unsigned long long kk = 0, c96 = 0, c64 = 0, c128 = 0, kb = 0, ns = 0;
+    unsigned long long kk = 0, c96 = 0, c64 = 0, c128 = 0, kb = 0, ns = 0, ntr = 0, nsearch = 0;
     for (int q = 0; q < G; ++q) {
       const int nkq = __builtin_amdgcn_readlane(nk, q * Gr::GL);
       kk += (unsigned long long)nkq;
       c96 += nkq > 96;
       c64 += nkq > 64;
       c128 += nkq > 128;
-      kb += (unsigned long long)__builtin_amdgcn_readlane(have ? Kb : 0, q * Gr::GL);
-      ns += (unsigned long long)__builtin_amdgcn_readlane(nsrc, q * Gr::GL);
+      const unsigned long long kbq = (unsigned long long)__builtin_amdgcn_readlane(have ? Kb : 0, q * Gr::GL);
+      const unsigned long long nsq = (unsigned long long)__builtin_amdgcn_readlane(nsrc, q * Gr::GL);
+      kb += kbq;
+      ns += nsq;
+      if (__builtin_amdgcn_readlane((int)(have && search), q * Gr::GL)) {
+        ntr += kbq * nsq;  // transition entries this search wrote (K4)
+        ++nsearch;
+      }
     }
     if (threadIdx.x == 0) {
       const int sh = blockIdx.x & (kShards - 1);
       atomicAdd(&counters[3 * kShards + sh], settled);
       atomicAdd(&counters[4 * kShards + sh], relaxed);
+      atomicAdd(&counters[5 * kShards + sh], ntr);
+      atomicAdd(&counters[6 * kShards + sh], nsearch);
       atomicAdd(&counters[11 * kShards + sh], kb);
       atomicAdd(&counters[12 * kShards + sh], ns);
       atomicAdd(&counters[13 * kShards + sh], rounds);
@@ -1425,7 +1437,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
     K.sh = pack_shift(a.bt[s]);
     if (ej == ei && pj >= pi) {
       if (gl == 0) a.path_len[s] = -1;
-    } else if (((a.turn_modes >> mode) & 1u) || !pack_fits(bmm, K.sh)) {
+    } else if (((a.turn_modes >> mode) & 1u) || !pack_fits(bmm, K.sh)
+#ifdef OTR_FORCE_GENERAL
+               || true
+#endif
+    ) {
       if (gl == 0) a.overflow_flag[k] = 3;  // edge-based / 64-bit labels: k_general
     } else {
       active = true;

@@ -146,20 +146,24 @@ class Matcher:
     # --- batched API ----------------------------------------------------------------
     def match_batch(self, traces, report_levels=(0, 1), transition_levels=(0, 1), threshold_sec=15,
                     quantisation=3600, hist_base_time=0, hist_hours=0, copy_out=True, timing=False,
-                    device_arrays=None, hist_device=None, tile_rows=False, tile_rules=0):
+                    device_arrays=None, hist_device=None, tile_rows=False, tile_rules=0, host_arrays=None,
+                    copy_reports=False):
         """Match a gen.Traces-like SoA batch.  With device_arrays (dict of device
         pointers: trace_offsets, lat, lon, time, accuracy, mode) the inputs are
-        already resident in HBM."""
+        already resident in HBM; host_arrays: the same as host pointers (e.g. pinned
+        buffers the caller keeps alive).  copy_reports: segments, reports and stats
+        come back to the host (the JSON path's copy-out)."""
         b = _lib.TraceBatch()
         b.n_traces = int(traces.n_traces)
-        if device_arrays is not None:
-            b.memory = _lib.OTR_MEM_DEVICE
-            b.trace_offsets = device_arrays['trace_offsets']
-            b.lat = device_arrays['lat']
-            b.lon = device_arrays['lon']
-            b.time = device_arrays['time']
-            b.accuracy = device_arrays.get('accuracy') or None
-            b.mode = device_arrays['mode']
+        arrs = device_arrays if device_arrays is not None else host_arrays
+        if arrs is not None:
+            b.memory = _lib.OTR_MEM_DEVICE if device_arrays is not None else _lib.OTR_MEM_HOST
+            b.trace_offsets = arrs['trace_offsets']
+            b.lat = arrs['lat']
+            b.lon = arrs['lon']
+            b.time = arrs['time']
+            b.accuracy = arrs.get('accuracy') or None
+            b.mode = arrs['mode']
         else:
             b.memory = _lib.OTR_MEM_HOST
             keep = [np.ascontiguousarray(traces.offsets, np.int64), np.ascontiguousarray(traces.lat, np.float64),
@@ -178,11 +182,12 @@ class Matcher:
         b.hist_device = hist_device
         b.tile_rules = int(tile_rules)
         b.flags = (_lib.OTR_BATCH_COPY_OUT if copy_out else 0) | (_lib.OTR_BATCH_TIMING if timing else 0) | \
-            (_lib.OTR_BATCH_TILE_ROWS if tile_rows else 0)
+            (_lib.OTR_BATCH_TILE_ROWS if tile_rows else 0) | (_lib.OTR_BATCH_COPY_REPORTS if copy_reports else 0)
         r = _lib.BatchResult()
         rc = self._L.otr_match_batch(self._h, ctypes.byref(b), ctypes.byref(r))
         if rc != 0:
             raise RuntimeError('otr_match_batch failed (%d): %s' % (rc, _lib.last_error()))
+        r._owner = self  # the host arrays belong to this matcher: keep it alive with the result
         return r
 
     def ingest(self, text, rules=0, separator='|', uuid_index=1, time_index=0, lat_index=9, lon_index=10,

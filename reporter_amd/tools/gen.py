@@ -42,6 +42,11 @@ def lib():
                                     P(ctypes.c_double), P(ctypes.c_int64), P(ctypes.c_uint8),
                                     P(ctypes.c_uint32), ctypes.c_int64, ctypes.c_int64]
         L.otrgen_traces.restype = ctypes.c_int
+        L.otrgen_traces_ids.argtypes = [ctypes.c_char_p, ctypes.c_int, P(ctypes.c_int64), ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_double, ctypes.c_uint64, ctypes.c_double, ctypes.c_double,
+                                        P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_int64),
+                                        P(ctypes.c_uint8), P(ctypes.c_uint32), ctypes.c_int64, ctypes.c_int64]
+        L.otrgen_traces_ids.restype = ctypes.c_int
         _LIB = L
     return _LIB
 
@@ -117,6 +122,31 @@ def make_traces(graph, n_traces, n_points, sample_rate, sigma, seed, frac_bicycl
         acc = np.full(n, float(point_accuracy), np.float32)
     uuids = ['veh%07d' % (uuid_base + i) for i in range(n_traces)]
     return Traces(lat, lon, tm, off, mode, acc, truth, uuids)
+
+
+def make_traces_ids(graph, ids, n_points, sample_rate, sigma, seed, frac_bicycle=0.0, frac_ped=0.0,
+                    point_accuracy=None, t_begin=T_BEGIN, t_spread=86400 * 7):
+    """Traces of the vehicles numbered `ids` ("veh%07d" uuids), each drawn from its own
+    generator (seed, id): a uuid shard of a fleet is generated without the rest (C3)."""
+    ids = np.ascontiguousarray(ids, np.int64)
+    n_traces = len(ids)
+    n = n_traces * n_points
+    lat = np.zeros(n, np.float64)
+    lon = np.zeros(n, np.float64)
+    tm = np.zeros(n, np.int64)
+    mode = np.zeros(n_traces, np.uint8)
+    truth = np.zeros(n, np.uint32)
+    P = ctypes.POINTER
+    rc = lib().otrgen_traces_ids(graph.encode(), n_traces, ids.ctypes.data_as(P(ctypes.c_int64)), n_points,
+                                 sample_rate, sigma, seed, frac_bicycle, frac_ped,
+                                 lat.ctypes.data_as(P(ctypes.c_double)), lon.ctypes.data_as(P(ctypes.c_double)),
+                                 tm.ctypes.data_as(P(ctypes.c_int64)), mode.ctypes.data_as(P(ctypes.c_uint8)),
+                                 truth.ctypes.data_as(P(ctypes.c_uint32)), int(t_begin), int(t_spread))
+    if rc != 0:
+        raise RuntimeError('otrgen_traces_ids failed: %d' % rc)
+    off = np.arange(n_traces + 1, dtype=np.int64) * n_points
+    acc = None if point_accuracy is None else np.full(n, float(point_accuracy), np.float32)
+    return Traces(lat, lon, tm, off, mode, acc, truth, ['veh%07d' % int(i) for i in ids])
 
 
 def config_traces(name, n_traces=None, graph_cache=None):

@@ -366,10 +366,12 @@ int otrgen_graph(const char* path, int rows, int cols, double spacing_m, double 
 // `graph_path`.  Output arrays are caller-allocated with n_traces*n_points entries
 // (times are epoch seconds).  mode_mix: fractions of auto/bicycle/pedestrian traces;
 // out_mode[t] receives 0/1/2.  point_accuracy < 0 means "no accuracy field".
-int otrgen_traces(const char* graph_path, int n_traces, int n_points, int sample_rate, double noise_m,
-                  uint64_t seed, double frac_bicycle, double frac_pedestrian, double* out_lat,
-                  double* out_lon, int64_t* out_time, uint8_t* out_mode, uint32_t* out_truth_edge,
-                  int64_t t_begin, int64_t t_spread) {
+// ids != NULL: trace t is the drive of vehicle ids[t], drawn from its own generator
+// seeded by (seed, ids[t]) — any subset of a fleet (a uuid shard, C3) is generated alone.
+static int gen_traces(const char* graph_path, int n_traces, const int64_t* ids, int n_points, int sample_rate,
+                      double noise_m, uint64_t seed, double frac_bicycle, double frac_pedestrian, double* out_lat,
+                      double* out_lon, int64_t* out_time, uint8_t* out_mode, uint32_t* out_truth_edge,
+                      int64_t t_begin, int64_t t_spread) {
   FILE* f = fopen(graph_path, "rb");
   if (!f) return -1;
   otr_graph_header h;
@@ -396,6 +398,7 @@ int otrgen_traces(const char* graph_path, int n_traces, int n_points, int sample
   const int lookback = (int)std::ceil((double)(30 / (sample_rate + 2)));  // py2 int division
   Rng rng(seed);
   for (int t = 0; t < n_traces; ++t) {
+    if (ids) rng = Rng(seed * 0x100000001B3ull ^ (uint64_t)ids[t]);
     double um = rng.uni();
     int mode = um < frac_pedestrian ? 2 : (um < frac_pedestrian + frac_bicycle ? 1 : 0);
     uint32_t mbit = 1u << mode;
@@ -492,6 +495,22 @@ int otrgen_traces(const char* graph_path, int n_traces, int n_points, int sample
     }
   }
   return 0;
+}
+
+int otrgen_traces(const char* graph_path, int n_traces, int n_points, int sample_rate, double noise_m,
+                  uint64_t seed, double frac_bicycle, double frac_pedestrian, double* out_lat,
+                  double* out_lon, int64_t* out_time, uint8_t* out_mode, uint32_t* out_truth_edge,
+                  int64_t t_begin, int64_t t_spread) {
+  return gen_traces(graph_path, n_traces, nullptr, n_points, sample_rate, noise_m, seed, frac_bicycle,
+                    frac_pedestrian, out_lat, out_lon, out_time, out_mode, out_truth_edge, t_begin, t_spread);
+}
+
+int otrgen_traces_ids(const char* graph_path, int n_traces, const int64_t* ids, int n_points, int sample_rate,
+                      double noise_m, uint64_t seed, double frac_bicycle, double frac_pedestrian, double* out_lat,
+                      double* out_lon, int64_t* out_time, uint8_t* out_mode, uint32_t* out_truth_edge,
+                      int64_t t_begin, int64_t t_spread) {
+  return gen_traces(graph_path, n_traces, ids, n_points, sample_rate, noise_m, seed, frac_bicycle,
+                    frac_pedestrian, out_lat, out_lon, out_time, out_mode, out_truth_edge, t_begin, t_spread);
 }
 
 }  // extern "C"

@@ -21,9 +21,11 @@ from oracle import pyoracle as po
 from oracle.compare import compare
 from reporter_amd import matcher as M
 from reporter_amd.tools import gen
-for g, nt, npnt, sr, sig, seed, acc, over in [('city', 40, 100, 15, 10.0, 2, None, {}),
+# turn_penalty_factor 0 (generate_test_trace.py:47): node searches, i.e. the LDS tiers
+for g, nt, npnt, sr, sig, seed, acc, over in [('city', 40, 100, 15, 10.0, 2, None, {'turn_penalty_factor': 0}),
                                              ('metro', 30, 60, 60, 50.0, 4, 50.0,
-                                              {'search_radius': 200, 'max_search_radius': 200})]:
+                                              {'search_radius': 200, 'max_search_radius': 200,
+                                               'turn_penalty_factor': 0})]:
     path = gen.graph_path(g, %r)
     M.configure(M.default_config(path, **over))
     tr = gen.make_traces(path, nt, npnt, sr, sig, seed, 0.0, 0.0, acc)
@@ -55,3 +57,45 @@ def test_retry_tiers_equal_first_tier(graph_dir, tiers, direct):
     p = subprocess.run([sys.executable, '-c', CHILD % (ROOT, graph_dir)], env=env, capture_output=True, text=True,
                        timeout=240)
     assert p.returncode == 0 and 'tiers ok' in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
+
+
+GENERAL_CHILD = r'''
+import sys
+sys.path.insert(0, %r)
+from oracle import pyoracle as po
+from oracle.compare import compare
+from reporter_amd import matcher as M
+from reporter_amd import _lib
+from reporter_amd.tools import gen
+cases = [('city', 40, 100, 15, 10.0, 2, 0.0, 0.0, None, {'turn_penalty_factor': 0}),
+         ('metro', 30, 60, 60, 50.0, 4, 0.0, 0.0, 50.0, {'search_radius': 200, 'max_search_radius': 200,
+                                                      'turn_penalty_factor': 0}),
+         ('metro', 40, 100, 15, 10.0, 5, 0.25, 0.15, None, {})]
+for g, nt, npnt, sr, sig, seed, fb, fp, acc, over in cases:
+    path = gen.graph_path(g, %r)
+    M.configure(M.default_config(path, **over))
+    tr = gen.make_traces(path, nt, npnt, sr, sig, seed, fb, fp, acc)
+    m = M.Matcher()
+    r = m.match_batch(tr, copy_out=True)
+    assert r.status == 0, r.status
+    c = [int(r.counters[k]) for k in range(24)]
+    gen_searches = int(r.route_tier_work[6][0])
+    assert c[3] == 0 and gen_searches > 0, (c, gen_searches)  # nothing in the LDS tiers, all in k_general
+    got = _lib.result_to_numpy(r)
+    want = po.match_batch(po.Graph(path), tr, po.params(**over), threads=8)
+    errors, stats = compare(got, want)
+    assert not errors, errors
+print('general ok')
+'''
+
+
+def test_general_search_equals_oracle(graph_dir):
+    """libotr_generalcheck.so (-DOTR_FORCE_GENERAL) runs EVERY route search and winner
+    path in the global-memory kernel (k_general, edge states, 64-bit labels), also the
+    node searches the LDS tiers normally take: it must equal the oracle field by field."""
+    lib = os.path.join(ROOT, 'reporter_amd', 'libotr_generalcheck.so')
+    assert os.path.exists(lib), 'build first: python -m reporter_amd.build'
+    env = dict(os.environ, OTR_LIB=lib)
+    p = subprocess.run([sys.executable, '-c', GENERAL_CHILD % (ROOT, graph_dir)], env=env, capture_output=True,
+                       text=True, timeout=280)
+    assert p.returncode == 0 and 'general ok' in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]

@@ -73,3 +73,21 @@ def test_struct_layouts_against_c_header(tmp_path):
         assert int(got[cname]) == ctypes.sizeof(cls), cname
         for f in cls._fields_:
             assert int(got['%s.%s' % (cname, f[0])]) == getattr(cls, f[0]).offset, (cname, f[0])
+
+
+def test_result_subset_equals_subset_match(graph_dir):
+    """oracle.compare.subset: the results of a trace subset sliced out of a batch equal
+    matching that subset alone (the property the full-size GPU tests rely on)."""
+    import numpy as np
+    from oracle import pyoracle as po
+    from oracle.compare import compare, subset
+    from reporter_amd.tools import gen
+    path = gen.graph_path('city', graph_dir)
+    tr = gen.make_traces(path, 30, 60, 15, 10.0, 3)
+    prm = po.params(turn_penalty_factor=0)
+    full = po.match_batch(po.Graph(path), tr, prm, threads=8)
+    idx = np.arange(0, 30, 3)
+    errors, stats = compare(subset(full, idx, tr.offsets), po.match_batch(po.Graph(path), tr.subset(idx), prm,
+                                                                            threads=8))
+    assert not errors, errors
+    assert stats['n_seg'] > 0
