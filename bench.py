@@ -68,10 +68,27 @@ def route_bytes(work):
 
 
 def usable_cores():
+    """Host cores this process may use: its CPU affinity, capped by a cgroup CPU quota
+    (cpu.max), which a shared GPU box sets below the machine's core count."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    for path in ('/sys/fs/cgroup/cpu.max',):
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota != 'max':
+                n = min(n, max(1, int(int(quota) / int(period))))
+        except (OSError, ValueError):
+            pass
+    try:  # cgroup v1
+        q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+        p = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+        if q > 0:
+            n = min(n, max(1, q // p))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def main():
@@ -92,6 +109,9 @@ def main():
                          'accuracy 50 m, search radius 200 m; c5mix: C2 with the C5 mode mix '
                          '(60%% auto / 25%% bicycle / 15%% pedestrian) on the metro graph')
     ap.add_argument('--e2e-steps', type=int, default=3, help='host-to-host drop-in steps (0 = skip)')
+    ap.add_argument('--opt', action='append', default=[],
+                    help='A/B only (not the headline config): KEY=VALUE match option override, e.g. '
+                         'max_route_time_factor=0')
     ap.add_argument('--tiles', type=int, default=0,
                     help='privacy > 0: the step also runs the device tile stage (K9 rows, K10 sort + cull, '
                          'simple_reporter.py:176-239) on each matcher (not part of the headline config)')
@@ -147,6 +167,9 @@ def main():
          'c5mix': dict(points=100, rate=15, sigma=10.0, seed=5, bike=0.25, ped=0.15, acc=None, traces=10000,
                        meili=dict(gtt, search_radius=50, gps_accuracy=16.45))}[args.workload]
 
+    for kv in args.opt:
+        k, v = kv.split('=', 1)
+        W['meili'][k] = float(v)
     t0 = time.time()
     if args.workload == 'c3':
         # C3: 1,000,000 uuids "veh%07d" x 100 probes, sharded by
@@ -208,10 +231,10 @@ def main():
     tile_stats = []
     torch.cuda.synchronize()
 
-    def run_part(k):
+    def run_part(k, route_work=False):
         r = matchers[k].match_batch(parts[k], device_arrays=darrs[k], hist_device=hists[k].data_ptr(),
                                     hist_hours=hours, hist_base_time=T_BEGIN, copy_out=False, timing=True,
-                                    tile_rows=args.tiles > 0)
+                                    tile_rows=args.tiles > 0, route_work=route_work)
         if r.status != 0:
             raise RuntimeError('batch status %d (%d traces beyond every search tier)' % (r.status,
                                                                                           r.n_overflow_traces))
@@ -221,8 +244,8 @@ def main():
             tile_stats.append((int(r.n_rows), len(kept), time.perf_counter() - tc))
         return r
 
-    def step():
-        rs = list(pool.map(run_part, range(ns)))
+    def step(route_work=False):
+        rs = list(pool.map(lambda k: run_part(k, route_work), range(ns)))
         torch.sum(torch.stack(hists), dim=0, out=hist)  # combine the per-stream histograms
         if world > 1 and backend == 'nccl':
             dist.reduce_scatter_tensor(hist_out, hist, op=dist.ReduceOp.SUM)
@@ -255,9 +278,23 @@ def main():
     total_probes = float(probes.item())
     value = total_probes * args.steps / elapsed
 
-    # ---- per-kernel work and device time over the timed steps (every stream, every step)
+    # ---- per-kernel device time over the timed steps (every stream, every step); the work
+    # each kernel did comes from one more, instrumented step over the same batch (the
+    # route kernels count their work only on request, OTR_BATCH_ROUTE_WORK: the counting
+    # itself costs ~7% of the first tier).  The path is deterministic, so the counts are
+    # those of every timed step (the bench checks the output segment counts agree).
     rs = results[-1]
-    counters = [sum(int(r.counters[k]) for r in rs) for k in range(len(rs[0].counters))]
+    work_rs = step(route_work=True)
+    barrier()
+    counters = [sum(int(r.counters[k]) for r in work_rs) for k in range(len(rs[0].counters))]
+    if [int(r.counters[7]) for r in work_rs] != [int(r.counters[7]) for r in rs]:
+        raise RuntimeError('instrumented step differs from the timed steps')
+    work_of = {}
+    for r in work_rs:
+        for t in range(8):
+            if int(r.route_tier_code[t]) != 0:
+                w = work_of.setdefault(t, np.zeros(4, np.int64))
+                w += np.array([int(x) for x in r.route_tier_work[t]], np.int64)
     stage_ms = {s: round(float(np.mean([r.kernel_ms[i] for r in rs])), 3) for i, s in enumerate(_lib.STAGES)
                 if rs[0].kernel_ms[i] > 0}
     tiers = {}
@@ -270,7 +307,8 @@ def main():
                 d = tiers.setdefault(t, {'code': code, 'launches': 0, 'ms': 0.0, 'work': np.zeros(4, np.int64)})
                 d['launches'] += 1
                 d['ms'] += float(r.route_tier_ms[t])
-                d['work'] += np.array([int(x) for x in r.route_tier_work[t]], np.int64)
+    for t, d in tiers.items():  # per-launch work of the instrumented step, times the launches
+        d['work'] = work_of.get(t, np.zeros(4, np.int64)) * (d['launches'] // max(1, ns))
     dom_t = max(tiers, key=lambda t: tiers[t]['ms'])
     dom = tiers[dom_t]
     launch_ms = dom['ms'] / dom['launches']
@@ -307,8 +345,8 @@ def main():
         dt = time.perf_counter() - tc
         cpu = {'value': round(sample.n_probes / dt, 1), 'unit': 'probes/s', 'cores': threads, 'kind': 'port',
                'sample': '%d traces x %d probes of the same %s workload through oracle/liboracle.so '
-                         '(scalar C restatement, %d pthreads = the cores this process may use; os.cpu_count() '
-                         '= %d; %.1f s)' % (sample.n_traces, W['points'], args.workload.upper(), threads,
+                         '(scalar C restatement, %d pthreads = the cores this process may use: affinity capped by '
+                         'the cgroup CPU quota; os.cpu_count() = %d; %.1f s)' % (sample.n_traces, W['points'], args.workload.upper(), threads,
                                             os.cpu_count() or 0, dt)}
         # the GPU output of the same traces: this batch (copy-out run, untimed), sliced
         got_full = _lib.result_to_numpy(M.Matcher().match_batch(mine, copy_out=True))

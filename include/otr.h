@@ -115,6 +115,8 @@ typedef struct otr_trace_batch {
 #define OTR_BATCH_TIMING 2     /* record per-kernel HIP-event timings */
 #define OTR_BATCH_COPY_REPORTS 4  /* host copies of segments, reports, stats only (the JSON path) */
 #define OTR_BATCH_TILE_ROWS 8  /* also emit simple_reporter tile rows on device (d_rows / n_rows) */
+#define OTR_BATCH_ROUTE_WORK 16  /* count the LDS route tiers' work (route_tier_work, counters
+                                    3, 4, 9, 10, 13, 14): instrumentation, ~7% of the first tier */
 
 /* One simple_reporter tile line (simple_reporter.py:188-195) in binary form: the line
  * "id,next_id,duration,1,length,queue_length,start,end,source,MODE" of the file
@@ -128,7 +130,7 @@ typedef struct otr_tile_row {
   int32_t duration;    /* int(round(t1 - t0)), Python 2 rounding (:179) */
   int32_t length;
   int32_t queue_length;
-  int32_t pad;
+  int32_t speed_bin;   /* min(int(length / (t1 - t0) * 3.6 / 20), 7): the report's 20 km/h speed bin */
 } otr_tile_row;
 #define OTR_INVALID_SEGMENT_ID 0x3fffffffffffull
 
@@ -182,8 +184,8 @@ typedef struct otr_batch_result {
                                   1 shape segments tested, 2 candidates, 3 settled nodes and
                                   4 relaxed edges (first-tier route launch), 5 search tasks,
                                   6 transition entries, 7 output segments, 8 tile rows,
-                                  9/10 settled/relaxed of the large-table retry, 11 target reads,
-                                  12 source candidates, 13 search rounds,
+                                  9/10 settled/relaxed of the large-table retry, 13 search rounds
+                                  and 14 table keys (first-tier route launch),
                                   16-19 diagnostic-build search phase cycles */
   float kernel_ms[16];         /* OTR_BATCH_TIMING: device time per stage, OTR_STAGE_* */
   int32_t* trace_status;       /* host, per trace (with COPY_OUT / COPY_REPORTS): OTR_OK, or
@@ -213,6 +215,29 @@ int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result*
  * in host memory owned by the matcher (valid until its next call). */
 int otr_tiles_cull(otr_matcher* m, const otr_tile_row* rows, int64_t n, int32_t memory, int32_t privacy,
                    int32_t rules, const otr_tile_row** out, int64_t* n_out);
+
+/* ---- keyed speed histogram -------------------------------------------
+ * One entry per (hour-tile file, segment pair, speed bin) with its observation count:
+ * the per-GPU histogram is the tile rows sort-reduced by that key; GPUs exchange entries
+ * with the rank owning their (hour, tile) file (RCCL all-to-all, simple_reporter.
+ * file_owner) and each owner reduces what it received and applies the privacy cull to
+ * complete pairs (a pair's total count over its bins >= privacy; the reference cull's
+ * trailing-singleton rule belongs to the line-based tile files, otr_tiles_cull). */
+typedef struct otr_hist_entry {
+  uint64_t file;       /* bucket << 25 | level << 22 | tile index, as otr_tile_row.file */
+  uint64_t id;
+  uint64_t next_id;    /* or OTR_INVALID_SEGMENT_ID */
+  uint32_t speed_bin;  /* 20 km/h bins 0..7 */
+  uint32_t count;
+} otr_hist_entry;
+
+/* Sort-reduce n entries (in: host or device memory) by (file, id, next_id, speed_bin),
+ * summing counts; with privacy > 1 also drop the (file, id, next_id) pairs whose total
+ * count is below privacy.  The reduced entries, in key order, are copied to `out`
+ * (out_memory: host or device; room for out_cap entries, n suffices) and *n_out is
+ * their number.  rows_in != 0: the input is n tile rows, count 1 each. */
+int otr_hist_reduce(otr_matcher* m, const void* in, int64_t n, int32_t memory, int32_t rows_in, int32_t privacy,
+                    otr_hist_entry* out, int64_t out_cap, int32_t out_memory, int64_t* n_out);
 
 /* The CSV lines of n (host) rows in order.  OTR_TILE_RULES_SIMPLE: "id,next,duration,1,
  * length,queue,start,end,source,MODE\n" each (simple_reporter.py:188-195).

@@ -16,7 +16,7 @@ import math
 import numpy as np
 
 TILE_ROW = np.dtype([('file', '<u8'), ('id', '<u8'), ('next_id', '<u8'), ('start', '<i8'), ('end', '<i8'),
-                     ('duration', '<i4'), ('length', '<i4'), ('queue_length', '<i4'), ('pad', '<i4')])
+                     ('duration', '<i4'), ('length', '<i4'), ('queue_length', '<i4'), ('speed_bin', '<i4')])
 INVALID_SEGMENT_ID = 0x3fffffffffff
 NO_ID = 0xFFFFFFFFFFFFFFFF
 
@@ -24,6 +24,12 @@ NO_ID = 0xFFFFFFFFFFFFFFFF
 def _py2_round_int(x):
     f = math.floor(x)
     return int(f + 1 if x - f >= 0.5 else f) if x >= 0 else -_py2_round_int(-x)
+
+
+def speed_bin(length, t0, t1):
+    """The report's 20 km/h speed bin (0..7) carried by the rows (otr_tile_row.speed_bin)."""
+    kmh = (length / (t1 - t0)) * 3.6
+    return min(max(int(kmh / 20.0), 0), 7)
 
 
 def rows_from_reports(res, first_time, last_time, q=3600):
@@ -44,9 +50,10 @@ def rows_from_reports(res, first_time, last_time, q=3600):
             sid = int(res['rep_id'][k])
             nx = int(res['rep_next'][k])
             nx = INVALID_SEGMENT_ID if nx == NO_ID else nx                    # :193
+            sb = speed_bin(ln, t0, t1)
             for b in range(mn, mx + 1):                                       # :188
                 f = (b << 25) | ((sid & 7) << 22) | ((sid >> 3) & 0x3FFFFF)    # :189-191
-                out.append((f, sid, nx, start, end, duration, ln, qu, 0))
+                out.append((f, sid, nx, start, end, duration, ln, qu, sb))
     return np.array(out, dtype=TILE_ROW) if out else np.zeros(0, TILE_ROW)
 
 
@@ -113,7 +120,8 @@ def stream_rows_from_reports(res, q=3600):
             nx = INVALID_SEGMENT_ID if nx == NO_ID else nx                    # Segment.java:26
             for b in range(int(t0) // q, int(t1) // q + 1):                   # getTiles: (long) casts
                 f = (b << 25) | ((sid & 7) << 22) | ((sid >> 3) & 0x3FFFFF)
-                out.append((f, sid, nx, int(math.floor(t0)), int(math.ceil(t1)), _java_round(t1 - t0), ln, qu, 0))
+                out.append((f, sid, nx, int(math.floor(t0)), int(math.ceil(t1)), _java_round(t1 - t0), ln, qu,
+                            speed_bin(ln, t0, t1)))
     return np.array(out, dtype=TILE_ROW) if out else np.zeros(0, TILE_ROW)
 
 

@@ -17,6 +17,7 @@ OTR_BATCH_COPY_OUT = 1
 OTR_BATCH_TIMING = 2
 OTR_BATCH_COPY_REPORTS = 4
 OTR_BATCH_TILE_ROWS = 8
+OTR_BATCH_ROUTE_WORK = 16
 OTR_TILE_RULES_SIMPLE = 0
 OTR_TILE_RULES_STREAM = 1
 OTR_INGEST_SHARD = 0
@@ -36,7 +37,7 @@ STAGES = ['states', 'candidates', 'link', 'route', 'route_big', 'viterbi', 'path
 EXPORTS = ['otr_configure', 'otr_configure_json', 'otr_matcher_new', 'otr_matcher_free', 'otr_match',
            'otr_report', 'otr_report_segments', 'otr_free', 'otr_last_error', 'otr_match_batch',
            'otr_graph_info', 'otr_matcher_stream', 'otr_device', 'otr_report_batch', 'otr_coalesce',
-           'otr_tiles_cull', 'otr_tiles_format', 'otr_ingest', 'otr_report_lists_device']
+           'otr_tiles_cull', 'otr_tiles_format', 'otr_ingest', 'otr_report_lists_device', 'otr_hist_reduce']
 
 
 class TraceBatch(ctypes.Structure):
@@ -91,9 +92,12 @@ class BatchResult(ctypes.Structure):
                 ('route_tier_work', (ctypes.c_uint64 * 4) * 8)]
 
 
+# otr_hist_entry (include/otr.h), 32 bytes
+HIST_ENTRY = np.dtype([('file', '<u8'), ('id', '<u8'), ('next_id', '<u8'), ('speed_bin', '<u4'), ('count', '<u4')])
+
 # otr_tile_row (include/otr.h), 56 bytes
 TILE_ROW = np.dtype([('file', '<u8'), ('id', '<u8'), ('next_id', '<u8'), ('start', '<i8'), ('end', '<i8'),
-                     ('duration', '<i4'), ('length', '<i4'), ('queue_length', '<i4'), ('pad', '<i4')])
+                     ('duration', '<i4'), ('length', '<i4'), ('queue_length', '<i4'), ('speed_bin', '<i4')])
 
 
 _L = None

@@ -376,6 +376,26 @@ int otr_tiles_cull(otr_matcher* m, const otr_tile_row* rows, int64_t n, int32_t 
   return rc;
 }
 
+// keyed speed histogram: per-GPU sort-reduce and the owner's merge + privacy cull
+int otr_hist_reduce(otr_matcher* m, const void* in, int64_t n, int32_t memory, int32_t rows_in, int32_t privacy,
+                    otr_hist_entry* out, int64_t out_cap, int32_t out_memory, int64_t* n_out) {
+  if (!m || !n_out || (n > 0 && (!in || !out))) {
+    g_last_error = "null argument";
+    return OTR_BAD_REQUEST;
+  }
+  std::string err;
+  const otr_hist_entry* dev = nullptr;
+  int rc = m->m.hist_reduce(in, n, memory, rows_in, privacy, &dev, n_out, &err);
+  if (rc == OTR_OK && *n_out > out_cap) {
+    err = "otr_hist_reduce: output buffer too small";
+    rc = OTR_BAD_REQUEST;
+  }
+  if (rc == OTR_OK && *n_out > 0)
+    rc = m->m.copy_out(out, dev, sizeof(otr_hist_entry) * (size_t)*n_out, out_memory, &err);
+  if (rc != OTR_OK) g_last_error = err;
+  return rc;
+}
+
 // simple_reporter.py:140-160 (shard lines), :99-111 (raw feed), Formatter.java:103-114
 int otr_ingest(otr_matcher* m, const char* text, int64_t len, int32_t memory, const otr_ingest_format* fmt,
                otr_ingest_result* out) {

@@ -156,7 +156,13 @@ __device__ inline uint4 ld16(const uint4* p) {
   return r;
 }
 
-constexpr int kShards = 64;  // device counters are sharded [kind][64] to avoid one hot address
+constexpr int kShards = 64;  // path-buffer regions and bump cursors are sharded 64 ways
+// device work counters: [bank][kind][kCShards], a wave adds to shard blockIdx % kCShards.
+// 256 shards spread one kind over 16 cache lines: with 64 (4 lines a kind) the route
+// kernels' end-of-wave atomics queued on the L2 lines (k_route<160,2> 15.1 -> 13.9 ms
+// without them, tools/ab_libs.sh); k_ctr_reduce folds the shards before the copy-out.
+constexpr int kCShards = 256;
+__device__ inline int cshard() { return (int)(blockIdx.x & (kCShards - 1)); }
 constexpr uint32_t kAdjDstMask = 0x0FFFFFFFu;
 constexpr uint32_t kAdjMore = 0x80000000u;
 

@@ -379,7 +379,7 @@ enum Slot {
   S_C_ROUTE_OFF, S_C_SEG_OFF, S_C_WAY_OFF, S_C_REP_OFF, S_C_ARGS, S_C_ROUTE, S_C_SEG_ID, S_C_SEG_START,
   S_C_SEG_END, S_C_SEG_LEN, S_C_SEG_QUEUE, S_C_SEG_INTERNAL, S_C_SEG_BSHAPE, S_C_SEG_ESHAPE, S_C_SEG_WAY_N,
   S_C_SEG_WAY, S_C_SEG_WAY_OFF, S_C_REP_ID, S_C_REP_NEXT, S_C_REP_T0, S_C_REP_T1, S_C_REP_LEN, S_C_REP_QUEUE,
-  S_TASK_REC, S_BT, S_CPREP_T, S_TRANS_TC, S_TURN, S_LIST2, S_GFLAG, S_IN_TEXT, S_IN_CNT, S_IN_CSCAN, S_IN_NL, S_IN_HASH, S_IN_UOFF, S_IN_ULEN, S_IN_TIME, S_IN_LAT, S_IN_LON,
+  S_TASK_REC, S_BT, S_CPREP_T, S_TRANS_TC, S_TURN, S_LIST2, S_GFLAG, S_HE_IN, S_HE_SORTED, S_HE_RED, S_HE_OUT, S_IN_TEXT, S_IN_CNT, S_IN_CSCAN, S_IN_NL, S_IN_HASH, S_IN_UOFF, S_IN_ULEN, S_IN_TIME, S_IN_LAT, S_IN_LON,
   S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
@@ -482,6 +482,21 @@ __global__ void k_step_list(int64_t n_states, const int64_t* prev, const uint8_t
   block_append(s < n_states && cand_count[s] > 0 && prev[s] >= 0 && !brk[s], s, list, count);
 }
 
+// work counters: fold the kCShards shards of every (bank, kind) into one value before the
+// copy-out (one block of kCShards threads per pair)
+__global__ __launch_bounds__(kCShards) void k_ctr_fold(const unsigned long long* in, unsigned long long* out) {
+  __shared__ unsigned long long part[kCShards / OTR_WAVE];
+  unsigned long long v = in[(size_t)blockIdx.x * kCShards + threadIdx.x];
+  for (int o = OTR_WAVE / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (lane_id() == 0) part[threadIdx.x / OTR_WAVE] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kCShards / OTR_WAVE; ++w) t += part[w];
+    out[blockIdx.x] = t;
+  }
+}
+
 static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 
 // Retry tiers of the route search after the first (160-slot, 2 per wave) tier, as
@@ -578,12 +593,13 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   }
   out->n_probes = N;
   h_trace_status.assign(T, OTR_OK);
-  // counter banks of OTR_COUNTERS kinds x kShards: 0 the batch (and the first route
-  // tier), 2..6 the LDS retry tiers, 8..9 the global-memory tiers
-  const size_t bank = (size_t)OTR_COUNTERS * kShards;
-  const size_t n_ctr = 10 * bank;
-  unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, n_ctr);
-  HIPCHK(hipMemsetAsync(d_counters, 0, n_ctr * 8, stream));
+  // counter banks of OTR_COUNTERS kinds x kCShards: 0 the batch (and the first route
+  // tier), 2..6 the LDS retry tiers, 8..9 the global-memory tiers; folded at the end
+  // into n_ctr values behind them
+  const size_t bank = (size_t)OTR_COUNTERS * kCShards;
+  const size_t n_ctr = 10 * (size_t)OTR_COUNTERS;
+  unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, 10 * bank + n_ctr);
+  HIPCHK(hipMemsetAsync(d_counters, 0, 10 * bank * 8, stream));
   size_t scan_bytes = 0;
   auto scan = [&](const int64_t* src, int64_t* dst_np1, int64_t n) -> int {
     // dst[0] = 0, dst[1..n] = inclusive prefix sums
@@ -799,12 +815,15 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     tb(OTR_STAGE_ROUTE);
     // two searches per wave (CAP 160 tables); wider steps and overflows retry below
     static const int route_g = getenv("OTR_ROUTE_G") ? atoi(getenv("OTR_ROUTE_G")) : 2;  // A/B knob
+    // the LDS tiers count their work only when asked (OTR_BATCH_ROUTE_WORK): the end-of-
+    // wave counter atomics cost ~7% of the first tier (tools/ab_libs.sh)
+    unsigned long long* rwork = (in->flags & OTR_BATCH_ROUTE_WORK) ? d_counters : nullptr;
     if (route_g == 2) {
       const int64_t units = (NT + 1) / 2;
-      k_route<160, 2, false><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
+      k_route<160, 2, false><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, ra, rwork);
       out->route_tier_code[0] = 1602;
     } else {
-      k_route<256, 1, false><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, d_counters);
+      k_route<256, 1, false><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, rwork);
       out->route_tier_code[0] = 2561;
     }
     te(OTR_STAGE_ROUTE);
@@ -824,7 +843,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.list_count = c;
-      unsigned long long* rcn = d_counters + (2 + tier) * bank;
+      unsigned long long* rcn = rwork ? d_counters + (2 + tier) * bank : nullptr;
       out->route_tier_code[1 + tier] = tiers[tier];
       if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier)], stream);
       switch (tiers[tier]) {
@@ -1061,7 +1080,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   ha.base_time = in->hist_base_time;
   ha.hours = in->hist_hours;
   ha.n_segments = g.n_segments;
-  ha.n_rows = d_counters + 8 * kShards;
+  ha.n_rows = d_counters + 8 * kCShards;
   size_t hist_len = (size_t)(in->hist_hours > 0 ? in->hist_hours : 0) * g.n_segments * OTR_HIST_BINS;
   ha.hist = hist_len ? (in->hist_device ? in->hist_device : need<uint32_t>(S_HIST, hist_len)) : nullptr;
   if (hist_len) HIPCHK(hipMemsetAsync(ha.hist, 0, hist_len * 4, stream));
@@ -1097,7 +1116,8 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   HIPCHK(hipGetLastError());
   std::vector<unsigned long long> hc(n_ctr);
   unsigned long long h_fail[2] = {0ull, 0ull};  // route tasks / paths beyond every search tier
-  HIPCHK(hipMemcpyAsync(hc.data(), d_counters, n_ctr * 8, hipMemcpyDeviceToHost, stream));
+  k_ctr_fold<<<(unsigned)n_ctr, kCShards, 0, stream>>>(d_counters, d_counters + 10 * bank);
+  HIPCHK(hipMemcpyAsync(hc.data(), d_counters + 10 * bank, n_ctr * 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipMemcpyAsync(&h_fail[0], cnt + 10, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipMemcpyAsync(&h_fail[1], cnt + 18, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
@@ -1122,9 +1142,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     }
   }
   auto ctr = [&](int b, int k) {
-    unsigned long long v = 0;
-    for (int sh = 0; sh < kShards; ++sh) v += hc[(size_t)b * bank + (size_t)k * kShards + sh];
-    return v;
+    return hc[(size_t)b * OTR_COUNTERS + (size_t)k];
   };
   for (int k = 0; k < OTR_COUNTERS; ++k) out->counters[k] = ctr(0, k);
   // per route kernel: searches, settled, relaxed, transition entries (banks 0, 2..6, 8..9)
@@ -1471,6 +1489,175 @@ int Matcher::tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int pri
   HIPCHK(hipGetLastError());
   *out = h_tile_rows.data();
   *n_out = nk;
+  return OTR_OK;
+}
+
+// ---- keyed speed histogram (include/otr.h otr_hist_reduce) -----------------
+__global__ void k_rows_to_entries(const otr_tile_row* r, int64_t n, otr_hist_entry* e) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  otr_hist_entry x;
+  x.file = r[i].file;
+  x.id = r[i].id;
+  x.next_id = r[i].next_id;
+  x.speed_bin = (uint32_t)r[i].speed_bin;
+  x.count = 1u;
+  e[i] = x;
+}
+__global__ void k_entry_key(const otr_hist_entry* e, const int32_t* perm, int64_t n, int field,
+                            unsigned long long* key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const otr_hist_entry& x = e[perm[i]];
+  key[i] = field == 0 ? x.file : (field == 1 ? x.id : (field == 2 ? x.next_id : (unsigned long long)x.speed_bin));
+}
+__global__ void k_gather_entries(const otr_hist_entry* in, const int32_t* idx, int64_t n, otr_hist_entry* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[idx[i]];
+}
+// run heads over sorted entries: pair = 0 the full key, 1 the (file, id, next_id) pair
+__global__ void k_entry_heads(const otr_hist_entry* e, int64_t n, int pair, int64_t* head) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool h = i == 0;
+  if (!h) {
+    const otr_hist_entry &a = e[i - 1], &b = e[i];
+    h = a.file != b.file || a.id != b.id || a.next_id != b.next_id || (!pair && a.speed_bin != b.speed_bin);
+  }
+  head[i] = h ? 1 : 0;
+}
+__global__ void k_entry_counts(const otr_hist_entry* e, int64_t n, int64_t* c) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) c[i] = e[i].count;
+}
+// the last entry of every run carries its run's count sum: csum = inclusive scan of counts,
+// run r spans [start_r, next start); out[r] = entry at start_r with count = the sum
+__global__ void k_entry_reduce(const otr_hist_entry* e, int64_t n, const int64_t* run_start, int64_t n_runs,
+                               const int64_t* csum, otr_hist_entry* out) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_runs) return;
+  const int64_t s = run_start[r], t = r + 1 < n_runs ? run_start[r + 1] : n;
+  otr_hist_entry x = e[s];
+  const int64_t tot = csum[t - 1] - (s > 0 ? csum[s - 1] : 0);
+  x.count = (uint32_t)(tot < 0xFFFFFFFFll ? tot : 0xFFFFFFFFll);
+  out[r] = x;
+}
+// privacy: keep an entry when its pair's total count (over its bins) reaches privacy
+__global__ void k_entry_keep(const int64_t* pair_pos, const int64_t* pair_start, int64_t n_pairs, int64_t n,
+                             const int64_t* csum, int32_t privacy, int64_t* keep) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t p = pair_pos[i] - 1;
+  const int64_t s = pair_start[p], t = p + 1 < n_pairs ? pair_start[p + 1] : n;
+  const int64_t tot = csum[t - 1] - (s > 0 ? csum[s - 1] : 0);
+  keep[i] = tot >= (int64_t)privacy ? 1 : 0;
+}
+
+int Matcher::copy_out(void* dst, const void* src, size_t bytes, int dst_memory, std::string* err) {
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, dst_memory == OTR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                        stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  return OTR_OK;
+}
+
+int Matcher::hist_reduce(const void* in, int64_t n, int memory, int rows_in, int privacy, const otr_hist_entry** out,
+                         int64_t* n_out, std::string* err) {
+  GraphState& gs = graph_state();
+  HIPCHK(hipSetDevice(gs.device));
+  if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  *out = nullptr;
+  *n_out = 0;
+  if (n <= 0) return OTR_OK;
+  if (n >= (int64_t)INT32_MAX) {
+    if (err) *err = "too many histogram entries for one call";
+    return OTR_BAD_REQUEST;
+  }
+  auto fail = [&](const char* what) {
+    if (err) *err = what;
+    return OTR_DEVICE_ERROR;
+  };
+  otr_hist_entry* e_in = need<otr_hist_entry>(S_HE_IN, n);
+  otr_hist_entry* e_sorted = need<otr_hist_entry>(S_HE_SORTED, n);
+  otr_hist_entry* e_red = need<otr_hist_entry>(S_HE_RED, n);
+  otr_hist_entry* e_out = need<otr_hist_entry>(S_HE_OUT, n);
+  int32_t* perm_a = need<int32_t>(S_IDX_A, n);
+  int32_t* perm_b = need<int32_t>(S_IDX_B, n);
+  unsigned long long* key_a = need<unsigned long long>(S_KEY_A, n);
+  unsigned long long* key_b = need<unsigned long long>(S_KEY_B, n);
+  int64_t* head = need<int64_t>(S_FILE_HEAD, n);
+  int64_t* pos = need<int64_t>(S_POS_SCAN, n);
+  int64_t* rstart = need<int64_t>(S_FILE_START, n);
+  int64_t* csum = need<int64_t>(S_KEEP, n);
+  if (!e_in || !e_sorted || !e_red || !e_out || !perm_a || !perm_b || !key_a || !key_b || !head || !pos || !rstart ||
+      !csum)
+    return fail("device allocation failed (histogram)");
+  const hipMemcpyKind kind = memory == OTR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  if (rows_in) {
+    otr_tile_row* rows = need<otr_tile_row>(S_ROWS_IN, n);
+    if (!rows) return fail("device allocation failed (histogram)");
+    HIPCHK(hipMemcpyAsync(rows, in, sizeof(otr_tile_row) * n, kind, stream));
+    k_rows_to_entries<<<grid_for(n, 256), 256, 0, stream>>>(rows, n, e_in);
+  } else {
+    HIPCHK(hipMemcpyAsync(e_in, in, sizeof(otr_hist_entry) * n, kind, stream));
+  }
+  const int ni = (int)n;
+  size_t tb_sort = 0, tb_scan = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, key_a, key_b, perm_a, perm_b, ni, 0, 64, stream));
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb_scan, head, pos, ni, stream));
+  void* tmp = need<char>(S_SORT_TMP, std::max(tb_sort, tb_scan));
+  if (!tmp) return fail("device allocation failed (histogram)");
+  // LSD: speed bin, next id, id, file (stable passes over a permutation)
+  k_iota_i32<<<grid_for(n, 256), 256, 0, stream>>>(perm_a, n);
+  for (int f = 3; f >= 0; --f) {
+    k_entry_key<<<grid_for(n, 256), 256, 0, stream>>>(e_in, perm_a, n, f, key_a);
+    size_t tb = tb_sort;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key_a, key_b, perm_a, perm_b, ni, 0, f == 3 ? 3 : 64,
+                                              stream));
+    std::swap(perm_a, perm_b);
+  }
+  k_gather_entries<<<grid_for(n, 256), 256, 0, stream>>>(e_in, perm_a, n, e_sorted);
+  // runs of equal keys -> one entry each, counts summed
+  k_entry_heads<<<grid_for(n, 256), 256, 0, stream>>>(e_sorted, n, 0, head);
+  size_t tb = tb_scan;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, head, pos, ni, stream));
+  k_scatter_index<<<grid_for(n, 256), 256, 0, stream>>>(head, pos, n, rstart);
+  k_entry_counts<<<grid_for(n, 256), 256, 0, stream>>>(e_sorted, n, head);  // head reused: counts
+  tb = tb_scan;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, head, csum, ni, stream));
+  int64_t nr = 0;
+  HIPCHK(hipMemcpyAsync(&nr, pos + (n - 1), 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  if (nr < 1 || nr > n) return fail("histogram run split failed");
+  k_entry_reduce<<<grid_for(nr, 256), 256, 0, stream>>>(e_sorted, n, rstart, nr, csum, e_red);
+  otr_hist_entry* result = e_red;
+  int64_t nres = nr;
+  if (privacy > 1) {
+    // pairs over the reduced entries: heads, totals, keep flags, compaction
+    const int nri = (int)nr;
+    k_entry_heads<<<grid_for(nr, 256), 256, 0, stream>>>(e_red, nr, 1, head);
+    tb = tb_scan;
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, head, pos, nri, stream));
+    k_scatter_index<<<grid_for(nr, 256), 256, 0, stream>>>(head, pos, nr, rstart);
+    int64_t np = 0;
+    HIPCHK(hipMemcpyAsync(&np, pos + (nr - 1), 8, hipMemcpyDeviceToHost, stream));
+    k_entry_counts<<<grid_for(nr, 256), 256, 0, stream>>>(e_red, nr, head);
+    tb = tb_scan;
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, head, csum, nri, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    int64_t* keep = head;  // counts no longer needed
+    k_entry_keep<<<grid_for(nr, 256), 256, 0, stream>>>(pos, rstart, np, nr, csum, privacy, keep);
+    int64_t* kpos = rstart;  // pair starts no longer needed after k_entry_keep
+    tb = tb_scan;
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, keep, kpos, nri, stream));
+    k_scatter_flagged<otr_hist_entry><<<grid_for(nr, 256), 256, 0, stream>>>(e_red, keep, kpos, nr, e_out);
+    HIPCHK(hipMemcpyAsync(&nres, kpos + (nr - 1), 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    result = e_out;
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(stream));
+  *out = result;
+  *n_out = nres;
   return OTR_OK;
 }
 

@@ -234,9 +234,9 @@ __device__ bool g_search(const DevGraph& G, const GTask& T, uint32_t* key, unsig
   }
   __syncthreads();
   if (work) {  // this tier's counter bank (kinds 3 settled, 4 relaxed)
-    const int sh = blockIdx.x & (kShards - 1);
-    atomicAdd(&work[4 * kShards + sh], my_relaxed);
-    if (tid == 0) atomicAdd(&work[3 * kShards + sh], expanded);
+    const int sh = cshard();
+    atomicAdd(&work[4 * kCShards + sh], my_relaxed);
+    if (tid == 0) atomicAdd(&work[3 * kCShards + sh], expanded);
   }
   return *s_ovf == 0;
 }
@@ -332,9 +332,9 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
       if (ok) {
         const int Kb = a.cand_count[s];
         if (a.counters && tid == 0) {  // kinds 5 transition entries, 6 searches
-          const int sh = blockIdx.x & (kShards - 1);
-          atomicAdd(&a.counters[5 * kShards + sh], (unsigned long long)Kb * (unsigned long long)__popcll(mask));
-          atomicAdd(&a.counters[6 * kShards + sh], 1ull);
+          const int sh = cshard();
+          atomicAdd(&a.counters[5 * kCShards + sh], (unsigned long long)Kb * (unsigned long long)__popcll(mask));
+          atomicAdd(&a.counters[6 * kCShards + sh], 1ull);
         }
         uint32_t* trow = a.trans + a.trans_off[s];
         uint32_t* crow = a.trans_tc + a.trans_off[s];

@@ -306,17 +306,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
 #ifdef OTR_STAMPS_CAND
   if (lane == 0 && counters) {
     const unsigned long long cs3 = __builtin_amdgcn_s_memtime();
-    const int sh = blockIdx.x & (kShards - 1);
-    atomicAdd(&counters[16 * kShards + sh], cs1 - cs0);
-    atomicAdd(&counters[17 * kShards + sh], cs2 - cs1);
-    atomicAdd(&counters[18 * kShards + sh], cs3 - cs2);
+    const int sh = cshard();
+    atomicAdd(&counters[16 * kCShards + sh], cs1 - cs0);
+    atomicAdd(&counters[17 * kCShards + sh], cs2 - cs1);
+    atomicAdd(&counters[18 * kCShards + sh], cs3 - cs2);
   }
 #endif
   if (lane == 0 && counters) {
-    const int sh = blockIdx.x & (kShards - 1);
-    atomicAdd(&counters[0 * kShards + sh], (unsigned long long)((r1 - r0 + 1) * (c1 - c0 + 1)));
-    atomicAdd(&counters[1 * kShards + sh], tests);
-    atomicAdd(&counters[2 * kShards + sh], (unsigned long long)n);
+    const int sh = cshard();
+    atomicAdd(&counters[0 * kCShards + sh], (unsigned long long)((r1 - r0 + 1) * (c1 - c0 + 1)));
+    atomicAdd(&counters[1 * kCShards + sh], tests);
+    atomicAdd(&counters[2 * kCShards + sh], (unsigned long long)n);
   }
 }
 
@@ -868,7 +868,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
   }
 #ifdef OTR_STAMPS
   if (stamps && threadIdx.x == 0)
-    for (int q = 0; q < 4; ++q) atomicAdd(&stamps[q * kShards + (blockIdx.x & (kShards - 1))], cyc[q]);
+    for (int q = 0; q < 4; ++q) atomicAdd(&stamps[q * kCShards + cshard()], cyc[q]);
 #endif
   if (settled) *settled += my_settled;
   if (relaxed) *relaxed += my_relaxed;
@@ -1004,15 +1004,12 @@ __global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const uns
 // LIST = false: the first tier, one unit per block over all tasks (XCD-mapped); LIST =
 // true: a retry tier, a fixed grid striding over the device-side task list (its length
 // never crosses to the host)
+// one unit = G search tasks of the wave (ordinal w of the task range or list)
 template <int CAP, int G, bool LIST>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR_ROUTE2_WAVES : 8, G == 2 ? OTR_ROUTE2_WAVES : 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
+__device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& a, unsigned long long* counters,
+                                           SearchLds<CAP, false>* Ls, int64_t w, int64_t n_tasks) {
   using Gr = Grp<G>;
-  __shared__ SearchLds<CAP, false> Ls[G];
   const int lane = Gr::gl();
-  const int64_t n_tasks = LIST ? (int64_t)*a.list_count : a.n_tasks;
-  const int64_t n_units = (n_tasks + G - 1) / G;
-  const int64_t w0 = LIST ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, (n_units + 7) / 8);
-  for (int64_t w = w0; w < n_units; w += (LIST ? (int64_t)gridDim.x : n_units)) {
   const int64_t tw = w * G + Gr::g();
   const bool have = tw < n_tasks;
   const int64_t task = have ? (LIST ? a.task_list[tw] : tw) : 0;
@@ -1068,7 +1065,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   search_init<CAP, false, G>(Ls);
   bool ok = search_run<CAP, false, G>(Ls, gr, H, K, mode_bit, search, root, bmm,
                                       (uint32_t)(a.delta * 1000.0), tnode, tpart, hT, d0min, Kb, &settled, &relaxed,
-                                      &rounds, counters ? counters + 16 * kShards : nullptr) &&
+                                      &rounds, counters ? counters + 16 * kCShards : nullptr) &&
             fits;
 #ifdef OTR_FORCE_RETRY
   if (G == 2 && !LIST) ok = false;  // test build: every first-tier task takes the retry tiers
@@ -1082,10 +1079,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   }
   // ---- transition rows: re-read the step (cached) rather than hold it live through the search
   asm volatile("" ::: "memory");
+  uint32_t ntr = 0;  // transition entries this search wrote (K4), for the work counters
   if (have && (ok || forced)) {
     const uint4 r0 = a.rec[2 * task], r1 = a.rec[2 * task + 1];
     const int64_t s = r0.x;
     const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
+    if (search) ntr = (uint32_t)Kb * (uint32_t)__popcll(mask);
     const int64_t sp = r0.y;
     const int32_t bt = a.bt[s];
     const int md = (int)((r1.y >> 8) & 3u);
@@ -1123,9 +1122,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
 #ifdef OTR_STAMPS
   if (G == 2 && counters && threadIdx.x == 0) {  // task setup and transition rows, wave cycles
     OTR_STAMP(ts_out);
-    const int sh = blockIdx.x & (kShards - 1);
-    atomicAdd(&counters[20 * kShards + sh], ts_set - ts_in);
-    atomicAdd(&counters[21 * kShards + sh], ts_out - ts_srch);
+    const int sh = cshard();
+    atomicAdd(&counters[20 * kCShards + sh], ts_set - ts_in);
+    atomicAdd(&counters[21 * kCShards + sh], ts_out - ts_srch);
   }
 #endif
   if (counters) {
@@ -1134,39 +1133,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
     relaxed = wave_sum_u32((uint32_t)relaxed);
     rounds = wave_sum_u32((uint32_t)rounds);
     const int nk = have && search ? L.n_keys : 0;
-    const int nsrc = have ? __popcll(a.task_mask[task]) : 0;
-    unsigned long long kk = 0, c96 = 0, c64 = 0, c128 = 0, kb = 0, ns = 0, ntr = 0, nsearch = 0;
+    unsigned long long kk = 0, ntrw = 0, nsearch = 0;
     for (int q = 0; q < G; ++q) {
-      const int nkq = __builtin_amdgcn_readlane(nk, q * Gr::GL);
-      kk += (unsigned long long)nkq;
-      c96 += nkq > 96;
-      c64 += nkq > 64;
-      c128 += nkq > 128;
-      const unsigned long long kbq = (unsigned long long)__builtin_amdgcn_readlane(have ? Kb : 0, q * Gr::GL);
-      const unsigned long long nsq = (unsigned long long)__builtin_amdgcn_readlane(nsrc, q * Gr::GL);
-      kb += kbq;
-      ns += nsq;
-      if (__builtin_amdgcn_readlane((int)(have && search), q * Gr::GL)) {
-        ntr += kbq * nsq;  // transition entries this search wrote (K4)
-        ++nsearch;
-      }
+      kk += (unsigned long long)__builtin_amdgcn_readlane(nk, q * Gr::GL);
+      ntrw += (unsigned long long)__builtin_amdgcn_readlane(ntr, q * Gr::GL);
+      nsearch += (unsigned long long)__builtin_amdgcn_readlane((int)(have && search), q * Gr::GL);
     }
     if (threadIdx.x == 0) {
-      const int sh = blockIdx.x & (kShards - 1);
-      atomicAdd(&counters[3 * kShards + sh], settled);
-      atomicAdd(&counters[4 * kShards + sh], relaxed);
-      atomicAdd(&counters[5 * kShards + sh], ntr);
-      atomicAdd(&counters[6 * kShards + sh], nsearch);
-      atomicAdd(&counters[11 * kShards + sh], kb);
-      atomicAdd(&counters[12 * kShards + sh], ns);
-      atomicAdd(&counters[13 * kShards + sh], rounds);
-      atomicAdd(&counters[14 * kShards + sh], kk);
-      if (c96) atomicAdd(&counters[15 * kShards + sh], c96);
-      if (c64) atomicAdd(&counters[22 * kShards + sh], c64);
-      if (c128) atomicAdd(&counters[23 * kShards + sh], c128);
+      const int sh = cshard();
+      atomicAdd(&counters[3 * kCShards + sh], settled);
+      atomicAdd(&counters[4 * kCShards + sh], relaxed);
+      atomicAdd(&counters[5 * kCShards + sh], ntrw);
+      atomicAdd(&counters[6 * kCShards + sh], nsearch);
+      atomicAdd(&counters[13 * kCShards + sh], rounds);
+      atomicAdd(&counters[14 * kCShards + sh], kk);
     }
   }
-  __syncthreads();
+}
+
+template <int CAP, int G, bool LIST>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR_ROUTE2_WAVES : 8, G == 2 ? OTR_ROUTE2_WAVES : 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
+  __shared__ SearchLds<CAP, false> Ls[G];
+  if (!LIST) {  // the first tier: one unit per block, XCD-mapped (no loop: fewer live registers)
+    const int64_t n_units = (a.n_tasks + G - 1) / G;
+    const int64_t w = xcd_remap(blockIdx.x, (n_units + 7) / 8);
+    if (w < n_units) route_unit<CAP, G, LIST>(gr, a, counters, Ls, w, a.n_tasks);
+    return;
+  }
+  const int64_t n_tasks = (int64_t)*a.list_count;
+  const int64_t n_units = (n_tasks + G - 1) / G;
+  for (int64_t w = blockIdx.x; w < n_units; w += gridDim.x) {
+    route_unit<CAP, G, LIST>(gr, a, counters, Ls, w, n_tasks);
+    __syncthreads();  // the next unit re-initialises the tables
   }
 }
 
@@ -1870,7 +1868,7 @@ __global__ __launch_bounds__(64) void k_segments(DevGraph g, SegArgs a, unsigned
     a.stats[7 * t + 6] = 0;
     a.stats_len[2 * t] = rs.lengths[0];
     a.stats_len[2 * t + 1] = rs.lengths[1];
-    if (counters) atomicAdd(&counters[7 * kShards + (blockIdx.x & (kShards - 1))], (unsigned long long)ng);
+    if (counters) atomicAdd(&counters[7 * kCShards + cshard()], (unsigned long long)ng);
   }
 }
 
@@ -1983,7 +1981,7 @@ __global__ void k_histogram(HistArgs a) {
         atomicAdd(&a.hist[((size_t)h * a.n_segments + seg) * OTR_HIST_BINS + bin], 1u);
     }
   }
-  if (rows) atomicAdd(&a.n_rows[blockIdx.x & (kShards - 1)], rows);
+  if (rows) atomicAdd(&a.n_rows[cshard()], rows);
 }
 
 // ------------------------------------------------------------------------------
@@ -2036,6 +2034,9 @@ __global__ void k_tile_rows(TileArgs a) {
         if (!sp.ok) continue;
       }
       const unsigned long long id = a.rep_id[co + r], nx = a.rep_next[co + r];
+      // the report's 20 km/h speed bin, as K8 bins it (oracle/tiles.py speed_bin)
+      const double bq = (((double)len / (t1 - t0)) * 3.6) / 20.0;
+      const int speed_bin = bq >= (double)(OTR_HIST_BINS - 1) ? OTR_HIST_BINS - 1 : (bq < 0.0 ? 0 : (int)bq);
       for (int64_t bk = sp.min_bucket; bk <= sp.max_bucket; ++bk, ++k) {
         if (!a.rows) continue;
         otr_tile_row row;
@@ -2047,7 +2048,7 @@ __global__ void k_tile_rows(TileArgs a) {
         row.duration = (int32_t)sp.duration;
         row.length = len;
         row.queue_length = qu;
-        row.pad = 0;
+        row.speed_bin = speed_bin;
         a.rows[k] = row;
       }
     }

@@ -147,12 +147,13 @@ class Matcher:
     def match_batch(self, traces, report_levels=(0, 1), transition_levels=(0, 1), threshold_sec=15,
                     quantisation=3600, hist_base_time=0, hist_hours=0, copy_out=True, timing=False,
                     device_arrays=None, hist_device=None, tile_rows=False, tile_rules=0, host_arrays=None,
-                    copy_reports=False):
+                    copy_reports=False, route_work=False):
         """Match a gen.Traces-like SoA batch.  With device_arrays (dict of device
         pointers: trace_offsets, lat, lon, time, accuracy, mode) the inputs are
         already resident in HBM; host_arrays: the same as host pointers (e.g. pinned
         buffers the caller keeps alive).  copy_reports: segments, reports and stats
-        come back to the host (the JSON path's copy-out)."""
+        come back to the host (the JSON path's copy-out).  route_work: the LDS route
+        tiers count their work (route_tier_work; instrumentation, ~7% of the first tier)."""
         b = _lib.TraceBatch()
         b.n_traces = int(traces.n_traces)
         arrs = device_arrays if device_arrays is not None else host_arrays
@@ -182,7 +183,8 @@ class Matcher:
         b.hist_device = hist_device
         b.tile_rules = int(tile_rules)
         b.flags = (_lib.OTR_BATCH_COPY_OUT if copy_out else 0) | (_lib.OTR_BATCH_TIMING if timing else 0) | \
-            (_lib.OTR_BATCH_TILE_ROWS if tile_rows else 0) | (_lib.OTR_BATCH_COPY_REPORTS if copy_reports else 0)
+            (_lib.OTR_BATCH_TILE_ROWS if tile_rows else 0) | (_lib.OTR_BATCH_COPY_REPORTS if copy_reports else 0) | \
+            (_lib.OTR_BATCH_ROUTE_WORK if route_work else 0)
         r = _lib.BatchResult()
         rc = self._L.otr_match_batch(self._h, ctypes.byref(b), ctypes.byref(r))
         if rc != 0:

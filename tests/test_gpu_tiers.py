@@ -30,7 +30,7 @@ for g, nt, npnt, sr, sig, seed, acc, over in [('city', 40, 100, 15, 10.0, 2, Non
     M.configure(M.default_config(path, **over))
     tr = gen.make_traces(path, nt, npnt, sr, sig, seed, 0.0, 0.0, acc)
     m = M.Matcher()  # owns the host result arrays
-    r = m.match_batch(tr, copy_out=True)
+    r = m.match_batch(tr, copy_out=True, route_work=True)
     assert r.status == 0, r.status
     c = [int(r.counters[k]) for k in range(24)]
     assert c[9] > 0, c  # the retry tiers settled nodes (and wrote every transition row)
@@ -76,7 +76,7 @@ for g, nt, npnt, sr, sig, seed, fb, fp, acc, over in cases:
     M.configure(M.default_config(path, **over))
     tr = gen.make_traces(path, nt, npnt, sr, sig, seed, fb, fp, acc)
     m = M.Matcher()
-    r = m.match_batch(tr, copy_out=True)
+    r = m.match_batch(tr, copy_out=True, route_work=True)
     assert r.status == 0, r.status
     c = [int(r.counters[k]) for k in range(24)]
     gen_searches = int(r.route_tier_work[6][0])

@@ -1,31 +1,26 @@
 #!/usr/bin/env python3
-"""Per-kernel summary (calls, total/avg ns, %) from a rocprofv3 SQLite (rocpd) output, as
-the --stats CSV gives it, with rocPRIM template names shortened.
-
-  python tools/rocpd_stats.py gpurun_out/.../run_results.db > profiles/<name>.csv
-"""
-import re
+"""Per-kernel stats (calls, average / total ns, % of kernel time) from a rocprofv3
+kernel-trace SQLite database (rocpd, the default output format):
+    python tools/rocpd_stats.py gpurun_out/.../run_results.db [out.csv]"""
+import csv
 import sqlite3
 import sys
 
 
-def short(name):
-    if 'rocprim' in name:
-        m = re.search(r'detail::(\w+?)_config<[^,]*, ([\w ]+)(?:, ([\w ]+))?>', name)
-        kind = re.search(r'wrapped_(\w+?)_config', name)
-        return 'rocprim::%s<%s>' % (kind.group(1) if kind else 'kernel', m.group(2) if m else '?') \
-            if kind else re.sub(r'<.*', '', name)[:80]
-    return name
-
-
-def main(path):
-    c = sqlite3.connect(path)
-    rows = list(c.execute('select name, total_calls, total_duration, average, percentage from top_kernels'))
-    print('"Name","Calls","TotalDurationNs","AverageNs","Percentage"')
-    for name, calls, total, avg, pct in rows:
-        # top_kernels reports microseconds; the CSV keeps --stats' nanoseconds
-        print('"%s",%d,%d,%.1f,%.2f' % (short(name).replace('"', "'"), calls, round(total * 1e3), avg * 1e3, pct))
+def stats(db):
+    c = sqlite3.connect(db)
+    q = ('select s.display_name, count(*), avg(d.end - d.start), sum(d.end - d.start) '
+         'from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id = s.id '
+         'group by s.display_name order by sum(d.end - d.start) desc')
+    rows = list(c.execute(q))
+    tot = sum(r[3] for r in rows) or 1
+    return [{'Name': r[0], 'Calls': r[1], 'AverageNs': round(r[2], 1), 'TotalDurationNs': r[3],
+             'Percentage': round(100.0 * r[3] / tot, 3)} for r in rows]
 
 
 if __name__ == '__main__':
-    main(sys.argv[1])
+    rows = stats(sys.argv[1])
+    out = open(sys.argv[2], 'w', newline='') if len(sys.argv) > 2 else sys.stdout
+    w = csv.DictWriter(out, fieldnames=['Name', 'Calls', 'AverageNs', 'TotalDurationNs', 'Percentage'])
+    w.writeheader()
+    w.writerows(rows)
