@@ -91,6 +91,14 @@ def usable_cores():
     return n
 
 
+class _DevBytes:
+    """A device byte range (library-owned) as a torch tensor view, without a copy."""
+
+    def __init__(self, ptr, nbytes):
+        self.__cuda_array_interface__ = {'shape': (int(nbytes),), 'typestr': '|u1', 'data': (int(ptr), False),
+                                         'version': 2}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -112,6 +120,12 @@ def main():
     ap.add_argument('--opt', action='append', default=[],
                     help='A/B only (not the headline config): KEY=VALUE match option override, e.g. '
                          'max_route_time_factor=0')
+    ap.add_argument('--hist', choices=['keyed', 'dense'], default='keyed',
+                    help='keyed (default, SURVEY 8e): tile rows (K9) sort-reduced per GPU into (hour-tile file, '
+                         'segment pair, speed bin) counts, all-to-all to the (hour, tile) owner, owner merge + '
+                         'privacy cull; dense: the [hour][segment][speed] K8 histogram reduce-scattered')
+    ap.add_argument('--privacy', type=int, default=2,
+                    help='owner-side pair cull threshold of the keyed histogram (simple_reporter.py:345 default)')
     ap.add_argument('--tiles', type=int, default=0,
                     help='privacy > 0: the step also runs the device tile stage (K9 rows, K10 sort + cull, '
                          'simple_reporter.py:176-239) on each matcher (not part of the headline config)')
@@ -231,21 +245,72 @@ def main():
     tile_stats = []
     torch.cuda.synchronize()
 
+    keyed = args.hist == 'keyed'
+    EW = _lib.HIST_ENTRY.itemsize
+    ebufs = [torch.zeros(0, dtype=torch.uint8, device=dev) for _ in range(ns)]  # per-stream local entries
+    n_local, n_rows, row_views = [0] * ns, [0] * ns, [None] * ns
+    hist_stats = {}
+
     def run_part(k, route_work=False):
-        r = matchers[k].match_batch(parts[k], device_arrays=darrs[k], hist_device=hists[k].data_ptr(),
-                                    hist_hours=hours, hist_base_time=T_BEGIN, copy_out=False, timing=True,
-                                    tile_rows=args.tiles > 0, route_work=route_work)
+        r = matchers[k].match_batch(parts[k], device_arrays=darrs[k],
+                                    hist_device=None if keyed else hists[k].data_ptr(),
+                                    hist_hours=0 if keyed else hours, hist_base_time=T_BEGIN, copy_out=False,
+                                    timing=True, tile_rows=keyed or args.tiles > 0, route_work=route_work)
         if r.status != 0:
             raise RuntimeError('batch status %d (%d traces beyond every search tier)' % (r.status,
                                                                                           r.n_overflow_traces))
+        n_rows[k] = int(r.n_rows)
+        if keyed and world == 1:  # the only owner: its one reduce takes the rows themselves
+            row_views[k] = (torch.as_tensor(_DevBytes(r.d_rows, int(r.n_rows) * _lib.TILE_ROW.itemsize), device=dev)
+                            if int(r.n_rows) > 0 else torch.zeros(0, dtype=torch.uint8, device=dev))
+        elif keyed:  # this GPU's (file, pair, speed bin) counts, on the matcher's stream
+            if ebufs[k].numel() < int(r.n_rows) * EW:
+                ebufs[k] = torch.empty(int(r.n_rows) * EW * 5 // 4 + EW, dtype=torch.uint8, device=dev)
+            n_local[k] = sr.hist_reduce(matchers[k], r.d_rows, r.n_rows, privacy=1, rows_in=True,
+                                        out=ebufs[k].data_ptr())
         if args.tiles > 0:
             tc = time.perf_counter()
             kept = sr.cull_rows(matchers[k], None, args.tiles, device_ptr=r.d_rows, n=r.n_rows)
             tile_stats.append((int(r.n_rows), len(kept), time.perf_counter() - tc))
         return r
 
+    owned = {'buf': torch.zeros(0, dtype=torch.uint8, device=dev), 'n': 0}
+
+    def keyed_exchange():
+        """§8e: the streams' entries → all-to-all by (hour, tile) owner → the owner's
+        merge + privacy cull (one more sort-reduce, on the first matcher's stream)."""
+        torch.cuda.synchronize()
+        if world == 1:
+            rows = torch.cat(row_views)
+            n_in = rows.numel() // _lib.TILE_ROW.itemsize
+            if owned['buf'].numel() < max(n_in, 1) * EW:
+                owned['buf'] = torch.empty(max(n_in, 1) * EW * 5 // 4, dtype=torch.uint8, device=dev)
+            owned['n'] = sr.hist_reduce(matchers[0], rows.data_ptr(), n_in, privacy=args.privacy, rows_in=True,
+                                        out=owned['buf'].data_ptr())
+            hist_stats.update(rows=int(sum(n_rows)), owned=int(owned['n']))
+            return
+        local_e = torch.cat([ebufs[k][:n_local[k] * EW] for k in range(ns)])
+        if world > 1:
+            send = local_e if backend == 'nccl' else local_e.cpu()
+            recv = sr.exchange_hist(send, world)
+            recv = recv if recv.is_cuda else recv.to(dev)
+        else:
+            recv = local_e
+        n_in = recv.numel() // EW
+        if owned['buf'].numel() < max(n_in, 1) * EW:
+            owned['buf'] = torch.empty(max(n_in, 1) * EW * 5 // 4, dtype=torch.uint8, device=dev)
+        owned['n'] = sr.hist_reduce(matchers[0], recv.data_ptr(), n_in, privacy=args.privacy,
+                                    out=owned['buf'].data_ptr())
+        hist_stats.update(rows=int(sum(n_rows)), local_entries=int(sum(n_local)), received=int(n_in),
+                          owned=int(owned['n']))
+
     def step(route_work=False):
+        hist_stats.clear()
         rs = list(pool.map(lambda k: run_part(k, route_work), range(ns)))
+        if keyed:
+            keyed_exchange()
+            torch.cuda.current_stream().synchronize()
+            return rs
         torch.sum(torch.stack(hists), dim=0, out=hist)  # combine the per-stream histograms
         if world > 1 and backend == 'nccl':
             dist.reduce_scatter_tensor(hist_out, hist, op=dist.ReduceOp.SUM)
@@ -365,17 +430,23 @@ def main():
             pin[name] = torch.from_numpy(np.ascontiguousarray(arr)).pin_memory()
         if mine.accuracy is not None:
             pin['accuracy'] = torch.from_numpy(np.ascontiguousarray(mine.accuracy, np.float32)).pin_memory()
-        hist_host = torch.zeros(hist_len, dtype=torch.int32).pin_memory()
+        hist_host = torch.zeros(hist_len, dtype=torch.int32).pin_memory() if not keyed else None
         harr = {'trace_offsets': pin['offsets'].data_ptr(), 'lat': pin['lat'].data_ptr(),
                 'lon': pin['lon'].data_ptr(), 'time': pin['time'].data_ptr(), 'mode': pin['mode'].data_ptr(),
                 'accuracy': pin['accuracy'].data_ptr() if 'accuracy' in pin else None}
 
         def e2e_step():
-            r = m.match_batch(mine, host_arrays=harr, hist_device=hists[0].data_ptr(), hist_hours=hours,
-                              hist_base_time=T_BEGIN, copy_out=False, copy_reports=True)
-            hist_host.copy_(hists[0], non_blocking=False)
+            if not keyed:
+                r = m.match_batch(mine, host_arrays=harr, hist_device=hists[0].data_ptr(), hist_hours=hours,
+                                  hist_base_time=T_BEGIN, copy_out=False, copy_reports=True)
+                hist_host.copy_(hists[0], non_blocking=False)
+                return r
+            # keyed: the tile rows reduced and culled in HBM, the owned entries to the host
+            r = m.match_batch(mine, host_arrays=harr, copy_out=False, copy_reports=True, tile_rows=True)
+            e2e_hist['entries'] = sr.hist_reduce(m, r.d_rows, r.n_rows, privacy=args.privacy, rows_in=True)
             return r
 
+        e2e_hist = {}
         e2e_step()
         torch.cuda.synchronize()
         te0 = time.perf_counter()
@@ -385,8 +456,9 @@ def main():
         tel = time.perf_counter() - te0
         e2e = {'value': round(mine.n_probes * args.e2e_steps / tel, 1), 'unit': 'probes/s',
                'ms_per_step': round(1e3 * tel / args.e2e_steps, 3), 'streams': 1, 'reports': int(r.n_rep),
-               'what': 'SoA input in pinned host memory -> H2D -> match -> reports (dense, host) and the '
-                       '[hour][segment][speed] histogram (host); SURVEY 8(d) drop-in definition'}
+               'what': 'SoA input in pinned host memory -> H2D -> match -> reports (dense, host) and the ' +
+                       ('keyed (hour-tile, pair, speed) histogram entries after the privacy cull'
+                        if keyed else '[hour][segment][speed] histogram') + ' (host); SURVEY 8(d) drop-in definition'}
 
     if rank == 0:
         line = {
@@ -412,10 +484,13 @@ def main():
                                         'c5mix': ', modes 60% auto / 25% bicycle / 15% pedestrian'}[
                                            args.workload]),
                        'probes_per_step': int(total_probes),
-                       'parallelism': ('uuid-sharded dp%d + ' + ('RCCL reduce-scatter' if backend == 'nccl'
-                                                                 else 'gloo all-reduce (rehearsal)') +
-                                       ' of [hour][segment][speed] histogram') % world if world > 1 else
-                       'single GPU',
+                       'parallelism': ('uuid-sharded dp%d + ' % world + (
+                           ('keyed (hour-tile, pair, speed) entries all-to-all to the tile owner over ' +
+                            ('RCCL' if backend == 'nccl' else 'gloo (rehearsal)')) if keyed else
+                           (('RCCL reduce-scatter' if backend == 'nccl' else 'gloo all-reduce (rehearsal)') +
+                            ' of the dense [hour][segment][speed] histogram'))) if world > 1 else 'single GPU',
+                       'histogram': ({'kind': 'keyed (SURVEY 8e)', 'privacy': args.privacy, **hist_stats}
+                                     if keyed else {'kind': 'dense [hour][segment][speed]'}),
                        'streams': ns,
                        'stage_ms_per_stream': stage_ms,
                        'route_kernels': tier_table,

@@ -1,7 +1,20 @@
-"""CPU restatement of the device K8 stage — TEST INFRASTRUCTURE ONLY.
+"""CPU restatement of the device histogram stages — TEST INFRASTRUCTURE ONLY.
 
-simple_reporter.py:176-187 filter + hour buckets, accumulated into the dense
-[hour][segment][speed bin] count histogram that the HIP path reduces across GPUs."""
+histogram(): the dense K8 stage — simple_reporter.py:176-187 filter + hour buckets,
+accumulated into the [hour][segment][speed bin] count histogram of OTR batches.
+
+Keyed speed histogram: the per-GPU histogram is simple_reporter's tile
+rows (oracle/tiles.rows_from_reports, simple_reporter.py:176-196) counted by (hour-tile
+file, segment id, next id, speed bin): one entry per key with its number of
+observations.  The keyed exchange sends each entry to the rank owning its file
+(reporter_amd.simple_reporter.file_owner, the (hour, tile) partition of §8e); the owner
+sums the counts of equal keys it received and applies the privacy threshold to whole
+segment pairs: a (file, id, next_id) pair survives when its total count over all speed
+bins reaches `privacy` (simple_reporter.py:218-239 keeps runs of >= privacy identical
+(id, next_id) lines per file; the trailing-singleton quirk of that loop is a property of
+the line files and stays with oracle/tiles.sort_and_cull).  Checker for otr_hist_reduce
+(include/otr.h) and simple_reporter.exchange_hist.
+"""
 import math
 
 import numpy as np
@@ -39,3 +52,53 @@ def histogram(res, first_time, last_time, seg_index_of_id, n_segments, base_time
                 if 0 <= hh < hours:
                     h[hh, seg, b] += 1
     return h, rows
+
+
+HIST_ENTRY = np.dtype([('file', '<u8'), ('id', '<u8'), ('next_id', '<u8'), ('speed_bin', '<u4'), ('count', '<u4')])
+
+
+def entries_from_rows(rows):
+    """Tile rows -> unreduced entries, count 1 each (rows keep their order)."""
+    e = np.zeros(len(rows), HIST_ENTRY)
+    for k in ('file', 'id', 'next_id'):
+        e[k] = rows[k]
+    e['speed_bin'] = rows['speed_bin'].astype(np.uint32)
+    e['count'] = 1
+    return e
+
+
+def reduce(entries, privacy=1):
+    """Sum the counts of equal (file, id, next_id, speed_bin) keys, in key order; with
+    privacy > 1 drop the pairs whose total count is below privacy.  Counts saturate at
+    2^32 - 1 as the device's u32 field does."""
+    if len(entries) == 0:
+        return np.zeros(0, HIST_ENTRY)
+    acc = {}
+    for f, i, n, b, c in zip(entries['file'].tolist(), entries['id'].tolist(), entries['next_id'].tolist(),
+                             entries['speed_bin'].tolist(), entries['count'].tolist()):
+        acc[(f, i, n, b)] = acc.get((f, i, n, b), 0) + c
+    keys = sorted(acc)
+    pair_tot = {}
+    for k in keys:
+        pair_tot[k[:3]] = pair_tot.get(k[:3], 0) + acc[k]
+    out = [(k[0], k[1], k[2], k[3], min(acc[k], 0xFFFFFFFF)) for k in keys
+           if privacy <= 1 or pair_tot[k[:3]] >= privacy]
+    return np.array(out, dtype=HIST_ENTRY) if out else np.zeros(0, HIST_ENTRY)
+
+
+def owner_of(files, world):
+    """The (hour, tile) owner rank: the same fixed mix as simple_reporter.file_owner."""
+    files = np.asarray(files, dtype=np.uint64).astype(np.int64)
+    return ((files >> 25) * 40503 + (files & 0x1FFFFFF)) % world
+
+
+def keyed_exchange(per_rank_entries, world, privacy):
+    """The whole exchange on one host: every rank's entries reduced locally, routed to
+    their owners, and reduced + culled there.  Returns the owners' results by rank."""
+    inbox = [[] for _ in range(world)]
+    for e in per_rank_entries:
+        r = reduce(e, 1)
+        own = owner_of(r['file'], world) if len(r) else np.zeros(0, np.int64)
+        for q in range(world):
+            inbox[q].append(r[own == q])
+    return [reduce(np.concatenate(b) if b else np.zeros(0, HIST_ENTRY), privacy) for b in inbox]

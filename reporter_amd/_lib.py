@@ -143,6 +143,8 @@ def lib():
                                    ctypes.c_int32, P(ctypes.c_void_p), P(ctypes.c_size_t)]
     L.otr_ingest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, P(IngestFormat),
                              P(IngestResult)]
+    L.otr_hist_reduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                  ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, P(ctypes.c_int64)]
     _L = L
     return L
 

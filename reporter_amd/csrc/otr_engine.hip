@@ -379,7 +379,7 @@ enum Slot {
   S_C_ROUTE_OFF, S_C_SEG_OFF, S_C_WAY_OFF, S_C_REP_OFF, S_C_ARGS, S_C_ROUTE, S_C_SEG_ID, S_C_SEG_START,
   S_C_SEG_END, S_C_SEG_LEN, S_C_SEG_QUEUE, S_C_SEG_INTERNAL, S_C_SEG_BSHAPE, S_C_SEG_ESHAPE, S_C_SEG_WAY_N,
   S_C_SEG_WAY, S_C_SEG_WAY_OFF, S_C_REP_ID, S_C_REP_NEXT, S_C_REP_T0, S_C_REP_T1, S_C_REP_LEN, S_C_REP_QUEUE,
-  S_TASK_REC, S_BT, S_CPREP_T, S_TRANS_TC, S_TURN, S_LIST2, S_GFLAG, S_HE_IN, S_HE_SORTED, S_HE_RED, S_HE_OUT, S_IN_TEXT, S_IN_CNT, S_IN_CSCAN, S_IN_NL, S_IN_HASH, S_IN_UOFF, S_IN_ULEN, S_IN_TIME, S_IN_LAT, S_IN_LON,
+  S_TASK_REC, S_BT, S_CPREP_T, S_TRANS_TC, S_TURN, S_LIST2, S_GFLAG, S_HE_IN, S_HE_SORTED, S_HE_RED, S_HE_OUT, S_HE_RANGE, S_IN_TEXT, S_IN_CNT, S_IN_CSCAN, S_IN_NL, S_IN_HASH, S_IN_UOFF, S_IN_ULEN, S_IN_TIME, S_IN_LAT, S_IN_LON,
   S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
@@ -1085,7 +1085,9 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   ha.hist = hist_len ? (in->hist_device ? in->hist_device : need<uint32_t>(S_HIST, hist_len)) : nullptr;
   if (hist_len) HIPCHK(hipMemsetAsync(ha.hist, 0, hist_len * 4, stream));
   tb(OTR_STAGE_HISTOGRAM);
-  k_histogram<<<grid_for(T, 256), 256, 0, stream>>>(ha);
+  // K8 also counts the rows (n_rows) when K9 does not
+  if (hist_len || !(in->flags & OTR_BATCH_TILE_ROWS))
+    k_histogram<<<grid_for(T, kTraceWaves), 256, 0, stream>>>(ha);
   te(OTR_STAGE_HISTOGRAM);
   // ---- K9: simple_reporter tile rows (optional)
   if (in->flags & OTR_BATCH_TILE_ROWS) {
@@ -1102,14 +1104,14 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     ta.quantisation = ha.quantisation;
     ta.rules = in->tile_rules;
     ta.row_cnt = need<int64_t>(S_ROW_CNT, T);
-    k_tile_rows<<<grid_for(T, 256), 256, 0, stream>>>(ta);
+    k_tile_rows<<<grid_for(T, kTraceWaves), 256, 0, stream>>>(ta);
     int64_t* row_off = need<int64_t>(S_ROW_OFF, T + 1);
     if ((rc = scan(ta.row_cnt, row_off, T))) return rc;
     int64_t R = 0;
     if ((rc = read_i64(row_off + T, &R))) return rc;
     ta.row_off = row_off;
     ta.rows = need<otr_tile_row>(S_ROWS, R > 0 ? R : 1);
-    if (R > 0) k_tile_rows<<<grid_for(T, 256), 256, 0, stream>>>(ta);
+    if (R > 0) k_tile_rows<<<grid_for(T, kTraceWaves), 256, 0, stream>>>(ta);
     out->d_rows = ta.rows;
     out->n_rows = R;
   }
@@ -1160,6 +1162,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   out->counters[5] = (uint64_t)NT;
   out->counters[6] = (uint64_t)NTR;
   if (!(in->flags & OTR_BATCH_TILE_ROWS)) out->n_rows = (int64_t)out->counters[8];
+  else out->counters[8] = (uint64_t)out->n_rows;  // K9 counted them (K8 may not have run)
   out->d_hist = ha.hist;
   out->hist_len = (int64_t)hist_len;
   if (timing) {
@@ -1504,12 +1507,72 @@ __global__ void k_rows_to_entries(const otr_tile_row* r, int64_t n, otr_hist_ent
   x.count = 1u;
   e[i] = x;
 }
+// key ranges of the entries, for the fewest radix-sort bits: OR of the ids and next ids
+// (their widths), min / max hour bucket, and whether every file is the one K9 derives
+// from its id (bucket << 25 | level << 22 | tile: then (file, id) order is (bucket,
+// level, tile, index) order, one packed key)
+struct EntryRange {
+  unsigned long long id_or, next_or, file_or, bmin, bmax, foreign;
+};
+// a fixed grid (kRangeBlocks x 1024) strides over the entries; one set of atomics per
+// block (one per wave queued ~23K atomics on a single line: 263 us for 244K entries)
+constexpr int kRangeBlocks = 128;
+__global__ __launch_bounds__(1024) void k_entry_range(const otr_hist_entry* e, int64_t n, EntryRange* r) {
+  unsigned long long v[6] = {0ull, 0ull, 0ull, ~0ull, 0ull, 0ull};  // id, next, file OR; bmin; bmax; foreign
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const otr_hist_entry x = e[i];
+    v[0] |= x.id;
+    v[1] |= x.next_id;
+    v[2] |= x.file;
+    const unsigned long long b = x.file >> 25;
+    v[3] = b < v[3] ? b : v[3];
+    v[4] = b > v[4] ? b : v[4];
+    v[5] |= (x.file & 0x1FFFFFFull) != (((x.id & 7ull) << 22) | ((x.id >> 3) & 0x3FFFFFull)) ? 1ull : 0ull;
+  }
+  for (int o = OTR_WAVE / 2; o > 0; o >>= 1) {
+    for (int q : {0, 1, 2, 5}) v[q] |= __shfl_xor(v[q], o);
+    const unsigned long long a = __shfl_xor(v[3], o), b = __shfl_xor(v[4], o);
+    v[3] = a < v[3] ? a : v[3];
+    v[4] = b > v[4] ? b : v[4];
+  }
+  __shared__ unsigned long long part[1024 / OTR_WAVE][6];
+  if (lane_id() == 0)
+    for (int q = 0; q < 6; ++q) part[threadIdx.x / OTR_WAVE][q] = v[q];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x / OTR_WAVE); ++w) {
+      for (int q : {0, 1, 2, 5}) v[q] |= part[w][q];
+      v[3] = part[w][3] < v[3] ? part[w][3] : v[3];
+      v[4] = part[w][4] > v[4] ? part[w][4] : v[4];
+    }
+    atomicOr(&r->id_or, v[0]);
+    atomicOr(&r->next_or, v[1]);
+    atomicOr(&r->file_or, v[2]);
+    atomicMin(&r->bmin, v[3]);
+    atomicMax(&r->bmax, v[4]);
+    atomicOr(&r->foreign, v[5]);
+  }
+}
+static int bit_width(unsigned long long v) { return v ? 64 - __builtin_clzll(v) : 0; }
+// sort key of one LSD pass: 0 file, 1 id, 2 next id, 3 speed bin, 4 next id << 3 | bin,
+// 5 (bucket - bmin) << 46 | level << 43 | tile << 21 | index (K9 files, 46-bit ids)
 __global__ void k_entry_key(const otr_hist_entry* e, const int32_t* perm, int64_t n, int field,
-                            unsigned long long* key) {
+                            unsigned long long bmin, unsigned long long* key) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const otr_hist_entry& x = e[perm[i]];
-  key[i] = field == 0 ? x.file : (field == 1 ? x.id : (field == 2 ? x.next_id : (unsigned long long)x.speed_bin));
+  unsigned long long k;
+  switch (field) {
+    case 0: k = x.file; break;
+    case 1: k = x.id; break;
+    case 2: k = x.next_id; break;
+    case 3: k = x.speed_bin; break;
+    case 4: k = (x.next_id << 3) | (x.speed_bin & 7u); break;
+    default:
+      k = (((x.file >> 25) - bmin) << 46) | ((x.id & 7ull) << 43) | (((x.id >> 3) & 0x3FFFFFull) << 21) |
+          ((x.id >> 25) & 0x1FFFFFull);
+  }
+  key[i] = k;
 }
 __global__ void k_gather_entries(const otr_hist_entry* in, const int32_t* idx, int64_t n, otr_hist_entry* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1606,13 +1669,27 @@ int Matcher::hist_reduce(const void* in, int64_t n, int memory, int rows_in, int
   HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb_scan, head, pos, ni, stream));
   void* tmp = need<char>(S_SORT_TMP, std::max(tb_sort, tb_scan));
   if (!tmp) return fail("device allocation failed (histogram)");
-  // LSD: speed bin, next id, id, file (stable passes over a permutation)
+  // LSD over (file, id, next_id, speed_bin), stable passes over a permutation, each only
+  // as wide as the keys' range: typically two passes of ~49 bits (next id and bin) and
+  // ~47 bits (hour offset and the id in file order), instead of 3 + 3 x 64 bits
+  EntryRange* rng = need<EntryRange>(S_HE_RANGE, 1);
+  if (!rng) return fail("device allocation failed (histogram)");
+  EntryRange hr{0ull, 0ull, 0ull, ~0ull, 0ull, 0ull};
+  HIPCHK(hipMemcpyAsync(rng, &hr, sizeof(hr), hipMemcpyHostToDevice, stream));
+  k_entry_range<<<(unsigned)std::min<int64_t>(kRangeBlocks, (n + 1023) / 1024), 1024, 0, stream>>>(e_in, n, rng);
+  HIPCHK(hipMemcpyAsync(&hr, rng, sizeof(hr), hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  std::vector<std::pair<int, int>> passes;  // (field, end bit), least significant first
+  const int wn = bit_width(hr.next_or), wi = bit_width(hr.id_or), ws = bit_width(hr.bmax - hr.bmin);
+  if (wn + 3 <= 64) passes.push_back({4, wn + 3});
+  else passes.insert(passes.end(), {{3, 3}, {2, wn}});
+  if (!hr.foreign && wi <= 46 && ws + 46 <= 64) passes.push_back({5, std::max(46 + ws, 1)});
+  else passes.insert(passes.end(), {{1, std::max(wi, 1)}, {0, std::max(bit_width(hr.file_or), 1)}});
   k_iota_i32<<<grid_for(n, 256), 256, 0, stream>>>(perm_a, n);
-  for (int f = 3; f >= 0; --f) {
-    k_entry_key<<<grid_for(n, 256), 256, 0, stream>>>(e_in, perm_a, n, f, key_a);
+  for (const auto& ps : passes) {
+    k_entry_key<<<grid_for(n, 256), 256, 0, stream>>>(e_in, perm_a, n, ps.first, hr.bmin, key_a);
     size_t tb = tb_sort;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key_a, key_b, perm_a, perm_b, ni, 0, f == 3 ? 3 : 64,
-                                              stream));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key_a, key_b, perm_a, perm_b, ni, 0, ps.second, stream));
     std::swap(perm_a, perm_b);
   }
   k_gather_entries<<<grid_for(n, 256), 256, 0, stream>>>(e_in, perm_a, n, e_sorted);

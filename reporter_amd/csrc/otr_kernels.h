@@ -1934,9 +1934,20 @@ __global__ __launch_bounds__(64) void k_compact(CompactArgs a) {
   }
 }
 
+// inclusive prefix sum over the wave (lane order)
+__device__ inline unsigned long long wave_incl_scan_u64(unsigned long long v) {
+  const int l = lane_id();
+  for (int o = 1; o < OTR_WAVE; o <<= 1) {
+    const unsigned long long u = __shfl_up(v, o);
+    if (l >= o) v += u;
+  }
+  return v;
+}
+
 // ------------------------------------------------------------------------------
 // K8: simple_reporter filter + hour bucketing (simple_reporter.py:176-196) into a
-// dense [hour][segment][speed bin] count histogram; one thread per trace.
+// dense [hour][segment][speed bin] count histogram; one wave per trace, a lane per
+// report (one thread per trace left ~40 CUs busy on a 10K-trace batch: 105 us).
 // ------------------------------------------------------------------------------
 struct HistArgs {
   BatchDev b;
@@ -1956,15 +1967,16 @@ struct HistArgs {
   unsigned long long* n_rows;
 };
 
-__global__ void k_histogram(HistArgs a) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.b.n_traces) return;
+constexpr int kTraceWaves = 4;  // K8 / K9: waves (traces) per 256-thread block
+__global__ __launch_bounds__(256) void k_histogram(HistArgs a) {
+  const int t = blockIdx.x * kTraceWaves + threadIdx.x / OTR_WAVE;
+  if (t >= a.b.n_traces) return;  // wave-uniform
   const int64_t lo = a.b.trace_off[t], hi = a.b.trace_off[t + 1];
   if (hi <= lo) return;
   const int64_t first = a.b.time[lo], last = a.b.time[hi - 1];
-  const int64_t co = a.cap_off[t];
+  const int64_t co = a.cap_off[t], nrep = a.rep_n[t];
   unsigned long long rows = 0;
-  for (int64_t r = 0; r < a.rep_n[t]; ++r) {
+  for (int64_t r = lane_id(); r < nrep; r += OTR_WAVE) {
     const double t0 = a.rep_t0[co + r], t1 = a.rep_t1[co + r];
     const int32_t len = a.rep_length[co + r];
     if (!bucket_keep(t0, t1, len, a.rep_queue[co + r])) continue;
@@ -1981,7 +1993,8 @@ __global__ void k_histogram(HistArgs a) {
         atomicAdd(&a.hist[((size_t)h * a.n_segments + seg) * OTR_HIST_BINS + bin], 1u);
     }
   }
-  if (rows) atomicAdd(&a.n_rows[cshard()], rows);
+  for (int o = OTR_WAVE / 2; o > 0; o >>= 1) rows += __shfl_xor(rows, o);
+  if (rows && lane_id() == 0) atomicAdd(&a.n_rows[cshard()], rows);
 }
 
 // ------------------------------------------------------------------------------
@@ -2005,55 +2018,71 @@ struct TileArgs {
   otr_tile_row* rows;      // pass 2 output
 };
 
-__global__ void k_tile_rows(TileArgs a) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.b.n_traces) return;
+// one wave per trace, a lane per report; a report's rows are contiguous, reports in order
+// (wave prefix sums place them), so the rows come out trace by trace in report order
+__global__ __launch_bounds__(256) void k_tile_rows(TileArgs a) {
+  const int t = blockIdx.x * kTraceWaves + threadIdx.x / OTR_WAVE;
+  if (t >= a.b.n_traces) return;  // wave-uniform
   const int64_t lo = a.b.trace_off[t], hi = a.b.trace_off[t + 1];
-  int64_t k = a.rows ? a.row_off[t] : 0;
-  const int64_t k0 = k;
+  int64_t base = a.rows ? a.row_off[t] : 0;
+  const int64_t base0 = base;
   if (hi > lo) {
     const int64_t first = a.b.time[lo], last = a.b.time[hi - 1];
-    const int64_t co = a.cap_off[t];
-    for (int64_t r = 0; r < a.rep_n[t]; ++r) {
-      const double t0 = a.rep_t0[co + r], t1 = a.rep_t1[co + r];
-      const int32_t len = a.rep_length[co + r], qu = a.rep_queue[co + r];
+    const int64_t co = a.cap_off[t], nrep = a.rep_n[t];
+    for (int64_t r0 = 0; r0 < nrep; r0 += OTR_WAVE) {
+      const int64_t r = r0 + lane_id();
       BucketSpan sp;
-      if (a.rules == OTR_TILE_RULES_STREAM) {
-        // BatchingProcessor.java:119-126 (Segment.valid, Segment.java:38-40) and
-        // TimeQuantisedTile.getTiles (TimeQuantisedTile.java:26-35): buckets from the
-        // truncated times, no span limit; duration Math.round (ties up), Segment.java:65-71
-        if (!(t0 > 0 && t1 > 0 && t1 > t0 && len > 0 && qu >= 0)) continue;
-        sp.duration = py2_round_int(t1 - t0);
-        sp.start = (int64_t)floor(t0);
-        sp.end = (int64_t)ceil(t1);
-        sp.min_bucket = (int64_t)t0 / a.quantisation;
-        sp.max_bucket = (int64_t)t1 / a.quantisation;
-      } else {
-        if (!bucket_keep(t0, t1, len, qu)) continue;
-        sp = bucket_span(t0, t1, first, last, a.quantisation);
-        if (!sp.ok) continue;
+      bool keep = false;
+      double t0 = 0, t1 = 0;
+      int32_t len = 0, qu = 0;
+      if (r < nrep) {
+        t0 = a.rep_t0[co + r];
+        t1 = a.rep_t1[co + r];
+        len = a.rep_length[co + r];
+        qu = a.rep_queue[co + r];
+        if (a.rules == OTR_TILE_RULES_STREAM) {
+          // BatchingProcessor.java:119-126 (Segment.valid, Segment.java:38-40) and
+          // TimeQuantisedTile.getTiles (TimeQuantisedTile.java:26-35): buckets from the
+          // truncated times, no span limit; duration Math.round (ties up), Segment.java:65-71
+          if (t0 > 0 && t1 > 0 && t1 > t0 && len > 0 && qu >= 0) {
+            sp.duration = py2_round_int(t1 - t0);
+            sp.start = (int64_t)floor(t0);
+            sp.end = (int64_t)ceil(t1);
+            sp.min_bucket = (int64_t)t0 / a.quantisation;
+            sp.max_bucket = (int64_t)t1 / a.quantisation;
+            keep = true;
+          }
+        } else if (bucket_keep(t0, t1, len, qu)) {
+          sp = bucket_span(t0, t1, first, last, a.quantisation);
+          keep = sp.ok;
+        }
       }
-      const unsigned long long id = a.rep_id[co + r], nx = a.rep_next[co + r];
-      // the report's 20 km/h speed bin, as K8 bins it (oracle/tiles.py speed_bin)
-      const double bq = (((double)len / (t1 - t0)) * 3.6) / 20.0;
-      const int speed_bin = bq >= (double)(OTR_HIST_BINS - 1) ? OTR_HIST_BINS - 1 : (bq < 0.0 ? 0 : (int)bq);
-      for (int64_t bk = sp.min_bucket; bk <= sp.max_bucket; ++bk, ++k) {
-        if (!a.rows) continue;
-        otr_tile_row row;
-        row.file = ((unsigned long long)bk << 25) | ((id & 7ull) << 22) | ((id >> 3) & 0x3FFFFFull);
-        row.id = id;
-        row.next_id = nx == OTR_NO_ID ? OTR_INVALID_SEGMENT_ID : nx;
-        row.start = sp.start;
-        row.end = sp.end;
-        row.duration = (int32_t)sp.duration;
-        row.length = len;
-        row.queue_length = qu;
-        row.speed_bin = speed_bin;
-        a.rows[k] = row;
+      const unsigned long long nb = keep ? (unsigned long long)(sp.max_bucket - sp.min_bucket + 1) : 0ull;
+      const unsigned long long incl = wave_incl_scan_u64(nb);
+      if (a.rows && keep) {
+        const unsigned long long id = a.rep_id[co + r], nx = a.rep_next[co + r];
+        // the report's 20 km/h speed bin, as K8 bins it (oracle/tiles.py speed_bin)
+        const double bq = (((double)len / (t1 - t0)) * 3.6) / 20.0;
+        const int speed_bin = bq >= (double)(OTR_HIST_BINS - 1) ? OTR_HIST_BINS - 1 : (bq < 0.0 ? 0 : (int)bq);
+        int64_t k = base + (int64_t)(incl - nb);
+        for (int64_t bk = sp.min_bucket; bk <= sp.max_bucket; ++bk, ++k) {
+          otr_tile_row row;
+          row.file = ((unsigned long long)bk << 25) | ((id & 7ull) << 22) | ((id >> 3) & 0x3FFFFFull);
+          row.id = id;
+          row.next_id = nx == OTR_NO_ID ? OTR_INVALID_SEGMENT_ID : nx;
+          row.start = sp.start;
+          row.end = sp.end;
+          row.duration = (int32_t)sp.duration;
+          row.length = len;
+          row.queue_length = qu;
+          row.speed_bin = speed_bin;
+          a.rows[k] = row;
+        }
       }
+      base += (int64_t)__shfl(incl, OTR_WAVE - 1);
     }
   }
-  if (!a.rows) a.row_cnt[t] = k - k0;
+  if (!a.rows && lane_id() == 0) a.row_cnt[t] = base - base0;
 }
 
 // Line order of simple_reporter.py:218 (segments.sort() over whole text lines).  Every

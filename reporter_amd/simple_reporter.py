@@ -311,15 +311,13 @@ def stream_tiles_device(matcher, traces, privacy, mode='auto', report_levels=(0,
     return rows_to_tiles(kept, quantisation, mode, source, rules=_lib.OTR_TILE_RULES_STREAM)
 
 
-def exchange_rows(rows, world, group=None):
-    """Route every row to the rank owning its file (all-to-all, one exchange step):
-    rows is a uint8 tensor of n*56 bytes (device for RCCL, host for gloo); returns the
-    rows this rank owns (uint8 tensor).  Owners then cull complete files locally."""
+def _exchange_by_file_owner(buf, itemsize, world, group=None):
+    """All-to-all of fixed-size records whose first 8 bytes are their (hour, tile) file:
+    each record goes to file_owner(file); returns the records this rank received (uint8
+    tensor, grouped by sender rank)."""
     import torch
     import torch.distributed as dist
-    from . import _lib
-    w = _lib.TILE_ROW.itemsize
-    r8 = rows.view(-1, w)
+    r8 = buf.view(-1, itemsize)
     files = r8[:, 0:8].contiguous().view(torch.int64).reshape(-1)
     owner = file_owner(files, world)
     order = torch.argsort(owner, stable=True)
@@ -327,7 +325,55 @@ def exchange_rows(rows, world, group=None):
     counts = torch.bincount(owner, minlength=world).to(torch.int64)
     recv = torch.empty_like(counts)
     dist.all_to_all_single(recv, counts, group=group)
-    out = torch.empty(int(recv.sum().item()) * w, dtype=torch.uint8, device=rows.device)
-    dist.all_to_all_single(out, send, output_split_sizes=[int(x) * w for x in recv.tolist()],
-                           input_split_sizes=[int(x) * w for x in counts.tolist()], group=group)
+    out = torch.empty(int(recv.sum().item()) * itemsize, dtype=torch.uint8, device=buf.device)
+    dist.all_to_all_single(out, send, output_split_sizes=[int(x) * itemsize for x in recv.tolist()],
+                           input_split_sizes=[int(x) * itemsize for x in counts.tolist()], group=group)
     return out
+
+
+def exchange_rows(rows, world, group=None):
+    """Route every row to the rank owning its file (all-to-all, one exchange step):
+    rows is a uint8 tensor of n*56 bytes (device for RCCL, host for gloo); returns the
+    rows this rank owns (uint8 tensor).  Owners then cull complete files locally."""
+    from . import _lib
+    return _exchange_by_file_owner(rows, _lib.TILE_ROW.itemsize, world, group)
+
+
+def hist_reduce(matcher, src, n, privacy=1, rows_in=False, memory='device', out=None, out_memory=None):
+    """otr_hist_reduce: n tile rows (rows_in) or histogram entries → entries summed per
+    (file, id, next_id, speed_bin) in key order, pairs below `privacy` dropped.  src: a
+    device pointer (memory='device') or a numpy array (memory='host').  out: a device
+    pointer with room for n entries (returns their number), or None for a numpy array."""
+    import ctypes
+    from . import _lib
+    L = _lib.lib()
+    n = int(n)
+    mem = _lib.OTR_MEM_DEVICE if memory == 'device' else _lib.OTR_MEM_HOST
+    if memory != 'device':
+        src = np.ascontiguousarray(src, dtype=_lib.TILE_ROW if rows_in else _lib.HIST_ENTRY)
+        ptr = src.ctypes.data if n else None
+    else:
+        ptr = int(src) if n else None
+    nout = ctypes.c_int64()
+    if out is not None:
+        rc = L.otr_hist_reduce(matcher._h, ptr, n, mem, int(bool(rows_in)), int(privacy), int(out), max(n, 1),
+                               _lib.OTR_MEM_DEVICE if out_memory in (None, 'device') else _lib.OTR_MEM_HOST,
+                               ctypes.byref(nout))
+        if rc != 0:
+            raise RuntimeError('otr_hist_reduce failed (%d): %s' % (rc, _lib.last_error()))
+        return nout.value
+    res = np.zeros(max(n, 1), _lib.HIST_ENTRY)
+    rc = L.otr_hist_reduce(matcher._h, ptr, n, mem, int(bool(rows_in)), int(privacy), res.ctypes.data, max(n, 1),
+                           _lib.OTR_MEM_HOST, ctypes.byref(nout))
+    if rc != 0:
+        raise RuntimeError('otr_hist_reduce failed (%d): %s' % (rc, _lib.last_error()))
+    return res[:nout.value].copy()
+
+
+def exchange_hist(entries, world, group=None):
+    """The keyed histogram exchange: every 32-B histogram entry goes to
+    the rank owning its (hour, tile) file (one all-to-all); returns the entries this rank
+    received (uint8 tensor; device for RCCL, host for gloo).  The owner then reduces and
+    culls them with hist_reduce(..., privacy)."""
+    from . import _lib
+    return _exchange_by_file_owner(entries, _lib.HIST_ENTRY.itemsize, world, group)

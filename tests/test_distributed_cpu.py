@@ -77,3 +77,66 @@ def test_two_rank_shard_and_combine(tmp_path, graph_dir):
     assert int(np.load(out + '.cnt.npy')[0]) == tr.n_traces  # shards partition the traces
     assert rows > 0 and whole.sum() > 0
     assert np.array_equal(combined, whole.reshape(-1))
+
+
+def _entries_for(path, tr):
+    """Oracle match → tile rows (simple_reporter.py:176-196) → keyed entries, reduced
+    locally (the CPU stands in for the GPU's otr_hist_reduce here)."""
+    from oracle import pyoracle as po
+    from oracle import hist, tiles
+    r = po.match_batch(po.Graph(path), tr, po.params())
+    first = tr.time[tr.offsets[:-1]]
+    last = tr.time[tr.offsets[1:] - 1]
+    rows = tiles.rows_from_reports(r, first, last)
+    return hist.reduce(hist.entries_from_rows(rows), 1), rows
+
+
+def _keyed_rank(rank, world, port, graph_dir, out, privacy):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from oracle import hist
+    from reporter_amd import simple_reporter as sr
+    path, tr = _workload(graph_dir)
+    mine = np.array([i for i, u in enumerate(tr.uuids) if sr.shard_of(u, world) == rank])
+    local, _ = _entries_for(path, tr.subset(mine))
+    got = sr.exchange_hist(torch.from_numpy(local.view(np.uint8).copy()), world)
+    recv = got.numpy().view(hist.HIST_ENTRY)
+    owned = hist.reduce(recv, privacy)  # the owner's merge + cull
+    ok = bool(np.all(hist.owner_of(recv['file'], world) == rank))
+    # gather every owner's result on rank 0 (sizes first: gloo all_gather needs equal shapes)
+    n = torch.tensor([len(owned)])
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    m = max(int(x) for x in ns)
+    buf = torch.zeros(m * hist.HIST_ENTRY.itemsize, dtype=torch.uint8)
+    buf[:len(owned) * hist.HIST_ENTRY.itemsize] = torch.from_numpy(owned.view(np.uint8).copy())
+    bufs = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf)
+    oks = torch.tensor([int(ok)])
+    dist.all_reduce(oks)
+    if rank == 0:
+        parts = [b.numpy()[:int(k) * hist.HIST_ENTRY.itemsize].view(hist.HIST_ENTRY) for b, k in zip(bufs, ns)]
+        np.save(out, np.concatenate(parts))
+        np.save(out + '.ok.npy', oks.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('privacy', [1, 2])
+def test_two_rank_keyed_histogram_exchange(tmp_path, graph_dir, privacy):
+    """§8e keyed exchange: per-rank (file, pair, speed bin) entries → all-to-all by the
+    (hour, tile) owner → owner reduce + pair cull; the owners' union equals the
+    single-process reduction of the whole set, and every entry reached its owner."""
+    from oracle import hist
+    world = 2
+    out = str(tmp_path / 'keyed.npy')
+    mp.spawn(_keyed_rank, args=(world, _free_port(), graph_dir, out, privacy), nprocs=world, join=True)
+    path, tr = _workload(graph_dir)
+    _, rows = _entries_for(path, tr)
+    whole = hist.reduce(hist.entries_from_rows(rows), privacy)
+    got = np.load(out)
+    assert int(np.load(out + '.ok.npy')[0]) == world
+    assert len(whole) > 0 and int(whole['count'].sum()) > 0
+    order = np.lexsort((got['speed_bin'], got['next_id'], got['id'], got['file']))
+    assert np.array_equal(got[order], whole)
