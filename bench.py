@@ -509,7 +509,13 @@ def main():
                          'settled_nodes': int(dom['work'][1] // dom['launches']),
                          'relaxed_edges': int(dom['work'][2] // dom['launches']),
                          'transition_entries': int(dom['work'][3] // dom['launches']),
-                         'search_rounds': int(counters[13]), 'table_keys': int(counters[14])},
+                         'search_rounds': int(counters[13]), 'table_keys': int(counters[14]),
+                         # diagnostic build only (OTR_STAMPS, OTR_LIB=libotr_stamps.so): shader
+                         # clocks of the first tier's search phases, summed over waves
+                         'phase_cycles': ({'pending': int(counters[16]), 'resolved': int(counters[17]),
+                                           'partition': int(counters[18]), 'relax': int(counters[19]),
+                                           'setup': int(counters[20]), 'rows': int(counters[21])}
+                                          if counters[19] else None)},
             'cpu_baseline': cpu,
             'parity': parity,
             'end_to_end': e2e,

@@ -596,14 +596,16 @@ __device__ inline int lds_find(const SearchLds<CAP, PRED>& L, uint32_t node) {
   return -1;
 }
 
-template <int CAP, bool PRED>
+// COUNT: add new keys to L.n_keys; the main relax loop instead counts them by ballot in a
+// register (one LDS atomic less per new key, and no same-address atomic serialisation)
+template <int CAP, bool PRED, bool COUNT = true>
 __device__ inline int lds_insert(SearchLds<CAP, PRED>& L, uint32_t node, bool* isnew) {
   uint32_t h = hslot<CAP>(node);
   for (int probe = 0; probe < CAP; ++probe) {
     // CAS first: one LDS round trip both claims an empty slot and reads an occupied one
     const uint32_t k = atomicCAS(&L.key[h], kEmpty, node);
     if (k == kEmpty) {
-      atomicAdd(&L.n_keys, 1);  // load factor checked once per round (search_run)
+      if (COUNT) atomicAdd(&L.n_keys, 1);  // load factor checked once per round (search_run)
       *isnew = true;
       return (int)h;
     }
@@ -680,10 +682,12 @@ __device__ inline bool target_resolved(const SearchLds<CAP, PRED>& L, const Pack
 // be writing; the round's minimum over improvements and kept pending nodes is the next
 // round's fmin.  A label improves when its packed word does (a shorter length, or the
 // same length sooner): the node is then pending again.
-template <int CAP, bool PRED>
+template <int CAP, bool PRED, bool COUNT = true>
 __device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, const Pack& K, uint32_t dw, uint32_t len_mm,
                                 uint32_t time_ds, int32_t vlat, int32_t vlon, uint32_t pu, uint32_t edge,
-                                uint32_t bound_mm, uint32_t mode_bit, uint32_t& relaxed, uint32_t& fnext) {
+                                uint32_t bound_mm, uint32_t mode_bit, uint32_t& relaxed, uint32_t& fnext,
+                                bool& isnew) {
+  isnew = false;
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
   const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
@@ -691,8 +695,7 @@ __device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, const Pa
   const uint32_t tt = K.t(pu) + time_ds;  // both < 2^31
   const uint32_t nw = (nd << K.sh) | (tt < K.tcap() ? tt : K.tcap());
   const uint32_t h = H(vlat, vlon);
-  bool isnew = false;
-  const int sl = lds_insert(L, dw & kAdjDstMask, &isnew);
+  const int sl = lds_insert<CAP, PRED, COUNT>(L, dw & kAdjDstMask, &isnew);
   if (sl < 0) return -1;
   if (isnew) L.hv[sl] = h;
   const typename LabelT<PRED>::T nb = LabelT<PRED>::make(nw, edge);
@@ -731,6 +734,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
   using Idx = typename SearchLds<CAP, PRED>::Idx;
   constexpr int WCAP = SearchLds<CAP, PRED>::WCAP;
   const bool timed = K.sh != 0u;  // group-uniform
+  const uint32_t* adjt = g.adj_t + (size_t)__builtin_ctz(mode_bit) * g.adj_t_stride;
   if (active && gl == 0) {
     bool isnew;
     const int sl = lds_insert(L, start, &isnew);
@@ -754,6 +758,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
   const uint32_t hTm = hT + H.margin;  // h(T) with the evaluation margin (see Heur)
   bool done = !active;
   int npend = active ? 1 : 0;  // pending-list length (group-uniform register)
+  int nkeys = 0;               // keys the main relax loop added (group-uniform; L.n_keys has the rest)
   for (;;) {
     OTR_STAMP(t0);
     const int np = done ? 0 : npend;
@@ -808,19 +813,24 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
     for (int base = 0; base < nwx; base += Gr::GL) {
       const int k = base + gl;
       int psl = -1;
+      bool isnew = false;
       if (k < 4 * nw) {
         const uint2 wk = L.work[k >> 2];
         const int slot = k & 3;
         if (slot == 0) ++my_settled;
+        // the mode's route time of the slot (DevGraph::adj_t, one block per mode), loaded
+        // ahead of the adjacency record and unconditionally: both loads in flight together
+        // (issued after ld16's register barrier it had made every relaxation wait for two
+        // global loads in a row)
+        const uint32_t tq = adjt[4 * (size_t)wk.x + slot];
         const uint4 r = ld16(g.adj + 4 * (size_t)wk.x + slot);
-        // the mode's route times (DevGraph::adj_t, one block per mode)
-        const uint32_t tt =
-            timed ? g.adj_t[(size_t)__builtin_ctz(mode_bit) * g.adj_t_stride + 4 * (size_t)wk.x + slot] : 0u;
+        const uint32_t tt = timed ? tq : 0u;
         const uint32_t e0 = PRED ? g.node_row[wk.x] : 0u;  // edge id = CSR row start + slot
-        psl = relax_one(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.y, e0 + slot, bound_mm,
-                        mode_bit, my_relaxed, fnext);
+        psl = relax_one<CAP, PRED, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.y,
+                                          e0 + slot, bound_mm, mode_bit, my_relaxed, fnext, isnew);
         tail = tail || (slot == 3 && (r.x & kAdjMore));
       }
+      nkeys += Gr::count(__ballot(isnew));
       // append newly pending nodes by ballot (no shared counter)
       const unsigned long long mp = __ballot(psl >= 0);
       if (psl >= 0) {
@@ -844,8 +854,9 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
               const uint4 pk = ld16(g.edge_pack + e);
               const int2 vll = g.node_ll[pk.x];
               const uint32_t tt = timed ? g.et(__builtin_ctz(mode_bit))[e] : 0u;
+              bool isnew;
               const int psl = relax_one(L, H, K, pk.x | ((pk.z & 7u) << 28), pk.y, tt, vll.x, vll.y, wk.y, e,
-                                        bound_mm, mode_bit, my_relaxed, fnext);
+                                        bound_mm, mode_bit, my_relaxed, fnext, isnew);
               if (psl >= 0) {
                 const int p = atomicAdd(&L.n_pend, 1);
                 if (p < CAP) L.pend[p] = (Idx)psl;
@@ -862,10 +873,12 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
     OTR_STAMP(t4);
     cyc[3] += t4 - t3;
     fmin = Gr::min_u32(fnext);
-    if (!done && (L.overflow || L.n_keys > kMaxKeys)) done = true;
+    const int keys = L.n_keys + nkeys;
+    if (!done && (L.overflow || keys > kMaxKeys)) done = true;
     __syncthreads();
-    if (done && active && gl == 0 && L.n_keys > kMaxKeys) L.overflow = 1;
+    if (done && active && gl == 0 && keys > kMaxKeys) L.overflow = 1;
   }
+  if (gl == 0) L.n_keys += nkeys;  // the table's key count, for the caller
 #ifdef OTR_STAMPS
   if (stamps && threadIdx.x == 0)
     for (int q = 0; q < 4; ++q) atomicAdd(&stamps[q * kCShards + cshard()], cyc[q]);
@@ -1004,6 +1017,12 @@ __global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const uns
 // LIST = false: the first tier, one unit per block over all tasks (XCD-mapped); LIST =
 // true: a retry tier, a fixed grid striding over the device-side task list (its length
 // never crosses to the host)
+// index of the q-th set bit of m (q < popcount(m))
+__device__ inline int nth_set_bit(unsigned long long m, int q) {
+  for (int j = 0; j < q; ++j) m &= m - 1;
+  return __ffsll((long long)m) - 1;
+}
+
 // one unit = G search tasks of the wave (ordinal w of the task range or list)
 template <int CAP, int G, bool LIST>
 __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& a, unsigned long long* counters,
@@ -1045,10 +1064,27 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
       cq = a.cprep[s * OTR_KMAX + lane];
       tpart = cq.x;
     }
-    for (unsigned long long m = mask; m; m &= m - 1) {
-      const int i = __ffsll((long long)m) - 1;
-      const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
-      const double pi = a.cand_p[sp * OTR_KMAX + i];
+    // the task's sources staged one per lane (lane q: the q-th set bit of mask), read in
+    // the loop by group shuffles: one parallel load instead of a dependent one per source
+    const int nsrc = have ? __popcll(mask) : 0;
+    const int iq = lane < nsrc ? nth_set_bit(mask, lane) : 0;
+    uint32_t e_q = 0;
+    double p_q = 0;
+    if (lane < nsrc) {
+      e_q = a.cand_edge[sp * OTR_KMAX + iq];
+      p_q = a.cand_p[sp * OTR_KMAX + iq];
+    }
+    for (int q = 0; q < nsrc; ++q) {  // group-uniform trip count
+      uint32_t ei;
+      double pi;
+      if (q < Gr::GL) {
+        ei = (uint32_t)__shfl((int)e_q, q, Gr::GL);
+        pi = __shfl(p_q, q, Gr::GL);
+      } else {  // more sources than lanes (K > 32 at G = 2): direct loads
+        const int i = nth_set_bit(mask, q);
+        ei = a.cand_edge[sp * OTR_KMAX + i];
+        pi = a.cand_p[sp * OTR_KMAX + i];
+      }
       if (lane < Kb && !(ej == ei && pj >= pi)) needed = true;
     }
     forced = have && ((r1.y >> 10) & 1u);
@@ -1089,14 +1125,43 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     const int32_t bt = a.bt[s];
     const int md = (int)((r1.y >> 8) & 3u);
     uint32_t* trow = a.trans + a.trans_off[s];
+    // sources staged one per lane as in the setup: {index, edge, fraction, exit part mm,
+    // exit part time}, read by group shuffles in the row loop
+    const int nsrc = __popcll(mask);
+    const int iq = lane < nsrc ? nth_set_bit(mask, lane) : 0;
+    uint32_t e_q = 0, w_q = 0, t_q = 0;
+    double p_q = 0;
+    if (lane < nsrc) {
+      e_q = a.cand_edge[sp * OTR_KMAX + iq];
+      p_q = a.cand_p[sp * OTR_KMAX + iq];
+      w_q = a.cprep[sp * OTR_KMAX + iq].w;
+      if (bt >= 0) t_q = a.cprep_t[sp * OTR_KMAX + iq].y;
+    }
+    uint32_t ej = 0, tpt = 0;
+    double pj = 0;
     if (lane < Kb) {
-      const uint32_t ej = a.cand_edge[s * OTR_KMAX + lane];
-      const double pj = a.cand_p[s * OTR_KMAX + lane];
-      const uint32_t tpt = bt >= 0 ? a.cprep_t[s * OTR_KMAX + lane].x : 0u;
-      for (unsigned long long m = mask; m; m &= m - 1) {
-        const int i = __ffsll((long long)m) - 1;
-        const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
-        const double pi = a.cand_p[sp * OTR_KMAX + i];
+      ej = a.cand_edge[s * OTR_KMAX + lane];
+      pj = a.cand_p[s * OTR_KMAX + lane];
+      tpt = bt >= 0 ? a.cprep_t[s * OTR_KMAX + lane].x : 0u;
+    }
+    for (int q = 0; q < nsrc; ++q) {  // group-uniform trip count
+      int i;
+      uint32_t ei, wi, ti;
+      double pi;
+      if (q < Gr::GL) {
+        i = __shfl(iq, q, Gr::GL);
+        ei = (uint32_t)__shfl((int)e_q, q, Gr::GL);
+        pi = __shfl(p_q, q, Gr::GL);
+        wi = (uint32_t)__shfl((int)w_q, q, Gr::GL);
+        ti = (uint32_t)__shfl((int)t_q, q, Gr::GL);
+      } else {  // more sources than lanes (K > 32 at G = 2): direct loads
+        i = nth_set_bit(mask, q);
+        ei = a.cand_edge[sp * OTR_KMAX + i];
+        pi = a.cand_p[sp * OTR_KMAX + i];
+        wi = a.cprep[sp * OTR_KMAX + i].w;
+        ti = bt >= 0 ? a.cprep_t[sp * OTR_KMAX + i].y : 0u;
+      }
+      if (lane < Kb) {
         int64_t r = -1, rt = 0;
         if (forced) {
           r = -1;
@@ -1104,8 +1169,8 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
           r = part_mm(pj - pi, gr.len_mm[ei]);
           if (bt >= 0) rt = part_mm(pj - pi, gr.et(md)[ei]);
         } else if (lab >= 0) {
-          r = (int64_t)a.cprep[sp * OTR_KMAX + i].w + K.d((uint32_t)lab) + tpart;
-          if (bt >= 0) rt = (int64_t)a.cprep_t[sp * OTR_KMAX + i].y + K.t((uint32_t)lab) + tpt;
+          r = (int64_t)wi + K.d((uint32_t)lab) + tpart;
+          if (bt >= 0) rt = (int64_t)ti + K.t((uint32_t)lab) + tpt;
         }
         const bool valid = r >= 0 && r <= (int64_t)bmm && (bt < 0 || rt <= (int64_t)bt);
         trow[(int64_t)i * Kb + lane] = valid ? (uint32_t)r : kNoRoute;

@@ -4,7 +4,8 @@
 set -e -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/sq
+O=gpurun_out/${1:-sq}
+shift || true
 mkdir -p $O
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
 P2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA"
@@ -13,6 +14,6 @@ i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $O/p$i -o run -- \
-    python3 bench.py --steps 1 --warmup 1 --cpu-traces 0 > $O/bench_p$i.json 2> $O/bench_p$i.err
+    python3 bench.py --steps 1 --warmup 1 --cpu-traces 0 --e2e-steps 0 --streams 1 "$@" > $O/bench_p$i.json 2> $O/bench_p$i.err
 done
 echo done
