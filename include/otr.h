@@ -246,6 +246,56 @@ int otr_hist_reduce(otr_matcher* m, const void* in, int64_t n, int32_t memory, i
 int otr_tiles_format(const otr_tile_row* rows, int64_t n, const char* source, const char* mode, int32_t rules,
                      char** out, size_t* out_len);
 
+/* ---- graph building (§8 f rank 1) -------------------------------------------------------
+ * Tile hierarchy of the reference's py/get_tiles.py:30-102 (Valhalla baldr): levels 0/1/2
+ * tile the world with 4 / 1 / 0.25 degree tiles, tile id = row * ncolumns + col.
+ *   otr_tilehier_row / otr_tilehier_col: Tiles.Row / Tiles.Col (:51-72), -1 outside the world.
+ *   otr_tilehier_file: Tiles.GetFile (:81-102), e.g. level 2, id 745313, "gph" ->
+ *     "2/000/745/313.gph"; out gets the NUL-terminated name (cap bytes of room).
+ *   otr_tilehier_files: the script's listing (:132-171) for a bbox — split at the
+ *     antimeridian, levels 0, 1, 2 (Python 2 dict order), rows then columns — as
+ *     newline-terminated names in *out (release with otr_free). */
+int32_t otr_tilehier_row(int32_t level, double lat);
+int32_t otr_tilehier_col(int32_t level, double lon);
+int otr_tilehier_file(int32_t level, int64_t tile_id, const char* suffix, char* out, size_t cap);
+int otr_tilehier_files(double min_lon, double min_lat, double max_lon, double max_lat, const char* suffix, char** out,
+                   size_t* out_len);
+
+/* The flattener: decoded road-graph arrays (what a Valhalla GraphTile reader yields for
+ * the tiles otr_tilehier_files lists: nodes, directed edges, edge shapes, way ids, OSMLR
+ * associations) -> the .otrg file otr_configure uploads (include/otr_graph_format.h).
+ * Edges may come in any order; the file's edges are sorted by (src, dst), stable.
+ * Edges shorter than 5 cm are contracted (their end nodes merge into the smallest node
+ * id; DESIGN.md §3.4: the route search's A* finality margin needs edges >= 5 cm); a
+ * contracted edge's OSMLR begin/end flag moves to its segment's neighbouring edge.
+ * Routing lengths are the shapes' lengths.  Decoding the .gph binary itself needs
+ * Valhalla 2.3.6's GraphTile layout (UPSTREAM, absent here): out of scope. */
+typedef struct otr_flat_graph {
+  uint32_t n_nodes;
+  const int32_t* node_ll;      /* [2*n_nodes] lat_e6, lon_e6 */
+  uint32_t n_edges;
+  const uint32_t* edge_src;    /* node index */
+  const uint32_t* edge_dst;
+  const uint32_t* edge_attr;   /* OTR_ATTR_* fields of otr_graph_format.h (access, speed, level,
+                                  internal, OSMLR segment begin / end) */
+  const uint32_t* edge_seg;    /* OSMLR segment index into seg_id, OTR_NO_SEGMENT; may be NULL */
+  const uint32_t* edge_way;    /* OSM way id (low 32 bits); may be NULL */
+  const uint32_t* shape_off;   /* [n_edges+1] into shape_ll; a shape holds both end nodes */
+  const int32_t* shape_ll;     /* lat_e6, lon_e6 pairs */
+  uint32_t n_segments;
+  const uint64_t* seg_id;      /* OSMLR ids: level(3) | tile(22) | index(21) */
+  const uint32_t* seg_len;     /* whole metres */
+  double cell_deg;             /* candidate grid cell (degrees); 0 = 0.0005 (meili's 500 per tile) */
+} otr_flat_graph;
+
+typedef struct otr_flat_stats {
+  uint32_t n_nodes, n_edges;          /* written */
+  uint32_t n_contracted_edges;        /* edges < 5 cm (and edges inside merged clusters) */
+  uint32_t n_merged_nodes;
+} otr_flat_stats;
+
+int otr_flatten(const otr_flat_graph* in, const char* out_path, otr_flat_stats* stats);
+
 /* ---- ingest: probe text → windowed traces in HBM (§8 f rank 4) -------------------------
  * OTR_INGEST_SHARD: the "uuid,time,lat,lon,acc" lines simple_reporter.match() reads
  *   (simple_reporter.py:140-160): line.strip().split(',') into exactly 5 fields,

@@ -37,7 +37,22 @@ STAGES = ['states', 'candidates', 'link', 'route', 'route_big', 'viterbi', 'path
 EXPORTS = ['otr_configure', 'otr_configure_json', 'otr_matcher_new', 'otr_matcher_free', 'otr_match',
            'otr_report', 'otr_report_segments', 'otr_free', 'otr_last_error', 'otr_match_batch',
            'otr_graph_info', 'otr_matcher_stream', 'otr_device', 'otr_report_batch', 'otr_coalesce',
-           'otr_tiles_cull', 'otr_tiles_format', 'otr_ingest', 'otr_report_lists_device', 'otr_hist_reduce']
+           'otr_tiles_cull', 'otr_tiles_format', 'otr_ingest', 'otr_report_lists_device', 'otr_hist_reduce',
+           'otr_tilehier_row', 'otr_tilehier_col', 'otr_tilehier_file', 'otr_tilehier_files', 'otr_flatten']
+
+
+class FlatGraph(ctypes.Structure):
+    """otr_flat_graph (include/otr.h): decoded road-graph arrays for otr_flatten."""
+    _fields_ = [('n_nodes', ctypes.c_uint32), ('node_ll', ctypes.c_void_p), ('n_edges', ctypes.c_uint32),
+                ('edge_src', ctypes.c_void_p), ('edge_dst', ctypes.c_void_p), ('edge_attr', ctypes.c_void_p),
+                ('edge_seg', ctypes.c_void_p), ('edge_way', ctypes.c_void_p), ('shape_off', ctypes.c_void_p),
+                ('shape_ll', ctypes.c_void_p), ('n_segments', ctypes.c_uint32), ('seg_id', ctypes.c_void_p),
+                ('seg_len', ctypes.c_void_p), ('cell_deg', ctypes.c_double)]
+
+
+class FlatStats(ctypes.Structure):
+    _fields_ = [('n_nodes', ctypes.c_uint32), ('n_edges', ctypes.c_uint32), ('n_contracted_edges', ctypes.c_uint32),
+                ('n_merged_nodes', ctypes.c_uint32)]
 
 
 class TraceBatch(ctypes.Structure):
@@ -143,6 +158,14 @@ def lib():
                                    ctypes.c_int32, P(ctypes.c_void_p), P(ctypes.c_size_t)]
     L.otr_ingest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, P(IngestFormat),
                              P(IngestResult)]
+    L.otr_tilehier_row.argtypes = [ctypes.c_int32, ctypes.c_double]
+    L.otr_tilehier_row.restype = ctypes.c_int32
+    L.otr_tilehier_col.argtypes = [ctypes.c_int32, ctypes.c_double]
+    L.otr_tilehier_col.restype = ctypes.c_int32
+    L.otr_tilehier_file.argtypes = [ctypes.c_int32, ctypes.c_int64, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+    L.otr_tilehier_files.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_char_p,
+                                 P(ctypes.c_void_p), P(ctypes.c_size_t)]
+    L.otr_flatten.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
     L.otr_hist_reduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                   ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, P(ctypes.c_int64)]
     _L = L

@@ -62,7 +62,7 @@ def build_otr(force=False, stamps=False, variant=None, defines=()):
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
     headers += [os.path.join(ROOT, 'include', f) for f in os.listdir(os.path.join(ROOT, 'include'))]
     objs, jobs = [], []
-    for src in ('otr_engine.hip', 'otr_api.cpp', 'otr_service.cpp'):
+    for src in ('otr_engine.hip', 'otr_api.cpp', 'otr_service.cpp', 'otr_graph_build.cpp'):
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, src + suffix + '.o')
         objs.append(o)
@@ -70,7 +70,7 @@ def build_otr(force=False, stamps=False, variant=None, defines=()):
             lang = [] if src.endswith('.hip') else ['-x', 'hip']
             jobs.append([HIPCC] + HIP_FLAGS + extra + lang + ['-c', s, '-o', o])
     from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(max_workers=3) as ex:
+    with ThreadPoolExecutor(max_workers=4) as ex:
         list(ex.map(_run, jobs))
     lib = os.path.join(PKG, 'libotr%s.so' % suffix)
     if force or not _newer(lib, objs):

@@ -737,7 +737,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
     return OTR_DEVICE_ERROR;
   }
   if (S > 0) k_prep<<<grid_for(S, 4), 256, 0, stream>>>(g, pr);
-  uint4* task_rec = need<uint4>(S_TASK_REC, 2 * (size_t)std::max<int64_t>(NT, 1));
+  uint4* task_rec = need<uint4>(S_TASK_REC, 3 * (size_t)std::max<int64_t>(NT, 1));
   if (!task_rec) {
     if (err) *err = "device allocation failed (task records)";
     return OTR_DEVICE_ERROR;
@@ -745,7 +745,7 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   if (NT > 0)
     k_task_rec<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_state, task_mask, sb.prev, sb.bound, sb.forced, cb.count,
                                                       cb.edge, g.edge_dst, state_trace, b.mode, pr.cprep, sb.bt,
-                                                      turn_modes, task_rec);
+                                                      turn_modes, pr.heur, g.node_ll, trans_off, task_rec);
   ra.heur = pr.heur;
   ra.cprep = pr.cprep;
   ra.cprep_t = pr.cprep_t;

@@ -720,7 +720,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
                            bool active, uint32_t start, uint32_t bound_mm, uint32_t delta_mm, uint32_t tnode,
                            uint32_t tpart, uint32_t hT, uint32_t d0min, int n_tgt, unsigned long long* settled,
                            unsigned long long* relaxed, unsigned long long* rounds,
-                           unsigned long long* stamps = nullptr) {
+                           unsigned long long* stamps = nullptr, uint32_t hroot_in = 0xFFFFFFFFu) {
   using Gr = Grp<G>;
   // load-factor limit (probe chains stay short); small tables run fuller
   // (7/8 on the retry tiers: fewer searches outgrow 448/512 slots; C4 4.79M -> 5.11M
@@ -729,8 +729,12 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
   constexpr int kMaxKeys = (CAP <= 128 || CAP >= 256) ? (CAP * 7) / 8 : (CAP * 3) / 4;
   const int gl = Gr::gl();
   SearchLds<CAP, PRED>& L = Ls[Gr::g()];
-  const int2 sll = g.node_ll[active ? start : 0u];
-  const uint32_t hroot = H(sll.x, sll.y);
+  // h(root): given (k_task_rec), or from the root's coordinates
+  uint32_t hroot = hroot_in;
+  if (hroot_in == 0xFFFFFFFFu) {
+    const int2 sll = g.node_ll[active ? start : 0u];
+    hroot = H(sll.x, sll.y);
+  }
   using Idx = typename SearchLds<CAP, PRED>::Idx;
   constexpr int WCAP = SearchLds<CAP, PRED>::WCAP;
   const bool timed = K.sh != 0u;  // group-uniform
@@ -977,15 +981,18 @@ struct RouteArgs {
 // need that sits behind a chain of dependent loads (task → state → previous state →
 // first source edge → root node; mode through the trace): the search kernels read two
 // 16-B words instead of walking that chain twice (before and after the search).
-//   rec[2t]   = {s, sp, root, bound_mm}
-//   rec[2t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16, mask lo, mask hi}
+//   rec[3t]   = {s, sp, root, bound_mm}
+//   rec[3t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16, mask lo, mask hi}
+//   rec[3t+2] = {h(root), time bound bt, trans_off[s] lo, hi}
+// (h(root) here takes the root's coordinates, the search's first dependent global load,
+// off the search kernels' critical path)
 // general: the task runs in the global-memory search (turn costs: edge-based labels; or
 // a bound whose packed labels would not fit 32 bits).
 __global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const unsigned long long* task_mask,
                            const int64_t* prev, const double* bound, const uint8_t* forced, const int32_t* cand_count,
                            const uint32_t* cand_edge, const uint32_t* edge_dst, const int32_t* state_trace,
                            const uint8_t* mode, const uint4* cprep, const int32_t* bt, uint32_t turn_modes,
-                           uint4* rec) {
+                           const Heur* heur, const int2* node_ll, const int64_t* trans_off, uint4* rec) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tasks) return;
   const int64_t s = task_state[t];
@@ -1007,8 +1014,12 @@ __global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const uns
 #endif
   const uint32_t meta = (uint32_t)cand_count[s] | ((uint32_t)md << 8) | ((forced[s] ? 1u : 0u) << 10) | (sh << 11) |
                         ((general ? 1u : 0u) << 16);
-  rec[2 * t] = make_uint4((uint32_t)s, (uint32_t)sp, root, bmm);
-  rec[2 * t + 1] = make_uint4(d0min, meta, (uint32_t)mask, (uint32_t)(mask >> 32));
+  const int2 rll = node_ll[root];
+  const uint32_t hroot = heur[s](rll.x, rll.y);
+  const int64_t to = trans_off[s];
+  rec[3 * t] = make_uint4((uint32_t)s, (uint32_t)sp, root, bmm);
+  rec[3 * t + 1] = make_uint4(d0min, meta, (uint32_t)mask, (uint32_t)(mask >> 32));
+  rec[3 * t + 2] = make_uint4(hroot, (uint32_t)bt[s], (uint32_t)to, (uint32_t)((uint64_t)to >> 32));
 }
 
 #ifndef OTR_ROUTE2_WAVES
@@ -1035,13 +1046,14 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   OTR_STAMP(ts_in);
   // ---- search inputs (only these stay live through the search)
   bool search, fits, forced;
-  uint32_t tnode = kEmpty, tpart = 0, hT = 0, d0min = 0xFFFFFFFFu, root = 0, bmm = 0, mode_bit = 1;
+  uint32_t tnode = kEmpty, tpart = 0, hT = 0, d0min = 0xFFFFFFFFu, root = 0, bmm = 0, mode_bit = 1, hroot = 0;
   int Kb;
   Pack K;
   Heur H;
   {
-    const uint4 r0 = have ? a.rec[2 * task] : make_uint4(0u, 0u, 0u, 0u);
-    const uint4 r1 = have ? a.rec[2 * task + 1] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+    const uint4 r0 = have ? a.rec[3 * task] : make_uint4(0u, 0u, 0u, 0u);
+    const uint4 r1 = have ? a.rec[3 * task + 1] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+    hroot = have ? a.rec[3 * task + 2].x : 0u;
     const int64_t s = r0.x;
     const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
     const int64_t sp = r0.y;
@@ -1101,7 +1113,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   search_init<CAP, false, G>(Ls);
   bool ok = search_run<CAP, false, G>(Ls, gr, H, K, mode_bit, search, root, bmm,
                                       (uint32_t)(a.delta * 1000.0), tnode, tpart, hT, d0min, Kb, &settled, &relaxed,
-                                      &rounds, counters ? counters + 16 * kCShards : nullptr) &&
+                                      &rounds, counters ? counters + 16 * kCShards : nullptr, hroot) &&
             fits;
 #ifdef OTR_FORCE_RETRY
   if (G == 2 && !LIST) ok = false;  // test build: every first-tier task takes the retry tiers
@@ -1117,14 +1129,14 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   asm volatile("" ::: "memory");
   uint32_t ntr = 0;  // transition entries this search wrote (K4), for the work counters
   if (have && (ok || forced)) {
-    const uint4 r0 = a.rec[2 * task], r1 = a.rec[2 * task + 1];
+    const uint4 r0 = a.rec[3 * task], r1 = a.rec[3 * task + 1], r2 = a.rec[3 * task + 2];
     const int64_t s = r0.x;
     const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
     if (search) ntr = (uint32_t)Kb * (uint32_t)__popcll(mask);
     const int64_t sp = r0.y;
-    const int32_t bt = a.bt[s];
+    const int32_t bt = (int32_t)r2.y;
     const int md = (int)((r1.y >> 8) & 3u);
-    uint32_t* trow = a.trans + a.trans_off[s];
+    uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
     // sources staged one per lane as in the setup: {index, edge, fraction, exit part mm,
     // exit part time}, read by group shuffles in the row loop
     const int nsrc = __popcll(mask);
@@ -1181,7 +1193,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   // first-tier search with a long bound (> 1.9 km) that outgrew 160 slots goes straight
   // to the 1024-slot tier (flag 2)
   if (have && !ok && !forced && lane == 0) {
-    const bool general = (a.rec[2 * task + 1].y >> 16) & 1u;
+    const bool general = (a.rec[3 * task + 1].y >> 16) & 1u;
     a.overflow_flag[task] = general ? 3 : ((G == 2 && !LIST && bmm > 1900000u) ? 2 : 1);
   }
 #ifdef OTR_STAMPS

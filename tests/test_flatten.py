@@ -1,0 +1,113 @@
+"""otr_flatten (include/otr.h, §8f rank 1): decoded road-graph arrays -> .otrg, on the
+CPU (host code in libotr.so).  A generated graph given back as raw arrays in shuffled
+edge order flattens to a byte-identical file; with edges split by extra nodes on their
+heads (duplicate OSM nodes: zero-length pieces, which carry the OSMLR segment-end
+flags), the 5 cm contraction restores the original graph byte for byte; and the
+contracted graph's node / edge counts are reported."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from reporter_amd import _lib
+from reporter_amd.graphfile import ATTR_SEG_BEGIN, ATTR_SEG_END, GraphFile
+from reporter_amd.tools import gen
+
+
+def _flatten(arrays, out, cell_deg):
+    keep = {k: np.ascontiguousarray(v) for k, v in arrays.items()}
+    fg = _lib.FlatGraph()
+    fg.n_nodes = len(keep['node_ll']) // 2
+    fg.node_ll = keep['node_ll'].ctypes.data
+    fg.n_edges = len(keep['edge_src'])
+    for k in ('edge_src', 'edge_dst', 'edge_attr', 'edge_seg', 'edge_way', 'shape_off', 'shape_ll', 'seg_id',
+              'seg_len'):
+        setattr(fg, k, keep[k].ctypes.data if len(keep[k]) else None)
+    fg.n_segments = len(keep['seg_id'])
+    fg.cell_deg = cell_deg
+    st = _lib.FlatStats()
+    rc = _lib.lib().otr_flatten(ctypes.byref(fg), out.encode(), ctypes.byref(st))
+    assert rc == 0
+    return st
+
+
+def _raw(G, order):
+    shp = [G.shape_ll[2 * G.edge_shape[e]:2 * G.edge_shape[e + 1]] for e in order]
+    off = np.zeros(len(order) + 1, np.uint32)
+    off[1:] = np.cumsum([len(s) // 2 for s in shp])
+    return {'node_ll': G.node_ll.copy(), 'edge_src': G.edge_src[order], 'edge_dst': G.edge_dst[order],
+            'edge_attr': G.edge_attr[order], 'edge_seg': G.edge_seg[order], 'edge_way': G.edge_way[order],
+            'shape_off': off, 'shape_ll': np.concatenate(shp).astype(np.int32), 'seg_id': G.seg_id.copy(),
+            'seg_len': G.seg_len.copy()}
+
+
+@pytest.fixture(scope='module')
+def city(graph_dir):
+    return gen.graph_path('city', graph_dir)
+
+
+def test_round_trip_byte_identical(city, tmp_path):
+    G = GraphFile(city)
+    order = np.random.default_rng(5).permutation(G.n_edges)
+    out = str(tmp_path / 'flat.otrg')
+    st = _flatten(_raw(G, order), out, G.h['grid_cell_deg'])
+    assert (st.n_nodes, st.n_edges, st.n_contracted_edges, st.n_merged_nodes) == (G.n_nodes, G.n_edges, 0, 0)
+    assert open(out, 'rb').read() == open(city, 'rb').read()
+
+
+def test_short_edges_contracted(city, tmp_path):
+    """Split edges by a duplicate of their head node: the new zero-length pieces (carrying
+    the segment-end flag) are contracted away and the file equals the original."""
+    G = GraphFile(city)
+    raw = _raw(G, np.arange(G.n_edges))
+    rng = np.random.default_rng(7)
+    picks = set(rng.choice(G.n_edges, 300, replace=False).tolist())
+    # make sure segment-end edges are among them
+    ends = np.flatnonzero(G.edge_attr & ATTR_SEG_END)
+    picks |= set(ends[:50].tolist())
+    node_ll = list(raw['node_ll'].reshape(-1, 2))
+    src, dst, attr, seg, way, shapes = [], [], [], [], [], []
+    n_new = 0
+    for e in range(G.n_edges):
+        s = raw['shape_ll'][2 * raw['shape_off'][e]:2 * raw['shape_off'][e + 1]].reshape(-1, 2)
+        if e not in picks:
+            src.append(G.edge_src[e]); dst.append(G.edge_dst[e]); attr.append(G.edge_attr[e])
+            seg.append(G.edge_seg[e]); way.append(G.edge_way[e]); shapes.append(s)
+            continue
+        x = s[-1].astype(np.int32)  # a duplicate of the head (micro-degree grid: 0.11 m steps)
+        xid = len(node_ll)
+        node_ll.append(x)
+        n_new += 1
+        head = G.edge_attr[e] & ~np.uint32(ATTR_SEG_END)
+        tail = G.edge_attr[e] & ~np.uint32(ATTR_SEG_BEGIN)
+        src.append(G.edge_src[e]); dst.append(xid); attr.append(head); seg.append(G.edge_seg[e])
+        way.append(G.edge_way[e]); shapes.append(np.vstack([s[:-1], x[None]]))
+        src.append(xid); dst.append(G.edge_dst[e]); attr.append(tail); seg.append(G.edge_seg[e])
+        way.append(G.edge_way[e]); shapes.append(np.vstack([x[None], s[-1:]]))
+    off = np.zeros(len(shapes) + 1, np.uint32)
+    off[1:] = np.cumsum([len(s) for s in shapes])
+    split = {'node_ll': np.array(node_ll, np.int32).reshape(-1), 'edge_src': np.array(src, np.uint32),
+             'edge_dst': np.array(dst, np.uint32), 'edge_attr': np.array(attr, np.uint32),
+             'edge_seg': np.array(seg, np.uint32), 'edge_way': np.array(way, np.uint32), 'shape_off': off,
+             'shape_ll': np.concatenate(shapes).astype(np.int32).reshape(-1), 'seg_id': raw['seg_id'],
+             'seg_len': raw['seg_len']}
+    out = str(tmp_path / 'split.otrg')
+    st = _flatten(split, out, G.h['grid_cell_deg'])
+    assert st.n_merged_nodes == n_new and st.n_contracted_edges == n_new
+    assert (st.n_nodes, st.n_edges) == (G.n_nodes, G.n_edges)
+    assert open(out, 'rb').read() == open(city, 'rb').read()
+
+
+def test_bad_input_rejected(tmp_path):
+    fg = _lib.FlatGraph()
+    fg.n_nodes = 1
+    ll = np.zeros(2, np.int32)
+    fg.node_ll = ll.ctypes.data
+    fg.n_edges = 1
+    e = np.array([0], np.uint32)
+    bad = np.array([5], np.uint32)
+    off = np.array([0, 2], np.uint32)
+    sh = np.zeros(4, np.int32)
+    fg.edge_src, fg.edge_dst, fg.edge_attr = e.ctypes.data, bad.ctypes.data, e.ctypes.data
+    fg.shape_off, fg.shape_ll = off.ctypes.data, sh.ctypes.data
+    assert _lib.lib().otr_flatten(ctypes.byref(fg), str(tmp_path / 'x').encode(), None) != 0
