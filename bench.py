@@ -111,11 +111,12 @@ def main():
     ap.add_argument('--delta', type=float, default=None, help='routing round width (perf knob, metres)')
     ap.add_argument('--streams', type=int, default=2,
                     help='matchers (one HIP stream + host thread each) sharing the batch')
-    ap.add_argument('--workload', choices=['c2', 'c3', 'c4', 'c5mix'], default='c2',
+    ap.add_argument('--workload', choices=['c2', 'c3', 'c4', 'c5mix', 'c5'], default='c2',
                     help='c2 (default, the headline): 100 probes @15 s, sigma 10 m; c3: the C3 shard of '
                          '1M veh%%07d uuids x 100 probes this GPU owns; c4: 60 probes @60 s, sigma 50 m, '
                          'accuracy 50 m, search radius 200 m; c5mix: C2 with the C5 mode mix '
-                         '(60%% auto / 25%% bicycle / 15%% pedestrian) on the metro graph')
+                         '(60%% auto / 25%% bicycle / 15%% pedestrian) on the metro graph; c5: the country graph '
+                         '(50M nodes), this GPU\'s N = 8 share (125,000) of 1M vehicles over 24 h, C5 mode mix')
     ap.add_argument('--e2e-steps', type=int, default=3, help='host-to-host drop-in steps (0 = skip)')
     ap.add_argument('--opt', action='append', default=[],
                     help='A/B only (not the headline config): KEY=VALUE match option override, e.g. '
@@ -163,10 +164,13 @@ def main():
         raise SystemExit('libotr.so missing: run python __graft_entry__.py build first')
 
     gdir = os.path.join(ROOT, 'build', 'graphs')
+    gname = 'country' if args.workload == 'c5' else 'metro'
     if rank == 0:
-        gpath = gen.graph_path('metro', gdir)
+        tg = time.time()
+        gpath = gen.graph_path(gname, gdir)
+        log('graph %s ready (%.1fs)' % (gname, time.time() - tg))
     barrier()
-    gpath = gen.graph_path('metro', gdir)
+    gpath = gen.graph_path(gname, gdir)
 
     # match_options as generate_test_trace.py:44-52 sends them (turn_penalty_factor 0,
     # gps_accuracy = the 95th percentile of the noise); max_route_time_factor stays the
@@ -179,25 +183,31 @@ def main():
          'c4': dict(points=60, rate=60, sigma=50.0, seed=4, bike=0.0, ped=0.0, acc=50.0, traces=20000,
                     meili=dict(gtt, search_radius=200, max_search_radius=200, gps_accuracy=82.24)),
          'c5mix': dict(points=100, rate=15, sigma=10.0, seed=5, bike=0.25, ped=0.15, acc=None, traces=10000,
-                       meili=dict(gtt, search_radius=50, gps_accuracy=16.45))}[args.workload]
+                       meili=dict(gtt, search_radius=50, gps_accuracy=16.45)),
+         # C5: the country graph, 1M vehicles' traces over 24 h with the 60/25/15 mode mix,
+         # uuid-sharded like C3; per GPU the N = 8 share (125,000 traces, 12.5M probes)
+         'c5': dict(points=100, rate=15, sigma=10.0, seed=5, bike=0.25, ped=0.15, acc=None, traces=125000,
+                    spread=86400, meili=dict(gtt, search_radius=50, gps_accuracy=16.45))}[args.workload]
 
     for kv in args.opt:
         k, v = kv.split('=', 1)
         W['meili'][k] = float(v)
     t0 = time.time()
-    if args.workload == 'c3':
-        # C3: 1,000,000 uuids "veh%07d" x 100 probes, sharded by
+    if args.workload in ('c3', 'c5'):
+        # C3 / C5: 1,000,000 uuids "veh%07d" x 100 probes, sharded by
         # int(sha1(uuid)[:3], 16) % N (simple_reporter.py:116); each rank generates only the
         # uuids it owns (a uuid's trace is seeded by its number, so shards are independent).
-        # --traces-per-gpu bounds the uuids per rank (a one-GPU rehearsal).
+        # --traces-per-gpu bounds the uuids per rank (C3: a one-GPU rehearsal; C5: the
+        # N = 8 share by default).
         n_uuid = 1000000
         owner = np.array([int(hashlib.sha1(('veh%07d' % u).encode()).hexdigest()[:3], 16) % world
                           for u in range(n_uuid)])
         mine_ids = np.flatnonzero(owner == rank)
-        if args.traces_per_gpu:
-            mine_ids = mine_ids[:args.traces_per_gpu]
-        mine = gen.make_traces_ids(gpath, mine_ids, W['points'], W['rate'], W['sigma'], W['seed'],
-                                   t_begin=T_BEGIN, t_spread=1800)
+        cap = args.traces_per_gpu or W['traces']
+        if cap:
+            mine_ids = mine_ids[:cap]
+        mine = gen.make_traces_ids(gpath, mine_ids, W['points'], W['rate'], W['sigma'], W['seed'], W['bike'],
+                                   W['ped'], W['acc'], t_begin=T_BEGIN, t_spread=W.get('spread', 1800))
     else:
         n_per = args.traces_per_gpu or W['traces']
         n_global = n_per * world
@@ -224,7 +234,11 @@ def main():
     parts = [mine.subset(np.arange(cuts[k], cuts[k + 1])) for k in range(ns)]
     matchers = [M.Matcher() for _ in range(ns)]
     dev = torch.device('cuda', local)
-    hours = 3  # traces start within 30 min of T_BEGIN and last <= 100 min
+    # dense histogram hours: traces start within `spread` of T_BEGIN and last <= 100 min
+    hours = (W.get('spread', 1800) + W['points'] * W['rate']) // 3600 + 2
+    if args.hist == 'dense' and args.workload == 'c5':
+        raise SystemExit('bench: the dense [hour][segment][speed] histogram of C5 would take %d GB; use --hist keyed'
+                         % (hours * 60 * 8 * 4 // 1000))
     hist_len = hours * n_segments * _lib.HIST_BINS
     hist_len += (-hist_len) % world
     keep, darrs, hists = [], [], []
@@ -396,7 +410,7 @@ def main():
 
     # ---- rank 0, N = 1: oracle sample (CPU baseline) and its bit-exact comparison
     cpu, parity = None, None
-    n_cpu = args.cpu_traces if args.cpu_traces is not None else {'c2': 6000, 'c5mix': 6000, 'c4': 600,
+    n_cpu = args.cpu_traces if args.cpu_traces is not None else {'c2': 6000, 'c5mix': 6000, 'c4': 600, 'c5': 3000,
                                                                  'c3': 6000}[args.workload]
     if rank == 0 and world == 1 and n_cpu > 0:
         from oracle import pyoracle as po
@@ -474,14 +488,17 @@ def main():
             'vs_baseline': None,
             'dtype': 'f64',
             'data': 'synthetic',
-            'config': {'workload': '%s: metro street grid (%d nodes, %d directed edges, %d OSMLR segments), '
+            'config': {'workload': '%s: %s street grid (%d nodes, %d directed edges, %d OSMLR segments), '
                                    '%d traces x %d probes per GPU @%d s, sigma %g m%s; generate_test_trace '
                                    'match_options, max_route_time_factor 2' % (
-                                       args.workload.upper(), n_nodes, n_edges, n_segments, mine.n_traces,
+                                       args.workload.upper(), 'country' if gname == 'country' else 'metro', n_nodes,
+                                       n_edges, n_segments, mine.n_traces,
                                        W['points'], W['rate'], W['sigma'],
                                        {'c2': '', 'c3': ', C3 uuid shard (1M veh%07d uuids, sha1[:3] % N)',
                                         'c4': ', accuracy 50 m, search radius 200 m',
-                                        'c5mix': ', modes 60% auto / 25% bicycle / 15% pedestrian'}[
+                                        'c5mix': ', modes 60% auto / 25% bicycle / 15% pedestrian',
+                                        'c5': ', 1M veh%07d uuids sha1[:3] % 8 share over 24 h, modes 60% auto / '
+                                              '25% bicycle / 15% pedestrian'}[
                                            args.workload]),
                        'probes_per_step': int(total_probes),
                        'parallelism': ('uuid-sharded dp%d + ' % world + (

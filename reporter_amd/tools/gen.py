@@ -16,6 +16,9 @@ GRAPHS = {
     'tiny': (24, 24, 60.0, 14.55, 121.03, 0.10, 11, 0.0005),
     'city': (200, 200, 50.0, 14.55, 121.03, 0.15, 1, 0.0005),
     'metro': (1024, 1024, 50.0, 14.55, 121.03, 0.15, 2, 0.0005),
+    # C5: a country-scale grid, 7072 x 7072 = 50M nodes over ~700 x 700 km,
+    # ~135M directed edges (minutes to generate; 12 GB file)
+    'country': (7072, 7072, 100.0, 14.55, 121.03, 0.40, 5, 0.0005),
 }
 CONFIGS = {
     # graph, n_traces, points/trace, sample_rate s, sigma m, seed, frac_bicycle, frac_ped, search_radius

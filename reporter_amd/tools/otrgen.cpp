@@ -64,7 +64,8 @@ struct Link {  // undirected street link between grid nodes a→b (a < b in walk
   int dir;            // 0 both, +1 a→b only, -1 b→a only
   bool internal, unassociated;
   uint32_t access;
-  std::vector<std::pair<int32_t, int32_t>> mid;  // intermediate shape points (lat_e6, lon_e6)
+  uint64_t mid_off;  // intermediate shape points (lat_e6, lon_e6): mids[mid_off, mid_off + nmid)
+  uint32_t nmid;
 };
 
 struct DEdge {
@@ -105,6 +106,14 @@ extern "C" {
 // Generates a street-grid graph and writes it to `path`.  Returns 0 on success.
 int otrgen_graph(const char* path, int rows, int cols, double spacing_m, double center_lat,
                  double center_lon, double p_remove, uint64_t seed, double cell_deg) {
+  // country-scale graphs (C5, ~50M nodes) take minutes: progress on stderr
+  const bool big = (uint64_t)rows * (uint64_t)cols > 4000000ull;
+  auto say = [&](const char* what) {
+    if (big) {
+      fprintf(stderr, "otrgen: %s\n", what);
+      fflush(stderr);
+    }
+  };
   Rng rng(seed);
   const double mlon = kMetersPerDeg * std::cos(center_lat * M_PI / 180.0);
   const uint32_t n_nodes = (uint32_t)rows * (uint32_t)cols;
@@ -121,6 +130,8 @@ int otrgen_graph(const char* path, int rows, int cols, double spacing_m, double 
   auto line_level = [](int k) { return k % 16 == 0 ? 0 : (k % 4 == 0 ? 1 : 2); };
   std::vector<Link> links;
   links.reserve(2 * (size_t)n_nodes);
+  std::vector<std::pair<int32_t, int32_t>> mids;
+  mids.reserve(2 * (size_t)n_nodes);
   // horizontal lines (rows), then vertical lines (cols)
   for (int pass = 0; pass < 2; ++pass) {
     int nl = pass == 0 ? rows : cols, len = pass == 0 ? cols : rows;
@@ -147,14 +158,16 @@ int otrgen_graph(const char* path, int rows, int cols, double spacing_m, double 
         int nmid = (int)rng.below(3);
         int32_t la = node_ll[2 * L.a], loa = node_ll[2 * L.a + 1];
         int32_t lb = node_ll[2 * L.b], lob = node_ll[2 * L.b + 1];
+        L.mid_off = mids.size();
+        L.nmid = (uint32_t)nmid;
         for (int m = 1; m <= nmid; ++m) {
           double f = (double)m / (nmid + 1);
           double off = (rng.uni() * 2 - 1) * 4.0;  // metres, perpendicular wiggle
           double lat = (la + f * (lb - la)) * 1e-6, lon = (loa + f * (lob - loa)) * 1e-6;
           if (pass == 0) lat += off / kMetersPerDeg; else lon += off / mlon;
-          L.mid.push_back({(int32_t)std::llround(lat * 1e6), (int32_t)std::llround(lon * 1e6)});
+          mids.push_back({(int32_t)std::llround(lat * 1e6), (int32_t)std::llround(lon * 1e6)});
         }
-        links.push_back(std::move(L));
+        links.push_back(L);
       }
     }
   }
@@ -174,6 +187,7 @@ int otrgen_graph(const char* path, int rows, int cols, double spacing_m, double 
     }
     if (!changed) break;
   }
+  say("links done");
   // directed edges
   std::vector<DEdge> de;
   de.reserve(2 * links.size());
@@ -185,6 +199,8 @@ int otrgen_graph(const char* path, int rows, int cols, double spacing_m, double 
   std::sort(de.begin(), de.end(), [](const DEdge& x, const DEdge& y) {
     return x.src != y.src ? x.src < y.src : x.dst < y.dst;
   });
+  say("directed edges sorted");
+  if (de.size() >= 0xFFFFFFFFull) return -3;
   const uint32_t n_edges = (uint32_t)de.size();
   std::vector<uint32_t> node_row(n_nodes + 1, 0), edge_src(n_edges), edge_dst(n_edges), edge_attr(n_edges),
       edge_shape(n_edges + 1), edge_seg(n_edges, OTR_NO_SEGMENT), edge_way(n_edges);
@@ -205,13 +221,14 @@ int otrgen_graph(const char* path, int rows, int cols, double spacing_m, double 
     edge_attr[e] = attr;
     edge_way[e] = 100000u + L.line * 64u + L.pos / 20u;
     edge_shape[e] = (uint32_t)(shape_ll.size() / 2);
-    std::vector<std::pair<int32_t, int32_t>> pts;
-    pts.push_back({node_ll[2 * d.src], node_ll[2 * d.src + 1]});
-    if (d.fwd) for (auto& m : L.mid) pts.push_back(m);
-    else for (auto it = L.mid.rbegin(); it != L.mid.rend(); ++it) pts.push_back(*it);
-    pts.push_back({node_ll[2 * d.dst], node_ll[2 * d.dst + 1]});
+    std::pair<int32_t, int32_t> pts[4];
+    size_t np = 0;
+    pts[np++] = {node_ll[2 * (size_t)d.src], node_ll[2 * (size_t)d.src + 1]};
+    if (d.fwd) for (uint32_t m = 0; m < L.nmid; ++m) pts[np++] = mids[L.mid_off + m];
+    else for (uint32_t m = L.nmid; m-- > 0;) pts[np++] = mids[L.mid_off + m];
+    pts[np++] = {node_ll[2 * (size_t)d.dst], node_ll[2 * (size_t)d.dst + 1]};
     double len = 0;
-    for (size_t k = 0; k < pts.size(); ++k) {
+    for (size_t k = 0; k < np; ++k) {
       shape_ll.push_back(pts[k].first);
       shape_ll.push_back(pts[k].second);
       if (k) len += seg_len_m(pts[k - 1].first, pts[k - 1].second, pts[k].first, pts[k].second);
@@ -291,6 +308,7 @@ int otrgen_graph(const char* path, int rows, int cols, double spacing_m, double 
     std::vector<uint32_t> fill(rev_row.begin(), rev_row.end() - 1);
     for (uint32_t e = 0; e < n_edges; ++e) rev_edge[fill[edge_dst[e]]++] = e;
   }
+  say("segments done");
   // grid index
   int32_t mnla = INT32_MAX, mnlo = INT32_MAX, mxla = INT32_MIN, mxlo = INT32_MIN;
   for (size_t k = 0; k < shape_ll.size(); k += 2) {
@@ -301,32 +319,46 @@ int otrgen_graph(const char* path, int rows, int cols, double spacing_m, double 
   double gmin_lon = std::floor(mnlo * 1e-6 / cell_deg) * cell_deg - cell_deg;
   uint32_t grows = (uint32_t)std::ceil((mxla * 1e-6 - gmin_lat) / cell_deg) + 2;
   uint32_t gcols = (uint32_t)std::ceil((mxlo * 1e-6 - gmin_lon) / cell_deg) + 2;
+  if ((uint64_t)grows * gcols >= 0xFFFFFFFFull) return -4;
   uint32_t n_cells = grows * gcols;
-  std::vector<std::pair<uint32_t, uint32_t>> ce;  // (cell, edge)
-  ce.reserve((size_t)n_edges * 4);
-  for (uint32_t e = 0; e < n_edges; ++e) {
-    size_t first = ce.size();
+  // (cell, edge) entries by a counting sort over cells: every cell lists its edges in
+  // ascending order, each once (what sorting the (cell, edge) pairs gives)
+  auto edge_cells = [&](uint32_t e, std::vector<uint32_t>& cells) {
+    cells.clear();
     for (uint32_t k = edge_shape[e]; k + 1 < edge_shape[e + 1]; ++k) {
-      double la0 = shape_ll[2 * k] * 1e-6, lo0 = shape_ll[2 * k + 1] * 1e-6;
-      double la1 = shape_ll[2 * k + 2] * 1e-6, lo1 = shape_ll[2 * k + 3] * 1e-6;
+      double la0 = shape_ll[2 * (size_t)k] * 1e-6, lo0 = shape_ll[2 * (size_t)k + 1] * 1e-6;
+      double la1 = shape_ll[2 * (size_t)k + 2] * 1e-6, lo1 = shape_ll[2 * (size_t)k + 3] * 1e-6;
       double a = std::min(la0, la1) - OTR_GRID_PAD_DEG, b = std::max(la0, la1) + OTR_GRID_PAD_DEG;
       double c = std::min(lo0, lo1) - OTR_GRID_PAD_DEG, d = std::max(lo0, lo1) + OTR_GRID_PAD_DEG;
       int64_t r0 = (int64_t)std::floor((a - gmin_lat) / cell_deg), r1 = (int64_t)std::floor((b - gmin_lat) / cell_deg);
       int64_t c0 = (int64_t)std::floor((c - gmin_lon) / cell_deg), c1 = (int64_t)std::floor((d - gmin_lon) / cell_deg);
       for (int64_t r = std::max<int64_t>(r0, 0); r <= std::min<int64_t>(r1, grows - 1); ++r)
         for (int64_t cc = std::max<int64_t>(c0, 0); cc <= std::min<int64_t>(c1, gcols - 1); ++cc)
-          ce.push_back({(uint32_t)(r * gcols + cc), e});
+          cells.push_back((uint32_t)(r * gcols + cc));
     }
-    std::sort(ce.begin() + first, ce.end());
-    ce.erase(std::unique(ce.begin() + first, ce.end()), ce.end());
+    std::sort(cells.begin(), cells.end());
+    cells.erase(std::unique(cells.begin(), cells.end()), cells.end());
+  };
+  std::vector<uint32_t> cell_row(n_cells + 1, 0), cells;
+  for (uint32_t e = 0; e < n_edges; ++e) {
+    edge_cells(e, cells);
+    for (uint32_t c : cells) cell_row[c + 1]++;
   }
-  std::sort(ce.begin(), ce.end());
-  std::vector<uint32_t> cell_row(n_cells + 1, 0), cell_edge(ce.size());
-  for (size_t k = 0; k < ce.size(); ++k) {
-    cell_row[ce[k].first + 1]++;
-    cell_edge[k] = ce[k].second;
+  {
+    uint64_t total = 0;
+    for (uint32_t c = 0; c < n_cells; ++c) total += cell_row[c + 1];
+    if (total >= 0xFFFFFFFFull) return -5;  // u32 cell offsets (include/otr_graph_format.h)
   }
   for (uint32_t c = 0; c < n_cells; ++c) cell_row[c + 1] += cell_row[c];
+  std::vector<uint32_t> cell_edge(cell_row[n_cells]);
+  {
+    std::vector<uint32_t> fill(cell_row.begin(), cell_row.end() - 1);
+    for (uint32_t e = 0; e < n_edges; ++e) {
+      edge_cells(e, cells);
+      for (uint32_t c : cells) cell_edge[fill[c]++] = e;
+    }
+  }
+  say("grid done");
 
   FILE* f = fopen(path, "wb");
   if (!f) return -1;
