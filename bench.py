@@ -239,7 +239,9 @@ def main():
     if args.hist == 'dense' and args.workload == 'c5':
         raise SystemExit('bench: the dense [hour][segment][speed] histogram of C5 would take %d GB; use --hist keyed'
                          % (hours * 60 * 8 * 4 // 1000))
-    hist_len = hours * n_segments * _lib.HIST_BINS
+    keyed = args.hist == 'keyed'
+    # the dense histogram's tensors exist only in dense mode (C5's would be 4 x 51 GB)
+    hist_len = hours * n_segments * _lib.HIST_BINS if not keyed else world
     hist_len += (-hist_len) % world
     keep, darrs, hists = [], [], []
     for part in parts:
@@ -259,7 +261,6 @@ def main():
     tile_stats = []
     torch.cuda.synchronize()
 
-    keyed = args.hist == 'keyed'
     EW = _lib.HIST_ENTRY.itemsize
     ebufs = [torch.zeros(0, dtype=torch.uint8, device=dev) for _ in range(ns)]  # per-stream local entries
     n_local, n_rows, row_views = [0] * ns, [0] * ns, [None] * ns

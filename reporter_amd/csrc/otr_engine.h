@@ -100,11 +100,20 @@ struct Matcher {
 
   template <class T>
   T* need(int slot, size_t n);
+  // entry points: a device allocation failure inside returns OTR_DEVICE_ERROR (no kernel
+  // runs on a missing buffer); the *_impl bodies do the work
   int run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err);
   int tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int privacy, int rules, const otr_tile_row** out,
                  int64_t* n_out, std::string* err);
   int hist_reduce(const void* in, int64_t n, int memory, int rows_in, int privacy, const otr_hist_entry** out,
                   int64_t* n_out, std::string* err);
+  int run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err);
+  int tiles_cull_impl(const otr_tile_row* rows, int64_t n, int memory, int privacy, int rules,
+                      const otr_tile_row** out, int64_t* n_out, std::string* err);
+  int hist_reduce_impl(const void* in, int64_t n, int memory, int rows_in, int privacy, const otr_hist_entry** out,
+                       int64_t* n_out, std::string* err);
+  int ingest_impl(const char* text, int64_t len, int memory, const otr_ingest_format* fmt, otr_ingest_result* out,
+                  std::string* err);
   int copy_out(void* dst, const void* src, size_t bytes, int dst_memory, std::string* err);
   int ingest(const char* text, int64_t len, int memory, const otr_ingest_format* fmt, otr_ingest_result* out,
              std::string* err);

@@ -386,6 +386,14 @@ enum Slot {
   S_NUM
 };
 
+// A device buffer that cannot be allocated ends the call: need() throws, the entry
+// points (run, tiles_cull, hist_reduce, ingest) catch it after draining the stream and
+// return OTR_DEVICE_ERROR naming the buffer — no kernel ever runs on a missing buffer.
+struct DeviceOom {
+  int slot;
+  size_t bytes;
+};
+
 template <class T>
 T* Matcher::need(int slot, size_t n) {
   if ((int)bufs.size() < S_NUM) bufs.resize(S_NUM);
@@ -393,15 +401,29 @@ T* Matcher::need(int slot, size_t n) {
   size_t bytes = (n ? n : 1) * sizeof(T);
   if (b.bytes < bytes) {
     if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
     size_t nb = bytes + bytes / 4;
-    if (hipMalloc(&b.p, nb) != hipSuccess) {
+    if (hipMalloc(&b.p, nb) != hipSuccess && hipMalloc(&b.p, bytes) != hipSuccess) {
+      (void)hipGetLastError();  // clear the sticky allocation error
       b.p = nullptr;
-      b.bytes = 0;
-      return nullptr;
+      throw DeviceOom{slot, bytes};
     }
-    b.bytes = nb;
+    b.bytes = b.p ? nb : 0;
   }
   return (T*)b.p;
+}
+
+static int oom_error(hipStream_t stream, const DeviceOom& o, std::string* err) {
+  if (stream) (void)hipStreamSynchronize(stream);  // nothing of this call still running
+  (void)hipGetLastError();
+  size_t fr = 0, tot = 0;
+  (void)hipMemGetInfo(&fr, &tot);
+  if (err)
+    *err = "out of device memory: buffer " + std::to_string(o.slot) + " needs " + std::to_string(o.bytes >> 20) +
+           " MiB (" + std::to_string(fr >> 20) + " of " + std::to_string(tot >> 20) +
+           " MiB free): split the batch";
+  return OTR_DEVICE_ERROR;
 }
 
 Matcher::~Matcher() {
@@ -526,6 +548,14 @@ static std::vector<int> route_tiers() {
 }
 
 int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err) {
+  try {
+    return run_impl(in, mp, out, err);
+  } catch (const DeviceOom& o) {
+    return oom_error(stream, o, err);
+  }
+}
+
+int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err) {
   GraphState& gs = graph_state();
   std::shared_lock<std::shared_mutex> graph_lock(gs.mu);  // a reconfigure waits for this batch
   if (!gs.ready) {
@@ -1406,6 +1436,15 @@ int report_lists_device(const ReportLists& h, std::string* err) {
 // (K10).  Result rows are copied to host (matcher-owned).
 int Matcher::tiles_cull(const otr_tile_row* rows, int64_t n, int memory, int privacy, int rules,
                         const otr_tile_row** out, int64_t* n_out, std::string* err) {
+  try {
+    return tiles_cull_impl(rows, n, memory, privacy, rules, out, n_out, err);
+  } catch (const DeviceOom& o) {
+    return oom_error(stream, o, err);
+  }
+}
+
+int Matcher::tiles_cull_impl(const otr_tile_row* rows, int64_t n, int memory, int privacy, int rules,
+                        const otr_tile_row** out, int64_t* n_out, std::string* err) {
   GraphState& gs = graph_state();
   HIPCHK(hipSetDevice(gs.device));
   if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -1625,6 +1664,15 @@ int Matcher::copy_out(void* dst, const void* src, size_t bytes, int dst_memory, 
 
 int Matcher::hist_reduce(const void* in, int64_t n, int memory, int rows_in, int privacy, const otr_hist_entry** out,
                          int64_t* n_out, std::string* err) {
+  try {
+    return hist_reduce_impl(in, n, memory, rows_in, privacy, out, n_out, err);
+  } catch (const DeviceOom& o) {
+    return oom_error(stream, o, err);
+  }
+}
+
+int Matcher::hist_reduce_impl(const void* in, int64_t n, int memory, int rows_in, int privacy, const otr_hist_entry** out,
+                         int64_t* n_out, std::string* err) {
   GraphState& gs = graph_state();
   HIPCHK(hipSetDevice(gs.device));
   if (!stream) HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -1740,6 +1788,15 @@ int Matcher::hist_reduce(const void* in, int64_t n, int memory, int rows_in, int
 
 // ---- K11 ingest (include/otr.h otr_ingest) ----------------------------------------------
 int Matcher::ingest(const char* text, int64_t len, int memory, const otr_ingest_format* fmt, otr_ingest_result* out,
+                    std::string* err) {
+  try {
+    return ingest_impl(text, len, memory, fmt, out, err);
+  } catch (const DeviceOom& o) {
+    return oom_error(stream, o, err);
+  }
+}
+
+int Matcher::ingest_impl(const char* text, int64_t len, int memory, const otr_ingest_format* fmt, otr_ingest_result* out,
                     std::string* err) {
   GraphState& gs = graph_state();
   HIPCHK(hipSetDevice(gs.device));
