@@ -698,7 +698,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   te(OTR_STAGE_LINK);
   if (S > 0)
     k_tasks<<<grid_for(S, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, nullptr,
-                                                nullptr, nullptr, state_trace, b.mode, turn_modes);
+                                                nullptr, nullptr);
   if ((rc = scan(sb.ntask, task_off, S))) return rc;
   if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
   int64_t NT = 0, NTR = 0;
@@ -709,14 +709,14 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   unsigned long long* task_mask = need<unsigned long long>(S_TASK_MASK, NT);
   int32_t* task_ovf = need<int32_t>(S_TASK_OVF, NT);
   uint32_t* trans = need<uint32_t>(S_TRANS, NTR);
-  uint32_t* trans_tc = need<uint32_t>(S_TRANS_TC, NTR);
+  uint32_t* trans_tc = need<uint32_t>(S_TRANS_TC, turn_modes ? NTR : 1);  // read for turn modes only
   if (!task_state || !task_mask || !task_ovf || !trans || !trans_tc) {
     if (err) *err = "device allocation failed (transitions)";
     return OTR_DEVICE_ERROR;
   }
   if (S > 0)
     k_tasks<<<grid_for(S, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, task_off,
-                                                task_state, task_mask, state_trace, b.mode, turn_modes);
+                                                task_state, task_mask);
   if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
   // turn cost tables of this batch's parameters (oracle orc_turn_table)
   int32_t* d_turn = need<int32_t>(S_TURN, 181 * OTR_MODES);
@@ -777,6 +777,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
                                                       cb.edge, g.edge_dst, state_trace, b.mode, pr.cprep, sb.bt,
                                                       turn_modes, pr.heur, g.node_ll, trans_off, task_rec);
   ra.heur = pr.heur;
+  ra.turn = d_turn;
+  ra.trans_tc = trans_tc;
   ra.cprep = pr.cprep;
   ra.cprep_t = pr.cprep_t;
   ra.rec = task_rec;
@@ -848,12 +850,18 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // the LDS tiers count their work only when asked (OTR_BATCH_ROUTE_WORK): the end-of-
     // wave counter atomics cost ~7% of the first tier (tools/ab_libs.sh)
     unsigned long long* rwork = (in->flags & OTR_BATCH_ROUTE_WORK) ? d_counters : nullptr;
+    // batches with turn-cost modes take the kernels compiled with the turn walk
+    const bool turns = turn_modes != 0u;
     if (route_g == 2) {
       const int64_t units = (NT + 1) / 2;
-      k_route<160, 2, false><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, ra, rwork);
+      const unsigned grid = (unsigned)(8 * ((units + 7) / 8));
+      if (turns) k_route<160, 2, false, true><<<grid, 64, 0, stream>>>(g, ra, rwork);
+      else k_route<160, 2, false><<<grid, 64, 0, stream>>>(g, ra, rwork);
       out->route_tier_code[0] = 1602;
     } else {
-      k_route<256, 1, false><<<(unsigned)(8 * ((NT + 7) / 8)), 64, 0, stream>>>(g, ra, rwork);
+      const unsigned grid = (unsigned)(8 * ((NT + 7) / 8));
+      if (turns) k_route<256, 1, false, true><<<grid, 64, 0, stream>>>(g, ra, rwork);
+      else k_route<256, 1, false><<<grid, 64, 0, stream>>>(g, ra, rwork);
       out->route_tier_code[0] = 2561;
     }
     te(OTR_STAGE_ROUTE);
@@ -876,16 +884,20 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       unsigned long long* rcn = rwork ? d_counters + (2 + tier) * bank : nullptr;
       out->route_tier_code[1 + tier] = tiers[tier];
       if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier)], stream);
+#define OTR_TIER(C, G_)                                                     \
+  (turns ? k_route<C, G_, true, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn) \
+         : k_route<C, G_, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn))
       switch (tiers[tier]) {
-        case 2561: k_route<256, 1, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 5121: k_route<512, 1, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 10241: k_route<1024, 1, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 20481: k_route<2048, 1, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 3842: k_route<384, 2, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 4482: k_route<448, 2, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        case 5122: k_route<512, 2, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
-        default: k_route<4096, 1, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn); break;
+        case 2561: OTR_TIER(256, 1); break;
+        case 5121: OTR_TIER(512, 1); break;
+        case 10241: OTR_TIER(1024, 1); break;
+        case 20481: OTR_TIER(2048, 1); break;
+        case 3842: OTR_TIER(384, 2); break;
+        case 4482: OTR_TIER(448, 2); break;
+        case 5122: OTR_TIER(512, 2); break;
+        default: OTR_TIER(4096, 1); break;
       }
+#undef OTR_TIER
       if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier) + 1], stream);
     }
     // everything left — turn-cost (edge-based) tasks, tasks whose labels need 64 bits,

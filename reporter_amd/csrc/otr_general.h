@@ -322,18 +322,28 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
   for (int64_t k = blockIdx.x; k < count; k += gridDim.x) {
     const int64_t item = a.list[k];
     if (a.mode == 0) {
-      // ---- route task: transitions of every source sharing the root
+      // ---- route task: transitions of every source sharing the root node; with turn
+      // costs (edge mode) every source edge is its own root: one search each
       const int64_t s = a.task_state[item];
       const unsigned long long mask = a.task_mask[item];
       const int64_t sp = a.prev[s];
-      const int i0 = __ffsll((long long)mask) - 1;
-      const GTask T = g_task(G, a, s, sp, a.cand_edge[sp * OTR_KMAX + i0]);
-      const bool ok = g_search(G, T, key, lab, qmark, fr, touched, cap, s_n, &s_touched, &s_ovf, a.counters);
-      if (ok) {
+      GTask T = g_task(G, a, s, sp, a.cand_edge[sp * OTR_KMAX + (__ffsll((long long)mask) - 1)]);
+      bool ok = true;
+      for (unsigned long long todo = mask; todo && ok;) {
+        const int ia = __ffsll((long long)todo) - 1;
+        const unsigned long long grp = T.edge_mode ? (1ull << ia) : todo;
+        todo &= ~grp;
+        if (T.edge_mode) T.root = a.cand_edge[sp * OTR_KMAX + ia];
+        if (grp != mask) {  // a later source: a fresh slab
+          __syncthreads();
+          g_reset(key, lab, qmark, touched, s_touched, cap);
+        }
+        ok = g_search(G, T, key, lab, qmark, fr, touched, cap, s_n, &s_touched, &s_ovf, a.counters);
+        if (!ok) break;
         const int Kb = a.cand_count[s];
         if (a.counters && tid == 0) {  // kinds 5 transition entries, 6 searches
           const int sh = cshard();
-          atomicAdd(&a.counters[5 * kCShards + sh], (unsigned long long)Kb * (unsigned long long)__popcll(mask));
+          atomicAdd(&a.counters[5 * kCShards + sh], (unsigned long long)Kb * (unsigned long long)__popcll(grp));
           atomicAdd(&a.counters[6 * kCShards + sh], 1ull);
         }
         uint32_t* trow = a.trans + a.trans_off[s];
@@ -346,7 +356,7 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
           unsigned long long L;
           uint32_t via;
           const bool reached = g_node_key(G, T, key, lab, cap, ej, &L, &via);
-          for (unsigned long long m = mask; m; m &= m - 1) {
+          for (unsigned long long m = grp; m; m &= m - 1) {
             const int i = __ffsll((long long)m) - 1;
             const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
             const double pi = a.cand_p[sp * OTR_KMAX + i];
@@ -364,9 +374,11 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
             }
             const bool valid = rd >= 0 && rd <= (int64_t)T.bmm && (!T.time_on || rt <= (int64_t)T.bt);
             trow[(int64_t)i * Kb + j] = valid ? (uint32_t)rd : kNoRoute;
-            crow[(int64_t)i * Kb + j] = rc;
+            if (T.edge_mode) crow[(int64_t)i * Kb + j] = rc;  // allocated for turn modes only
           }
         }
+      }
+      if (ok) {
         if (tid == 0) a.flag[item] = 0;
       } else if (tid == 0) {
         a.flag[item] = 1;

@@ -380,8 +380,7 @@ __global__ __launch_bounds__(256) void k_link(BatchDev b, ModeParams mp, const i
 __global__ __launch_bounds__(256) void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* cand_count,
                                                const uint32_t* cand_edge, const uint32_t* edge_dst, int64_t* ntask,
                                                const int64_t* task_off, int64_t* task_state,
-                                               unsigned long long* task_mask, const int32_t* state_trace,
-                                               const uint8_t* mode, uint32_t turn_modes) {
+                                               unsigned long long* task_mask) {
   // one wave per state, lane i = source candidate i of the previous state
   const int64_t s = (int64_t)blockIdx.x * (blockDim.x / OTR_WAVE) + threadIdx.x / OTR_WAVE;
   const int lane = threadIdx.x % OTR_WAVE;
@@ -392,11 +391,11 @@ __global__ __launch_bounds__(256) void k_tasks(int64_t n_states, const int64_t* 
     return;
   }
   const int Ka = cand_count[sp];
-  // with turn costs the search is edge-based: sources share it only on the same edge
-  const int md = mode[state_trace[s]] < OTR_MODES ? mode[state_trace[s]] : 0;
-  const bool by_edge = (turn_modes >> md) & 1u;
+  // sources share a task when their edges end at the same node: the node-based search
+  // serves them all (with turn costs too: only the first turn differs, k_route adds it;
+  // the edge-based fallback in k_general searches each source edge on its own)
   const uint32_t ce = lane < Ka ? cand_edge[sp * OTR_KMAX + lane] : 0xFFFFFFFFu;
-  const uint32_t root = lane < Ka ? (by_edge ? ce : edge_dst[ce]) : 0xFFFFFFFFu;
+  const uint32_t root = lane < Ka ? edge_dst[ce] : 0xFFFFFFFFu;
   // sources sharing my root, then: am I the lowest of them (the task's representative)?
   unsigned long long same = 0;
   for (int k = 0; k < Ka; ++k)
@@ -510,6 +509,10 @@ struct SearchLds {
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
   uint2 work[WCAP];                   // this round's settled nodes: {node, label}
   int n_pend, n_keys, overflow;
+  // PRED: 1 when a second in-edge reached the node with its label (a tie the turn costs
+  // of an edge-based route would decide; never cleared, so it may also flag a label
+  // that later improved — only ever sending a path to the edge-based search)
+  uint8_t tie[PRED ? CAP : 1];
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
@@ -626,6 +629,7 @@ __device__ inline void search_init(SearchLds<CAP, PRED>* Ls) {
     for (int k = threadIdx.x; k < CAP; k += OTR_WAVE) {
       L.key[k] = kEmpty;
       L.lab[k] = LabelT<PRED>::kInf;
+      if (PRED) L.tie[k] = 0;
     }
     if (threadIdx.x == 0) {
       L.n_pend = 0;
@@ -705,6 +709,8 @@ __device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, const Pa
     fnext = f < fnext ? f : fnext;
     const uint32_t ok = atomicOr(&L.key[sl], kInq);
     if (!(ok & kInq)) return sl;  // newly pending: the caller appends it
+  } else if (PRED && LabelT<PRED>::label(nb) == LabelT<PRED>::label(old) && nb != old) {
+    L.tie[sl] = 1;
   }
   return -1;
 }
@@ -971,6 +977,8 @@ struct RouteArgs {
   const int32_t* bt;          // per state: the step's time bound (0.1 s), -1 none
   const uint4* rec;           // per task, 2 x uint4 (k_task_rec)
   const unsigned long long* list_count;  // retry tiers: length of task_list, on the device
+  const int32_t* turn;        // [OTR_MODES][181] turn cost tables (mm), turn modes only
+  uint32_t* trans_tc;         // turn cost (mm) per transition, turn modes only
   double delta;
   double inv_beta[OTR_MODES];
   int32_t* overflow_flag;     // per task: 1/2 retry in a larger LDS table, 3 the global-memory search
@@ -982,12 +990,14 @@ struct RouteArgs {
 // first source edge → root node; mode through the trace): the search kernels read two
 // 16-B words instead of walking that chain twice (before and after the search).
 //   rec[3t]   = {s, sp, root, bound_mm}
-//   rec[3t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16, mask lo, mask hi}
+//   rec[3t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16 | turn << 17, mask lo, mask hi}
 //   rec[3t+2] = {h(root), time bound bt, trans_off[s] lo, hi}
 // (h(root) here takes the root's coordinates, the search's first dependent global load,
 // off the search kernels' critical path)
-// general: the task runs in the global-memory search (turn costs: edge-based labels; or
-// a bound whose packed labels would not fit 32 bits).
+// general: the task runs in the global-memory search (a bound whose packed labels would
+// not fit 32 bits).  turn: the mode has turn costs (edge-based semantics): the LDS search
+// runs node-based and the transition rows walk the unique tight in-edges back to the
+// root to add the turns; a tie on the way sends the task to the global-memory search.
 __global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const unsigned long long* task_mask,
                            const int64_t* prev, const double* bound, const uint8_t* forced, const int32_t* cand_count,
                            const uint32_t* cand_edge, const uint32_t* edge_dst, const int32_t* state_trace,
@@ -1010,10 +1020,11 @@ __global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const uns
 #ifdef OTR_FORCE_GENERAL
   const bool general = true;  // test build: every search in k_general (tests/test_gpu_tiers.py)
 #else
-  const bool general = ((turn_modes >> md) & 1u) || !pack_fits(bmm, sh);
+  const bool general = !pack_fits(bmm, sh);
 #endif
+  const uint32_t turn = (turn_modes >> md) & 1u;
   const uint32_t meta = (uint32_t)cand_count[s] | ((uint32_t)md << 8) | ((forced[s] ? 1u : 0u) << 10) | (sh << 11) |
-                        ((general ? 1u : 0u) << 16);
+                        ((general ? 1u : 0u) << 16) | (turn << 17);
   const int2 rll = node_ll[root];
   const uint32_t hroot = heur[s](rll.x, rll.y);
   const int64_t to = trans_off[s];
@@ -1028,16 +1039,52 @@ __global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const uns
 // LIST = false: the first tier, one unit per block over all tasks (XCD-mapped); LIST =
 // true: a retry tier, a fixed grid striding over the device-side task list (its length
 // never crosses to the host)
+// Turn costs of a node-based route: the edge-based search's label at a
+// target edge ej = the node label of v = src(ej) plus the turn costs along the route,
+// whose choice among equal (length, time) routes is decided by those turn costs.  The
+// TURN kernels search with predecessor labels (label << 32 | smallest in-edge) and tie
+// bits: when no node from v back to the root saw two in-edges reach its label, the route
+// is unique and its turn costs are summed on the walk back along the predecessor edges;
+// a tie anywhere -> false (the task goes to the edge-based global-memory search).
+// *first: the route's first edge out of the root (ej itself when v is the root); *c: the
+// turns after it, saturating.
+template <int CAP>
+__device__ bool turn_walk(const DevGraph& g, const SearchLds<CAP, true>& L, uint32_t v, uint32_t root, uint32_t ej,
+                          const int32_t* turn, uint32_t* first, uint32_t* c) {
+  uint32_t next = ej, acc = 0;
+  int hb_next = g.edge_head[ej].x;
+  for (int hop = 0; hop < CAP && v != root; ++hop) {
+    const int sv = lds_find(L, v);
+    if (sv < 0 || L.tie[sv]) return false;
+    const uint32_t a = (uint32_t)(L.lab[sv] & 0xFFFFFFFFull);
+    if (a == kEmpty) return false;
+    const short2 ha = g.edge_head[a];
+    const uint32_t u = g.edge_src[a];
+    acc += (uint32_t)turn[turn_degree(ha.y, hb_next)];
+    acc = acc < kTcCap ? acc : kTcCap;
+    next = a;
+    hb_next = ha.x;
+    v = u;
+  }
+  if (v != root) return false;
+  *first = next;
+  *c = acc;
+  return true;
+}
+
 // index of the q-th set bit of m (q < popcount(m))
 __device__ inline int nth_set_bit(unsigned long long m, int q) {
   for (int j = 0; j < q; ++j) m &= m - 1;
   return __ffsll((long long)m) - 1;
 }
 
-// one unit = G search tasks of the wave (ordinal w of the task range or list)
-template <int CAP, int G, bool LIST>
+// one unit = G search tasks of the wave (ordinal w of the task range or list).  TURN:
+// the batch has turn-cost modes, whose transition rows walk the routes (turn_walk); a
+// batch without them runs the kernel compiled without that code (its register budget
+// belongs to the search)
+template <int CAP, int G, bool LIST, bool TURN>
 __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& a, unsigned long long* counters,
-                                           SearchLds<CAP, false>* Ls, int64_t w, int64_t n_tasks) {
+                                           SearchLds<CAP, TURN>* Ls, int64_t w, int64_t n_tasks) {
   using Gr = Grp<G>;
   const int lane = Gr::gl();
   const int64_t tw = w * G + Gr::g();
@@ -1110,8 +1157,8 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   }
   unsigned long long settled = 0, relaxed = 0, rounds = 0;
   OTR_STAMP(ts_set);
-  search_init<CAP, false, G>(Ls);
-  bool ok = search_run<CAP, false, G>(Ls, gr, H, K, mode_bit, search, root, bmm,
+  search_init<CAP, TURN, G>(Ls);
+  bool ok = search_run<CAP, TURN, G>(Ls, gr, H, K, mode_bit, search, root, bmm,
                                       (uint32_t)(a.delta * 1000.0), tnode, tpart, hT, d0min, Kb, &settled, &relaxed,
                                       &rounds, counters ? counters + 16 * kCShards : nullptr, hroot) &&
             fits;
@@ -1119,15 +1166,20 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   if (G == 2 && !LIST) ok = false;  // test build: every first-tier task takes the retry tiers
 #endif
   OTR_STAMP(ts_srch);
-  SearchLds<CAP, false>& L = Ls[Gr::g()];
+  SearchLds<CAP, TURN>& L = Ls[Gr::g()];
   int64_t lab = -1;
   if (ok && tnode != kEmpty && !forced) {
     const int sl = lds_find(L, tnode);
-    if (sl >= 0 && L.lab[sl] != kNoLabel) lab = (int64_t)L.lab[sl];
+    if (sl >= 0 && LabelT<TURN>::label(L.lab[sl]) != kNoLabel) lab = (int64_t)LabelT<TURN>::label(L.lab[sl]);
   }
   // ---- transition rows: re-read the step (cached) rather than hold it live through the search
   asm volatile("" ::: "memory");
   uint32_t ntr = 0;  // transition entries this search wrote (K4), for the work counters
+  // turn modes: each target's turn costs come from a walk back along its route
+  // (turn_walk), run once per target with a valid route; a tie anywhere sends the task to
+  // the edge-based global-memory search (flag 3)
+  uint32_t t_first = kEmpty, t_c = 0;
+  bool turn_task = false, tie = false, walked = false;
   if (have && (ok || forced)) {
     const uint4 r0 = a.rec[3 * task], r1 = a.rec[3 * task + 1], r2 = a.rec[3 * task + 2];
     const int64_t s = r0.x;
@@ -1136,6 +1188,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     const int64_t sp = r0.y;
     const int32_t bt = (int32_t)r2.y;
     const int md = (int)((r1.y >> 8) & 3u);
+    turn_task = TURN && !forced && ((r1.y >> 17) & 1u);
     uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
     // sources staged one per lane as in the setup: {index, edge, fraction, exit part mm,
     // exit part time}, read by group shuffles in the row loop
@@ -1186,14 +1239,36 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
         }
         const bool valid = r >= 0 && r <= (int64_t)bmm && (bt < 0 || rt <= (int64_t)bt);
         trow[(int64_t)i * Kb + lane] = valid ? (uint32_t)r : kNoRoute;
+        if constexpr (TURN) {
+          if (turn_task) {
+            // turn cost of the edge-based route: the source edge into the route's first edge,
+            // then the walk's turns (same edge forward: none)
+            uint32_t tc = 0;
+            if (valid && !(ej == ei && pj >= pi)) {
+              if (!walked) {
+                walked = true;
+                tie = !turn_walk<CAP>(gr, L, tnode, root, ej, a.turn + 181 * md, &t_first, &t_c);
+              }
+              const uint32_t fe = t_first == kEmpty ? ej : t_first;
+              const short2 hs = gr.edge_head[ei], hf = gr.edge_head[fe];
+              tc = (uint32_t)a.turn[181 * md + turn_degree(hs.y, hf.x)] + t_c;
+              tc = tc < kTcCap ? tc : kTcCap;
+            }
+            a.trans_tc[trow - a.trans + (int64_t)i * Kb + lane] = tc;
+          }
+        }
       }
     }
+  }
+  if (TURN && turn_task && Gr::mine(__ballot(tie)) != 0ull) {  // the whole task, edge-based
+    tie = true;
+    ok = false;
   }
   // general: the global-memory search (flag 3); overflow: retry with a bigger table; a
   // first-tier search with a long bound (> 1.9 km) that outgrew 160 slots goes straight
   // to the 1024-slot tier (flag 2)
   if (have && !ok && !forced && lane == 0) {
-    const bool general = (a.rec[3 * task + 1].y >> 16) & 1u;
+    const bool general = ((a.rec[3 * task + 1].y >> 16) & 1u) || tie;
     a.overflow_flag[task] = general ? 3 : ((G == 2 && !LIST && bmm > 1900000u) ? 2 : 1);
   }
 #ifdef OTR_STAMPS
@@ -1228,19 +1303,19 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   }
 }
 
-template <int CAP, int G, bool LIST>
+template <int CAP, int G, bool LIST, bool TURN = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR_ROUTE2_WAVES : 8, G == 2 ? OTR_ROUTE2_WAVES : 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
-  __shared__ SearchLds<CAP, false> Ls[G];
+  __shared__ SearchLds<CAP, TURN> Ls[G];
   if (!LIST) {  // the first tier: one unit per block, XCD-mapped (no loop: fewer live registers)
     const int64_t n_units = (a.n_tasks + G - 1) / G;
     const int64_t w = xcd_remap(blockIdx.x, (n_units + 7) / 8);
-    if (w < n_units) route_unit<CAP, G, LIST>(gr, a, counters, Ls, w, a.n_tasks);
+    if (w < n_units) route_unit<CAP, G, LIST, TURN>(gr, a, counters, Ls, w, a.n_tasks);
     return;
   }
   const int64_t n_tasks = (int64_t)*a.list_count;
   const int64_t n_units = (n_tasks + G - 1) / G;
   for (int64_t w = blockIdx.x; w < n_units; w += gridDim.x) {
-    route_unit<CAP, G, LIST>(gr, a, counters, Ls, w, n_tasks);
+    route_unit<CAP, G, LIST, TURN>(gr, a, counters, Ls, w, n_tasks);
     __syncthreads();  // the next unit re-initialises the tables
   }
 }
@@ -1497,7 +1572,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
   const int64_t k = have ? (step_list ? step_list[iw] : iw) : 0;
   const int64_t s = have ? a.steps[k] : 0;
   const int64_t sp = have ? a.prev[s] : 0;
-  bool active = false;
+  bool active = false, turn = false;
   uint32_t S = 0, T = kEmpty, bmm = 0, tpart = 0, hT = 0, d0 = 0, mode_bit = 1;
   int mode = 0;
   Pack K;
@@ -1512,13 +1587,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
     K.sh = pack_shift(a.bt[s]);
     if (ej == ei && pj >= pi) {
       if (gl == 0) a.path_len[s] = -1;
-    } else if (((a.turn_modes >> mode) & 1u) || !pack_fits(bmm, K.sh)
+    } else if (!pack_fits(bmm, K.sh)
 #ifdef OTR_FORCE_GENERAL
                || true
 #endif
     ) {
-      if (gl == 0) a.overflow_flag[k] = 3;  // edge-based / 64-bit labels: k_general
+      if (gl == 0) a.overflow_flag[k] = 3;  // 64-bit labels: k_general
     } else {
+      // turn modes: the node-based path is the edge-based one when no node on it has a
+      // tie (checked on the walk); otherwise k_general
+      turn = (a.turn_modes >> mode) & 1u;
       active = true;
       mode_bit = 1u << mode;
       const uint4 cs = a.cprep[sp * OTR_KMAX + wi], ct = a.cprep[s * OTR_KMAX + wj];
@@ -1551,6 +1629,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
         n = -1;
         break;
       }
+      if (turn && L.tie[sv]) {
+        n = -2;  // a tie the turn costs decide: the edge-based search
+        break;
+      }
       lp[n++] = e;
       v = gr.edge_src[e];
     }
@@ -1558,7 +1640,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
   n = __shfl(n, Gr::g() * Gr::GL);
   __syncthreads();
   if (active && n < 0) {
-    if (gl == 0) a.overflow_flag[k] = 1;
+    if (gl == 0) a.overflow_flag[k] = n == -2 ? 3 : 1;
     active = false;
   }
   // bump allocation in one of 64 regions (a single cursor serialises ~1M returning
