@@ -172,6 +172,33 @@ def build_slow(path):
     return {k: int(new[v]) for k, v in ids.items()}
 
 
+def build_square(path):
+    """Equal-length alternatives (DESIGN.md §3.5 ties): W (0, -100) -> S (0, 0), then a
+    diamond S-P-T / S-Q-T with P = (100, 100), Q = (-100, 100), T = (0, 200), mirror images
+    in whole micro-degrees (equal lengths and times to the millimetre), then T -> N
+    (100, 200) east; all two-way, 50 km/h, level 1.  The turns at S and at P / Q mirror
+    each other; at T the route from Q bends 45 degrees into T-N and the one from P 135."""
+    lat0, lon0 = int(round(LAT0 * 1e6)), int(round(LON0 * 1e6))
+    dx, dy = int(round(100 / MLON * 1e6)), int(round(100 / M * 1e6))
+
+    def e6(i, j):  # i, j: multiples of 100 m east / north, exact micro-degrees
+        return ((lat0 + j * dy) * 1e-6, (lon0 + i * dx) * 1e-6)
+    nodes = [e6(0, -1), e6(0, 0), e6(1, 1), e6(-1, 1), e6(0, 2), e6(1, 2)]
+    W, S, P, Q, T, N = range(6)
+    edges, ids = [], {}
+    for name, a, b, way in (('WS', W, S, 71), ('SP', S, P, 72), ('PT', P, T, 73), ('SQ', S, Q, 74),
+                            ('QT', Q, T, 75), ('TN', T, N, 76)):
+        ids[name + '>'], ids[name + '<'] = two_way(edges, a, b, way, level=1, speed=50)
+    segs = [dict(id=osmlr(1, 401, 1), edges=[ids['WS>']]), dict(id=osmlr(1, 401, 2), edges=[ids['TN>']])]
+    new = write_graph(path, nodes, edges, segs)
+    return {k: int(new[v]) for k, v in ids.items()}
+
+
+def square_trace():
+    """North on W-S, then east on T-N: two probes each (20 s apart)."""
+    return [(2, -60), (2, -20), (40, 202), (80, 202)]
+
+
 def slow_scenarios():
     """Eastbound at 12.5 m/s, a probe every 4 s (50 m), 3 m north of the centreline."""
     return {'through_slow_block': [(20 + 50 * k, 3) for k in range(10)]}

@@ -158,10 +158,35 @@ def test_queue_length_on_deceleration(kat):
     assert r2['seg_queue'][k] == 110
 
 
+@pytest.fixture(scope='module')
+def square(graph_dir):
+    path = os.path.join(graph_dir, 'kat_square.otrg')
+    return path, K.build_square(path)
+
+
+def test_equal_length_routes_decided_by_turns(square):
+    """Both ways around the diamond have the same length and time to the millimetre: without
+    turn costs the route takes T's smaller-id in-edge; with them it comes via Q, whose
+    turn into T-N (45 degrees off straight: turn degree 135) costs less than P's (135 off:
+    degree 45); the turns at S and at P / Q mirror each other."""
+    path, ids = square
+    g = po.Graph(path)
+    tab = po.turn_table(po.params())
+    d, t, c = g.route(ids['WS>'], 0.5, ids['TN>'], 0.5, 2000.0, dt_sec=40, prm=po.params())
+    assert c == tab[135] + tab[90] + tab[135]  # S: 45 off, Q: 90, T: 45 off
+    d_p = g.route(ids['WS>'], 0.5, ids['PT>'], 0.999, 2000.0, dt_sec=40, prm=po.params())[0]
+    d_q = g.route(ids['WS>'], 0.5, ids['QT>'], 0.999, 2000.0, dt_sec=40, prm=po.params())[0]
+    assert d_p == d_q  # the tie
+    b, r = _match(path, K.square_trace(), 20)
+    route = [int(e) for e in r['route_edge'] if e != 0xFFFFFFFF]
+    assert ids['QT>'] in route and ids['PT>'] not in route
+
+
 # ---- GPU parity on the same inputs -----------------------------------------------------
 @pytest.mark.gpu
 @pytest.mark.parametrize('opts', [{}, {'turn_penalty_factor': 0}, {'max_route_time_factor': 0}])
-def test_semantics_gpu_parity(kat, slow, opts):
+def test_semantics_gpu_parity(kat, slow, square, opts):
+    from reporter_amd import _lib
     from reporter_amd import matcher as M
     path, ids, segs = kat
     M.configure(M.default_config(path, **opts))
@@ -175,6 +200,16 @@ def test_semantics_gpu_parity(kat, slow, opts):
     want = po.match_batch(po.Graph(path), b, po.params(**opts))
     errors, stats = compare(got, want)
     assert not errors, errors
+    # a (length, time) tie the turn costs decide: the LDS tiers hand it to the edge-based
+    # global-memory search (with turn costs), the result equals the oracle either way
+    qpath, qids = square
+    M.configure(M.default_config(qpath, **opts))
+    b = K.batch([K.trace(K.square_trace(), dt=20)])
+    r = M.Matcher().match_batch(b, copy_out=True, route_work=True)
+    errors, _ = compare(_lib.result_to_numpy(r), po.match_batch(po.Graph(qpath), b, po.params(**opts)))
+    assert not errors, errors
+    if opts.get('turn_penalty_factor', 1) != 0:
+        assert int(r.route_tier_work[6][0]) > 0  # the tie went to k_general
     spath, sid = slow
     M.configure(M.default_config(spath, **opts))
     b = K.batch([K.trace(p, dt=4) for p in K.slow_scenarios().values()])
