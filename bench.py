@@ -51,12 +51,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def kernel_name(code):
-    """rocprofv3 name of a route kernel (otr_batch_result.route_tier_code)."""
+def kernel_name(code, turns=False):
+    """rocprofv3 name of a route kernel (otr_batch_result.route_tier_code); turns: the
+    batch had turn-cost modes (the kernels compiled with the turn walk)."""
     if code < 0:
         return 'k_general'
     cap, g = code // 10, code % 10
-    return 'k_route<%d, %d, %s>' % (cap, g, 'false' if code == 1602 or code == 2561 else 'true')
+    return 'k_route<%d, %d, %s, %s>' % (cap, g, 'false' if code == 1602 or code == 2561 else 'true',
+                                        'true' if turns else 'false')
 
 
 def route_bytes(work):
@@ -109,8 +111,10 @@ def main():
     ap.add_argument('--cpu-traces', type=int, default=None,
                     help='bounded oracle sample for the CPU baseline and the parity check (0 = skip)')
     ap.add_argument('--delta', type=float, default=None, help='routing round width (perf knob, metres)')
-    ap.add_argument('--streams', type=int, default=2,
-                    help='matchers (one HIP stream + host thread each) sharing the batch')
+    ap.add_argument('--streams', type=int, default=1,
+                    help='matchers (one HIP stream + host thread each) sharing the batch; 2 overlaps one '
+                         "stream's host syncs and kernel tails with the other's kernels (+1.6%% at C2) but "
+                         'the two route launches then share the GPU, halving the per-launch roofline figure')
     ap.add_argument('--workload', choices=['c2', 'c3', 'c4', 'c5mix', 'c5'], default='c2',
                     help='c2 (default, the headline): 100 probes @15 s, sigma 10 m; c3: the C3 shard of '
                          '1M veh%%07d uuids x 100 probes this GPU owns; c4: 60 probes @60 s, sigma 50 m, '
@@ -394,7 +398,9 @@ def main():
     launch_ms = dom['ms'] / dom['launches']
     dom_bytes = route_bytes(dom['work'] / dom['launches'])
     achieved = dom_bytes / (launch_ms * 1e-3) / 1e9
-    tier_table = {kernel_name(d['code']): {'ms_per_launch': round(d['ms'] / d['launches'], 3),
+    # turn-cost modes run the route kernels compiled with the turn walk
+    turns = float(W['meili'].get('turn_penalty_factor', 1.0)) > 0.0
+    tier_table = {kernel_name(d['code'], turns): {'ms_per_launch': round(d['ms'] / d['launches'], 3),
                                           'searches_per_launch': int(d['work'][0] // d['launches']),
                                           'settled_per_launch': int(d['work'][1] // d['launches']),
                                           'relaxed_per_launch': int(d['work'][2] // d['launches']),
@@ -404,7 +410,7 @@ def main():
                   for t, d in sorted(tiers.items())}
     traffic, traffic_src = None, None
     if os.path.exists(PMC_SUMMARY):
-        k = json.load(open(PMC_SUMMARY)).get('kernels', {}).get(kernel_name(dom['code']), {})
+        k = json.load(open(PMC_SUMMARY)).get('kernels', {}).get(kernel_name(dom['code'], turns), {})
         if 'fetch_bytes_per_launch' in k and 'write_bytes_per_launch' in k:
             traffic = int(k['fetch_bytes_per_launch'] + k['write_bytes_per_launch'])
             traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
@@ -517,7 +523,7 @@ def main():
                        'work': {'states': int(sum(r.n_states for r in rs)), 'grid_cells': int(counters[0]),
                                 'shape_segments_tested': int(counters[1]), 'candidates': int(counters[2]),
                                 'output_segments': int(counters[7])}},
-            'roofline': {'kernel': kernel_name(dom['code']) + ' (dominant route-search kernel of this workload)',
+            'roofline': {'kernel': kernel_name(dom['code'], turns) + ' (dominant route-search kernel of this workload)',
                          'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': traffic,
                          'traffic_source': traffic_src, 'launch_ms': round(launch_ms, 3),
