@@ -56,6 +56,8 @@ def kernel_name(code, turns=False):
     batch had turn-cost modes (the kernels compiled with the turn walk)."""
     if code < 0:
         return 'k_general'
+    if code >= 1000000:  # the multi-root step kernel: 1,000,000 + CAP * 100 + RMAX
+        return 'k_route_step<%d, %d>' % ((code - 1000000) // 100, code % 100)
     cap, g = code // 10, code % 10
     return 'k_route<%d, %d, %s, %s>' % (cap, g, 'false' if code == 1602 or code == 2561 else 'true',
                                         'true' if turns else 'false')

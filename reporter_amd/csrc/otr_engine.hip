@@ -13,6 +13,7 @@
 #include "otr_engine.h"
 #include "otr_kernels.h"
 #include "otr_general.h"
+#include "otr_route_step.h"
 #include "otr_ingest.h"
 
 namespace otr {
@@ -366,7 +367,7 @@ enum Slot {
   S_TRACE_OFF, S_LAT, S_LON, S_TIME, S_ACC, S_MODE,
   S_STATE_CNT, S_TRACE_STATE_OFF, S_STATE_PROBE, S_STATE_TRACE,
   S_CAND_EDGE, S_CAND_P, S_CAND_SQD, S_CAND_COUNT, S_CAND_RADIUS,
-  S_PREV, S_G, S_BOUND, S_FORCED, S_NTASK, S_NTRANS, S_TASK_OFF, S_TRANS_OFF,
+  S_PREV, S_G, S_BOUND, S_FORCED, S_NTASK, S_NTRANS, S_TASK_OFF, S_TRANS_OFF, S_NUNIT, S_UNIT_OFF, S_UNIT,
   S_TASK_STATE, S_TASK_MASK, S_TASK_OVF, S_TRANS,
   S_BP, S_BRK, S_END_WIN, S_WINNER, S_SUBPATH,
   S_PATH_OFF, S_PATH_LEN, S_PATH, S_STEP_OVF,
@@ -701,9 +702,29 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
                                                 nullptr, nullptr);
   if ((rc = scan(sb.ntask, task_off, S))) return rc;
   if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
-  int64_t NT = 0, NTR = 0;
+  // OTR_ROUTE_STEP=1 (A/B knob, read per call): batches without turn-cost
+  // modes route in the multi-root step kernel (otr_route_step.h), one unit per (state,
+  // group of kStepRoots of its search tasks); measured slower than the per-root first
+  // tier at C2, so off by default
+  const char* step_env = getenv("OTR_ROUTE_STEP");
+  const bool step_on = step_env && atoi(step_env) != 0;
+  const bool use_step = step_on && turn_modes == 0u;
+  constexpr int kStepRoots = 8;
+  int64_t* unit_off = nullptr;
+  if (use_step) {
+    int64_t* nunit = need<int64_t>(S_NUNIT, S);
+    unit_off = need<int64_t>(S_UNIT_OFF, S + 1);
+    if (!nunit || !unit_off) {
+      if (err) *err = "device allocation failed (step units)";
+      return OTR_DEVICE_ERROR;
+    }
+    if (S > 0) k_step_nunit<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.ntask, kStepRoots, nunit);
+    if ((rc = scan(nunit, unit_off, S))) return rc;
+  }
+  int64_t NT = 0, NTR = 0, NU = 0;
   HIPCHK(hipMemcpyAsync(&NT, task_off + S, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipMemcpyAsync(&NTR, trans_off + S, 8, hipMemcpyDeviceToHost, stream));
+  if (use_step) HIPCHK(hipMemcpyAsync(&NU, unit_off + S, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
   int64_t* task_state = need<int64_t>(S_TASK_STATE, NT);
   unsigned long long* task_mask = need<unsigned long long>(S_TASK_MASK, NT);
@@ -844,7 +865,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ga.counters = d_counters;
   ga.n_overflow = cnt + 19;
   if (NT > 0) {
-    tb(OTR_STAGE_ROUTE);
     // two searches per wave (CAP 160 tables); wider steps and overflows retry below
     static const int route_g = getenv("OTR_ROUTE_G") ? atoi(getenv("OTR_ROUTE_G")) : 2;  // A/B knob
     // the LDS tiers count their work only when asked (OTR_BATCH_ROUTE_WORK): the end-of-
@@ -852,13 +872,31 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     unsigned long long* rwork = (in->flags & OTR_BATCH_ROUTE_WORK) ? d_counters : nullptr;
     // batches with turn-cost modes take the kernels compiled with the turn walk
     const bool turns = turn_modes != 0u;
-    if (route_g == 2) {
+    if (use_step) {
+      StepArgs st{};
+      int64_t* units = need<int64_t>(S_UNIT, std::max<int64_t>(NU, 1));
+      st.unit = units;
+      if (!units) {
+        if (err) *err = "device allocation failed (step units)";
+        return OTR_DEVICE_ERROR;
+      }
+      st.n_units = NU;
+      st.task_off = task_off;
+      st.ntask = sb.ntask;
+      k_step_units<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.ntask, unit_off, kStepRoots, units);
+      tb(OTR_STAGE_ROUTE);
+      const unsigned grid = (unsigned)(8 * ((NU + 7) / 8));
+      if (NU > 0) k_route_step<kStepCap, kStepRoots><<<grid, 64, 0, stream>>>(g, ra, st, rwork);
+      out->route_tier_code[0] = kStepCode;
+    } else if (route_g == 2) {
+      tb(OTR_STAGE_ROUTE);
       const int64_t units = (NT + 1) / 2;
       const unsigned grid = (unsigned)(8 * ((units + 7) / 8));
       if (turns) k_route<160, 2, false, true><<<grid, 64, 0, stream>>>(g, ra, rwork);
       else k_route<160, 2, false><<<grid, 64, 0, stream>>>(g, ra, rwork);
       out->route_tier_code[0] = 1602;
     } else {
+      tb(OTR_STAGE_ROUTE);
       const unsigned grid = (unsigned)(8 * ((NT + 7) / 8));
       if (turns) k_route<256, 1, false, true><<<grid, 64, 0, stream>>>(g, ra, rwork);
       else k_route<256, 1, false><<<grid, 64, 0, stream>>>(g, ra, rwork);

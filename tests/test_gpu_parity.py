@@ -6,6 +6,7 @@ import pytest
 
 from oracle import pyoracle as po
 from oracle.compare import compare
+from reporter_amd import _lib
 from reporter_amd import matcher as M
 from reporter_amd.tools import gen
 
@@ -53,4 +54,24 @@ def test_batch_parity(name, cfg, graph_dir, matcher):
     errors, stats = compare(got, want)
     assert not errors, errors
     assert stats['n_seg'] > 0
+    assert got['status'] == 0
+
+
+@pytest.mark.parametrize('name', ['tiny_mixed', 'city_15s', 'metro_15s', 'metro_sparse_60s', 'metro_mixed_modes'])
+def test_step_kernel_parity(name, graph_dir, matcher, monkeypatch):
+    """The multi-root step kernel (otr_route_step.h, OTR_ROUTE_STEP=1: one LDS table per
+    step, a label per root) gives the per-root kernels' transition rows: bit-exact oracle parity."""
+    g, nt, npnt, sr, sig, seed, fb, fp, acc, over = CASES[name]
+    over = dict(over, **CONFIGS['gtt'])
+    path = gen.graph_path(g, graph_dir)
+    M.configure(M.default_config(path, **over))
+    traces = gen.make_traces(path, nt, npnt, sr, sig, seed, fb, fp, acc)
+    monkeypatch.setenv('OTR_ROUTE_STEP', '1')
+    r = matcher.match_batch(traces, copy_out=True)
+    assert int(r.route_tier_code[0]) >= 1000000  # the step kernel ran (route_tier_code 1,000,000 + CAP * 100 + RMAX)
+    got = _lib.result_to_numpy(r)
+    prm = po.params(**{k: float(v) for k, v in over.items()})
+    want = po.match_batch(po.Graph(path), traces, prm, threads=8)
+    errors, stats = compare(got, want)
+    assert not errors, errors
     assert got['status'] == 0
