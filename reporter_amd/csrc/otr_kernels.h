@@ -14,6 +14,7 @@
 // Every decision-path expression mirrors oracle/oracle.c operation for operation
 // (DESIGN.md §3); the tests compare the two bit for bit.
 #pragma once
+#include <cstddef>
 #include <type_traits>
 
 #include "otr_device.h"
@@ -503,9 +504,10 @@ template <int CAP, bool PRED>
 struct SearchLds {
   typename LabelT<PRED>::T lab[CAP];  // label (| pred edge)
   uint32_t key[CAP];                  // node id | INQ bit, 0xFFFFFFFF empty
-  uint32_t hv[CAP];                   // A* heuristic, mm
+  uint16_t hv[CAP];                   // A* heuristic in 64-mm units, rounded down (hq_of): a lower bound of h
   using Idx = typename std::conditional<(CAP <= 256 && !PRED), uint8_t, uint16_t>::type;
-  static constexpr int WCAP = CAP <= 160 ? 48 : CAP / 4;  // nodes settled per round (at most)
+  // nodes settled per round (at most); k_paths (PRED) reuses pend + work as CAP u32 words
+  static constexpr int WCAP = CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : 128));
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
   uint2 work[WCAP];                   // this round's settled nodes: {node, label}
   int n_pend, n_keys, overflow;
@@ -516,6 +518,13 @@ struct SearchLds {
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+// A node's heuristic as stored in the search table: 64-mm units rounded down, saturating
+// at 65535 (4.19 km).  A lower bound of h keeps every finality / unreachability test
+// valid (fmin = min over pending nodes of L(u) + hq(u) <= L(u) + h(u), and any path through
+// u reaches T with length >= L(u) + h(u) - h(T)): the stored value only
+// orders the search.  The relaxing lanes' own improvements still report exact f.
+__device__ inline uint16_t hq_of(uint32_t h) { return (uint16_t)((h >> 6) < 65535u ? (h >> 6) : 65535u); }
 constexpr uint32_t kInq = 0x80000000u;
 constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
 constexpr uint32_t kNoRoute = 0xFFFFFFFFu;  // transition array: no valid route within the bound
@@ -701,7 +710,7 @@ __device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, const Pa
   const uint32_t h = H(vlat, vlon);
   const int sl = lds_insert<CAP, PRED, COUNT>(L, dw & kAdjDstMask, &isnew);
   if (sl < 0) return -1;
-  if (isnew) L.hv[sl] = h;
+  if (isnew) L.hv[sl] = hq_of(h);
   const typename LabelT<PRED>::T nb = LabelT<PRED>::make(nw, edge);
   const typename LabelT<PRED>::T old = atomicMin(&L.lab[sl], nb);
   if (LabelT<PRED>::label(nb) < LabelT<PRED>::label(old)) {
@@ -715,6 +724,61 @@ __device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, const Pa
   return -1;
 }
 
+// relax_one for the plain (non-PRED) tables with its common path branch-free: the
+// group's lanes all issue the insert, label and pending-bit atomics, a lane with nothing
+// to do aiming them at its own word of `sink` (a per-wave scratch row in LDS whose values
+// are never read), so the exec-mask bookkeeping of the nested ifs is gone — the scalar
+// unit, which carries it, was the search's busiest issue port.  Only a
+// probe chain past the home slot takes a loop (wave-uniform branch, rare).  Same slots,
+// labels and pending list as relax_one.
+template <int CAP>
+__device__ inline int relax_sink(SearchLds<CAP, false>& L, uint32_t* sink, const Heur& H, const Pack& K,
+                                 uint32_t dw, uint32_t len_mm, uint32_t time_ds, int32_t vlat, int32_t vlon,
+                                 uint32_t pu, uint32_t bound_mm, uint32_t mode_bit, uint32_t& relaxed,
+                                 uint32_t& fnext, bool& isnew) {
+  const bool mode_ok = (((dw >> 28) & 7u) & mode_bit) != 0u;
+  relaxed += mode_ok ? 1u : 0u;
+  const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
+  const uint32_t tt = K.t(pu) + time_ds;
+  const uint32_t nw = (nd << K.sh) | (tt < K.tcap() ? tt : K.tcap());
+  const uint32_t node = dw & kAdjDstMask;
+  bool go = mode_ok && nd <= bound_mm;
+  uint32_t* mine = sink + lane_id();
+  const uint32_t h0 = hslot<CAP>(node);
+  const uint32_t k0 = atomicCAS(go ? &L.key[h0] : mine, kEmpty, node);
+  isnew = go && k0 == kEmpty;
+  int sl = (go && (k0 == kEmpty || (k0 & ~kInq) == node)) ? (int)h0 : -1;
+  const bool coll = go && sl < 0;
+  if (__ballot(coll) != 0ull) {  // the home slot holds another node: linear probing
+    if (coll) {
+      uint32_t hh = h0;
+      for (int probe = 1; probe < CAP; ++probe) {
+        hh = hh + 1 == (uint32_t)CAP ? 0u : hh + 1;
+        const uint32_t k = atomicCAS(&L.key[hh], kEmpty, node);
+        if (k == kEmpty) {
+          isnew = true;
+          sl = (int)hh;
+          break;
+        }
+        if ((k & ~kInq) == node) {
+          sl = (int)hh;
+          break;
+        }
+      }
+      if (sl < 0) L.overflow = 1;
+    }
+  }
+  go = go && sl >= 0;
+  const uint32_t h = H(vlat, vlon);
+  *((go && isnew) ? &L.hv[sl] : reinterpret_cast<uint16_t*>(mine)) = hq_of(h);
+  const uint32_t old = atomicMin(go ? &L.lab[sl] : mine, nw);
+  const bool imp = go && nw < old;
+  const uint32_t f = nd + h;
+  fnext = (imp && f < fnext) ? f : fnext;
+  const uint32_t was = atomicOr(imp ? &L.key[sl] : mine, kInq);
+  return (imp && !(was & kInq)) ? sl : -1;  // newly pending: the caller appends it
+}
+
 // G searches per wave, one per lane group, each in its own table Ls[g]: search g is
 // rooted at `start` (label 0); lanes gl < n_tgt of the group hold a target node tnode, its
 // heuristic hT and partial length tpart (mm).  active = false: the group idles.  K packs
@@ -726,7 +790,8 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
                            bool active, uint32_t start, uint32_t bound_mm, uint32_t delta_mm, uint32_t tnode,
                            uint32_t tpart, uint32_t hT, uint32_t d0min, int n_tgt, unsigned long long* settled,
                            unsigned long long* relaxed, unsigned long long* rounds,
-                           unsigned long long* stamps = nullptr, uint32_t hroot_in = 0xFFFFFFFFu) {
+                           unsigned long long* stamps = nullptr, uint32_t hroot_in = 0xFFFFFFFFu,
+                           uint32_t* sink = nullptr) {
   using Gr = Grp<G>;
   // load-factor limit (probe chains stay short); small tables run fuller
   // (7/8 on the retry tiers: fewer searches outgrow 448/512 slots; C4 4.79M -> 5.11M
@@ -748,7 +813,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
   if (active && gl == 0) {
     bool isnew;
     const int sl = lds_insert(L, start, &isnew);
-    L.hv[sl] = hroot;
+    L.hv[sl] = hq_of(hroot);
     L.lab[sl] = LabelT<PRED>::make(0u, kEmpty);
     L.key[sl] |= kInq;
     L.pend[0] = (Idx)sl;
@@ -759,7 +824,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
   if (active && gl < n_tgt && tnode != kEmpty) {
     bool isnew;
     tslot = lds_insert(L, tnode, &isnew);
-    if (tslot >= 0 && isnew) L.hv[tslot] = (uint32_t)hT;
+    if (tslot >= 0 && isnew) L.hv[tslot] = hq_of(hT);
   }
   __syncthreads();
   uint32_t my_settled = 0, my_relaxed = 0, my_rounds = 0;
@@ -795,7 +860,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
         sl = L.pend[k];
         lb = LabelT<PRED>::label(L.lab[sl]);
         node = L.key[sl] & ~kInq;
-        f = K.d(lb) + L.hv[sl];  // < 2^32: labels, h < 2^31
+        f = K.d(lb) + ((uint32_t)L.hv[sl] << 6);  // < 2^32: labels, h < 2^31
         take = f < theta;
       }
       // at most WCAP settles per round; the rest stay pending (order only, never labels)
@@ -836,8 +901,17 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
         const uint4 r = ld16(g.adj + 4 * (size_t)wk.x + slot);
         const uint32_t tt = timed ? tq : 0u;
         const uint32_t e0 = PRED ? g.node_row[wk.x] : 0u;  // edge id = CSR row start + slot
-        psl = relax_one<CAP, PRED, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.y,
-                                          e0 + slot, bound_mm, mode_bit, my_relaxed, fnext, isnew);
+        if constexpr (!PRED) {
+          if (sink)
+            psl = relax_sink<CAP>(L, sink, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.y, bound_mm,
+                                  mode_bit, my_relaxed, fnext, isnew);
+          else
+            psl = relax_one<CAP, PRED, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.y,
+                                              e0 + slot, bound_mm, mode_bit, my_relaxed, fnext, isnew);
+        } else {
+          psl = relax_one<CAP, PRED, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.y,
+                                            e0 + slot, bound_mm, mode_bit, my_relaxed, fnext, isnew);
+        }
         tail = tail || (slot == 3 && (r.x & kAdjMore));
       }
       nkeys += Gr::count(__ballot(isnew));
@@ -1084,7 +1158,7 @@ __device__ inline int nth_set_bit(unsigned long long m, int q) {
 // belongs to the search)
 template <int CAP, int G, bool LIST, bool TURN>
 __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& a, unsigned long long* counters,
-                                           SearchLds<CAP, TURN>* Ls, int64_t w, int64_t n_tasks) {
+                                           SearchLds<CAP, TURN>* Ls, int64_t w, int64_t n_tasks, uint32_t* sink) {
   using Gr = Grp<G>;
   const int lane = Gr::gl();
   const int64_t tw = w * G + Gr::g();
@@ -1160,7 +1234,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   search_init<CAP, TURN, G>(Ls);
   bool ok = search_run<CAP, TURN, G>(Ls, gr, H, K, mode_bit, search, root, bmm,
                                       (uint32_t)(a.delta * 1000.0), tnode, tpart, hT, d0min, Kb, &settled, &relaxed,
-                                      &rounds, counters ? counters + 16 * kCShards : nullptr, hroot) &&
+                                      &rounds, counters ? counters + 16 * kCShards : nullptr, hroot, sink) &&
             fits;
 #ifdef OTR_FORCE_RETRY
   if (G == 2 && !LIST) ok = false;  // test build: every first-tier task takes the retry tiers
@@ -1306,16 +1380,22 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
 template <int CAP, int G, bool LIST, bool TURN = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR_ROUTE2_WAVES : 8, G == 2 ? OTR_ROUTE2_WAVES : 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
   __shared__ SearchLds<CAP, TURN> Ls[G];
+#ifdef OTR_NO_SINK
+  uint32_t* sink = nullptr;  // A/B build: the branching relax_one everywhere
+#else
+  __shared__ uint32_t sink_row[OTR_WAVE];  // relax_sink's per-lane scratch words (non-TURN tables)
+  uint32_t* sink = TURN ? nullptr : sink_row;
+#endif
   if (!LIST) {  // the first tier: one unit per block, XCD-mapped (no loop: fewer live registers)
     const int64_t n_units = (a.n_tasks + G - 1) / G;
     const int64_t w = xcd_remap(blockIdx.x, (n_units + 7) / 8);
-    if (w < n_units) route_unit<CAP, G, LIST, TURN>(gr, a, counters, Ls, w, a.n_tasks);
+    if (w < n_units) route_unit<CAP, G, LIST, TURN>(gr, a, counters, Ls, w, a.n_tasks, sink);
     return;
   }
   const int64_t n_tasks = (int64_t)*a.list_count;
   const int64_t n_units = (n_tasks + G - 1) / G;
   for (int64_t w = blockIdx.x; w < n_units; w += gridDim.x) {
-    route_unit<CAP, G, LIST, TURN>(gr, a, counters, Ls, w, n_tasks);
+    route_unit<CAP, G, LIST, TURN>(gr, a, counters, Ls, w, n_tasks, sink);
     __syncthreads();  // the next unit re-initialises the tables
   }
 }
@@ -1618,6 +1698,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
     active = false;
   }
   // walk predecessor edges T → S (the group's lane 0), staging the edges in LDS
+  static_assert(sizeof(L.pend) + sizeof(L.work) >= 4 * CAP, "path staging reuses pend + work");
+  using PL = SearchLds<CAP, true>;
+  static_assert(offsetof(PL, work) == offsetof(PL, pend) + sizeof(L.pend), "pend and work are contiguous");
   uint32_t* lp = reinterpret_cast<uint32_t*>(L.pend);  // pend+work are contiguous: >= CAP u32
   int n = 0;
   if (active && gl == 0) {
