@@ -54,13 +54,15 @@ def log(*a):
 def kernel_name(code, turns=False):
     """rocprofv3 name of a route kernel (otr_batch_result.route_tier_code); turns: the
     batch had turn-cost modes (the kernels compiled with the turn walk)."""
-    if code < 0:
-        return 'k_general'
+    if code < 0:  # the global-memory search: -1 on 32K-state slabs, -2 on 1M-state slabs
+        return 'k_general' if code == -1 else 'k_general (1M-state slabs)'
+    if 900000 <= code < 1000000:  # the 64-bit label tier: 900,000 + CAP
+        return 'k_route<%d, 1, true, false, true>' % (code - 900000)
     if code >= 1000000:  # the multi-root step kernel: 1,000,000 + CAP * 100 + RMAX
         return 'k_route_step<%d, %d>' % ((code - 1000000) // 100, code % 100)
     cap, g = code // 10, code % 10
-    return 'k_route<%d, %d, %s, %s>' % (cap, g, 'false' if code == 1602 or code == 2561 else 'true',
-                                        'true' if turns else 'false')
+    return 'k_route<%d, %d, %s, %s, false>' % (cap, g, 'false' if code == 1602 or code == 2561 else 'true',
+                                               'true' if turns else 'false')
 
 
 def route_bytes(work):
@@ -377,7 +379,7 @@ def main():
         raise RuntimeError('instrumented step differs from the timed steps')
     work_of = {}
     for r in work_rs:
-        for t in range(8):
+        for t in range(len(r.route_tier_code)):
             if int(r.route_tier_code[t]) != 0:
                 w = work_of.setdefault(t, np.zeros(4, np.int64))
                 w += np.array([int(x) for x in r.route_tier_work[t]], np.int64)
@@ -386,7 +388,7 @@ def main():
     tiers = {}
     for step_rs in results:
         for r in step_rs:
-            for t in range(8):
+            for t in range(len(r.route_tier_code)):
                 code = int(r.route_tier_code[t])
                 if code == 0:
                     continue

@@ -938,9 +938,25 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
 #undef OTR_TIER
       if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier) + 1], stream);
     }
-    // everything left — turn-cost (edge-based) tasks, tasks whose labels need 64 bits,
-    // overflows of the largest LDS table — runs in the global-memory search: first on
-    // 32K-slot slabs, then what outgrew those on 1M-slot slabs
+#ifndef OTR_FORCE_GENERAL  // (test build: every search in k_general)
+    // batches without turn costs: the tasks whose (length << sh | time) words need more
+    // than 32 bits (flag 3: long gaps between states) run in an LDS table of 64-bit words
+    // (same labels); what outgrows it is flagged 3 again
+    if (!turns) {
+      unsigned long long* c = cnt + 7;
+      k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, 0x8u, list, c);
+      RouteArgs rb = ra;
+      rb.task_list = list;
+      rb.list_count = c;
+      out->route_tier_code[8] = 900000 + 2048;
+      if (timing) (void)hipEventRecord(ev[24 + 2 * 8], stream);
+      k_route<2048, 1, true, false, true><<<4096, 64, 0, stream>>>(g, rb, rwork ? d_counters + 7 * bank : nullptr);
+      if (timing) (void)hipEventRecord(ev[24 + 2 * 8 + 1], stream);
+    }
+#endif
+    // everything left — turn-cost (edge-based) tasks, (turn-mode) tasks whose labels need
+    // 64 bits, overflows of the largest LDS tables — runs in the global-memory search:
+    // first on 32K-slot slabs, then what outgrew those on 1M-slot slabs
     for (int gt = 0; gt < 2; ++gt) {
       unsigned long long* c = cnt + 8 + gt;
       k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, gt == 0 ? 0xEu : 0x2u, list, c);
@@ -1228,13 +1244,13 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   };
   for (int k = 0; k < OTR_COUNTERS; ++k) out->counters[k] = ctr(0, k);
   // per route kernel: searches, settled, relaxed, transition entries (banks 0, 2..6, 8..9)
-  for (int t = 0; t < 8; ++t) {
-    const int b = t == 0 ? 0 : (t < 6 ? 1 + t : 2 + t);
+  for (int t = 0; t < 9; ++t) {
+    const int b = t == 0 ? 0 : (t < 6 ? 1 + t : (t < 8 ? 2 + t : 7));  // slot 8 (64-bit LDS tier): bank 7
     out->route_tier_work[t][0] = ctr(b, 6);
     out->route_tier_work[t][1] = ctr(b, 3);
     out->route_tier_work[t][2] = ctr(b, 4);
     out->route_tier_work[t][3] = ctr(b, 5);
-    if (t >= 1 && t < 6) {  // the LDS retry tiers together (counters 9 / 10)
+    if ((t >= 1 && t < 6) || t == 8) {  // the LDS retry tiers together (counters 9 / 10)
       out->counters[9] += ctr(b, 3);
       out->counters[10] += ctr(b, 4);
     }
@@ -1249,7 +1265,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     for (int k = 0; k < 10; ++k)
       if (used[k]) (void)hipEventElapsedTime(&out->kernel_ms[k], ev[2 * k], ev[2 * k + 1]);
     out->route_tier_ms[0] = out->kernel_ms[OTR_STAGE_ROUTE];
-    for (int t = 1; t < 8; ++t)
+    for (int t = 1; t < 9; ++t)
       if (out->route_tier_code[t] != 0)
         (void)hipEventElapsedTime(&out->route_tier_ms[t], ev[24 + 2 * t], ev[24 + 2 * t + 1]);
   }

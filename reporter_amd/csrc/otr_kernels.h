@@ -485,31 +485,57 @@ struct Grp {
   }
 };
 
-template <bool PRED>
+// Label word of a search table, by label mode LM: 0 the packed (length << sh | time) word
+// in 32 bits; 1 (PRED) that word << 32 | the smallest predecessor edge; 2 (WIDE) the
+// packed word in 64 bits, for steps whose length and time bits exceed 32 (long gaps
+// between states).  W: the packed word as label() returns it.
+template <int LM>
 struct LabelT {
   using T = uint32_t;
+  using W = uint32_t;
   static constexpr T kInf = 0xFFFFFFFFu;
-  __device__ static uint32_t label(T x) { return x; }
-  __device__ static T make(uint32_t l, uint32_t) { return l; }
+  static constexpr W kNone = 0xFFFFFFFFu;
+  __device__ static W label(T x) { return x; }
+  __device__ static T make(W l, uint32_t) { return l; }
 };
 template <>
-struct LabelT<true> {
+struct LabelT<1> {
   using T = unsigned long long;
+  using W = uint32_t;
   static constexpr T kInf = 0xFFFFFFFFFFFFFFFFull;
-  __device__ static uint32_t label(T x) { return (uint32_t)(x >> 32); }
-  __device__ static T make(uint32_t l, uint32_t e) { return ((unsigned long long)l << 32) | e; }
+  static constexpr W kNone = 0xFFFFFFFFu;
+  __device__ static W label(T x) { return (uint32_t)(x >> 32); }
+  __device__ static T make(W l, uint32_t e) { return ((unsigned long long)l << 32) | e; }
+};
+template <>
+struct LabelT<2> {
+  using T = unsigned long long;
+  using W = unsigned long long;
+  static constexpr T kInf = 0xFFFFFFFFFFFFFFFFull;
+  static constexpr W kNone = 0xFFFFFFFFFFFFFFFFull;
+  __device__ static W label(T x) { return x; }
+  __device__ static T make(W l, uint32_t) { return l; }
 };
 
-template <int CAP, bool PRED>
+// a settled node of this round: its id and the packed label it was settled with
+template <class W>
+struct WorkE {
+  uint32_t node;
+  W lab;
+};
+
+template <int CAP, int LM>
 struct SearchLds {
-  typename LabelT<PRED>::T lab[CAP];  // label (| pred edge)
+  static constexpr bool PRED = LM == 1;
+  using W = typename LabelT<LM>::W;
+  typename LabelT<LM>::T lab[CAP];  // label (| pred edge)
   uint32_t key[CAP];                  // node id | INQ bit, 0xFFFFFFFF empty
   uint16_t hv[CAP];                   // A* heuristic in 64-mm units, rounded down (hq_of): a lower bound of h
   using Idx = typename std::conditional<(CAP <= 256 && !PRED), uint8_t, uint16_t>::type;
   // nodes settled per round (at most); k_paths (PRED) reuses pend + work as CAP u32 words
   static constexpr int WCAP = CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : 128));
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
-  uint2 work[WCAP];                   // this round's settled nodes: {node, label}
+  WorkE<W> work[WCAP];                // this round's settled nodes: {node, label}
   int n_pend, n_keys, overflow;
   // PRED: 1 when a second in-edge reached the node with its label (a tie the turn costs
   // of an edge-based route would decide; never cleared, so it may also flag a label
@@ -596,8 +622,8 @@ __device__ inline uint32_t hslot(uint32_t node) {
   return __umulhi(node * 0x9E3779B1u, (uint32_t)CAP);
 }
 
-template <int CAP, bool PRED>
-__device__ inline int lds_find(const SearchLds<CAP, PRED>& L, uint32_t node) {
+template <int CAP, int LM>
+__device__ inline int lds_find(const SearchLds<CAP, LM>& L, uint32_t node) {
   uint32_t h = hslot<CAP>(node);
   for (int probe = 0; probe < CAP; ++probe) {
     const uint32_t k = L.key[h];
@@ -610,8 +636,8 @@ __device__ inline int lds_find(const SearchLds<CAP, PRED>& L, uint32_t node) {
 
 // COUNT: add new keys to L.n_keys; the main relax loop instead counts them by ballot in a
 // register (one LDS atomic less per new key, and no same-address atomic serialisation)
-template <int CAP, bool PRED, bool COUNT = true>
-__device__ inline int lds_insert(SearchLds<CAP, PRED>& L, uint32_t node, bool* isnew) {
+template <int CAP, int LM, bool COUNT = true>
+__device__ inline int lds_insert(SearchLds<CAP, LM>& L, uint32_t node, bool* isnew) {
   uint32_t h = hslot<CAP>(node);
   for (int probe = 0; probe < CAP; ++probe) {
     // CAS first: one LDS round trip both claims an empty slot and reads an occupied one
@@ -631,13 +657,14 @@ __device__ inline int lds_insert(SearchLds<CAP, PRED>& L, uint32_t node, bool* i
   return -1;
 }
 
-template <int CAP, bool PRED, int G = 1>
-__device__ inline void search_init(SearchLds<CAP, PRED>* Ls) {
+template <int CAP, int LM, int G = 1>
+__device__ inline void search_init(SearchLds<CAP, LM>* Ls) {
+  constexpr bool PRED = LM == 1;
   for (int q = 0; q < G; ++q) {
-    SearchLds<CAP, PRED>& L = Ls[q];
+    SearchLds<CAP, LM>& L = Ls[q];
     for (int k = threadIdx.x; k < CAP; k += OTR_WAVE) {
       L.key[k] = kEmpty;
-      L.lab[k] = LabelT<PRED>::kInf;
+      L.lab[k] = LabelT<LM>::kInf;
       if (PRED) L.tie[k] = 0;
     }
     if (threadIdx.x == 0) {
@@ -656,8 +683,10 @@ __device__ inline void search_init(SearchLds<CAP, PRED>* Ls) {
 struct Pack {
   uint32_t sh;
   __device__ uint32_t tcap() const { return (1u << sh) - 1u; }
-  __device__ uint32_t d(uint32_t w) const { return w >> sh; }
-  __device__ uint32_t t(uint32_t w) const { return w & tcap(); }
+  template <class W>
+  __device__ uint32_t d(W w) const { return (uint32_t)(w >> sh); }
+  template <class W>
+  __device__ uint32_t t(W w) const { return (uint32_t)(w & (W)tcap()); }
 };
 // the step's shift: the smallest sh with 2^sh - 1 >= bt + 1; 0 without a time bound
 __host__ __device__ inline uint32_t pack_shift(int32_t bt) {
@@ -676,13 +705,13 @@ __host__ __device__ inline bool pack_fits(uint32_t bmm, uint32_t sh) {
 // length is strictly shorter than any path not yet found, so its time is final too);
 // if even min(L(T), fmin - h(T)) cannot make d0 + L + tpart fit the bound, T is
 // unreachable for every source of the task.  Integer arithmetic: no rounding margins needed.
-template <int CAP, bool PRED>
-__device__ inline bool target_resolved(const SearchLds<CAP, PRED>& L, const Pack& K, int tslot, uint32_t tpart,
+template <int CAP, int LM>
+__device__ inline bool target_resolved(const SearchLds<CAP, LM>& L, const Pack& K, int tslot, uint32_t tpart,
                                        uint32_t hT, uint32_t d0min, uint32_t bound_mm, uint32_t fmin,
                                        bool pend_empty) {
   if (tslot < 0 || pend_empty) return true;
-  const uint32_t l32 = LabelT<PRED>::label(L.lab[tslot]);
-  const int64_t lab = l32 == kNoLabel ? INT64_MAX / 4 : (int64_t)K.d(l32);
+  const typename LabelT<LM>::W lw = LabelT<LM>::label(L.lab[tslot]);
+  const int64_t lab = lw == LabelT<LM>::kNone ? INT64_MAX / 4 : (int64_t)K.d(lw);
   if (lab + (int64_t)hT < (int64_t)fmin) return true;
   const int64_t rest = (int64_t)fmin - (int64_t)hT;
   const int64_t lb = lab < rest ? lab : rest;
@@ -695,30 +724,32 @@ __device__ inline bool target_resolved(const SearchLds<CAP, PRED>& L, const Pack
 // be writing; the round's minimum over improvements and kept pending nodes is the next
 // round's fmin.  A label improves when its packed word does (a shorter length, or the
 // same length sooner): the node is then pending again.
-template <int CAP, bool PRED, bool COUNT = true>
-__device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, const Pack& K, uint32_t dw, uint32_t len_mm,
-                                uint32_t time_ds, int32_t vlat, int32_t vlon, uint32_t pu, uint32_t edge,
+template <int CAP, int LM, bool COUNT = true>
+__device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack& K, uint32_t dw, uint32_t len_mm,
+                                uint32_t time_ds, int32_t vlat, int32_t vlon, typename LabelT<LM>::W pu, uint32_t edge,
                                 uint32_t bound_mm, uint32_t mode_bit, uint32_t& relaxed, uint32_t& fnext,
                                 bool& isnew) {
+  constexpr bool PRED = LM == 1;
+  using W = typename LabelT<LM>::W;
   isnew = false;
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
   const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
   if (nd > bound_mm) return -1;
   const uint32_t tt = K.t(pu) + time_ds;  // both < 2^31
-  const uint32_t nw = (nd << K.sh) | (tt < K.tcap() ? tt : K.tcap());
+  const W nw = ((W)nd << K.sh) | (W)(tt < K.tcap() ? tt : K.tcap());
   const uint32_t h = H(vlat, vlon);
-  const int sl = lds_insert<CAP, PRED, COUNT>(L, dw & kAdjDstMask, &isnew);
+  const int sl = lds_insert<CAP, LM, COUNT>(L, dw & kAdjDstMask, &isnew);
   if (sl < 0) return -1;
   if (isnew) L.hv[sl] = hq_of(h);
-  const typename LabelT<PRED>::T nb = LabelT<PRED>::make(nw, edge);
-  const typename LabelT<PRED>::T old = atomicMin(&L.lab[sl], nb);
-  if (LabelT<PRED>::label(nb) < LabelT<PRED>::label(old)) {
+  const typename LabelT<LM>::T nb = LabelT<LM>::make(nw, edge);
+  const typename LabelT<LM>::T old = atomicMin(&L.lab[sl], nb);
+  if (LabelT<LM>::label(nb) < LabelT<LM>::label(old)) {
     const uint32_t f = nd + h;
     fnext = f < fnext ? f : fnext;
     const uint32_t ok = atomicOr(&L.key[sl], kInq);
     if (!(ok & kInq)) return sl;  // newly pending: the caller appends it
-  } else if (PRED && LabelT<PRED>::label(nb) == LabelT<PRED>::label(old) && nb != old) {
+  } else if (PRED && LabelT<LM>::label(nb) == LabelT<LM>::label(old) && nb != old) {
     L.tie[sl] = 1;
   }
   return -1;
@@ -732,7 +763,7 @@ __device__ inline int relax_one(SearchLds<CAP, PRED>& L, const Heur& H, const Pa
 // probe chain past the home slot takes a loop (wave-uniform branch, rare).  Same slots,
 // labels and pending list as relax_one.
 template <int CAP>
-__device__ inline int relax_sink(SearchLds<CAP, false>& L, uint32_t* sink, const Heur& H, const Pack& K,
+__device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heur& H, const Pack& K,
                                  uint32_t dw, uint32_t len_mm, uint32_t time_ds, int32_t vlat, int32_t vlon,
                                  uint32_t pu, uint32_t bound_mm, uint32_t mode_bit, uint32_t& relaxed,
                                  uint32_t& fnext, bool& isnew) {
@@ -784,8 +815,8 @@ __device__ inline int relax_sink(SearchLds<CAP, false>& L, uint32_t* sink, const
 // heuristic hT and partial length tpart (mm).  active = false: the group idles.  K packs
 // the labels (route time tracked when K.sh > 0, from adj_t / edge_t: the mode's times).
 // Returns false (per lane, group-uniform) on an LDS-table overflow.
-template <int CAP, bool PRED, int G = 1>
-__device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const Heur& H, const Pack& K,
+template <int CAP, int LM, int G = 1>
+__device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur& H, const Pack& K,
                            uint32_t mode_bit,
                            bool active, uint32_t start, uint32_t bound_mm, uint32_t delta_mm, uint32_t tnode,
                            uint32_t tpart, uint32_t hT, uint32_t d0min, int n_tgt, unsigned long long* settled,
@@ -799,22 +830,24 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
   // only delays the overflow of the searches that outgrow it)
   constexpr int kMaxKeys = (CAP <= 128 || CAP >= 256) ? (CAP * 7) / 8 : (CAP * 3) / 4;
   const int gl = Gr::gl();
-  SearchLds<CAP, PRED>& L = Ls[Gr::g()];
+  constexpr bool PRED = LM == 1;
+  using W = typename LabelT<LM>::W;
+  SearchLds<CAP, LM>& L = Ls[Gr::g()];
   // h(root): given (k_task_rec), or from the root's coordinates
   uint32_t hroot = hroot_in;
   if (hroot_in == 0xFFFFFFFFu) {
     const int2 sll = g.node_ll[active ? start : 0u];
     hroot = H(sll.x, sll.y);
   }
-  using Idx = typename SearchLds<CAP, PRED>::Idx;
-  constexpr int WCAP = SearchLds<CAP, PRED>::WCAP;
+  using Idx = typename SearchLds<CAP, LM>::Idx;
+  constexpr int WCAP = SearchLds<CAP, LM>::WCAP;
   const bool timed = K.sh != 0u;  // group-uniform
   const uint32_t* adjt = g.adj_t + (size_t)__builtin_ctz(mode_bit) * g.adj_t_stride;
   if (active && gl == 0) {
     bool isnew;
     const int sl = lds_insert(L, start, &isnew);
     L.hv[sl] = hq_of(hroot);
-    L.lab[sl] = LabelT<PRED>::make(0u, kEmpty);
+    L.lab[sl] = LabelT<LM>::make(0u, kEmpty);
     L.key[sl] |= kInq;
     L.pend[0] = (Idx)sl;
   }
@@ -854,11 +887,12 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
       const int k = base + gl;
       const bool in = k < np;
       int sl = 0;
-      uint32_t f = 0, lb = 0, node = 0;
+      uint32_t f = 0, node = 0;
+      W lb = 0;
       bool take = false;
       if (in) {
         sl = L.pend[k];
-        lb = LabelT<PRED>::label(L.lab[sl]);
+        lb = LabelT<LM>::label(L.lab[sl]);
         node = L.key[sl] & ~kInq;
         f = K.d(lb) + ((uint32_t)L.hv[sl] << 6);  // < 2^32: labels, h < 2^31
         take = f < theta;
@@ -868,7 +902,7 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
       const unsigned long long mt = __ballot(take), mk = __ballot(in && !take);
       __syncthreads();
       if (take) {
-        L.work[nw + Gr::prefix(mt)] = make_uint2(node, lb);
+        L.work[nw + Gr::prefix(mt)] = WorkE<W>{node, lb};
         atomicAnd(&L.key[sl], ~kInq);
       } else if (in) {
         L.pend[kept + Gr::prefix(mk)] = (Idx)sl;
@@ -890,26 +924,26 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
       int psl = -1;
       bool isnew = false;
       if (k < 4 * nw) {
-        const uint2 wk = L.work[k >> 2];
+        const WorkE<W> wk = L.work[k >> 2];
         const int slot = k & 3;
         if (slot == 0) ++my_settled;
         // the mode's route time of the slot (DevGraph::adj_t, one block per mode), loaded
         // ahead of the adjacency record and unconditionally: both loads in flight together
         // (issued after ld16's register barrier it had made every relaxation wait for two
         // global loads in a row)
-        const uint32_t tq = adjt[4 * (size_t)wk.x + slot];
-        const uint4 r = ld16(g.adj + 4 * (size_t)wk.x + slot);
+        const uint32_t tq = adjt[4 * (size_t)wk.node + slot];
+        const uint4 r = ld16(g.adj + 4 * (size_t)wk.node + slot);
         const uint32_t tt = timed ? tq : 0u;
-        const uint32_t e0 = PRED ? g.node_row[wk.x] : 0u;  // edge id = CSR row start + slot
-        if constexpr (!PRED) {
+        const uint32_t e0 = PRED ? g.node_row[wk.node] : 0u;  // edge id = CSR row start + slot
+        if constexpr (LM == 0) {
           if (sink)
-            psl = relax_sink<CAP>(L, sink, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.y, bound_mm,
+            psl = relax_sink<CAP>(L, sink, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab, bound_mm,
                                   mode_bit, my_relaxed, fnext, isnew);
           else
-            psl = relax_one<CAP, PRED, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.y,
+            psl = relax_one<CAP, LM, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab,
                                               e0 + slot, bound_mm, mode_bit, my_relaxed, fnext, isnew);
         } else {
-          psl = relax_one<CAP, PRED, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.y,
+          psl = relax_one<CAP, LM, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab,
                                             e0 + slot, bound_mm, mode_bit, my_relaxed, fnext, isnew);
         }
         tail = tail || (slot == 3 && (r.x & kAdjMore));
@@ -932,14 +966,14 @@ __device__ bool search_run(SearchLds<CAP, PRED>* Ls, const DevGraph& g, const He
       for (int base = 0; base < nwx; base += Gr::GL) {
         const int k = base + gl;
         if (k < 4 * nw && (k & 3) == 3) {
-          const uint2 wk = L.work[k >> 2];
-          if (g.adj[4 * (size_t)wk.x + 3].x & kAdjMore)
-            for (uint32_t e = g.node_row[wk.x] + 4; e < g.node_row[wk.x + 1]; ++e) {
+          const WorkE<W> wk = L.work[k >> 2];
+          if (g.adj[4 * (size_t)wk.node + 3].x & kAdjMore)
+            for (uint32_t e = g.node_row[wk.node] + 4; e < g.node_row[wk.node + 1]; ++e) {
               const uint4 pk = ld16(g.edge_pack + e);
               const int2 vll = g.node_ll[pk.x];
               const uint32_t tt = timed ? g.et(__builtin_ctz(mode_bit))[e] : 0u;
               bool isnew;
-              const int psl = relax_one(L, H, K, pk.x | ((pk.z & 7u) << 28), pk.y, tt, vll.x, vll.y, wk.y, e,
+              const int psl = relax_one(L, H, K, pk.x | ((pk.z & 7u) << 28), pk.y, tt, vll.x, vll.y, wk.lab, e,
                                         bound_mm, mode_bit, my_relaxed, fnext, isnew);
               if (psl >= 0) {
                 const int p = atomicAdd(&L.n_pend, 1);
@@ -1155,10 +1189,14 @@ __device__ inline int nth_set_bit(unsigned long long m, int q) {
 // one unit = G search tasks of the wave (ordinal w of the task range or list).  TURN:
 // the batch has turn-cost modes, whose transition rows walk the routes (turn_walk); a
 // batch without them runs the kernel compiled without that code (its register budget
-// belongs to the search)
-template <int CAP, int G, bool LIST, bool TURN>
+// belongs to the search).  WIDE: the table keeps 64-bit packed words and takes the
+// tasks whose (length << sh | time) words do not fit 32 bits (`general` in the record)
+template <int CAP, int G, bool LIST, bool TURN, bool WIDE = false>
 __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& a, unsigned long long* counters,
-                                           SearchLds<CAP, TURN>* Ls, int64_t w, int64_t n_tasks, uint32_t* sink) {
+                                           SearchLds<CAP, TURN ? 1 : (WIDE ? 2 : 0)>* Ls, int64_t w, int64_t n_tasks,
+                                           uint32_t* sink) {
+  constexpr int LM = TURN ? 1 : (WIDE ? 2 : 0);
+  static_assert(!(TURN && WIDE), "turn-mode tables carry predecessor edges in the low word");
   using Gr = Grp<G>;
   const int lane = Gr::gl();
   const int64_t tw = w * G + Gr::g();
@@ -1181,7 +1219,9 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     Kb = (int)(r1.y & 0xFFu);
     K.sh = (r1.y >> 11) & 31u;
     const bool general = (r1.y >> 16) & 1u;  // re-read after the search
-    fits = Kb <= Gr::GL && !general;  // targets are lanes of the group: wider steps go to a G = 1 tier
+    // targets are lanes of the group (wider steps go to a G = 1 tier); 32-bit tables leave
+    // the tasks whose packed words need 64 bits to the WIDE tier
+    fits = Kb <= Gr::GL && (WIDE || !general);
     if (G == 2 && !LIST && r0.w > a.direct_bmm) fits = false;
     mode_bit = 1u << ((r1.y >> 8) & 3u);
     bmm = r0.w;
@@ -1231,8 +1271,8 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   }
   unsigned long long settled = 0, relaxed = 0, rounds = 0;
   OTR_STAMP(ts_set);
-  search_init<CAP, TURN, G>(Ls);
-  bool ok = search_run<CAP, TURN, G>(Ls, gr, H, K, mode_bit, search, root, bmm,
+  search_init<CAP, LM, G>(Ls);
+  bool ok = search_run<CAP, LM, G>(Ls, gr, H, K, mode_bit, search, root, bmm,
                                       (uint32_t)(a.delta * 1000.0), tnode, tpart, hT, d0min, Kb, &settled, &relaxed,
                                       &rounds, counters ? counters + 16 * kCShards : nullptr, hroot, sink) &&
             fits;
@@ -1240,11 +1280,11 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   if (G == 2 && !LIST) ok = false;  // test build: every first-tier task takes the retry tiers
 #endif
   OTR_STAMP(ts_srch);
-  SearchLds<CAP, TURN>& L = Ls[Gr::g()];
+  SearchLds<CAP, LM>& L = Ls[Gr::g()];
   int64_t lab = -1;
   if (ok && tnode != kEmpty && !forced) {
     const int sl = lds_find(L, tnode);
-    if (sl >= 0 && LabelT<TURN>::label(L.lab[sl]) != kNoLabel) lab = (int64_t)LabelT<TURN>::label(L.lab[sl]);
+    if (sl >= 0 && LabelT<LM>::label(L.lab[sl]) != LabelT<LM>::kNone) lab = (int64_t)LabelT<LM>::label(L.lab[sl]);
   }
   // ---- transition rows: re-read the step (cached) rather than hold it live through the search
   asm volatile("" ::: "memory");
@@ -1308,8 +1348,8 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
           r = part_mm(pj - pi, gr.len_mm[ei]);
           if (bt >= 0) rt = part_mm(pj - pi, gr.et(md)[ei]);
         } else if (lab >= 0) {
-          r = (int64_t)wi + K.d((uint32_t)lab) + tpart;
-          if (bt >= 0) rt = (int64_t)ti + K.t((uint32_t)lab) + tpt;
+          r = (int64_t)wi + K.d((uint64_t)lab) + tpart;
+          if (bt >= 0) rt = (int64_t)ti + K.t((uint64_t)lab) + tpt;
         }
         const bool valid = r >= 0 && r <= (int64_t)bmm && (bt < 0 || rt <= (int64_t)bt);
         trow[(int64_t)i * Kb + lane] = valid ? (uint32_t)r : kNoRoute;
@@ -1377,25 +1417,25 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   }
 }
 
-template <int CAP, int G, bool LIST, bool TURN = false>
+template <int CAP, int G, bool LIST, bool TURN = false, bool WIDE = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR_ROUTE2_WAVES : 8, G == 2 ? OTR_ROUTE2_WAVES : 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
-  __shared__ SearchLds<CAP, TURN> Ls[G];
+  __shared__ SearchLds<CAP, TURN ? 1 : (WIDE ? 2 : 0)> Ls[G];
 #ifdef OTR_NO_SINK
   uint32_t* sink = nullptr;  // A/B build: the branching relax_one everywhere
 #else
   __shared__ uint32_t sink_row[OTR_WAVE];  // relax_sink's per-lane scratch words (non-TURN tables)
-  uint32_t* sink = TURN ? nullptr : sink_row;
+  uint32_t* sink = (TURN || WIDE) ? nullptr : sink_row;
 #endif
   if (!LIST) {  // the first tier: one unit per block, XCD-mapped (no loop: fewer live registers)
     const int64_t n_units = (a.n_tasks + G - 1) / G;
     const int64_t w = xcd_remap(blockIdx.x, (n_units + 7) / 8);
-    if (w < n_units) route_unit<CAP, G, LIST, TURN>(gr, a, counters, Ls, w, a.n_tasks, sink);
+    if (w < n_units) route_unit<CAP, G, LIST, TURN, WIDE>(gr, a, counters, Ls, w, a.n_tasks, sink);
     return;
   }
   const int64_t n_tasks = (int64_t)*a.list_count;
   const int64_t n_units = (n_tasks + G - 1) / G;
   for (int64_t w = blockIdx.x; w < n_units; w += gridDim.x) {
-    route_unit<CAP, G, LIST, TURN>(gr, a, counters, Ls, w, n_tasks, sink);
+    route_unit<CAP, G, LIST, TURN, WIDE>(gr, a, counters, Ls, w, n_tasks, sink);
     __syncthreads();  // the next unit re-initialises the tables
   }
 }

@@ -75,3 +75,23 @@ def test_step_kernel_parity(name, graph_dir, matcher, monkeypatch):
     errors, stats = compare(got, want)
     assert not errors, errors
     assert got['status'] == 0
+
+
+def test_wide_label_tier_parity(graph_dir, matcher):
+    """Steps whose packed (length << sh | time) words need more than 32 bits — 120 s between
+    states: time bound 2400 ds = 12 time bits, 2 km bound = 21 length bits — run in the
+    64-bit-label LDS tier (k_route<2048, 1, true, false, true>): bit-exact oracle parity,
+    and that tier did the searches."""
+    path = gen.graph_path('metro', graph_dir)
+    over = dict(CONFIGS['gtt'])
+    M.configure(M.default_config(path, **over))
+    traces = gen.make_traces(path, 40, 30, 120, 10.0, 6)
+    r = matcher.match_batch(traces, copy_out=True, route_work=True)
+    assert r.status == 0
+    assert int(r.route_tier_code[8]) == 900000 + 2048
+    assert int(r.route_tier_work[8][0]) > 0  # searches in the 64-bit tier
+    got = _lib.result_to_numpy(r)
+    want = po.match_batch(po.Graph(path), traces, po.params(**{k: float(v) for k, v in over.items()}), threads=8)
+    errors, stats = compare(got, want)
+    assert not errors, errors
+    assert stats['n_seg'] > 0
