@@ -56,13 +56,15 @@ def kernel_name(code, turns=False):
     batch had turn-cost modes (the kernels compiled with the turn walk)."""
     if code < 0:  # the global-memory search: -1 on 32K-state slabs, -2 on 1M-state slabs
         return 'k_general' if code == -1 else 'k_general (1M-state slabs)'
+    # the timed launches run the LDS route kernels compiled without work counting (the
+    # last template argument, CNT = false; the instrumented step runs CNT = true)
     if 900000 <= code < 1000000:  # the 64-bit label tier: 900,000 + CAP
-        return 'k_route<%d, 1, true, false, true>' % (code - 900000)
+        return 'k_route<%d, 1, true, false, true, false>' % (code - 900000)
     if code >= 1000000:  # the multi-root step kernel: 1,000,000 + CAP * 100 + RMAX
         return 'k_route_step<%d, %d>' % ((code - 1000000) // 100, code % 100)
     cap, g = code // 10, code % 10
-    return 'k_route<%d, %d, %s, %s, false>' % (cap, g, 'false' if code == 1602 or code == 2561 else 'true',
-                                               'true' if turns else 'false')
+    return 'k_route<%d, %d, %s, %s, false, false>' % (cap, g, 'false' if code == 1602 or code == 2561 else 'true',
+                                                      'true' if turns else 'false')
 
 
 def route_bytes(work):

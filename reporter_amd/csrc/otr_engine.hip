@@ -872,6 +872,17 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     unsigned long long* rwork = (in->flags & OTR_BATCH_ROUTE_WORK) ? d_counters : nullptr;
     // batches with turn-cost modes take the kernels compiled with the turn walk
     const bool turns = turn_modes != 0u;
+    // the LDS route kernels: with the work counters (CNT) only when counting was asked for
+#define OTR_ROUTE_LAUNCH(C, G_, LIST_, GRID, ARGS, CTR)                                                  \
+  do {                                                                                                 \
+    if (CTR) {                                                                                         \
+      if (turns) k_route<C, G_, LIST_, true, false, true><<<GRID, 64, 0, stream>>>(g, ARGS, CTR);      \
+      else k_route<C, G_, LIST_, false, false, true><<<GRID, 64, 0, stream>>>(g, ARGS, CTR);           \
+    } else {                                                                                           \
+      if (turns) k_route<C, G_, LIST_, true, false, false><<<GRID, 64, 0, stream>>>(g, ARGS, nullptr); \
+      else k_route<C, G_, LIST_, false, false, false><<<GRID, 64, 0, stream>>>(g, ARGS, nullptr);      \
+    }                                                                                                  \
+  } while (0)
     if (use_step) {
       StepArgs st{};
       int64_t* units = need<int64_t>(S_UNIT, std::max<int64_t>(NU, 1));
@@ -892,14 +903,12 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       tb(OTR_STAGE_ROUTE);
       const int64_t units = (NT + 1) / 2;
       const unsigned grid = (unsigned)(8 * ((units + 7) / 8));
-      if (turns) k_route<160, 2, false, true><<<grid, 64, 0, stream>>>(g, ra, rwork);
-      else k_route<160, 2, false><<<grid, 64, 0, stream>>>(g, ra, rwork);
+      OTR_ROUTE_LAUNCH(160, 2, false, grid, ra, rwork);
       out->route_tier_code[0] = 1602;
     } else {
       tb(OTR_STAGE_ROUTE);
       const unsigned grid = (unsigned)(8 * ((NT + 7) / 8));
-      if (turns) k_route<256, 1, false, true><<<grid, 64, 0, stream>>>(g, ra, rwork);
-      else k_route<256, 1, false><<<grid, 64, 0, stream>>>(g, ra, rwork);
+      OTR_ROUTE_LAUNCH(256, 1, false, grid, ra, rwork);
       out->route_tier_code[0] = 2561;
     }
     te(OTR_STAGE_ROUTE);
@@ -922,9 +931,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       unsigned long long* rcn = rwork ? d_counters + (2 + tier) * bank : nullptr;
       out->route_tier_code[1 + tier] = tiers[tier];
       if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier)], stream);
-#define OTR_TIER(C, G_)                                                     \
-  (turns ? k_route<C, G_, true, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn) \
-         : k_route<C, G_, true><<<tgrid, 64, 0, stream>>>(g, rb, rcn))
+#define OTR_TIER(C, G_) OTR_ROUTE_LAUNCH(C, G_, true, tgrid, rb, rcn)
       switch (tiers[tier]) {
         case 2561: OTR_TIER(256, 1); break;
         case 5121: OTR_TIER(512, 1); break;
@@ -950,7 +957,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       rb.list_count = c;
       out->route_tier_code[8] = 900000 + 2048;
       if (timing) (void)hipEventRecord(ev[24 + 2 * 8], stream);
-      k_route<2048, 1, true, false, true><<<4096, 64, 0, stream>>>(g, rb, rwork ? d_counters + 7 * bank : nullptr);
+      if (rwork) k_route<2048, 1, true, false, true, true><<<4096, 64, 0, stream>>>(g, rb, d_counters + 7 * bank);
+      else k_route<2048, 1, true, false, true, false><<<4096, 64, 0, stream>>>(g, rb, nullptr);
       if (timing) (void)hipEventRecord(ev[24 + 2 * 8 + 1], stream);
     }
 #endif

@@ -1191,7 +1191,7 @@ __device__ inline int nth_set_bit(unsigned long long m, int q) {
 // batch without them runs the kernel compiled without that code (its register budget
 // belongs to the search).  WIDE: the table keeps 64-bit packed words and takes the
 // tasks whose (length << sh | time) words do not fit 32 bits (`general` in the record)
-template <int CAP, int G, bool LIST, bool TURN, bool WIDE = false>
+template <int CAP, int G, bool LIST, bool TURN, bool WIDE = false, bool CNT = true>
 __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& a, unsigned long long* counters,
                                            SearchLds<CAP, TURN ? 1 : (WIDE ? 2 : 0)>* Ls, int64_t w, int64_t n_tasks,
                                            uint32_t* sink) {
@@ -1393,7 +1393,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     atomicAdd(&counters[21 * kCShards + sh], ts_out - ts_srch);
   }
 #endif
-  if (counters) {
+  if (CNT && counters) {
     // wave totals: lane sums by DPP, per-group values read from each group's lane 0
     settled = wave_sum_u32((uint32_t)settled);
     relaxed = wave_sum_u32((uint32_t)relaxed);
@@ -1417,7 +1417,11 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   }
 }
 
-template <int CAP, int G, bool LIST, bool TURN = false, bool WIDE = false>
+// CNT = false: the timed launches, compiled without the work counting (the per-lane
+// settled / relaxed / round tallies are dead code there: fewer registers and
+// instructions in the search loop); CNT = true: the instrumented launches
+// (OTR_BATCH_ROUTE_WORK) that fill the work counters
+template <int CAP, int G, bool LIST, bool TURN = false, bool WIDE = false, bool CNT = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR_ROUTE2_WAVES : 8, G == 2 ? OTR_ROUTE2_WAVES : 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
   __shared__ SearchLds<CAP, TURN ? 1 : (WIDE ? 2 : 0)> Ls[G];
 #ifdef OTR_NO_SINK
@@ -1429,13 +1433,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   if (!LIST) {  // the first tier: one unit per block, XCD-mapped (no loop: fewer live registers)
     const int64_t n_units = (a.n_tasks + G - 1) / G;
     const int64_t w = xcd_remap(blockIdx.x, (n_units + 7) / 8);
-    if (w < n_units) route_unit<CAP, G, LIST, TURN, WIDE>(gr, a, counters, Ls, w, a.n_tasks, sink);
+    if (w < n_units) route_unit<CAP, G, LIST, TURN, WIDE, CNT>(gr, a, counters, Ls, w, a.n_tasks, sink);
     return;
   }
   const int64_t n_tasks = (int64_t)*a.list_count;
   const int64_t n_units = (n_tasks + G - 1) / G;
   for (int64_t w = blockIdx.x; w < n_units; w += gridDim.x) {
-    route_unit<CAP, G, LIST, TURN, WIDE>(gr, a, counters, Ls, w, n_tasks, sink);
+    route_unit<CAP, G, LIST, TURN, WIDE, CNT>(gr, a, counters, Ls, w, n_tasks, sink);
     __syncthreads();  // the next unit re-initialises the tables
   }
 }
@@ -1491,6 +1495,40 @@ __device__ inline void argmin_lane(double c, int j, double* oc, int* oj) {
 // instead of a chain of dependent global loads; other traces use the global copies.
 constexpr int kVitLds = 128;
 
+// One Viterbi step's min-plus scan for lane j < K: 16 independent transition loads in
+// flight per chunk, then ascending i (strict <: lowest index among equal minima).  The
+// array holds route lengths (u32 mm, half the bytes of a cost); the transition cost
+// (turn_cost + |route - gc|) / beta (K4) is evaluated here.  TURNS = false: the batch
+// mode has no turn costs, so the turn term (0) is not added.
+template <bool TURNS>
+__device__ __forceinline__ void vit_scan(const uint32_t* tr, const uint32_t* tcr, const double* s_cost, int Kp, int K,
+                                         int lane, double gcd, double inv_beta, double* best_io, int* bi_io) {
+  double best = *best_io;
+  int bi = *bi_io;
+  for (int i0 = 0; i0 < Kp; i0 += 16) {
+    uint32_t tv[16], tc[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) tv[u] = i0 + u < Kp ? tr[(int64_t)(i0 + u) * K + lane] : kNoRoute;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) tc[u] = (TURNS && i0 + u < Kp) ? tcr[(int64_t)(i0 + u) * K + lane] : 0u;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (tv[u] == kNoRoute) continue;
+      const double dg = fabs(div1000((double)tv[u]) - gcd);
+      const double ti = (TURNS ? div1000((double)tc[u]) + dg : dg) * inv_beta;
+      const double ci = s_cost[i0 + u];
+      if (ci == __builtin_huge_val()) continue;
+      const double c = ci + ti;
+      if (c < best) {
+        best = c;
+        bi = i0 + u;
+      }
+    }
+  }
+  *best_io = best;
+  *bi_io = bi;
+}
+
 __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long long* counters) {
   __shared__ double s_cost[OTR_KMAX];
   __shared__ int8_t s_bp[kVitLds][32];
@@ -1526,26 +1564,10 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
           const uint32_t* tr = a.trans + a.trans_off[s];
           const uint32_t* tcr = a.trans_tc + a.trans_off[s];
           const double gcd = a.g[s];
-          for (int i0 = 0; i0 < Kp; i0 += 16) {
-            uint32_t tv[16], tc[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) tv[u] = i0 + u < Kp ? tr[(int64_t)(i0 + u) * K + lane] : kNoRoute;
-#pragma unroll
-            for (int u = 0; u < 16; ++u) tc[u] = (turns && i0 + u < Kp) ? tcr[(int64_t)(i0 + u) * K + lane] : 0u;
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-              if (tv[u] == kNoRoute) continue;
-              // (turn_cost + |route - gc|) / beta; 0 + x == x exactly when there are no turn costs
-              const double ti = (div1000((double)tc[u]) + fabs(div1000((double)tv[u]) - gcd)) * inv_beta;
-              const double ci = s_cost[i0 + u];
-              if (ci == __builtin_huge_val()) continue;
-              const double c = ci + ti;
-              if (c < best) {
-                best = c;
-                bi = i0 + u;
-              }
-            }
-          }
+          // wave-uniform: without turn costs the 0 + x term is left out (0 + x == x exactly:
+          // same bits, five fp64 operations fewer per transition)
+          if (turns) vit_scan<true>(tr, tcr, s_cost, Kp, K, lane, gcd, inv_beta, &best, &bi);
+          else vit_scan<false>(tr, tcr, s_cost, Kp, K, lane, gcd, inv_beta, &best, &bi);
         }
         const bool any = __ballot(lane < K && bi >= 0) != 0ull;
         if (!any) {
