@@ -384,6 +384,7 @@ enum Slot {
   S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
+  S_CLEN, S_CAND_NROOT,
   S_NUM
 };
 
@@ -697,9 +698,32 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   tb(OTR_STAGE_LINK);
   k_link<<<grid_for(T, 4), 256, 0, stream>>>(b, mp, trace_state_off, state_probe, cb.count, sb);
   te(OTR_STAGE_LINK);
-  if (S > 0)
-    k_tasks<<<grid_for(S, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, nullptr,
-                                                nullptr, nullptr);
+  // K2b: per-state search inputs
+  PrepArgs pr{};
+  pr.n_states = S;
+  pr.prev = sb.prev;
+  pr.bound = sb.bound;
+  pr.cand_count = cb.count;
+  pr.cand_edge = cb.edge;
+  pr.cand_p = cb.p;
+  pr.state_probe = state_probe;
+  pr.lat = b.lat;
+  pr.lon = b.lon;
+  pr.radius = cb.radius;
+  pr.state_trace = state_trace;
+  pr.mode = b.mode;
+  pr.heur = need<Heur>(S_HEUR, S);
+  pr.cprep = need<uint4>(S_CPREP, (size_t)S * OTR_KMAX);
+  pr.cprep_t = need<uint2>(S_CPREP_T, (size_t)S * OTR_KMAX);
+  pr.clen = need<uint2>(S_CLEN, (size_t)S * OTR_KMAX);
+  pr.nroot = need<int32_t>(S_CAND_NROOT, S);
+  if (!pr.heur || !pr.cprep || !pr.cprep_t || !pr.clen || !pr.nroot) {
+    if (err) *err = "device allocation failed (prep)";
+    return OTR_DEVICE_ERROR;
+  }
+  if (S > 0) k_prep<<<grid_for(S, 4), 256, 0, stream>>>(g, pr);
+  // the step's task count: the distinct roots (k_prep) of the previous state's candidates
+  if (S > 0) k_ntask<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, pr.nroot, sb.ntask);
   if ((rc = scan(sb.ntask, task_off, S))) return rc;
   if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
   // OTR_ROUTE_STEP=1 (A/B knob, read per call): batches without turn-cost
@@ -766,28 +790,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ra.lon = b.lon;
   ra.radius = cb.radius;
   ra.bt = sb.bt;
-  // K2b: per-state search inputs
-  PrepArgs pr{};
-  pr.n_states = S;
-  pr.prev = sb.prev;
-  pr.bound = sb.bound;
-  pr.cand_count = cb.count;
-  pr.cand_edge = cb.edge;
-  pr.cand_p = cb.p;
-  pr.state_probe = state_probe;
-  pr.lat = b.lat;
-  pr.lon = b.lon;
-  pr.radius = cb.radius;
-  pr.state_trace = state_trace;
-  pr.mode = b.mode;
-  pr.heur = need<Heur>(S_HEUR, S);
-  pr.cprep = need<uint4>(S_CPREP, (size_t)S * OTR_KMAX);
-  pr.cprep_t = need<uint2>(S_CPREP_T, (size_t)S * OTR_KMAX);
-  if (!pr.heur || !pr.cprep || !pr.cprep_t) {
-    if (err) *err = "device allocation failed (prep)";
-    return OTR_DEVICE_ERROR;
-  }
-  if (S > 0) k_prep<<<grid_for(S, 4), 256, 0, stream>>>(g, pr);
   uint4* task_rec = need<uint4>(S_TASK_REC, 3 * (size_t)std::max<int64_t>(NT, 1));
   if (!task_rec) {
     if (err) *err = "device allocation failed (task records)";
@@ -802,6 +804,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ra.trans_tc = trans_tc;
   ra.cprep = pr.cprep;
   ra.cprep_t = pr.cprep_t;
+  ra.clen = pr.clen;
   ra.rec = task_rec;
   ra.delta = mp.delta;
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;

@@ -376,8 +376,9 @@ __global__ __launch_bounds__(256) void k_link(BatchDev b, ModeParams mp, const i
 
 // One search task per (step, distinct search root).  Labels are rooted (label 0) at
 // dst(e_i), so every source candidate whose edge ends at the same node shares the
-// search; the task carries the bit mask of those sources.  Pass 1 (task_off == null)
-// counts, pass 2 writes.
+// search; the task carries the bit mask of those sources.  The counts come from k_prep
+// (PrepArgs::nroot, per state) through k_ntask; task_off == null counts here instead (the
+// same number, a pass of its own).
 __global__ __launch_bounds__(256) void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* cand_count,
                                                const uint32_t* cand_edge, const uint32_t* edge_dst, int64_t* ntask,
                                                const int64_t* task_off, int64_t* task_state,
@@ -409,8 +410,10 @@ __global__ __launch_bounds__(256) void k_tasks(int64_t n_states, const int64_t* 
   }
   if (rep) {
     const int64_t o = task_off[s] + __popcll(reps & ((1ull << lane) - 1ull));
-    task_state[o] = s;
-    task_mask[o] = same;
+    if (o < task_off[s + 1]) {  // the count (k_prep's nroot) and this rule agree; never write past it
+      task_state[o] = s;
+      task_mask[o] = same;
+    }
   }
 }
 
@@ -1029,6 +1032,9 @@ struct PrepArgs {
   Heur* heur;     // [S]
   uint4* cprep;   // [S][OTR_KMAX]: {part(p), src(e), h(src(e)), part(1 - p)}
   uint2* cprep_t; // [S][OTR_KMAX]: {part_t(p), part_t(1 - p)}: the same parts of the edge's route time
+  uint2* clen;    // [S][OTR_KMAX]: {len_mm(e), route time(e)}: a same-edge transition's whole-edge terms
+  int32_t* nroot; // [S]: distinct end nodes dst(e) of the state's candidates = the search
+                  // tasks of the step leaving it
 };
 
 __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
@@ -1052,7 +1058,26 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
         make_uint4((uint32_t)part_mm(p, len), tn, H(ll.x, ll.y), (uint32_t)part_mm(1.0 - p, len));
     const uint32_t et = g.et(md)[e];
     a.cprep_t[s * OTR_KMAX + lane] = make_uint2((uint32_t)part_mm(p, et), (uint32_t)part_mm(1.0 - p, et));
+    a.clen[s * OTR_KMAX + lane] = make_uint2(len, et);
   }
+  // distinct search roots dst(e) (K <= OTR_KMAX: one candidate per lane): a lane is its
+  // root's first holder when no lower lane has the same root (k_tasks' rule)
+  const uint32_t root = lane < K ? g.edge_dst[a.cand_edge[s * OTR_KMAX + lane]] : 0xFFFFFFFFu;
+  bool first = lane < K;
+  for (int k = 0; k < K; ++k) {
+    const uint32_t rk = (uint32_t)__shfl((int)root, k);  // every lane takes part (source lane k active)
+    if (k < lane && rk == root) first = false;
+  }
+  const int nr = __popcll(__ballot(first));
+  if (lane == 0) a.nroot[s] = nr;
+}
+
+// search tasks of each step: one per distinct root among the previous state's candidates
+__global__ void k_ntask(int64_t n_states, const int64_t* prev, const int32_t* nroot, int64_t* ntask) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_states) return;
+  const int64_t sp = prev[s];  // -1: first state of a sub-trace, -2: no candidates (k_link)
+  ntask[s] = sp >= 0 ? nroot[sp] : 0;
 }
 
 // ------------------------------------------------------------------------------
@@ -1082,6 +1107,7 @@ struct RouteArgs {
   const Heur* heur;           // per state (k_prep)
   const uint4* cprep;         // per state candidate (k_prep)
   const uint2* cprep_t;       // per state candidate: route-time parts (k_prep)
+  const uint2* clen;          // per state candidate: {len_mm(e), route time(e)} (k_prep)
   const int32_t* bt;          // per state: the step's time bound (0.1 s), -1 none
   const uint4* rec;           // per task, 2 x uint4 (k_task_rec)
   const unsigned long long* list_count;  // retry tiers: length of task_list, on the device
@@ -1186,6 +1212,7 @@ __device__ inline int nth_set_bit(unsigned long long m, int q) {
   return __ffsll((long long)m) - 1;
 }
 
+
 // one unit = G search tasks of the wave (ordinal w of the task range or list).  TURN:
 // the batch has turn-cost modes, whose transition rows walk the routes (turn_walk); a
 // batch without them runs the kernel compiled without that code (its register budget
@@ -1194,7 +1221,7 @@ __device__ inline int nth_set_bit(unsigned long long m, int q) {
 template <int CAP, int G, bool LIST, bool TURN, bool WIDE = false, bool CNT = true>
 __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& a, unsigned long long* counters,
                                            SearchLds<CAP, TURN ? 1 : (WIDE ? 2 : 0)>* Ls, int64_t w, int64_t n_tasks,
-                                           uint32_t* sink) {
+                                           uint32_t* sink, uint4 (*trec)[3]) {
   constexpr int LM = TURN ? 1 : (WIDE ? 2 : 0);
   static_assert(!(TURN && WIDE), "turn-mode tables carry predecessor edges in the low word");
   using Gr = Grp<G>;
@@ -1212,7 +1239,15 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   {
     const uint4 r0 = have ? a.rec[3 * task] : make_uint4(0u, 0u, 0u, 0u);
     const uint4 r1 = have ? a.rec[3 * task + 1] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
-    hroot = have ? a.rec[3 * task + 2].x : 0u;
+    const uint4 r2 = have ? a.rec[3 * task + 2] : make_uint4(0u, 0u, 0u, 0u);
+    hroot = r2.x;
+    // the record, stashed in LDS for the transition rows (one LDS read after the search
+    // instead of an L2 round trip ahead of the rows' own loads)
+    if (lane == 0) {
+      trec[Gr::g()][0] = r0;
+      trec[Gr::g()][1] = r1;
+      trec[Gr::g()][2] = r2;
+    }
     const int64_t s = r0.x;
     const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
     const int64_t sp = r0.y;
@@ -1295,7 +1330,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   uint32_t t_first = kEmpty, t_c = 0;
   bool turn_task = false, tie = false, walked = false;
   if (have && (ok || forced)) {
-    const uint4 r0 = a.rec[3 * task], r1 = a.rec[3 * task + 1], r2 = a.rec[3 * task + 2];
+    const uint4 r0 = trec[Gr::g()][0], r1 = trec[Gr::g()][1], r2 = trec[Gr::g()][2];
     const int64_t s = r0.x;
     const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
     if (search) ntr = (uint32_t)Kb * (uint32_t)__popcll(mask);
@@ -1305,16 +1340,18 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     turn_task = TURN && !forced && ((r1.y >> 17) & 1u);
     uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
     // sources staged one per lane as in the setup: {index, edge, fraction, exit part mm,
-    // exit part time}, read by group shuffles in the row loop
+    // exit part time, edge length mm, edge time}, read by group shuffles in the row loop
     const int nsrc = __popcll(mask);
     const int iq = lane < nsrc ? nth_set_bit(mask, lane) : 0;
     uint32_t e_q = 0, w_q = 0, t_q = 0;
+    uint2 l_q = make_uint2(0u, 0u);
     double p_q = 0;
     if (lane < nsrc) {
       e_q = a.cand_edge[sp * OTR_KMAX + iq];
       p_q = a.cand_p[sp * OTR_KMAX + iq];
       w_q = a.cprep[sp * OTR_KMAX + iq].w;
       if (bt >= 0) t_q = a.cprep_t[sp * OTR_KMAX + iq].y;
+      l_q = a.clen[sp * OTR_KMAX + iq];
     }
     uint32_t ej = 0, tpt = 0;
     double pj = 0;
@@ -1325,7 +1362,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     }
     for (int q = 0; q < nsrc; ++q) {  // group-uniform trip count
       int i;
-      uint32_t ei, wi, ti;
+      uint32_t ei, wi, ti, li, lti;
       double pi;
       if (q < Gr::GL) {
         i = __shfl(iq, q, Gr::GL);
@@ -1333,20 +1370,25 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
         pi = __shfl(p_q, q, Gr::GL);
         wi = (uint32_t)__shfl((int)w_q, q, Gr::GL);
         ti = (uint32_t)__shfl((int)t_q, q, Gr::GL);
+        li = (uint32_t)__shfl((int)l_q.x, q, Gr::GL);
+        lti = (uint32_t)__shfl((int)l_q.y, q, Gr::GL);
       } else {  // more sources than lanes (K > 32 at G = 2): direct loads
         i = nth_set_bit(mask, q);
         ei = a.cand_edge[sp * OTR_KMAX + i];
         pi = a.cand_p[sp * OTR_KMAX + i];
         wi = a.cprep[sp * OTR_KMAX + i].w;
         ti = bt >= 0 ? a.cprep_t[sp * OTR_KMAX + i].y : 0u;
+        const uint2 l = a.clen[sp * OTR_KMAX + i];
+        li = l.x;
+        lti = l.y;
       }
       if (lane < Kb) {
         int64_t r = -1, rt = 0;
         if (forced) {
           r = -1;
         } else if (ej == ei && pj >= pi) {
-          r = part_mm(pj - pi, gr.len_mm[ei]);
-          if (bt >= 0) rt = part_mm(pj - pi, gr.et(md)[ei]);
+          r = part_mm(pj - pi, li);  // li = len_mm[ei], lti = et(md)[ei] (k_prep)
+          if (bt >= 0) rt = part_mm(pj - pi, lti);
         } else if (lab >= 0) {
           r = (int64_t)wi + K.d((uint64_t)lab) + tpart;
           if (bt >= 0) rt = (int64_t)ti + K.t((uint64_t)lab) + tpt;
@@ -1424,6 +1466,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
 template <int CAP, int G, bool LIST, bool TURN = false, bool WIDE = false, bool CNT = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR_ROUTE2_WAVES : 8, G == 2 ? OTR_ROUTE2_WAVES : 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
   __shared__ SearchLds<CAP, TURN ? 1 : (WIDE ? 2 : 0)> Ls[G];
+  __shared__ uint4 trec[G][3];  // each group's task record, for its transition rows
 #ifdef OTR_NO_SINK
   uint32_t* sink = nullptr;  // A/B build: the branching relax_one everywhere
 #else
@@ -1433,13 +1476,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   if (!LIST) {  // the first tier: one unit per block, XCD-mapped (no loop: fewer live registers)
     const int64_t n_units = (a.n_tasks + G - 1) / G;
     const int64_t w = xcd_remap(blockIdx.x, (n_units + 7) / 8);
-    if (w < n_units) route_unit<CAP, G, LIST, TURN, WIDE, CNT>(gr, a, counters, Ls, w, a.n_tasks, sink);
+    if (w < n_units) route_unit<CAP, G, LIST, TURN, WIDE, CNT>(gr, a, counters, Ls, w, a.n_tasks, sink, trec);
     return;
   }
   const int64_t n_tasks = (int64_t)*a.list_count;
   const int64_t n_units = (n_tasks + G - 1) / G;
   for (int64_t w = blockIdx.x; w < n_units; w += gridDim.x) {
-    route_unit<CAP, G, LIST, TURN, WIDE, CNT>(gr, a, counters, Ls, w, n_tasks, sink);
+    route_unit<CAP, G, LIST, TURN, WIDE, CNT>(gr, a, counters, Ls, w, n_tasks, sink, trec);
     __syncthreads();  // the next unit re-initialises the tables
   }
 }
