@@ -1008,7 +1008,17 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   va.winner = need<int32_t>(S_WINNER, S);
   va.subpath = need<int32_t>(S_SUBPATH, S);
   tb(OTR_STAGE_VITERBI);
-  k_viterbi<<<(unsigned)(T < 1048576 ? T : 1048576), 64, 0, stream>>>(va, d_counters);
+  {
+    // two traces per wave when no mode keeps more than 32 candidates (K <= 32 lanes)
+    bool k32 = true;
+    for (int m = 0; m < OTR_MODES; ++m) k32 = k32 && mp.m[m].kmax <= 32;
+    if (k32) {
+      const int64_t w = (T + 1) / 2;
+      k_viterbi<2><<<(unsigned)(w < 1048576 ? w : 1048576), 64, 0, stream>>>(va, d_counters);
+    } else {
+      k_viterbi<1><<<(unsigned)(T < 1048576 ? T : 1048576), 64, 0, stream>>>(va, d_counters);
+    }
+  }
   te(OTR_STAGE_VITERBI);
   // ---- K6: winner paths (step list, tiers and general fallback counted on the device)
   int64_t* path_off = need<int64_t>(S_PATH_OFF, S);

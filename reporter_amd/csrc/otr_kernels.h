@@ -1520,8 +1520,10 @@ __device__ inline double div1000(double x) {
   return __builtin_fma(e, 0.001, q0);
 }
 
+// lowest-index argmin over the GL lanes of my group (GL = 64 / G)
+template <int G>
 __device__ inline void argmin_lane(double c, int j, double* oc, int* oj) {
-  for (int off = 32; off > 0; off >>= 1) {
+  for (int off = OTR_WAVE / G / 2; off > 0; off >>= 1) {
     const double c2 = __shfl_xor(c, off);
     const int j2 = __shfl_xor(j, off);
     if (c2 < c || (c2 == c && j2 < j)) {
@@ -1534,32 +1536,49 @@ __device__ inline void argmin_lane(double c, int j, double* oc, int* oj) {
 }
 
 // Back-pointers, break flags and sub-path-end winners of a trace's states are also kept
-// in LDS (traces of up to kVitLds states, K <= 32) so the serial backtrack reads LDS
+// in LDS (traces of up to VitLds<G>::N states, K <= 32) so the serial backtrack reads LDS
 // instead of a chain of dependent global loads; other traces use the global copies.
-constexpr int kVitLds = 128;
+// G = 2 (every mode's max_candidates <= 32): two traces per wave, 32 lanes each, and a
+// table of 104 states per trace (7.6 KB per wave: five waves per SIMD, so a C2 batch's
+// 5,000 waves are resident at once instead of 10,000 one-trace waves in two rounds).
+template <int G>
+struct VitLds {
+  static constexpr int N = G == 1 ? 128 : 104;
+};
 
 // One Viterbi step's min-plus scan for lane j < K: 16 independent transition loads in
 // flight per chunk, then ascending i (strict <: lowest index among equal minima).  The
 // array holds route lengths (u32 mm, half the bytes of a cost); the transition cost
-// (turn_cost + |route - gc|) / beta (K4) is evaluated here.  TURNS = false: the batch
-// mode has no turn costs, so the turn term (0) is not added.
-template <bool TURNS>
-__device__ __forceinline__ void vit_scan(const uint32_t* tr, const uint32_t* tcr, const double* s_cost, int Kp, int K,
-                                         int lane, double gcd, double inv_beta, double* best_io, int* bi_io) {
+// (turn_cost + |route - gc|) / beta (K4) is evaluated here.  TURNS = false: no trace of
+// the wave has turn costs, so the turn term (0) is not added; TURNS = true: turn costs
+// are read where `turn` (my trace's mode has them) and are 0 otherwise (0 + x == x).
+// Kw: a wave-uniform bound >= Kp (the larger Kp of the wave's traces): the loads run
+// unconditionally at clamped rows (i < Kp), rows past Kp read as no route.  U loads in
+// flight per chunk.
+template <bool TURNS, int U = 16>
+__device__ __forceinline__ void vit_scan(const uint32_t* tr, const uint32_t* tcr, const double* s_cost, int Kp, int Kw,
+                                         int K, int lane, double gcd, double inv_beta, bool turn, double* best_io,
+                                         int* bi_io) {
   double best = *best_io;
   int bi = *bi_io;
-  for (int i0 = 0; i0 < Kp; i0 += 16) {
-    uint32_t tv[16], tc[16];
+  for (int i0 = 0; i0 < Kw; i0 += U) {
+    uint32_t tv[U], tc[U];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) tv[u] = i0 + u < Kp ? tr[(int64_t)(i0 + u) * K + lane] : kNoRoute;
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u < Kp ? i0 + u : Kp - 1;
+      tv[u] = tr[(int64_t)i * K + lane];
+    }
 #pragma unroll
-    for (int u = 0; u < 16; ++u) tc[u] = (TURNS && i0 + u < Kp) ? tcr[(int64_t)(i0 + u) * K + lane] : 0u;
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u < Kp ? i0 + u : Kp - 1;
+      tc[u] = (TURNS && turn) ? tcr[(int64_t)i * K + lane] : 0u;
+    }
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      if (tv[u] == kNoRoute) continue;
+    for (int u = 0; u < U; ++u) {
+      if (i0 + u >= Kp || tv[u] == kNoRoute) continue;
       const double dg = fabs(div1000((double)tv[u]) - gcd);
       const double ti = (TURNS ? div1000((double)tc[u]) + dg : dg) * inv_beta;
-      const double ci = s_cost[i0 + u];
+      const double ci = s_cost[i0 + u < Kp ? i0 + u : Kp - 1];
       if (ci == __builtin_huge_val()) continue;
       const double c = ci + ti;
       if (c < best) {
@@ -1572,47 +1591,66 @@ __device__ __forceinline__ void vit_scan(const uint32_t* tr, const uint32_t* tcr
   *bi_io = bi;
 }
 
+// One wave per G traces (group g = lane / GL), lane j = candidate j of the current state.
+// The state loop runs to the longer trace of the wave; every per-state decision is
+// group-uniform and the LDS hand-over of the state costs sits between two wave-uniform
+// barriers.
+template <int G>
 __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long long* counters) {
-  __shared__ double s_cost[OTR_KMAX];
-  __shared__ int8_t s_bp[kVitLds][32];
-  __shared__ int8_t s_brk[kVitLds];  // 1 break, 0 no break, -1 no candidates
-  __shared__ int8_t s_win[kVitLds];  // end_win of the states that end a sub-path
-  const int lane = threadIdx.x;
-  unsigned long long cells = 0;
-  for (int t = blockIdx.x; t < a.n_traces; t += gridDim.x) {
-    const int md = a.mode[t] < OTR_MODES ? a.mode[t] : 0;
+  constexpr int GL = OTR_WAVE / G;
+  constexpr int NL = VitLds<G>::N;
+  __shared__ double s_cost[G][OTR_KMAX / G];
+  __shared__ int8_t s_bp[G][NL][32];
+  __shared__ int8_t s_brk[G][NL];  // 1 break, 0 no break, -1 no candidates
+  __shared__ int8_t s_win[G][NL];  // end_win of the states that end a sub-path
+  const int gi = G == 1 ? 0 : (int)threadIdx.x / GL;
+  const int lane = G == 1 ? (int)threadIdx.x : (int)threadIdx.x % GL;
+  double* const cst = s_cost[gi];
+  for (int64_t tw = blockIdx.x; tw * G < a.n_traces; tw += gridDim.x) {
+    const int64_t t = tw * G + gi;
+    const bool have = t < a.n_traces;  // group-uniform
+    const int md = have && a.mode[t] < OTR_MODES ? a.mode[t] : 0;
     const double inv2s2 = a.inv2s2[md], inv_beta = a.inv_beta[md];
-    const bool turns = (a.turn_modes >> md) & 1u;  // wave-uniform
-    const int64_t so = a.trace_state_off[t], eo = a.trace_state_off[t + 1];
+    const bool turns = (a.turn_modes >> md) & 1u;  // group-uniform
+    // wave-uniform: does any trace of the wave have turn costs (one scan variant per wave)
+    const bool wturns = G == 1 ? turns : __ballot(turns) != 0ull;
+    const int64_t so = have ? a.trace_state_off[t] : 0, eo = have ? a.trace_state_off[t + 1] : 0;
+    int64_t len = eo - so;
+    if (G == 2) {  // the wave runs to its longer trace
+      const int64_t l0 = __builtin_amdgcn_readlane((int)len, 0), l1 = __builtin_amdgcn_readlane((int)len, 32);
+      len = l0 > l1 ? l0 : l1;
+    }
     int64_t prev_s = -1;
     int Kp = 0;
-    bool lds_ok = eo - so <= kVitLds;  // wave-uniform: every state cached (and K <= 32, below)
-    for (int64_t s = so; s < eo; ++s) {
-      const int K = a.cand_count[s];
-      if (lds_ok && lane == 0) s_brk[s - so] = -1;
-      if (K <= 0) continue;
-      lds_ok = lds_ok && K <= 32;
+    bool lds_ok = eo - so <= NL;  // group-uniform: every state cached (and K <= 32, below)
+    for (int64_t k = 0; k < len; ++k) {
+      const int Kw = G == 1 ? Kp : max(__builtin_amdgcn_readlane(Kp, 0), __builtin_amdgcn_readlane(Kp, 32));
+      const int64_t s = so + k;
+      const bool in = s < eo;
+      const int K = in ? a.cand_count[s] : 0;
+      if (in && lds_ok && lane == 0) s_brk[gi][k] = -1;
+      const bool act = in && K > 0;  // group-uniform (the state has candidates)
+      if (act) lds_ok = lds_ok && K <= 32;
       double emis = 0.0;
-      if (lane < K) emis = a.cand_sqd[s * OTR_KMAX + lane] * inv2s2;
+      if (act && lane < K) emis = a.cand_sqd[s * OTR_KMAX + lane] * inv2s2;
       double cost = __builtin_huge_val();
       int bi = -1;
       bool brk = prev_s < 0;
-      if (!brk) {
+      if (act && !brk) {
         double best = __builtin_huge_val();
         if (lane < K) {
-          // 16 independent transition loads in flight per chunk, then the min-plus scan in
-          // ascending i (strict <: lowest index among equal minima).  The array holds route
-          // lengths (u32 mm, half the bytes of a cost); the transition cost |route - g| / beta
-          // (K4) is evaluated here, with the same operations k_route used to apply.
+          // the array holds route lengths (u32 mm); the transition cost (turn_cost +
+          // |route - gc|) / beta (K4) is evaluated here.  Without turn costs (group-
+          // uniform) the 0 + x term is left out (0 + x == x exactly)
           const uint32_t* tr = a.trans + a.trans_off[s];
           const uint32_t* tcr = a.trans_tc + a.trans_off[s];
           const double gcd = a.g[s];
-          // wave-uniform: without turn costs the 0 + x term is left out (0 + x == x exactly:
-          // same bits, five fp64 operations fewer per transition)
-          if (turns) vit_scan<true>(tr, tcr, s_cost, Kp, K, lane, gcd, inv_beta, &best, &bi);
-          else vit_scan<false>(tr, tcr, s_cost, Kp, K, lane, gcd, inv_beta, &best, &bi);
+          // (G = 2: 8 loads in flight per chunk, so the kernel fits five waves per SIMD)
+          if (wturns) vit_scan<true, G == 1 ? 16 : 8>(tr, tcr, cst, Kp, Kw, K, lane, gcd, inv_beta, turns, &best, &bi);
+          else vit_scan<false, G == 1 ? 16 : 8>(tr, tcr, cst, Kp, Kw, K, lane, gcd, inv_beta, false, &best, &bi);
         }
-        const bool any = __ballot(lane < K && bi >= 0) != 0ull;
+        const unsigned long long am = __ballot(lane < K && bi >= 0);
+        const bool any = (G == 1 ? am : (am >> (GL * gi)) & ((1ull << GL) - 1ull)) != 0ull;
         if (!any) {
           brk = true;
           bi = -1;
@@ -1620,60 +1658,67 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
           cost = bi >= 0 ? best + emis : __builtin_huge_val();
         }
       }
-      if (brk) {
-        if (prev_s >= 0) {  // previous sub-path ends at prev_s
-          double mc;
-          int mj;
-          argmin_lane(lane < Kp ? s_cost[lane] : __builtin_huge_val(), lane < Kp ? lane : OTR_KMAX, &mc, &mj);
+      // a break ends the previous sub-path at prev_s: its winner = lowest-index argmin
+      double mc;
+      int mj;
+      argmin_lane<G>(lane < Kp ? cst[lane] : __builtin_huge_val(), lane < Kp ? lane : OTR_KMAX, &mc, &mj);
+      if (act && brk) {
+        if (prev_s >= 0) {
           if (lane == 0) a.end_win[prev_s] = mj;
-          if (lds_ok && lane == 0) s_win[prev_s - so] = (int8_t)mj;
+          if (lds_ok && lane == 0) s_win[gi][prev_s - so] = (int8_t)mj;
         }
         cost = emis;
         bi = -1;
       }
-      if (lane < K) a.bp[s * OTR_KMAX + lane] = (int8_t)bi;
-      if (lane == 0) a.brk[s] = brk ? 1 : 0;
-      if (lds_ok) {
-        if (lane < K) s_bp[s - so][lane] = (int8_t)bi;
-        if (lane == 0) s_brk[s - so] = brk ? 1 : 0;
+      if (act) {
+        if (lane < K) a.bp[s * OTR_KMAX + lane] = (int8_t)bi;
+        if (lane == 0) a.brk[s] = brk ? 1 : 0;
+        if (lds_ok) {
+          if (lane < K) s_bp[gi][k][lane] = (int8_t)bi;
+          if (lane == 0) s_brk[gi][k] = brk ? 1 : 0;
+        }
       }
       __syncthreads();
-      if (lane < K) s_cost[lane] = cost;
+      if (act && lane < K) cst[lane] = cost;
       __syncthreads();
-      prev_s = s;
-      Kp = K;
+      if (act) {
+        prev_s = s;
+        Kp = K;
+      }
     }
-    if (prev_s >= 0) {
+    {
       double mc;
       int mj;
-      argmin_lane(lane < Kp ? s_cost[lane] : __builtin_huge_val(), lane < Kp ? lane : OTR_KMAX, &mc, &mj);
-      if (lane == 0) a.end_win[prev_s] = mj;
-      if (lds_ok && lane == 0) s_win[prev_s - so] = (int8_t)mj;
+      argmin_lane<G>(lane < Kp ? cst[lane] : __builtin_huge_val(), lane < Kp ? lane : OTR_KMAX, &mc, &mj);
+      if (prev_s >= 0) {
+        if (lane == 0) a.end_win[prev_s] = mj;
+        if (lds_ok && lane == 0) s_win[gi][prev_s - so] = (int8_t)mj;
+      }
     }
     __syncthreads();
-    // backtrack (lane 0), then sub-path ordinals
-    if (lds_ok && lane == 0) {
+    // backtrack (lane 0 of each group), then sub-path ordinals
+    if (have && lds_ok && lane == 0) {
       int cur = -1;
       bool next_brk = true;  // "state after this one starts a sub-path" (true past the end)
       for (int64_t s = eo - 1; s >= so; --s) {
         const int k = (int)(s - so);
-        const int b = s_brk[k];
+        const int b = s_brk[gi][k];
         if (b < 0) {
           a.winner[s] = -1;
           continue;
         }
-        if (next_brk) cur = s_win[k];
+        if (next_brk) cur = s_win[gi][k];
         a.winner[s] = cur;
-        if (!b) cur = s_bp[k][cur];
+        if (!b) cur = s_bp[gi][k][cur];
         next_brk = b != 0;
       }
       int sp = -1;
       for (int64_t s = so; s < eo; ++s) {
-        const int b = s_brk[s - so];
+        const int b = s_brk[gi][s - so];
         sp += b > 0 ? 1 : 0;
         a.subpath[s] = b < 0 ? -1 : sp;
       }
-    } else if (lane == 0) {
+    } else if (have && lane == 0) {
       int cur = -1;
       bool next_brk = true;  // "state after this one starts a sub-path" (true past the end)
       for (int64_t s = eo - 1; s >= so; --s) {
@@ -1697,7 +1742,6 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
     }
     __syncthreads();
   }
-  (void)cells;
   (void)counters;
 }
 
