@@ -384,7 +384,7 @@ enum Slot {
   S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
-  S_CLEN, S_CAND_NROOT,
+  S_CLEN, S_CAND_NROOT, S_FLAGGED,
   S_NUM
 };
 
@@ -487,6 +487,28 @@ __global__ void k_collect_tier(int64_t n, int32_t* flag, uint32_t want, int64_t*
   const bool sel = f != 0 && ((want >> f) & 1u);
   if (sel) flag[i] = 0;
   block_append(sel, i, list, count);
+}
+
+// every task the first route tier flagged (overflow or general): the superset of what the
+// later tiers collect, so their collects scan this short list instead of every task
+__global__ void k_collect_flagged(int64_t n, const int32_t* flag, int64_t* list, unsigned long long* count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  block_append(i < n && flag[i] != 0, i, list, count);
+}
+
+// k_collect_tier over the device-counted task list cand[0..*n_cand): a fixed grid
+// strides over it (block-uniform trip count: block_append synchronises the block)
+__global__ void k_collect_tier_from(const int64_t* cand, const unsigned long long* n_cand, int32_t* flag,
+                                    uint32_t want, int64_t* list, unsigned long long* count) {
+  const int64_t n = (int64_t)*n_cand;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t task = i < n ? cand[i] : 0;
+    const int f = i < n ? flag[task] : 0;
+    const bool sel = f != 0 && ((want >> f) & 1u);
+    if (sel) flag[task] = 0;
+    block_append(sel, task, list, count);
+  }
 }
 
 // the same over a device-counted list (steps of the path stage): entries list_in[0..*n_in)
@@ -816,11 +838,16 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   // device-side counters of the retry lists: [0..7] route tiers, [8] general tier 1,
   // [9] general tier 2, [10] route tasks left unrouted, [11] steps, [12..15] path tiers,
   // [16] path general 1, [17] path general 2, [18] paths left, [19] general overflow
-  // count, [20] cap flag, [32..96) path bump cursors
+  // count, [20] cap flag, [24] tasks the first route tier flagged, [32..96) path bump cursors
   unsigned long long* cnt = need<unsigned long long>(S_MISC, 32 + kShards);
   HIPCHK(hipMemsetAsync(cnt, 0, 8 * (32 + kShards), stream));
   int64_t* list = need<int64_t>(S_LIST, std::max<int64_t>(NT, S));
   int64_t* fail_tasks = need<int64_t>(S_GFLAG, std::max<int64_t>(NT, 1));
+  int64_t* flagged = need<int64_t>(S_FLAGGED, std::max<int64_t>(NT, 1));
+  if (!list || !fail_tasks || !flagged) {
+    if (err) *err = "device allocation failed (retry lists)";
+    return OTR_DEVICE_ERROR;
+  }
   // general (global-memory) search slabs: allocated on first use, cleared once
   auto slabs = [&](int tier, GSlabs* out) -> int {
     GSlab& sl = gslab[tier];
@@ -925,9 +952,13 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // persistent grids: twice the resident waves of the widest tier (256 CUs x 4 SIMDs x
     // 8 waves), so no tier is starved; blocks past the list length exit at once
     const unsigned tgrid = 16384;
+    // the first tier's flagged tasks, once; every later collect scans only them
+    k_collect_flagged<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, flagged, cnt + 24);
+    constexpr unsigned kCollectGrid = 512;
     for (int tier = 0; tier < ntier; ++tier) {
       unsigned long long* c = cnt + tier;
-      k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, tier == 0 ? 0x2u : 0x6u, list + 0, c);
+      k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, tier == 0 ? 0x2u : 0x6u,
+                                                            list + 0, c);
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.list_count = c;
@@ -954,7 +985,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // (same labels); what outgrows it is flagged 3 again
     if (!turns) {
       unsigned long long* c = cnt + 7;
-      k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, 0x8u, list, c);
+      k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x8u, list, c);
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.list_count = c;
@@ -970,7 +1001,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // first on 32K-slot slabs, then what outgrew those on 1M-slot slabs
     for (int gt = 0; gt < 2; ++gt) {
       unsigned long long* c = cnt + 8 + gt;
-      k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, gt == 0 ? 0xEu : 0x2u, list, c);
+      k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, gt == 0 ? 0xEu : 0x2u, list,
+                                                            c);
       GSlabs gs2;
       if ((rc = slabs(gt, &gs2))) return rc;
       ga.mode = 0;
@@ -984,7 +1016,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       if (timing) (void)hipEventRecord(ev[24 + 2 * (6 + gt) + 1], stream);
     }
     // tasks still flagged (beyond a 1M-state slab): their traces get OTR_MATCH_ERROR
-    k_collect_tier<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, 0xEu, fail_tasks, cnt + 10);
+    k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0xEu, fail_tasks, cnt + 10);
     te(OTR_STAGE_ROUTE_BIG);
   }
   // ---- K5: Viterbi
