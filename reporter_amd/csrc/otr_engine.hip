@@ -743,7 +743,13 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     if (err) *err = "device allocation failed (prep)";
     return OTR_DEVICE_ERROR;
   }
-  if (S > 0) k_prep<<<grid_for(S, 4), 256, 0, stream>>>(g, pr);
+  // two states per wave when no mode keeps more than 32 candidates (K <= 32 lanes)
+  bool k32 = true;
+  for (int m = 0; m < OTR_MODES; ++m) k32 = k32 && mp.m[m].kmax <= 32;
+  if (S > 0) {
+    if (k32) k_prep<2><<<grid_for((S + 1) / 2, 4), 256, 0, stream>>>(g, pr);
+    else k_prep<1><<<grid_for(S, 4), 256, 0, stream>>>(g, pr);
+  }
   // the step's task count: the distinct roots (k_prep) of the previous state's candidates
   if (S > 0) k_ntask<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, pr.nroot, sb.ntask);
   if ((rc = scan(sb.ntask, task_off, S))) return rc;
@@ -781,9 +787,14 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     if (err) *err = "device allocation failed (transitions)";
     return OTR_DEVICE_ERROR;
   }
-  if (S > 0)
-    k_tasks<<<grid_for(S, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, task_off,
-                                                task_state, task_mask);
+  if (S > 0) {
+    if (k32)
+      k_tasks<2><<<grid_for((S + 1) / 2, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask,
+                                                               task_off, task_state, task_mask);
+    else
+      k_tasks<1><<<grid_for(S, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, task_off,
+                                                     task_state, task_mask);
+  }
   if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
   // turn cost tables of this batch's parameters (oracle orc_turn_table)
   int32_t* d_turn = need<int32_t>(S_TURN, 181 * OTR_MODES);
@@ -1042,8 +1053,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   tb(OTR_STAGE_VITERBI);
   {
     // two traces per wave when no mode keeps more than 32 candidates (K <= 32 lanes)
-    bool k32 = true;
-    for (int m = 0; m < OTR_MODES; ++m) k32 = k32 && mp.m[m].kmax <= 32;
     if (k32) {
       const int64_t w = (T + 1) / 2;
       k_viterbi<2><<<(unsigned)(w < 1048576 ? w : 1048576), 64, 0, stream>>>(va, d_counters);
@@ -1062,6 +1071,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     if (S > 0) k_step_list<<<grid_for(S, 1024), 1024, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, nsteps_d);
     int32_t* step_ovf = need<int32_t>(S_STEP_OVF, S + 1);
     int64_t capacity = kShards * ((int64_t)S * 24 / kShards + 1024);
+    bool paths_fit = S == 0;
     for (int attempt = 0; attempt < 8 && S > 0; ++attempt) {
       uint32_t* path = need<uint32_t>(S_PATH, capacity);
       if (!path || !step_ovf) {
@@ -1144,10 +1154,17 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       HIPCHK(hipMemcpyAsync(&capflag, cnt + 20, 8, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipMemcpyAsync(cur.data(), cnt + 32, 8 * kShards, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
-      if ((capflag & 0xFFFFFFFFu) == 0) break;  // every path fitted its region
+      if ((capflag & 0xFFFFFFFFu) == 0) {  // every path fitted its region
+        paths_fit = true;
+        break;
+      }
       unsigned long long mx = 0;
       for (auto c : cur) mx = c > mx ? c : mx;
       capacity = kShards * ((int64_t)mx + (int64_t)mx / 2 + 1024);  // grow and redo
+    }
+    if (!paths_fit) {  // (the capacity grows 1.5x past the largest shard: never seen)
+      if (err) *err = "winner paths did not fit the path buffer after 8 attempts";
+      return OTR_DEVICE_ERROR;
     }
   }
   // ---- K7: stitching, segments, report()

@@ -379,13 +379,28 @@ __global__ __launch_bounds__(256) void k_link(BatchDev b, ModeParams mp, const i
 // search; the task carries the bit mask of those sources.  The counts come from k_prep
 // (PrepArgs::nroot, per state) through k_ntask; task_off == null counts here instead (the
 // same number, a pass of its own).
+// my lane group's bits of a wave ballot, for kernels whose blocks hold several waves
+// (Grp<G> assumes one wave per block)
+template <int G>
+__device__ inline unsigned long long group_bits(unsigned long long m) {
+  if (G == 1) return m;
+  constexpr int GL = OTR_WAVE / G;
+  const int gi = (int)(threadIdx.x % OTR_WAVE) / GL;
+  return (m >> (GL * gi)) & ((1ull << GL) - 1ull);
+}
+
+// G states per wave (G = 2 when every mode keeps <= 32 candidates: lane groups of 32, half
+// the waves of this latency-bound kernel)
+template <int G>
 __global__ __launch_bounds__(256) void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* cand_count,
                                                const uint32_t* cand_edge, const uint32_t* edge_dst, int64_t* ntask,
                                                const int64_t* task_off, int64_t* task_state,
                                                unsigned long long* task_mask) {
-  // one wave per state, lane i = source candidate i of the previous state
-  const int64_t s = (int64_t)blockIdx.x * (blockDim.x / OTR_WAVE) + threadIdx.x / OTR_WAVE;
-  const int lane = threadIdx.x % OTR_WAVE;
+  // one lane group per state, lane i = source candidate i of the previous state
+  constexpr int GL = OTR_WAVE / G;
+  const int64_t s = ((int64_t)blockIdx.x * (blockDim.x / OTR_WAVE) + threadIdx.x / OTR_WAVE) * G +
+                    (threadIdx.x % OTR_WAVE) / GL;
+  const int lane = threadIdx.x % GL;
   if (s >= n_states) return;
   const int64_t sp = prev[s];
   if (sp < 0 || cand_count[s] <= 0) {
@@ -401,9 +416,9 @@ __global__ __launch_bounds__(256) void k_tasks(int64_t n_states, const int64_t* 
   // sources sharing my root, then: am I the lowest of them (the task's representative)?
   unsigned long long same = 0;
   for (int k = 0; k < Ka; ++k)
-    if ((uint32_t)__shfl((int)root, k) == root) same |= 1ull << k;
+    if ((uint32_t)__shfl((int)root, k, GL) == root) same |= 1ull << k;
   const bool rep = lane < Ka && (__ffsll((long long)same) - 1) == lane;
-  const unsigned long long reps = __ballot(rep);
+  const unsigned long long reps = group_bits<G>(__ballot(rep));
   if (!task_off) {
     if (lane == 0) ntask[s] = __popcll(reps);
     return;
@@ -1037,9 +1052,14 @@ struct PrepArgs {
                   // tasks of the step leaving it
 };
 
+// G states per wave (G = 2 when every mode keeps <= 32 candidates: lane groups of 32;
+// the kernel waits on dependent loads, so half the waves take about half the time)
+template <int G>
 __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
-  const int64_t s = (int64_t)blockIdx.x * (blockDim.x / OTR_WAVE) + threadIdx.x / OTR_WAVE;
-  const int lane = threadIdx.x % OTR_WAVE;
+  constexpr int GL = OTR_WAVE / G;
+  const int64_t s = ((int64_t)blockIdx.x * (blockDim.x / OTR_WAVE) + threadIdx.x / OTR_WAVE) * G +
+                    (threadIdx.x % OTR_WAVE) / GL;
+  const int lane = threadIdx.x % GL;
   if (s >= a.n_states) return;
   const int K = a.cand_count[s];
   if (K <= 0) return;
@@ -1065,10 +1085,10 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
   const uint32_t root = lane < K ? g.edge_dst[a.cand_edge[s * OTR_KMAX + lane]] : 0xFFFFFFFFu;
   bool first = lane < K;
   for (int k = 0; k < K; ++k) {
-    const uint32_t rk = (uint32_t)__shfl((int)root, k);  // every lane takes part (source lane k active)
+    const uint32_t rk = (uint32_t)__shfl((int)root, k, GL);  // every lane of the group takes part
     if (k < lane && rk == root) first = false;
   }
-  const int nr = __popcll(__ballot(first));
+  const int nr = __popcll(group_bits<G>(__ballot(first)));
   if (lane == 0) a.nroot[s] = nr;
 }
 
