@@ -783,17 +783,34 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   int32_t* task_ovf = need<int32_t>(S_TASK_OVF, NT);
   uint32_t* trans = need<uint32_t>(S_TRANS, NTR);
   uint32_t* trans_tc = need<uint32_t>(S_TRANS_TC, turn_modes ? NTR : 1);  // read for turn modes only
-  if (!task_state || !task_mask || !task_ovf || !trans || !trans_tc) {
+  uint4* task_rec = need<uint4>(S_TASK_REC, 3 * (size_t)std::max<int64_t>(NT, 1));
+  if (!task_state || !task_mask || !task_ovf || !trans || !trans_tc || !task_rec) {
     if (err) *err = "device allocation failed (transitions)";
     return OTR_DEVICE_ERROR;
   }
-  if (S > 0) {
-    if (k32)
-      k_tasks<2><<<grid_for((S + 1) / 2, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask,
-                                                               task_off, task_state, task_mask);
-    else
-      k_tasks<1><<<grid_for(S, 4), 256, 0, stream>>>(S, sb.prev, cb.count, cb.edge, g.edge_dst, sb.ntask, task_off,
-                                                     task_state, task_mask);
+  if (S > 0) {  // tasks and their records (K2 + K2c)
+    TaskArgs ta{};
+    ta.n_states = S;
+    ta.prev = sb.prev;
+    ta.cand_count = cb.count;
+    ta.cand_edge = cb.edge;
+    ta.edge_dst = g.edge_dst;
+    ta.node_ll = g.node_ll;
+    ta.task_off = task_off;
+    ta.bound = sb.bound;
+    ta.forced = sb.forced;
+    ta.bt = sb.bt;
+    ta.state_trace = state_trace;
+    ta.mode = b.mode;
+    ta.cprep = pr.cprep;
+    ta.heur = pr.heur;
+    ta.trans_off = trans_off;
+    ta.turn_modes = turn_modes;
+    ta.task_state = task_state;
+    ta.task_mask = task_mask;
+    ta.rec = task_rec;
+    if (k32) k_tasks<2><<<grid_for((S + 1) / 2, 4), 256, 0, stream>>>(ta);
+    else k_tasks<1><<<grid_for(S, 4), 256, 0, stream>>>(ta);
   }
   if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
   // turn cost tables of this batch's parameters (oracle orc_turn_table)
@@ -823,15 +840,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ra.lon = b.lon;
   ra.radius = cb.radius;
   ra.bt = sb.bt;
-  uint4* task_rec = need<uint4>(S_TASK_REC, 3 * (size_t)std::max<int64_t>(NT, 1));
-  if (!task_rec) {
-    if (err) *err = "device allocation failed (task records)";
-    return OTR_DEVICE_ERROR;
-  }
-  if (NT > 0)
-    k_task_rec<<<grid_for(NT, 256), 256, 0, stream>>>(NT, task_state, task_mask, sb.prev, sb.bound, sb.forced, cb.count,
-                                                      cb.edge, g.edge_dst, state_trace, b.mode, pr.cprep, sb.bt,
-                                                      turn_modes, pr.heur, g.node_ll, trans_off, task_rec);
   ra.heur = pr.heur;
   ra.turn = d_turn;
   ra.trans_tc = trans_tc;
@@ -842,7 +850,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ra.delta = mp.delta;
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
   ra.overflow_flag = task_ovf;
-  // bounds > 1.9 km skip the first tier (most outgrow 160 slots: C4 route 24 -> 15 ms)
+  // bounds > 1.9 km skip the first tier (most outgrow 160 slots: C4 route 24 -> 15 ms);
+  // 1.5 km: C4 6.99M -> 7.21M probes/s but C2 -1.6 % (its 1.5-1.9 km steps then retry)
   static const uint32_t direct_bmm =
       getenv("OTR_DIRECT_BMM") ? (uint32_t)strtoul(getenv("OTR_DIRECT_BMM"), nullptr, 10) : 1900000u;  // A/B knob
   ra.direct_bmm = direct_bmm;

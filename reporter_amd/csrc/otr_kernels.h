@@ -41,18 +41,27 @@ __global__ void k_select_states(BatchDev b, ModeParams mp, int64_t* state_cnt, c
   if (t >= b.n_traces) return;
   const int64_t lo = b.trace_off[t], hi = b.trace_off[t + 1];
   const MatchParams& P = mp.m[b.mode[t] < OTR_MODES ? b.mode[t] : 0];
-  int64_t cnt = 0, last = lo;
+  int64_t cnt = 0;
   int64_t base = state_off ? state_off[t] : 0;
+  // the last state's coordinates stay in registers and the next probe's are loaded one
+  // iteration ahead: the loop's only dependence is the distance test itself
+  double la_last = 0.0, lo_last = 0.0;
+  double la_n = lo < hi ? b.lat[lo] : 0.0, lo_n = lo < hi ? b.lon[lo] : 0.0;
   for (int64_t i = lo; i < hi; ++i) {
-    bool st = (i == lo || i == hi - 1) ||
-              gc_dist(b.lat[last], b.lon[last], b.lat[i], b.lon[i]) >= P.interpolation_distance;
+    const double la = la_n, lg = lo_n;
+    if (i + 1 < hi) {
+      la_n = b.lat[i + 1];
+      lo_n = b.lon[i + 1];
+    }
+    const bool st = (i == lo || i == hi - 1) || gc_dist(la_last, lo_last, la, lg) >= P.interpolation_distance;
     if (st) {
       if (state_off) {
         state_probe[base + cnt] = i;
         state_trace[base + cnt] = t;
       }
       ++cnt;
-      last = i;
+      la_last = la;
+      lo_last = lg;
     }
   }
   if (!state_off) state_cnt[t] = cnt;
@@ -387,49 +396,6 @@ __device__ inline unsigned long long group_bits(unsigned long long m) {
   constexpr int GL = OTR_WAVE / G;
   const int gi = (int)(threadIdx.x % OTR_WAVE) / GL;
   return (m >> (GL * gi)) & ((1ull << GL) - 1ull);
-}
-
-// G states per wave (G = 2 when every mode keeps <= 32 candidates: lane groups of 32, half
-// the waves of this latency-bound kernel)
-template <int G>
-__global__ __launch_bounds__(256) void k_tasks(int64_t n_states, const int64_t* prev, const int32_t* cand_count,
-                                               const uint32_t* cand_edge, const uint32_t* edge_dst, int64_t* ntask,
-                                               const int64_t* task_off, int64_t* task_state,
-                                               unsigned long long* task_mask) {
-  // one lane group per state, lane i = source candidate i of the previous state
-  constexpr int GL = OTR_WAVE / G;
-  const int64_t s = ((int64_t)blockIdx.x * (blockDim.x / OTR_WAVE) + threadIdx.x / OTR_WAVE) * G +
-                    (threadIdx.x % OTR_WAVE) / GL;
-  const int lane = threadIdx.x % GL;
-  if (s >= n_states) return;
-  const int64_t sp = prev[s];
-  if (sp < 0 || cand_count[s] <= 0) {
-    if (!task_off && lane == 0) ntask[s] = 0;
-    return;
-  }
-  const int Ka = cand_count[sp];
-  // sources share a task when their edges end at the same node: the node-based search
-  // serves them all (with turn costs too: only the first turn differs, k_route adds it;
-  // the edge-based fallback in k_general searches each source edge on its own)
-  const uint32_t ce = lane < Ka ? cand_edge[sp * OTR_KMAX + lane] : 0xFFFFFFFFu;
-  const uint32_t root = lane < Ka ? edge_dst[ce] : 0xFFFFFFFFu;
-  // sources sharing my root, then: am I the lowest of them (the task's representative)?
-  unsigned long long same = 0;
-  for (int k = 0; k < Ka; ++k)
-    if ((uint32_t)__shfl((int)root, k, GL) == root) same |= 1ull << k;
-  const bool rep = lane < Ka && (__ffsll((long long)same) - 1) == lane;
-  const unsigned long long reps = group_bits<G>(__ballot(rep));
-  if (!task_off) {
-    if (lane == 0) ntask[s] = __popcll(reps);
-    return;
-  }
-  if (rep) {
-    const int64_t o = task_off[s] + __popcll(reps & ((1ull << lane) - 1ull));
-    if (o < task_off[s + 1]) {  // the count (k_prep's nroot) and this rule agree; never write past it
-      task_state[o] = s;
-      task_mask[o] = same;
-    }
-  }
 }
 
 // ------------------------------------------------------------------------------
@@ -857,7 +823,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
   constexpr bool PRED = LM == 1;
   using W = typename LabelT<LM>::W;
   SearchLds<CAP, LM>& L = Ls[Gr::g()];
-  // h(root): given (k_task_rec), or from the root's coordinates
+  // h(root): given (the task record, k_tasks), or from the root's coordinates
   uint32_t hroot = hroot_in;
   if (hroot_in == 0xFFFFFFFFu) {
     const int2 sll = g.node_ll[active ? start : 0u];
@@ -1135,7 +1101,7 @@ struct RouteArgs {
   const uint2* cprep_t;       // per state candidate: route-time parts (k_prep)
   const uint2* clen;          // per state candidate: {len_mm(e), route time(e)} (k_prep)
   const int32_t* bt;          // per state: the step's time bound (0.1 s), -1 none
-  const uint4* rec;           // per task, 2 x uint4 (k_task_rec)
+  const uint4* rec;           // per task, 3 x uint4 (k_tasks)
   const unsigned long long* list_count;  // retry tiers: length of task_list, on the device
   const int32_t* turn;        // [OTR_MODES][181] turn cost tables (mm), turn modes only
   uint32_t* trans_tc;         // turn cost (mm) per transition, turn modes only
@@ -1145,52 +1111,90 @@ struct RouteArgs {
   uint32_t direct_bmm;        // first tier: bounds above this go straight to the retry tiers
 };
 
-// K2c: one record per search task with everything its setup and its transition rows
-// need that sits behind a chain of dependent loads (task → state → previous state →
-// first source edge → root node; mode through the trace): the search kernels read two
-// 16-B words instead of walking that chain twice (before and after the search).
+// k_tasks' inputs and outputs
+struct TaskArgs {
+  int64_t n_states;
+  const int64_t* prev;
+  const int32_t* cand_count;
+  const uint32_t* cand_edge;
+  const uint32_t* edge_dst;
+  const int2* node_ll;
+  const int64_t* task_off;    // exclusive offsets of each step's tasks (scan of k_ntask's counts)
+  const double* bound;
+  const uint8_t* forced;
+  const int32_t* bt;
+  const int32_t* state_trace;
+  const uint8_t* mode;
+  const uint4* cprep;         // k_prep
+  const Heur* heur;           // k_prep
+  const int64_t* trans_off;
+  uint32_t turn_modes;
+  int64_t* task_state;
+  unsigned long long* task_mask;
+  uint4* rec;                 // 3 per task (the K2c record, below)
+};
+
+// One lane group per step s (G states per wave: G = 2 when every mode keeps <= 32
+// candidates), lane i = source candidate i of the previous state: the sources whose edges
+// end at the same node share a task (the node-based search serves them all; with turn
+// costs too: only the first turn differs, k_route adds it; the edge-based fallback in
+// k_general searches each source edge on its own).  The task's representative (its
+// lowest source) writes task_state, task_mask and the task record k_route reads:
 //   rec[3t]   = {s, sp, root, bound_mm}
 //   rec[3t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16 | turn << 17, mask lo, mask hi}
 //   rec[3t+2] = {h(root), time bound bt, trans_off[s] lo, hi}
-// (h(root) here takes the root's coordinates, the search's first dependent global load,
-// off the search kernels' critical path)
 // general: the task runs in the global-memory search (a bound whose packed labels would
 // not fit 32 bits).  turn: the mode has turn costs (edge-based semantics): the LDS search
 // runs node-based and the transition rows walk the unique tight in-edges back to the
 // root to add the turns; a tie on the way sends the task to the global-memory search.
-__global__ void k_task_rec(int64_t n_tasks, const int64_t* task_state, const unsigned long long* task_mask,
-                           const int64_t* prev, const double* bound, const uint8_t* forced, const int32_t* cand_count,
-                           const uint32_t* cand_edge, const uint32_t* edge_dst, const int32_t* state_trace,
-                           const uint8_t* mode, const uint4* cprep, const int32_t* bt, uint32_t turn_modes,
-                           const Heur* heur, const int2* node_ll, const int64_t* trans_off, uint4* rec) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_tasks) return;
-  const int64_t s = task_state[t];
-  const unsigned long long mask = task_mask[t];
-  const int64_t sp = prev[s];
-  const int md = mode[state_trace[s]] < OTR_MODES ? mode[state_trace[s]] : 0;
-  const uint32_t root = edge_dst[cand_edge[sp * OTR_KMAX + (__ffsll((long long)mask) - 1)]];
+template <int G>
+__global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
+  constexpr int GL = OTR_WAVE / G;
+  const int64_t s = ((int64_t)blockIdx.x * (blockDim.x / OTR_WAVE) + threadIdx.x / OTR_WAVE) * G +
+                    (threadIdx.x % OTR_WAVE) / GL;
+  const int lane = threadIdx.x % GL;
+  if (s >= a.n_states) return;
+  const int64_t sp = a.prev[s];
+  if (sp < 0 || a.cand_count[s] <= 0) return;
+  const int Ka = a.cand_count[sp];
+  const uint32_t ce = lane < Ka ? a.cand_edge[sp * OTR_KMAX + lane] : 0xFFFFFFFFu;
+  const uint32_t root = lane < Ka ? a.edge_dst[ce] : 0xFFFFFFFFu;
+  const uint32_t w = lane < Ka ? a.cprep[sp * OTR_KMAX + lane].w : 0xFFFFFFFFu;  // exit part mm
+  // sources sharing my root, their smallest exit part, then: am I the lowest of them?
+  unsigned long long same = 0;
   uint32_t d0min = 0xFFFFFFFFu;
-  for (unsigned long long m = mask; m; m &= m - 1) {
-    const uint32_t d0 = cprep[sp * OTR_KMAX + (__ffsll((long long)m) - 1)].w;
-    d0min = d0 < d0min ? d0 : d0min;
+  for (int k = 0; k < Ka; ++k) {
+    const uint32_t rk = (uint32_t)__shfl((int)root, k, GL), wk = (uint32_t)__shfl((int)w, k, GL);
+    if (rk == root) {
+      same |= 1ull << k;
+      d0min = wk < d0min ? wk : d0min;
+    }
   }
-  const uint32_t bmm = (uint32_t)bound_mm_of(bound[s]);
-  const uint32_t sh = pack_shift(bt[s]);
+  const bool rep = lane < Ka && (__ffsll((long long)same) - 1) == lane;
+  const unsigned long long reps = group_bits<G>(__ballot(rep));
+  if (!rep) return;
+  const int64_t o = a.task_off[s] + __popcll(reps & ((1ull << lane) - 1ull));
+  if (o >= a.task_off[s + 1]) return;  // the count (k_prep's nroot) and this rule agree; never write past it
+  a.task_state[o] = s;
+  a.task_mask[o] = same;
+  const int md = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+  const uint32_t bmm = (uint32_t)bound_mm_of(a.bound[s]);
+  const int32_t bt = a.bt[s];
+  const uint32_t sh = pack_shift(bt);
 #ifdef OTR_FORCE_GENERAL
   const bool general = true;  // test build: every search in k_general (tests/test_gpu_tiers.py)
 #else
   const bool general = !pack_fits(bmm, sh);
 #endif
-  const uint32_t turn = (turn_modes >> md) & 1u;
-  const uint32_t meta = (uint32_t)cand_count[s] | ((uint32_t)md << 8) | ((forced[s] ? 1u : 0u) << 10) | (sh << 11) |
-                        ((general ? 1u : 0u) << 16) | (turn << 17);
-  const int2 rll = node_ll[root];
-  const uint32_t hroot = heur[s](rll.x, rll.y);
-  const int64_t to = trans_off[s];
-  rec[3 * t] = make_uint4((uint32_t)s, (uint32_t)sp, root, bmm);
-  rec[3 * t + 1] = make_uint4(d0min, meta, (uint32_t)mask, (uint32_t)(mask >> 32));
-  rec[3 * t + 2] = make_uint4(hroot, (uint32_t)bt[s], (uint32_t)to, (uint32_t)((uint64_t)to >> 32));
+  const uint32_t turn = (a.turn_modes >> md) & 1u;
+  const uint32_t meta = (uint32_t)a.cand_count[s] | ((uint32_t)md << 8) | ((a.forced[s] ? 1u : 0u) << 10) |
+                        (sh << 11) | ((general ? 1u : 0u) << 16) | (turn << 17);
+  const int2 rll = a.node_ll[root];
+  const uint32_t hroot = a.heur[s](rll.x, rll.y);  // the search's first dependent load, done here
+  const int64_t to = a.trans_off[s];
+  a.rec[3 * o] = make_uint4((uint32_t)s, (uint32_t)sp, root, bmm);
+  a.rec[3 * o + 1] = make_uint4(d0min, meta, (uint32_t)same, (uint32_t)(same >> 32));
+  a.rec[3 * o + 2] = make_uint4(hroot, (uint32_t)bt, (uint32_t)to, (uint32_t)((uint64_t)to >> 32));
 }
 
 #ifndef OTR_ROUTE2_WAVES
