@@ -1118,6 +1118,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       pa.capacity = capacity;
       pa.overflow_flag = step_ovf;
       pa.cap_flag = (int32_t*)(cnt + 20);
+      pa.cand_count = cb.count;
+      pa.trans_off = trans_off;
+      pa.trans = trans;
       tb(OTR_STAGE_PATHS);
       {
         const int64_t units = (S + 1) / 2;  // upper bound: two searches per wave

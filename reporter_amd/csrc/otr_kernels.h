@@ -1809,6 +1809,9 @@ struct PathArgs {
   int64_t capacity;
   int32_t* overflow_flag;      // per step index: 1 table overflow, 3 global-memory search
   int32_t* cap_flag;           // global: path buffer too small
+  const int32_t* cand_count;
+  const int64_t* trans_off;    // the route lengths k_route found (u32 mm per transition)
+  const uint32_t* trans;
 };
 
 // G searches per wave (G = 2 for the first tier, lanes split 32/32), each a
@@ -1843,6 +1846,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
     const double pi = a.cand_p[sp * OTR_KMAX + wi], pj = a.cand_p[s * OTR_KMAX + wj];
     mode = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
     bmm = (uint32_t)bound_mm_of(a.bound[s]);
+    // the winning transition's route (mm, k_route) bounds the search instead of the step's
+    // bound: every node of the route and every in-edge achieving a node's label lies within
+    // it, so labels, predecessor edges and tie bits along the route are unchanged, while
+    // nothing beyond the route's length is relaxed
+    {
+      const uint32_t r = a.trans[a.trans_off[s] + (int64_t)wi * a.cand_count[s] + wj];
+      if (r < bmm) bmm = r;
+    }
     K.sh = pack_shift(a.bt[s]);
     if (ej == ei && pj >= pi) {
       if (gl == 0) a.path_len[s] = -1;
@@ -1876,11 +1887,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
     if (gl == 0) a.overflow_flag[k] = 1;
     active = false;
   }
-  // walk predecessor edges T → S (the group's lane 0), staging the edges in LDS
-  static_assert(sizeof(L.pend) + sizeof(L.work) >= 4 * CAP, "path staging reuses pend + work");
+  // walk predecessor edges T → S (the group's lane 0).  The predecessor node of every
+  // labelled slot, src(pred edge), is loaded first by all lanes in parallel (one memory
+  // latency instead of one per path edge), into the pend + work area (>= CAP u32); the
+  // walks then stay in LDS: one to count the edges, one to store them in path order.
+  static_assert(sizeof(L.pend) + sizeof(L.work) >= 4 * CAP, "predecessor nodes reuse pend + work");
   using PL = SearchLds<CAP, true>;
   static_assert(offsetof(PL, work) == offsetof(PL, pend) + sizeof(L.pend), "pend and work are contiguous");
-  uint32_t* lp = reinterpret_cast<uint32_t*>(L.pend);  // pend+work are contiguous: >= CAP u32
+  uint32_t* pn = reinterpret_cast<uint32_t*>(L.pend);  // pend+work are contiguous: >= CAP u32
+  constexpr int kPer = (CAP + Gr::GL - 1) / Gr::GL;
+  if (active) {
+    for (int r0 = 0; r0 < kPer; r0 += 8) {  // 8 loads in flight per lane
+      uint32_t u[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int q = gl + (r0 + r) * Gr::GL;
+        u[r] = kEmpty;
+        if (q < CAP && L.key[q] != kEmpty) {
+          const uint32_t e = (uint32_t)(L.lab[q] & 0xFFFFFFFFull);
+          if (e != kEmpty) u[r] = gr.edge_src[e];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (gl + (r0 + r) * Gr::GL < CAP) pn[gl + (r0 + r) * Gr::GL] = u[r];
+    }
+  }
+  __syncthreads();
   int n = 0;
   if (active && gl == 0) {
     uint32_t v = T;
@@ -1895,12 +1928,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
         n = -2;  // a tie the turn costs decide: the edge-based search
         break;
       }
-      lp[n++] = e;
-      v = gr.edge_src[e];
+      ++n;
+      v = pn[sv];
     }
   }
   n = __shfl(n, Gr::g() * Gr::GL);
-  __syncthreads();
   if (active && n < 0) {
     if (gl == 0) a.overflow_flag[k] = n == -2 ? 3 : 1;
     active = false;
@@ -1916,13 +1948,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
     if (gl == 0) *a.cap_flag = 1;
     active = false;
   }
-  if (active) {
+  if (active && gl == 0) {
     off += (int64_t)shard * region;
-    for (int q = gl; q < n; q += Gr::GL) a.path[off + q] = lp[n - 1 - q];
-    if (gl == 0) {
-      a.path_off[s] = off;
-      a.path_len[s] = n;
+    uint32_t v = T;
+    for (int q = n - 1; q >= 0; --q) {  // the same walk, storing S → T order
+      const int sv = lds_find(L, v);
+      a.path[off + q] = (uint32_t)(L.lab[sv] & 0xFFFFFFFFull);
+      v = pn[sv];
     }
+    a.path_off[s] = off;
+    a.path_len[s] = n;
   }
   __syncthreads();
   }
