@@ -95,3 +95,22 @@ def test_wide_label_tier_parity(graph_dir, matcher):
     errors, stats = compare(got, want)
     assert not errors, errors
     assert stats['n_seg'] > 0
+
+
+def test_more_than_32_candidates(graph_dir, matcher):
+    """max_candidates 64 with a 200 m radius: states keep more than 32 candidates, so the
+    one-state/one-trace-per-wave variants of k_prep, k_tasks and k_viterbi run (every
+    other case takes the two-per-wave kernels) and steps with K > 32 targets go to the
+    G = 1 route tiers; bit-exact with the oracle."""
+    over = {'search_radius': 200, 'max_search_radius': 200, 'max_candidates': 64, 'turn_penalty_factor': 0}
+    path = gen.graph_path('metro', graph_dir)
+    M.configure(M.default_config(path, **over))
+    traces = gen.make_traces(path, 30, 60, 30, 30.0, 9, 0.0, 0.0, 50.0)
+    got = matcher.match_batch_numpy(traces)
+    assert int(np.max(got['cand_count'])) > 32
+    prm = po.params(**{k: float(v) for k, v in over.items()})
+    want = po.match_batch(po.Graph(path), traces, prm, threads=8)
+    errors, stats = compare(got, want)
+    assert not errors, errors
+    assert stats['n_seg'] > 0
+    assert got['status'] == 0
