@@ -245,22 +245,27 @@ static int find_candidates(const orc_graph* g, double plat, double plon, double 
 /* ---------------------------------------------------------------------------- */
 /* bounded one-to-many routing (UPSTREAM meili routing.cc)     */
 /* ---------------------------------------------------------------------------- */
-/* Route labels are lexicographic keys (d, t, c): d = length in whole mm, t = route time
- * in 0.1 s (only while the step's time bound is active, else 0; saturating at
- * ORC_TCAP), c = accumulated turn cost in mm (only when the mode's turn_penalty_factor
- * is > 0, else 0; saturating at ORC_TCCAP).  Every component is an exact integer, so
- * the labels are the unique lexicographic shortest-path values whatever the order of
- * processing (the GPU's label-correcting search reaches the same fixed point). */
+/* A route label is (k, d, t): k = the search key = length + accumulated turn cost (mm;
+ * k = d when the mode has no turn costs), d = length in whole mm, t = route time in 0.1 s
+ * (tracked only while the step's time bound is active, else 0).  Labels are compared
+ * lexicographically on (k, d, t).  The search is label-setting in that order (UPSTREAM
+ * meili find_shortest_path: a priority queue on the distance-plus-turn sort cost), it
+ * starts at the source candidate with the exit part of its edge, and it PRUNES every
+ * relaxation whose route exceeds a bound: length > B_mm, time > bt (the step's
+ * max_route_time_factor bound), or turn cost > ORC_TCCAP.  A label is therefore the
+ * lexicographic minimum over the feasible offers of the FINAL labels of its
+ * predecessors — a unique fixed point (by induction on k: every step adds >= 1 mm), which
+ * the GPU's parallel search must reproduce exactly. */
 typedef struct {
-  int64_t d, t, c;
+  int64_t k, d, t;
 } rkey;
 
 static int rk_lt(rkey a, rkey b) {
+  if (a.k != b.k) return a.k < b.k;
   if (a.d != b.d) return a.d < b.d;
-  if (a.t != b.t) return a.t < b.t;
-  return a.c < b.c;
+  return a.t < b.t;
 }
-static int rk_eq(rkey a, rkey b) { return a.d == b.d && a.t == b.t && a.c == b.c; }
+static int rk_eq(rkey a, rkey b) { return a.k == b.k && a.d == b.d && a.t == b.t; }
 
 typedef struct {
   uint32_t* key;  /* node or edge id, UINT32_MAX empty */
@@ -311,9 +316,9 @@ static uint32_t nm_insert(nodemap_t* m, uint32_t k, int* isnew) {
     s = (s + 1) & (m->cap - 1);
   }
   m->key[s] = k;
+  m->lab[s].k = INT64_MAX;
   m->lab[s].d = INT64_MAX;
-  m->lab[s].t = 0;
-  m->lab[s].c = 0;
+  m->lab[s].t = INT64_MAX;
   m->done[s] = 0;
   m->n++;
   *isnew = 1;
@@ -430,37 +435,51 @@ typedef struct {
   int64_t bmm;      /* the distance bound, mm */
 } rctx;
 
+/* a label is feasible when its route keeps every bound (the search prunes the others) */
+static int feasible(const rctx* X, rkey L) {
+  return L.d <= X->bmm && (!X->time_on || L.t <= X->bt) && L.k - L.d <= ORC_TCCAP;
+}
+
+/* label L extended by edge e (and, with turn costs, by the turn from in-edge turn_from
+ * into e); `frac_mm`/`frac_t` >= 0 replace the whole edge by a part of it (a target's
+ * entry part) */
 static rkey step_key(const rctx* X, rkey L, uint32_t e, int turn_from /* in-edge or -1 */) {
   rkey k;
-  k.d = L.d + (int64_t)X->g->len_mm[e];
-  k.t = 0;
-  if (X->time_on) {
-    k.t = L.t + (int64_t)X->md->time_ds[e];
-    if (k.t > ORC_TCAP) k.t = ORC_TCAP;
-  }
-  k.c = 0;
-  if (X->md->turn_on && turn_from >= 0) {
-    k.c = L.c + X->md->turn[turn_degree(X->g, (uint32_t)turn_from, e)];
-    if (k.c > ORC_TCCAP) k.c = ORC_TCCAP;
-  }
+  const int64_t len = (int64_t)X->g->len_mm[e];
+  const int64_t c = (X->md->turn_on && turn_from >= 0) ? X->md->turn[turn_degree(X->g, (uint32_t)turn_from, e)] : 0;
+  k.d = L.d + len;
+  k.k = L.k + len + c;
+  k.t = X->time_on ? L.t + (int64_t)X->md->time_ds[e] : 0;
   return k;
 }
 
-/* Label-setting search (binary heap) over lexicographic keys, labels with d <= bmm.
- * Node mode (turn costs off): states are nodes, rooted at node `root` with label 0.
- * Edge mode (turn costs on): states are edges (arrived at dst(e) through e), rooted at
- * edge `root` with label 0; moving from a to b adds turn(a, b). */
-static void search(const rctx* X, uint32_t root, nodemap_t* m) {
+/* The source candidate's start label: the exit part of its edge (length, time) */
+static rkey start_key(const rctx* X, uint32_t ei, double pi) {
+  rkey L;
+  L.d = part_mm(1.0 - pi, X->g->len_mm[ei]);
+  L.k = L.d;
+  L.t = X->time_on ? part_mm(1.0 - pi, X->md->time_ds[ei]) : 0;
+  return L;
+}
+
+/* Label-setting search (binary heap, lexicographic (k, d, t)) from source candidate
+ * (ei, pi), pruning infeasible relaxations.  Node mode (turn costs off): states are
+ * nodes, the root node dst(ei) starts with the exit part.  Edge mode (turn costs on):
+ * states are edges (arrived at dst(e) through e), the root state is edge ei; moving from
+ * a to b adds turn(a, b). */
+static void search(const rctx* X, uint32_t ei, double pi, nodemap_t* m) {
   const orc_graph* g = X->g;
   const int edge_mode = X->md->turn_on;
   m->n = 0;
   memset(m->key, 0xFF, m->cap * sizeof(uint32_t));
+  const rkey L0 = start_key(X, ei, pi);
+  if (!feasible(X, L0)) return;
+  const uint32_t root = edge_mode ? ei : g->edge_dst[ei];
   heap_t hp = {0};
   int nw;
   uint32_t s = nm_insert(m, root, &nw);
-  const rkey zero = {0, 0, 0};
-  m->lab[s] = zero;
-  heap_item it0 = {zero, root};
+  m->lab[s] = L0;
+  heap_item it0 = {L0, root};
   hpush(&hp, it0);
   while (hp.n) {
     heap_item it = hpop(&hp);
@@ -472,7 +491,7 @@ static void search(const rctx* X, uint32_t root, nodemap_t* m) {
     for (uint32_t e = g->node_row[u]; e < g->node_row[u + 1]; ++e) {
       if (!(g->edge_attr[e] & X->md->mode_bit)) continue;
       const rkey k = step_key(X, L, e, edge_mode ? (int)it.id : -1);
-      if (k.d > X->bmm) continue;
+      if (!feasible(X, k)) continue; /* pruned during the search */
       const uint32_t id = edge_mode ? e : g->edge_dst[e];
       uint32_t sv = nm_insert(m, id, &nw);
       if (rk_lt(k, m->lab[sv])) {
@@ -485,36 +504,42 @@ static void search(const rctx* X, uint32_t root, nodemap_t* m) {
   free(hp.d);
 }
 
-/* Best label at the start node v = src(ej) of a target edge, with the turn into ej:
- * node mode: v's own label; edge mode: the lexicographic minimum over the labelled
- * in-edges a of v (and the root edge when it ends at v) of (d, t, c + turn(a, ej)),
- * smallest edge id among equals (*via).  Returns 0 when v was not reached. */
-static int target_key(const rctx* X, const nodemap_t* m, uint32_t root, uint32_t ej, rkey* out, uint32_t* via) {
+/* the entry part of target edge ej appended to label L (after the turn into ej) */
+static rkey entry_key(const rctx* X, rkey L, uint32_t ej, double pj, int64_t turn) {
+  rkey r;
+  const int64_t dp = part_mm(pj, X->g->len_mm[ej]);
+  r.d = L.d + dp;
+  r.k = L.k + turn + dp;
+  r.t = X->time_on ? L.t + part_mm(pj, X->md->time_ds[ej]) : 0;
+  return r;
+}
+
+/* Route to target (ej, pj) of the search rooted at source edge ei:
+ * the target is a state whose offers come from v = src(ej): node mode v's label; edge
+ * mode every labelled in-edge a of v with the turn (a, ej) — the lexicographic minimum
+ * over the FEASIBLE offers (entry part included), smallest a among equals (*via). */
+static int target_key(const rctx* X, const nodemap_t* m, uint32_t ej, double pj, rkey* out, uint32_t* via) {
   const orc_graph* g = X->g;
   const uint32_t v = g->edge_src[ej];
   if (!X->md->turn_on) {
-    if (v == root) {
-      const rkey z = {0, 0, 0};
-      *out = z;
-      return 1;
-    }
     uint32_t s = nm_find(m, v);
     if (s == 0xFFFFFFFFu) return 0;
-    *out = m->lab[s];
+    const rkey r = entry_key(X, m->lab[s], ej, pj, 0);
+    if (!feasible(X, r)) return 0;
+    *out = r;
     return 1;
   }
   int found = 0;
   rkey best = {0, 0, 0};
   uint32_t bid = 0xFFFFFFFFu;
-  for (uint32_t r = g->rev_row[v]; r < g->rev_row[v + 1]; ++r) {
-    const uint32_t a = g->rev_edge[r];
+  for (uint32_t q = g->rev_row[v]; q < g->rev_row[v + 1]; ++q) {
+    const uint32_t a = g->rev_edge[q];
     const uint32_t s = nm_find(m, a);
     if (s == 0xFFFFFFFFu) continue;
-    rkey k = m->lab[s];
-    k.c = k.c + X->md->turn[turn_degree(g, a, ej)];
-    if (k.c > ORC_TCCAP) k.c = ORC_TCCAP;
-    if (!found || rk_lt(k, best) || (rk_eq(k, best) && a < bid)) {
-      best = k;
+    const rkey r = entry_key(X, m->lab[s], ej, pj, X->md->turn[turn_degree(g, a, ej)]);
+    if (!feasible(X, r)) continue;
+    if (!found || rk_lt(r, best) || (rk_eq(r, best) && a < bid)) {
+      best = r;
       bid = a;
       found = 1;
     }
@@ -527,26 +552,21 @@ static int target_key(const rctx* X, const nodemap_t* m, uint32_t root, uint32_t
 }
 
 /* route of a transition: same edge forward: the part between the two
- * fractions; else exit part + label + entry part.  Returns 1 when valid (within the
- * distance bound and, when active, the time bound). */
-static int route_of(const rctx* X, const nodemap_t* m, uint32_t root, uint32_t ei, double pi, uint32_t ej, double pj,
+ * fractions (valid when within the bounds); else the target's label in the search from
+ * (ei, pi).  Returns 1 when a valid route exists. */
+static int route_of(const rctx* X, const nodemap_t* m, uint32_t ei, double pi, uint32_t ej, double pj,
                     rkey* out) {
   const orc_graph* g = X->g;
-  rkey r;
   if (ej == ei && pj >= pi) {
+    rkey r;
     r.d = part_mm(pj - pi, g->len_mm[ei]);
+    r.k = r.d;
     r.t = X->time_on ? part_mm(pj - pi, X->md->time_ds[ei]) : 0;
-    r.c = 0;
-  } else {
-    rkey L;
-    uint32_t via;
-    if (!target_key(X, m, root, ej, &L, &via)) return 0;
-    r.d = part_mm(1.0 - pi, g->len_mm[ei]) + L.d + part_mm(pj, g->len_mm[ej]);
-    r.t = X->time_on ? part_mm(1.0 - pi, X->md->time_ds[ei]) + L.t + part_mm(pj, X->md->time_ds[ej]) : 0;
-    r.c = L.c;
+    *out = r;
+    return feasible(X, r);
   }
-  *out = r;
-  return r.d <= X->bmm && (!X->time_on || r.t <= X->bt);
+  uint32_t via;
+  return target_key(X, m, ej, pj, out, &via);
 }
 
 /* the step's routing context: distance bound from the great-circle distance, time
@@ -570,15 +590,11 @@ static void step_ctx(rctx* X, const orc_graph* g, const mode_data* md, const orc
   }
 }
 
-/* the search root of a source candidate: its edge's end node, or the edge itself when
- * turn costs make the search edge-based */
-static uint32_t root_of(const rctx* X, uint32_t ei) { return X->md->turn_on ? ei : X->g->edge_dst[ei]; }
-
 /* winner path: edges strictly between ei and ej, walking back from ej
- * through the smallest-id in-edge (in-state) whose label plus the step is exactly the
- * label reached.  Appends to *path in travel order. */
+ * through the smallest-id in-edge (in-state) whose final label extended by the step is
+ * exactly the label reached.  Appends to *path in travel order. */
 typedef VEC(uint32_t) u32vec;
-static int walk_path(const rctx* X, const nodemap_t* m, uint32_t ei, uint32_t ej, u32vec* path) {
+static int walk_path(const rctx* X, const nodemap_t* m, uint32_t ei, uint32_t ej, double pj, u32vec* path) {
   const orc_graph* g = X->g;
   u32vec rev = {0};
   int ok = 1;
@@ -596,17 +612,9 @@ static int walk_path(const rctx* X, const nodemap_t* m, uint32_t ei, uint32_t ej
       for (uint32_t r = g->rev_row[v]; r < g->rev_row[v + 1]; ++r) {
         const uint32_t ed = g->rev_edge[r];
         if (!(g->edge_attr[ed] & X->md->mode_bit)) continue;
-        const uint32_t u = g->edge_src[ed];
-        rkey Lu;
-        if (u == S) {
-          const rkey z = {0, 0, 0};
-          Lu = z;
-        } else {
-          const uint32_t su = nm_find(m, u);
-          if (su == 0xFFFFFFFFu) continue;
-          Lu = m->lab[su];
-        }
-        if (rk_eq(step_key(X, Lu, ed, -1), Lv) && ed < best_e) best_e = ed;
+        const uint32_t su = nm_find(m, g->edge_src[ed]);
+        if (su == 0xFFFFFFFFu) continue;
+        if (rk_eq(step_key(X, m->lab[su], ed, -1), Lv) && ed < best_e) best_e = ed;
       }
       if (best_e == 0xFFFFFFFFu) {
         ok = 0;
@@ -618,7 +626,7 @@ static int walk_path(const rctx* X, const nodemap_t* m, uint32_t ei, uint32_t ej
   } else {
     rkey L;
     uint32_t a;
-    if (!target_key(X, m, ei, ej, &L, &a)) ok = 0;
+    if (!target_key(X, m, ej, pj, &L, &a)) ok = 0;
     while (ok && a != ei && rev.n <= g->h.n_edges) {
       VPUSH(rev, a);
       const uint32_t sa = nm_find(m, a);
@@ -666,14 +674,14 @@ int orc_route(const orc_graph* g, const orc_params* p, int mode, uint32_t src_ed
   step_ctx(&X, g, &md, &q, bound, dt_sec);
   nodemap_t m;
   nm_init(&m, 1024);
-  if (!(dst_edge == src_edge && dst_p >= src_p)) search(&X, root_of(&X, src_edge), &m);
+  if (!(dst_edge == src_edge && dst_p >= src_p)) search(&X, src_edge, src_p, &m);
   rkey r;
-  const int ok = route_of(&X, &m, root_of(&X, src_edge), src_edge, src_p, dst_edge, dst_p, &r);
+  const int ok = route_of(&X, &m, src_edge, src_p, dst_edge, dst_p, &r);
   nm_free(&m);
   free(md.time_ds);
   *out_dist = ok ? (double)r.d / 1000.0 : INFINITY;
   *out_time_ds = ok ? r.t : -1;
-  *out_turn_mm = ok ? r.c : -1;
+  *out_turn_mm = ok ? r.k - r.d : -1;
   return ok;
 }
 
@@ -892,24 +900,19 @@ static void match_trace(job_t* J, int32_t t) {
     int forced = gcd > P->breakage_distance;
     rctx X;
     step_ctx(&X, g, MD, P, gcd, tm[ib] - tm[ia]);
-    uint32_t searched = 0xFFFFFFFFu; /* labels rooted here are in nm */
     for (int i = 0; i < Ka; ++i) {
       for (int j = 0; j < Kb; ++j) trans[i * ORC_KMAX + j] = INFINITY;
       if (forced) continue;
       int need = 0;
       for (int j = 0; j < Kb; ++j)
         if (!(cb[j].e == ca[i].e && cb[j].p >= ca[i].p)) need = 1;
-      /* one search per root (node, or edge with turn costs): labels do not depend on
-       * the source's fraction along its edge */
-      const uint32_t root = root_of(&X, ca[i].e);
-      if (need && root != searched) {
-        searched = root;
-        search(&X, root, &nm);
-      }
+      /* one search per source candidate: its exit part counts toward the bounds that
+       * prune the search */
+      if (need) search(&X, ca[i].e, ca[i].p, &nm);
       for (int j = 0; j < Kb; ++j) {
         rkey r;
-        if (route_of(&X, &nm, root, ca[i].e, ca[i].p, cb[j].e, cb[j].p, &r))
-          trans[i * ORC_KMAX + j] = ((double)r.c / 1000.0 + fabs((double)r.d / 1000.0 - gcd)) * inv_beta;
+        if (route_of(&X, &nm, ca[i].e, ca[i].p, cb[j].e, cb[j].p, &r))
+          trans[i * ORC_KMAX + j] = ((double)(r.k - r.d) / 1000.0 + fabs((double)r.d / 1000.0 - gcd)) * inv_beta;
       }
     }
     int any = 0;
@@ -1003,9 +1006,9 @@ static void match_trace(job_t* J, int32_t t) {
         double gcd = gc_dist(lat[ia], lon[ia], lat[ib], lon[ib]);
         rctx X;
         step_ctx(&X, g, MD, P, gcd, tm[ib] - tm[ia]);
-        search(&X, root_of(&X, ci->e), &nm);
+        search(&X, ci->e, ci->p, &nm);
         u32vec path = {0};
-        walk_path(&X, &nm, ci->e, cj->e, &path); /* the winner's route is valid by construction */
+        walk_path(&X, &nm, ci->e, cj->e, cj->p, &path); /* the winner's route is valid by construction */
         for (size_t z = 0; z < path.n; ++z) {
           uint32_t ed = path.d[z];
           portion_t pp = {ed, 0, s, s + (int64_t)g->len_mm[ed]};

@@ -54,10 +54,11 @@ typedef struct orc_params {
 } orc_params;
 
 #define ORC_MODES 3
-#define ORC_MAX_BREAKAGE 30000.0     /* metres: route labels pack d in 25 bits of mm */
-#define ORC_TCAP 131071              /* route-time labels saturate here (0.1 s, 17 bits) */
-#define ORC_TB_MAX 131070            /* time bounds above this are not applied */
-#define ORC_TCCAP 4194303            /* turn-cost labels saturate here (mm, 22 bits) */
+#define ORC_MAX_BREAKAGE 30000.0     /* metres: route length <= 3e7 mm */
+#define ORC_TB_MAX 131070            /* time bounds above this are not applied (0.1 s; t < 2^17) */
+#define ORC_TCCAP 2097151            /* routes whose turn cost exceeds this are pruned (mm, 21 bits):
+                                        key = length + turn < 2^25, so (key, length, time) packs in
+                                        one 64-bit word on the GPU */
 
 typedef struct orc_graph orc_graph;
 
@@ -137,8 +138,10 @@ int orc_report(int32_t n, const uint8_t* has_id, const uint64_t* seg_id, const d
 
 /* One transition's route from candidate (src_edge, src_p) to (dst_edge, dst_p) under
  * the mode's parameters p: distance bound `bound` metres, time
- * bound from the probes' time difference dt_sec (<= 0: none).  Returns 1 and the route
- * length (m), time (0.1 s) and turn cost (mm) when valid, 0 when no valid route. */
+ * bound from the probes' time difference dt_sec (<= 0: none), both pruning the search.
+ * The route is the lexicographic minimum of (length + turn cost, length, time) over the
+ * search's labels.  Returns 1 and the route length (m), time (0.1 s) and turn cost (mm)
+ * when valid, 0 when no valid route. */
 int orc_route(const orc_graph* g, const orc_params* p, int mode, uint32_t src_edge, double src_p, uint32_t dst_edge,
               double dst_p, double bound, int64_t dt_sec, double* out_dist, int64_t* out_time_ds,
               int64_t* out_turn_mm);

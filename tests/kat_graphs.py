@@ -220,3 +220,93 @@ def queue_scenario():
     pts = [(30 + 20 * k, 3) for k in range(9)]        # x = 30..190, t = 0..16 s
     pts += [(201 + 2 * m, 3) for m in range(60)]      # x = 201..319, t = 18..136 s
     return pts
+
+
+def build_block(path):
+    """Turn costs against length (the route key is length + turn cost): a
+    two-way main street y = 0 with nodes P0 (-100, 0), R (-20, 0), P1 (0, 0), P2 (100, 0)
+    and a one-way block north of it, P1 -> Q1 (0, 20) -> Q0 (-20, 20) -> R, all 50 km/h,
+    level 1.  Eastbound at x = -10 to westbound at x = -40: the U-turn at P1 is 50 m long
+    with a 200 m turn (auto), the block is 90 m long with four 90-degree turns (4 x 27.067
+    m): under turn costs the longer block wins."""
+    nodes = [ll(-100, 0), ll(-20, 0), ll(0, 0), ll(100, 0), ll(0, 20), ll(-20, 20)]
+    P0, R, P1, P2, Q1, Q0 = range(6)
+    edges, ids = [], {}
+    ids['P0R>'], ids['P0R<'] = two_way(edges, P0, R, 81, level=1, speed=50)
+    ids['RP1>'], ids['RP1<'] = two_way(edges, R, P1, 81, level=1, speed=50)
+    ids['P1P2>'], ids['P1P2<'] = two_way(edges, P1, P2, 81, level=1, speed=50)
+    for name, a, b in (('P1Q1', P1, Q1), ('Q1Q0', Q1, Q0), ('Q0R', Q0, R)):
+        edges.append(dict(src=a, dst=b, way=82, level=1, speed=50))
+        ids[name] = len(edges) - 1
+    segs = [dict(id=osmlr(1, 402, 1), edges=[ids['P0R>'], ids['RP1>'], ids['P1P2>']]),
+            dict(id=osmlr(1, 402, 2), edges=[ids['P1P2<'], ids['RP1<'], ids['P0R<']])]
+    new = write_graph(path, nodes, edges, segs)
+    return {k: int(new[v]) for k, v in ids.items()}
+
+
+def block_trace():
+    """East past x = -10, then west at x = -40 (10 s apart: 90 m at 50 km/h is 6.5 s)."""
+    return [(-60, 2), (-10, 2), (-40, -2), (-80, -2)]
+
+
+def build_bypass(path):
+    """The time bound during the search: the road T0..T5 of build_slow
+    (the block T2-T3 at 5 km/h) plus a 50 km/h bypass T2 -> U2 (200, 50) -> U3 (300, 50)
+    -> T3 (one-way).  T1 at 0.5 -> T3 at 0.5 with a 40 s bound: the 200 m route through the
+    block takes 79.2 s and is pruned, the 300 m bypass (21.6 s) is the route."""
+    nodes = [ll(100 * k, 0) for k in range(6)] + [ll(200, 50), ll(300, 50)]
+    edges, ids = [], {}
+    for k in range(5):
+        sp = 5 if k == 2 else 50
+        ids['T%d>' % k], ids['T%d<' % k] = two_way(edges, k, k + 1, 50 + k, level=1, speed=sp)
+    for name, a, b in (('TU2', 2, 6), ('U2U3', 6, 7), ('U3T', 7, 3)):
+        edges.append(dict(src=a, dst=b, way=59, level=1, speed=50))
+        ids[name] = len(edges) - 1
+    segs = [dict(id=osmlr(1, 403, 1), edges=[ids['T%d>' % k] for k in range(5)])]
+    new = write_graph(path, nodes, edges, segs)
+    return {k: int(new[v]) for k, v in ids.items()}
+
+
+def bypass_trace():
+    """Eastbound at 15 m/s on the fast road, a probe every 20 s (x = 50, 150, 350, 450):
+    the step from x = 150 to x = 350 is only routable through the bypass."""
+    return [(50, 3), (150, 3), (350, 3), (450, 3)]
+
+
+def build_stale(path):
+    """A label the parallel search sets early and must withdraw: from S
+    (0, 0) to U (90, 0) a single 50 km/h edge whose stored length is 100 m (7.2 s), and a
+    chain of nine 10 m edges along the same line at 9 km/h (90 m, 36 s).  U -> V (190, 0)
+    is 100 m at 50 km/h (7.2 s), V -> Z (290, 0) continues.  Under a 40 s bound U's label
+    is the chain's (shorter) one, so V is out of time reach (43.2 s): a search that
+    relaxed U with the fast edge's label first must not keep V's label from it.  The
+    source road W (-100, 0) -> S, and a second road Y (0, -100) -> S so that candidates near
+    S share the search root with different exit times."""
+    nodes = [ll(0, 0), ll(90, 0), ll(190, 0), ll(290, 0), ll(-100, 0), ll(0, -100)]
+    S, U, V, Z, W, Y = range(6)
+    chain = []
+    for k in range(1, 9):
+        chain.append(len(nodes))
+        nodes.append(ll(10 * k, 0.0))
+    edges, ids = [], {}
+
+    def one(name, a, b, **kw):
+        edges.append(dict(src=a, dst=b, way=90 + len(ids), level=1, **kw))
+        ids[name] = len(edges) - 1
+    one('WS', W, S, speed=50)
+    one('YS', Y, S, speed=50)
+    one('SU', S, U, speed=50, length=100.0)
+    seq = [S] + chain + [U]
+    for k in range(9):
+        one('C%d' % k, seq[k], seq[k + 1], speed=9, length=10.0)
+    one('UV', U, V, speed=50)
+    one('VZ', V, Z, speed=50)
+    segs = [dict(id=osmlr(1, 404, 1), edges=[ids['UV'], ids['VZ']])]
+    new = write_graph(path, nodes, edges, segs)
+    return {k: int(new[v]) for k, v in ids.items()}
+
+
+def stale_traces():
+    """Probes 20 s apart: near S on W-S (and near the Y-S road), then on V-Z."""
+    return [[(-60, 2), (-3, 3), (230, 2), (270, 2)],
+            [(-60, 2), (-5, -2), (210, 2), (250, 2)]]

@@ -182,6 +182,87 @@ def test_equal_length_routes_decided_by_turns(square):
     assert ids['QT>'] in route and ids['PT>'] not in route
 
 
+# ---- the route key is length + turn cost; the bounds prune during the search ------------
+@pytest.fixture(scope='module')
+def block(graph_dir):
+    path = os.path.join(graph_dir, 'kat_block.otrg')
+    return path, K.build_block(path)
+
+
+@pytest.fixture(scope='module')
+def bypass(graph_dir):
+    path = os.path.join(graph_dir, 'kat_bypass.otrg')
+    return path, K.build_bypass(path)
+
+
+@pytest.fixture(scope='module')
+def stale(graph_dir):
+    path = os.path.join(graph_dir, 'kat_stale.otrg')
+    return path, K.build_stale(path)
+
+
+def test_turn_cost_detour_wins(block):
+    """A detour shorter than the turn penalty it avoids: eastbound at x = -10 to westbound
+    at x = -40.  The U-turn at P1 is 50 m with turn cost 200 m (+ 3.663 m straight on at R):
+    key 253.663 m; round the block it is 90 m with four 90-degree turns (4 x 27.067 m): key
+    198.268 m.  At the auto factor (200) the longer block is the route; with no turn costs
+    the 50 m U-turn is."""
+    path, ids = block
+    g = po.Graph(path)
+    tab = po.turn_table(po.params())
+    assert tab[90] == 27067 and tab[0] == 200000 and tab[180] == 3663
+    d, t, c = g.route(ids['RP1>'], 0.5, ids['P0R<'], 0.25, 1000.0, dt_sec=10, prm=po.params())
+    assert abs(d - 90.0) < 0.2 and c == 4 * tab[90]  # lengths from micro-degree nodes
+    d0, t0, c0 = g.route(ids['RP1>'], 0.5, ids['P0R<'], 0.25, 1000.0, dt_sec=10, prm=po.params(turn_penalty_factor=0))
+    assert abs(d0 - 50.0) < 0.2 and c0 == 0
+    # the matched trace takes the block under turn costs, the U-turn without them
+    b, r = _match(path, K.block_trace(), 10)
+    rt = [int(e) for e in r['route_edge']]
+    assert 0xFFFFFFFF not in rt
+    assert rt[rt.index(ids['RP1>']) + 1:rt.index(ids['RP1>']) + 4] == [ids['P1Q1'], ids['Q1Q0'], ids['Q0R']]
+    b, r0 = _match(path, K.block_trace(), 10, turn_penalty_factor=0)
+    rt0 = [int(e) for e in r0['route_edge']]
+    assert ids['P1Q1'] not in rt0 and ids['RP1<'] in rt0
+
+
+def test_time_bound_prunes_during_search(bypass):
+    """T1 at 0.5 -> T3 at 0.5: through the 5 km/h block 200 m in 79.2 s, round the bypass
+    300 m in 21.6 s.  With a 40 s bound (probes 20 s apart) the block's labels are pruned
+    while searching and the longer, faster bypass is the route; with an 80 s bound (or
+    none) the block is."""
+    path, ids = bypass
+    g = po.Graph(path)
+    prm = po.params(turn_penalty_factor=0)
+    d, t, c = g.route(ids['T1>'], 0.5, ids['T3>'], 0.5, 1000.0, dt_sec=20, prm=prm)
+    assert abs(d - 300.0) < 0.1 and t == 36 + 36 + 72 + 36 + 36
+    d, t, c = g.route(ids['T1>'], 0.5, ids['T3>'], 0.5, 1000.0, dt_sec=40, prm=prm)
+    assert abs(d - 200.0) < 0.1 and t == 792
+    d, t, c = g.route(ids['T1>'], 0.5, ids['T3>'], 0.5, 1000.0, dt_sec=0, prm=prm)
+    assert abs(d - 200.0) < 0.1 and t == 0
+    # matched: one sub-path through the bypass
+    b, r = _match(path, K.bypass_trace(), 20, turn_penalty_factor=0)
+    assert r['subpath'].max() == 0
+    rt = [int(e) for e in r['route_edge']]
+    k = rt.index(ids['TU2'])
+    assert rt[k - 1:k + 4] == [ids['T1>'], ids['TU2'], ids['U2U3'], ids['U3T'], ids['T3>']]
+    assert ids['T2>'] not in rt
+
+
+def test_label_setting_order_withdraws_fast_label(stale):
+    """Node labels follow the search key (length), so U's label is the 90 m chain's (36 s),
+    not the fast 100 m edge's (7.2 s): under a 40 s bound V (43.2 s through the chain) is out
+    of reach and the transition has no route; with a 60 s bound the chain route is valid,
+    and with no bound too."""
+    path, ids = stale
+    g = po.Graph(path)
+    prm = po.params(turn_penalty_factor=0)
+    assert g.route(ids['WS'], 0.97, ids['VZ'], 0.4, 2000.0, dt_sec=20, prm=prm) is None
+    d, t, c = g.route(ids['WS'], 0.97, ids['VZ'], 0.4, 2000.0, dt_sec=30, prm=prm)
+    assert abs(d - 233.0) < 0.1 and t == 2 + 9 * 40 + 72 + 29
+    d, t, c = g.route(ids['WS'], 0.97, ids['VZ'], 0.4, 2000.0, dt_sec=0, prm=prm)
+    assert abs(d - 233.0) < 0.1
+
+
 # ---- GPU parity on the same inputs -----------------------------------------------------
 @pytest.mark.gpu
 @pytest.mark.parametrize('opts', [{}, {'turn_penalty_factor': 0}, {'max_route_time_factor': 0}])
