@@ -52,19 +52,18 @@ def log(*a):
 
 
 def kernel_name(code, turns=False):
-    """rocprofv3 name of a route kernel (otr_batch_result.route_tier_code); turns: the
-    batch had turn-cost modes (the kernels compiled with the turn walk)."""
+    """rocprofv3 name of a route kernel (otr_batch_result.route_tier_code); turns: kept for
+    callers (turn-mode tasks run in the edge-state kernels, code 700,000 + CAP)."""
     if code < 0:  # the global-memory search: -1 on 32K-state slabs, -2 on 1M-state slabs
         return 'k_general' if code == -1 else 'k_general (1M-state slabs)'
+    if 700000 <= code < 800000:  # the edge-state tiers (turn costs): 700,000 + first CAP
+        return 'k_route_edge<%d>' % (code - 700000)
     # the timed launches run the LDS route kernels compiled without work counting (the
     # last template argument, CNT = false; the instrumented step runs CNT = true)
     if 900000 <= code < 1000000:  # the 64-bit label tier: 900,000 + CAP
-        return 'k_route<%d, 1, true, false, true, false>' % (code - 900000)
-    if code >= 1000000:  # the multi-root step kernel: 1,000,000 + CAP * 100 + RMAX
-        return 'k_route_step<%d, %d>' % ((code - 1000000) // 100, code % 100)
+        return 'k_route<%d, 1, true, true, false>' % (code - 900000)
     cap, g = code // 10, code % 10
-    return 'k_route<%d, %d, %s, %s, false, false>' % (cap, g, 'false' if code == 1602 or code == 2561 else 'true',
-                                                      'true' if turns else 'false')
+    return 'k_route<%d, %d, %s, false, false>' % (cap, g, 'false' if code == 1602 or code == 2561 else 'true')
 
 
 def route_bytes(work):
@@ -121,8 +120,10 @@ def main():
                     help='matchers (one HIP stream + host thread each) sharing the batch; 2 overlaps one '
                          "stream's host syncs and kernel tails with the other's kernels (+1.6%% at C2) but "
                          'the two route launches then share the GPU, halving the per-launch roofline figure')
-    ap.add_argument('--workload', choices=['c2', 'c3', 'c4', 'c5mix', 'c5'], default='c2',
-                    help='c2 (default, the headline): 100 probes @15 s, sigma 10 m; c3: the C3 shard of '
+    ap.add_argument('--workload', choices=['c2', 'c2dep', 'c3', 'c4', 'c5mix', 'c5'], default='c2',
+                    help='c2 (default, the headline): 100 probes @15 s, sigma 10 m; c2dep: the same traces '
+                         'matched with the deployed configuration only (what Batch.java requests get: mode '
+                         'defaults, turn penalties auto 200 / bicycle 140 / pedestrian 100); c3: the C3 shard of '
                          '1M veh%%07d uuids x 100 probes this GPU owns; c4: 60 probes @60 s, sigma 50 m, '
                          'accuracy 50 m, search radius 200 m; c5mix: C2 with the C5 mode mix '
                          '(60%% auto / 25%% bicycle / 15%% pedestrian) on the metro graph; c5: the country graph '
@@ -188,6 +189,10 @@ def main():
     gtt = {'turn_penalty_factor': 0, 'beta': 3, 'sigma_z': 4.07, 'breakage_distance': 2000}
     W = {'c2': dict(points=100, rate=15, sigma=10.0, seed=2, bike=0.0, ped=0.0, acc=None, traces=10000,
                     meili=dict(gtt, search_radius=50, gps_accuracy=16.45)),
+         # the deployed configuration (Dockerfile:14-17,42-49 + the per-mode defaults): a
+         # Batch.java request carries only mode and levels (Batch.java:56-65)
+         'c2dep': dict(points=100, rate=15, sigma=10.0, seed=2, bike=0.0, ped=0.0, acc=None, traces=10000,
+                       meili={}),
          'c3': dict(points=100, rate=15, sigma=10.0, seed=3, bike=0.0, ped=0.0, acc=None, traces=None,
                     meili=dict(gtt, search_radius=50, gps_accuracy=16.45)),
          'c4': dict(points=60, rate=60, sigma=50.0, seed=4, bike=0.0, ped=0.0, acc=50.0, traces=20000,
@@ -423,8 +428,8 @@ def main():
 
     # ---- rank 0, N = 1: oracle sample (CPU baseline) and its bit-exact comparison
     cpu, parity = None, None
-    n_cpu = args.cpu_traces if args.cpu_traces is not None else {'c2': 6000, 'c5mix': 6000, 'c4': 600, 'c5': 3000,
-                                                                 'c3': 6000}[args.workload]
+    n_cpu = args.cpu_traces if args.cpu_traces is not None else {'c2': 6000, 'c2dep': 2000, 'c5mix': 6000, 'c4': 600,
+                                                                 'c5': 3000, 'c3': 6000}[args.workload]
     if rank == 0 and world == 1 and n_cpu > 0:
         from oracle import pyoracle as po
         from oracle.compare import compare, subset
@@ -502,17 +507,20 @@ def main():
             'dtype': 'f64',
             'data': 'synthetic',
             'config': {'workload': '%s: %s street grid (%d nodes, %d directed edges, %d OSMLR segments), '
-                                   '%d traces x %d probes per GPU @%d s, sigma %g m%s; generate_test_trace '
-                                   'match_options, max_route_time_factor 2' % (
+                                   '%d traces x %d probes per GPU @%d s, sigma %g m%s; %s' % (
                                        args.workload.upper(), 'country' if gname == 'country' else 'metro', n_nodes,
                                        n_edges, n_segments, mine.n_traces,
                                        W['points'], W['rate'], W['sigma'],
                                        {'c2': '', 'c3': ', C3 uuid shard (1M veh%07d uuids, sha1[:3] % N)',
                                         'c4': ', accuracy 50 m, search radius 200 m',
                                         'c5mix': ', modes 60% auto / 25% bicycle / 15% pedestrian',
+                                        'c2dep': '',
                                         'c5': ', 1M veh%07d uuids sha1[:3] % 8 share over 24 h, modes 60% auto / '
                                               '25% bicycle / 15% pedestrian'}[
-                                           args.workload]),
+                                           args.workload],
+                                       'the deployed configuration (mode defaults: turn_penalty_factor auto 200, '
+                                       'max_route_time_factor 2)' if args.workload == 'c2dep' else
+                                       'generate_test_trace match_options, max_route_time_factor 2'),
                        'probes_per_step': int(total_probes),
                        'parallelism': ('uuid-sharded dp%d + ' % world + (
                            ('keyed (hour-tile, pair, speed) entries all-to-all to the tile owner over ' +

@@ -44,10 +44,9 @@ struct ModeParams {
 };
 
 // Route-label limits shared with the oracle (oracle/oracle.h ORC_*)
-constexpr double kMaxBreakage = 30000.0;  // metres: d fits 25 bits of mm in 64-bit labels
-constexpr uint32_t kTCap = 131071;        // route time saturates here (0.1 s, 17 bits)
-constexpr int64_t kTbMax = 131070;        // larger time bounds are not applied
-constexpr uint32_t kTcCap = 4194303;      // turn cost saturates here (mm, 22 bits)
+constexpr double kMaxBreakage = 30000.0;  // metres: route lengths <= 3e7 mm
+constexpr int64_t kTbMax = 131070;        // larger time bounds are not applied (route times < 2^17)
+constexpr uint32_t kTcCap = 2097151;      // routes whose turn cost exceeds this are pruned (mm, 21 bits)
 
 // the step's time bound in 0.1 s from the states' time difference, -1 = none (oracle step_ctx)
 __host__ __device__ inline int32_t time_bound_ds(const MatchParams& p, int64_t dt) {
@@ -89,6 +88,7 @@ struct DevGraph {
   const uint32_t* edge_t;      // [mode][edge]: route time, 0.1 s
   uint32_t adj_t_stride, edge_t_stride;  // elements per mode
   const short2* edge_head;     // per edge {begin heading, end heading}, integer degrees
+  const uint2* adj_e;          // 4 per node like adj: {edge id, begin heading | end heading << 16} (edge-state searches)
   uint32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double grid_min_lat, grid_min_lon, grid_cell_deg;
   __device__ const uint32_t* et(int mode) const { return edge_t + (size_t)mode * edge_t_stride; }

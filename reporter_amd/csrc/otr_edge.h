@@ -1,0 +1,579 @@
+// otr_edge.h — K3e/K6e: the edge-state route search in LDS, for modes with turn costs.
+//
+// With turn costs a route's key (length + turn cost) depends on the edge a
+// node is entered by, so the states of the search are edges: state b = "at dst(b), having
+// arrived through b".  The search is the node search of otr_kernels.h (search_run) over
+// those states — A* rounds on f = key + h(node), partition of the pending list, one lane
+// per (settled state, adjacency slot), LDS hash insert + 64-bit atomicMin — with:
+//   * 64-bit labels key << 38 | (kTcCap - turn) << 17 | time (otr_general.h gpack): the
+//     atomicMin keeps the lexicographic minimum of (key, length, time), the oracle's order;
+//   * the turn cost of every relaxation from the table of the mode, by the turn degree
+//     between the state's end heading (kept in the table) and the out-edge's begin heading
+//     (DevGraph::adj_e, loaded beside the adjacency record: no dependent load);
+//   * targets are not states: the target edge ej is entered from any state at src(ej), so
+//     every settled state at a target node offers to the target (with the turn into ej
+//     and the entry part) and the target keeps the lexicographic minimum offer (tlab);
+//   * two search frontiers: fmin over key + h orders the search and decides finality,
+//     dmin over length + h decides unreachability (the bounds are on the length);
+//   * the same pruning and stale test as search_run (time, length and turn cost all
+//     prune; a pruned re-relaxation whose head holds a label above the offer sends the
+//     task to the exact global-memory search).
+// One source edge per task (k_tasks), one search per wave (G = 1).
+#pragma once
+#include "otr_general.h"
+
+namespace otr {
+
+template <int CAP>
+struct EdgeLds {
+  static constexpr int WCAP = CAP <= 512 ? 64 : 128;
+  unsigned long long lab[CAP];   // gpack label, kGInf: none
+  uint32_t key[CAP];             // edge id | kInq | kRel, kEmpty
+  uint32_t node[CAP];            // dst(edge): where the state stands
+  uint16_t hv[CAP];              // hq_of(h(node))
+  uint16_t hend[CAP];            // end heading of the edge (the turn out of the state)
+  uint16_t pend[CAP];            // pending slots
+  uint16_t wslot[WCAP];          // this round's settled states: slot | again << 15
+  unsigned long long wlab[WCAP];  // ... and their labels
+  // targets (lanes of the wave): the best offer, entry parts, begin heading of ej
+  unsigned long long tlab[OTR_WAVE];
+  uint32_t tpart[OTR_WAVE], tpt[OTR_WAVE];
+  uint16_t thb[OTR_WAVE];
+  // target nodes src(ej) → lane masks (open addressing)
+  uint32_t tmap_node[OTR_WAVE];
+  unsigned long long tmap_mask[OTR_WAVE];
+  int n_pend, n_keys, overflow;
+};
+
+template <int CAP>
+__device__ inline int e_find(const EdgeLds<CAP>& L, uint32_t e) {
+  uint32_t h = hslot<CAP>(e);
+  for (int probe = 0; probe < CAP; ++probe) {
+    const uint32_t k = L.key[h];
+    if (k == kEmpty) return -1;
+    if ((k & kNodeMask) == e) return (int)h;
+    h = h + 1 == (uint32_t)CAP ? 0u : h + 1;
+  }
+  return -1;
+}
+
+template <int CAP>
+__device__ inline int e_insert(EdgeLds<CAP>& L, uint32_t e, bool* isnew) {
+  uint32_t h = hslot<CAP>(e);
+  for (int probe = 0; probe < CAP; ++probe) {
+    const uint32_t k = atomicCAS(&L.key[h], kEmpty, e);
+    if (k == kEmpty) {
+      *isnew = true;
+      return (int)h;
+    }
+    if ((k & kNodeMask) == e) {
+      *isnew = false;
+      return (int)h;
+    }
+    h = h + 1 == (uint32_t)CAP ? 0u : h + 1;
+  }
+  L.overflow = 1;
+  *isnew = false;
+  return -1;
+}
+
+__device__ inline uint32_t tmap_home(uint32_t v) { return (v * 0x9E3779B1u) >> 26; }  // 64 slots
+
+template <int CAP>
+__device__ inline unsigned long long tmap_get(const EdgeLds<CAP>& L, uint32_t v) {
+  uint32_t h = tmap_home(v);
+  for (int probe = 0; probe < OTR_WAVE; ++probe) {
+    const uint32_t k = L.tmap_node[h];
+    if (k == kEmpty) return 0ull;
+    if (k == v) return L.tmap_mask[h];
+    h = (h + 1) & (OTR_WAVE - 1);
+  }
+  return 0ull;
+}
+
+// an offer (relative key, length, time, turn) and its feasibility under the task's bounds
+struct EOffer {
+  uint32_t k, d, t, c;
+};
+__device__ inline bool e_feasible(const EOffer& o, uint32_t pd, uint32_t pt) {
+  return o.d <= pd && o.t <= pt && o.c <= kTcCap;
+}
+__device__ inline bool e_above(unsigned long long L, const EOffer& o) {
+  if (L == kGInf) return false;
+  const uint32_t k = g_k(L), d = g_d(L), t = g_t(L);
+  if (k != o.k) return k > o.k;
+  if (d != o.d) return d > o.d;
+  return t > o.t;
+}
+
+// Relax state (label lb, at node v, end heading ha) through the edge b (head w, length
+// len, time tt, begin / end headings hb / he, access in dw's high bits).  Returns the slot
+// when b became newly pending.
+template <int CAP>
+__device__ inline int e_relax(EdgeLds<CAP>& L, const Heur& H, const int32_t* turn, unsigned long long lb, uint32_t ha,
+                              uint32_t dw, uint32_t len, uint32_t tt, uint32_t b, uint32_t hb, uint32_t he,
+                              int32_t wlat, int32_t wlon, uint32_t pd, uint32_t pt, uint32_t mode_bit, bool again,
+                              uint32_t& relaxed, uint32_t& fnext, uint32_t& dnext, bool& isnew, bool& stale) {
+  isnew = false;
+  if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
+  ++relaxed;
+  EOffer o;
+  o.c = g_c(lb) + (uint32_t)turn[turn_degree((int)ha, (int)hb)];
+  o.d = g_d(lb) + len;
+  o.k = o.d + o.c;
+  o.t = g_t(lb) + tt;
+  if (!e_feasible(o, pd, pt)) {
+    if (again) {  // the stale test (relax_one): b holds a label above this pruned offer
+      const int sv = e_find(L, b);
+      if (sv >= 0 && e_above(L.lab[sv], o)) stale = true;
+    }
+    return -1;
+  }
+  const uint32_t w = dw & kAdjDstMask;
+  const uint32_t h = H(wlat, wlon);
+  const int sl = e_insert(L, b, &isnew);
+  if (sl < 0) return -1;
+  if (isnew) {
+    L.node[sl] = w;
+    L.hend[sl] = (uint16_t)he;
+    L.hv[sl] = hq_of(h);
+  }
+  const unsigned long long nw = gpack(o.k, o.c, o.t);
+  const unsigned long long old = atomicMin(&L.lab[sl], nw);
+  if (nw < old) {
+    const uint32_t f = o.k + h, fd = o.d + h;
+    fnext = f < fnext ? f : fnext;
+    dnext = fd < dnext ? fd : dnext;
+    const uint32_t was = atomicOr(&L.key[sl], kInq);
+    if (!(was & kInq)) return sl;
+  }
+  return -1;
+}
+
+// The settled state's offers to the targets at its node v (the turn into ej + the entry
+// part), kept as each target's lexicographic minimum.
+template <int CAP>
+__device__ inline void e_target_offers(EdgeLds<CAP>& L, const int32_t* turn, unsigned long long lb, uint32_t ha,
+                                       uint32_t v, uint32_t pd, uint32_t pt, bool again, bool& stale) {
+  unsigned long long m = tmap_get(L, v);
+  while (m) {
+    const int q = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    EOffer o;
+    o.c = g_c(lb) + (uint32_t)turn[turn_degree((int)ha, (int)L.thb[q])];
+    o.d = g_d(lb) + L.tpart[q];
+    o.k = o.d + o.c;
+    o.t = g_t(lb) + L.tpt[q];
+    if (e_feasible(o, pd, pt)) atomicMin(&L.tlab[q], gpack(o.k, o.c, o.t));
+    else if (again && e_above(L.tlab[q], o)) stale = true;
+  }
+}
+
+template <int CAP>
+__device__ inline void e_init(EdgeLds<CAP>& L) {
+  for (int k = threadIdx.x; k < CAP; k += OTR_WAVE) {
+    L.key[k] = kEmpty;
+    L.lab[k] = kGInf;
+  }
+  L.tlab[threadIdx.x] = kGInf;
+  L.tmap_node[threadIdx.x] = kEmpty;
+  L.tmap_mask[threadIdx.x] = 0ull;
+  if (threadIdx.x == 0) {
+    L.n_pend = 0;
+    L.n_keys = 0;
+    L.overflow = 0;
+  }
+  __syncthreads();
+}
+
+// One search (one wave) from root edge `root` (label 0 at dst(root) = rnode, end heading
+// rhe).  Lanes < n_tgt hold a target: node tv = src(ej), h(tv) hT, entry parts tpart /
+// tpt, begin heading thb.  pd / pt: the relative bounds.  Returns false on overflow;
+// *stale as in search_run.  timed = false: route times are not tracked (pt unused).
+template <int CAP>
+__device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const Heur& H, const int32_t* turn, int md,
+                            bool active, uint32_t root, uint32_t rnode, uint32_t rhe, uint32_t hroot, uint32_t pd,
+                            uint32_t pt, bool timed, uint32_t delta_mm, int n_tgt, uint32_t tv, uint32_t hT,
+                            uint32_t tpart, uint32_t tpt, uint32_t thb, bool* stale_out, unsigned long long* settled,
+                            unsigned long long* relaxed) {
+  constexpr int kMaxKeys = (CAP * 7) / 8;
+  constexpr int WCAP = EdgeLds<CAP>::WCAP;
+  const int gl = (int)threadIdx.x;
+  const uint32_t mode_bit = 1u << md;
+  const uint32_t* adjt = g.adj_t + (size_t)md * g.adj_t_stride;
+  const uint32_t* et = g.et(md);
+  if (!timed) pt = 0xFFFFFFFFu;
+  // targets
+  const bool tgt = active && gl < n_tgt && tv != kEmpty;
+  if (tgt) {
+    L.tpart[gl] = tpart;
+    L.tpt[gl] = timed ? tpt : 0u;
+    L.thb[gl] = (uint16_t)thb;
+    uint32_t h = tmap_home(tv);
+    for (int probe = 0; probe < OTR_WAVE; ++probe) {
+      const uint32_t k = atomicCAS(&L.tmap_node[h], kEmpty, tv);
+      if (k == kEmpty || k == tv) {
+        atomicOr(&L.tmap_mask[h], 1ull << gl);
+        break;
+      }
+      h = (h + 1) & (OTR_WAVE - 1);
+    }
+  }
+  if (active && gl == 0) {
+    bool isnew;
+    const int sl = e_insert(L, root, &isnew);
+    L.node[sl] = rnode;
+    L.hend[sl] = (uint16_t)rhe;
+    L.hv[sl] = hq_of(hroot);
+    L.lab[sl] = gpack(0u, 0u, 0u);
+    L.key[sl] |= kInq;
+    L.pend[0] = (uint16_t)sl;
+  }
+  __syncthreads();
+  uint32_t my_settled = 0, my_relaxed = 0;
+  bool stale = false;
+  uint32_t fmin = hroot, dmin = hroot;
+  const uint32_t hTm = hT + H.margin;
+  bool done = !active;
+  int npend = active ? 1 : 0;
+  int nkeys = active ? 1 : 0;
+  for (;;) {
+    const int np = done ? 0 : npend;
+    bool res = true;
+    if (!done && tgt && np > 0) {
+      const unsigned long long tl = L.tlab[gl];
+      if (tl != kGInf) res = (int64_t)g_k(tl) + (int64_t)hTm < (int64_t)fmin;  // final
+      else res = (int64_t)dmin - (int64_t)hTm + (int64_t)tpart > (int64_t)pd;  // no feasible offer can come
+    }
+    done = done || __ballot(!res) == 0ull || np == 0;
+    if (__builtin_amdgcn_readfirstlane((int)done)) break;
+    const uint32_t theta = fmin + delta_mm < fmin ? 0xFFFFFFFFu : fmin + delta_mm;
+    uint32_t fnext = 0xFFFFFFFFu, dnext = 0xFFFFFFFFu;
+    int kept = 0, nw = 0;
+    for (int base = 0; base < np; base += OTR_WAVE) {
+      const int k = base + gl;
+      const bool in = k < np;
+      int sl = 0;
+      uint32_t f = 0, fd = 0, key = 0;
+      unsigned long long lb = 0;
+      bool take = false;
+      if (in) {
+        sl = L.pend[k];
+        lb = L.lab[sl];
+        key = L.key[sl];
+        const uint32_t hq = (uint32_t)L.hv[sl] << 6;
+        f = g_k(lb) + hq;
+        fd = g_d(lb) + hq;
+        take = f < theta;
+      }
+      take = take && nw + prefix_count(__ballot(take)) < WCAP;
+      const unsigned long long mt = __ballot(take), mk = __ballot(in && !take);
+      __syncthreads();
+      if (take) {
+        const int w = nw + prefix_count(mt);
+        L.wslot[w] = (uint16_t)(sl | ((key & kRel) ? 0x8000 : 0));
+        L.wlab[w] = lb;
+        L.key[sl] = (key & kNodeMask) | kRel;
+      } else if (in) {
+        L.pend[kept + prefix_count(mk)] = (uint16_t)sl;
+        fnext = f < fnext ? f : fnext;
+        dnext = fd < dnext ? fd : dnext;
+      }
+      nw += __popcll(mt);
+      kept += __popcll(mk);
+      __syncthreads();
+    }
+    npend = kept;
+    // relax: lane = (settled state, adjacency slot); slot-0 lanes also make the state's
+    // target offers; slot 3 of a node with more than 4 out-edges walks the CSR tail
+    bool tail = false;
+    for (int base = 0; base < 4 * nw; base += OTR_WAVE) {
+      const int k = base + gl;
+      int psl = -1;
+      bool isnew = false;
+      if (k < 4 * nw) {
+        const uint16_t ws = L.wslot[k >> 2];
+        const int sl = ws & 0x7FFF;
+        const bool again = (ws & 0x8000) != 0;
+        const unsigned long long lb = L.wlab[k >> 2];
+        const uint32_t v = L.node[sl], ha = L.hend[sl];
+        const int slot = k & 3;
+        if (slot == 0) ++my_settled;
+        const uint32_t tq = adjt[4 * (size_t)v + slot];
+        const uint2 xe = g.adj_e[4 * (size_t)v + slot];
+        const uint4 r = ld16(g.adj + 4 * (size_t)v + slot);
+        if (slot == 0) e_target_offers(L, turn, lb, ha, v, pd, pt, again, stale);
+        psl = e_relax(L, H, turn, lb, ha, r.x & ~kAdjMore, r.y, timed ? tq : 0u, xe.x, xe.y & 0xFFFFu, xe.y >> 16,
+                      (int32_t)r.z, (int32_t)r.w, pd, pt, mode_bit, again, my_relaxed, fnext, dnext, isnew, stale);
+        tail = tail || (slot == 3 && (r.x & kAdjMore));
+      }
+      nkeys += __popcll(__ballot(isnew));
+      const unsigned long long mp = __ballot(psl >= 0);
+      if (psl >= 0) {
+        const int p = npend + prefix_count(mp);
+        if (p < CAP) L.pend[p] = (uint16_t)psl;
+        else L.overflow = 1;
+      }
+      npend += __popcll(mp);
+    }
+    if (__ballot(tail) != 0ull) {
+      if (gl == 0) L.n_pend = npend;
+      __syncthreads();
+      for (int base = 0; base < 4 * nw; base += OTR_WAVE) {
+        const int k = base + gl;
+        if (k < 4 * nw && (k & 3) == 3) {
+          const uint16_t ws = L.wslot[k >> 2];
+          const int sl = ws & 0x7FFF;
+          const bool again = (ws & 0x8000) != 0;
+          const unsigned long long lb = L.wlab[k >> 2];
+          const uint32_t v = L.node[sl], ha = L.hend[sl];
+          if (g.adj[4 * (size_t)v + 3].x & kAdjMore)
+            for (uint32_t e = g.node_row[v] + 4; e < g.node_row[v + 1]; ++e) {
+              const uint4 pk = ld16(g.edge_pack + e);
+              const int2 wll = g.node_ll[pk.x];
+              const short2 hh = g.edge_head[e];
+              bool isnew;
+              const int psl = e_relax(L, H, turn, lb, ha, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e,
+                                      (uint32_t)hh.x, (uint32_t)hh.y, wll.x, wll.y, pd, pt, mode_bit, again,
+                                      my_relaxed, fnext, dnext, isnew, stale);
+              if (isnew) atomicAdd(&L.n_keys, 1);
+              if (psl >= 0) {
+                const int p = atomicAdd(&L.n_pend, 1);
+                if (p < CAP) L.pend[p] = (uint16_t)psl;
+                else L.overflow = 1;
+              }
+            }
+        }
+      }
+      __syncthreads();
+      npend = L.n_pend;
+      if (npend > CAP) npend = CAP;
+    }
+    __syncthreads();
+    fmin = wave_min_u32(fnext);
+    dmin = wave_min_u32(dnext);
+    const int keys = L.n_keys + nkeys;
+    if (!done && (L.overflow || keys > kMaxKeys)) done = true;
+    __syncthreads();
+    if (done && active && gl == 0 && keys > kMaxKeys) L.overflow = 1;
+  }
+  if (settled) *settled += my_settled;
+  if (relaxed) *relaxed += my_relaxed;
+  *stale_out = __ballot(stale) != 0ull;
+  __syncthreads();
+  return !L.overflow;
+}
+
+// ------------------------------------------------------------------------------
+// K3e: edge-state route tasks (turn modes), a fixed grid over the device-side list of
+// the tasks flagged 5 (k_route) or 6 (this tier's overflows, for the larger table).
+// ------------------------------------------------------------------------------
+template <int CAP>
+__global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, unsigned long long* counters) {
+  __shared__ EdgeLds<CAP> L;
+  const int64_t n_tasks = (int64_t)*a.list_count;
+  const int lane = (int)threadIdx.x;
+  for (int64_t w = blockIdx.x; w < n_tasks; w += gridDim.x) {
+    const int64_t task = a.task_list[w];
+    const uint4 r0 = a.rec[3 * task], r1 = a.rec[3 * task + 1], r2 = a.rec[3 * task + 2];
+    const int64_t s = r0.x, sp = r0.y;
+    const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
+    const int i = __ffsll((long long)mask) - 1;  // the task's one source
+    const int Kb = (int)(r1.y & 0xFFu);
+    const int md = (int)((r1.y >> 8) & 3u);
+    const bool forced = (r1.y >> 10) & 1u;
+    const uint32_t bmm = r0.w;
+    const int32_t bt = (int32_t)r2.y;
+    const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
+    const double pi = a.cand_p[sp * OTR_KMAX + i];
+    const uint32_t d0 = a.cprep[sp * OTR_KMAX + i].w;
+    const uint32_t t0 = bt >= 0 ? a.cprep_t[sp * OTR_KMAX + i].y : 0u;
+    const uint2 li = a.clen[sp * OTR_KMAX + i];
+    uint32_t ej = 0, tv = kEmpty, hT = 0, tpart = 0, tpt = 0, thb = 0;
+    double pj = 0;
+    bool needed = false;
+    if (lane < Kb) {
+      ej = a.cand_edge[s * OTR_KMAX + lane];
+      pj = a.cand_p[s * OTR_KMAX + lane];
+      const uint4 cq = a.cprep[s * OTR_KMAX + lane];
+      tpart = cq.x;
+      tpt = bt >= 0 ? a.cprep_t[s * OTR_KMAX + lane].x : 0u;
+      needed = !(ej == ei && pj >= pi);
+      if (needed) {
+        tv = cq.y;
+        hT = cq.z;
+        thb = (uint32_t)gr.edge_head[ej].x;
+      }
+    }
+    const bool root_ok = d0 <= bmm && (bt < 0 || t0 <= (uint32_t)bt);
+    const bool search = Kb <= OTR_WAVE && !forced && root_ok && __ballot(needed) != 0ull;
+    const uint32_t pd = bmm >= d0 ? bmm - d0 : 0u;
+    const uint32_t pt = bt >= 0 && t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
+    const Heur H = a.heur[s];
+    e_init(L);
+    bool stale = false;
+    unsigned long long settled = 0, relaxed = 0;
+    const bool ok = edge_search<CAP>(L, gr, H, a.turn + 181 * md, md, search, ei, gr.edge_dst[ei],
+                                     (uint32_t)(uint16_t)gr.edge_head[ei].y, r2.x, pd, pt, bt >= 0,
+                                     (uint32_t)(a.delta * 1000.0), Kb, tv, hT, tpart, tpt, thb, &stale,
+                                     counters ? &settled : nullptr, counters ? &relaxed : nullptr) &&
+                    Kb <= OTR_WAVE;
+    if (ok && !stale) {
+      uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
+      if (lane < Kb) {
+        int64_t r = -1, rt = 0;
+        uint32_t rc = 0;
+        if (forced) {
+          r = -1;
+        } else if (ej == ei && pj >= pi) {
+          r = part_mm(pj - pi, li.x);
+          if (bt >= 0) rt = part_mm(pj - pi, li.y);
+        } else if (search) {
+          const unsigned long long tl = L.tlab[lane];
+          if (tl != kGInf) {
+            r = (int64_t)d0 + g_d(tl);
+            rt = (int64_t)t0 + g_t(tl);
+            rc = g_c(tl);
+          }
+        }
+        const bool valid = r >= 0 && r <= (int64_t)bmm && (bt < 0 || rt <= (int64_t)bt);
+        trow[(int64_t)i * Kb + lane] = valid ? (uint32_t)r : kNoRoute;
+        a.trans_tc[trow - a.trans + (int64_t)i * Kb + lane] = valid ? rc : 0u;
+      }
+    } else if (lane == 0) {
+      a.overflow_flag[task] = stale ? 4 : (CAP < 2048 ? 6 : 3);
+    }
+    if (counters) {
+      settled = wave_sum_u32((uint32_t)settled);
+      relaxed = wave_sum_u32((uint32_t)relaxed);
+      if (lane == 0) {
+        const int sh = cshard();
+        atomicAdd(&counters[3 * kCShards + sh], settled);
+        atomicAdd(&counters[4 * kCShards + sh], relaxed);
+        atomicAdd(&counters[5 * kCShards + sh], ok && search ? (unsigned long long)Kb : 0ull);
+        atomicAdd(&counters[6 * kCShards + sh], search ? 1ull : 0ull);
+        atomicAdd(&counters[15 * kCShards + sh], stale ? 1ull : 0ull);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------
+// K6e: winner paths of turn-mode steps: the winner's edge-state search with the winner's
+// target only, then a walk back: at each state a, the smallest-id in-edge p of src(a)
+// whose label extended by (turn(p, a), a) is exactly a's label (oracle walk_path); the
+// first hop from the target takes the smallest a whose offer is the target's label.  The
+// lanes test the in-edges of one node in parallel.
+// ------------------------------------------------------------------------------
+template <int CAP>
+__global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, const int32_t* turn_tab,
+                                                   const int64_t* step_list, const unsigned long long* list_count,
+                                                   int32_t fail_flag) {
+  __shared__ EdgeLds<CAP> L;
+  __shared__ uint32_t s_rev[CAP];
+  const int64_t n_list = (int64_t)*list_count;
+  const int lane = (int)threadIdx.x;
+  for (int64_t w = blockIdx.x; w < n_list; w += gridDim.x) {
+    const int64_t k = step_list[w];
+    const int64_t s = a.steps[k];
+    const int64_t sp = a.prev[s];
+    const int wi = a.winner[sp], wj = a.winner[s];
+    const uint32_t ei = a.cand_edge[sp * OTR_KMAX + wi], ej = a.cand_edge[s * OTR_KMAX + wj];
+    const int md = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+    const int32_t* turn = turn_tab + 181 * md;
+    const uint32_t bmm = (uint32_t)bound_mm_of(a.bound[s]);
+    const int32_t bt = a.bt[s];
+    const uint4 cs = a.cprep[sp * OTR_KMAX + wi], ct = a.cprep[s * OTR_KMAX + wj];
+    const uint32_t d0 = cs.w, t0 = bt >= 0 ? a.cprep_t[sp * OTR_KMAX + wi].y : 0u;
+    const uint32_t tpt = bt >= 0 ? a.cprep_t[s * OTR_KMAX + wj].x : 0u;
+    const uint32_t pd = bmm >= d0 ? bmm - d0 : 0u;
+    const uint32_t pt = bt >= 0 && t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
+    const uint32_t thb = (uint32_t)gr.edge_head[ej].x;
+    const Heur H = a.heur[s];
+    e_init(L);
+    bool stale = false;
+    const uint32_t hroot = H(gr.node_ll[gr.edge_dst[ei]].x, gr.node_ll[gr.edge_dst[ei]].y);
+    const bool ok = edge_search<CAP>(L, gr, H, turn, md, true, ei, gr.edge_dst[ei], (uint32_t)(uint16_t)gr.edge_head[ei].y,
+                                     hroot, pd, pt, bt >= 0, (uint32_t)(a.delta * 1000.0), 1, ct.y, ct.z, ct.x, tpt,
+                                     thb, &stale, nullptr, nullptr);
+    const unsigned long long tl = L.tlab[0];
+    int n = -1;
+    if (ok && !stale && tl != kGInf) {
+      // first hop: the smallest in-edge a of src(ej) whose offer is the target's label
+      uint32_t cur = kEmpty;
+      {
+        const uint32_t v = ct.y;
+        const uint32_t r0 = gr.rev_row[v], r1 = gr.rev_row[v + 1];
+        uint32_t best = kEmpty;
+        for (uint32_t r = r0 + lane; r < r1; r += OTR_WAVE) {
+          const uint32_t x = gr.rev_edge[r];
+          const int sx = e_find(L, x);
+          if (sx < 0 || L.lab[sx] == kGInf) continue;
+          const unsigned long long lx = L.lab[sx];
+          EOffer o;
+          o.c = g_c(lx) + (uint32_t)turn[turn_degree((int)L.hend[sx], (int)thb)];
+          o.d = g_d(lx) + ct.x;
+          o.k = o.d + o.c;
+          o.t = (bt >= 0 ? g_t(lx) + tpt : 0u);
+          if (e_feasible(o, pd, bt >= 0 ? pt : 0xFFFFFFFFu) && gpack(o.k, o.c, o.t) == tl && x < best) best = x;
+        }
+        cur = wave_min_u32(best);
+      }
+      n = 0;
+      while (cur != kEmpty && cur != ei) {
+        if (n >= CAP) {
+          n = -1;
+          break;
+        }
+        if (lane == 0) s_rev[n] = cur;
+        ++n;
+        const int sa = e_find(L, cur);
+        const unsigned long long la = sa >= 0 ? L.lab[sa] : kGInf;
+        const uint32_t v = gr.edge_src[cur];
+        const uint32_t len = gr.len_mm[cur], tt = bt >= 0 ? gr.et(md)[cur] : 0u;
+        const uint32_t hb = (uint32_t)gr.edge_head[cur].x;
+        const uint32_t r0 = gr.rev_row[v], r1 = gr.rev_row[v + 1];
+        uint32_t best = kEmpty;
+        for (uint32_t r = r0 + lane; r < r1; r += OTR_WAVE) {
+          const uint32_t p = gr.rev_edge[r];
+          const int sx = e_find(L, p);
+          if (sx < 0 || L.lab[sx] == kGInf) continue;
+          const unsigned long long lp = L.lab[sx];
+          EOffer o;
+          o.c = g_c(lp) + (uint32_t)turn[turn_degree((int)L.hend[sx], (int)hb)];
+          o.d = g_d(lp) + len;
+          o.k = o.d + o.c;
+          o.t = g_t(lp) + tt;
+          if (la != kGInf && e_feasible(o, pd, bt >= 0 ? pt : 0xFFFFFFFFu) && gpack(o.k, o.c, o.t) == la && p < best)
+            best = p;
+        }
+        cur = wave_min_u32(best);
+        if (cur == kEmpty) n = -1;
+      }
+    }
+    if (n < 0) {
+      if (lane == 0) a.overflow_flag[k] = fail_flag;  // overflow / withdrawn label: the next tier
+    } else {
+      const int shard = (int)(blockIdx.x & (kShards - 1));
+      const int64_t region = a.capacity / kShards;
+      int64_t off = 0;
+      if (lane == 0) off = (int64_t)atomicAdd(&a.cursor[shard], (unsigned long long)n);
+      off = __shfl(off, 0);
+      if (off + n > region) {
+        if (lane == 0) *a.cap_flag = 1;
+      } else {
+        __syncthreads();
+        off += (int64_t)shard * region;
+        for (int q = lane; q < n; q += OTR_WAVE) a.path[off + q] = s_rev[n - 1 - q];
+        if (lane == 0) {
+          a.path_off[s] = off;
+          a.path_len[s] = n;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace otr

@@ -12,8 +12,7 @@
 
 #include "otr_engine.h"
 #include "otr_kernels.h"
-#include "otr_general.h"
-#include "otr_route_step.h"
+#include "otr_edge.h"
 #include "otr_ingest.h"
 
 namespace otr {
@@ -235,6 +234,14 @@ int engine_configure(const Config& cfg, std::string* err) {
     for (uint32_t k = k1 - 1; k > k0 && he < 0; --k) he = seg_heading(sll + 2ull * k - 2, sll + 2ull * k);
     head[e] = make_short2((short)(hb < 0 ? 0 : hb), (short)(he < 0 ? 0 : he));
   }
+  // edge-state view of the adjacency slots (turn-cost searches, otr_edge.h): the slot's
+  // edge id and its begin / end headings
+  std::vector<uint2> adje(4ull * h.n_nodes + 4, make_uint2(0u, 0u));
+  for (uint32_t u = 0; u < h.n_nodes; ++u)
+    for (uint32_t k = 0; k < 4 && row[u] + k < row[u + 1]; ++k) {
+      const uint32_t e = row[u] + k;
+      adje[4ull * u + k] = make_uint2(e, (uint32_t)(uint16_t)head[e].x | ((uint32_t)(uint16_t)head[e].y << 16));
+    }
   // heuristic scale: every edge must satisfy len_mm >= scale * (straight-line mm in any
   // search's metric); the upper bound of that metric distance uses the edge's own
   // more equatorward cosine.  Generated graphs give 1; lengths rounded
@@ -318,6 +325,7 @@ int engine_configure(const Config& cfg, std::string* err) {
     g.adj_t_stride = (uint32_t)at[0].size();
   }
   g.edge_head = (const short2*)upv(head.data(), sizeof(short2) * head.size());
+  g.adj_e = (const uint2*)upv(adje.data(), sizeof(uint2) * adje.size());
   g.cell_rec = (const uint4*)upv(crec.data(), sizeof(uint4) * crec.size());
   if (!alloc_ok) {
     if (err) *err = "device allocation for the graph failed";
@@ -739,6 +747,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   pr.cprep_t = need<uint2>(S_CPREP_T, (size_t)S * OTR_KMAX);
   pr.clen = need<uint2>(S_CLEN, (size_t)S * OTR_KMAX);
   pr.nroot = need<int32_t>(S_CAND_NROOT, S);
+  pr.turn_modes = turn_modes;
   if (!pr.heur || !pr.cprep || !pr.cprep_t || !pr.clen || !pr.nroot) {
     if (err) *err = "device allocation failed (prep)";
     return OTR_DEVICE_ERROR;
@@ -754,29 +763,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   if (S > 0) k_ntask<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, pr.nroot, sb.ntask);
   if ((rc = scan(sb.ntask, task_off, S))) return rc;
   if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
-  // OTR_ROUTE_STEP=1 (A/B knob, read per call): batches without turn-cost
-  // modes route in the multi-root step kernel (otr_route_step.h), one unit per (state,
-  // group of kStepRoots of its search tasks); measured slower than the per-root first
-  // tier at C2, so off by default
-  const char* step_env = getenv("OTR_ROUTE_STEP");
-  const bool step_on = step_env && atoi(step_env) != 0;
-  const bool use_step = step_on && turn_modes == 0u;
-  constexpr int kStepRoots = 8;
-  int64_t* unit_off = nullptr;
-  if (use_step) {
-    int64_t* nunit = need<int64_t>(S_NUNIT, S);
-    unit_off = need<int64_t>(S_UNIT_OFF, S + 1);
-    if (!nunit || !unit_off) {
-      if (err) *err = "device allocation failed (step units)";
-      return OTR_DEVICE_ERROR;
-    }
-    if (S > 0) k_step_nunit<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.ntask, kStepRoots, nunit);
-    if ((rc = scan(nunit, unit_off, S))) return rc;
-  }
-  int64_t NT = 0, NTR = 0, NU = 0;
+  int64_t NT = 0, NTR = 0;
   HIPCHK(hipMemcpyAsync(&NT, task_off + S, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipMemcpyAsync(&NTR, trans_off + S, 8, hipMemcpyDeviceToHost, stream));
-  if (use_step) HIPCHK(hipMemcpyAsync(&NU, unit_off + S, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
   int64_t* task_state = need<int64_t>(S_TASK_STATE, NT);
   unsigned long long* task_mask = need<unsigned long long>(S_TASK_MASK, NT);
@@ -803,6 +792,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     ta.state_trace = state_trace;
     ta.mode = b.mode;
     ta.cprep = pr.cprep;
+    ta.cprep_t = pr.cprep_t;
     ta.heur = pr.heur;
     ta.trans_off = trans_off;
     ta.turn_modes = turn_modes;
@@ -858,7 +848,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   // device-side counters of the retry lists: [0..7] route tiers, [8] general tier 1,
   // [9] general tier 2, [10] route tasks left unrouted, [11] steps, [12..15] path tiers,
   // [16] path general 1, [17] path general 2, [18] paths left, [19] general overflow
-  // count, [20] cap flag, [24] tasks the first route tier flagged, [32..96) path bump cursors
+  // count, [20] cap flag, [24] tasks the first route tier flagged, [25..26] edge-state
+  // route tiers, [27..28] edge-state path tiers, [32..96) path bump cursors
   unsigned long long* cnt = need<unsigned long long>(S_MISC, 32 + kShards);
   HIPCHK(hipMemsetAsync(cnt, 0, 8 * (32 + kShards), stream));
   int64_t* list = need<int64_t>(S_LIST, std::max<int64_t>(NT, S));
@@ -874,15 +865,28 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     const uint32_t cap = tier == 0 ? (1u << 15) : (1u << 20);
     const uint32_t n = tier == 0 ? 1024u : 8u;
     if (!sl.key) {
+      // all five arrays or none: a partial set is freed and the batch fails with
+      // OTR_DEVICE_ERROR (a later batch never sees a half-allocated slab)
       const size_t c = (size_t)cap * n;
-      HIPCHK(hipMalloc(&sl.key, 4 * c));
-      HIPCHK(hipMalloc(&sl.lab, 8 * c));
-      HIPCHK(hipMalloc(&sl.qmark, 4 * c));
-      HIPCHK(hipMalloc(&sl.fr, 8 * c));
-      HIPCHK(hipMalloc(&sl.touched, 4 * c));
-      HIPCHK(hipMemsetAsync(sl.key, 0xFF, 4 * c, stream));
-      HIPCHK(hipMemsetAsync(sl.lab, 0xFF, 8 * c, stream));
-      HIPCHK(hipMemsetAsync(sl.qmark, 0, 4 * c, stream));
+      void* p[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+      const size_t bytes[5] = {4 * c, 8 * c, 4 * c, 8 * c, 4 * c};
+      bool good = true;
+      for (int q = 0; q < 5 && good; ++q) good = hipMalloc(&p[q], bytes[q]) == hipSuccess;
+      if (good)
+        good = hipMemsetAsync(p[0], 0xFF, 4 * c, stream) == hipSuccess &&
+               hipMemsetAsync(p[1], 0xFF, 8 * c, stream) == hipSuccess &&
+               hipMemsetAsync(p[2], 0, 4 * c, stream) == hipSuccess;
+      if (!good) {
+        (void)hipGetLastError();
+        for (void* q : p)
+          if (q) (void)hipFree(q);
+        throw DeviceOom{S_NUM + tier, 28 * c};  // (the global-search slabs of this tier)
+      }
+      sl.key = (uint32_t*)p[0];
+      sl.lab = (unsigned long long*)p[1];
+      sl.qmark = (uint32_t*)p[2];
+      sl.fr = (uint32_t*)p[3];
+      sl.touched = (uint32_t*)p[4];
     }
     out->key = sl.key;
     out->lab = sl.lab;
@@ -920,36 +924,15 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // the LDS tiers count their work only when asked (OTR_BATCH_ROUTE_WORK): the end-of-
     // wave counter atomics cost ~7% of the first tier (tools/ab_libs.sh)
     unsigned long long* rwork = (in->flags & OTR_BATCH_ROUTE_WORK) ? d_counters : nullptr;
-    // batches with turn-cost modes take the kernels compiled with the turn walk
-    const bool turns = turn_modes != 0u;
     // the LDS route kernels: with the work counters (CNT) only when counting was asked for
-#define OTR_ROUTE_LAUNCH(C, G_, LIST_, GRID, ARGS, CTR)                                                  \
-  do {                                                                                                 \
-    if (CTR) {                                                                                         \
-      if (turns) k_route<C, G_, LIST_, true, false, true><<<GRID, 64, 0, stream>>>(g, ARGS, CTR);      \
-      else k_route<C, G_, LIST_, false, false, true><<<GRID, 64, 0, stream>>>(g, ARGS, CTR);           \
-    } else {                                                                                           \
-      if (turns) k_route<C, G_, LIST_, true, false, false><<<GRID, 64, 0, stream>>>(g, ARGS, nullptr); \
-      else k_route<C, G_, LIST_, false, false, false><<<GRID, 64, 0, stream>>>(g, ARGS, nullptr);      \
-    }                                                                                                  \
+#define OTR_ROUTE_LAUNCH(C, G_, LIST_, GRID, ARGS, CTR)                                       \
+  do {                                                                                      \
+    if (CTR) k_route<C, G_, LIST_, false, true><<<GRID, 64, 0, stream>>>(g, ARGS, CTR);      \
+    else k_route<C, G_, LIST_, false, false><<<GRID, 64, 0, stream>>>(g, ARGS, nullptr);     \
   } while (0)
-    if (use_step) {
-      StepArgs st{};
-      int64_t* units = need<int64_t>(S_UNIT, std::max<int64_t>(NU, 1));
-      st.unit = units;
-      if (!units) {
-        if (err) *err = "device allocation failed (step units)";
-        return OTR_DEVICE_ERROR;
-      }
-      st.n_units = NU;
-      st.task_off = task_off;
-      st.ntask = sb.ntask;
-      k_step_units<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.ntask, unit_off, kStepRoots, units);
-      tb(OTR_STAGE_ROUTE);
-      const unsigned grid = (unsigned)(8 * ((NU + 7) / 8));
-      if (NU > 0) k_route_step<kStepCap, kStepRoots><<<grid, 64, 0, stream>>>(g, ra, st, rwork);
-      out->route_tier_code[0] = kStepCode;
-    } else if (route_g == 2) {
+    // turn-mode (edge-based) tasks are `general` (k_tasks): the LDS tiers pass them on
+    const bool turns = turn_modes != 0u;
+    if (route_g == 2) {
       tb(OTR_STAGE_ROUTE);
       const int64_t units = (NT + 1) / 2;
       const unsigned grid = (unsigned)(8 * ((units + 7) / 8));
@@ -1000,10 +983,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier) + 1], stream);
     }
 #ifndef OTR_FORCE_GENERAL  // (test build: every search in k_general)
-    // batches without turn costs: the tasks whose (length << sh | time) words need more
-    // than 32 bits (flag 3: long gaps between states) run in an LDS table of 64-bit words
-    // (same labels); what outgrows it is flagged 3 again
-    if (!turns) {
+    // the node-mode tasks whose (length << sh | time) words need more than 32 bits
+    // (flag 3: long gaps between states) run in an LDS table of 64-bit words (same labels,
+    // DESIGN.md §3.5); what outgrows it is flagged 3 again
+    {
       unsigned long long* c = cnt + 7;
       k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x8u, list, c);
       RouteArgs rb = ra;
@@ -1011,17 +994,36 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       rb.list_count = c;
       out->route_tier_code[8] = 900000 + 2048;
       if (timing) (void)hipEventRecord(ev[24 + 2 * 8], stream);
-      if (rwork) k_route<2048, 1, true, false, true, true><<<4096, 64, 0, stream>>>(g, rb, d_counters + 7 * bank);
-      else k_route<2048, 1, true, false, true, false><<<4096, 64, 0, stream>>>(g, rb, nullptr);
+      if (rwork) k_route<2048, 1, true, true, true><<<4096, 64, 0, stream>>>(g, rb, d_counters + 7 * bank);
+      else k_route<2048, 1, true, true, false><<<4096, 64, 0, stream>>>(g, rb, nullptr);
       if (timing) (void)hipEventRecord(ev[24 + 2 * 8 + 1], stream);
     }
 #endif
-    // everything left — turn-cost (edge-based) tasks, (turn-mode) tasks whose labels need
-    // 64 bits, overflows of the largest LDS tables — runs in the global-memory search:
+    // turn-mode tasks (flag 5): the edge-state LDS search, 384 then 2048 states; what
+    // outgrows it (flag 3) or may have kept a withdrawn label (flag 4) goes on below
+    if (turns) {
+      out->route_tier_code[9] = 700000 + 384;
+      if (timing) (void)hipEventRecord(ev[24 + 2 * 9], stream);
+      for (int et = 0; et < 2; ++et) {
+        unsigned long long* c = cnt + 25 + et;
+        k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, et == 0 ? 0x20u : 0x40u,
+                                                              list, c);
+        RouteArgs rb = ra;
+        rb.task_list = list;
+        rb.list_count = c;
+        unsigned long long* rcn = rwork ? d_counters + 1 * bank : nullptr;
+        if (et == 0) k_route_edge<384><<<4096, 64, 0, stream>>>(g, rb, rcn);
+        else k_route_edge<2048><<<512, 64, 0, stream>>>(g, rb, rcn);
+      }
+      if (timing) (void)hipEventRecord(ev[24 + 2 * 9 + 1], stream);
+    }
+    // everything left — turn-cost (edge-based) tasks, tasks whose labels need 64 bits,
+    // overflows of the largest LDS tables, searches that may have kept a withdrawn label
+    // (flag 4: k_general's exact mode settles it) — runs in the global-memory search:
     // first on 32K-slot slabs, then what outgrew those on 1M-slot slabs
     for (int gt = 0; gt < 2; ++gt) {
       unsigned long long* c = cnt + 8 + gt;
-      k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, gt == 0 ? 0xEu : 0x2u, list,
+      k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, gt == 0 ? 0x1Eu : 0x2u, list,
                                                             c);
       GSlabs gs2;
       if ((rc = slabs(gt, &gs2))) return rc;
@@ -1036,7 +1038,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       if (timing) (void)hipEventRecord(ev[24 + 2 * (6 + gt) + 1], stream);
     }
     // tasks still flagged (beyond a 1M-state slab): their traces get OTR_MATCH_ERROR
-    k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0xEu, fail_tasks, cnt + 10);
+    k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x1Eu, fail_tasks, cnt + 10);
     te(OTR_STAGE_ROUTE_BIG);
   }
   // ---- K5: Viterbi
@@ -1089,6 +1091,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       }
       HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (S + 1), stream));
       HIPCHK(hipMemsetAsync(cnt + 12, 0, 8 * 9, stream));  // path tier counts, cap flag
+      HIPCHK(hipMemsetAsync(cnt + 27, 0, 8 * 2, stream));  // edge-state path tier counts
       HIPCHK(hipMemsetAsync(cnt + 32, 0, 8 * kShards, stream));
       PathArgs pa{};
       pa.steps = steps;
@@ -1108,6 +1111,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       pa.radius = cb.radius;
       pa.heur = ra.heur;
       pa.cprep = ra.cprep;
+      pa.cprep_t = ra.cprep_t;
       pa.bt = sb.bt;
       pa.turn_modes = turn_modes;
       pa.delta = mp.delta;
@@ -1136,7 +1140,17 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         else if (tier == 1) k_paths<1024, 1><<<8192, 64, 0, stream>>>(g, pa, list, c);
         else k_paths<4096, 1><<<4096, 64, 0, stream>>>(g, pa, list, c);
       }
-      // turn-cost winners, 64-bit labels and the largest-table overflows: k_general
+      // turn-cost winners (flag 5): the edge-state LDS search, 384 then 2048 states
+      if (turn_modes != 0u) {
+        for (int et = 0; et < 2; ++et) {
+          unsigned long long* c = cnt + 27 + et;
+          k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, et == 0 ? 0x20u : 0x40u,
+                                                                       list, c);
+          if (et == 0) k_paths_edge<384><<<4096, 64, 0, stream>>>(g, pa, d_turn, list, c, 6);
+          else k_paths_edge<2048><<<512, 64, 0, stream>>>(g, pa, d_turn, list, c, 3);
+        }
+      }
+      // 64-bit labels, the largest-table overflows and what the edge tiers left: k_general
       ga.steps = steps;
       ga.winner = va.winner;
       ga.path_off = path_off;
@@ -1325,9 +1339,11 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     return hc[(size_t)b * OTR_COUNTERS + (size_t)k];
   };
   for (int k = 0; k < OTR_COUNTERS; ++k) out->counters[k] = ctr(0, k);
-  // per route kernel: searches, settled, relaxed, transition entries (banks 0, 2..6, 8..9)
-  for (int t = 0; t < 9; ++t) {
-    const int b = t == 0 ? 0 : (t < 6 ? 1 + t : (t < 8 ? 2 + t : 7));  // slot 8 (64-bit LDS tier): bank 7
+  // per route kernel: searches, settled, relaxed, transition entries (banks 0, 2..6, 8..9;
+  // slot 8, the 64-bit LDS tier: bank 7; slot 9, the edge-state tiers: bank 1)
+  for (int b = 1; b < 10; ++b) out->counters[15] += ctr(b, 15);  // withdrawn-label flags, every tier
+  for (int t = 0; t < 10; ++t) {
+    const int b = t == 0 ? 0 : (t < 6 ? 1 + t : (t < 8 ? 2 + t : (t == 8 ? 7 : 1)));
     out->route_tier_work[t][0] = ctr(b, 6);
     out->route_tier_work[t][1] = ctr(b, 3);
     out->route_tier_work[t][2] = ctr(b, 4);
@@ -1347,7 +1363,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     for (int k = 0; k < 10; ++k)
       if (used[k]) (void)hipEventElapsedTime(&out->kernel_ms[k], ev[2 * k], ev[2 * k + 1]);
     out->route_tier_ms[0] = out->kernel_ms[OTR_STAGE_ROUTE];
-    for (int t = 1; t < 9; ++t)
+    for (int t = 1; t < 10; ++t)
       if (out->route_tier_code[t] != 0)
         (void)hipEventElapsedTime(&out->route_tier_ms[t], ev[24 + 2 * t], ev[24 + 2 * t + 1]);
   }

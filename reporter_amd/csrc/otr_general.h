@@ -6,17 +6,23 @@
 //   * turn costs (turn_penalty_factor > 0): the search is over EDGE states, because
 //     the turn cost at a node depends on the edge that entered it;
 //   * steps whose bounds do not fit the 32-bit packing;
-//   * searches that outgrew the largest LDS table.
-// Labels are 64-bit lexicographic keys d:25 | t:17 | c:22 (length mm, time 0.1 s, turn
-// cost mm; oracle rkey with the ORC_* caps), so one atomicMin keeps the exact
-// lexicographic minimum and the fixed point is independent of the processing order.
+//   * searches that outgrew the largest LDS table;
+//   * searches whose LDS run may have kept a withdrawn label (flag 4, relax_one).
+// Labels are 64-bit words key << 38 | (kTcCap - turn) << 17 | time: key = length + turn
+// cost (mm), so one atomicMin keeps the lexicographic minimum of (key, length, time), the
+// oracle's order (oracle.c rkey).  Labels are relative to the search root; relaxations
+// beyond the task's relative bounds (length pd, time pt, turn cost kTcCap) are pruned.
 //
 // One workgroup (kGenThreads) per task, persistent over a device task list whose length
 // is read on the device (no host round trip).  Each workgroup owns a slab: an open-
-// addressing hash table {state, label, round stamp} plus two frontier lists and the
-// list of claimed slots (reset at the end of the task, so a slab is never cleared as a
-// whole).  Rounds are label-correcting (a state is re-expanded whenever its label
-// improves) over the frontier; the search ends when no label improved.
+// addressing hash table {state | relaxed bit, label, round stamp} plus two frontier lists
+// and the list of claimed slots (reset after every search, so a slab is never cleared as
+// a whole).  A search first runs label-correcting rounds over the frontier (every state
+// whose label improved is expanded again); when a time- or turn-pruned re-expansion may
+// have left a withdrawn label (the stale test of relax_one) it is run again in EXACT
+// mode: each round expands only the frontier states of the smallest key, which are final
+// (every offer adds >= 1 mm), i.e. the label-setting search of the oracle, in parallel
+// over equal keys.
 #pragma once
 #include "otr_kernels.h"
 
@@ -24,16 +30,19 @@ namespace otr {
 
 constexpr int kGenThreads = 256;
 constexpr unsigned long long kGInf = 0xFFFFFFFFFFFFFFFFull;
+constexpr uint32_t kGRel = 0x80000000u;  // key bit: the state has been expanded before
+constexpr uint32_t kGIdMask = 0x7FFFFFFFu;
 
-__host__ __device__ inline unsigned long long gpack(uint64_t d, uint64_t t, uint64_t c) {
-  return (d << 39) | (t << 22) | c;
+__host__ __device__ inline unsigned long long gpack(uint64_t k, uint64_t c, uint64_t t) {
+  return (k << 38) | ((uint64_t)(kTcCap - c) << 17) | t;
 }
-__host__ __device__ inline uint32_t g_d(unsigned long long w) { return (uint32_t)(w >> 39); }
-__host__ __device__ inline uint32_t g_t(unsigned long long w) { return (uint32_t)((w >> 22) & 0x1FFFFull); }
-__host__ __device__ inline uint32_t g_c(unsigned long long w) { return (uint32_t)(w & 0x3FFFFFull); }
+__host__ __device__ inline uint32_t g_k(unsigned long long w) { return (uint32_t)(w >> 38); }
+__host__ __device__ inline uint32_t g_c(unsigned long long w) { return kTcCap - (uint32_t)((w >> 17) & 0x1FFFFFull); }
+__host__ __device__ inline uint32_t g_t(unsigned long long w) { return (uint32_t)(w & 0x1FFFFull); }
+__host__ __device__ inline uint32_t g_d(unsigned long long w) { return g_k(w) - g_c(w); }
 
 struct GSlabs {
-  uint32_t* key;                // [n][cap] edge state, kEmpty
+  uint32_t* key;                // [n][cap] state | kGRel, kEmpty
   unsigned long long* lab;      // [n][cap]
   uint32_t* qmark;              // [n][cap] round + 1 when queued for that round
   uint32_t* fr;                 // [n][2][cap] frontier slot lists
@@ -98,7 +107,7 @@ __device__ inline int g_claim(uint32_t* key, uint32_t cap, uint32_t e, bool* cla
       *claimed = true;
       return (int)h;
     }
-    if (k == e) {
+    if ((k & kGIdMask) == e) {
       *claimed = false;
       return (int)h;
     }
@@ -111,7 +120,7 @@ __device__ inline int g_find(const uint32_t* key, uint32_t cap, uint32_t e) {
   for (uint32_t probe = 0; probe < cap; ++probe) {
     const uint32_t k = ld_u32(&key[h]);
     if (k == kEmpty) return -1;
-    if (k == e) return (int)h;
+    if ((k & kGIdMask) == e) return (int)h;
     h = (h + 1u) & (cap - 1u);
   }
   return -1;
@@ -121,162 +130,240 @@ struct GTask {
   int64_t s, sp;
   uint32_t root;        // node (node mode) or edge (edge mode)
   bool edge_mode, time_on;
-  uint32_t bmm;
-  int32_t bt;
+  uint32_t bmm;         // the step's length bound (mm)
+  int32_t bt;           // the step's time bound (0.1 s), -1 none
+  uint32_t pd, pt;      // the relative pruning bounds of this search (bound - exit part)
   int mode;
   const uint32_t* et;   // the mode's edge times
   const int32_t* turn;  // the mode's turn table
   uint32_t mode_bit;
 };
 
-// Workgroup-wide bounded label-correcting search of one task in slab `sl`.  Returns
-// false (workgroup-uniform) on slab overflow.
-__device__ bool g_search(const DevGraph& G, const GTask& T, uint32_t* key, unsigned long long* lab, uint32_t* qmark,
-                         uint32_t* fr, uint32_t* touched, uint32_t cap, uint32_t* s_n, uint32_t* s_touched,
-                         uint32_t* s_ovf, unsigned long long* work) {
+// the relaxation of state a (label L) through edge b: relative (key, length, time, turn);
+// a == kEmpty: no turn (node mode)
+struct GOffer {
+  uint32_t k, d, t, c;
+};
+__device__ inline GOffer g_offer(const DevGraph& G, const GTask& T, uint32_t a, unsigned long long L, uint32_t b) {
+  GOffer o;
+  const uint32_t len = G.len_mm[b];
+  o.c = g_c(L);
+  if (T.edge_mode && a != kEmpty) o.c += (uint32_t)T.turn[turn_degree(G.edge_head[a].y, G.edge_head[b].x)];
+  o.d = g_d(L) + len;
+  o.k = o.d + o.c;
+  o.t = T.time_on ? g_t(L) + T.et[b] : 0u;
+  return o;
+}
+__device__ inline bool g_feasible(const GTask& T, const GOffer& o) {
+  return o.d <= T.pd && (!T.time_on || o.t <= T.pt) && o.c <= kTcCap;
+}
+// label L (lexicographically) above offer o?  (stale test: o may be infeasible, so it is
+// compared by components, not packed)
+__device__ inline bool g_above(unsigned long long L, const GOffer& o) {
+  const uint32_t k = g_k(L), d = g_d(L), t = g_t(L);
+  if (k != o.k) return k > o.k;
+  if (d != o.d) return d > o.d;
+  return t > o.t;
+}
+
+// block-wide minimum of a u32 (kGenThreads threads)
+__device__ inline uint32_t g_block_min(uint32_t v, uint32_t* s_red) {
+  for (int off = OTR_WAVE / 2; off > 0; off >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)v, off);
+    v = o < v ? o : v;
+  }
+  __syncthreads();
+  if (lane_id() == 0) s_red[threadIdx.x / OTR_WAVE] = v;
+  __syncthreads();
+  uint32_t m = s_red[0];
+  for (int w = 1; w < kGenThreads / OTR_WAVE; ++w) m = s_red[w] < m ? s_red[w] : m;
+  return m;
+}
+
+struct GShared {
+  uint32_t n[2], touched, ovf, stale, red[kGenThreads / OTR_WAVE];
+};
+
+// Workgroup-wide bounded search of one task in the slab (see the file comment): label-
+// correcting rounds, or EXACT key-order rounds.  Returns false (workgroup-uniform) on slab
+// overflow; *stale (label-correcting mode) when a pruned re-expansion may have left a
+// withdrawn label — the caller resets the slab and searches again in exact mode.
+__device__ bool g_search(const DevGraph& G, const GTask& T, bool exact, uint32_t* key, unsigned long long* lab,
+                         uint32_t* qmark, uint32_t* fr, uint32_t* touched, uint32_t cap, GShared* sh, bool* stale,
+                         unsigned long long* work) {
   const int tid = threadIdx.x;
   const uint32_t maxk = cap - cap / 8u;
   unsigned long long my_relaxed = 0;
   if (tid == 0) {
-    *s_touched = 0;
-    *s_ovf = 0;
-    s_n[0] = 0;
-    s_n[1] = 0;
-  }
-  __syncthreads();
-  // relax state a (or the virtual root node when a == kEmpty) with label L into edge b
-  auto relax = [&](uint32_t a, unsigned long long L, uint32_t b, uint32_t round, int nxt) {
-    const uint32_t attr = G.edge_attr[b];
-    if (!(attr & T.mode_bit)) return;
-    ++my_relaxed;
-    const uint32_t nd = g_d(L) + G.len_mm[b];
-    if (nd > T.bmm) return;
-    uint32_t nt = 0, nc = 0;
-    if (T.time_on) {
-      const uint32_t x = g_t(L) + T.et[b];
-      nt = x < kTCap ? x : kTCap;
-    }
-    if (T.edge_mode && a != kEmpty) {
-      const int td = turn_degree(G.edge_head[a].y, G.edge_head[b].x);
-      const uint32_t x = g_c(L) + (uint32_t)T.turn[td];
-      nc = x < kTcCap ? x : kTcCap;
-    } else if (T.edge_mode) {
-      nc = g_c(L);
-    }
-    const unsigned long long w = gpack(nd, nt, nc);
+    sh->ovf = 0;
+    sh->stale = 0;
+    sh->n[0] = 0;
+    sh->n[1] = 0;
+    // the root state, label 0, queued for round 0
     bool claimed = false;
-    const int sl = g_claim(key, cap, b, &claimed);
+    const int sl = g_claim(key, cap, T.root, &claimed);
+    if (sl >= 0) {
+      if (claimed) {
+        const uint32_t k = sh->touched++;
+        if (k < cap) touched[k] = (uint32_t)sl;
+      }
+      lab[sl] = gpack(0u, 0u, 0u);
+      qmark[sl] = 1u;
+      fr[0] = (uint32_t)sl;
+      sh->n[0] = 1;
+    } else {
+      sh->ovf = 1;
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  // relax state a (label L, expanded before: again) through edge b, queueing for round nr
+  auto relax = [&](uint32_t a, unsigned long long L, bool again, uint32_t b, uint32_t nr, int nxt) {
+    if (!(G.edge_attr[b] & T.mode_bit)) return;
+    ++my_relaxed;
+    const GOffer o = g_offer(G, T, T.edge_mode ? a : kEmpty, L, b);
+    const uint32_t sid = T.edge_mode ? b : G.edge_dst[b];
+    if (!g_feasible(T, o)) {
+      if (again && !exact) {  // the stale test (relax_one): the head holds a label above this offer
+        const int sv = g_find(key, cap, sid);
+        if (sv >= 0) {
+          const unsigned long long Lv = ld_u64(&lab[sv]);
+          if (Lv != kGInf && g_above(Lv, o)) sh->stale = 1;
+        }
+      }
+      return;
+    }
+    const unsigned long long w = gpack(o.k, o.c, o.t);
+    bool claimed = false;
+    const int sl = g_claim(key, cap, sid, &claimed);
     if (sl < 0) {
-      *s_ovf = 1;
+      sh->ovf = 1;
       return;
     }
     if (claimed) {
-      const uint32_t k = atomicAdd(s_touched, 1u);
+      const uint32_t k = atomicAdd(&sh->touched, 1u);
       if (k < cap) touched[k] = (uint32_t)sl;
-      if (k >= maxk) *s_ovf = 1;
+      if (k >= maxk) sh->ovf = 1;
     }
     const unsigned long long old = atomicMin(&lab[sl], w);
-    if (w < old && atomicExch(&qmark[sl], round + 1u) != round + 1u) {
-      const uint32_t p = atomicAdd(&s_n[nxt], 1u);
+    if (w < old && atomicExch(&qmark[sl], nr + 1u) != nr + 1u) {
+      const uint32_t p = atomicAdd(&sh->n[nxt], 1u);
       if (p < cap) fr[(size_t)nxt * cap + p] = (uint32_t)sl;
-      else *s_ovf = 1;
+      else sh->ovf = 1;
     }
   };
-  // round 0: the root's out-edges
-  {
-    uint32_t v;
-    unsigned long long L0 = 0ull;
-    uint32_t from = kEmpty;
-    if (T.edge_mode) {
-      // the root edge is a state with label 0 (labels are relative to its exit)
-      if (tid == 0) {
-        bool claimed = false;
-        const int sl = g_claim(key, cap, T.root, &claimed);
-        if (sl >= 0) {
-          lab[sl] = 0ull;
-          if (claimed) touched[atomicAdd(s_touched, 1u)] = (uint32_t)sl;
-        } else {
-          *s_ovf = 1;
-        }
-      }
-      v = G.edge_dst[T.root];
-      from = T.root;
-    } else {
-      v = T.root;
-    }
-    __syncthreads();
-    const uint32_t e0 = G.node_row[v], e1 = G.node_row[v + 1];
-    for (uint32_t e = e0 + tid; e < e1; e += kGenThreads) relax(from, L0, e, 0u, 0);
-  }
-  __syncthreads();
   uint32_t round = 0;
   int cur = 0;
   unsigned long long expanded = 0;  // states expanded (uniform): the search's "settled" count
   for (;;) {
-    const uint32_t n = s_n[cur];
-    if (n == 0 || *s_ovf) break;
+    const uint32_t n = sh->n[cur];
+    if (n == 0 || sh->ovf || (!exact && sh->stale)) break;
     const int nxt = cur ^ 1;
-    ++round;
-    if (tid == 0) s_n[nxt] = 0;
     __syncthreads();
+    if (tid == 0) sh->n[nxt] = 0;
     const uint32_t nn = n < cap ? n : cap;
-    expanded += nn;
+    // exact mode: only the frontier's smallest key is final
+    uint32_t kmin = 0;
+    if (exact) {
+      uint32_t m = 0xFFFFFFFFu;
+      for (uint32_t i = tid; i < nn; i += kGenThreads) {
+        const uint32_t sl = ld_u32(&fr[(size_t)cur * cap + i]);
+        const uint32_t k = g_k(ld_u64(&lab[sl]));
+        m = k < m ? k : m;
+      }
+      kmin = g_block_min(m, sh->red);
+    }
+    __syncthreads();
     for (uint32_t i = tid; i < nn; i += kGenThreads) {
       const uint32_t sl = ld_u32(&fr[(size_t)cur * cap + i]);
-      const uint32_t a = ld_u32(&key[sl]);
       const unsigned long long L = ld_u64(&lab[sl]);
-      const uint32_t v = G.edge_dst[a];
-      for (uint32_t e = G.node_row[v]; e < G.node_row[v + 1]; ++e) relax(a, L, e, round, nxt);
+      if (exact && g_k(L) != kmin) {  // not final yet: carried to the next round
+        if (atomicExch(&qmark[sl], round + 2u) != round + 2u) {
+          const uint32_t p = atomicAdd(&sh->n[nxt], 1u);
+          if (p < cap) fr[(size_t)nxt * cap + p] = sl;
+          else sh->ovf = 1;
+        }
+        continue;
+      }
+      const uint32_t was = atomicOr(&key[sl], kGRel);
+      const uint32_t a = was & kGIdMask;
+      const bool again = (was & kGRel) != 0u;
+      ++expanded;
+      const uint32_t v = T.edge_mode ? G.edge_dst[a] : a;
+      for (uint32_t e = G.node_row[v]; e < G.node_row[v + 1]; ++e) relax(a, L, again, e, round + 1u, nxt);
     }
     __threadfence_block();
     __syncthreads();
+    ++round;
     cur = nxt;
   }
   __syncthreads();
   if (work) {  // this tier's counter bank (kinds 3 settled, 4 relaxed)
-    const int sh = cshard();
-    atomicAdd(&work[4 * kCShards + sh], my_relaxed);
-    if (tid == 0) atomicAdd(&work[3 * kCShards + sh], expanded);
+    const int shd = cshard();
+    atomicAdd(&work[4 * kCShards + shd], my_relaxed);
+    atomicAdd(&work[3 * kCShards + shd], expanded);
   }
-  return *s_ovf == 0;
+  *stale = !exact && sh->stale != 0;
+  const bool ok = sh->ovf == 0;
+  __syncthreads();
+  return ok;
 }
 
-// the best label at node v: node mode the minimum over labelled in-edge states (the
-// root node: 0); edge mode with the turn into edge ej added (min id among equals)
-__device__ inline bool g_node_key(const DevGraph& G, const GTask& T, const uint32_t* key,
-                                  const unsigned long long* lab, uint32_t cap, uint32_t ej,
-                                  unsigned long long* out, uint32_t* via) {
+// The route to target (ej, pj): node mode the label of v = src(ej) (relative; the root
+// node has 0); edge mode the lexicographic minimum over the labelled in-edges a of v of
+// the offer with the turn (a, ej) — smallest a among equals (*via).  The target's entry
+// part (tpart mm, tpt 0.1 s) is included and the offer must keep the relative bounds
+// (oracle target_key).  Returns false when no feasible offer exists.
+__device__ inline bool g_target(const DevGraph& G, const GTask& T, const uint32_t* key, const unsigned long long* lab,
+                                uint32_t cap, uint32_t ej, uint32_t tpart, uint32_t tpt, GOffer* out, uint32_t* via) {
   const uint32_t v = G.edge_src[ej];
-  if (!T.edge_mode && v == T.root) {
-    *out = 0ull;
+  if (!T.edge_mode) {
+    const int sl = g_find(key, cap, v);
+    if (sl < 0) return false;
+    const unsigned long long L = ld_u64(&lab[sl]);
+    if (L == kGInf) return false;
+    GOffer o;
+    o.c = 0;
+    o.d = g_d(L) + tpart;
+    o.k = o.d;
+    o.t = T.time_on ? g_t(L) + tpt : 0u;
+    *out = o;
     *via = kEmpty;
-    return true;
+    return g_feasible(T, o);
   }
   bool found = false;
   unsigned long long best = kGInf;
   uint32_t bid = kEmpty;
+  GOffer bo{};
   for (uint32_t r = G.rev_row[v]; r < G.rev_row[v + 1]; ++r) {
     const uint32_t a = G.rev_edge[r];
     const int sl = g_find(key, cap, a);
     if (sl < 0) continue;
-    unsigned long long k = ld_u64(&lab[sl]);
-    if (k == kGInf) continue;
-    if (T.edge_mode) {
-      const uint32_t x = g_c(k) + (uint32_t)T.turn[turn_degree(G.edge_head[a].y, G.edge_head[ej].x)];
-      k = (k & ~0x3FFFFFull) | (x < kTcCap ? x : kTcCap);
-    }
-    if (!found || k < best || (k == best && a < bid)) {
-      best = k;
+    const unsigned long long L = ld_u64(&lab[sl]);
+    if (L == kGInf) continue;
+    GOffer o;
+    o.c = g_c(L) + (uint32_t)T.turn[turn_degree(G.edge_head[a].y, G.edge_head[ej].x)];
+    o.d = g_d(L) + tpart;
+    o.k = o.d + o.c;
+    o.t = T.time_on ? g_t(L) + tpt : 0u;
+    if (!g_feasible(T, o)) continue;
+    const unsigned long long w = gpack(o.k, o.c, o.t);
+    if (!found || w < best || (w == best && a < bid)) {
+      best = w;
       bid = a;
+      bo = o;
       found = true;
     }
   }
-  *out = best;
+  *out = bo;
   *via = bid;
   return found;
 }
 
-__device__ inline GTask g_task(const DevGraph& G, const GenArgs& a, int64_t s, int64_t sp, uint32_t ei) {
+// the task of source candidate ei (node mode: the group's common root dst(ei)); the
+// relative bounds use the exit part d0 (node mode: the group's smallest) and exit time t0
+__device__ inline GTask g_task(const DevGraph& G, const GenArgs& a, int64_t s, int64_t sp, uint32_t ei, uint32_t d0,
+                               uint32_t t0) {
   GTask T;
   T.s = s;
   T.sp = sp;
@@ -291,13 +378,16 @@ __device__ inline GTask g_task(const DevGraph& G, const GenArgs& a, int64_t s, i
   T.root = T.edge_mode ? ei : G.edge_dst[ei];
   T.et = G.et(md);
   T.turn = a.turn + 181 * md;
+  T.pd = T.bmm >= d0 ? T.bmm - d0 : 0u;
+  T.pt = !T.time_on ? 0xFFFFFFFFu : (t0 <= (uint32_t)T.bt ? (uint32_t)T.bt - t0 : 0u);
   return T;
 }
 
-// reset the claimed slots of a slab (workgroup-wide), ready for the next task
+// reset the claimed slots of a slab (workgroup-wide), ready for the next search
 __device__ inline void g_reset(uint32_t* key, unsigned long long* lab, uint32_t* qmark, const uint32_t* touched,
-                               uint32_t n_touched, uint32_t cap) {
-  const uint32_t n = n_touched < cap ? n_touched : cap;
+                               GShared* sh, uint32_t cap) {
+  __syncthreads();
+  const uint32_t n = sh->touched < cap ? sh->touched : cap;
   for (uint32_t i = threadIdx.x; i < n; i += kGenThreads) {
     const uint32_t sl = touched[i];
     key[sl] = kEmpty;
@@ -306,10 +396,17 @@ __device__ inline void g_reset(uint32_t* key, unsigned long long* lab, uint32_t*
   }
   __threadfence_block();
   __syncthreads();
+  if (threadIdx.x == 0) sh->touched = 0;
+  __syncthreads();
+}
+
+// a feasible root: the sources' exit parts keep both bounds
+__device__ inline bool g_root_ok(const GTask& T, uint32_t d0, uint32_t t0) {
+  return d0 <= T.bmm && (!T.time_on || t0 <= (uint32_t)T.bt);
 }
 
 __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, GSlabs S) {
-  __shared__ uint32_t s_n[2], s_touched, s_ovf;
+  __shared__ GShared sh;
   __shared__ uint32_t s_path[1];
   const uint32_t cap = S.cap;
   uint32_t* key = S.key + (size_t)blockIdx.x * cap;
@@ -319,32 +416,65 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
   uint32_t* touched = S.touched + (size_t)blockIdx.x * cap;
   const int64_t count = (int64_t)*a.list_count;
   const int tid = threadIdx.x;
+  if (tid == 0) sh.touched = 0;  // the slab is clean (cleared at allocation, reset after every search)
+  __syncthreads();
+  // one search (label-correcting, then exact if it may have kept a withdrawn label),
+  // leaving its labels in the slab; false on slab overflow
+  auto run = [&](const GTask& T, unsigned long long* work) -> bool {
+    bool stale = false;
+    bool ok = g_search(G, T, false, key, lab, qmark, fr, touched, cap, &sh, &stale, work);
+    if (ok && stale) {
+      g_reset(key, lab, qmark, touched, &sh, cap);
+      ok = g_search(G, T, true, key, lab, qmark, fr, touched, cap, &sh, &stale, work);
+    }
+    return ok;
+  };
   for (int64_t k = blockIdx.x; k < count; k += gridDim.x) {
     const int64_t item = a.list[k];
     if (a.mode == 0) {
-      // ---- route task: transitions of every source sharing the root node; with turn
-      // costs (edge mode) every source edge is its own root: one search each
+      // ---- route task: transitions of every source of the task.  Node mode: one search
+      // from the common root per group of sources with equal exit times (the time bound
+      // prunes each group at its own bt - t0; the length bound at B - the group's smallest
+      // exit part); turn costs: the task has one source edge
       const int64_t s = a.task_state[item];
       const unsigned long long mask = a.task_mask[item];
       const int64_t sp = a.prev[s];
-      GTask T = g_task(G, a, s, sp, a.cand_edge[sp * OTR_KMAX + (__ffsll((long long)mask) - 1)]);
+      const int Kb = a.cand_count[s];
       bool ok = true;
       for (unsigned long long todo = mask; todo && ok;) {
-        const int ia = __ffsll((long long)todo) - 1;
-        const unsigned long long grp = T.edge_mode ? (1ull << ia) : todo;
-        todo &= ~grp;
-        if (T.edge_mode) T.root = a.cand_edge[sp * OTR_KMAX + ia];
-        if (grp != mask) {  // a later source: a fresh slab
-          __syncthreads();
-          g_reset(key, lab, qmark, touched, s_touched, cap);
+        const int i0 = __ffsll((long long)todo) - 1;
+        const bool timed = a.bt[s] >= 0;
+        const uint32_t t0 = timed ? a.cprep_t[sp * OTR_KMAX + i0].y : 0u;
+        unsigned long long grp = 0;
+        uint32_t d0 = 0xFFFFFFFFu;
+        for (unsigned long long m = todo; m; m &= m - 1) {
+          const int i = __ffsll((long long)m) - 1;
+          if (timed && a.cprep_t[sp * OTR_KMAX + i].y != t0) continue;
+          grp |= 1ull << i;
+          const uint32_t w = a.cprep[sp * OTR_KMAX + i].w;
+          d0 = w < d0 ? w : d0;
         }
-        ok = g_search(G, T, key, lab, qmark, fr, touched, cap, s_n, &s_touched, &s_ovf, a.counters);
+        todo &= ~grp;
+        const GTask T = g_task(G, a, s, sp, a.cand_edge[sp * OTR_KMAX + i0], d0, t0);
+        bool need = false;
+        for (int j = 0; j < Kb && !need; ++j) {
+          const uint32_t ej = a.cand_edge[s * OTR_KMAX + j];
+          const double pj = a.cand_p[s * OTR_KMAX + j];
+          for (unsigned long long m = grp; m; m &= m - 1) {
+            const int i = __ffsll((long long)m) - 1;
+            if (!(ej == a.cand_edge[sp * OTR_KMAX + i] && pj >= a.cand_p[sp * OTR_KMAX + i])) need = true;
+          }
+        }
+        bool searched = false;
+        if (need && g_root_ok(T, d0, t0)) {
+          ok = run(T, a.counters);
+          searched = true;
+        }
         if (!ok) break;
-        const int Kb = a.cand_count[s];
-        if (a.counters && tid == 0) {  // kinds 5 transition entries, 6 searches
-          const int sh = cshard();
-          atomicAdd(&a.counters[5 * kCShards + sh], (unsigned long long)Kb * (unsigned long long)__popcll(grp));
-          atomicAdd(&a.counters[6 * kCShards + sh], 1ull);
+        if (a.counters && tid == 0 && searched) {  // kinds 5 transition entries, 6 searches
+          const int shd = cshard();
+          atomicAdd(&a.counters[5 * kCShards + shd], (unsigned long long)Kb * (unsigned long long)__popcll(grp));
+          atomicAdd(&a.counters[6 * kCShards + shd], 1ull);
         }
         uint32_t* trow = a.trans + a.trans_off[s];
         uint32_t* crow = a.trans_tc + a.trans_off[s];
@@ -353,9 +483,9 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
           const double pj = a.cand_p[s * OTR_KMAX + j];
           const uint4 cj = a.cprep[s * OTR_KMAX + j];
           const uint2 cjt = a.cprep_t[s * OTR_KMAX + j];
-          unsigned long long L;
+          GOffer o;
           uint32_t via;
-          const bool reached = g_node_key(G, T, key, lab, cap, ej, &L, &via);
+          const bool reached = searched && g_target(G, T, key, lab, cap, ej, cj.x, cjt.x, &o, &via);
           for (unsigned long long m = grp; m; m &= m - 1) {
             const int i = __ffsll((long long)m) - 1;
             const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
@@ -366,17 +496,16 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
               rd = part_mm(pj - pi, G.len_mm[ei]);
               rt = T.time_on ? part_mm(pj - pi, T.et[ei]) : 0;
             } else if (reached) {
-              const uint4 ci = a.cprep[sp * OTR_KMAX + i];
-              const uint2 cit = a.cprep_t[sp * OTR_KMAX + i];
-              rd = (int64_t)ci.w + g_d(L) + cj.x;
-              rt = T.time_on ? (int64_t)cit.y + g_t(L) + cjt.x : 0;
-              rc = g_c(L);
+              rd = (int64_t)a.cprep[sp * OTR_KMAX + i].w + o.d;
+              rt = T.time_on ? (int64_t)t0 + o.t : 0;
+              rc = o.c;
             }
             const bool valid = rd >= 0 && rd <= (int64_t)T.bmm && (!T.time_on || rt <= (int64_t)T.bt);
             trow[(int64_t)i * Kb + j] = valid ? (uint32_t)rd : kNoRoute;
-            if (T.edge_mode) crow[(int64_t)i * Kb + j] = rc;  // allocated for turn modes only
+            if (T.edge_mode) crow[(int64_t)i * Kb + j] = valid ? rc : 0u;  // allocated for turn modes only
           }
         }
+        g_reset(key, lab, qmark, touched, &sh, cap);
       }
       if (ok) {
         if (tid == 0) a.flag[item] = 0;
@@ -385,13 +514,15 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
         atomicAdd(a.n_overflow, 1ull);
       }
     } else {
-      // ---- winner path of a step: search from the winner's root, then walk back
+      // ---- winner path of a step: search from the winner, then walk back
       const int64_t s = a.steps[item];
       const int64_t sp = a.prev[s];
       const int wi = a.winner[sp], wj = a.winner[s];
       const uint32_t ei = a.cand_edge[sp * OTR_KMAX + wi], ej = a.cand_edge[s * OTR_KMAX + wj];
-      const GTask T = g_task(G, a, s, sp, ei);
-      const bool ok = g_search(G, T, key, lab, qmark, fr, touched, cap, s_n, &s_touched, &s_ovf, nullptr);
+      const double pj = a.cand_p[s * OTR_KMAX + wj];
+      const uint4 ci = a.cprep[sp * OTR_KMAX + wi], cj = a.cprep[s * OTR_KMAX + wj];
+      const GTask T = g_task(G, a, s, sp, ei, ci.w, a.cprep_t[sp * OTR_KMAX + wi].y);
+      const bool ok = run(T, nullptr);
       if (!ok) {
         if (tid == 0) {
           a.flag[item] = 1;
@@ -404,26 +535,25 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
         if (tid == 0) {
           int n = 0;
           bool good = true;
-          unsigned long long L;
-          uint32_t e;
           if (!T.edge_mode) {
-            // node labels: at v, the smallest-id in-edge whose state label is v's label
+            // node labels: at v, the smallest-id in-edge whose tail's label plus the edge is
+            // exactly v's label (oracle walk_path)
             uint32_t v = G.edge_src[ej];
-            const uint32_t S0 = T.root;
-            while (v != S0) {
+            while (v != T.root) {
+              const int sv = g_find(key, cap, v);
+              const unsigned long long Lv = sv >= 0 ? ld_u64(&lab[sv]) : kGInf;
               uint32_t best = kEmpty;
-              unsigned long long bl = kGInf;
-              for (uint32_t r = G.rev_row[v]; r < G.rev_row[v + 1]; ++r) {
+              for (uint32_t r = G.rev_row[v]; r < G.rev_row[v + 1] && Lv != kGInf; ++r) {
                 const uint32_t x = G.rev_edge[r];
-                const int sl = g_find(key, cap, x);
-                if (sl < 0) continue;
-                const unsigned long long k2 = ld_u64(&lab[sl]);
-                if (k2 < bl || (k2 == bl && x < best)) {
-                  bl = k2;
-                  best = x;
-                }
+                if (!(G.edge_attr[x] & T.mode_bit) || x >= best) continue;
+                const int su = g_find(key, cap, G.edge_src[x]);
+                if (su < 0) continue;
+                const unsigned long long Lu = ld_u64(&lab[su]);
+                if (Lu == kGInf) continue;
+                const GOffer o = g_offer(G, T, kEmpty, Lu, x);
+                if (g_feasible(T, o) && gpack(o.k, o.c, o.t) == Lv) best = x;
               }
-              if (best == kEmpty || bl == kGInf || n >= (int)cap) {
+              if (best == kEmpty || n >= (int)cap) {
                 good = false;
                 break;
               }
@@ -431,7 +561,9 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
               v = G.edge_src[best];
             }
           } else {
-            good = g_node_key(G, T, key, lab, cap, ej, &L, &e);
+            GOffer o;
+            uint32_t e;
+            good = g_target(G, T, key, lab, cap, ej, cj.x, a.cprep_t[s * OTR_KMAX + wj].x, &o, &e);
             while (good && e != ei) {
               if (n >= (int)cap) {
                 good = false;
@@ -444,22 +576,13 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
               uint32_t best = kEmpty;
               for (uint32_t r = G.rev_row[v]; r < G.rev_row[v + 1]; ++r) {
                 const uint32_t p = G.rev_edge[r];
+                if (p >= best) continue;
                 const int sp2 = g_find(key, cap, p);
                 if (sp2 < 0) continue;
                 const unsigned long long Lp = ld_u64(&lab[sp2]);
                 if (Lp == kGInf) continue;
-                // Lp + step(p -> e) == La ?
-                const uint32_t nd = g_d(Lp) + G.len_mm[e];
-                uint32_t nt = 0, nc = 0;
-                if (T.time_on) {
-                  const uint32_t x = g_t(Lp) + T.et[e];
-                  nt = x < kTCap ? x : kTCap;
-                }
-                {
-                  const uint32_t x = g_c(Lp) + (uint32_t)T.turn[turn_degree(G.edge_head[p].y, G.edge_head[e].x)];
-                  nc = x < kTcCap ? x : kTcCap;
-                }
-                if (nd <= 0x1FFFFFFu && gpack(nd, nt, nc) == La && p < best) best = p;
+                const GOffer q = g_offer(G, T, p, Lp, e);
+                if (g_feasible(T, q) && gpack(q.k, q.c, q.t) == La) best = p;
               }
               if (best == kEmpty) {
                 good = false;
@@ -468,6 +591,7 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
               e = best;
             }
           }
+          (void)pj;
           s_path[0] = good ? (uint32_t)n : 0xFFFFFFFFu;
         }
         __threadfence_block();
@@ -499,8 +623,7 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
         }
       }
     }
-    __syncthreads();
-    g_reset(key, lab, qmark, touched, s_touched, cap);
+    g_reset(key, lab, qmark, touched, &sh, cap);
   }
 }
 

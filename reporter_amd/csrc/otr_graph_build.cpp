@@ -244,12 +244,14 @@ int otr_flatten(const otr_flat_graph* in, const char* out_path, otr_flat_stats* 
         dsu.unite(src[e], dst[e]);
         any = true;
       }
-    // edges inside one cluster vanish; their segment flags move to the same segment's
-    // neighbouring edge; the others are re-attached to the clusters' representatives
+    // edges inside one cluster vanish (short ones, and those whose distinct end nodes
+    // merged); their segment flags move to the same segment's neighbouring edge; the
+    // others — a true self-loop (a loop road) of 5 cm or more included — are re-attached
+    // to the clusters' representatives
     for (uint32_t e = 0; e < E; ++e) {
       if (!alive[e]) continue;
       const uint32_t s = dsu.find(src[e]), d = dsu.find(dst[e]);
-      if (s == d) {
+      if (s == d && (in->edge_src[e] != in->edge_dst[e] || shape_len(shp[e]) < kMinEdgeM)) {
         alive[e] = 0;
         ++n_contracted;
         const uint32_t sg = in->edge_seg ? in->edge_seg[e] : OTR_NO_SEGMENT;

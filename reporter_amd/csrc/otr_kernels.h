@@ -519,12 +519,10 @@ struct SearchLds {
   // nodes settled per round (at most); k_paths (PRED) reuses pend + work as CAP u32 words
   static constexpr int WCAP = CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : 128));
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
-  WorkE<W> work[WCAP];                // this round's settled nodes: {node, label}
+  WorkE<W> work[WCAP];                // this round's settled nodes: {node | kAgain, label}
+  uint16_t rt[CAP];                   // time of the label the node was last relaxed with (0xFFFF: >= 65535)
+  uint16_t wt[WCAP];                  // this round's settled nodes: rt before this relaxation
   int n_pend, n_keys, overflow;
-  // PRED: 1 when a second in-edge reached the node with its label (a tie the turn costs
-  // of an edge-based route would decide; never cleared, so it may also flag a label
-  // that later improved — only ever sending a path to the edge-based search)
-  uint8_t tie[PRED ? CAP : 1];
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
@@ -535,7 +533,10 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 // u reaches T with length >= L(u) + h(u) - h(T)): the stored value only
 // orders the search.  The relaxing lanes' own improvements still report exact f.
 __device__ inline uint16_t hq_of(uint32_t h) { return (uint16_t)((h >> 6) < 65535u ? (h >> 6) : 65535u); }
-constexpr uint32_t kInq = 0x80000000u;
+constexpr uint32_t kInq = 0x80000000u;   // key bit: the node is on the pending list
+constexpr uint32_t kRel = 0x40000000u;   // key bit: the node has been relaxed (settled) before
+constexpr uint32_t kNodeMask = 0x3FFFFFFFu;
+constexpr uint32_t kAgain = 0x80000000u; // WorkE::node bit: settled before (a re-relaxation)
 constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
 constexpr uint32_t kNoRoute = 0xFFFFFFFFu;  // transition array: no valid route within the bound
 
@@ -618,7 +619,7 @@ __device__ inline int lds_find(const SearchLds<CAP, LM>& L, uint32_t node) {
   for (int probe = 0; probe < CAP; ++probe) {
     const uint32_t k = L.key[h];
     if (k == kEmpty) return -1;
-    if ((k & ~kInq) == node) return (int)h;
+    if ((k & kNodeMask) == node) return (int)h;
     h = h + 1 == (uint32_t)CAP ? 0u : h + 1;
   }
   return -1;
@@ -637,7 +638,7 @@ __device__ inline int lds_insert(SearchLds<CAP, LM>& L, uint32_t node, bool* isn
       *isnew = true;
       return (int)h;
     }
-    if ((k & ~kInq) == node) {
+    if ((k & kNodeMask) == node) {
       *isnew = false;
       return (int)h;
     }
@@ -649,13 +650,11 @@ __device__ inline int lds_insert(SearchLds<CAP, LM>& L, uint32_t node, bool* isn
 
 template <int CAP, int LM, int G = 1>
 __device__ inline void search_init(SearchLds<CAP, LM>* Ls) {
-  constexpr bool PRED = LM == 1;
   for (int q = 0; q < G; ++q) {
     SearchLds<CAP, LM>& L = Ls[q];
     for (int k = threadIdx.x; k < CAP; k += OTR_WAVE) {
       L.key[k] = kEmpty;
       L.lab[k] = LabelT<LM>::kInf;
-      if (PRED) L.tie[k] = 0;
     }
     if (threadIdx.x == 0) {
       L.n_pend = 0;
@@ -693,19 +692,19 @@ __host__ __device__ inline bool pack_fits(uint32_t bmm, uint32_t sh) {
 // Target (lane) resolved?  Every path through a pending node u reaches T with length >=
 // L(u) + h(u) - h(T) >= fmin - h(T), so L(T) + h(T) < fmin makes T's label final (its
 // length is strictly shorter than any path not yet found, so its time is final too);
-// if even min(L(T), fmin - h(T)) cannot make d0 + L + tpart fit the bound, T is
-// unreachable for every source of the task.  Integer arithmetic: no rounding margins needed.
+// if even min(L(T), fmin - h(T)) cannot make L + tpart fit the relative bound pd (= B -
+// the sources' smallest exit part), T is unreachable for every source of the task.
+// Integer arithmetic: no rounding margins needed.
 template <int CAP, int LM>
 __device__ inline bool target_resolved(const SearchLds<CAP, LM>& L, const Pack& K, int tslot, uint32_t tpart,
-                                       uint32_t hT, uint32_t d0min, uint32_t bound_mm, uint32_t fmin,
-                                       bool pend_empty) {
+                                       uint32_t hT, uint32_t pd, uint32_t fmin, bool pend_empty) {
   if (tslot < 0 || pend_empty) return true;
   const typename LabelT<LM>::W lw = LabelT<LM>::label(L.lab[tslot]);
   const int64_t lab = lw == LabelT<LM>::kNone ? INT64_MAX / 4 : (int64_t)K.d(lw);
   if (lab + (int64_t)hT < (int64_t)fmin) return true;
   const int64_t rest = (int64_t)fmin - (int64_t)hT;
   const int64_t lb = lab < rest ? lab : rest;
-  return (int64_t)d0min + lb + (int64_t)tpart > (int64_t)bound_mm;
+  return lb + (int64_t)tpart > (int64_t)pd;
 }
 
 // Relax edge (u → dw) with u's packed label pu.  Every relaxing lane evaluates the
@@ -714,20 +713,53 @@ __device__ inline bool target_resolved(const SearchLds<CAP, LM>& L, const Pack& 
 // be writing; the round's minimum over improvements and kept pending nodes is the next
 // round's fmin.  A label improves when its packed word does (a shorter length, or the
 // same length sooner): the node is then pending again.
+//
+// The bounds prune the relaxation: labels are relative to the search
+// root, so a relaxation is dropped when its length exceeds pd (= B - the sources' exit
+// part) or its time exceeds pt (= bt - their exit time).  Length pruning is monotone in
+// the label order (a shorter label never loses an offer its longer predecessor made), time
+// pruning is not: when `again` (u was relaxed before, with a longer but faster label) an
+// offer cut by the time bound may leave the head holding the withdrawn offer's label.
+// Then the head's label is longer than this offer and *stale is set: the task's labels
+// are not the label-setting search's, and the task is re-run in the exact search
+// (k_general).  Without a stale flag every label below the final fmin is exact (the
+// label-setting fixed point).
+template <int CAP, int LM>
+__device__ inline void stale_check(const SearchLds<CAP, LM>& L, const Pack& K, uint32_t node, uint32_t nd,
+                                   bool& stale) {
+  using W = typename LabelT<LM>::W;
+  const int sv = lds_find(L, node);
+  if (sv >= 0) {
+    const W lv = LabelT<LM>::label(L.lab[sv]);
+    if (lv != LabelT<LM>::kNone && K.d(lv) > nd) stale = true;
+  }
+}
+
+// the time-window and stale tests of a relaxation with length nd (within pd) and time tt:
+// a time between the sources' own bounds (ptw, pt] means the shared search is not each
+// source's (the task goes to per-source searches); a pruned offer whose previous one
+// (time t_old + dt of the label last relaxed, 0xFFFF: unknown) was not is the stale case
+__device__ inline bool window_or_stale_chk(uint32_t tt, uint32_t pt, uint32_t ptw, bool again, uint32_t t_old,
+                                           uint32_t dt, bool& stale) {
+  if (tt > ptw && tt <= pt) stale = true;
+  return again && tt > pt && (t_old == 0xFFFFu || t_old + dt <= pt);
+}
+
 template <int CAP, int LM, bool COUNT = true>
 __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack& K, uint32_t dw, uint32_t len_mm,
                                 uint32_t time_ds, int32_t vlat, int32_t vlon, typename LabelT<LM>::W pu, uint32_t edge,
-                                uint32_t bound_mm, uint32_t mode_bit, uint32_t& relaxed, uint32_t& fnext,
-                                bool& isnew) {
-  constexpr bool PRED = LM == 1;
+                                uint32_t pd, uint32_t pt, uint32_t ptw, uint32_t mode_bit, bool again, uint32_t t_old,
+                                uint32_t& relaxed, uint32_t& fnext, bool& isnew, bool& stale) {
   using W = typename LabelT<LM>::W;
   isnew = false;
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
   const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
-  if (nd > bound_mm) return -1;
+  if (nd > pd) return -1;
   const uint32_t tt = K.t(pu) + time_ds;  // both < 2^31
-  const W nw = ((W)nd << K.sh) | (W)(tt < K.tcap() ? tt : K.tcap());
+  if (window_or_stale_chk(tt, pt, ptw, again, t_old, time_ds, stale)) stale_check(L, K, dw & kAdjDstMask, nd, stale);
+  if (tt > pt) return -1;
+  const W nw = ((W)nd << K.sh) | (W)tt;  // tt <= pt <= bt < 2^sh - 1
   const uint32_t h = H(vlat, vlon);
   const int sl = lds_insert<CAP, LM, COUNT>(L, dw & kAdjDstMask, &isnew);
   if (sl < 0) return -1;
@@ -739,8 +771,6 @@ __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack
     fnext = f < fnext ? f : fnext;
     const uint32_t ok = atomicOr(&L.key[sl], kInq);
     if (!(ok & kInq)) return sl;  // newly pending: the caller appends it
-  } else if (PRED && LabelT<LM>::label(nb) == LabelT<LM>::label(old) && nb != old) {
-    L.tie[sl] = 1;
   }
   return -1;
 }
@@ -750,25 +780,27 @@ __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack
 // to do aiming them at its own word of `sink` (a per-wave scratch row in LDS whose values
 // are never read), so the exec-mask bookkeeping of the nested ifs is gone — the scalar
 // unit, which carries it, was the search's busiest issue port.  Only a
-// probe chain past the home slot takes a loop (wave-uniform branch, rare).  Same slots,
-// labels and pending list as relax_one.
+// probe chain past the home slot and a time-pruned re-relaxation take branches
+// (wave-uniform, rare).  Same slots, labels and pending list as relax_one.
 template <int CAP>
 __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heur& H, const Pack& K,
                                  uint32_t dw, uint32_t len_mm, uint32_t time_ds, int32_t vlat, int32_t vlon,
-                                 uint32_t pu, uint32_t bound_mm, uint32_t mode_bit, uint32_t& relaxed,
-                                 uint32_t& fnext, bool& isnew) {
+                                 uint32_t pu, uint32_t pd, uint32_t pt, uint32_t ptw, uint32_t mode_bit, bool again,
+                                 uint32_t t_old, uint32_t& relaxed, uint32_t& fnext, bool& isnew, bool& stale) {
   const bool mode_ok = (((dw >> 28) & 7u) & mode_bit) != 0u;
   relaxed += mode_ok ? 1u : 0u;
   const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
   const uint32_t tt = K.t(pu) + time_ds;
-  const uint32_t nw = (nd << K.sh) | (tt < K.tcap() ? tt : K.tcap());
+  const uint32_t nw = (nd << K.sh) | tt;  // read only where tt <= pt < 2^sh - 1
   const uint32_t node = dw & kAdjDstMask;
-  bool go = mode_ok && nd <= bound_mm;
+  const bool dok = mode_ok && nd <= pd;
+  bool go = dok && tt <= pt;
+  const bool chk = dok && window_or_stale_chk(tt, pt, ptw, again, t_old, time_ds, stale);
   uint32_t* mine = sink + lane_id();
   const uint32_t h0 = hslot<CAP>(node);
   const uint32_t k0 = atomicCAS(go ? &L.key[h0] : mine, kEmpty, node);
   isnew = go && k0 == kEmpty;
-  int sl = (go && (k0 == kEmpty || (k0 & ~kInq) == node)) ? (int)h0 : -1;
+  int sl = (go && (k0 == kEmpty || (k0 & kNodeMask) == node)) ? (int)h0 : -1;
   const bool coll = go && sl < 0;
   if (__ballot(coll) != 0ull) {  // the home slot holds another node: linear probing
     if (coll) {
@@ -781,7 +813,7 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heu
           sl = (int)hh;
           break;
         }
-        if ((k & ~kInq) == node) {
+        if ((k & kNodeMask) == node) {
           sl = (int)hh;
           break;
         }
@@ -797,6 +829,9 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heu
   const uint32_t f = nd + h;
   fnext = (imp && f < fnext) ? f : fnext;
   const uint32_t was = atomicOr(imp ? &L.key[sl] : mine, kInq);
+  if (__ballot(chk) != 0ull) {
+    if (chk) stale_check(L, K, node, nd, stale);
+  }
   return (imp && !(was & kInq)) ? sl : -1;  // newly pending: the caller appends it
 }
 
@@ -804,13 +839,16 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heu
 // rooted at `start` (label 0); lanes gl < n_tgt of the group hold a target node tnode, its
 // heuristic hT and partial length tpart (mm).  active = false: the group idles.  K packs
 // the labels (route time tracked when K.sh > 0, from adj_t / edge_t: the mode's times).
-// Returns false (per lane, group-uniform) on an LDS-table overflow.
+// pd / pt prune the relaxations (relative length and time bounds, relax_one); pd also
+// decides when a target is unreachable.  Returns false (per lane, group-uniform) on an LDS-table overflow; *stale
+// (group-uniform) when a time-pruned re-relaxation may have left a withdrawn label.
 template <int CAP, int LM, int G = 1>
 __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur& H, const Pack& K,
                            uint32_t mode_bit,
-                           bool active, uint32_t start, uint32_t bound_mm, uint32_t delta_mm, uint32_t tnode,
-                           uint32_t tpart, uint32_t hT, uint32_t d0min, int n_tgt, unsigned long long* settled,
-                           unsigned long long* relaxed, unsigned long long* rounds,
+                           bool active, uint32_t start, uint32_t pd, uint32_t pt, uint32_t ptw,
+                           uint32_t delta_mm, uint32_t tnode,
+                           uint32_t tpart, uint32_t hT, int n_tgt, bool* stale_out,
+                           unsigned long long* settled, unsigned long long* relaxed, unsigned long long* rounds,
                            unsigned long long* stamps = nullptr, uint32_t hroot_in = 0xFFFFFFFFu,
                            uint32_t* sink = nullptr) {
   using Gr = Grp<G>;
@@ -820,7 +858,6 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
   // only delays the overflow of the searches that outgrow it)
   constexpr int kMaxKeys = (CAP <= 128 || CAP >= 256) ? (CAP * 7) / 8 : (CAP * 3) / 4;
   const int gl = Gr::gl();
-  constexpr bool PRED = LM == 1;
   using W = typename LabelT<LM>::W;
   SearchLds<CAP, LM>& L = Ls[Gr::g()];
   // h(root): given (the task record, k_tasks), or from the root's coordinates
@@ -851,6 +888,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
   }
   __syncthreads();
   uint32_t my_settled = 0, my_relaxed = 0, my_rounds = 0;
+  bool stale = false;
   unsigned long long cyc[4] = {0, 0, 0, 0};
   uint32_t fmin = hroot;  // 0xFFFFFFFF: nothing pending
   const uint32_t hTm = hT + H.margin;  // h(T) with the evaluation margin (see Heur)
@@ -862,7 +900,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
     const int np = done ? 0 : npend;
     OTR_STAMP(t1);
     const bool res =
-        done || gl >= n_tgt || target_resolved(L, K, tslot, tpart, hTm, d0min, bound_mm, fmin, np == 0);
+        done || gl >= n_tgt || target_resolved(L, K, tslot, tpart, hTm, pd, fmin, np == 0);
     done = done || Gr::mine(__ballot(!res)) == 0ull || np == 0;
     OTR_STAMP(t2);
     cyc[0] += t1 - t0;
@@ -877,13 +915,13 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
       const int k = base + gl;
       const bool in = k < np;
       int sl = 0;
-      uint32_t f = 0, node = 0;
+      uint32_t f = 0, key = 0;
       W lb = 0;
       bool take = false;
       if (in) {
         sl = L.pend[k];
         lb = LabelT<LM>::label(L.lab[sl]);
-        node = L.key[sl] & ~kInq;
+        key = L.key[sl];
         f = K.d(lb) + ((uint32_t)L.hv[sl] << 6);  // < 2^32: labels, h < 2^31
         take = f < theta;
       }
@@ -892,8 +930,16 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
       const unsigned long long mt = __ballot(take), mk = __ballot(in && !take);
       __syncthreads();
       if (take) {
-        L.work[nw + Gr::prefix(mt)] = WorkE<W>{node, lb};
-        atomicAnd(&L.key[sl], ~kInq);
+        // off the pending list and marked relaxed: a later improvement re-relaxes it with
+        // kAgain (relax_one's stale check); the relax phase's atomics on this key come after
+        // the barrier below, so a plain store suffices
+        const uint32_t node = key & kNodeMask;
+        const int wi = nw + Gr::prefix(mt);
+        L.work[wi] = WorkE<W>{node | ((key & kRel) ? kAgain : 0u), lb};
+        if (key & kRel) L.wt[wi] = L.rt[sl];
+        const uint32_t tl = K.t(lb);
+        L.rt[sl] = (uint16_t)(tl < 0xFFFFu ? tl : 0xFFFFu);
+        L.key[sl] = node | kRel;
       } else if (in) {
         L.pend[kept + Gr::prefix(mk)] = (Idx)sl;
         fnext = f < fnext ? f : fnext;
@@ -915,26 +961,30 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
       bool isnew = false;
       if (k < 4 * nw) {
         const WorkE<W> wk = L.work[k >> 2];
+        const uint32_t wnode = wk.node & kAdjDstMask;
+        const bool again = (wk.node & kAgain) != 0u;
+        const uint32_t t_old = again ? L.wt[k >> 2] : 0xFFFFu;
         const int slot = k & 3;
         if (slot == 0) ++my_settled;
         // the mode's route time of the slot (DevGraph::adj_t, one block per mode), loaded
         // ahead of the adjacency record and unconditionally: both loads in flight together
         // (issued after ld16's register barrier it had made every relaxation wait for two
         // global loads in a row)
-        const uint32_t tq = adjt[4 * (size_t)wk.node + slot];
-        const uint4 r = ld16(g.adj + 4 * (size_t)wk.node + slot);
+        const uint32_t tq = adjt[4 * (size_t)wnode + slot];
+        const uint4 r = ld16(g.adj + 4 * (size_t)wnode + slot);
         const uint32_t tt = timed ? tq : 0u;
-        const uint32_t e0 = PRED ? g.node_row[wk.node] : 0u;  // edge id = CSR row start + slot
         if constexpr (LM == 0) {
           if (sink)
-            psl = relax_sink<CAP>(L, sink, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab, bound_mm,
-                                  mode_bit, my_relaxed, fnext, isnew);
+            psl = relax_sink<CAP>(L, sink, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab, pd, pt,
+                                  ptw, mode_bit, again, t_old, my_relaxed, fnext, isnew, stale);
           else
-            psl = relax_one<CAP, LM, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab,
-                                              e0 + slot, bound_mm, mode_bit, my_relaxed, fnext, isnew);
+            psl = relax_one<CAP, LM, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab, 0u,
+                                              pd, pt, ptw, mode_bit, again, t_old, my_relaxed, fnext, isnew, stale);
         } else {
+          const uint32_t e0 = LM == 1 ? g.node_row[wnode] : 0u;  // edge id = CSR row start + slot
           psl = relax_one<CAP, LM, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab,
-                                            e0 + slot, bound_mm, mode_bit, my_relaxed, fnext, isnew);
+                                            e0 + slot, pd, pt, ptw, mode_bit, again, t_old, my_relaxed, fnext, isnew,
+                                            stale);
         }
         tail = tail || (slot == 3 && (r.x & kAdjMore));
       }
@@ -957,14 +1007,17 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
         const int k = base + gl;
         if (k < 4 * nw && (k & 3) == 3) {
           const WorkE<W> wk = L.work[k >> 2];
-          if (g.adj[4 * (size_t)wk.node + 3].x & kAdjMore)
-            for (uint32_t e = g.node_row[wk.node] + 4; e < g.node_row[wk.node + 1]; ++e) {
+          const uint32_t wnode = wk.node & kAdjDstMask;
+          const bool again = (wk.node & kAgain) != 0u;
+          const uint32_t t_old = again ? L.wt[k >> 2] : 0xFFFFu;
+          if (g.adj[4 * (size_t)wnode + 3].x & kAdjMore)
+            for (uint32_t e = g.node_row[wnode] + 4; e < g.node_row[wnode + 1]; ++e) {
               const uint4 pk = ld16(g.edge_pack + e);
               const int2 vll = g.node_ll[pk.x];
               const uint32_t tt = timed ? g.et(__builtin_ctz(mode_bit))[e] : 0u;
               bool isnew;
-              const int psl = relax_one(L, H, K, pk.x | ((pk.z & 7u) << 28), pk.y, tt, vll.x, vll.y, wk.lab, e,
-                                        bound_mm, mode_bit, my_relaxed, fnext, isnew);
+              const int psl = relax_one(L, H, K, pk.x | ((pk.z & 7u) << 28), pk.y, tt, vll.x, vll.y, wk.lab, e, pd, pt,
+                                        ptw, mode_bit, again, t_old, my_relaxed, fnext, isnew, stale);
               if (psl >= 0) {
                 const int p = atomicAdd(&L.n_pend, 1);
                 if (p < CAP) L.pend[p] = (Idx)psl;
@@ -994,6 +1047,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
   if (settled) *settled += my_settled;
   if (relaxed) *relaxed += my_relaxed;
   if (rounds) *rounds += my_rounds;
+  *stale_out = Gr::mine(__ballot(stale)) != 0ull;
   __syncthreads();
   return !L.overflow;
 }
@@ -1020,8 +1074,8 @@ struct PrepArgs {
   uint4* cprep;   // [S][OTR_KMAX]: {part(p), src(e), h(src(e)), part(1 - p)}
   uint2* cprep_t; // [S][OTR_KMAX]: {part_t(p), part_t(1 - p)}: the same parts of the edge's route time
   uint2* clen;    // [S][OTR_KMAX]: {len_mm(e), route time(e)}: a same-edge transition's whole-edge terms
-  int32_t* nroot; // [S]: distinct end nodes dst(e) of the state's candidates = the search
-                  // tasks of the step leaving it
+  int32_t* nroot; // [S]: the search tasks of the step leaving the state (k_tasks' grouping)
+  uint32_t turn_modes;  // bit m: mode m has turn costs (edge-based searches, one per source)
 };
 
 // G states per wave (G = 2 when every mode keeps <= 32 candidates: lane groups of 32;
@@ -1039,8 +1093,9 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
   const double bound = a.prev[s] >= 0 ? a.bound[s] : 0.0;  // set by k_link for steps only
   const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], bound, g.h_scale);
   if (lane == 0) a.heur[s] = H;
+  const int md = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+  const bool turn = (a.turn_modes >> md) & 1u;
   if (lane < K) {
-    const int md = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
     const uint32_t e = a.cand_edge[s * OTR_KMAX + lane];
     const double p = a.cand_p[s * OTR_KMAX + lane];
     const uint32_t len = g.len_mm[e];
@@ -1052,9 +1107,13 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
     a.cprep_t[s * OTR_KMAX + lane] = make_uint2((uint32_t)part_mm(p, et), (uint32_t)part_mm(1.0 - p, et));
     a.clen[s * OTR_KMAX + lane] = make_uint2(len, et);
   }
-  // distinct search roots dst(e) (K <= OTR_KMAX: one candidate per lane): a lane is its
-  // root's first holder when no lower lane has the same root (k_tasks' rule)
-  const uint32_t root = lane < K ? g.edge_dst[a.cand_edge[s * OTR_KMAX + lane]] : 0xFFFFFFFFu;
+  // distinct search tasks (K <= OTR_KMAX: one candidate per lane): a lane is its task's
+  // first holder when no lower lane has the same root (k_tasks' rule)
+  uint32_t root = 0xFFFFFFFFu;
+  if (lane < K) {
+    const uint32_t e = a.cand_edge[s * OTR_KMAX + lane];
+    root = turn ? e : g.edge_dst[e];
+  }
   bool first = lane < K;
   for (int k = 0; k < K; ++k) {
     const uint32_t rk = (uint32_t)__shfl((int)root, k, GL);  // every lane of the group takes part
@@ -1126,6 +1185,7 @@ struct TaskArgs {
   const int32_t* state_trace;
   const uint8_t* mode;
   const uint4* cprep;         // k_prep
+  const uint2* cprep_t;       // k_prep
   const Heur* heur;           // k_prep
   const int64_t* trans_off;
   uint32_t turn_modes;
@@ -1135,18 +1195,19 @@ struct TaskArgs {
 };
 
 // One lane group per step s (G states per wave: G = 2 when every mode keeps <= 32
-// candidates), lane i = source candidate i of the previous state: the sources whose edges
-// end at the same node share a task (the node-based search serves them all; with turn
-// costs too: only the first turn differs, k_route adds it; the edge-based fallback in
-// k_general searches each source edge on its own).  The task's representative (its
-// lowest source) writes task_state, task_mask and the task record k_route reads:
+// candidates), lane i = source candidate i of the previous state.  Node mode: the sources
+// whose edges end at the same node share a task (one search rooted at that node; the
+// length bound prunes it at B - the smallest exit part, which is monotone in the label
+// order, so each source's labels within its own bound are the shared ones; the time
+// bound prunes at bt - the smallest exit time, and a relaxation whose time falls between
+// the sources' own bounds flags the task for per-source searches).  Turn
+// modes: every source edge is its own task (the edge-state search).  The task's representative (its lowest source) writes task_state,
+// task_mask and the task record k_route reads:
 //   rec[3t]   = {s, sp, root, bound_mm}
 //   rec[3t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16 | turn << 17, mask lo, mask hi}
 //   rec[3t+2] = {h(root), time bound bt, trans_off[s] lo, hi}
 // general: the task runs in the global-memory search (a bound whose packed labels would
-// not fit 32 bits).  turn: the mode has turn costs (edge-based semantics): the LDS search
-// runs node-based and the transition rows walk the unique tight in-edges back to the
-// root to add the turns; a tie on the way sends the task to the global-memory search.
+// not fit 32 bits, or a turn mode: edge-based labels).
 template <int G>
 __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
   constexpr int GL = OTR_WAVE / G;
@@ -1157,8 +1218,10 @@ __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
   const int64_t sp = a.prev[s];
   if (sp < 0 || a.cand_count[s] <= 0) return;
   const int Ka = a.cand_count[sp];
+  const int md = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
+  const uint32_t turn = (a.turn_modes >> md) & 1u;
   const uint32_t ce = lane < Ka ? a.cand_edge[sp * OTR_KMAX + lane] : 0xFFFFFFFFu;
-  const uint32_t root = lane < Ka ? a.edge_dst[ce] : 0xFFFFFFFFu;
+  const uint32_t root = lane < Ka ? (turn ? ce : a.edge_dst[ce]) : 0xFFFFFFFFu;
   const uint32_t w = lane < Ka ? a.cprep[sp * OTR_KMAX + lane].w : 0xFFFFFFFFu;  // exit part mm
   // sources sharing my root, their smallest exit part, then: am I the lowest of them?
   unsigned long long same = 0;
@@ -1177,19 +1240,17 @@ __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
   if (o >= a.task_off[s + 1]) return;  // the count (k_prep's nroot) and this rule agree; never write past it
   a.task_state[o] = s;
   a.task_mask[o] = same;
-  const int md = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
   const uint32_t bmm = (uint32_t)bound_mm_of(a.bound[s]);
   const int32_t bt = a.bt[s];
   const uint32_t sh = pack_shift(bt);
 #ifdef OTR_FORCE_GENERAL
   const bool general = true;  // test build: every search in k_general (tests/test_gpu_tiers.py)
 #else
-  const bool general = !pack_fits(bmm, sh);
+  const bool general = !pack_fits(bmm, sh) || turn;
 #endif
-  const uint32_t turn = (a.turn_modes >> md) & 1u;
   const uint32_t meta = (uint32_t)a.cand_count[s] | ((uint32_t)md << 8) | ((a.forced[s] ? 1u : 0u) << 10) |
                         (sh << 11) | ((general ? 1u : 0u) << 16) | (turn << 17);
-  const int2 rll = a.node_ll[root];
+  const int2 rll = a.node_ll[turn ? a.edge_dst[root] : root];
   const uint32_t hroot = a.heur[s](rll.x, rll.y);  // the search's first dependent load, done here
   const int64_t to = a.trans_off[s];
   a.rec[3 * o] = make_uint4((uint32_t)s, (uint32_t)sp, root, bmm);
@@ -1198,43 +1259,8 @@ __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
 }
 
 #ifndef OTR_ROUTE2_WAVES
-#define OTR_ROUTE2_WAVES 8
+#define OTR_ROUTE2_WAVES 7
 #endif
-// LIST = false: the first tier, one unit per block over all tasks (XCD-mapped); LIST =
-// true: a retry tier, a fixed grid striding over the device-side task list (its length
-// never crosses to the host)
-// Turn costs of a node-based route: the edge-based search's label at a
-// target edge ej = the node label of v = src(ej) plus the turn costs along the route,
-// whose choice among equal (length, time) routes is decided by those turn costs.  The
-// TURN kernels search with predecessor labels (label << 32 | smallest in-edge) and tie
-// bits: when no node from v back to the root saw two in-edges reach its label, the route
-// is unique and its turn costs are summed on the walk back along the predecessor edges;
-// a tie anywhere -> false (the task goes to the edge-based global-memory search).
-// *first: the route's first edge out of the root (ej itself when v is the root); *c: the
-// turns after it, saturating.
-template <int CAP>
-__device__ bool turn_walk(const DevGraph& g, const SearchLds<CAP, true>& L, uint32_t v, uint32_t root, uint32_t ej,
-                          const int32_t* turn, uint32_t* first, uint32_t* c) {
-  uint32_t next = ej, acc = 0;
-  int hb_next = g.edge_head[ej].x;
-  for (int hop = 0; hop < CAP && v != root; ++hop) {
-    const int sv = lds_find(L, v);
-    if (sv < 0 || L.tie[sv]) return false;
-    const uint32_t a = (uint32_t)(L.lab[sv] & 0xFFFFFFFFull);
-    if (a == kEmpty) return false;
-    const short2 ha = g.edge_head[a];
-    const uint32_t u = g.edge_src[a];
-    acc += (uint32_t)turn[turn_degree(ha.y, hb_next)];
-    acc = acc < kTcCap ? acc : kTcCap;
-    next = a;
-    hb_next = ha.x;
-    v = u;
-  }
-  if (v != root) return false;
-  *first = next;
-  *c = acc;
-  return true;
-}
 
 // index of the q-th set bit of m (q < popcount(m))
 __device__ inline int nth_set_bit(unsigned long long m, int q) {
@@ -1242,18 +1268,18 @@ __device__ inline int nth_set_bit(unsigned long long m, int q) {
   return __ffsll((long long)m) - 1;
 }
 
-
-// one unit = G search tasks of the wave (ordinal w of the task range or list).  TURN:
-// the batch has turn-cost modes, whose transition rows walk the routes (turn_walk); a
-// batch without them runs the kernel compiled without that code (its register budget
-// belongs to the search).  WIDE: the table keeps 64-bit packed words and takes the
-// tasks whose (length << sh | time) words do not fit 32 bits (`general` in the record)
-template <int CAP, int G, bool LIST, bool TURN, bool WIDE = false, bool CNT = true>
+// one unit = G search tasks of the wave (ordinal w of the task range or list).  LIST =
+// false: the first tier, one unit per block over all tasks (XCD-mapped); LIST = true: a
+// retry tier, a fixed grid striding over the device-side task list (its length never
+// crosses to the host).  WIDE: the table keeps 64-bit packed words and takes the tasks
+// whose (length << sh | time) words do not fit 32 bits (`general` in the record).  The
+// LDS tiers run node-mode tasks; turn-mode (edge-based) tasks are `general` from k_tasks
+// and go to k_general.
+template <int CAP, int G, bool LIST, bool WIDE = false, bool CNT = true>
 __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& a, unsigned long long* counters,
-                                           SearchLds<CAP, TURN ? 1 : (WIDE ? 2 : 0)>* Ls, int64_t w, int64_t n_tasks,
+                                           SearchLds<CAP, WIDE ? 2 : 0>* Ls, int64_t w, int64_t n_tasks,
                                            uint32_t* sink, uint4 (*trec)[3]) {
-  constexpr int LM = TURN ? 1 : (WIDE ? 2 : 0);
-  static_assert(!(TURN && WIDE), "turn-mode tables carry predecessor edges in the low word");
+  constexpr int LM = WIDE ? 2 : 0;
   using Gr = Grp<G>;
   const int lane = Gr::gl();
   const int64_t tw = w * G + Gr::g();
@@ -1263,6 +1289,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   // ---- search inputs (only these stay live through the search)
   bool search, fits, forced;
   uint32_t tnode = kEmpty, tpart = 0, hT = 0, d0min = 0xFFFFFFFFu, root = 0, bmm = 0, mode_bit = 1, hroot = 0;
+  uint32_t pd = 0, pt = 0xFFFFFFFFu, ptw = 0xFFFFFFFFu;  // pruning bounds relative to the root (length, time)
   int Kb;
   Pack K;
   Heur H;
@@ -1286,12 +1313,13 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     const bool general = (r1.y >> 16) & 1u;  // re-read after the search
     // targets are lanes of the group (wider steps go to a G = 1 tier); 32-bit tables leave
     // the tasks whose packed words need 64 bits to the WIDE tier
-    fits = Kb <= Gr::GL && (WIDE || !general);
+    fits = Kb <= Gr::GL && (WIDE || !general) && !((r1.y >> 17) & 1u);
     if (G == 2 && !LIST && r0.w > a.direct_bmm) fits = false;
     mode_bit = 1u << ((r1.y >> 8) & 3u);
     bmm = r0.w;
     root = r0.z;
     d0min = r1.x;
+    const int32_t bt = (int32_t)r2.y;
     uint32_t ej = 0;
     double pj = 0;
     bool needed = false;
@@ -1306,11 +1334,12 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     // the loop by group shuffles: one parallel load instead of a dependent one per source
     const int nsrc = have ? __popcll(mask) : 0;
     const int iq = lane < nsrc ? nth_set_bit(mask, lane) : 0;
-    uint32_t e_q = 0;
+    uint32_t e_q = 0, t_q = 0;
     double p_q = 0;
     if (lane < nsrc) {
       e_q = a.cand_edge[sp * OTR_KMAX + iq];
       p_q = a.cand_p[sp * OTR_KMAX + iq];
+      if (bt >= 0) t_q = a.cprep_t[sp * OTR_KMAX + iq].y;  // exit time
     }
     for (int q = 0; q < nsrc; ++q) {  // group-uniform trip count
       uint32_t ei;
@@ -1325,9 +1354,22 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
       }
       if (lane < Kb && !(ej == ei && pj >= pi)) needed = true;
     }
+    // the bounds relative to the root: B - (smallest exit part) and bt - (smallest exit
+    // time), and the tight time bound bt - (largest exit time) of the window test
+    // (window_or_stale_chk); a task whose exit parts alone break a bound has no route
+    // through the graph (sources past the tight bound: their rows' own test)
+    const uint32_t t0 = Gr::min_u32(lane < nsrc ? t_q : 0xFFFFFFFFu);
+    const uint32_t t0x = ~Gr::min_u32(lane < nsrc ? ~t_q : 0xFFFFFFFFu);
+    bool feasible_root = d0min <= bmm;
+    pd = feasible_root ? bmm - d0min : 0u;
+    if (bt >= 0) {
+      feasible_root = feasible_root && t0 <= (uint32_t)bt;
+      pt = t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
+      ptw = t0x <= (uint32_t)bt ? (uint32_t)bt - t0x : 0u;
+    }
     forced = have && ((r1.y >> 10) & 1u);
     const unsigned long long need_mask = __ballot(needed);
-    search = have && fits && !forced && Gr::mine(need_mask) != 0ull;
+    search = have && fits && !forced && feasible_root && Gr::mine(need_mask) != 0ull;
     H = a.heur[s];
     if (needed) {
       tnode = cq.y;
@@ -1335,30 +1377,26 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     }
   }
   unsigned long long settled = 0, relaxed = 0, rounds = 0;
+  bool stale = false;
   OTR_STAMP(ts_set);
   search_init<CAP, LM, G>(Ls);
-  bool ok = search_run<CAP, LM, G>(Ls, gr, H, K, mode_bit, search, root, bmm,
-                                      (uint32_t)(a.delta * 1000.0), tnode, tpart, hT, d0min, Kb, &settled, &relaxed,
-                                      &rounds, counters ? counters + 16 * kCShards : nullptr, hroot, sink) &&
-            fits;
+  bool ok = search_run<CAP, LM, G>(Ls, gr, H, K, mode_bit, search, root, pd, pt, ptw,
+                                   (uint32_t)(a.delta * 1000.0), tnode, tpart, hT, Kb, &stale, &settled,
+                                   &relaxed, &rounds, counters ? counters + 16 * kCShards : nullptr, hroot, sink) &&
+            fits && !stale;
 #ifdef OTR_FORCE_RETRY
   if (G == 2 && !LIST) ok = false;  // test build: every first-tier task takes the retry tiers
 #endif
   OTR_STAMP(ts_srch);
   SearchLds<CAP, LM>& L = Ls[Gr::g()];
   int64_t lab = -1;
-  if (ok && tnode != kEmpty && !forced) {
+  if (ok && search && tnode != kEmpty && !forced) {
     const int sl = lds_find(L, tnode);
     if (sl >= 0 && LabelT<LM>::label(L.lab[sl]) != LabelT<LM>::kNone) lab = (int64_t)LabelT<LM>::label(L.lab[sl]);
   }
   // ---- transition rows: re-read the step (cached) rather than hold it live through the search
   asm volatile("" ::: "memory");
   uint32_t ntr = 0;  // transition entries this search wrote (K4), for the work counters
-  // turn modes: each target's turn costs come from a walk back along its route
-  // (turn_walk), run once per target with a valid route; a tie anywhere sends the task to
-  // the edge-based global-memory search (flag 3)
-  uint32_t t_first = kEmpty, t_c = 0;
-  bool turn_task = false, tie = false, walked = false;
   if (have && (ok || forced)) {
     const uint4 r0 = trec[Gr::g()][0], r1 = trec[Gr::g()][1], r2 = trec[Gr::g()][2];
     const int64_t s = r0.x;
@@ -1366,8 +1404,6 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     if (search) ntr = (uint32_t)Kb * (uint32_t)__popcll(mask);
     const int64_t sp = r0.y;
     const int32_t bt = (int32_t)r2.y;
-    const int md = (int)((r1.y >> 8) & 3u);
-    turn_task = TURN && !forced && ((r1.y >> 17) & 1u);
     uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
     // sources staged one per lane as in the setup: {index, edge, fraction, exit part mm,
     // exit part time, edge length mm, edge time}, read by group shuffles in the row loop
@@ -1420,42 +1456,24 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
           r = part_mm(pj - pi, li);  // li = len_mm[ei], lti = et(md)[ei] (k_prep)
           if (bt >= 0) rt = part_mm(pj - pi, lti);
         } else if (lab >= 0) {
+          // the target's offer: its node's label plus the entry part, within both bounds
           r = (int64_t)wi + K.d((uint64_t)lab) + tpart;
           if (bt >= 0) rt = (int64_t)ti + K.t((uint64_t)lab) + tpt;
         }
         const bool valid = r >= 0 && r <= (int64_t)bmm && (bt < 0 || rt <= (int64_t)bt);
         trow[(int64_t)i * Kb + lane] = valid ? (uint32_t)r : kNoRoute;
-        if constexpr (TURN) {
-          if (turn_task) {
-            // turn cost of the edge-based route: the source edge into the route's first edge,
-            // then the walk's turns (same edge forward: none)
-            uint32_t tc = 0;
-            if (valid && !(ej == ei && pj >= pi)) {
-              if (!walked) {
-                walked = true;
-                tie = !turn_walk<CAP>(gr, L, tnode, root, ej, a.turn + 181 * md, &t_first, &t_c);
-              }
-              const uint32_t fe = t_first == kEmpty ? ej : t_first;
-              const short2 hs = gr.edge_head[ei], hf = gr.edge_head[fe];
-              tc = (uint32_t)a.turn[181 * md + turn_degree(hs.y, hf.x)] + t_c;
-              tc = tc < kTcCap ? tc : kTcCap;
-            }
-            a.trans_tc[trow - a.trans + (int64_t)i * Kb + lane] = tc;
-          }
-        }
       }
     }
   }
-  if (TURN && turn_task && Gr::mine(__ballot(tie)) != 0ull) {  // the whole task, edge-based
-    tie = true;
-    ok = false;
-  }
-  // general: the global-memory search (flag 3); overflow: retry with a bigger table; a
-  // first-tier search with a long bound (> 1.9 km) that outgrew 160 slots goes straight
-  // to the 1024-slot tier (flag 2)
+  // general (flag 3): the global-memory search; stale (flag 4): the exact search there too;
+  // overflow: retry with a bigger table; a first-tier search with a long bound (> 1.9 km)
+  // that outgrew 160 slots goes straight to the 1024-slot tier (flag 2)
+  // turn modes (flag 5): the edge-state LDS search (otr_edge.h)
   if (have && !ok && !forced && lane == 0) {
-    const bool general = ((a.rec[3 * task + 1].y >> 16) & 1u) || tie;
-    a.overflow_flag[task] = general ? 3 : ((G == 2 && !LIST && bmm > 1900000u) ? 2 : 1);
+    const uint32_t meta = a.rec[3 * task + 1].y;
+    const bool general = ((meta >> 16) & 1u) != 0u, turn = ((meta >> 17) & 1u) != 0u;
+    a.overflow_flag[task] =
+        stale ? 4 : (turn ? 5 : (general ? 3 : ((G == 2 && !LIST && bmm > 1900000u) ? 2 : 1)));
   }
 #ifdef OTR_STAMPS
   if (G == 2 && counters && threadIdx.x == 0) {  // task setup and transition rows, wave cycles
@@ -1471,11 +1489,12 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     relaxed = wave_sum_u32((uint32_t)relaxed);
     rounds = wave_sum_u32((uint32_t)rounds);
     const int nk = have && search ? L.n_keys : 0;
-    unsigned long long kk = 0, ntrw = 0, nsearch = 0;
+    unsigned long long kk = 0, ntrw = 0, nsearch = 0, nstale = 0;
     for (int q = 0; q < G; ++q) {
       kk += (unsigned long long)__builtin_amdgcn_readlane(nk, q * Gr::GL);
       ntrw += (unsigned long long)__builtin_amdgcn_readlane(ntr, q * Gr::GL);
       nsearch += (unsigned long long)__builtin_amdgcn_readlane((int)(have && search), q * Gr::GL);
+      nstale += (unsigned long long)__builtin_amdgcn_readlane((int)(have && stale), q * Gr::GL);
     }
     if (threadIdx.x == 0) {
       const int sh = cshard();
@@ -1485,6 +1504,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
       atomicAdd(&counters[6 * kCShards + sh], nsearch);
       atomicAdd(&counters[13 * kCShards + sh], rounds);
       atomicAdd(&counters[14 * kCShards + sh], kk);
+      atomicAdd(&counters[15 * kCShards + sh], nstale);
     }
   }
 }
@@ -1493,26 +1513,26 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
 // settled / relaxed / round tallies are dead code there: fewer registers and
 // instructions in the search loop); CNT = true: the instrumented launches
 // (OTR_BATCH_ROUTE_WORK) that fill the work counters
-template <int CAP, int G, bool LIST, bool TURN = false, bool WIDE = false, bool CNT = true>
+template <int CAP, int G, bool LIST, bool WIDE = false, bool CNT = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR_ROUTE2_WAVES : 8, G == 2 ? OTR_ROUTE2_WAVES : 8))) void k_route(DevGraph gr, RouteArgs a, unsigned long long* counters) {
-  __shared__ SearchLds<CAP, TURN ? 1 : (WIDE ? 2 : 0)> Ls[G];
+  __shared__ SearchLds<CAP, WIDE ? 2 : 0> Ls[G];
   __shared__ uint4 trec[G][3];  // each group's task record, for its transition rows
 #ifdef OTR_NO_SINK
   uint32_t* sink = nullptr;  // A/B build: the branching relax_one everywhere
 #else
-  __shared__ uint32_t sink_row[OTR_WAVE];  // relax_sink's per-lane scratch words (non-TURN tables)
-  uint32_t* sink = (TURN || WIDE) ? nullptr : sink_row;
+  __shared__ uint32_t sink_row[OTR_WAVE];  // relax_sink's per-lane scratch words (32-bit tables)
+  uint32_t* sink = WIDE ? nullptr : sink_row;
 #endif
   if (!LIST) {  // the first tier: one unit per block, XCD-mapped (no loop: fewer live registers)
     const int64_t n_units = (a.n_tasks + G - 1) / G;
     const int64_t w = xcd_remap(blockIdx.x, (n_units + 7) / 8);
-    if (w < n_units) route_unit<CAP, G, LIST, TURN, WIDE, CNT>(gr, a, counters, Ls, w, a.n_tasks, sink, trec);
+    if (w < n_units) route_unit<CAP, G, LIST, WIDE, CNT>(gr, a, counters, Ls, w, a.n_tasks, sink, trec);
     return;
   }
   const int64_t n_tasks = (int64_t)*a.list_count;
   const int64_t n_units = (n_tasks + G - 1) / G;
   for (int64_t w = blockIdx.x; w < n_units; w += gridDim.x) {
-    route_unit<CAP, G, LIST, TURN, WIDE, CNT>(gr, a, counters, Ls, w, n_tasks, sink, trec);
+    route_unit<CAP, G, LIST, WIDE, CNT>(gr, a, counters, Ls, w, n_tasks, sink, trec);
     __syncthreads();  // the next unit re-initialises the tables
   }
 }
@@ -1798,6 +1818,7 @@ struct PathArgs {
   const double* radius;
   const Heur* heur;            // per state (k_prep)
   const uint4* cprep;          // per state candidate (k_prep)
+  const uint2* cprep_t;        // per state candidate: route-time parts (k_prep)
   const int32_t* bt;           // per state: the step's time bound (0.1 s), -1 none
   uint32_t turn_modes;         // bit m: mode m has turn costs (its paths run in k_general)
   const unsigned long long* n_steps_dev;  // number of steps, on the device
@@ -1834,8 +1855,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
   const int64_t k = have ? (step_list ? step_list[iw] : iw) : 0;
   const int64_t s = have ? a.steps[k] : 0;
   const int64_t sp = have ? a.prev[s] : 0;
-  bool active = false, turn = false;
-  uint32_t S = 0, T = kEmpty, bmm = 0, tpart = 0, hT = 0, d0 = 0, mode_bit = 1;
+  bool active = false;
+  uint32_t S = 0, T = kEmpty, bmm = 0, tpart = 0, hT = 0, d0 = 0, mode_bit = 1, pd = 0, pt = 0xFFFFFFFFu;
   int mode = 0;
   Pack K;
   K.sh = 0;
@@ -1854,9 +1875,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
       const uint32_t r = a.trans[a.trans_off[s] + (int64_t)wi * a.cand_count[s] + wj];
       if (r < bmm) bmm = r;
     }
-    K.sh = pack_shift(a.bt[s]);
+    const int32_t bt = a.bt[s];
+    K.sh = pack_shift(bt);
     if (ej == ei && pj >= pi) {
       if (gl == 0) a.path_len[s] = -1;
+    } else if ((a.turn_modes >> mode) & 1u) {
+      if (gl == 0) a.overflow_flag[k] = 5;  // turn costs: the edge-state search (otr_edge.h)
     } else if (!pack_fits(bmm, K.sh)
 #ifdef OTR_FORCE_GENERAL
                || true
@@ -1864,13 +1888,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
     ) {
       if (gl == 0) a.overflow_flag[k] = 3;  // 64-bit labels: k_general
     } else {
-      // turn modes: the node-based path is the edge-based one when no node on it has a
-      // tie (checked on the walk); otherwise k_general
-      turn = (a.turn_modes >> mode) & 1u;
       active = true;
       mode_bit = 1u << mode;
       const uint4 cs = a.cprep[sp * OTR_KMAX + wi], ct = a.cprep[s * OTR_KMAX + wj];
       d0 = cs.w;
+      // the search from the winner's root, pruned at the bounds relative to it (the
+      // route's length bounds the length: pruning is monotone in length, so every label
+      // on the route is the full step's, route_unit)
+      pd = bmm >= d0 ? bmm - d0 : 0u;
+      if (bt >= 0) {
+        const uint32_t t0 = a.cprep_t[sp * OTR_KMAX + wi].y;
+        pt = t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
+      }
       S = gr.edge_dst[ei];
       T = ct.y;
       H = a.heur[s];
@@ -1879,12 +1908,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
     }
   }
   search_init<CAP, true, G>(Ls);
-  const bool ok = search_run<CAP, true, G>(Ls, gr, H, K, mode_bit, active, S, bmm,
-                                           (uint32_t)(a.delta * 1000.0), gl == 0 ? T : kEmpty, tpart, hT, d0, 1,
-                                           nullptr, nullptr, nullptr);
+  bool stale = false;
+  const bool ok = search_run<CAP, true, G>(Ls, gr, H, K, mode_bit, active, S, pd, pt, pt,
+                                           (uint32_t)(a.delta * 1000.0), gl == 0 ? T : kEmpty, tpart, hT, 1,
+                                           &stale, nullptr, nullptr, nullptr);
   SearchLds<CAP, true>& L = Ls[Gr::g()];
-  if (active && !ok) {
-    if (gl == 0) a.overflow_flag[k] = 1;
+  if (active && (!ok || stale)) {
+    if (gl == 0) a.overflow_flag[k] = stale ? 3 : 1;  // a withdrawn label: the exact search (k_general)
     active = false;
   }
   // walk predecessor edges T → S (the group's lane 0).  The predecessor node of every
@@ -1924,17 +1954,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
         n = -1;
         break;
       }
-      if (turn && L.tie[sv]) {
-        n = -2;  // a tie the turn costs decide: the edge-based search
-        break;
-      }
       ++n;
       v = pn[sv];
     }
   }
   n = __shfl(n, Gr::g() * Gr::GL);
   if (active && n < 0) {
-    if (gl == 0) a.overflow_flag[k] = n == -2 ? 3 : 1;
+    if (gl == 0) a.overflow_flag[k] = 1;
     active = false;
   }
   // bump allocation in one of 64 regions (a single cursor serialises ~1M returning

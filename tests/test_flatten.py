@@ -111,3 +111,32 @@ def test_bad_input_rejected(tmp_path):
     fg.edge_src, fg.edge_dst, fg.edge_attr = e.ctypes.data, bad.ctypes.data, e.ctypes.data
     fg.shape_off, fg.shape_ll = off.ctypes.data, sh.ctypes.data
     assert _lib.lib().otr_flatten(ctypes.byref(fg), str(tmp_path / 'x').encode(), None) != 0
+
+
+def test_self_loops(city, tmp_path):
+    """A true self-loop (a loop road: both ends on one node, 30 m of shape) survives the
+    contraction with its shape; a zero-length self-loop is contracted like any edge under
+    5 cm."""
+    G = GraphFile(city)
+    raw = _raw(G, np.arange(G.n_edges))
+    v = int(G.edge_src[0])
+    la, lo = int(G.node_ll[2 * v]), int(G.node_ll[2 * v + 1])
+    loop = np.array([[la, lo], [la + 200, lo], [la + 200, lo + 200], [la, lo]], np.int32)  # ~2 x 22 m + 31 m
+    dot = np.array([[la, lo], [la, lo]], np.int32)
+    shapes = [raw['shape_ll'][2 * raw['shape_off'][e]:2 * raw['shape_off'][e + 1]].reshape(-1, 2)
+              for e in range(G.n_edges)] + [loop, dot]
+    off = np.zeros(len(shapes) + 1, np.uint32)
+    off[1:] = np.cumsum([len(s) for s in shapes])
+    extra = lambda a, x: np.concatenate([a, np.array(x, a.dtype)])
+    arr = dict(raw, edge_src=extra(raw['edge_src'], [v, v]), edge_dst=extra(raw['edge_dst'], [v, v]),
+               edge_attr=extra(raw['edge_attr'], [G.edge_attr[0] & 0x3FFF] * 2),
+               edge_seg=extra(raw['edge_seg'], [0xFFFFFFFF] * 2), edge_way=extra(raw['edge_way'], [999999] * 2),
+               shape_off=off, shape_ll=np.concatenate(shapes).astype(np.int32).reshape(-1))
+    out = str(tmp_path / 'loops.otrg')
+    st = _flatten(arr, out, G.h['grid_cell_deg'])
+    assert (st.n_nodes, st.n_edges, st.n_contracted_edges) == (G.n_nodes, G.n_edges + 1, 1)
+    F = GraphFile(out)
+    loops = np.flatnonzero((F.edge_src == F.edge_dst) & (F.edge_way == 999999))
+    assert len(loops) == 1
+    e = int(loops[0])
+    assert F.edge_shape[e + 1] - F.edge_shape[e] == 4 and float(F.edge_len[e]) > 60.0

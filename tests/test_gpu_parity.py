@@ -57,26 +57,6 @@ def test_batch_parity(name, cfg, graph_dir, matcher):
     assert got['status'] == 0
 
 
-@pytest.mark.parametrize('name', ['tiny_mixed', 'city_15s', 'metro_15s', 'metro_sparse_60s', 'metro_mixed_modes'])
-def test_step_kernel_parity(name, graph_dir, matcher, monkeypatch):
-    """The multi-root step kernel (otr_route_step.h, OTR_ROUTE_STEP=1: one LDS table per
-    step, a label per root) gives the per-root kernels' transition rows: bit-exact oracle parity."""
-    g, nt, npnt, sr, sig, seed, fb, fp, acc, over = CASES[name]
-    over = dict(over, **CONFIGS['gtt'])
-    path = gen.graph_path(g, graph_dir)
-    M.configure(M.default_config(path, **over))
-    traces = gen.make_traces(path, nt, npnt, sr, sig, seed, fb, fp, acc)
-    monkeypatch.setenv('OTR_ROUTE_STEP', '1')
-    r = matcher.match_batch(traces, copy_out=True)
-    assert int(r.route_tier_code[0]) >= 1000000  # the step kernel ran (route_tier_code 1,000,000 + CAP * 100 + RMAX)
-    got = _lib.result_to_numpy(r)
-    prm = po.params(**{k: float(v) for k, v in over.items()})
-    want = po.match_batch(po.Graph(path), traces, prm, threads=8)
-    errors, stats = compare(got, want)
-    assert not errors, errors
-    assert got['status'] == 0
-
-
 def test_wide_label_tier_parity(graph_dir, matcher):
     """Steps whose packed (length << sh | time) words need more than 32 bits — 120 s between
     states: time bound 2400 ds = 12 time bits, 2 km bound = 21 length bits — run in the

@@ -281,8 +281,8 @@ def test_semantics_gpu_parity(kat, slow, square, opts):
     want = po.match_batch(po.Graph(path), b, po.params(**opts))
     errors, stats = compare(got, want)
     assert not errors, errors
-    # a (length, time) tie the turn costs decide: the LDS tiers hand it to the edge-based
-    # global-memory search (with turn costs), the result equals the oracle either way
+    # routes whose turns decide between equal lengths: turn modes search edge states
+    # (the global-memory search), the result equals the oracle either way
     qpath, qids = square
     M.configure(M.default_config(qpath, **opts))
     b = K.batch([K.trace(K.square_trace(), dt=20)])
@@ -290,7 +290,7 @@ def test_semantics_gpu_parity(kat, slow, square, opts):
     errors, _ = compare(_lib.result_to_numpy(r), po.match_batch(po.Graph(qpath), b, po.params(**opts)))
     assert not errors, errors
     if opts.get('turn_penalty_factor', 1) != 0:
-        assert int(r.route_tier_work[6][0]) > 0  # the tie went to k_general
+        assert int(r.route_tier_work[9][0]) > 0  # turn modes: the edge-state search
     spath, sid = slow
     M.configure(M.default_config(spath, **opts))
     b = K.batch([K.trace(p, dt=4) for p in K.slow_scenarios().values()])
@@ -298,3 +298,40 @@ def test_semantics_gpu_parity(kat, slow, square, opts):
     want = po.match_batch(po.Graph(spath), b, po.params(**opts))
     errors, stats = compare(got, want)
     assert not errors, errors
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('opts', [{}, {'turn_penalty_factor': 0}, {'max_route_time_factor': 0}])
+def test_pruning_semantics_gpu_parity(block, bypass, stale, opts):
+    """The graphs where the route key (length + turn cost) and the pruning during the search
+    decide the answer: bit-exact with the oracle under the deployed options, without turn
+    costs and without a time bound."""
+    from reporter_amd import matcher as M
+    for (path, _), trs, dt in ((block, [K.block_trace()], 10), (bypass, [K.bypass_trace()], 20),
+                               (stale, K.stale_traces(), 20)):
+        M.configure(M.default_config(path, **opts))
+        b = K.batch([K.trace(p, dt=dt) for p in trs])
+        got = M.Matcher().match_batch_numpy(b)
+        want = po.match_batch(po.Graph(path), b, po.params(**opts))
+        errors, stats = compare(got, want)
+        assert not errors, (path, errors)
+
+
+@pytest.mark.gpu
+def test_withdrawn_label_goes_to_exact_search(stale):
+    """The parallel search relaxes U with the fast edge's label before the chain's shorter
+    one arrives: the time-pruned re-relaxation flags the search (counter 15) and the exact
+    global-memory search settles it: the transition from W-S has no route, as in the
+    oracle (the trace continues through the candidate on S-U)."""
+    from reporter_amd import _lib
+    from reporter_amd import matcher as M
+    path, ids = stale
+    M.configure(M.default_config(path, turn_penalty_factor=0))
+    b = K.batch([K.trace(K.stale_traces()[0], dt=20)])
+    r = M.Matcher().match_batch(b, copy_out=True, route_work=True)
+    got = _lib.result_to_numpy(r)
+    want = po.match_batch(po.Graph(path), b, po.params(turn_penalty_factor=0))
+    errors, _ = compare(got, want)
+    assert not errors, errors
+    assert int(r.counters[15]) > 0  # the first tier flagged the search
+    assert int(r.route_tier_work[6][0]) > 0  # k_general ran it
