@@ -106,6 +106,16 @@ __device__ inline bool e_above(unsigned long long L, const EOffer& o) {
   return t > o.t;
 }
 
+// the offer of label lb through a step (turn tc, length len, time tt)
+__device__ inline EOffer e_step(unsigned long long lb, uint32_t tc, uint32_t len, uint32_t tt) {
+  EOffer o;
+  o.c = g_c(lb) + tc;
+  o.d = g_d(lb) + len;
+  o.k = o.d + o.c;
+  o.t = g_t(lb) + tt;
+  return o;
+}
+
 // Relax state (label lb, at node v, end heading ha) through the edge b (head w, length
 // len, time tt, begin / end headings hb / he, access in dw's high bits).  Returns the slot
 // when b became newly pending.
@@ -117,11 +127,8 @@ __device__ inline int e_relax(EdgeLds<CAP>& L, const Heur& H, const int32_t* tur
   isnew = false;
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
-  EOffer o;
-  o.c = g_c(lb) + (uint32_t)turn[turn_degree((int)ha, (int)hb)];
-  o.d = g_d(lb) + len;
-  o.k = o.d + o.c;
-  o.t = g_t(lb) + tt;
+  const uint32_t tc = (uint32_t)turn[turn_degree((int)ha, (int)hb)];
+  const EOffer o = e_step(lb, tc, len, tt);
   if (!e_feasible(o, pd, pt)) {
     if (again) {  // the stale test (relax_one): b holds a label above this pruned offer
       const int sv = e_find(L, b);
@@ -159,11 +166,8 @@ __device__ inline void e_target_offers(EdgeLds<CAP>& L, const int32_t* turn, uns
   while (m) {
     const int q = __ffsll((long long)m) - 1;
     m &= m - 1;
-    EOffer o;
-    o.c = g_c(lb) + (uint32_t)turn[turn_degree((int)ha, (int)L.thb[q])];
-    o.d = g_d(lb) + L.tpart[q];
-    o.k = o.d + o.c;
-    o.t = g_t(lb) + L.tpt[q];
+    const uint32_t tc = (uint32_t)turn[turn_degree((int)ha, (int)L.thb[q])];
+    const EOffer o = e_step(lb, tc, L.tpart[q], L.tpt[q]);
     if (e_feasible(o, pd, pt)) atomicMin(&L.tlab[q], gpack(o.k, o.c, o.t));
     else if (again && e_above(L.tlab[q], o)) stale = true;
   }
@@ -368,7 +372,9 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const Heur& H, c
 // K3e: edge-state route tasks (turn modes), a fixed grid over the device-side list of
 // the tasks flagged 5 (k_route) or 6 (this tier's overflows, for the larger table).
 // ------------------------------------------------------------------------------
-template <int CAP>
+// EXACT: label-setting order (zero_heur, 1 mm rounds) for the tasks flagged 7 (a
+// withdrawn label in the A* tiers); what it cannot hold goes to k_general (3)
+template <int CAP, bool EXACT = false>
 __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, unsigned long long* counters) {
   __shared__ EdgeLds<CAP> L;
   const int64_t n_tasks = (int64_t)*a.list_count;
@@ -409,14 +415,14 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
     const bool search = Kb <= OTR_WAVE && !forced && root_ok && __ballot(needed) != 0ull;
     const uint32_t pd = bmm >= d0 ? bmm - d0 : 0u;
     const uint32_t pt = bt >= 0 && t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
-    const Heur H = a.heur[s];
+    const Heur H = EXACT ? zero_heur(a.heur[s]) : a.heur[s];
     e_init(L);
     bool stale = false;
     unsigned long long settled = 0, relaxed = 0;
     const bool ok = edge_search<CAP>(L, gr, H, a.turn + 181 * md, md, search, ei, gr.edge_dst[ei],
-                                     (uint32_t)(uint16_t)gr.edge_head[ei].y, r2.x, pd, pt, bt >= 0,
-                                     (uint32_t)(a.delta * 1000.0), Kb, tv, hT, tpart, tpt, thb, &stale,
-                                     counters ? &settled : nullptr, counters ? &relaxed : nullptr) &&
+                                     (uint32_t)(uint16_t)gr.edge_head[ei].y, EXACT ? 0u : r2.x, pd, pt, bt >= 0,
+                                     EXACT ? 1u : (uint32_t)(a.delta * 1000.0), Kb, tv, EXACT ? 0u : hT, tpart, tpt,
+                                     thb, &stale, counters ? &settled : nullptr, counters ? &relaxed : nullptr) &&
                     Kb <= OTR_WAVE;
     if (ok && !stale) {
       uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
         a.trans_tc[trow - a.trans + (int64_t)i * Kb + lane] = valid ? rc : 0u;
       }
     } else if (lane == 0) {
-      a.overflow_flag[task] = stale ? 4 : (CAP < 2048 ? 6 : 3);
+      a.overflow_flag[task] = EXACT ? 3 : (stale ? 7 : (CAP < 2048 ? 6 : 3));
     }
     if (counters) {
       settled = wave_sum_u32((uint32_t)settled);
@@ -466,10 +472,12 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
 // first hop from the target takes the smallest a whose offer is the target's label.  The
 // lanes test the in-edges of one node in parallel.
 // ------------------------------------------------------------------------------
-template <int CAP>
+// overflow_flag / stale_flag: the step's flag when the table overflows / a label was
+// withdrawn (7: the exact tier, EXACT = true: label-setting order)
+template <int CAP, bool EXACT = false>
 __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, const int32_t* turn_tab,
                                                    const int64_t* step_list, const unsigned long long* list_count,
-                                                   int32_t fail_flag) {
+                                                   int32_t overflow_flag, int32_t stale_flag) {
   __shared__ EdgeLds<CAP> L;
   __shared__ uint32_t s_rev[CAP];
   const int64_t n_list = (int64_t)*list_count;
@@ -490,13 +498,13 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
     const uint32_t pd = bmm >= d0 ? bmm - d0 : 0u;
     const uint32_t pt = bt >= 0 && t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
     const uint32_t thb = (uint32_t)gr.edge_head[ej].x;
-    const Heur H = a.heur[s];
+    const Heur H = EXACT ? zero_heur(a.heur[s]) : a.heur[s];
     e_init(L);
     bool stale = false;
     const uint32_t hroot = H(gr.node_ll[gr.edge_dst[ei]].x, gr.node_ll[gr.edge_dst[ei]].y);
     const bool ok = edge_search<CAP>(L, gr, H, turn, md, true, ei, gr.edge_dst[ei], (uint32_t)(uint16_t)gr.edge_head[ei].y,
-                                     hroot, pd, pt, bt >= 0, (uint32_t)(a.delta * 1000.0), 1, ct.y, ct.z, ct.x, tpt,
-                                     thb, &stale, nullptr, nullptr);
+                                     hroot, pd, pt, bt >= 0, EXACT ? 1u : (uint32_t)(a.delta * 1000.0), 1, ct.y,
+                                     EXACT ? 0u : ct.z, ct.x, tpt, thb, &stale, nullptr, nullptr);
     const unsigned long long tl = L.tlab[0];
     int n = -1;
     if (ok && !stale && tl != kGInf) {
@@ -553,7 +561,7 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
       }
     }
     if (n < 0) {
-      if (lane == 0) a.overflow_flag[k] = fail_flag;  // overflow / withdrawn label: the next tier
+      if (lane == 0) a.overflow_flag[k] = (ok && stale) ? stale_flag : overflow_flag;  // the next tier
     } else {
       const int shard = (int)(blockIdx.x & (kShards - 1));
       const int64_t region = a.capacity / kShards;

@@ -848,8 +848,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   // device-side counters of the retry lists: [0..7] route tiers, [8] general tier 1,
   // [9] general tier 2, [10] route tasks left unrouted, [11] steps, [12..15] path tiers,
   // [16] path general 1, [17] path general 2, [18] paths left, [19] general overflow
-  // count, [20] cap flag, [24] tasks the first route tier flagged, [25..26] edge-state
-  // route tiers, [27..28] edge-state path tiers, [32..96) path bump cursors
+  // count, [20] cap flag, [21] exact node path tier, [24] tasks the first route tier
+  // flagged, [25..26] edge-state route tiers, [27..28] edge-state path tiers, [29] exact
+  // edge route tier, [30] exact node route tier, [31] exact edge path tier, [32..96) path
+  // bump cursors
   unsigned long long* cnt = need<unsigned long long>(S_MISC, 32 + kShards);
   HIPCHK(hipMemsetAsync(cnt, 0, 8 * (32 + kShards), stream));
   int64_t* list = need<int64_t>(S_LIST, std::max<int64_t>(NT, S));
@@ -1001,9 +1003,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
 #endif
     // turn-mode tasks (flag 5): the edge-state LDS search, 384 then 2048 states; what
     // outgrows it (flag 3) or may have kept a withdrawn label (flag 4) goes on below
+    // slot 9 (bank 1): the edge-state tiers and the exact tiers, timed together
+    if (timing) (void)hipEventRecord(ev[24 + 2 * 9], stream);
     if (turns) {
       out->route_tier_code[9] = 700000 + 384;
-      if (timing) (void)hipEventRecord(ev[24 + 2 * 9], stream);
       for (int et = 0; et < 2; ++et) {
         unsigned long long* c = cnt + 25 + et;
         k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, et == 0 ? 0x20u : 0x40u,
@@ -1015,8 +1018,31 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         if (et == 0) k_route_edge<384><<<4096, 64, 0, stream>>>(g, rb, rcn);
         else k_route_edge<2048><<<512, 64, 0, stream>>>(g, rb, rcn);
       }
-      if (timing) (void)hipEventRecord(ev[24 + 2 * 9 + 1], stream);
+      // what the edge tiers may have settled with a withdrawn label (flag 7): label-setting order
+      {
+        unsigned long long* c = cnt + 29;
+        k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x80u, list, c);
+        RouteArgs rb = ra;
+        rb.task_list = list;
+        rb.list_count = c;
+        k_route_edge<384, true><<<4096, 64, 0, stream>>>(g, rb, rwork ? d_counters + 1 * bank : nullptr);
+      }
     }
+    // node-mode searches that may have kept a withdrawn label (flag 4): the exact tier,
+    // label-setting order in 512-slot tables (the 64-bit-label and turn-mode tasks among
+    // them, and what outgrows it, go on to k_general)
+    {
+      unsigned long long* c = cnt + 30;
+      k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x10u, list, c);
+      RouteArgs rb = ra;
+      rb.task_list = list;
+      rb.list_count = c;
+      rb.exact = 1;
+      if (!out->route_tier_code[9]) out->route_tier_code[9] = 800000 + 512;  // (bank 1: exact + edge-state tiers)
+      if (rwork) k_route<512, 1, true, false, true><<<8192, 64, 0, stream>>>(g, rb, d_counters + 1 * bank);
+      else k_route<512, 1, true, false, false><<<8192, 64, 0, stream>>>(g, rb, nullptr);
+    }
+    if (timing) (void)hipEventRecord(ev[24 + 2 * 9 + 1], stream);
     // everything left — turn-cost (edge-based) tasks, tasks whose labels need 64 bits,
     // overflows of the largest LDS tables, searches that may have kept a withdrawn label
     // (flag 4: k_general's exact mode settles it) — runs in the global-memory search:
@@ -1092,6 +1118,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (S + 1), stream));
       HIPCHK(hipMemsetAsync(cnt + 12, 0, 8 * 9, stream));  // path tier counts, cap flag
       HIPCHK(hipMemsetAsync(cnt + 27, 0, 8 * 2, stream));  // edge-state path tier counts
+      HIPCHK(hipMemsetAsync(cnt + 31, 0, 8, stream));      // edge-state exact path tier count
+      HIPCHK(hipMemsetAsync(cnt + 21, 0, 8, stream));      // exact node path tier count
       HIPCHK(hipMemsetAsync(cnt + 32, 0, 8 * kShards, stream));
       PathArgs pa{};
       pa.steps = steps;
@@ -1146,9 +1174,20 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
           unsigned long long* c = cnt + 27 + et;
           k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, et == 0 ? 0x20u : 0x40u,
                                                                        list, c);
-          if (et == 0) k_paths_edge<384><<<4096, 64, 0, stream>>>(g, pa, d_turn, list, c, 6);
-          else k_paths_edge<2048><<<512, 64, 0, stream>>>(g, pa, d_turn, list, c, 3);
+          if (et == 0) k_paths_edge<384><<<4096, 64, 0, stream>>>(g, pa, d_turn, list, c, 6, 7);
+          else k_paths_edge<2048><<<512, 64, 0, stream>>>(g, pa, d_turn, list, c, 3, 7);
         }
+        unsigned long long* c = cnt + 31;
+        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0x80u, list, c);
+        k_paths_edge<384, true><<<4096, 64, 0, stream>>>(g, pa, d_turn, list, c, 3, 3);
+      }
+      // winners whose search may have kept a withdrawn label (flag 4): label-setting order
+      {
+        unsigned long long* c = cnt + 21;
+        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0x10u, list, c);
+        PathArgs pe = pa;
+        pe.exact = 1;
+        k_paths<512, 1><<<16384, 64, 0, stream>>>(g, pe, list, c);
       }
       // 64-bit labels, the largest-table overflows and what the edge tiers left: k_general
       ga.steps = steps;
@@ -1366,6 +1405,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     for (int t = 1; t < 10; ++t)
       if (out->route_tier_code[t] != 0)
         (void)hipEventElapsedTime(&out->route_tier_ms[t], ev[24 + 2 * t], ev[24 + 2 * t + 1]);
+    (void)hipGetLastError();  // an unrecorded pair must not leave a sticky error for the next call
   }
   // ---- copy-out (tests / JSON path), compacting the capacity layout
   std::vector<int64_t> route_n(T), seg_n(T), way_n(T), rep_n(T), h_cap_off(T + 1);

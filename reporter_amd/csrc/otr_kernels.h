@@ -520,8 +520,6 @@ struct SearchLds {
   static constexpr int WCAP = CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : 128));
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
   WorkE<W> work[WCAP];                // this round's settled nodes: {node | kAgain, label}
-  uint16_t rt[CAP];                   // time of the label the node was last relaxed with (0xFFFF: >= 65535)
-  uint16_t wt[WCAP];                  // this round's settled nodes: rt before this relaxation
   int n_pend, n_keys, overflow;
 };
 
@@ -535,8 +533,10 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 __device__ inline uint16_t hq_of(uint32_t h) { return (uint16_t)((h >> 6) < 65535u ? (h >> 6) : 65535u); }
 constexpr uint32_t kInq = 0x80000000u;   // key bit: the node is on the pending list
 constexpr uint32_t kRel = 0x40000000u;   // key bit: the node has been relaxed (settled) before
-constexpr uint32_t kNodeMask = 0x3FFFFFFFu;
+constexpr uint32_t kTaint = 0x20000000u; // key bit: the label may rest on a withdrawn one (stale_check)
+constexpr uint32_t kNodeMask = 0x0FFFFFFFu;
 constexpr uint32_t kAgain = 0x80000000u; // WorkE::node bit: settled before (a re-relaxation)
+constexpr uint32_t kTsrc = 0x40000000u;  // WorkE::node bit: the settled node is tainted
 constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
 constexpr uint32_t kNoRoute = 0xFFFFFFFFu;  // transition array: no valid route within the bound
 
@@ -724,32 +724,35 @@ __device__ inline bool target_resolved(const SearchLds<CAP, LM>& L, const Pack& 
 // are not the label-setting search's, and the task is re-run in the exact search
 // (k_general).  Without a stale flag every label below the final fmin is exact (the
 // label-setting fixed point).
+// Taint: a head whose label may be a withdrawn offer is tainted and put
+// back on the pending list; a tainted node's relaxations taint every head they improve or
+// equal (relax_one), so every label that may rest on a withdrawn one carries the taint.
+// Untainted labels below the final fmin are exact; a task whose target ends tainted is
+// re-run in the exact tier.  Returns the slot when it became pending.
 template <int CAP, int LM>
-__device__ inline void stale_check(const SearchLds<CAP, LM>& L, const Pack& K, uint32_t node, uint32_t nd,
-                                   bool& stale) {
+__device__ inline int stale_check(SearchLds<CAP, LM>& L, const Pack& K, uint32_t node, uint32_t nd) {
   using W = typename LabelT<LM>::W;
   const int sv = lds_find(L, node);
   if (sv >= 0) {
     const W lv = LabelT<LM>::label(L.lab[sv]);
-    if (lv != LabelT<LM>::kNone && K.d(lv) > nd) stale = true;
+    if (lv != LabelT<LM>::kNone && K.d(lv) > nd) {
+      const uint32_t was = atomicOr(&L.key[sv], kTaint | kInq);
+      if (!(was & kInq)) return sv;
+    }
   }
+  return -1;
 }
 
-// the time-window and stale tests of a relaxation with length nd (within pd) and time tt:
-// a time between the sources' own bounds (ptw, pt] means the shared search is not each
-// source's (the task goes to per-source searches); a pruned offer whose previous one
-// (time t_old + dt of the label last relaxed, 0xFFFF: unknown) was not is the stale case
-__device__ inline bool window_or_stale_chk(uint32_t tt, uint32_t pt, uint32_t ptw, bool again, uint32_t t_old,
-                                           uint32_t dt, bool& stale) {
-  if (tt > ptw && tt <= pt) stale = true;
-  return again && tt > pt && (t_old == 0xFFFFu || t_old + dt <= pt);
-}
+// The stale test (relax_one): a relaxation pruned by the time bound (tt > pt) from a
+// node relaxed before (again) — its earlier, longer label may have made this offer
+// feasibly, and the head may still hold it (a head whose label is longer than this offer).
+__device__ inline bool stale_chk(bool again, uint32_t tt, uint32_t pt) { return again && tt > pt; }
 
 template <int CAP, int LM, bool COUNT = true>
 __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack& K, uint32_t dw, uint32_t len_mm,
                                 uint32_t time_ds, int32_t vlat, int32_t vlon, typename LabelT<LM>::W pu, uint32_t edge,
-                                uint32_t pd, uint32_t pt, uint32_t ptw, uint32_t mode_bit, bool again, uint32_t t_old,
-                                uint32_t& relaxed, uint32_t& fnext, bool& isnew, bool& stale) {
+                                uint32_t pd, uint32_t pt, uint32_t mode_bit, bool again, bool tsrc,
+                                uint32_t& relaxed, uint32_t& fnext, bool& isnew) {
   using W = typename LabelT<LM>::W;
   isnew = false;
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
@@ -757,8 +760,7 @@ __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack
   const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
   if (nd > pd) return -1;
   const uint32_t tt = K.t(pu) + time_ds;  // both < 2^31
-  if (window_or_stale_chk(tt, pt, ptw, again, t_old, time_ds, stale)) stale_check(L, K, dw & kAdjDstMask, nd, stale);
-  if (tt > pt) return -1;
+  if (tt > pt) return stale_chk(again, tt, pt) ? stale_check(L, K, dw & kAdjDstMask, nd) : -1;
   const W nw = ((W)nd << K.sh) | (W)tt;  // tt <= pt <= bt < 2^sh - 1
   const uint32_t h = H(vlat, vlon);
   const int sl = lds_insert<CAP, LM, COUNT>(L, dw & kAdjDstMask, &isnew);
@@ -766,10 +768,13 @@ __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack
   if (isnew) L.hv[sl] = hq_of(h);
   const typename LabelT<LM>::T nb = LabelT<LM>::make(nw, edge);
   const typename LabelT<LM>::T old = atomicMin(&L.lab[sl], nb);
-  if (LabelT<LM>::label(nb) < LabelT<LM>::label(old)) {
+  const bool imp = LabelT<LM>::label(nb) < LabelT<LM>::label(old);
+  if (imp) {
     const uint32_t f = nd + h;
     fnext = f < fnext ? f : fnext;
-    const uint32_t ok = atomicOr(&L.key[sl], kInq);
+  }
+  if (imp || (tsrc && LabelT<LM>::label(nb) == LabelT<LM>::label(old))) {
+    const uint32_t ok = atomicOr(&L.key[sl], kInq | (tsrc ? kTaint : 0u));
     if (!(ok & kInq)) return sl;  // newly pending: the caller appends it
   }
   return -1;
@@ -785,8 +790,8 @@ __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack
 template <int CAP>
 __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heur& H, const Pack& K,
                                  uint32_t dw, uint32_t len_mm, uint32_t time_ds, int32_t vlat, int32_t vlon,
-                                 uint32_t pu, uint32_t pd, uint32_t pt, uint32_t ptw, uint32_t mode_bit, bool again,
-                                 uint32_t t_old, uint32_t& relaxed, uint32_t& fnext, bool& isnew, bool& stale) {
+                                 uint32_t pu, uint32_t pd, uint32_t pt, uint32_t mode_bit, bool again, bool tsrc,
+                                 uint32_t& relaxed, uint32_t& fnext, bool& isnew) {
   const bool mode_ok = (((dw >> 28) & 7u) & mode_bit) != 0u;
   relaxed += mode_ok ? 1u : 0u;
   const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
@@ -795,7 +800,7 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heu
   const uint32_t node = dw & kAdjDstMask;
   const bool dok = mode_ok && nd <= pd;
   bool go = dok && tt <= pt;
-  const bool chk = dok && window_or_stale_chk(tt, pt, ptw, again, t_old, time_ds, stale);
+  const bool chk = dok && stale_chk(again, tt, pt);
   uint32_t* mine = sink + lane_id();
   const uint32_t h0 = hslot<CAP>(node);
   const uint32_t k0 = atomicCAS(go ? &L.key[h0] : mine, kEmpty, node);
@@ -828,11 +833,14 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heu
   const bool imp = go && nw < old;
   const uint32_t f = nd + h;
   fnext = (imp && f < fnext) ? f : fnext;
-  const uint32_t was = atomicOr(imp ? &L.key[sl] : mine, kInq);
+  // a tainted node's offer taints the head it improves or equals (stale_check)
+  const bool mark = imp || (tsrc && go && nw == old);
+  const uint32_t was = atomicOr(mark ? &L.key[sl] : mine, kInq | (tsrc ? kTaint : 0u));
+  int psl = (mark && !(was & kInq)) ? sl : -1;  // newly pending: the caller appends it
   if (__ballot(chk) != 0ull) {
-    if (chk) stale_check(L, K, node, nd, stale);
+    if (chk) psl = stale_check(L, K, node, nd);  // (chk lanes relaxed nothing above)
   }
-  return (imp && !(was & kInq)) ? sl : -1;  // newly pending: the caller appends it
+  return psl;
 }
 
 // G searches per wave, one per lane group, each in its own table Ls[g]: search g is
@@ -845,7 +853,7 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heu
 template <int CAP, int LM, int G = 1>
 __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur& H, const Pack& K,
                            uint32_t mode_bit,
-                           bool active, uint32_t start, uint32_t pd, uint32_t pt, uint32_t ptw,
+                           bool active, uint32_t start, uint32_t pd, uint32_t pt,
                            uint32_t delta_mm, uint32_t tnode,
                            uint32_t tpart, uint32_t hT, int n_tgt, bool* stale_out,
                            unsigned long long* settled, unsigned long long* relaxed, unsigned long long* rounds,
@@ -888,7 +896,6 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
   }
   __syncthreads();
   uint32_t my_settled = 0, my_relaxed = 0, my_rounds = 0;
-  bool stale = false;
   unsigned long long cyc[4] = {0, 0, 0, 0};
   uint32_t fmin = hroot;  // 0xFFFFFFFF: nothing pending
   const uint32_t hTm = hT + H.margin;  // h(T) with the evaluation margin (see Heur)
@@ -935,11 +942,8 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
         // the barrier below, so a plain store suffices
         const uint32_t node = key & kNodeMask;
         const int wi = nw + Gr::prefix(mt);
-        L.work[wi] = WorkE<W>{node | ((key & kRel) ? kAgain : 0u), lb};
-        if (key & kRel) L.wt[wi] = L.rt[sl];
-        const uint32_t tl = K.t(lb);
-        L.rt[sl] = (uint16_t)(tl < 0xFFFFu ? tl : 0xFFFFu);
-        L.key[sl] = node | kRel;
+        L.work[wi] = WorkE<W>{node | ((key & kRel) ? kAgain : 0u) | ((key & kTaint) ? kTsrc : 0u), lb};
+        L.key[sl] = node | kRel | (key & kTaint);
       } else if (in) {
         L.pend[kept + Gr::prefix(mk)] = (Idx)sl;
         fnext = f < fnext ? f : fnext;
@@ -962,8 +966,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
       if (k < 4 * nw) {
         const WorkE<W> wk = L.work[k >> 2];
         const uint32_t wnode = wk.node & kAdjDstMask;
-        const bool again = (wk.node & kAgain) != 0u;
-        const uint32_t t_old = again ? L.wt[k >> 2] : 0xFFFFu;
+        const bool again = (wk.node & kAgain) != 0u, tsrc = (wk.node & kTsrc) != 0u;
         const int slot = k & 3;
         if (slot == 0) ++my_settled;
         // the mode's route time of the slot (DevGraph::adj_t, one block per mode), loaded
@@ -976,15 +979,14 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
         if constexpr (LM == 0) {
           if (sink)
             psl = relax_sink<CAP>(L, sink, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab, pd, pt,
-                                  ptw, mode_bit, again, t_old, my_relaxed, fnext, isnew, stale);
+                                  mode_bit, again, tsrc, my_relaxed, fnext, isnew);
           else
             psl = relax_one<CAP, LM, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab, 0u,
-                                              pd, pt, ptw, mode_bit, again, t_old, my_relaxed, fnext, isnew, stale);
+                                              pd, pt, mode_bit, again, tsrc, my_relaxed, fnext, isnew);
         } else {
           const uint32_t e0 = LM == 1 ? g.node_row[wnode] : 0u;  // edge id = CSR row start + slot
           psl = relax_one<CAP, LM, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab,
-                                            e0 + slot, pd, pt, ptw, mode_bit, again, t_old, my_relaxed, fnext, isnew,
-                                            stale);
+                                            e0 + slot, pd, pt, mode_bit, again, tsrc, my_relaxed, fnext, isnew);
         }
         tail = tail || (slot == 3 && (r.x & kAdjMore));
       }
@@ -1008,8 +1010,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
         if (k < 4 * nw && (k & 3) == 3) {
           const WorkE<W> wk = L.work[k >> 2];
           const uint32_t wnode = wk.node & kAdjDstMask;
-          const bool again = (wk.node & kAgain) != 0u;
-          const uint32_t t_old = again ? L.wt[k >> 2] : 0xFFFFu;
+          const bool again = (wk.node & kAgain) != 0u, tsrc = (wk.node & kTsrc) != 0u;
           if (g.adj[4 * (size_t)wnode + 3].x & kAdjMore)
             for (uint32_t e = g.node_row[wnode] + 4; e < g.node_row[wnode + 1]; ++e) {
               const uint4 pk = ld16(g.edge_pack + e);
@@ -1017,7 +1018,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
               const uint32_t tt = timed ? g.et(__builtin_ctz(mode_bit))[e] : 0u;
               bool isnew;
               const int psl = relax_one(L, H, K, pk.x | ((pk.z & 7u) << 28), pk.y, tt, vll.x, vll.y, wk.lab, e, pd, pt,
-                                        ptw, mode_bit, again, t_old, my_relaxed, fnext, isnew, stale);
+                                        mode_bit, again, tsrc, my_relaxed, fnext, isnew);
               if (psl >= 0) {
                 const int p = atomicAdd(&L.n_pend, 1);
                 if (p < CAP) L.pend[p] = (Idx)psl;
@@ -1047,7 +1048,9 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
   if (settled) *settled += my_settled;
   if (relaxed) *relaxed += my_relaxed;
   if (rounds) *rounds += my_rounds;
-  *stale_out = Gr::mine(__ballot(stale)) != 0ull;
+  // a tainted target: its label may rest on a withdrawn one (the task goes to the exact tier)
+  const bool tainted = tslot >= 0 && (L.key[tslot] & kTaint) != 0u;
+  *stale_out = Gr::mine(__ballot(tainted)) != 0ull;
   __syncthreads();
   return !L.overflow;
 }
@@ -1108,16 +1111,18 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
     a.clen[s * OTR_KMAX + lane] = make_uint2(len, et);
   }
   // distinct search tasks (K <= OTR_KMAX: one candidate per lane): a lane is its task's
-  // first holder when no lower lane has the same root (k_tasks' rule)
-  uint32_t root = 0xFFFFFFFFu;
+  // first holder when no lower lane has the same key (root, exit time) (k_tasks' rule)
+  uint32_t root = 0xFFFFFFFFu, t0 = 0u;
   if (lane < K) {
     const uint32_t e = a.cand_edge[s * OTR_KMAX + lane];
     root = turn ? e : g.edge_dst[e];
+    if (!turn) t0 = (uint32_t)part_mm(1.0 - a.cand_p[s * OTR_KMAX + lane], g.et(md)[e]);
   }
   bool first = lane < K;
   for (int k = 0; k < K; ++k) {
     const uint32_t rk = (uint32_t)__shfl((int)root, k, GL);  // every lane of the group takes part
-    if (k < lane && rk == root) first = false;
+    const uint32_t tk = (uint32_t)__shfl((int)t0, k, GL);
+    if (k < lane && rk == root && tk == t0) first = false;
   }
   const int nr = __popcll(group_bits<G>(__ballot(first)));
   if (lane == 0) a.nroot[s] = nr;
@@ -1166,9 +1171,25 @@ struct RouteArgs {
   uint32_t* trans_tc;         // turn cost (mm) per transition, turn modes only
   double delta;
   double inv_beta[OTR_MODES];
-  int32_t* overflow_flag;     // per task: 1/2 retry in a larger LDS table, 3 the global-memory search
+  int32_t* overflow_flag;     // per task: 1/2 retry in a larger LDS table, 3 the global-memory search,
+                              // 4 the exact tier, 5 / 6 the edge-state tiers
   uint32_t direct_bmm;        // first tier: bounds above this go straight to the retry tiers
+  int exact;                  // the exact tier: label-setting order (no A* heuristic, rounds of 1 mm)
 };
+
+// The exact order of a retry tier for searches flagged 4 (a withdrawn label, relax_one):
+// no heuristic and rounds 1 mm wide settle exactly the pending nodes of the smallest key,
+// whose labels are final (every step adds >= 1 mm) — the oracle's label-setting order,
+// in parallel over ties; no label is ever relaxed twice, so no label is withdrawn.
+__device__ inline Heur zero_heur(const Heur& H) {
+  Heur z = H;
+  z.mx = 0.0f;
+  z.my = 0.0f;
+  z.k = 0.0f;
+  z.c = 0.0f;
+  z.margin = 0u;
+  return z;
+}
 
 // k_tasks' inputs and outputs
 struct TaskArgs {
@@ -1196,12 +1217,11 @@ struct TaskArgs {
 
 // One lane group per step s (G states per wave: G = 2 when every mode keeps <= 32
 // candidates), lane i = source candidate i of the previous state.  Node mode: the sources
-// whose edges end at the same node share a task (one search rooted at that node; the
-// length bound prunes it at B - the smallest exit part, which is monotone in the label
-// order, so each source's labels within its own bound are the shared ones; the time
-// bound prunes at bt - the smallest exit time, and a relaxation whose time falls between
-// the sources' own bounds flags the task for per-source searches).  Turn
-// modes: every source edge is its own task (the edge-state search).  The task's representative (its lowest source) writes task_state,
+// whose edges end at the same node and whose exit parts take the same route time share a
+// task: one search rooted at that node, pruned at bt - that time and at B - the smallest
+// exit part — length pruning is monotone in the label order, so each source's labels
+// within its own length bound are the shared ones.  Turn modes: every
+// source edge is its own task (the edge-state search).  The task's representative (its lowest source) writes task_state,
 // task_mask and the task record k_route reads:
 //   rec[3t]   = {s, sp, root, bound_mm}
 //   rec[3t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16 | turn << 17, mask lo, mask hi}
@@ -1223,12 +1243,15 @@ __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
   const uint32_t ce = lane < Ka ? a.cand_edge[sp * OTR_KMAX + lane] : 0xFFFFFFFFu;
   const uint32_t root = lane < Ka ? (turn ? ce : a.edge_dst[ce]) : 0xFFFFFFFFu;
   const uint32_t w = lane < Ka ? a.cprep[sp * OTR_KMAX + lane].w : 0xFFFFFFFFu;  // exit part mm
-  // sources sharing my root, their smallest exit part, then: am I the lowest of them?
+  const uint32_t t0 = (lane < Ka && !turn) ? a.cprep_t[sp * OTR_KMAX + lane].y : 0u;  // exit part time
+  // sources sharing my task (root, exit time), their smallest exit part, then: am I the
+  // lowest of them?
   unsigned long long same = 0;
   uint32_t d0min = 0xFFFFFFFFu;
   for (int k = 0; k < Ka; ++k) {
     const uint32_t rk = (uint32_t)__shfl((int)root, k, GL), wk = (uint32_t)__shfl((int)w, k, GL);
-    if (rk == root) {
+    const uint32_t tk = (uint32_t)__shfl((int)t0, k, GL);
+    if (rk == root && tk == t0) {
       same |= 1ull << k;
       d0min = wk < d0min ? wk : d0min;
     }
@@ -1289,7 +1312,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   // ---- search inputs (only these stay live through the search)
   bool search, fits, forced;
   uint32_t tnode = kEmpty, tpart = 0, hT = 0, d0min = 0xFFFFFFFFu, root = 0, bmm = 0, mode_bit = 1, hroot = 0;
-  uint32_t pd = 0, pt = 0xFFFFFFFFu, ptw = 0xFFFFFFFFu;  // pruning bounds relative to the root (length, time)
+  uint32_t pd = 0, pt = 0xFFFFFFFFu;  // pruning bounds relative to the root (length, time)
   int Kb;
   Pack K;
   Heur H;
@@ -1339,7 +1362,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     if (lane < nsrc) {
       e_q = a.cand_edge[sp * OTR_KMAX + iq];
       p_q = a.cand_p[sp * OTR_KMAX + iq];
-      if (bt >= 0) t_q = a.cprep_t[sp * OTR_KMAX + iq].y;  // exit time
+      if (bt >= 0) t_q = a.cprep_t[sp * OTR_KMAX + iq].y;  // the task's common exit time
     }
     for (int q = 0; q < nsrc; ++q) {  // group-uniform trip count
       uint32_t ei;
@@ -1354,18 +1377,14 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
       }
       if (lane < Kb && !(ej == ei && pj >= pi)) needed = true;
     }
-    // the bounds relative to the root: B - (smallest exit part) and bt - (smallest exit
-    // time), and the tight time bound bt - (largest exit time) of the window test
-    // (window_or_stale_chk); a task whose exit parts alone break a bound has no route
-    // through the graph (sources past the tight bound: their rows' own test)
-    const uint32_t t0 = Gr::min_u32(lane < nsrc ? t_q : 0xFFFFFFFFu);
-    const uint32_t t0x = ~Gr::min_u32(lane < nsrc ? ~t_q : 0xFFFFFFFFu);
+    // the bounds relative to the root: B - (smallest exit part) and bt - (the task's exit
+    // time); a task whose exit parts alone break a bound has no route through the graph
+    const uint32_t t0 = (uint32_t)__shfl((int)t_q, 0, Gr::GL);
     bool feasible_root = d0min <= bmm;
     pd = feasible_root ? bmm - d0min : 0u;
     if (bt >= 0) {
       feasible_root = feasible_root && t0 <= (uint32_t)bt;
       pt = t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
-      ptw = t0x <= (uint32_t)bt ? (uint32_t)bt - t0x : 0u;
     }
     forced = have && ((r1.y >> 10) & 1u);
     const unsigned long long need_mask = __ballot(needed);
@@ -1375,13 +1394,19 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
       tnode = cq.y;
       hT = cq.z;
     }
+    if (LIST && a.exact) {  // the exact tier: label-setting order
+      H = zero_heur(H);
+      hroot = 0u;
+      hT = 0u;
+    }
   }
   unsigned long long settled = 0, relaxed = 0, rounds = 0;
   bool stale = false;
   OTR_STAMP(ts_set);
   search_init<CAP, LM, G>(Ls);
-  bool ok = search_run<CAP, LM, G>(Ls, gr, H, K, mode_bit, search, root, pd, pt, ptw,
-                                   (uint32_t)(a.delta * 1000.0), tnode, tpart, hT, Kb, &stale, &settled,
+  bool ok = search_run<CAP, LM, G>(Ls, gr, H, K, mode_bit, search, root, pd, pt,
+                                   (LIST && a.exact) ? 1u : (uint32_t)(a.delta * 1000.0), tnode, tpart, hT, Kb,
+                                   &stale, &settled,
                                    &relaxed, &rounds, counters ? counters + 16 * kCShards : nullptr, hroot, sink) &&
             fits && !stale;
 #ifdef OTR_FORCE_RETRY
@@ -1472,8 +1497,9 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   if (have && !ok && !forced && lane == 0) {
     const uint32_t meta = a.rec[3 * task + 1].y;
     const bool general = ((meta >> 16) & 1u) != 0u, turn = ((meta >> 17) & 1u) != 0u;
-    a.overflow_flag[task] =
-        stale ? 4 : (turn ? 5 : (general ? 3 : ((G == 2 && !LIST && bmm > 1900000u) ? 2 : 1)));
+    a.overflow_flag[task] = (LIST && a.exact)
+                                ? 3  // what outgrew the exact tier: k_general (exact mode on a withdrawn label)
+                                : (stale ? 4 : (turn ? 5 : (general ? 3 : ((G == 2 && !LIST && bmm > 1900000u) ? 2 : 1))));
   }
 #ifdef OTR_STAMPS
   if (G == 2 && counters && threadIdx.x == 0) {  // task setup and transition rows, wave cycles
@@ -1823,6 +1849,7 @@ struct PathArgs {
   uint32_t turn_modes;         // bit m: mode m has turn costs (its paths run in k_general)
   const unsigned long long* n_steps_dev;  // number of steps, on the device
   double delta;
+  int exact;                   // the exact path tier (zero_heur): label-setting order
   int64_t* path_off;           // per state
   int32_t* path_len;           // per state; -1 = same-edge step
   uint32_t* path;              // bump-allocated edge list
@@ -1905,16 +1932,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
       H = a.heur[s];
       hT = ct.z;
       tpart = ct.x;
+      if (a.exact) {  // the exact path tier: label-setting order
+        H = zero_heur(H);
+        hT = 0u;
+      }
     }
   }
   search_init<CAP, true, G>(Ls);
   bool stale = false;
-  const bool ok = search_run<CAP, true, G>(Ls, gr, H, K, mode_bit, active, S, pd, pt, pt,
-                                           (uint32_t)(a.delta * 1000.0), gl == 0 ? T : kEmpty, tpart, hT, 1,
-                                           &stale, nullptr, nullptr, nullptr);
+  const bool ok = search_run<CAP, true, G>(Ls, gr, H, K, mode_bit, active, S, pd, pt,
+                                           a.exact ? 1u : (uint32_t)(a.delta * 1000.0), gl == 0 ? T : kEmpty, tpart,
+                                           hT, 1, &stale, nullptr, nullptr, nullptr, nullptr, a.exact ? 0u : 0xFFFFFFFFu);
   SearchLds<CAP, true>& L = Ls[Gr::g()];
   if (active && (!ok || stale)) {
-    if (gl == 0) a.overflow_flag[k] = stale ? 3 : 1;  // a withdrawn label: the exact search (k_general)
+    // a withdrawn label: the exact tier (4); what outgrows that: k_general (3)
+    if (gl == 0) a.overflow_flag[k] = a.exact ? 3 : (stale ? 4 : 1);
     active = false;
   }
   // walk predecessor edges T → S (the group's lane 0).  The predecessor node of every

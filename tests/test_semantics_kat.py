@@ -320,9 +320,10 @@ def test_pruning_semantics_gpu_parity(block, bypass, stale, opts):
 @pytest.mark.gpu
 def test_withdrawn_label_goes_to_exact_search(stale):
     """The parallel search relaxes U with the fast edge's label before the chain's shorter
-    one arrives: the time-pruned re-relaxation flags the search (counter 15) and the exact
-    global-memory search settles it: the transition from W-S has no route, as in the
-    oracle (the trace continues through the candidate on S-U)."""
+    one arrives: the time-pruned re-relaxation taints V, the target's label is tainted, the
+    search is flagged (counter 15) and the exact tier (label-setting order) settles it: the
+    transition from W-S has no route, as in the oracle (the trace continues through the
+    candidate on S-U)."""
     from reporter_amd import _lib
     from reporter_amd import matcher as M
     path, ids = stale
@@ -334,4 +335,4 @@ def test_withdrawn_label_goes_to_exact_search(stale):
     errors, _ = compare(got, want)
     assert not errors, errors
     assert int(r.counters[15]) > 0  # the first tier flagged the search
-    assert int(r.route_tier_work[6][0]) > 0  # k_general ran it
+    assert int(r.route_tier_work[9][0]) > 0  # the exact tier ran it
