@@ -729,15 +729,22 @@ __device__ inline bool target_resolved(const SearchLds<CAP, LM>& L, const Pack& 
 // equal (relax_one), so every label that may rest on a withdrawn one carries the taint.
 // Untainted labels below the final fmin are exact; a task whose target ends tainted is
 // re-run in the exact tier.  Returns the slot when it became pending.
+// The re-queued head's key f enters the next round's fmin (fnext): until its taint has
+// reached its descendants no target resting on them may pass target_resolved.
 template <int CAP, int LM>
-__device__ inline int stale_check(SearchLds<CAP, LM>& L, const Pack& K, uint32_t node, uint32_t nd) {
+__device__ inline int stale_check(SearchLds<CAP, LM>& L, const Pack& K, uint32_t node, uint32_t nd,
+                                  uint32_t& fnext) {
   using W = typename LabelT<LM>::W;
   const int sv = lds_find(L, node);
   if (sv >= 0) {
     const W lv = LabelT<LM>::label(L.lab[sv]);
     if (lv != LabelT<LM>::kNone && K.d(lv) > nd) {
       const uint32_t was = atomicOr(&L.key[sv], kTaint | kInq);
-      if (!(was & kInq)) return sv;
+      if (!(was & kInq)) {
+        const uint32_t f = K.d(lv) + ((uint32_t)L.hv[sv] << 6);
+        fnext = f < fnext ? f : fnext;
+        return sv;
+      }
     }
   }
   return -1;
@@ -752,7 +759,7 @@ template <int CAP, int LM, bool COUNT = true>
 __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack& K, uint32_t dw, uint32_t len_mm,
                                 uint32_t time_ds, int32_t vlat, int32_t vlon, typename LabelT<LM>::W pu, uint32_t edge,
                                 uint32_t pd, uint32_t pt, uint32_t mode_bit, bool again, bool tsrc,
-                                uint32_t& relaxed, uint32_t& fnext, bool& isnew) {
+                                uint32_t& relaxed, uint32_t& fnext, bool& isnew, bool& stale) {
   using W = typename LabelT<LM>::W;
   isnew = false;
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
@@ -760,7 +767,13 @@ __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack
   const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
   if (nd > pd) return -1;
   const uint32_t tt = K.t(pu) + time_ds;  // both < 2^31
-  if (tt > pt) return stale_chk(again, tt, pt) ? stale_check(L, K, dw & kAdjDstMask, nd) : -1;
+  if (tt > pt) {
+    // a tainted label may be shorter but slower than the exact one: its time-pruned offer
+    // may hide an offer the exact search makes (to a head no taint reaches): the task goes
+    // to the exact tier
+    if (tsrc) stale = true;
+    return stale_chk(again, tt, pt) ? stale_check(L, K, dw & kAdjDstMask, nd, fnext) : -1;
+  }
   const W nw = ((W)nd << K.sh) | (W)tt;  // tt <= pt <= bt < 2^sh - 1
   const uint32_t h = H(vlat, vlon);
   const int sl = lds_insert<CAP, LM, COUNT>(L, dw & kAdjDstMask, &isnew);
@@ -769,11 +782,12 @@ __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack
   const typename LabelT<LM>::T nb = LabelT<LM>::make(nw, edge);
   const typename LabelT<LM>::T old = atomicMin(&L.lab[sl], nb);
   const bool imp = LabelT<LM>::label(nb) < LabelT<LM>::label(old);
-  if (imp) {
+  const bool mark = imp || (tsrc && LabelT<LM>::label(nb) == LabelT<LM>::label(old));
+  if (mark) {  // (a head re-queued with the taint holds f too: see stale_check)
     const uint32_t f = nd + h;
     fnext = f < fnext ? f : fnext;
   }
-  if (imp || (tsrc && LabelT<LM>::label(nb) == LabelT<LM>::label(old))) {
+  if (mark) {
     const uint32_t ok = atomicOr(&L.key[sl], kInq | (tsrc ? kTaint : 0u));
     if (!(ok & kInq)) return sl;  // newly pending: the caller appends it
   }
@@ -791,7 +805,7 @@ template <int CAP>
 __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heur& H, const Pack& K,
                                  uint32_t dw, uint32_t len_mm, uint32_t time_ds, int32_t vlat, int32_t vlon,
                                  uint32_t pu, uint32_t pd, uint32_t pt, uint32_t mode_bit, bool again, bool tsrc,
-                                 uint32_t& relaxed, uint32_t& fnext, bool& isnew) {
+                                 uint32_t& relaxed, uint32_t& fnext, bool& isnew, bool& stale) {
   const bool mode_ok = (((dw >> 28) & 7u) & mode_bit) != 0u;
   relaxed += mode_ok ? 1u : 0u;
   const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
@@ -801,6 +815,7 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heu
   const bool dok = mode_ok && nd <= pd;
   bool go = dok && tt <= pt;
   const bool chk = dok && stale_chk(again, tt, pt);
+  if (tsrc && dok && tt > pt) stale = true;  // (relax_one)
   uint32_t* mine = sink + lane_id();
   const uint32_t h0 = hslot<CAP>(node);
   const uint32_t k0 = atomicCAS(go ? &L.key[h0] : mine, kEmpty, node);
@@ -832,13 +847,14 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heu
   const uint32_t old = atomicMin(go ? &L.lab[sl] : mine, nw);
   const bool imp = go && nw < old;
   const uint32_t f = nd + h;
-  fnext = (imp && f < fnext) ? f : fnext;
-  // a tainted node's offer taints the head it improves or equals (stale_check)
+  // a tainted node's offer taints the head it improves or equals (stale_check); a head
+  // re-queued with the taint holds fnext like an improved one
   const bool mark = imp || (tsrc && go && nw == old);
+  fnext = (mark && f < fnext) ? f : fnext;
   const uint32_t was = atomicOr(mark ? &L.key[sl] : mine, kInq | (tsrc ? kTaint : 0u));
   int psl = (mark && !(was & kInq)) ? sl : -1;  // newly pending: the caller appends it
   if (__ballot(chk) != 0ull) {
-    if (chk) psl = stale_check(L, K, node, nd);  // (chk lanes relaxed nothing above)
+    if (chk) psl = stale_check(L, K, node, nd, fnext);  // (chk lanes relaxed nothing above)
   }
   return psl;
 }
@@ -896,6 +912,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
   }
   __syncthreads();
   uint32_t my_settled = 0, my_relaxed = 0, my_rounds = 0;
+  bool stale = false;
   unsigned long long cyc[4] = {0, 0, 0, 0};
   uint32_t fmin = hroot;  // 0xFFFFFFFF: nothing pending
   const uint32_t hTm = hT + H.margin;  // h(T) with the evaluation margin (see Heur)
@@ -979,14 +996,15 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
         if constexpr (LM == 0) {
           if (sink)
             psl = relax_sink<CAP>(L, sink, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab, pd, pt,
-                                  mode_bit, again, tsrc, my_relaxed, fnext, isnew);
+                                  mode_bit, again, tsrc, my_relaxed, fnext, isnew, stale);
           else
             psl = relax_one<CAP, LM, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab, 0u,
-                                              pd, pt, mode_bit, again, tsrc, my_relaxed, fnext, isnew);
+                                              pd, pt, mode_bit, again, tsrc, my_relaxed, fnext, isnew, stale);
         } else {
           const uint32_t e0 = LM == 1 ? g.node_row[wnode] : 0u;  // edge id = CSR row start + slot
           psl = relax_one<CAP, LM, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab,
-                                            e0 + slot, pd, pt, mode_bit, again, tsrc, my_relaxed, fnext, isnew);
+                                            e0 + slot, pd, pt, mode_bit, again, tsrc, my_relaxed, fnext, isnew,
+                                            stale);
         }
         tail = tail || (slot == 3 && (r.x & kAdjMore));
       }
@@ -1018,7 +1036,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
               const uint32_t tt = timed ? g.et(__builtin_ctz(mode_bit))[e] : 0u;
               bool isnew;
               const int psl = relax_one(L, H, K, pk.x | ((pk.z & 7u) << 28), pk.y, tt, vll.x, vll.y, wk.lab, e, pd, pt,
-                                        mode_bit, again, tsrc, my_relaxed, fnext, isnew);
+                                        mode_bit, again, tsrc, my_relaxed, fnext, isnew, stale);
               if (psl >= 0) {
                 const int p = atomicAdd(&L.n_pend, 1);
                 if (p < CAP) L.pend[p] = (Idx)psl;
@@ -1049,7 +1067,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
   if (relaxed) *relaxed += my_relaxed;
   if (rounds) *rounds += my_rounds;
   // a tainted target: its label may rest on a withdrawn one (the task goes to the exact tier)
-  const bool tainted = tslot >= 0 && (L.key[tslot] & kTaint) != 0u;
+  const bool tainted = stale || (tslot >= 0 && (L.key[tslot] & kTaint) != 0u);
   *stale_out = Gr::mine(__ballot(tainted)) != 0ull;
   __syncthreads();
   return !L.overflow;
