@@ -194,7 +194,8 @@ typedef struct otr_batch_result {
                                   trace by trace in report order */
   /* per route-search kernel: slot 0 the first tier (k_route<160,2>), 1..5 the LDS retry
    * tiers in order, 6 / 7 the global-memory search (32K / 1M-state slabs), 8 the 64-bit
-   * label LDS tier (steps whose length and time bits exceed 32), 9 spare.  code: CAP*10+G
+   * label LDS tier (steps whose length and time bits exceed 32), 9 the edge-state LDS
+   * tiers (modes with turn costs).  code: CAP*10+G
    * of an LDS tier, 900000 + CAP the 64-bit tier, -1 / -2 the global tiers, 0 unused.
    * work: searches, settled nodes (expanded states), relaxed edges, transition entries
    * written.  ms (OTR_BATCH_TIMING): HIP-event time of the kernel on the matcher's stream. */
@@ -267,7 +268,7 @@ int otr_tilehier_files(double min_lon, double min_lat, double max_lon, double ma
  * associations) -> the .otrg file otr_configure uploads (include/otr_graph_format.h).
  * Edges may come in any order; the file's edges are sorted by (src, dst), stable.
  * Edges shorter than 5 cm are contracted (their end nodes merge into the smallest node
- * id; DESIGN.md §3.4: the route search's A* finality margin needs edges >= 5 cm); a
+ * id; DESIGN.md §3.4: shorter edges only narrow the exact search rounds); a
  * contracted edge's OSMLR begin/end flag moves to its segment's neighbouring edge.
  * Routing lengths are the shapes' lengths.  Decoding the .gph binary itself needs
  * Valhalla 2.3.6's GraphTile layout (UPSTREAM, absent here): out of scope. */

@@ -80,8 +80,9 @@ struct DevGraph {
   const uint32_t* cell_row;
   const uint32_t* cell_edge;
   const uint4* cell_rec;       // per cell entry 3 x 16 B: {edge, shape begin, shape end, attr}, shape points 0-1, 2-3
-  const uint4* edge_pack;      // {dst, len_mm, attr, 0}: one 16-B load per relaxed edge (CSR tail)
-  const uint4* adj;            // 4 x uint4 per node: {dst | access<<28 | more<<31, len_mm, dst lat_e6, dst lon_e6}
+  const uint4* edge_pack;      // {dst, len_mm, attr, minin(dst)}: one 16-B load per relaxed edge (CSR tail)
+  const uint4* adj;            // 4 x uint4 per node: {dst | access<<28 | more<<31, len_mm, minin(dst), 0}
+  const uint32_t* node_minin;  // per node: its shortest in-edge, mm (0xFFFFFFFF: none), the IN criterion
   const uint32_t* len_mm;      // routing length, whole millimetres
   const int2* node_ll;         // (lat_e6, lon_e6)
   const uint32_t* adj_t;       // [mode][4 per node like adj]: route time of the slot's edge, 0.1 s
@@ -92,8 +93,6 @@ struct DevGraph {
   uint32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double grid_min_lat, grid_min_lon, grid_cell_deg;
   __device__ const uint32_t* et(int mode) const { return edge_t + (size_t)mode * edge_t_stride; }
-  float h_scale;               // min over edges of len_mm / straight-line mm (<= 1): keeps the A*
-                               // heuristic consistent for graphs whose lengths undercut geometry
 };
 
 // cos of an angle in degrees, |deg| <= 90: Taylor series to x^22 (Horner).

@@ -3,8 +3,9 @@
 // With turn costs a route's key (length + turn cost) depends on the edge a
 // node is entered by, so the states of the search are edges: state b = "at dst(b), having
 // arrived through b".  The search is the node search of otr_kernels.h (search_run) over
-// those states — A* rounds on f = key + h(node), partition of the pending list, one lane
-// per (settled state, adjacency slot), LDS hash insert + 64-bit atomicMin — with:
+// those states — exact rounds (the IN criterion: a state b is final once its key is below
+// the smallest pending key + len(b), since every later offer to b crosses b itself), one
+// lane per (settled state, adjacency slot), LDS hash insert + 64-bit atomicMin — with:
 //   * 64-bit labels key << 38 | (kTcCap - turn) << 17 | time (otr_general.h gpack): the
 //     atomicMin keeps the lexicographic minimum of (key, length, time), the oracle's order;
 //   * the turn cost of every relaxation from the table of the mode, by the turn degree
@@ -13,11 +14,10 @@
 //   * targets are not states: the target edge ej is entered from any state at src(ej), so
 //     every settled state at a target node offers to the target (with the turn into ej
 //     and the entry part) and the target keeps the lexicographic minimum offer (tlab);
-//   * two search frontiers: fmin over key + h orders the search and decides finality,
-//     dmin over length + h decides unreachability (the bounds are on the length);
-//   * the same pruning and stale test as search_run (time, length and turn cost all
-//     prune; a pruned re-relaxation whose head holds a label above the offer sends the
-//     task to the exact global-memory search).
+//   * two search frontiers: kmin over the key decides finality, dmin over the length
+//     decides unreachability (the bounds are on the length);
+//   * the same pruning as search_run (time, length and turn cost all prune); every offer
+//     comes from a final label, so the labels are the oracle's label-setting ones.
 // One source edge per task (k_tasks), one search per wave (G = 1).
 #pragma once
 #include "otr_general.h"
@@ -30,10 +30,10 @@ struct EdgeLds {
   unsigned long long lab[CAP];   // gpack label, kGInf: none
   uint32_t key[CAP];             // edge id | kInq | kRel, kEmpty
   uint32_t node[CAP];            // dst(edge): where the state stands
-  uint16_t hv[CAP];              // hq_of(h(node))
+  uint16_t mi[CAP];              // mi_of(len(edge)): the IN criterion's gap of the state
   uint16_t hend[CAP];            // end heading of the edge (the turn out of the state)
   uint16_t pend[CAP];            // pending slots
-  uint16_t wslot[WCAP];          // this round's settled states: slot | again << 15
+  uint16_t wslot[WCAP];          // this round's settled states' slots
   unsigned long long wlab[WCAP];  // ... and their labels
   // targets (lanes of the wave): the best offer, entry parts, begin heading of ej
   unsigned long long tlab[OTR_WAVE];
@@ -98,13 +98,6 @@ struct EOffer {
 __device__ inline bool e_feasible(const EOffer& o, uint32_t pd, uint32_t pt) {
   return o.d <= pd && o.t <= pt && o.c <= kTcCap;
 }
-__device__ inline bool e_above(unsigned long long L, const EOffer& o) {
-  if (L == kGInf) return false;
-  const uint32_t k = g_k(L), d = g_d(L), t = g_t(L);
-  if (k != o.k) return k > o.k;
-  if (d != o.d) return d > o.d;
-  return t > o.t;
-}
 
 // the offer of label lb through a step (turn tc, length len, time tt)
 __device__ inline EOffer e_step(unsigned long long lb, uint32_t tc, uint32_t len, uint32_t tt) {
@@ -116,52 +109,43 @@ __device__ inline EOffer e_step(unsigned long long lb, uint32_t tc, uint32_t len
   return o;
 }
 
-// Relax state (label lb, at node v, end heading ha) through the edge b (head w, length
-// len, time tt, begin / end headings hb / he, access in dw's high bits).  Returns the slot
-// when b became newly pending.
+// Relax the FINAL state (label lb, at node v, end heading ha) through the edge b (head w,
+// length len, time tt, begin / end headings hb / he, access in dw's high bits).  Returns
+// the slot when b became newly pending.
 template <int CAP>
-__device__ inline int e_relax(EdgeLds<CAP>& L, const Heur& H, const int32_t* turn, unsigned long long lb, uint32_t ha,
-                              uint32_t dw, uint32_t len, uint32_t tt, uint32_t b, uint32_t hb, uint32_t he,
-                              int32_t wlat, int32_t wlon, uint32_t pd, uint32_t pt, uint32_t mode_bit, bool again,
-                              uint32_t& relaxed, uint32_t& fnext, uint32_t& dnext, bool& isnew, bool& stale) {
+__device__ inline int e_relax(EdgeLds<CAP>& L, const int32_t* turn, unsigned long long lb, uint32_t ha, uint32_t dw,
+                              uint32_t len, uint32_t tt, uint32_t b, uint32_t hb, uint32_t he, uint32_t pd, uint32_t pt,
+                              uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext, uint32_t& dnext, bool& isnew) {
   isnew = false;
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
   const uint32_t tc = (uint32_t)turn[turn_degree((int)ha, (int)hb)];
   const EOffer o = e_step(lb, tc, len, tt);
-  if (!e_feasible(o, pd, pt)) {
-    if (again) {  // the stale test (relax_one): b holds a label above this pruned offer
-      const int sv = e_find(L, b);
-      if (sv >= 0 && e_above(L.lab[sv], o)) stale = true;
-    }
-    return -1;
-  }
+  if (!e_feasible(o, pd, pt)) return -1;  // pruned (label-setting semantics)
   const uint32_t w = dw & kAdjDstMask;
-  const uint32_t h = H(wlat, wlon);
   const int sl = e_insert(L, b, &isnew);
   if (sl < 0) return -1;
   if (isnew) {
     L.node[sl] = w;
     L.hend[sl] = (uint16_t)he;
-    L.hv[sl] = hq_of(h);
+    L.mi[sl] = mi_of(len);
   }
   const unsigned long long nw = gpack(o.k, o.c, o.t);
   const unsigned long long old = atomicMin(&L.lab[sl], nw);
   if (nw < old) {
-    const uint32_t f = o.k + h, fd = o.d + h;
-    fnext = f < fnext ? f : fnext;
-    dnext = fd < dnext ? fd : dnext;
+    knext = o.k < knext ? o.k : knext;
+    dnext = o.d < dnext ? o.d : dnext;
     const uint32_t was = atomicOr(&L.key[sl], kInq);
     if (!(was & kInq)) return sl;
   }
   return -1;
 }
 
-// The settled state's offers to the targets at its node v (the turn into ej + the entry
-// part), kept as each target's lexicographic minimum.
+// The settled (final) state's offers to the targets at its node v (the turn into ej + the
+// entry part), kept as each target's lexicographic minimum.
 template <int CAP>
 __device__ inline void e_target_offers(EdgeLds<CAP>& L, const int32_t* turn, unsigned long long lb, uint32_t ha,
-                                       uint32_t v, uint32_t pd, uint32_t pt, bool again, bool& stale) {
+                                       uint32_t v, uint32_t pd, uint32_t pt) {
   unsigned long long m = tmap_get(L, v);
   while (m) {
     const int q = __ffsll((long long)m) - 1;
@@ -169,7 +153,6 @@ __device__ inline void e_target_offers(EdgeLds<CAP>& L, const int32_t* turn, uns
     const uint32_t tc = (uint32_t)turn[turn_degree((int)ha, (int)L.thb[q])];
     const EOffer o = e_step(lb, tc, L.tpart[q], L.tpt[q]);
     if (e_feasible(o, pd, pt)) atomicMin(&L.tlab[q], gpack(o.k, o.c, o.t));
-    else if (again && e_above(L.tlab[q], o)) stale = true;
   }
 }
 
@@ -191,15 +174,14 @@ __device__ inline void e_init(EdgeLds<CAP>& L) {
 }
 
 // One search (one wave) from root edge `root` (label 0 at dst(root) = rnode, end heading
-// rhe).  Lanes < n_tgt hold a target: node tv = src(ej), h(tv) hT, entry parts tpart /
-// tpt, begin heading thb.  pd / pt: the relative bounds.  Returns false on overflow;
-// *stale as in search_run.  timed = false: route times are not tracked (pt unused).
+// rhe).  Lanes < n_tgt hold a target: node tv = src(ej), entry parts tpart / tpt, begin
+// heading thb.  pd / pt: the relative bounds.  Returns false on overflow.  timed = false:
+// route times are not tracked (pt unused).
 template <int CAP>
-__device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const Heur& H, const int32_t* turn, int md,
-                            bool active, uint32_t root, uint32_t rnode, uint32_t rhe, uint32_t hroot, uint32_t pd,
-                            uint32_t pt, bool timed, uint32_t delta_mm, int n_tgt, uint32_t tv, uint32_t hT,
-                            uint32_t tpart, uint32_t tpt, uint32_t thb, bool* stale_out, unsigned long long* settled,
-                            unsigned long long* relaxed) {
+__device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const int32_t* turn, int md, bool active,
+                            uint32_t root, uint32_t rnode, uint32_t rhe, uint32_t pd, uint32_t pt, bool timed,
+                            int n_tgt, uint32_t tv, uint32_t tpart, uint32_t tpt, uint32_t thb,
+                            unsigned long long* settled, unsigned long long* relaxed) {
   constexpr int kMaxKeys = (CAP * 7) / 8;
   constexpr int WCAP = EdgeLds<CAP>::WCAP;
   const int gl = (int)threadIdx.x;
@@ -228,16 +210,14 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const Heur& H, c
     const int sl = e_insert(L, root, &isnew);
     L.node[sl] = rnode;
     L.hend[sl] = (uint16_t)rhe;
-    L.hv[sl] = hq_of(hroot);
+    L.mi[sl] = 0;
     L.lab[sl] = gpack(0u, 0u, 0u);
     L.key[sl] |= kInq;
     L.pend[0] = (uint16_t)sl;
   }
   __syncthreads();
   uint32_t my_settled = 0, my_relaxed = 0;
-  bool stale = false;
-  uint32_t fmin = hroot, dmin = hroot;
-  const uint32_t hTm = hT + H.margin;
+  uint32_t kmin = 0, dmin = 0;  // the smallest pending key / length
   bool done = !active;
   int npend = active ? 1 : 0;
   int nkeys = active ? 1 : 0;
@@ -245,43 +225,42 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const Heur& H, c
     const int np = done ? 0 : npend;
     bool res = true;
     if (!done && tgt && np > 0) {
+      // every later offer to the target has key >= kmin + tpart and length >= dmin + tpart
       const unsigned long long tl = L.tlab[gl];
-      if (tl != kGInf) res = (int64_t)g_k(tl) + (int64_t)hTm < (int64_t)fmin;  // final
-      else res = (int64_t)dmin - (int64_t)hTm + (int64_t)tpart > (int64_t)pd;  // no feasible offer can come
+      res = (tl != kGInf && (int64_t)g_k(tl) < (int64_t)kmin + (int64_t)tpart) ||
+            (int64_t)dmin + (int64_t)tpart > (int64_t)pd;
     }
     done = done || __ballot(!res) == 0ull || np == 0;
     if (__builtin_amdgcn_readfirstlane((int)done)) break;
-    const uint32_t theta = fmin + delta_mm < fmin ? 0xFFFFFFFFu : fmin + delta_mm;
-    uint32_t fnext = 0xFFFFFFFFu, dnext = 0xFFFFFFFFu;
+    uint32_t knext = 0xFFFFFFFFu, dnext = 0xFFFFFFFFu;
     int kept = 0, nw = 0;
     for (int base = 0; base < np; base += OTR_WAVE) {
       const int k = base + gl;
       const bool in = k < np;
       int sl = 0;
-      uint32_t f = 0, fd = 0, key = 0;
+      uint32_t kk = 0, dd = 0, key = 0;
       unsigned long long lb = 0;
       bool take = false;
       if (in) {
         sl = L.pend[k];
         lb = L.lab[sl];
         key = L.key[sl];
-        const uint32_t hq = (uint32_t)L.hv[sl] << 6;
-        f = g_k(lb) + hq;
-        fd = g_d(lb) + hq;
-        take = f < theta;
+        kk = g_k(lb);
+        dd = g_d(lb);
+        take = (uint64_t)kk < (uint64_t)kmin + in_gap(L.mi[sl]);  // final (IN criterion)
       }
       take = take && nw + prefix_count(__ballot(take)) < WCAP;
       const unsigned long long mt = __ballot(take), mk = __ballot(in && !take);
       __syncthreads();
       if (take) {
         const int w = nw + prefix_count(mt);
-        L.wslot[w] = (uint16_t)(sl | ((key & kRel) ? 0x8000 : 0));
+        L.wslot[w] = (uint16_t)sl;
         L.wlab[w] = lb;
         L.key[sl] = (key & kNodeMask) | kRel;
       } else if (in) {
         L.pend[kept + prefix_count(mk)] = (uint16_t)sl;
-        fnext = f < fnext ? f : fnext;
-        dnext = fd < dnext ? fd : dnext;
+        knext = kk < knext ? kk : knext;
+        dnext = dd < dnext ? dd : dnext;
       }
       nw += __popcll(mt);
       kept += __popcll(mk);
@@ -296,9 +275,7 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const Heur& H, c
       int psl = -1;
       bool isnew = false;
       if (k < 4 * nw) {
-        const uint16_t ws = L.wslot[k >> 2];
-        const int sl = ws & 0x7FFF;
-        const bool again = (ws & 0x8000) != 0;
+        const int sl = L.wslot[k >> 2];
         const unsigned long long lb = L.wlab[k >> 2];
         const uint32_t v = L.node[sl], ha = L.hend[sl];
         const int slot = k & 3;
@@ -306,9 +283,9 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const Heur& H, c
         const uint32_t tq = adjt[4 * (size_t)v + slot];
         const uint2 xe = g.adj_e[4 * (size_t)v + slot];
         const uint4 r = ld16(g.adj + 4 * (size_t)v + slot);
-        if (slot == 0) e_target_offers(L, turn, lb, ha, v, pd, pt, again, stale);
-        psl = e_relax(L, H, turn, lb, ha, r.x & ~kAdjMore, r.y, timed ? tq : 0u, xe.x, xe.y & 0xFFFFu, xe.y >> 16,
-                      (int32_t)r.z, (int32_t)r.w, pd, pt, mode_bit, again, my_relaxed, fnext, dnext, isnew, stale);
+        if (slot == 0) e_target_offers(L, turn, lb, ha, v, pd, pt);
+        psl = e_relax(L, turn, lb, ha, r.x & ~kAdjMore, r.y, timed ? tq : 0u, xe.x, xe.y & 0xFFFFu, xe.y >> 16, pd, pt,
+                      mode_bit, my_relaxed, knext, dnext, isnew);
         tail = tail || (slot == 3 && (r.x & kAdjMore));
       }
       nkeys += __popcll(__ballot(isnew));
@@ -326,20 +303,17 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const Heur& H, c
       for (int base = 0; base < 4 * nw; base += OTR_WAVE) {
         const int k = base + gl;
         if (k < 4 * nw && (k & 3) == 3) {
-          const uint16_t ws = L.wslot[k >> 2];
-          const int sl = ws & 0x7FFF;
-          const bool again = (ws & 0x8000) != 0;
+          const int sl = L.wslot[k >> 2];
           const unsigned long long lb = L.wlab[k >> 2];
           const uint32_t v = L.node[sl], ha = L.hend[sl];
           if (g.adj[4 * (size_t)v + 3].x & kAdjMore)
             for (uint32_t e = g.node_row[v] + 4; e < g.node_row[v + 1]; ++e) {
               const uint4 pk = ld16(g.edge_pack + e);
-              const int2 wll = g.node_ll[pk.x];
               const short2 hh = g.edge_head[e];
               bool isnew;
-              const int psl = e_relax(L, H, turn, lb, ha, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e,
-                                      (uint32_t)hh.x, (uint32_t)hh.y, wll.x, wll.y, pd, pt, mode_bit, again,
-                                      my_relaxed, fnext, dnext, isnew, stale);
+              const int psl = e_relax(L, turn, lb, ha, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e,
+                                      (uint32_t)hh.x, (uint32_t)hh.y, pd, pt, mode_bit, my_relaxed, knext, dnext,
+                                      isnew);
               if (isnew) atomicAdd(&L.n_keys, 1);
               if (psl >= 0) {
                 const int p = atomicAdd(&L.n_pend, 1);
@@ -354,7 +328,7 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const Heur& H, c
       if (npend > CAP) npend = CAP;
     }
     __syncthreads();
-    fmin = wave_min_u32(fnext);
+    kmin = wave_min_u32(knext);
     dmin = wave_min_u32(dnext);
     const int keys = L.n_keys + nkeys;
     if (!done && (L.overflow || keys > kMaxKeys)) done = true;
@@ -363,7 +337,6 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const Heur& H, c
   }
   if (settled) *settled += my_settled;
   if (relaxed) *relaxed += my_relaxed;
-  *stale_out = __ballot(stale) != 0ull;
   __syncthreads();
   return !L.overflow;
 }
@@ -372,9 +345,8 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const Heur& H, c
 // K3e: edge-state route tasks (turn modes), a fixed grid over the device-side list of
 // the tasks flagged 5 (k_route) or 6 (this tier's overflows, for the larger table).
 // ------------------------------------------------------------------------------
-// EXACT: label-setting order (zero_heur, 1 mm rounds) for the tasks flagged 7 (a
-// withdrawn label in the A* tiers); what it cannot hold goes to k_general (3)
-template <int CAP, bool EXACT = false>
+// What outgrows the 2048-state table goes to k_general (3).
+template <int CAP>
 __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, unsigned long long* counters) {
   __shared__ EdgeLds<CAP> L;
   const int64_t n_tasks = (int64_t)*a.list_count;
@@ -395,7 +367,7 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
     const uint32_t d0 = a.cprep[sp * OTR_KMAX + i].w;
     const uint32_t t0 = bt >= 0 ? a.cprep_t[sp * OTR_KMAX + i].y : 0u;
     const uint2 li = a.clen[sp * OTR_KMAX + i];
-    uint32_t ej = 0, tv = kEmpty, hT = 0, tpart = 0, tpt = 0, thb = 0;
+    uint32_t ej = 0, tv = kEmpty, tpart = 0, tpt = 0, thb = 0;
     double pj = 0;
     bool needed = false;
     if (lane < Kb) {
@@ -407,7 +379,6 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
       needed = !(ej == ei && pj >= pi);
       if (needed) {
         tv = cq.y;
-        hT = cq.z;
         thb = (uint32_t)gr.edge_head[ej].x;
       }
     }
@@ -415,16 +386,13 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
     const bool search = Kb <= OTR_WAVE && !forced && root_ok && __ballot(needed) != 0ull;
     const uint32_t pd = bmm >= d0 ? bmm - d0 : 0u;
     const uint32_t pt = bt >= 0 && t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
-    const Heur H = EXACT ? zero_heur(a.heur[s]) : a.heur[s];
     e_init(L);
-    bool stale = false;
     unsigned long long settled = 0, relaxed = 0;
-    const bool ok = edge_search<CAP>(L, gr, H, a.turn + 181 * md, md, search, ei, gr.edge_dst[ei],
-                                     (uint32_t)(uint16_t)gr.edge_head[ei].y, EXACT ? 0u : r2.x, pd, pt, bt >= 0,
-                                     EXACT ? 1u : (uint32_t)(a.delta * 1000.0), Kb, tv, EXACT ? 0u : hT, tpart, tpt,
-                                     thb, &stale, counters ? &settled : nullptr, counters ? &relaxed : nullptr) &&
+    const bool ok = edge_search<CAP>(L, gr, a.turn + 181 * md, md, search, ei, gr.edge_dst[ei],
+                                     (uint32_t)(uint16_t)gr.edge_head[ei].y, pd, pt, bt >= 0, Kb, tv, tpart, tpt, thb,
+                                     counters ? &settled : nullptr, counters ? &relaxed : nullptr) &&
                     Kb <= OTR_WAVE;
-    if (ok && !stale) {
+    if (ok) {
       uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
       if (lane < Kb) {
         int64_t r = -1, rt = 0;
@@ -447,7 +415,7 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
         a.trans_tc[trow - a.trans + (int64_t)i * Kb + lane] = valid ? rc : 0u;
       }
     } else if (lane == 0) {
-      a.overflow_flag[task] = EXACT ? 3 : (stale ? 7 : (CAP < 2048 ? 6 : 3));
+      a.overflow_flag[task] = CAP < 2048 ? 6 : 3;
     }
     if (counters) {
       settled = wave_sum_u32((uint32_t)settled);
@@ -458,7 +426,6 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
         atomicAdd(&counters[4 * kCShards + sh], relaxed);
         atomicAdd(&counters[5 * kCShards + sh], ok && search ? (unsigned long long)Kb : 0ull);
         atomicAdd(&counters[6 * kCShards + sh], search ? 1ull : 0ull);
-        atomicAdd(&counters[15 * kCShards + sh], stale ? 1ull : 0ull);
       }
     }
     __syncthreads();
@@ -472,12 +439,11 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
 // first hop from the target takes the smallest a whose offer is the target's label.  The
 // lanes test the in-edges of one node in parallel.
 // ------------------------------------------------------------------------------
-// overflow_flag / stale_flag: the step's flag when the table overflows / a label was
-// withdrawn (7: the exact tier, EXACT = true: label-setting order)
-template <int CAP, bool EXACT = false>
+// overflow_flag: the step's flag when the table overflows (the next tier)
+template <int CAP>
 __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, const int32_t* turn_tab,
                                                    const int64_t* step_list, const unsigned long long* list_count,
-                                                   int32_t overflow_flag, int32_t stale_flag) {
+                                                   int32_t overflow_flag) {
   __shared__ EdgeLds<CAP> L;
   __shared__ uint32_t s_rev[CAP];
   const int64_t n_list = (int64_t)*list_count;
@@ -498,16 +464,12 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
     const uint32_t pd = bmm >= d0 ? bmm - d0 : 0u;
     const uint32_t pt = bt >= 0 && t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
     const uint32_t thb = (uint32_t)gr.edge_head[ej].x;
-    const Heur H = EXACT ? zero_heur(a.heur[s]) : a.heur[s];
     e_init(L);
-    bool stale = false;
-    const uint32_t hroot = H(gr.node_ll[gr.edge_dst[ei]].x, gr.node_ll[gr.edge_dst[ei]].y);
-    const bool ok = edge_search<CAP>(L, gr, H, turn, md, true, ei, gr.edge_dst[ei], (uint32_t)(uint16_t)gr.edge_head[ei].y,
-                                     hroot, pd, pt, bt >= 0, EXACT ? 1u : (uint32_t)(a.delta * 1000.0), 1, ct.y,
-                                     EXACT ? 0u : ct.z, ct.x, tpt, thb, &stale, nullptr, nullptr);
+    const bool ok = edge_search<CAP>(L, gr, turn, md, true, ei, gr.edge_dst[ei], (uint32_t)(uint16_t)gr.edge_head[ei].y,
+                                     pd, pt, bt >= 0, 1, ct.y, ct.x, tpt, thb, nullptr, nullptr);
     const unsigned long long tl = L.tlab[0];
     int n = -1;
-    if (ok && !stale && tl != kGInf) {
+    if (ok && tl != kGInf) {
       // first hop: the smallest in-edge a of src(ej) whose offer is the target's label
       uint32_t cur = kEmpty;
       {
@@ -561,7 +523,7 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
       }
     }
     if (n < 0) {
-      if (lane == 0) a.overflow_flag[k] = (ok && stale) ? stale_flag : overflow_flag;  // the next tier
+      if (lane == 0) a.overflow_flag[k] = overflow_flag;  // the next tier
     } else {
       const int shard = (int)(blockIdx.x & (kShards - 1));
       const int64_t region = a.capacity / kShards;

@@ -202,17 +202,20 @@ int engine_configure(const Config& cfg, std::string* err) {
       if (err) *err = "graph edge " + std::to_string(e) + " has a bad end node or shape range";
       return OTR_BAD_REQUEST;
     }
+  // minin(v): the shortest in-edge of every node (mm, any mode: a lower bound for each),
+  // the IN criterion of the exact search rounds; 0xFFFFFFFF: no in-edge
+  std::vector<uint32_t> minin(h.n_nodes + 1, 0xFFFFFFFFu);
+  for (uint32_t e = 0; e < h.n_edges; ++e) minin[dst[e]] = std::min(minin[dst[e]], len[e]);
   std::vector<uint4> pack(h.n_edges + 1);
-  for (uint32_t e = 0; e < h.n_edges; ++e) pack[e] = make_uint4(dst[e], len[e], attr[e], 0u);
+  for (uint32_t e = 0; e < h.n_edges; ++e) pack[e] = make_uint4(dst[e], len[e], attr[e], minin[dst[e]]);
   // per-node adjacency records: the first 4 out-edges of a node in one 64-B record,
-  // {dst | access<<28 | more<<31, len_mm, dst lat_e6, dst lon_e6} per edge
+  // {dst | access<<28 | more<<31, len_mm, minin(dst), 0} per edge
   std::vector<uint4> adj(4ull * h.n_nodes + 4, make_uint4(kAdjDstMask, 0u, 0u, 0u));
   for (uint32_t u = 0; u < h.n_nodes; ++u) {
     const uint32_t deg = row[u + 1] - row[u];
     for (uint32_t k = 0; k < deg && k < 4; ++k) {
       const uint32_t e = row[u] + k;
-      adj[4ull * u + k] = make_uint4(dst[e] | ((attr[e] & OTR_ATTR_ACCESS_MASK) << 28), len[e],
-                                     (uint32_t)nll[2ull * dst[e]], (uint32_t)nll[2ull * dst[e] + 1]);
+      adj[4ull * u + k] = make_uint4(dst[e] | ((attr[e] & OTR_ATTR_ACCESS_MASK) << 28), len[e], minin[dst[e]], 0u);
     }
     if (deg > 4) adj[4ull * u + 3].x |= kAdjMore;
   }
@@ -241,22 +244,6 @@ int engine_configure(const Config& cfg, std::string* err) {
     for (uint32_t k = 0; k < 4 && row[u] + k < row[u + 1]; ++k) {
       const uint32_t e = row[u] + k;
       adje[4ull * u + k] = make_uint2(e, (uint32_t)(uint16_t)head[e].x | ((uint32_t)(uint16_t)head[e].y << 16));
-    }
-  // heuristic scale: every edge must satisfy len_mm >= scale * (straight-line mm in any
-  // search's metric); the upper bound of that metric distance uses the edge's own
-  // more equatorward cosine.  Generated graphs give 1; lengths rounded
-  // below geometry (e.g. whole metres) lower it; a zero-length edge between distinct
-  // points makes it 0, i.e. plain Dijkstra order.
-  double scale = 1.0;
-  for (uint32_t u = 0; u < h.n_nodes; ++u)
-    for (uint32_t e = row[u]; e < row[u + 1]; ++e) {
-      const uint32_t v = dst[e];
-      const double la1 = nll[2ull * u] * 1e-6, lo1 = nll[2ull * u + 1] * 1e-6;
-      const double la2 = nll[2ull * v] * 1e-6, lo2 = nll[2ull * v + 1] * 1e-6;
-      const double cmax = cos_deg(fmin(fabs(la1), fabs(la2)));
-      const double x = (lo1 - lo2) * kMetersPerDeg * cmax, y = (la1 - la2) * kMetersPerDeg;
-      const double d_mm = sqrt(x * x + y * y) * 1000.0 * (1.0 + 1e-9) + 1e-6;
-      if (d_mm > 1e-3 && (double)len[e] < scale * d_mm) scale = (double)len[e] / d_mm;
     }
   // candidate-search view: each grid-cell entry carries its edge's shape range and
   // attributes, 48 B per entry: {edge, shape begin, shape end, attr} + the first four shape points
@@ -313,6 +300,7 @@ int engine_configure(const Config& cfg, std::string* err) {
   g.len_mm = (const uint32_t*)upv(len.data(), 4ull * len.size());
   g.edge_pack = (const uint4*)upv(pack.data(), sizeof(uint4) * pack.size());
   g.adj = (const uint4*)upv(adj.data(), sizeof(uint4) * adj.size());
+  g.node_minin = (const uint32_t*)upv(minin.data(), 4ull * minin.size());
   {
     std::vector<uint32_t> all_et, all_at;
     for (int m = 0; m < OTR_MODES; ++m) {
@@ -331,12 +319,6 @@ int engine_configure(const Config& cfg, std::string* err) {
     if (err) *err = "device allocation for the graph failed";
     return OTR_DEVICE_ERROR;  // the previous graph (if any) stays configured
   }
-  float hs = (float)scale;
-  if ((double)hs > scale) hs = nextafterf(hs, 0.0f);
-  g.h_scale = hs > 0.0f ? hs : 0.0f;
-#ifdef OTR_FORCE_H_SCALE1
-  g.h_scale = 1.0f;  // experiment only: the unscaled heuristic
-#endif
   g.n_nodes = h.n_nodes;
   g.n_edges = h.n_edges;
   g.n_segments = h.n_segments;
@@ -736,19 +718,14 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   pr.cand_count = cb.count;
   pr.cand_edge = cb.edge;
   pr.cand_p = cb.p;
-  pr.state_probe = state_probe;
-  pr.lat = b.lat;
-  pr.lon = b.lon;
-  pr.radius = cb.radius;
   pr.state_trace = state_trace;
   pr.mode = b.mode;
-  pr.heur = need<Heur>(S_HEUR, S);
   pr.cprep = need<uint4>(S_CPREP, (size_t)S * OTR_KMAX);
   pr.cprep_t = need<uint2>(S_CPREP_T, (size_t)S * OTR_KMAX);
   pr.clen = need<uint2>(S_CLEN, (size_t)S * OTR_KMAX);
   pr.nroot = need<int32_t>(S_CAND_NROOT, S);
   pr.turn_modes = turn_modes;
-  if (!pr.heur || !pr.cprep || !pr.cprep_t || !pr.clen || !pr.nroot) {
+  if (!pr.cprep || !pr.cprep_t || !pr.clen || !pr.nroot) {
     if (err) *err = "device allocation failed (prep)";
     return OTR_DEVICE_ERROR;
   }
@@ -784,7 +761,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     ta.cand_count = cb.count;
     ta.cand_edge = cb.edge;
     ta.edge_dst = g.edge_dst;
-    ta.node_ll = g.node_ll;
     ta.task_off = task_off;
     ta.bound = sb.bound;
     ta.forced = sb.forced;
@@ -793,7 +769,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     ta.mode = b.mode;
     ta.cprep = pr.cprep;
     ta.cprep_t = pr.cprep_t;
-    ta.heur = pr.heur;
     ta.trans_off = trans_off;
     ta.turn_modes = turn_modes;
     ta.task_state = task_state;
@@ -825,19 +800,13 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ra.cand_p = cb.p;
   ra.state_trace = state_trace;
   ra.mode = b.mode;
-  ra.state_probe = state_probe;
-  ra.lat = b.lat;
-  ra.lon = b.lon;
-  ra.radius = cb.radius;
   ra.bt = sb.bt;
-  ra.heur = pr.heur;
   ra.turn = d_turn;
   ra.trans_tc = trans_tc;
   ra.cprep = pr.cprep;
   ra.cprep_t = pr.cprep_t;
   ra.clen = pr.clen;
   ra.rec = task_rec;
-  ra.delta = mp.delta;
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
   ra.overflow_flag = task_ovf;
   // bounds > 1.9 km skip the first tier (most outgrow 160 slots: C4 route 24 -> 15 ms);
@@ -1002,8 +971,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     }
 #endif
     // turn-mode tasks (flag 5): the edge-state LDS search, 384 then 2048 states; what
-    // outgrows it (flag 3) or may have kept a withdrawn label (flag 4) goes on below
-    // slot 9 (bank 1): the edge-state tiers and the exact tiers, timed together
+    // outgrows it (flag 3) goes on below; slot 9 (bank 1): the edge-state tiers
     if (timing) (void)hipEventRecord(ev[24 + 2 * 9], stream);
     if (turns) {
       out->route_tier_code[9] = 700000 + 384;
@@ -1018,35 +986,11 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         if (et == 0) k_route_edge<384><<<4096, 64, 0, stream>>>(g, rb, rcn);
         else k_route_edge<2048><<<512, 64, 0, stream>>>(g, rb, rcn);
       }
-      // what the edge tiers may have settled with a withdrawn label (flag 7): label-setting order
-      {
-        unsigned long long* c = cnt + 29;
-        k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x80u, list, c);
-        RouteArgs rb = ra;
-        rb.task_list = list;
-        rb.list_count = c;
-        k_route_edge<384, true><<<4096, 64, 0, stream>>>(g, rb, rwork ? d_counters + 1 * bank : nullptr);
-      }
-    }
-    // node-mode searches that may have kept a withdrawn label (flag 4): the exact tier,
-    // label-setting order in 512-slot tables (the 64-bit-label and turn-mode tasks among
-    // them, and what outgrows it, go on to k_general)
-    {
-      unsigned long long* c = cnt + 30;
-      k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x10u, list, c);
-      RouteArgs rb = ra;
-      rb.task_list = list;
-      rb.list_count = c;
-      rb.exact = 1;
-      if (!out->route_tier_code[9]) out->route_tier_code[9] = 800000 + 512;  // (bank 1: exact + edge-state tiers)
-      if (rwork) k_route<512, 1, true, false, true><<<8192, 64, 0, stream>>>(g, rb, d_counters + 1 * bank);
-      else k_route<512, 1, true, false, false><<<8192, 64, 0, stream>>>(g, rb, nullptr);
     }
     if (timing) (void)hipEventRecord(ev[24 + 2 * 9 + 1], stream);
-    // everything left — turn-cost (edge-based) tasks, tasks whose labels need 64 bits,
-    // overflows of the largest LDS tables, searches that may have kept a withdrawn label
-    // (flag 4: k_general's exact mode settles it) — runs in the global-memory search:
-    // first on 32K-slot slabs, then what outgrew those on 1M-slot slabs
+    // everything left — tasks whose labels need 64 bits, overflows of the largest LDS
+    // tables (node and edge-state) — runs in the global-memory search: first on 32K-slot
+    // slabs, then what outgrew those on 1M-slot slabs
     for (int gt = 0; gt < 2; ++gt) {
       unsigned long long* c = cnt + 8 + gt;
       k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, gt == 0 ? 0x1Eu : 0x2u, list,
@@ -1118,8 +1062,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       HIPCHK(hipMemsetAsync(step_ovf, 0, 4 * (S + 1), stream));
       HIPCHK(hipMemsetAsync(cnt + 12, 0, 8 * 9, stream));  // path tier counts, cap flag
       HIPCHK(hipMemsetAsync(cnt + 27, 0, 8 * 2, stream));  // edge-state path tier counts
-      HIPCHK(hipMemsetAsync(cnt + 31, 0, 8, stream));      // edge-state exact path tier count
-      HIPCHK(hipMemsetAsync(cnt + 21, 0, 8, stream));      // exact node path tier count
       HIPCHK(hipMemsetAsync(cnt + 32, 0, 8 * kShards, stream));
       PathArgs pa{};
       pa.steps = steps;
@@ -1133,16 +1075,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       pa.cand_p = cb.p;
       pa.state_trace = state_trace;
       pa.mode = b.mode;
-      pa.state_probe = state_probe;
-      pa.lat = b.lat;
-      pa.lon = b.lon;
-      pa.radius = cb.radius;
-      pa.heur = ra.heur;
       pa.cprep = ra.cprep;
       pa.cprep_t = ra.cprep_t;
       pa.bt = sb.bt;
       pa.turn_modes = turn_modes;
-      pa.delta = mp.delta;
       pa.path_off = path_off;
       pa.path_len = path_len;
       pa.path = path;
@@ -1174,20 +1110,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
           unsigned long long* c = cnt + 27 + et;
           k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, et == 0 ? 0x20u : 0x40u,
                                                                        list, c);
-          if (et == 0) k_paths_edge<384><<<4096, 64, 0, stream>>>(g, pa, d_turn, list, c, 6, 7);
-          else k_paths_edge<2048><<<512, 64, 0, stream>>>(g, pa, d_turn, list, c, 3, 7);
+          if (et == 0) k_paths_edge<384><<<4096, 64, 0, stream>>>(g, pa, d_turn, list, c, 6);
+          else k_paths_edge<2048><<<512, 64, 0, stream>>>(g, pa, d_turn, list, c, 3);
         }
-        unsigned long long* c = cnt + 31;
-        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0x80u, list, c);
-        k_paths_edge<384, true><<<4096, 64, 0, stream>>>(g, pa, d_turn, list, c, 3, 3);
-      }
-      // winners whose search may have kept a withdrawn label (flag 4): label-setting order
-      {
-        unsigned long long* c = cnt + 21;
-        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0x10u, list, c);
-        PathArgs pe = pa;
-        pe.exact = 1;
-        k_paths<512, 1><<<16384, 64, 0, stream>>>(g, pe, list, c);
       }
       // 64-bit labels, the largest-table overflows and what the edge tiers left: k_general
       ga.steps = steps;
@@ -1380,7 +1305,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   for (int k = 0; k < OTR_COUNTERS; ++k) out->counters[k] = ctr(0, k);
   // per route kernel: searches, settled, relaxed, transition entries (banks 0, 2..6, 8..9;
   // slot 8, the 64-bit LDS tier: bank 7; slot 9, the edge-state tiers: bank 1)
-  for (int b = 1; b < 10; ++b) out->counters[15] += ctr(b, 15);  // withdrawn-label flags, every tier
   for (int t = 0; t < 10; ++t) {
     const int b = t == 0 ? 0 : (t < 6 ? 1 + t : (t < 8 ? 2 + t : (t == 8 ? 7 : 1)));
     out->route_tier_work[t][0] = ctr(b, 6);

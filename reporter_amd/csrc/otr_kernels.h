@@ -401,12 +401,18 @@ __device__ inline unsigned long long group_bits(unsigned long long m) {
 // ------------------------------------------------------------------------------
 // Bounded one-to-many search, one wave, node labels in an LDS hash table.
 //
-// Labels are whole millimetres (uint32), so every processing order reaches the same
-// fixed point as the oracle's binary-heap Dijkstra, exactly.  Rounds take every
-// pending node whose f = label + h is below (minimum pending f + delta); lane =
-// (node, adjacency slot); relaxation = LDS atomicMin.  With PRED the label word is
+// The oracle's search is label-setting with pruning: a label is the
+// minimum over the feasible offers of its predecessors' FINAL labels, and a time-pruned
+// offer from a label that later improves would leave a withdrawn label behind, so the
+// GPU search only ever relaxes final labels.  Rounds settle, in parallel, every pending
+// node u whose label is provably final by the IN criterion: any later offer to u comes
+// from a pending node (length >= kmin, the smallest pending length) through an in-edge
+// of u (length >= minin(u)), so d(u) < kmin + max(1, minin(u)) makes (d, t) final.
+// Lane = (settled node, adjacency slot); relaxation = LDS atomicMin.  Every offer comes
+// from a final label, so labels, pruning and the predecessor rule equal the oracle's
+// label-setting search whatever the round sizes.  With PRED the label word is
 // (label << 32 | edge id) so the minimum also records the smallest-id predecessor
-// edge among those achieving the label (the oracle's predecessor rule).
+// edge among those achieving the label (the oracle's walk_path rule).
 // ------------------------------------------------------------------------------
 // Wave sum (mod 2^32) by DPP row shifts and row broadcasts, result read from lane 63.
 __device__ inline uint32_t wave_sum_u32(uint32_t v) {
@@ -513,30 +519,26 @@ struct SearchLds {
   static constexpr bool PRED = LM == 1;
   using W = typename LabelT<LM>::W;
   typename LabelT<LM>::T lab[CAP];  // label (| pred edge)
-  uint32_t key[CAP];                  // node id | INQ bit, 0xFFFFFFFF empty
-  uint16_t hv[CAP];                   // A* heuristic in 64-mm units, rounded down (hq_of): a lower bound of h
+  uint32_t key[CAP];                  // node id | INQ / REL bits, 0xFFFFFFFF empty
+  uint16_t mi[CAP];                   // minin(node) in 16-mm units, rounded down (mi_of): the IN criterion
   using Idx = typename std::conditional<(CAP <= 256 && !PRED), uint8_t, uint16_t>::type;
   // nodes settled per round (at most); k_paths (PRED) reuses pend + work as CAP u32 words
   static constexpr int WCAP = CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : 128));
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
-  WorkE<W> work[WCAP];                // this round's settled nodes: {node | kAgain, label}
+  WorkE<W> work[WCAP];                // this round's settled nodes: {node, label}
   int n_pend, n_keys, overflow;
 };
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
-// A node's heuristic as stored in the search table: 64-mm units rounded down, saturating
-// at 65535 (4.19 km).  A lower bound of h keeps every finality / unreachability test
-// valid (fmin = min over pending nodes of L(u) + hq(u) <= L(u) + h(u), and any path through
-// u reaches T with length >= L(u) + h(u) - h(T)): the stored value only
-// orders the search.  The relaxing lanes' own improvements still report exact f.
-__device__ inline uint16_t hq_of(uint32_t h) { return (uint16_t)((h >> 6) < 65535u ? (h >> 6) : 65535u); }
+// minin(node) as stored in the search table: 16-mm units rounded down, saturating at
+// 65535 (1.05 km).  A lower bound of the shortest in-edge keeps the IN criterion exact.
+__device__ inline uint16_t mi_of(uint32_t m) { return (uint16_t)((m >> 4) < 65535u ? (m >> 4) : 65535u); }
+// the IN criterion's margin of a node: any later offer is >= kmin + this (every edge >= 1 mm)
+__device__ inline uint32_t in_gap(uint16_t mq) { return mq ? (uint32_t)mq << 4 : 1u; }
 constexpr uint32_t kInq = 0x80000000u;   // key bit: the node is on the pending list
-constexpr uint32_t kRel = 0x40000000u;   // key bit: the node has been relaxed (settled) before
-constexpr uint32_t kTaint = 0x20000000u; // key bit: the label may rest on a withdrawn one (stale_check)
+constexpr uint32_t kRel = 0x40000000u;   // key bit: the node is settled (its label is final)
 constexpr uint32_t kNodeMask = 0x0FFFFFFFu;
-constexpr uint32_t kAgain = 0x80000000u; // WorkE::node bit: settled before (a re-relaxation)
-constexpr uint32_t kTsrc = 0x40000000u;  // WorkE::node bit: the settled node is tainted
 constexpr uint32_t kNoLabel = 0xFFFFFFFFu;
 constexpr uint32_t kNoRoute = 0xFFFFFFFFu;  // transition array: no valid route within the bound
 
@@ -547,60 +549,6 @@ constexpr uint32_t kNoRoute = 0xFFFFFFFFu;  // transition array: no valid route 
 #else
 #define OTR_STAMP(v) const unsigned long long v = 0
 #endif
-
-// Straight-line lower bound (mm) toward the disk (P, min(r, 50 m)) around the target probe
-// for the A* order, in f32: h = trunc(990 s |v - P| - 1000 (0.99 r' + 1)) in a fixed metric, with
-// s = DevGraph::h_scale (1 unless the graph's lengths undercut its geometry),
-// whose lon scale is the cosine at the most poleward latitude the search can reach
-// (both scales rounded down).  The ideal value satisfies h(u) - h(T) <= 0.99 * dist(u, T);
-// f32 evaluation moves each h by at most ~5e-7 * |v - P| + 1 mm, so the finality and
-// unreachability tests (target_resolved) carry a margin covering twice that over the
-// whole search region: labels never depend on h, whatever the edge lengths
-// (DESIGN.md §3.4).  Coordinates differ by < 2^24 micro-degrees within a search, so
-// the integer differences convert exactly.
-struct Heur {
-  int32_t plat_e6, plon_e6;  // target probe rounded to micro-degrees (any fixed point keeps h consistent)
-  float mx, my;              // metres per micro-degree (lon at the most poleward latitude, lat), rounded down
-  float k;                   // 990 * DevGraph::h_scale (mm per metre), rounded down
-  float c;                   // 1000 * (0.99 r' + 1), mm, rounded up (r' = min(r, 50 m))
-  uint32_t margin;           // mm added to h(T) in the finality / unreachability tests
-  __device__ uint32_t operator()(int32_t lat_e6, int32_t lon_e6) const {
-    const float dx = (float)(lon_e6 - plon_e6) * mx;
-    const float dy = (float)(lat_e6 - plat_e6) * my;
-    const float d = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-    const float h = d * k - c;
-    return h > 0.0f ? (h < 2147483520.0f ? (uint32_t)h : 2147483520u) : 0u;
-  }
-};
-
-__device__ inline float f32_down(double x) {
-  float f = (float)x;
-  if ((double)f > x) f = __uint_as_float(__float_as_uint(f) - 1u);  // positive x: one ulp toward 0
-  return f;
-}
-
-constexpr double kHeurDiskCap = 50.0;  // m
-__device__ inline Heur make_heur(double plat, double plon, double r, double bound, float h_scale) {
-  double lat = fabs(plat) + 2.0 * bound / kMetersPerDeg;
-  if (lat > 89.9) lat = 89.9;
-  const float mx = f32_down(kMetersPerDeg * 1e-6 * cos_deg(lat));
-  const float my = f32_down(kMetersPerDeg * 1e-6);
-  // the disk the order aims at: the target disk's radius r capped at 50 m (any radius keeps
-  // h consistent, so labels never depend on it; a 200 m disk made the C4 searches expand
-  // it in Dijkstra order: capped, C4 5.8M -> 7.0M probes/s; C2's r = 50 m is unchanged,
-  // and a smaller disk there costs 3 %)
-  const double rd = r < kHeurDiskCap ? r : kHeurDiskCap;
-  const double c = 1000.0 * (0.99 * rd + 1.0);
-  float cf = (float)c;
-  if ((double)cf < c) cf = __uint_as_float(__float_as_uint(cf) + 1u);
-  // every node a search touches lies within ~2 * bound + r of P: relative error 1e-5
-  // (>> the f32 error of ~5e-7) over that distance, twice, plus the truncations
-  const double reach_mm = 1000.0 * (2.0 * bound + r);
-  const double m = 2e-5 * reach_mm + 8.0;
-  const uint32_t margin = m < 1e9 ? (uint32_t)m + 1u : 1000000000u;
-  const float k = f32_down(990.0 * (double)h_scale);
-  return Heur{(int32_t)llround(plat * 1e6), (int32_t)llround(plon * 1e6), mx, my, k, cf, margin};
-}
 
 // routing bound and partial edge lengths in whole mm (shared with the oracle)
 __device__ inline int64_t bound_mm_of(double bound) { return (int64_t)floor(bound * 1000.0); }
@@ -645,6 +593,7 @@ __device__ inline int lds_insert(SearchLds<CAP, LM>& L, uint32_t node, bool* isn
     h = h + 1 == (uint32_t)CAP ? 0u : h + 1;
   }
   L.overflow = 1;
+  *isnew = false;
   return -1;
 }
 
@@ -689,77 +638,34 @@ __host__ __device__ inline bool pack_fits(uint32_t bmm, uint32_t sh) {
   return (((uint64_t)bmm << sh) | ((1ull << sh) - 1ull)) < 0xFFFFFFFFull;
 }
 
-// Target (lane) resolved?  Every path through a pending node u reaches T with length >=
-// L(u) + h(u) - h(T) >= fmin - h(T), so L(T) + h(T) < fmin makes T's label final (its
-// length is strictly shorter than any path not yet found, so its time is final too);
-// if even min(L(T), fmin - h(T)) cannot make L + tpart fit the relative bound pd (= B -
-// the sources' smallest exit part), T is unreachable for every source of the task.
-// Integer arithmetic: no rounding margins needed.
+// Target (lane) resolved?  Every later offer to the target node T has length >= kmin +
+// minin(T) (IN criterion), so L(T) below that — or T settled — makes T's (length, time)
+// final; if even min(L(T), kmin + minin(T)) cannot make L + tpart fit the relative bound
+// pd (= B - the sources' smallest exit part), T is unreachable for every source.
 template <int CAP, int LM>
 __device__ inline bool target_resolved(const SearchLds<CAP, LM>& L, const Pack& K, int tslot, uint32_t tpart,
-                                       uint32_t hT, uint32_t pd, uint32_t fmin, bool pend_empty) {
+                                       uint32_t gapT, uint32_t pd, uint32_t kmin, bool pend_empty) {
   if (tslot < 0 || pend_empty) return true;
+  if (L.key[tslot] & kRel) return true;
   const typename LabelT<LM>::W lw = LabelT<LM>::label(L.lab[tslot]);
   const int64_t lab = lw == LabelT<LM>::kNone ? INT64_MAX / 4 : (int64_t)K.d(lw);
-  if (lab + (int64_t)hT < (int64_t)fmin) return true;
-  const int64_t rest = (int64_t)fmin - (int64_t)hT;
-  const int64_t lb = lab < rest ? lab : rest;
-  return lb + (int64_t)tpart > (int64_t)pd;
+  const int64_t next = (int64_t)kmin + (int64_t)gapT;
+  if (lab < next) return true;
+  return (lab < next ? lab : next) + (int64_t)tpart > (int64_t)pd;
 }
 
-// Relax edge (u → dw) with u's packed label pu.  Every relaxing lane evaluates the
-// heuristic of the head itself (deterministic, equal to the stored one), so an
-// improvement's key f = length + h is known without reading an hv entry another lane may
-// be writing; the round's minimum over improvements and kept pending nodes is the next
-// round's fmin.  A label improves when its packed word does (a shorter length, or the
-// same length sooner): the node is then pending again.
-//
-// The bounds prune the relaxation: labels are relative to the search
-// root, so a relaxation is dropped when its length exceeds pd (= B - the sources' exit
-// part) or its time exceeds pt (= bt - their exit time).  Length pruning is monotone in
-// the label order (a shorter label never loses an offer its longer predecessor made), time
-// pruning is not: when `again` (u was relaxed before, with a longer but faster label) an
-// offer cut by the time bound may leave the head holding the withdrawn offer's label.
-// Then the head's label is longer than this offer and *stale is set: the task's labels
-// are not the label-setting search's, and the task is re-run in the exact search
-// (k_general).  Without a stale flag every label below the final fmin is exact (the
-// label-setting fixed point).
-// Taint: a head whose label may be a withdrawn offer is tainted and put
-// back on the pending list; a tainted node's relaxations taint every head they improve or
-// equal (relax_one), so every label that may rest on a withdrawn one carries the taint.
-// Untainted labels below the final fmin are exact; a task whose target ends tainted is
-// re-run in the exact tier.  Returns the slot when it became pending.
-// The re-queued head's key f enters the next round's fmin (fnext): until its taint has
-// reached its descendants no target resting on them may pass target_resolved.
-template <int CAP, int LM>
-__device__ inline int stale_check(SearchLds<CAP, LM>& L, const Pack& K, uint32_t node, uint32_t nd,
-                                  uint32_t& fnext) {
-  using W = typename LabelT<LM>::W;
-  const int sv = lds_find(L, node);
-  if (sv >= 0) {
-    const W lv = LabelT<LM>::label(L.lab[sv]);
-    if (lv != LabelT<LM>::kNone && K.d(lv) > nd) {
-      const uint32_t was = atomicOr(&L.key[sv], kTaint | kInq);
-      if (!(was & kInq)) {
-        const uint32_t f = K.d(lv) + ((uint32_t)L.hv[sv] << 6);
-        fnext = f < fnext ? f : fnext;
-        return sv;
-      }
-    }
-  }
-  return -1;
-}
-
-// The stale test (relax_one): a relaxation pruned by the time bound (tt > pt) from a
-// node relaxed before (again) — its earlier, longer label may have made this offer
-// feasibly, and the head may still hold it (a head whose label is longer than this offer).
-__device__ inline bool stale_chk(bool again, uint32_t tt, uint32_t pt) { return again && tt > pt; }
-
+// Relax edge (u → dw) with u's FINAL packed label pu: the offer (length nd, time tt) is
+// pruned when it breaks a bound (pd / pt: B and bt relative to the root),
+// else it is inserted and kept by atomicMin.  A label improves when its packed word does
+// (a shorter length, or the same length sooner): the node is then pending (again).  The
+// improvement's length enters the next round's kmin.  mq: minin(head) in 16-mm units
+// (the adjacency record carries it), stored with a new key.  Returns the slot when it
+// became newly pending.
 template <int CAP, int LM, bool COUNT = true>
-__device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack& K, uint32_t dw, uint32_t len_mm,
-                                uint32_t time_ds, int32_t vlat, int32_t vlon, typename LabelT<LM>::W pu, uint32_t edge,
-                                uint32_t pd, uint32_t pt, uint32_t mode_bit, bool again, bool tsrc,
-                                uint32_t& relaxed, uint32_t& fnext, bool& isnew, bool& stale) {
+__device__ inline int relax_one(SearchLds<CAP, LM>& L, const Pack& K, uint32_t dw, uint32_t len_mm,
+                                uint32_t time_ds, uint32_t minin, typename LabelT<LM>::W pu, uint32_t edge,
+                                uint32_t pd, uint32_t pt, uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext,
+                                bool& isnew) {
   using W = typename LabelT<LM>::W;
   isnew = false;
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
@@ -767,28 +673,16 @@ __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack
   const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
   if (nd > pd) return -1;
   const uint32_t tt = K.t(pu) + time_ds;  // both < 2^31
-  if (tt > pt) {
-    // a tainted label may be shorter but slower than the exact one: its time-pruned offer
-    // may hide an offer the exact search makes (to a head no taint reaches): the task goes
-    // to the exact tier
-    if (tsrc) stale = true;
-    return stale_chk(again, tt, pt) ? stale_check(L, K, dw & kAdjDstMask, nd, fnext) : -1;
-  }
+  if (tt > pt) return -1;
   const W nw = ((W)nd << K.sh) | (W)tt;  // tt <= pt <= bt < 2^sh - 1
-  const uint32_t h = H(vlat, vlon);
   const int sl = lds_insert<CAP, LM, COUNT>(L, dw & kAdjDstMask, &isnew);
   if (sl < 0) return -1;
-  if (isnew) L.hv[sl] = hq_of(h);
+  if (isnew) L.mi[sl] = mi_of(minin);
   const typename LabelT<LM>::T nb = LabelT<LM>::make(nw, edge);
   const typename LabelT<LM>::T old = atomicMin(&L.lab[sl], nb);
-  const bool imp = LabelT<LM>::label(nb) < LabelT<LM>::label(old);
-  const bool mark = imp || (tsrc && LabelT<LM>::label(nb) == LabelT<LM>::label(old));
-  if (mark) {  // (a head re-queued with the taint holds f too: see stale_check)
-    const uint32_t f = nd + h;
-    fnext = f < fnext ? f : fnext;
-  }
-  if (mark) {
-    const uint32_t ok = atomicOr(&L.key[sl], kInq | (tsrc ? kTaint : 0u));
+  if (LabelT<LM>::label(nb) < LabelT<LM>::label(old)) {
+    knext = nd < knext ? nd : knext;
+    const uint32_t ok = atomicOr(&L.key[sl], kInq);
     if (!(ok & kInq)) return sl;  // newly pending: the caller appends it
   }
   return -1;
@@ -799,23 +693,19 @@ __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Heur& H, const Pack
 // to do aiming them at its own word of `sink` (a per-wave scratch row in LDS whose values
 // are never read), so the exec-mask bookkeeping of the nested ifs is gone — the scalar
 // unit, which carries it, was the search's busiest issue port.  Only a
-// probe chain past the home slot and a time-pruned re-relaxation take branches
-// (wave-uniform, rare).  Same slots, labels and pending list as relax_one.
+// probe chain past the home slot takes a branch (wave-uniform, rare).  Same slots, labels
+// and pending list as relax_one.
 template <int CAP>
-__device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heur& H, const Pack& K,
-                                 uint32_t dw, uint32_t len_mm, uint32_t time_ds, int32_t vlat, int32_t vlon,
-                                 uint32_t pu, uint32_t pd, uint32_t pt, uint32_t mode_bit, bool again, bool tsrc,
-                                 uint32_t& relaxed, uint32_t& fnext, bool& isnew, bool& stale) {
+__device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Pack& K, uint32_t dw, uint32_t len_mm,
+                                 uint32_t time_ds, uint32_t minin, uint32_t pu, uint32_t pd, uint32_t pt,
+                                 uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext, bool& isnew) {
   const bool mode_ok = (((dw >> 28) & 7u) & mode_bit) != 0u;
   relaxed += mode_ok ? 1u : 0u;
   const uint32_t nd = K.d(pu) + len_mm;  // d <= bound < 2^31, len_mm < 2^31: no wrap
   const uint32_t tt = K.t(pu) + time_ds;
   const uint32_t nw = (nd << K.sh) | tt;  // read only where tt <= pt < 2^sh - 1
   const uint32_t node = dw & kAdjDstMask;
-  const bool dok = mode_ok && nd <= pd;
-  bool go = dok && tt <= pt;
-  const bool chk = dok && stale_chk(again, tt, pt);
-  if (tsrc && dok && tt > pt) stale = true;  // (relax_one)
+  bool go = mode_ok && nd <= pd && tt <= pt;
   uint32_t* mine = sink + lane_id();
   const uint32_t h0 = hslot<CAP>(node);
   const uint32_t k0 = atomicCAS(go ? &L.key[h0] : mine, kEmpty, node);
@@ -842,54 +732,34 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Heu
     }
   }
   go = go && sl >= 0;
-  const uint32_t h = H(vlat, vlon);
-  *((go && isnew) ? &L.hv[sl] : reinterpret_cast<uint16_t*>(mine)) = hq_of(h);
+  *((go && isnew) ? &L.mi[sl] : reinterpret_cast<uint16_t*>(mine)) = mi_of(minin);
   const uint32_t old = atomicMin(go ? &L.lab[sl] : mine, nw);
   const bool imp = go && nw < old;
-  const uint32_t f = nd + h;
-  // a tainted node's offer taints the head it improves or equals (stale_check); a head
-  // re-queued with the taint holds fnext like an improved one
-  const bool mark = imp || (tsrc && go && nw == old);
-  fnext = (mark && f < fnext) ? f : fnext;
-  const uint32_t was = atomicOr(mark ? &L.key[sl] : mine, kInq | (tsrc ? kTaint : 0u));
-  int psl = (mark && !(was & kInq)) ? sl : -1;  // newly pending: the caller appends it
-  if (__ballot(chk) != 0ull) {
-    if (chk) psl = stale_check(L, K, node, nd, fnext);  // (chk lanes relaxed nothing above)
-  }
-  return psl;
+  knext = (imp && nd < knext) ? nd : knext;
+  const uint32_t was = atomicOr(imp ? &L.key[sl] : mine, kInq);
+  return (imp && !(was & kInq)) ? sl : -1;  // newly pending: the caller appends it
 }
 
 // G searches per wave, one per lane group, each in its own table Ls[g]: search g is
-// rooted at `start` (label 0); lanes gl < n_tgt of the group hold a target node tnode, its
-// heuristic hT and partial length tpart (mm).  active = false: the group idles.  K packs
-// the labels (route time tracked when K.sh > 0, from adj_t / edge_t: the mode's times).
-// pd / pt prune the relaxations (relative length and time bounds, relax_one); pd also
-// decides when a target is unreachable.  Returns false (per lane, group-uniform) on an LDS-table overflow; *stale
-// (group-uniform) when a time-pruned re-relaxation may have left a withdrawn label.
+// rooted at `start` (label 0); lanes gl < n_tgt of the group hold a target node tnode,
+// its minin gapT (in_gap units: mm, >= 1) and partial length tpart (mm).  active = false:
+// the group idles.  K packs the labels (route time tracked when K.sh > 0, from adj_t /
+// edge_t: the mode's times).  pd / pt prune the relaxations (relative length and time
+// bounds, relax_one); pd also decides when a target is unreachable.  Returns false (per
+// lane, group-uniform) on an LDS-table overflow.
 template <int CAP, int LM, int G = 1>
-__device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur& H, const Pack& K,
-                           uint32_t mode_bit,
-                           bool active, uint32_t start, uint32_t pd, uint32_t pt,
-                           uint32_t delta_mm, uint32_t tnode,
-                           uint32_t tpart, uint32_t hT, int n_tgt, bool* stale_out,
-                           unsigned long long* settled, unsigned long long* relaxed, unsigned long long* rounds,
-                           unsigned long long* stamps = nullptr, uint32_t hroot_in = 0xFFFFFFFFu,
-                           uint32_t* sink = nullptr) {
+__device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack& K, uint32_t mode_bit, bool active,
+                           uint32_t start, uint32_t pd, uint32_t pt, uint32_t tnode, uint32_t tpart, uint32_t gapT,
+                           int n_tgt, unsigned long long* settled, unsigned long long* relaxed,
+                           unsigned long long* rounds, unsigned long long* stamps = nullptr, uint32_t* sink = nullptr) {
   using Gr = Grp<G>;
-  // load-factor limit (probe chains stay short); small tables run fuller
-  // (7/8 on the retry tiers: fewer searches outgrow 448/512 slots; C4 4.79M -> 5.11M
-  // probes/s with the 448x2 tier; the first tier keeps 3/4, as a fuller 160-slot table
-  // only delays the overflow of the searches that outgrow it)
+  // load-factor limit (probe chains stay short); small tables run fuller (7/8 on the
+  // retry tiers; the first tier keeps 3/4, as a fuller 160-slot table only delays the
+  // overflow of the searches that outgrow it)
   constexpr int kMaxKeys = (CAP <= 128 || CAP >= 256) ? (CAP * 7) / 8 : (CAP * 3) / 4;
   const int gl = Gr::gl();
   using W = typename LabelT<LM>::W;
   SearchLds<CAP, LM>& L = Ls[Gr::g()];
-  // h(root): given (the task record, k_tasks), or from the root's coordinates
-  uint32_t hroot = hroot_in;
-  if (hroot_in == 0xFFFFFFFFu) {
-    const int2 sll = g.node_ll[active ? start : 0u];
-    hroot = H(sll.x, sll.y);
-  }
   using Idx = typename SearchLds<CAP, LM>::Idx;
   constexpr int WCAP = SearchLds<CAP, LM>::WCAP;
   const bool timed = K.sh != 0u;  // group-uniform
@@ -897,7 +767,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
   if (active && gl == 0) {
     bool isnew;
     const int sl = lds_insert(L, start, &isnew);
-    L.hv[sl] = hq_of(hroot);
+    L.mi[sl] = 0;
     L.lab[sl] = LabelT<LM>::make(0u, kEmpty);
     L.key[sl] |= kInq;
     L.pend[0] = (Idx)sl;
@@ -908,14 +778,12 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
   if (active && gl < n_tgt && tnode != kEmpty) {
     bool isnew;
     tslot = lds_insert(L, tnode, &isnew);
-    if (tslot >= 0 && isnew) L.hv[tslot] = hq_of(hT);
+    if (tslot >= 0 && isnew) L.mi[tslot] = mi_of(gapT);
   }
   __syncthreads();
   uint32_t my_settled = 0, my_relaxed = 0, my_rounds = 0;
-  bool stale = false;
   unsigned long long cyc[4] = {0, 0, 0, 0};
-  uint32_t fmin = hroot;  // 0xFFFFFFFF: nothing pending
-  const uint32_t hTm = hT + H.margin;  // h(T) with the evaluation margin (see Heur)
+  uint32_t kmin = 0;  // the smallest pending length (0xFFFFFFFF: nothing pending)
   bool done = !active;
   int npend = active ? 1 : 0;  // pending-list length (group-uniform register)
   int nkeys = 0;               // keys the main relax loop added (group-uniform; L.n_keys has the rest)
@@ -923,47 +791,43 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
     OTR_STAMP(t0);
     const int np = done ? 0 : npend;
     OTR_STAMP(t1);
-    const bool res =
-        done || gl >= n_tgt || target_resolved(L, K, tslot, tpart, hTm, pd, fmin, np == 0);
+    const bool res = done || gl >= n_tgt || target_resolved(L, K, tslot, tpart, gapT, pd, kmin, np == 0);
     done = done || Gr::mine(__ballot(!res)) == 0ull || np == 0;
     OTR_STAMP(t2);
     cyc[0] += t1 - t0;
     cyc[1] += t2 - t1;
     if (Gr::all(done)) break;
     if (!done && gl == 0) ++my_rounds;
-    const uint32_t theta = fmin + delta_mm < fmin ? 0xFFFFFFFFu : fmin + delta_mm;  // saturating
-    uint32_t fnext = 0xFFFFFFFFu;
+    uint32_t knext = 0xFFFFFFFFu;
     int kept = 0, nw = 0;
     const int npx = Gr::umax(np);
     for (int base = 0; base < npx; base += Gr::GL) {
       const int k = base + gl;
       const bool in = k < np;
       int sl = 0;
-      uint32_t f = 0, key = 0;
+      uint32_t d = 0, key = 0;
       W lb = 0;
       bool take = false;
       if (in) {
         sl = L.pend[k];
         lb = LabelT<LM>::label(L.lab[sl]);
         key = L.key[sl];
-        f = K.d(lb) + ((uint32_t)L.hv[sl] << 6);  // < 2^32: labels, h < 2^31
-        take = f < theta;
+        d = K.d(lb);
+        take = (uint64_t)d < (uint64_t)kmin + in_gap(L.mi[sl]);  // final (IN criterion)
       }
-      // at most WCAP settles per round; the rest stay pending (order only, never labels)
+      // at most WCAP settles per round; the rest stay pending (still final later)
       take = take && nw + Gr::prefix(__ballot(take)) < WCAP;
       const unsigned long long mt = __ballot(take), mk = __ballot(in && !take);
       __syncthreads();
       if (take) {
-        // off the pending list and marked relaxed: a later improvement re-relaxes it with
-        // kAgain (relax_one's stale check); the relax phase's atomics on this key come after
-        // the barrier below, so a plain store suffices
+        // off the pending list and marked settled; the relax phase's atomics on this key
+        // come after the barrier below, so a plain store suffices
         const uint32_t node = key & kNodeMask;
-        const int wi = nw + Gr::prefix(mt);
-        L.work[wi] = WorkE<W>{node | ((key & kRel) ? kAgain : 0u) | ((key & kTaint) ? kTsrc : 0u), lb};
-        L.key[sl] = node | kRel | (key & kTaint);
+        L.work[nw + Gr::prefix(mt)] = WorkE<W>{node, lb};
+        L.key[sl] = node | kRel;
       } else if (in) {
         L.pend[kept + Gr::prefix(mk)] = (Idx)sl;
-        fnext = f < fnext ? f : fnext;
+        knext = d < knext ? d : knext;
       }
       nw += Gr::count(mt);
       kept += Gr::count(mk);
@@ -982,29 +846,25 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
       bool isnew = false;
       if (k < 4 * nw) {
         const WorkE<W> wk = L.work[k >> 2];
-        const uint32_t wnode = wk.node & kAdjDstMask;
-        const bool again = (wk.node & kAgain) != 0u, tsrc = (wk.node & kTsrc) != 0u;
+        const uint32_t wnode = wk.node;
         const int slot = k & 3;
         if (slot == 0) ++my_settled;
         // the mode's route time of the slot (DevGraph::adj_t, one block per mode), loaded
-        // ahead of the adjacency record and unconditionally: both loads in flight together
-        // (issued after ld16's register barrier it had made every relaxation wait for two
-        // global loads in a row)
+        // beside the adjacency record and unconditionally: both loads in flight together
         const uint32_t tq = adjt[4 * (size_t)wnode + slot];
         const uint4 r = ld16(g.adj + 4 * (size_t)wnode + slot);
         const uint32_t tt = timed ? tq : 0u;
         if constexpr (LM == 0) {
           if (sink)
-            psl = relax_sink<CAP>(L, sink, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab, pd, pt,
-                                  mode_bit, again, tsrc, my_relaxed, fnext, isnew, stale);
+            psl = relax_sink<CAP>(L, sink, K, r.x & ~kAdjMore, r.y, tt, r.z, wk.lab, pd, pt, mode_bit, my_relaxed,
+                                  knext, isnew);
           else
-            psl = relax_one<CAP, LM, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab, 0u,
-                                              pd, pt, mode_bit, again, tsrc, my_relaxed, fnext, isnew, stale);
+            psl = relax_one<CAP, LM, false>(L, K, r.x & ~kAdjMore, r.y, tt, r.z, wk.lab, 0u, pd, pt, mode_bit,
+                                            my_relaxed, knext, isnew);
         } else {
           const uint32_t e0 = LM == 1 ? g.node_row[wnode] : 0u;  // edge id = CSR row start + slot
-          psl = relax_one<CAP, LM, false>(L, H, K, r.x & ~kAdjMore, r.y, tt, (int32_t)r.z, (int32_t)r.w, wk.lab,
-                                            e0 + slot, pd, pt, mode_bit, again, tsrc, my_relaxed, fnext, isnew,
-                                            stale);
+          psl = relax_one<CAP, LM, false>(L, K, r.x & ~kAdjMore, r.y, tt, r.z, wk.lab, e0 + slot, pd, pt, mode_bit,
+                                          my_relaxed, knext, isnew);
         }
         tail = tail || (slot == 3 && (r.x & kAdjMore));
       }
@@ -1027,16 +887,14 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
         const int k = base + gl;
         if (k < 4 * nw && (k & 3) == 3) {
           const WorkE<W> wk = L.work[k >> 2];
-          const uint32_t wnode = wk.node & kAdjDstMask;
-          const bool again = (wk.node & kAgain) != 0u, tsrc = (wk.node & kTsrc) != 0u;
+          const uint32_t wnode = wk.node;
           if (g.adj[4 * (size_t)wnode + 3].x & kAdjMore)
             for (uint32_t e = g.node_row[wnode] + 4; e < g.node_row[wnode + 1]; ++e) {
-              const uint4 pk = ld16(g.edge_pack + e);
-              const int2 vll = g.node_ll[pk.x];
+              const uint4 pk = ld16(g.edge_pack + e);  // {dst, len_mm, attr, minin(dst)}
               const uint32_t tt = timed ? g.et(__builtin_ctz(mode_bit))[e] : 0u;
               bool isnew;
-              const int psl = relax_one(L, H, K, pk.x | ((pk.z & 7u) << 28), pk.y, tt, vll.x, vll.y, wk.lab, e, pd, pt,
-                                        mode_bit, again, tsrc, my_relaxed, fnext, isnew, stale);
+              const int psl = relax_one(L, K, pk.x | ((pk.z & 7u) << 28), pk.y, tt, pk.w, wk.lab, e, pd, pt, mode_bit,
+                                        my_relaxed, knext, isnew);
               if (psl >= 0) {
                 const int p = atomicAdd(&L.n_pend, 1);
                 if (p < CAP) L.pend[p] = (Idx)psl;
@@ -1052,7 +910,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
     __syncthreads();
     OTR_STAMP(t4);
     cyc[3] += t4 - t3;
-    fmin = Gr::min_u32(fnext);
+    kmin = Gr::min_u32(knext);
     const int keys = L.n_keys + nkeys;
     if (!done && (L.overflow || keys > kMaxKeys)) done = true;
     __syncthreads();
@@ -1066,17 +924,14 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Heur
   if (settled) *settled += my_settled;
   if (relaxed) *relaxed += my_relaxed;
   if (rounds) *rounds += my_rounds;
-  // a tainted target: its label may rest on a withdrawn one (the task goes to the exact tier)
-  const bool tainted = stale || (tslot >= 0 && (L.key[tslot] & kTaint) != 0u);
-  *stale_out = Gr::mine(__ballot(tainted)) != 0ull;
   __syncthreads();
   return !L.overflow;
 }
 
 // ------------------------------------------------------------------------------
 // K2b: per-state search inputs, computed once per state instead of once per search
-// task (a step has ~9 tasks): the A* heuristic of the step ending at the state, and per
-// candidate j {entry part mm, source node, h(source node), exit part mm}.
+// task (a step has ~9 tasks): per candidate j {entry part mm, source node, minin(source
+// node) (the IN criterion's gap of a target), exit part mm}.
 // ------------------------------------------------------------------------------
 struct PrepArgs {
   int64_t n_states;
@@ -1085,14 +940,9 @@ struct PrepArgs {
   const int32_t* cand_count;
   const uint32_t* cand_edge;
   const double* cand_p;
-  const int64_t* state_probe;
-  const double* lat;
-  const double* lon;
-  const double* radius;
   const int32_t* state_trace;
   const uint8_t* mode;
-  Heur* heur;     // [S]
-  uint4* cprep;   // [S][OTR_KMAX]: {part(p), src(e), h(src(e)), part(1 - p)}
+  uint4* cprep;   // [S][OTR_KMAX]: {part(p), src(e), minin(src(e)), part(1 - p)}
   uint2* cprep_t; // [S][OTR_KMAX]: {part_t(p), part_t(1 - p)}: the same parts of the edge's route time
   uint2* clen;    // [S][OTR_KMAX]: {len_mm(e), route time(e)}: a same-edge transition's whole-edge terms
   int32_t* nroot; // [S]: the search tasks of the step leaving the state (k_tasks' grouping)
@@ -1110,10 +960,6 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
   if (s >= a.n_states) return;
   const int K = a.cand_count[s];
   if (K <= 0) return;
-  const int64_t pb = a.state_probe[s];
-  const double bound = a.prev[s] >= 0 ? a.bound[s] : 0.0;  // set by k_link for steps only
-  const Heur H = make_heur(a.lat[pb], a.lon[pb], a.radius[s], bound, g.h_scale);
-  if (lane == 0) a.heur[s] = H;
   const int md = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
   const bool turn = (a.turn_modes >> md) & 1u;
   if (lane < K) {
@@ -1121,9 +967,8 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
     const double p = a.cand_p[s * OTR_KMAX + lane];
     const uint32_t len = g.len_mm[e];
     const uint32_t tn = g.edge_src[e];
-    const int2 ll = g.node_ll[tn];
     a.cprep[s * OTR_KMAX + lane] =
-        make_uint4((uint32_t)part_mm(p, len), tn, H(ll.x, ll.y), (uint32_t)part_mm(1.0 - p, len));
+        make_uint4((uint32_t)part_mm(p, len), tn, g.node_minin[tn], (uint32_t)part_mm(1.0 - p, len));
     const uint32_t et = g.et(md)[e];
     a.cprep_t[s * OTR_KMAX + lane] = make_uint2((uint32_t)part_mm(p, et), (uint32_t)part_mm(1.0 - p, et));
     a.clen[s * OTR_KMAX + lane] = make_uint2(len, et);
@@ -1174,11 +1019,6 @@ struct RouteArgs {
   const double* cand_p;
   const int32_t* state_trace;
   const uint8_t* mode;
-  const int64_t* state_probe;
-  const double* lat;
-  const double* lon;
-  const double* radius;       // per state search radius (heuristic disk)
-  const Heur* heur;           // per state (k_prep)
   const uint4* cprep;         // per state candidate (k_prep)
   const uint2* cprep_t;       // per state candidate: route-time parts (k_prep)
   const uint2* clen;          // per state candidate: {len_mm(e), route time(e)} (k_prep)
@@ -1187,27 +1027,11 @@ struct RouteArgs {
   const unsigned long long* list_count;  // retry tiers: length of task_list, on the device
   const int32_t* turn;        // [OTR_MODES][181] turn cost tables (mm), turn modes only
   uint32_t* trans_tc;         // turn cost (mm) per transition, turn modes only
-  double delta;
   double inv_beta[OTR_MODES];
   int32_t* overflow_flag;     // per task: 1/2 retry in a larger LDS table, 3 the global-memory search,
-                              // 4 the exact tier, 5 / 6 the edge-state tiers
+                              // 5 / 6 the edge-state tiers
   uint32_t direct_bmm;        // first tier: bounds above this go straight to the retry tiers
-  int exact;                  // the exact tier: label-setting order (no A* heuristic, rounds of 1 mm)
 };
-
-// The exact order of a retry tier for searches flagged 4 (a withdrawn label, relax_one):
-// no heuristic and rounds 1 mm wide settle exactly the pending nodes of the smallest key,
-// whose labels are final (every step adds >= 1 mm) — the oracle's label-setting order,
-// in parallel over ties; no label is ever relaxed twice, so no label is withdrawn.
-__device__ inline Heur zero_heur(const Heur& H) {
-  Heur z = H;
-  z.mx = 0.0f;
-  z.my = 0.0f;
-  z.k = 0.0f;
-  z.c = 0.0f;
-  z.margin = 0u;
-  return z;
-}
 
 // k_tasks' inputs and outputs
 struct TaskArgs {
@@ -1216,7 +1040,6 @@ struct TaskArgs {
   const int32_t* cand_count;
   const uint32_t* cand_edge;
   const uint32_t* edge_dst;
-  const int2* node_ll;
   const int64_t* task_off;    // exclusive offsets of each step's tasks (scan of k_ntask's counts)
   const double* bound;
   const uint8_t* forced;
@@ -1225,7 +1048,6 @@ struct TaskArgs {
   const uint8_t* mode;
   const uint4* cprep;         // k_prep
   const uint2* cprep_t;       // k_prep
-  const Heur* heur;           // k_prep
   const int64_t* trans_off;
   uint32_t turn_modes;
   int64_t* task_state;
@@ -1243,7 +1065,7 @@ struct TaskArgs {
 // task_mask and the task record k_route reads:
 //   rec[3t]   = {s, sp, root, bound_mm}
 //   rec[3t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16 | turn << 17, mask lo, mask hi}
-//   rec[3t+2] = {h(root), time bound bt, trans_off[s] lo, hi}
+//   rec[3t+2] = {0, time bound bt, trans_off[s] lo, hi}
 // general: the task runs in the global-memory search (a bound whose packed labels would
 // not fit 32 bits, or a turn mode: edge-based labels).
 template <int G>
@@ -1291,12 +1113,10 @@ __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
 #endif
   const uint32_t meta = (uint32_t)a.cand_count[s] | ((uint32_t)md << 8) | ((a.forced[s] ? 1u : 0u) << 10) |
                         (sh << 11) | ((general ? 1u : 0u) << 16) | (turn << 17);
-  const int2 rll = a.node_ll[turn ? a.edge_dst[root] : root];
-  const uint32_t hroot = a.heur[s](rll.x, rll.y);  // the search's first dependent load, done here
   const int64_t to = a.trans_off[s];
   a.rec[3 * o] = make_uint4((uint32_t)s, (uint32_t)sp, root, bmm);
   a.rec[3 * o + 1] = make_uint4(d0min, meta, (uint32_t)same, (uint32_t)(same >> 32));
-  a.rec[3 * o + 2] = make_uint4(hroot, (uint32_t)bt, (uint32_t)to, (uint32_t)((uint64_t)to >> 32));
+  a.rec[3 * o + 2] = make_uint4(0u, (uint32_t)bt, (uint32_t)to, (uint32_t)((uint64_t)to >> 32));
 }
 
 #ifndef OTR_ROUTE2_WAVES
@@ -1329,16 +1149,14 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   OTR_STAMP(ts_in);
   // ---- search inputs (only these stay live through the search)
   bool search, fits, forced;
-  uint32_t tnode = kEmpty, tpart = 0, hT = 0, d0min = 0xFFFFFFFFu, root = 0, bmm = 0, mode_bit = 1, hroot = 0;
+  uint32_t tnode = kEmpty, tpart = 0, gapT = 1, d0min = 0xFFFFFFFFu, root = 0, bmm = 0, mode_bit = 1;
   uint32_t pd = 0, pt = 0xFFFFFFFFu;  // pruning bounds relative to the root (length, time)
   int Kb;
   Pack K;
-  Heur H;
   {
     const uint4 r0 = have ? a.rec[3 * task] : make_uint4(0u, 0u, 0u, 0u);
     const uint4 r1 = have ? a.rec[3 * task + 1] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
     const uint4 r2 = have ? a.rec[3 * task + 2] : make_uint4(0u, 0u, 0u, 0u);
-    hroot = r2.x;
     // the record, stashed in LDS for the transition rows (one LDS read after the search
     // instead of an L2 round trip ahead of the rows' own loads)
     if (lane == 0) {
@@ -1407,26 +1225,17 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     forced = have && ((r1.y >> 10) & 1u);
     const unsigned long long need_mask = __ballot(needed);
     search = have && fits && !forced && feasible_root && Gr::mine(need_mask) != 0ull;
-    H = a.heur[s];
     if (needed) {
       tnode = cq.y;
-      hT = cq.z;
-    }
-    if (LIST && a.exact) {  // the exact tier: label-setting order
-      H = zero_heur(H);
-      hroot = 0u;
-      hT = 0u;
+      gapT = cq.z ? cq.z : 1u;  // minin(target node), >= 1 mm
     }
   }
   unsigned long long settled = 0, relaxed = 0, rounds = 0;
-  bool stale = false;
   OTR_STAMP(ts_set);
   search_init<CAP, LM, G>(Ls);
-  bool ok = search_run<CAP, LM, G>(Ls, gr, H, K, mode_bit, search, root, pd, pt,
-                                   (LIST && a.exact) ? 1u : (uint32_t)(a.delta * 1000.0), tnode, tpart, hT, Kb,
-                                   &stale, &settled,
-                                   &relaxed, &rounds, counters ? counters + 16 * kCShards : nullptr, hroot, sink) &&
-            fits && !stale;
+  bool ok = search_run<CAP, LM, G>(Ls, gr, K, mode_bit, search, root, pd, pt, tnode, tpart, gapT, Kb, &settled,
+                                   &relaxed, &rounds, counters ? counters + 16 * kCShards : nullptr, sink) &&
+            fits;
 #ifdef OTR_FORCE_RETRY
   if (G == 2 && !LIST) ok = false;  // test build: every first-tier task takes the retry tiers
 #endif
@@ -1508,16 +1317,13 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
       }
     }
   }
-  // general (flag 3): the global-memory search; stale (flag 4): the exact search there too;
-  // overflow: retry with a bigger table; a first-tier search with a long bound (> 1.9 km)
-  // that outgrew 160 slots goes straight to the 1024-slot tier (flag 2)
-  // turn modes (flag 5): the edge-state LDS search (otr_edge.h)
+  // general (flag 3): the global-memory search; overflow: retry with a bigger table; a
+  // first-tier search with a long bound (> 1.9 km) that outgrew 160 slots goes straight to
+  // the 1024-slot tier (flag 2); turn modes (flag 5): the edge-state LDS search (otr_edge.h)
   if (have && !ok && !forced && lane == 0) {
     const uint32_t meta = a.rec[3 * task + 1].y;
     const bool general = ((meta >> 16) & 1u) != 0u, turn = ((meta >> 17) & 1u) != 0u;
-    a.overflow_flag[task] = (LIST && a.exact)
-                                ? 3  // what outgrew the exact tier: k_general (exact mode on a withdrawn label)
-                                : (stale ? 4 : (turn ? 5 : (general ? 3 : ((G == 2 && !LIST && bmm > 1900000u) ? 2 : 1))));
+    a.overflow_flag[task] = turn ? 5 : (general ? 3 : ((G == 2 && !LIST && bmm > 1900000u) ? 2 : 1));
   }
 #ifdef OTR_STAMPS
   if (G == 2 && counters && threadIdx.x == 0) {  // task setup and transition rows, wave cycles
@@ -1533,12 +1339,11 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     relaxed = wave_sum_u32((uint32_t)relaxed);
     rounds = wave_sum_u32((uint32_t)rounds);
     const int nk = have && search ? L.n_keys : 0;
-    unsigned long long kk = 0, ntrw = 0, nsearch = 0, nstale = 0;
+    unsigned long long kk = 0, ntrw = 0, nsearch = 0;
     for (int q = 0; q < G; ++q) {
       kk += (unsigned long long)__builtin_amdgcn_readlane(nk, q * Gr::GL);
       ntrw += (unsigned long long)__builtin_amdgcn_readlane(ntr, q * Gr::GL);
       nsearch += (unsigned long long)__builtin_amdgcn_readlane((int)(have && search), q * Gr::GL);
-      nstale += (unsigned long long)__builtin_amdgcn_readlane((int)(have && stale), q * Gr::GL);
     }
     if (threadIdx.x == 0) {
       const int sh = cshard();
@@ -1548,7 +1353,6 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
       atomicAdd(&counters[6 * kCShards + sh], nsearch);
       atomicAdd(&counters[13 * kCShards + sh], rounds);
       atomicAdd(&counters[14 * kCShards + sh], kk);
-      atomicAdd(&counters[15 * kCShards + sh], nstale);
     }
   }
 }
@@ -1856,18 +1660,11 @@ struct PathArgs {
   const double* cand_p;
   const int32_t* state_trace;
   const uint8_t* mode;
-  const int64_t* state_probe;
-  const double* lat;
-  const double* lon;
-  const double* radius;
-  const Heur* heur;            // per state (k_prep)
   const uint4* cprep;          // per state candidate (k_prep)
   const uint2* cprep_t;        // per state candidate: route-time parts (k_prep)
   const int32_t* bt;           // per state: the step's time bound (0.1 s), -1 none
   uint32_t turn_modes;         // bit m: mode m has turn costs (its paths run in k_general)
   const unsigned long long* n_steps_dev;  // number of steps, on the device
-  double delta;
-  int exact;                   // the exact path tier (zero_heur): label-setting order
   int64_t* path_off;           // per state
   int32_t* path_len;           // per state; -1 = same-edge step
   uint32_t* path;              // bump-allocated edge list
@@ -1901,11 +1698,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
   const int64_t s = have ? a.steps[k] : 0;
   const int64_t sp = have ? a.prev[s] : 0;
   bool active = false;
-  uint32_t S = 0, T = kEmpty, bmm = 0, tpart = 0, hT = 0, d0 = 0, mode_bit = 1, pd = 0, pt = 0xFFFFFFFFu;
+  uint32_t S = 0, T = kEmpty, bmm = 0, tpart = 0, gapT = 1, d0 = 0, mode_bit = 1, pd = 0, pt = 0xFFFFFFFFu;
   int mode = 0;
   Pack K;
   K.sh = 0;
-  Heur H{};
   if (have) {
     const int wi = a.winner[sp], wj = a.winner[s];
     const uint32_t ei = a.cand_edge[sp * OTR_KMAX + wi], ej = a.cand_edge[s * OTR_KMAX + wj];
@@ -1947,24 +1743,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
       }
       S = gr.edge_dst[ei];
       T = ct.y;
-      H = a.heur[s];
-      hT = ct.z;
+      gapT = ct.z ? ct.z : 1u;
       tpart = ct.x;
-      if (a.exact) {  // the exact path tier: label-setting order
-        H = zero_heur(H);
-        hT = 0u;
-      }
     }
   }
   search_init<CAP, true, G>(Ls);
-  bool stale = false;
-  const bool ok = search_run<CAP, true, G>(Ls, gr, H, K, mode_bit, active, S, pd, pt,
-                                           a.exact ? 1u : (uint32_t)(a.delta * 1000.0), gl == 0 ? T : kEmpty, tpart,
-                                           hT, 1, &stale, nullptr, nullptr, nullptr, nullptr, a.exact ? 0u : 0xFFFFFFFFu);
+  const bool ok = search_run<CAP, true, G>(Ls, gr, K, mode_bit, active, S, pd, pt, gl == 0 ? T : kEmpty, tpart, gapT,
+                                           1, nullptr, nullptr, nullptr);
   SearchLds<CAP, true>& L = Ls[Gr::g()];
-  if (active && (!ok || stale)) {
-    // a withdrawn label: the exact tier (4); what outgrows that: k_general (3)
-    if (gl == 0) a.overflow_flag[k] = a.exact ? 3 : (stale ? 4 : 1);
+  if (active && !ok) {
+    if (gl == 0) a.overflow_flag[k] = 1;  // the next (larger) table
     active = false;
   }
   // walk predecessor edges T → S (the group's lane 0).  The predecessor node of every

@@ -318,12 +318,12 @@ def test_pruning_semantics_gpu_parity(block, bypass, stale, opts):
 
 
 @pytest.mark.gpu
-def test_withdrawn_label_goes_to_exact_search(stale):
-    """The parallel search relaxes U with the fast edge's label before the chain's shorter
-    one arrives: the time-pruned re-relaxation taints V, the target's label is tainted, the
-    search is flagged (counter 15) and the exact tier (label-setting order) settles it: the
-    transition from W-S has no route, as in the oracle (the trace continues through the
-    candidate on S-U)."""
+def test_withdrawn_label_never_set(stale):
+    """The parallel search must never relax U with the fast edge's (non-final) label: the
+    exact rounds settle U only once the chain's shorter label is final (IN criterion), so V
+    is never labelled from the withdrawn offer and the first tier itself gives the oracle's
+    answer (the transition from W-S has no route; the trace continues through the
+    candidate on S-U) — no retry tier, no global-memory search."""
     from reporter_amd import _lib
     from reporter_amd import matcher as M
     path, ids = stale
@@ -334,5 +334,6 @@ def test_withdrawn_label_goes_to_exact_search(stale):
     want = po.match_batch(po.Graph(path), b, po.params(turn_penalty_factor=0))
     errors, _ = compare(got, want)
     assert not errors, errors
-    assert int(r.counters[15]) > 0  # the first tier flagged the search
-    assert int(r.route_tier_work[9][0]) > 0  # the exact tier ran it
+    assert int(r.route_tier_work[0][0]) > 0  # the first tier searched
+    for t in range(1, 10):
+        assert int(r.route_tier_work[t][0]) == 0, t  # and nothing was retried
