@@ -6,8 +6,7 @@
 //   * turn costs (turn_penalty_factor > 0): the search is over EDGE states, because
 //     the turn cost at a node depends on the edge that entered it;
 //   * steps whose bounds do not fit the 32-bit packing;
-//   * searches that outgrew the largest LDS table;
-//   * searches whose LDS run may have kept a withdrawn label (flag 4, relax_one).
+//   * searches that outgrew the largest LDS table.
 // Labels are 64-bit words key << 38 | (kTcCap - turn) << 17 | time: key = length + turn
 // cost (mm), so one atomicMin keeps the lexicographic minimum of (key, length, time), the
 // oracle's order (oracle.c rkey).  Labels are relative to the search root; relaxations
@@ -17,12 +16,10 @@
 // is read on the device (no host round trip).  Each workgroup owns a slab: an open-
 // addressing hash table {state | relaxed bit, label, round stamp} plus two frontier lists
 // and the list of claimed slots (reset after every search, so a slab is never cleared as
-// a whole).  A search first runs label-correcting rounds over the frontier (every state
-// whose label improved is expanded again); when a time- or turn-pruned re-expansion may
-// have left a withdrawn label (the stale test of relax_one) it is run again in EXACT
-// mode: each round expands only the frontier states of the smallest key, which are final
-// (every offer adds >= 1 mm), i.e. the label-setting search of the oracle, in parallel
-// over equal keys.
+// a whole).  Each round expands the frontier states whose labels are final by the IN
+// criterion of the LDS search (key < smallest frontier key + the state's shortest
+// in-edge: minin(node) in node mode, the state's own edge in edge mode) and carries the
+// others to the next round, i.e. the label-setting search of the oracle, in parallel.
 #pragma once
 #include "otr_kernels.h"
 
@@ -64,7 +61,7 @@ struct GenArgs {
   const int32_t* cand_count;
   const uint32_t* cand_edge;
   const double* cand_p;
-  const uint4* cprep;           // per candidate {part(p), src(e), h(src), part(1 - p)}
+  const uint4* cprep;           // per candidate {part(p), src(e), minin(src), part(1 - p)}
   const uint2* cprep_t;         // per candidate {part_t(p), part_t(1 - p)}
   const int32_t* state_trace;
   const uint8_t* mode_of_trace;
@@ -157,14 +154,6 @@ __device__ inline GOffer g_offer(const DevGraph& G, const GTask& T, uint32_t a, 
 __device__ inline bool g_feasible(const GTask& T, const GOffer& o) {
   return o.d <= T.pd && (!T.time_on || o.t <= T.pt) && o.c <= kTcCap;
 }
-// label L (lexicographically) above offer o?  (stale test: o may be infeasible, so it is
-// compared by components, not packed)
-__device__ inline bool g_above(unsigned long long L, const GOffer& o) {
-  const uint32_t k = g_k(L), d = g_d(L), t = g_t(L);
-  if (k != o.k) return k > o.k;
-  if (d != o.d) return d > o.d;
-  return t > o.t;
-}
 
 // block-wide minimum of a u32 (kGenThreads threads)
 __device__ inline uint32_t g_block_min(uint32_t v, uint32_t* s_red) {
@@ -181,22 +170,18 @@ __device__ inline uint32_t g_block_min(uint32_t v, uint32_t* s_red) {
 }
 
 struct GShared {
-  uint32_t n[2], touched, ovf, stale, red[kGenThreads / OTR_WAVE];
+  uint32_t n[2], touched, ovf, red[kGenThreads / OTR_WAVE];
 };
 
-// Workgroup-wide bounded search of one task in the slab (see the file comment): label-
-// correcting rounds, or EXACT key-order rounds.  Returns false (workgroup-uniform) on slab
-// overflow; *stale (label-correcting mode) when a pruned re-expansion may have left a
-// withdrawn label — the caller resets the slab and searches again in exact mode.
-__device__ bool g_search(const DevGraph& G, const GTask& T, bool exact, uint32_t* key, unsigned long long* lab,
-                         uint32_t* qmark, uint32_t* fr, uint32_t* touched, uint32_t cap, GShared* sh, bool* stale,
-                         unsigned long long* work) {
+// Workgroup-wide bounded search of one task in the slab (see the file comment).  Returns
+// false (workgroup-uniform) on slab overflow.
+__device__ bool g_search(const DevGraph& G, const GTask& T, uint32_t* key, unsigned long long* lab, uint32_t* qmark,
+                         uint32_t* fr, uint32_t* touched, uint32_t cap, GShared* sh, unsigned long long* work) {
   const int tid = threadIdx.x;
   const uint32_t maxk = cap - cap / 8u;
   unsigned long long my_relaxed = 0;
   if (tid == 0) {
     sh->ovf = 0;
-    sh->stale = 0;
     sh->n[0] = 0;
     sh->n[1] = 0;
     // the root state, label 0, queued for round 0
@@ -217,22 +202,13 @@ __device__ bool g_search(const DevGraph& G, const GTask& T, bool exact, uint32_t
   }
   __threadfence_block();
   __syncthreads();
-  // relax state a (label L, expanded before: again) through edge b, queueing for round nr
-  auto relax = [&](uint32_t a, unsigned long long L, bool again, uint32_t b, uint32_t nr, int nxt) {
+  // relax the final state a (label L) through edge b, queueing for round nr
+  auto relax = [&](uint32_t a, unsigned long long L, uint32_t b, uint32_t nr, int nxt) {
     if (!(G.edge_attr[b] & T.mode_bit)) return;
     ++my_relaxed;
     const GOffer o = g_offer(G, T, T.edge_mode ? a : kEmpty, L, b);
     const uint32_t sid = T.edge_mode ? b : G.edge_dst[b];
-    if (!g_feasible(T, o)) {
-      if (again && !exact) {  // the stale test (relax_one): the head holds a label above this offer
-        const int sv = g_find(key, cap, sid);
-        if (sv >= 0) {
-          const unsigned long long Lv = ld_u64(&lab[sv]);
-          if (Lv != kGInf && g_above(Lv, o)) sh->stale = 1;
-        }
-      }
-      return;
-    }
+    if (!g_feasible(T, o)) return;  // pruned (label-setting semantics)
     const unsigned long long w = gpack(o.k, o.c, o.t);
     bool claimed = false;
     const int sl = g_claim(key, cap, sid, &claimed);
@@ -257,14 +233,14 @@ __device__ bool g_search(const DevGraph& G, const GTask& T, bool exact, uint32_t
   unsigned long long expanded = 0;  // states expanded (uniform): the search's "settled" count
   for (;;) {
     const uint32_t n = sh->n[cur];
-    if (n == 0 || sh->ovf || (!exact && sh->stale)) break;
+    if (n == 0 || sh->ovf) break;
     const int nxt = cur ^ 1;
     __syncthreads();
     if (tid == 0) sh->n[nxt] = 0;
     const uint32_t nn = n < cap ? n : cap;
-    // exact mode: only the frontier's smallest key is final
-    uint32_t kmin = 0;
-    if (exact) {
+    // the frontier's smallest key: with each state's shortest in-edge it decides finality
+    uint32_t kmin;
+    {
       uint32_t m = 0xFFFFFFFFu;
       for (uint32_t i = tid; i < nn; i += kGenThreads) {
         const uint32_t sl = ld_u32(&fr[(size_t)cur * cap + i]);
@@ -277,7 +253,10 @@ __device__ bool g_search(const DevGraph& G, const GTask& T, bool exact, uint32_t
     for (uint32_t i = tid; i < nn; i += kGenThreads) {
       const uint32_t sl = ld_u32(&fr[(size_t)cur * cap + i]);
       const unsigned long long L = ld_u64(&lab[sl]);
-      if (exact && g_k(L) != kmin) {  // not final yet: carried to the next round
+      const uint32_t id = ld_u32(&key[sl]) & kGIdMask;
+      const uint32_t mi = T.edge_mode ? G.len_mm[id] : G.node_minin[id];
+      const uint32_t gap = id == T.root ? 1u : (mi ? mi : 1u);
+      if ((uint64_t)g_k(L) >= (uint64_t)kmin + gap) {  // not final yet: carried to the next round
         if (atomicExch(&qmark[sl], round + 2u) != round + 2u) {
           const uint32_t p = atomicAdd(&sh->n[nxt], 1u);
           if (p < cap) fr[(size_t)nxt * cap + p] = sl;
@@ -287,10 +266,9 @@ __device__ bool g_search(const DevGraph& G, const GTask& T, bool exact, uint32_t
       }
       const uint32_t was = atomicOr(&key[sl], kGRel);
       const uint32_t a = was & kGIdMask;
-      const bool again = (was & kGRel) != 0u;
       ++expanded;
       const uint32_t v = T.edge_mode ? G.edge_dst[a] : a;
-      for (uint32_t e = G.node_row[v]; e < G.node_row[v + 1]; ++e) relax(a, L, again, e, round + 1u, nxt);
+      for (uint32_t e = G.node_row[v]; e < G.node_row[v + 1]; ++e) relax(a, L, e, round + 1u, nxt);
     }
     __threadfence_block();
     __syncthreads();
@@ -303,7 +281,6 @@ __device__ bool g_search(const DevGraph& G, const GTask& T, bool exact, uint32_t
     atomicAdd(&work[4 * kCShards + shd], my_relaxed);
     atomicAdd(&work[3 * kCShards + shd], expanded);
   }
-  *stale = !exact && sh->stale != 0;
   const bool ok = sh->ovf == 0;
   __syncthreads();
   return ok;
@@ -418,16 +395,9 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
   const int tid = threadIdx.x;
   if (tid == 0) sh.touched = 0;  // the slab is clean (cleared at allocation, reset after every search)
   __syncthreads();
-  // one search (label-correcting, then exact if it may have kept a withdrawn label),
-  // leaving its labels in the slab; false on slab overflow
+  // one search, leaving its labels in the slab; false on slab overflow
   auto run = [&](const GTask& T, unsigned long long* work) -> bool {
-    bool stale = false;
-    bool ok = g_search(G, T, false, key, lab, qmark, fr, touched, cap, &sh, &stale, work);
-    if (ok && stale) {
-      g_reset(key, lab, qmark, touched, &sh, cap);
-      ok = g_search(G, T, true, key, lab, qmark, fr, touched, cap, &sh, &stale, work);
-    }
-    return ok;
+    return g_search(G, T, key, lab, qmark, fr, touched, cap, &sh, work);
   };
   for (int64_t k = blockIdx.x; k < count; k += gridDim.x) {
     const int64_t item = a.list[k];
