@@ -44,14 +44,14 @@ T_BEGIN = 1483228800
 # HBM bytes per launch of the dominant kernel from separate FETCH_SIZE / WRITE_SIZE
 # --pmc passes of this command (tools/profile_gpu.sh, tools/pmc_summary.py), when the
 # committed summary holds the kernel
-PMC_SUMMARY = os.environ.get('OTR_PMC_SUMMARY', os.path.join(ROOT, 'profiles', 'r02_pmc.json'))
+PMC_SUMMARY = os.environ.get('OTR_PMC_SUMMARY', os.path.join(ROOT, 'profiles', 'r03_exact_pmc.json'))
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def kernel_name(code, turns=False):
+def kernel_name(code, turns=False, first=False):
     """rocprofv3 name of a route kernel (otr_batch_result.route_tier_code); turns: kept for
     callers (turn-mode tasks run in the edge-state kernels, code 700,000 + CAP)."""
     if code < 0:  # the global-memory search: -1 on 32K-state slabs, -2 on 1M-state slabs
@@ -63,7 +63,7 @@ def kernel_name(code, turns=False):
     if 900000 <= code < 1000000:  # the 64-bit label tier: 900,000 + CAP
         return 'k_route<%d, 1, true, true, false>' % (code - 900000)
     cap, g = code // 10, code % 10
-    return 'k_route<%d, %d, %s, false, false>' % (cap, g, 'false' if code == 1602 or code == 2561 else 'true')
+    return 'k_route<%d, %d, %s, false, false>' % (cap, g, 'false' if first else 'true')
 
 
 def route_bytes(work):
@@ -411,7 +411,7 @@ def main():
     achieved = dom_bytes / (launch_ms * 1e-3) / 1e9
     # turn-cost modes run the route kernels compiled with the turn walk
     turns = float(W['meili'].get('turn_penalty_factor', 1.0)) > 0.0
-    tier_table = {kernel_name(d['code'], turns): {'ms_per_launch': round(d['ms'] / d['launches'], 3),
+    tier_table = {kernel_name(d['code'], turns, t == 0): {'ms_per_launch': round(d['ms'] / d['launches'], 3),
                                           'searches_per_launch': int(d['work'][0] // d['launches']),
                                           'settled_per_launch': int(d['work'][1] // d['launches']),
                                           'relaxed_per_launch': int(d['work'][2] // d['launches']),
@@ -421,16 +421,18 @@ def main():
                   for t, d in sorted(tiers.items())}
     traffic, traffic_src = None, None
     if os.path.exists(PMC_SUMMARY):
-        k = json.load(open(PMC_SUMMARY)).get('kernels', {}).get(kernel_name(dom['code'], turns), {})
+        k = json.load(open(PMC_SUMMARY)).get('kernels', {}).get(kernel_name(dom['code'], turns, dom_t == 0), {})
         if 'fetch_bytes_per_launch' in k and 'write_bytes_per_launch' in k:
             traffic = int(k['fetch_bytes_per_launch'] + k['write_bytes_per_launch'])
             traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
 
-    # ---- rank 0, N = 1: oracle sample (CPU baseline) and its bit-exact comparison
+    # ---- rank 0: oracle sample (CPU baseline) and its bit-exact comparison, on rank 0's
+    # own shard at every N (after the timed region; the other ranks wait at the closing
+    # barrier), so a multi-GPU line carries its own parity evidence
     cpu, parity = None, None
     n_cpu = args.cpu_traces if args.cpu_traces is not None else {'c2': 6000, 'c2dep': 2000, 'c5mix': 6000, 'c4': 600,
                                                                  'c5': 3000, 'c3': 6000}[args.workload]
-    if rank == 0 and world == 1 and n_cpu > 0:
+    if rank == 0 and n_cpu > 0:
         from oracle import pyoracle as po
         from oracle.compare import compare, subset
         g = po.Graph(gpath)
@@ -441,10 +443,12 @@ def main():
         want = po.match_batch(g, sample, po.params(**W['meili']), threads=threads)
         dt = time.perf_counter() - tc
         cpu = {'value': round(sample.n_probes / dt, 1), 'unit': 'probes/s', 'cores': threads, 'kind': 'port',
-               'sample': '%d traces x %d probes of the same %s workload through oracle/liboracle.so '
+               'sample': '%d traces x %d probes of the same %s workload%s through oracle/liboracle.so '
                          '(scalar C restatement, %d pthreads = the cores this process may use: affinity capped by '
-                         'the cgroup CPU quota; os.cpu_count() = %d; %.1f s)' % (sample.n_traces, W['points'], args.workload.upper(), threads,
-                                            os.cpu_count() or 0, dt)}
+                         'the cgroup CPU quota; os.cpu_count() = %d; %.1f s)' % (
+                             sample.n_traces, W['points'], args.workload.upper(),
+                             (' (rank 0 shard of %d)' % world) if world > 1 else '', threads, os.cpu_count() or 0,
+                             dt)}
         # the GPU output of the same traces: this batch (copy-out run, untimed), sliced
         got_full = _lib.result_to_numpy(M.Matcher().match_batch(mine, copy_out=True))
         errors, stats = compare(subset(got_full, idx, mine.offsets), want)
@@ -537,7 +541,7 @@ def main():
                        'work': {'states': int(sum(r.n_states for r in rs)), 'grid_cells': int(counters[0]),
                                 'shape_segments_tested': int(counters[1]), 'candidates': int(counters[2]),
                                 'output_segments': int(counters[7])}},
-            'roofline': {'kernel': kernel_name(dom['code'], turns) + ' (dominant route-search kernel of this workload)',
+            'roofline': {'kernel': kernel_name(dom['code'], turns, dom_t == 0) + ' (dominant route-search kernel of this workload)',
                          'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': traffic,
                          'traffic_source': traffic_src, 'launch_ms': round(launch_ms, 3),
@@ -562,6 +566,7 @@ def main():
         if parity is not None and not parity['ok']:
             raise SystemExit('bench: GPU output differs from the oracle sample: %s' % parity['errors'])
     if world > 1:
+        dist.barrier()  # rank 0's oracle sample and line come after the timed region
         dist.destroy_process_group()
 
 
