@@ -907,8 +907,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       tb(OTR_STAGE_ROUTE);
       const int64_t units = (NT + 1) / 2;
       const unsigned grid = (unsigned)(8 * ((units + 7) / 8));
-      OTR_ROUTE_LAUNCH(160, 2, false, grid, ra, rwork);
-      out->route_tier_code[0] = 1602;
+      OTR_ROUTE_LAUNCH(OTR_CAP1, 2, false, grid, ra, rwork);
+      out->route_tier_code[0] = OTR_CAP1 * 10 + 2;
     } else {
       tb(OTR_STAGE_ROUTE);
       const unsigned grid = (unsigned)(8 * ((NT + 7) / 8));
@@ -1092,7 +1092,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       tb(OTR_STAGE_PATHS);
       {
         const int64_t units = (S + 1) / 2;  // upper bound: two searches per wave
-        k_paths<160, 2><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, pa, nullptr, nullptr);
+        k_paths<OTR_CAP1, 2><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, pa, nullptr, nullptr);
       }
       te(OTR_STAGE_PATHS);
       tb(OTR_STAGE_PATHS_BIG);

@@ -20,6 +20,15 @@
 #include "otr_device.h"
 #include "otr_report.h"
 
+// the first tier's table (slots per search, two searches per wave) and its load limit in
+// eighths (A/B knobs)
+#ifndef OTR_CAP1
+#define OTR_CAP1 160
+#endif
+#ifndef OTR_LOAD1
+#define OTR_LOAD1 7
+#endif
+
 namespace otr {
 
 struct BatchDev {
@@ -753,10 +762,10 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
                            int n_tgt, unsigned long long* settled, unsigned long long* relaxed,
                            unsigned long long* rounds, unsigned long long* stamps = nullptr, uint32_t* sink = nullptr) {
   using Gr = Grp<G>;
-  // load-factor limit (probe chains stay short); small tables run fuller (7/8 on the
-  // retry tiers; the first tier keeps 3/4, as a fuller 160-slot table only delays the
-  // overflow of the searches that outgrow it)
-  constexpr int kMaxKeys = (CAP <= 128 || CAP >= 256) ? (CAP * 7) / 8 : (CAP * 3) / 4;
+  // load-factor limit (probe chains stay short): 7/8 (the exact searches run to the
+  // bounds, so a fuller first-tier table keeps more of them out of the retry tiers: C2
+  // 32.5M -> 33.1M probes/s against 3/4, profiles/r03_ab_load7_bench_c2.json)
+  constexpr int kMaxKeys = (CAP <= 128 || CAP >= 256) ? (CAP * 7) / 8 : (CAP * OTR_LOAD1) / 8;
   const int gl = Gr::gl();
   using W = typename LabelT<LM>::W;
   SearchLds<CAP, LM>& L = Ls[Gr::g()];
