@@ -56,8 +56,8 @@ def kernel_name(code, turns=False, first=False):
     callers (turn-mode tasks run in the edge-state kernels, code 700,000 + CAP)."""
     if code < 0:  # the global-memory search: -1 on 32K-state slabs, -2 on 1M-state slabs
         return 'k_general' if code == -1 else 'k_general (1M-state slabs)'
-    if 700000 <= code < 800000:  # the edge-state tiers (turn costs): 700,000 + first CAP
-        return 'k_route_edge<%d>' % (code - 700000)
+    if code >= 7000000:  # the edge-state tiers (turn costs): 7,000,000 + first CAP * 100 + targets
+        return 'k_route_edge<%d, %d>' % ((code - 7000000) // 100, code % 100)
     # the timed launches run the LDS route kernels compiled without work counting (the
     # last template argument, CNT = false; the instrumented step runs CNT = true)
     if 900000 <= code < 1000000:  # the 64-bit label tier: 900,000 + CAP

@@ -195,7 +195,8 @@ typedef struct otr_batch_result {
   /* per route-search kernel: slot 0 the first tier (k_route<160,2>), 1..5 the LDS retry
    * tiers in order, 6 / 7 the global-memory search (32K / 1M-state slabs), 8 the 64-bit
    * label LDS tier (steps whose length and time bits exceed 32), 9 the edge-state LDS
-   * tiers (modes with turn costs).  code: CAP*10+G
+   * tiers (modes with turn costs).  code: 7,000,000 + CAP*100 + targets of the edge-state
+   * tier, CAP*10+G
    * of an LDS tier, 900000 + CAP the 64-bit tier, -1 / -2 the global tiers, 0 unused.
    * work: searches, settled nodes (expanded states), relaxed edges, transition entries
    * written.  ms (OTR_BATCH_TIMING): HIP-event time of the kernel on the matcher's stream. */

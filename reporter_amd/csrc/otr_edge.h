@@ -24,29 +24,32 @@
 
 namespace otr {
 
-template <int CAP>
+// TG: the targets a search holds (lanes < TG; 32 when every mode keeps <= 32 candidates).
+// The state's end heading (the turn out of it) is read from DevGraph::edge_head by the
+// relaxing lane, beside the adjacency loads, rather than kept per slot: 18 B per state, so
+// more waves fit the LDS (the search waits on memory, not issue).
+template <int CAP, int TG = OTR_WAVE>
 struct EdgeLds {
   static constexpr int WCAP = CAP <= 512 ? 64 : 128;
   unsigned long long lab[CAP];   // gpack label, kGInf: none
   uint32_t key[CAP];             // edge id | kInq | kRel, kEmpty
   uint32_t node[CAP];            // dst(edge): where the state stands
   uint16_t mi[CAP];              // mi_of(len(edge)): the IN criterion's gap of the state
-  uint16_t hend[CAP];            // end heading of the edge (the turn out of the state)
   uint16_t pend[CAP];            // pending slots
   uint16_t wslot[WCAP];          // this round's settled states' slots
   unsigned long long wlab[WCAP];  // ... and their labels
   // targets (lanes of the wave): the best offer, entry parts, begin heading of ej
-  unsigned long long tlab[OTR_WAVE];
-  uint32_t tpart[OTR_WAVE], tpt[OTR_WAVE];
-  uint16_t thb[OTR_WAVE];
+  unsigned long long tlab[TG];
+  uint32_t tpart[TG], tpt[TG];
+  uint16_t thb[TG];
   // target nodes src(ej) → lane masks (open addressing)
-  uint32_t tmap_node[OTR_WAVE];
-  unsigned long long tmap_mask[OTR_WAVE];
+  uint32_t tmap_node[TG];
+  unsigned long long tmap_mask[TG];
   int n_pend, n_keys, overflow;
 };
 
-template <int CAP>
-__device__ inline int e_find(const EdgeLds<CAP>& L, uint32_t e) {
+template <int CAP, int TG>
+__device__ inline int e_find(const EdgeLds<CAP, TG>& L, uint32_t e) {
   uint32_t h = hslot<CAP>(e);
   for (int probe = 0; probe < CAP; ++probe) {
     const uint32_t k = L.key[h];
@@ -57,8 +60,8 @@ __device__ inline int e_find(const EdgeLds<CAP>& L, uint32_t e) {
   return -1;
 }
 
-template <int CAP>
-__device__ inline int e_insert(EdgeLds<CAP>& L, uint32_t e, bool* isnew) {
+template <int CAP, int TG>
+__device__ inline int e_insert(EdgeLds<CAP, TG>& L, uint32_t e, bool* isnew) {
   uint32_t h = hslot<CAP>(e);
   for (int probe = 0; probe < CAP; ++probe) {
     const uint32_t k = atomicCAS(&L.key[h], kEmpty, e);
@@ -77,16 +80,19 @@ __device__ inline int e_insert(EdgeLds<CAP>& L, uint32_t e, bool* isnew) {
   return -1;
 }
 
-__device__ inline uint32_t tmap_home(uint32_t v) { return (v * 0x9E3779B1u) >> 26; }  // 64 slots
+template <int TG>
+__device__ inline uint32_t tmap_home(uint32_t v) {  // TG slots (a power of two)
+  return (v * 0x9E3779B1u) >> (32 - __builtin_ctz((unsigned)TG));
+}
 
-template <int CAP>
-__device__ inline unsigned long long tmap_get(const EdgeLds<CAP>& L, uint32_t v) {
-  uint32_t h = tmap_home(v);
-  for (int probe = 0; probe < OTR_WAVE; ++probe) {
+template <int CAP, int TG>
+__device__ inline unsigned long long tmap_get(const EdgeLds<CAP, TG>& L, uint32_t v) {
+  uint32_t h = tmap_home<TG>(v);
+  for (int probe = 0; probe < TG; ++probe) {
     const uint32_t k = L.tmap_node[h];
     if (k == kEmpty) return 0ull;
     if (k == v) return L.tmap_mask[h];
-    h = (h + 1) & (OTR_WAVE - 1);
+    h = (h + 1) & (TG - 1);
   }
   return 0ull;
 }
@@ -112,9 +118,9 @@ __device__ inline EOffer e_step(unsigned long long lb, uint32_t tc, uint32_t len
 // Relax the FINAL state (label lb, at node v, end heading ha) through the edge b (head w,
 // length len, time tt, begin / end headings hb / he, access in dw's high bits).  Returns
 // the slot when b became newly pending.
-template <int CAP>
-__device__ inline int e_relax(EdgeLds<CAP>& L, const int32_t* turn, unsigned long long lb, uint32_t ha, uint32_t dw,
-                              uint32_t len, uint32_t tt, uint32_t b, uint32_t hb, uint32_t he, uint32_t pd, uint32_t pt,
+template <int CAP, int TG>
+__device__ inline int e_relax(EdgeLds<CAP, TG>& L, const int32_t* turn, unsigned long long lb, uint32_t ha, uint32_t dw,
+                              uint32_t len, uint32_t tt, uint32_t b, uint32_t hb, uint32_t pd, uint32_t pt,
                               uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext, uint32_t& dnext, bool& isnew) {
   isnew = false;
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
@@ -127,7 +133,6 @@ __device__ inline int e_relax(EdgeLds<CAP>& L, const int32_t* turn, unsigned lon
   if (sl < 0) return -1;
   if (isnew) {
     L.node[sl] = w;
-    L.hend[sl] = (uint16_t)he;
     L.mi[sl] = mi_of(len);
   }
   const unsigned long long nw = gpack(o.k, o.c, o.t);
@@ -143,8 +148,8 @@ __device__ inline int e_relax(EdgeLds<CAP>& L, const int32_t* turn, unsigned lon
 
 // The settled (final) state's offers to the targets at its node v (the turn into ej + the
 // entry part), kept as each target's lexicographic minimum.
-template <int CAP>
-__device__ inline void e_target_offers(EdgeLds<CAP>& L, const int32_t* turn, unsigned long long lb, uint32_t ha,
+template <int CAP, int TG>
+__device__ inline void e_target_offers(EdgeLds<CAP, TG>& L, const int32_t* turn, unsigned long long lb, uint32_t ha,
                                        uint32_t v, uint32_t pd, uint32_t pt) {
   unsigned long long m = tmap_get(L, v);
   while (m) {
@@ -156,15 +161,17 @@ __device__ inline void e_target_offers(EdgeLds<CAP>& L, const int32_t* turn, uns
   }
 }
 
-template <int CAP>
-__device__ inline void e_init(EdgeLds<CAP>& L) {
+template <int CAP, int TG>
+__device__ inline void e_init(EdgeLds<CAP, TG>& L) {
   for (int k = threadIdx.x; k < CAP; k += OTR_WAVE) {
     L.key[k] = kEmpty;
     L.lab[k] = kGInf;
   }
-  L.tlab[threadIdx.x] = kGInf;
-  L.tmap_node[threadIdx.x] = kEmpty;
-  L.tmap_mask[threadIdx.x] = 0ull;
+  if (threadIdx.x < TG) {
+    L.tlab[threadIdx.x] = kGInf;
+    L.tmap_node[threadIdx.x] = kEmpty;
+    L.tmap_mask[threadIdx.x] = 0ull;
+  }
   if (threadIdx.x == 0) {
     L.n_pend = 0;
     L.n_keys = 0;
@@ -173,43 +180,42 @@ __device__ inline void e_init(EdgeLds<CAP>& L) {
   __syncthreads();
 }
 
-// One search (one wave) from root edge `root` (label 0 at dst(root) = rnode, end heading
-// rhe).  Lanes < n_tgt hold a target: node tv = src(ej), entry parts tpart / tpt, begin
+// One search (one wave) from root edge `root` (label 0 at dst(root) = rnode).  Lanes <
+// n_tgt (<= TG) hold a target: node tv = src(ej), entry parts tpart / tpt, begin
 // heading thb.  pd / pt: the relative bounds.  Returns false on overflow.  timed = false:
 // route times are not tracked (pt unused).
-template <int CAP>
-__device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const int32_t* turn, int md, bool active,
-                            uint32_t root, uint32_t rnode, uint32_t rhe, uint32_t pd, uint32_t pt, bool timed,
+template <int CAP, int TG>
+__device__ bool edge_search(EdgeLds<CAP, TG>& L, const DevGraph& g, const int32_t* turn, int md, bool active,
+                            uint32_t root, uint32_t rnode, uint32_t pd, uint32_t pt, bool timed,
                             int n_tgt, uint32_t tv, uint32_t tpart, uint32_t tpt, uint32_t thb,
                             unsigned long long* settled, unsigned long long* relaxed) {
   constexpr int kMaxKeys = (CAP * 7) / 8;
-  constexpr int WCAP = EdgeLds<CAP>::WCAP;
+  constexpr int WCAP = EdgeLds<CAP, TG>::WCAP;
   const int gl = (int)threadIdx.x;
   const uint32_t mode_bit = 1u << md;
   const uint32_t* adjt = g.adj_t + (size_t)md * g.adj_t_stride;
   const uint32_t* et = g.et(md);
   if (!timed) pt = 0xFFFFFFFFu;
   // targets
-  const bool tgt = active && gl < n_tgt && tv != kEmpty;
+  const bool tgt = active && gl < n_tgt && gl < TG && tv != kEmpty;
   if (tgt) {
     L.tpart[gl] = tpart;
     L.tpt[gl] = timed ? tpt : 0u;
     L.thb[gl] = (uint16_t)thb;
-    uint32_t h = tmap_home(tv);
-    for (int probe = 0; probe < OTR_WAVE; ++probe) {
+    uint32_t h = tmap_home<TG>(tv);
+    for (int probe = 0; probe < TG; ++probe) {
       const uint32_t k = atomicCAS(&L.tmap_node[h], kEmpty, tv);
       if (k == kEmpty || k == tv) {
         atomicOr(&L.tmap_mask[h], 1ull << gl);
         break;
       }
-      h = (h + 1) & (OTR_WAVE - 1);
+      h = (h + 1) & (TG - 1);
     }
   }
   if (active && gl == 0) {
     bool isnew;
     const int sl = e_insert(L, root, &isnew);
     L.node[sl] = rnode;
-    L.hend[sl] = (uint16_t)rhe;
     L.mi[sl] = 0;
     L.lab[sl] = gpack(0u, 0u, 0u);
     L.key[sl] |= kInq;
@@ -277,15 +283,16 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const int32_t* t
       if (k < 4 * nw) {
         const int sl = L.wslot[k >> 2];
         const unsigned long long lb = L.wlab[k >> 2];
-        const uint32_t v = L.node[sl], ha = L.hend[sl];
+        const uint32_t v = L.node[sl], a = L.key[sl] & kNodeMask;
         const int slot = k & 3;
         if (slot == 0) ++my_settled;
+        const uint32_t ha = (uint32_t)(uint16_t)g.edge_head[a].y;  // beside the adjacency loads
         const uint32_t tq = adjt[4 * (size_t)v + slot];
         const uint2 xe = g.adj_e[4 * (size_t)v + slot];
         const uint4 r = ld16(g.adj + 4 * (size_t)v + slot);
         if (slot == 0) e_target_offers(L, turn, lb, ha, v, pd, pt);
-        psl = e_relax(L, turn, lb, ha, r.x & ~kAdjMore, r.y, timed ? tq : 0u, xe.x, xe.y & 0xFFFFu, xe.y >> 16, pd, pt,
-                      mode_bit, my_relaxed, knext, dnext, isnew);
+        psl = e_relax(L, turn, lb, ha, r.x & ~kAdjMore, r.y, timed ? tq : 0u, xe.x, xe.y & 0xFFFFu, pd, pt, mode_bit,
+                      my_relaxed, knext, dnext, isnew);
         tail = tail || (slot == 3 && (r.x & kAdjMore));
       }
       nkeys += __popcll(__ballot(isnew));
@@ -305,15 +312,15 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const int32_t* t
         if (k < 4 * nw && (k & 3) == 3) {
           const int sl = L.wslot[k >> 2];
           const unsigned long long lb = L.wlab[k >> 2];
-          const uint32_t v = L.node[sl], ha = L.hend[sl];
+          const uint32_t v = L.node[sl];
+          const uint32_t ha = (uint32_t)(uint16_t)g.edge_head[L.key[sl] & kNodeMask].y;
           if (g.adj[4 * (size_t)v + 3].x & kAdjMore)
             for (uint32_t e = g.node_row[v] + 4; e < g.node_row[v + 1]; ++e) {
               const uint4 pk = ld16(g.edge_pack + e);
               const short2 hh = g.edge_head[e];
               bool isnew;
               const int psl = e_relax(L, turn, lb, ha, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e,
-                                      (uint32_t)hh.x, (uint32_t)hh.y, pd, pt, mode_bit, my_relaxed, knext, dnext,
-                                      isnew);
+                                      (uint32_t)hh.x, pd, pt, mode_bit, my_relaxed, knext, dnext, isnew);
               if (isnew) atomicAdd(&L.n_keys, 1);
               if (psl >= 0) {
                 const int p = atomicAdd(&L.n_pend, 1);
@@ -345,10 +352,11 @@ __device__ bool edge_search(EdgeLds<CAP>& L, const DevGraph& g, const int32_t* t
 // K3e: edge-state route tasks (turn modes), a fixed grid over the device-side list of
 // the tasks flagged 5 (k_route) or 6 (this tier's overflows, for the larger table).
 // ------------------------------------------------------------------------------
-// What outgrows the 2048-state table goes to k_general (3).
-template <int CAP>
+// What outgrows the 2048-state table goes to k_general (3).  TG: the targets a search
+// holds (32 when every mode keeps <= 32 candidates, else 64).
+template <int CAP, int TG>
 __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, unsigned long long* counters) {
-  __shared__ EdgeLds<CAP> L;
+  __shared__ EdgeLds<CAP, TG> L;
   const int64_t n_tasks = (int64_t)*a.list_count;
   const int lane = (int)threadIdx.x;
   for (int64_t w = blockIdx.x; w < n_tasks; w += gridDim.x) {
@@ -383,15 +391,15 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
       }
     }
     const bool root_ok = d0 <= bmm && (bt < 0 || t0 <= (uint32_t)bt);
-    const bool search = Kb <= OTR_WAVE && !forced && root_ok && __ballot(needed) != 0ull;
+    const bool search = Kb <= TG && !forced && root_ok && __ballot(needed) != 0ull;
     const uint32_t pd = bmm >= d0 ? bmm - d0 : 0u;
     const uint32_t pt = bt >= 0 && t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
     e_init(L);
     unsigned long long settled = 0, relaxed = 0;
-    const bool ok = edge_search<CAP>(L, gr, a.turn + 181 * md, md, search, ei, gr.edge_dst[ei],
-                                     (uint32_t)(uint16_t)gr.edge_head[ei].y, pd, pt, bt >= 0, Kb, tv, tpart, tpt, thb,
-                                     counters ? &settled : nullptr, counters ? &relaxed : nullptr) &&
-                    Kb <= OTR_WAVE;
+    const bool ok = edge_search<CAP, TG>(L, gr, a.turn + 181 * md, md, search, ei, gr.edge_dst[ei], pd, pt, bt >= 0,
+                                         Kb, tv, tpart, tpt, thb, counters ? &settled : nullptr,
+                                         counters ? &relaxed : nullptr) &&
+                    Kb <= TG;
     if (ok) {
       uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
       if (lane < Kb) {
@@ -444,7 +452,7 @@ template <int CAP>
 __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, const int32_t* turn_tab,
                                                    const int64_t* step_list, const unsigned long long* list_count,
                                                    int32_t overflow_flag) {
-  __shared__ EdgeLds<CAP> L;
+  __shared__ EdgeLds<CAP, 32> L;
   __shared__ uint32_t s_rev[CAP];
   const int64_t n_list = (int64_t)*list_count;
   const int lane = (int)threadIdx.x;
@@ -465,8 +473,8 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
     const uint32_t pt = bt >= 0 && t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
     const uint32_t thb = (uint32_t)gr.edge_head[ej].x;
     e_init(L);
-    const bool ok = edge_search<CAP>(L, gr, turn, md, true, ei, gr.edge_dst[ei], (uint32_t)(uint16_t)gr.edge_head[ei].y,
-                                     pd, pt, bt >= 0, 1, ct.y, ct.x, tpt, thb, nullptr, nullptr);
+    const bool ok = edge_search<CAP, 32>(L, gr, turn, md, true, ei, gr.edge_dst[ei], pd, pt, bt >= 0, 1, ct.y, ct.x,
+                                         tpt, thb, nullptr, nullptr);
     const unsigned long long tl = L.tlab[0];
     int n = -1;
     if (ok && tl != kGInf) {
@@ -482,7 +490,7 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
           if (sx < 0 || L.lab[sx] == kGInf) continue;
           const unsigned long long lx = L.lab[sx];
           EOffer o;
-          o.c = g_c(lx) + (uint32_t)turn[turn_degree((int)L.hend[sx], (int)thb)];
+          o.c = g_c(lx) + (uint32_t)turn[turn_degree((int)gr.edge_head[x].y, (int)thb)];
           o.d = g_d(lx) + ct.x;
           o.k = o.d + o.c;
           o.t = (bt >= 0 ? g_t(lx) + tpt : 0u);
@@ -511,7 +519,7 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
           if (sx < 0 || L.lab[sx] == kGInf) continue;
           const unsigned long long lp = L.lab[sx];
           EOffer o;
-          o.c = g_c(lp) + (uint32_t)turn[turn_degree((int)L.hend[sx], (int)hb)];
+          o.c = g_c(lp) + (uint32_t)turn[turn_degree((int)gr.edge_head[p].y, (int)hb)];
           o.d = g_d(lp) + len;
           o.k = o.d + o.c;
           o.t = g_t(lp) + tt;

@@ -974,7 +974,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // outgrows it (flag 3) goes on below; slot 9 (bank 1): the edge-state tiers
     if (timing) (void)hipEventRecord(ev[24 + 2 * 9], stream);
     if (turns) {
-      out->route_tier_code[9] = 700000 + 384;
+      out->route_tier_code[9] = 7000000 + OTR_ECAP * 100 + (k32 ? 32 : 64);
       for (int et = 0; et < 2; ++et) {
         unsigned long long* c = cnt + 25 + et;
         k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, et == 0 ? 0x20u : 0x40u,
@@ -983,8 +983,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         rb.task_list = list;
         rb.list_count = c;
         unsigned long long* rcn = rwork ? d_counters + 1 * bank : nullptr;
-        if (et == 0) k_route_edge<384><<<4096, 64, 0, stream>>>(g, rb, rcn);
-        else k_route_edge<2048><<<512, 64, 0, stream>>>(g, rb, rcn);
+        // (the persistent grids hold every resident wave: ~19 per CU at 384 states)
+        if (et == 0 && k32) k_route_edge<OTR_ECAP, 32><<<8192, 64, 0, stream>>>(g, rb, rcn);
+        else if (et == 0) k_route_edge<OTR_ECAP, 64><<<8192, 64, 0, stream>>>(g, rb, rcn);
+        else k_route_edge<2048, 64><<<512, 64, 0, stream>>>(g, rb, rcn);
       }
     }
     if (timing) (void)hipEventRecord(ev[24 + 2 * 9 + 1], stream);

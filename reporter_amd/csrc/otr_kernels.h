@@ -28,6 +28,10 @@
 #ifndef OTR_LOAD1
 #define OTR_LOAD1 7
 #endif
+// the edge-state search's first table (states per search; turn-cost modes)
+#ifndef OTR_ECAP
+#define OTR_ECAP 384
+#endif
 
 namespace otr {
 
@@ -1332,7 +1336,11 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   if (have && !ok && !forced && lane == 0) {
     const uint32_t meta = a.rec[3 * task + 1].y;
     const bool general = ((meta >> 16) & 1u) != 0u, turn = ((meta >> 17) & 1u) != 0u;
+#ifdef OTR_FORCE_GENERAL
+    a.overflow_flag[task] = 3;  // test build: every search (edge-state ones too) in k_general
+#else
     a.overflow_flag[task] = turn ? 5 : (general ? 3 : ((G == 2 && !LIST && bmm > 1900000u) ? 2 : 1));
+#endif
   }
 #ifdef OTR_STAMPS
   if (G == 2 && counters && threadIdx.x == 0) {  // task setup and transition rows, wave cycles
@@ -1729,7 +1737,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
     K.sh = pack_shift(bt);
     if (ej == ei && pj >= pi) {
       if (gl == 0) a.path_len[s] = -1;
-    } else if ((a.turn_modes >> mode) & 1u) {
+    } else if (((a.turn_modes >> mode) & 1u)
+#ifdef OTR_FORCE_GENERAL
+               && false  // test build: every winner path in k_general
+#endif
+    ) {
       if (gl == 0) a.overflow_flag[k] = 5;  // turn costs: the edge-state search (otr_edge.h)
     } else if (!pack_fits(bmm, K.sh)
 #ifdef OTR_FORCE_GENERAL
