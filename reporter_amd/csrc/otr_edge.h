@@ -30,12 +30,14 @@ namespace otr {
 // more waves fit the LDS (the search waits on memory, not issue).
 template <int CAP, int TG = OTR_WAVE>
 struct EdgeLds {
-  static constexpr int WCAP = CAP <= 512 ? 64 : 128;
+  static constexpr int WCAP = CAP <= 512 ? 32 : 128;
   unsigned long long lab[CAP];   // gpack label, kGInf: none
   uint32_t key[CAP];             // edge id | kInq | kRel, kEmpty
   uint32_t node[CAP];            // dst(edge): where the state stands
-  uint16_t mi[CAP];              // mi_of(len(edge)): the IN criterion's gap of the state
   uint16_t pend[CAP];            // pending slots
+  uint8_t mi[CAP];               // mi8_of(len(edge)): the IN criterion's gap of the state
+  int32_t turn[181];             // the task's mode's turn cost table (mm), loaded per mode
+  int turn_md;                   // the mode whose table is loaded (-1: none)
   uint16_t wslot[WCAP];          // this round's settled states' slots
   unsigned long long wlab[WCAP];  // ... and their labels
   // targets (lanes of the wave): the best offer, entry parts, begin heading of ej
@@ -80,6 +82,23 @@ __device__ inline int e_insert(EdgeLds<CAP, TG>& L, uint32_t e, bool* isnew) {
   return -1;
 }
 
+// a state's IN-criterion gap in 256-mm units rounded down (a lower bound of its edge's
+// length, saturating at 65 m), 1 mm when below one unit
+__device__ inline uint8_t mi8_of(uint32_t len) { return (uint8_t)((len >> 8) < 255u ? (len >> 8) : 255u); }
+__device__ inline uint32_t in_gap8(uint8_t mq) { return mq ? (uint32_t)mq << 8 : 1u; }
+
+// the mode's turn table into LDS (one global read per task whose mode differs from the
+// last one's): every relaxation's turn cost is then an LDS read, not a dependent global load
+template <int CAP, int TG>
+__device__ inline void e_turn_table(EdgeLds<CAP, TG>& L, const int32_t* turn_tab, int md) {
+  if (L.turn_md != md) {  // (uniform: the whole wave runs one task)
+    __syncthreads();
+    for (int k = threadIdx.x; k < 181; k += OTR_WAVE) L.turn[k] = turn_tab[181 * md + k];
+    if (threadIdx.x == 0) L.turn_md = md;
+    __syncthreads();
+  }
+}
+
 template <int TG>
 __device__ inline uint32_t tmap_home(uint32_t v) {  // TG slots (a power of two)
   return (v * 0x9E3779B1u) >> (32 - __builtin_ctz((unsigned)TG));
@@ -119,13 +138,13 @@ __device__ inline EOffer e_step(unsigned long long lb, uint32_t tc, uint32_t len
 // length len, time tt, begin / end headings hb / he, access in dw's high bits).  Returns
 // the slot when b became newly pending.
 template <int CAP, int TG>
-__device__ inline int e_relax(EdgeLds<CAP, TG>& L, const int32_t* turn, unsigned long long lb, uint32_t ha, uint32_t dw,
+__device__ inline int e_relax(EdgeLds<CAP, TG>& L, unsigned long long lb, uint32_t ha, uint32_t dw,
                               uint32_t len, uint32_t tt, uint32_t b, uint32_t hb, uint32_t pd, uint32_t pt,
                               uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext, uint32_t& dnext, bool& isnew) {
   isnew = false;
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
-  const uint32_t tc = (uint32_t)turn[turn_degree((int)ha, (int)hb)];
+  const uint32_t tc = (uint32_t)L.turn[turn_degree((int)ha, (int)hb)];
   const EOffer o = e_step(lb, tc, len, tt);
   if (!e_feasible(o, pd, pt)) return -1;  // pruned (label-setting semantics)
   const uint32_t w = dw & kAdjDstMask;
@@ -133,7 +152,7 @@ __device__ inline int e_relax(EdgeLds<CAP, TG>& L, const int32_t* turn, unsigned
   if (sl < 0) return -1;
   if (isnew) {
     L.node[sl] = w;
-    L.mi[sl] = mi_of(len);
+    L.mi[sl] = mi8_of(len);
   }
   const unsigned long long nw = gpack(o.k, o.c, o.t);
   const unsigned long long old = atomicMin(&L.lab[sl], nw);
@@ -149,13 +168,13 @@ __device__ inline int e_relax(EdgeLds<CAP, TG>& L, const int32_t* turn, unsigned
 // The settled (final) state's offers to the targets at its node v (the turn into ej + the
 // entry part), kept as each target's lexicographic minimum.
 template <int CAP, int TG>
-__device__ inline void e_target_offers(EdgeLds<CAP, TG>& L, const int32_t* turn, unsigned long long lb, uint32_t ha,
+__device__ inline void e_target_offers(EdgeLds<CAP, TG>& L, unsigned long long lb, uint32_t ha,
                                        uint32_t v, uint32_t pd, uint32_t pt) {
   unsigned long long m = tmap_get(L, v);
   while (m) {
     const int q = __ffsll((long long)m) - 1;
     m &= m - 1;
-    const uint32_t tc = (uint32_t)turn[turn_degree((int)ha, (int)L.thb[q])];
+    const uint32_t tc = (uint32_t)L.turn[turn_degree((int)ha, (int)L.thb[q])];
     const EOffer o = e_step(lb, tc, L.tpart[q], L.tpt[q]);
     if (e_feasible(o, pd, pt)) atomicMin(&L.tlab[q], gpack(o.k, o.c, o.t));
   }
@@ -185,7 +204,7 @@ __device__ inline void e_init(EdgeLds<CAP, TG>& L) {
 // heading thb.  pd / pt: the relative bounds.  Returns false on overflow.  timed = false:
 // route times are not tracked (pt unused).
 template <int CAP, int TG>
-__device__ bool edge_search(EdgeLds<CAP, TG>& L, const DevGraph& g, const int32_t* turn, int md, bool active,
+__device__ bool edge_search(EdgeLds<CAP, TG>& L, const DevGraph& g, int md, bool active,
                             uint32_t root, uint32_t rnode, uint32_t pd, uint32_t pt, bool timed,
                             int n_tgt, uint32_t tv, uint32_t tpart, uint32_t tpt, uint32_t thb,
                             unsigned long long* settled, unsigned long long* relaxed) {
@@ -253,7 +272,7 @@ __device__ bool edge_search(EdgeLds<CAP, TG>& L, const DevGraph& g, const int32_
         key = L.key[sl];
         kk = g_k(lb);
         dd = g_d(lb);
-        take = (uint64_t)kk < (uint64_t)kmin + in_gap(L.mi[sl]);  // final (IN criterion)
+        take = (uint64_t)kk < (uint64_t)kmin + in_gap8(L.mi[sl]);  // final (IN criterion)
       }
       take = take && nw + prefix_count(__ballot(take)) < WCAP;
       const unsigned long long mt = __ballot(take), mk = __ballot(in && !take);
@@ -290,8 +309,8 @@ __device__ bool edge_search(EdgeLds<CAP, TG>& L, const DevGraph& g, const int32_
         const uint32_t tq = adjt[4 * (size_t)v + slot];
         const uint2 xe = g.adj_e[4 * (size_t)v + slot];
         const uint4 r = ld16(g.adj + 4 * (size_t)v + slot);
-        if (slot == 0) e_target_offers(L, turn, lb, ha, v, pd, pt);
-        psl = e_relax(L, turn, lb, ha, r.x & ~kAdjMore, r.y, timed ? tq : 0u, xe.x, xe.y & 0xFFFFu, pd, pt, mode_bit,
+        if (slot == 0) e_target_offers(L, lb, ha, v, pd, pt);
+        psl = e_relax(L, lb, ha, r.x & ~kAdjMore, r.y, timed ? tq : 0u, xe.x, xe.y & 0xFFFFu, pd, pt, mode_bit,
                       my_relaxed, knext, dnext, isnew);
         tail = tail || (slot == 3 && (r.x & kAdjMore));
       }
@@ -319,7 +338,7 @@ __device__ bool edge_search(EdgeLds<CAP, TG>& L, const DevGraph& g, const int32_
               const uint4 pk = ld16(g.edge_pack + e);
               const short2 hh = g.edge_head[e];
               bool isnew;
-              const int psl = e_relax(L, turn, lb, ha, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e,
+              const int psl = e_relax(L, lb, ha, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e,
                                       (uint32_t)hh.x, pd, pt, mode_bit, my_relaxed, knext, dnext, isnew);
               if (isnew) atomicAdd(&L.n_keys, 1);
               if (psl >= 0) {
@@ -357,6 +376,7 @@ __device__ bool edge_search(EdgeLds<CAP, TG>& L, const DevGraph& g, const int32_
 template <int CAP, int TG>
 __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, unsigned long long* counters) {
   __shared__ EdgeLds<CAP, TG> L;
+  if (threadIdx.x == 0) L.turn_md = -1;
   const int64_t n_tasks = (int64_t)*a.list_count;
   const int lane = (int)threadIdx.x;
   for (int64_t w = blockIdx.x; w < n_tasks; w += gridDim.x) {
@@ -395,8 +415,9 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
     const uint32_t pd = bmm >= d0 ? bmm - d0 : 0u;
     const uint32_t pt = bt >= 0 && t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
     e_init(L);
+    e_turn_table(L, a.turn, md);
     unsigned long long settled = 0, relaxed = 0;
-    const bool ok = edge_search<CAP, TG>(L, gr, a.turn + 181 * md, md, search, ei, gr.edge_dst[ei], pd, pt, bt >= 0,
+    const bool ok = edge_search<CAP, TG>(L, gr, md, search, ei, gr.edge_dst[ei], pd, pt, bt >= 0,
                                          Kb, tv, tpart, tpt, thb, counters ? &settled : nullptr,
                                          counters ? &relaxed : nullptr) &&
                     Kb <= TG;
@@ -454,6 +475,7 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
                                                    int32_t overflow_flag) {
   __shared__ EdgeLds<CAP, 32> L;
   __shared__ uint32_t s_rev[CAP];
+  if (threadIdx.x == 0) L.turn_md = -1;
   const int64_t n_list = (int64_t)*list_count;
   const int lane = (int)threadIdx.x;
   for (int64_t w = blockIdx.x; w < n_list; w += gridDim.x) {
@@ -473,7 +495,8 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
     const uint32_t pt = bt >= 0 && t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
     const uint32_t thb = (uint32_t)gr.edge_head[ej].x;
     e_init(L);
-    const bool ok = edge_search<CAP, 32>(L, gr, turn, md, true, ei, gr.edge_dst[ei], pd, pt, bt >= 0, 1, ct.y, ct.x,
+    e_turn_table(L, turn_tab, md);
+    const bool ok = edge_search<CAP, 32>(L, gr, md, true, ei, gr.edge_dst[ei], pd, pt, bt >= 0, 1, ct.y, ct.x,
                                          tpt, thb, nullptr, nullptr);
     const unsigned long long tl = L.tlab[0];
     int n = -1;
