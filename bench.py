@@ -129,8 +129,8 @@ def main():
                          '(60%% auto / 25%% bicycle / 15%% pedestrian) on the metro graph; c5: the country graph '
                          '(50M nodes), this GPU\'s N = 8 share (125,000) of 1M vehicles over 24 h, C5 mode mix')
     ap.add_argument('--e2e-steps', type=int, default=3, help='host-to-host drop-in steps (0 = skip)')
-    ap.add_argument('--e2e-streams', type=int, default=1,
-                    help='host threads (matchers, HIP streams, trace slices) of the host-to-host measurement')
+    ap.add_argument('--e2e-streams', type=int, default=2,
+                    help='worker threads (matchers, HIP streams, pinned batches) of the host-to-host measurement')
     ap.add_argument('--opt', action='append', default=[],
                     help='A/B only (not the headline config): KEY=VALUE match option override, e.g. '
                          'max_route_time_factor=0')
@@ -422,7 +422,8 @@ def main():
                                                        (max(d['ms'], 1e-9) / d['launches'] * 1e-3) / 1e9, 1)}
                   for t, d in sorted(tiers.items())}
     traffic, traffic_src = None, None
-    if os.path.exists(PMC_SUMMARY):
+    # (the PMC summary is of the default C2 command: other workloads report no traffic)
+    if os.path.exists(PMC_SUMMARY) and args.workload == 'c2' and args.streams == 1:
         k = json.load(open(PMC_SUMMARY)).get('kernels', {}).get(kernel_name(dom['code'], turns, dom_t == 0), {})
         if 'fetch_bytes_per_launch' in k and 'write_bytes_per_launch' in k:
             traffic = int(k['fetch_bytes_per_launch'] + k['write_bytes_per_launch'])
@@ -459,76 +460,66 @@ def main():
                   'floats_bitexact': all(v for k, v in stats.items() if k.endswith('_bitexact'))}
 
     # ---- rank 0, N = 1: the drop-in path host → host (PCIe included; never `value`).
-    # Keyed mode runs the batch as E host threads, each with its own matcher (own HIP
-    # stream) and a slice of the traces in pinned memory: while one thread's kernels run,
-    # another's H2D inputs and D2H reports/entries move (the copies use the DMA engines),
-    # as the reference's service threads each hold a matcher (reporter_service.py:51-52).
-    # Each slice's tile rows are reduced on its stream (privacy 1); the owner merge + pair
-    # cull over all slices then gives the single-batch entries (otr_hist_reduce is a sum
-    # per key: tests/test_gpu_hist_keyed.py::test_entries_merge_equals_oracle).
+    # E host threads (--e2e-streams), each a worker of the service with its own matcher (own
+    # HIP stream, reporter_service.py:51-52: one matcher per thread) and its own pinned copy
+    # of the batch, each running the full batch --e2e-steps times back to back: while one
+    # worker's kernels run, another's H2D inputs and D2H reports/entries move on the DMA
+    # engines.  Rate = E x steps x probes / wall time.
     e2e = None
     if rank == 0 and world == 1 and args.e2e_steps > 0:
         from concurrent.futures import ThreadPoolExecutor as _TPE
-        ne = max(1, args.e2e_streams) if keyed else 1
-        ecuts = np.linspace(0, mine.n_traces, ne + 1).astype(np.int64)
-        eparts = [mine.subset(np.arange(ecuts[k], ecuts[k + 1])) for k in range(ne)]
+        ne = max(1, args.e2e_streams)
         ematchers = [matchers[k] if k < len(matchers) else M.Matcher() for k in range(ne)]
         harrs, pins = [], []
-        for part in eparts:
+        for k in range(ne):
             pin = {}
-            for name, arr in (('offsets', part.offsets), ('lat', part.lat), ('lon', part.lon), ('time', part.time),
-                              ('mode', part.mode)):
+            for name, arr in (('offsets', mine.offsets), ('lat', mine.lat), ('lon', mine.lon), ('time', mine.time),
+                              ('mode', mine.mode)):
                 pin[name] = torch.from_numpy(np.ascontiguousarray(arr)).pin_memory()
-            if part.accuracy is not None:
-                pin['accuracy'] = torch.from_numpy(np.ascontiguousarray(part.accuracy, np.float32)).pin_memory()
+            if mine.accuracy is not None:
+                pin['accuracy'] = torch.from_numpy(np.ascontiguousarray(mine.accuracy, np.float32)).pin_memory()
             pins.append(pin)
             harrs.append({'trace_offsets': pin['offsets'].data_ptr(), 'lat': pin['lat'].data_ptr(),
                           'lon': pin['lon'].data_ptr(), 'time': pin['time'].data_ptr(),
                           'mode': pin['mode'].data_ptr(),
                           'accuracy': pin['accuracy'].data_ptr() if 'accuracy' in pin else None})
-        hist_host = torch.zeros(hist_len, dtype=torch.int32).pin_memory() if not keyed else None
+        hist_hosts = [torch.zeros(hist_len, dtype=torch.int32).pin_memory() for _ in range(ne)] if not keyed else None
+        ehists = ([hists[0]] + [torch.zeros_like(hists[0]) for _ in range(ne - 1)]) if not keyed else None
+        e2e_out = [None] * ne
 
-        def e2e_part(k):
+        def e2e_one(k):
             m = ematchers[k]
             if not keyed:
-                r = m.match_batch(eparts[k], host_arrays=harrs[k], hist_device=hists[0].data_ptr(), hist_hours=hours,
+                r = m.match_batch(mine, host_arrays=harrs[k], hist_device=ehists[k].data_ptr(), hist_hours=hours,
                                   hist_base_time=T_BEGIN, copy_out=False, copy_reports=True)
-                hist_host.copy_(hists[0], non_blocking=False)
-                return r, None
-            # keyed: the slice's tile rows reduced in HBM, its entries to the host
-            r = m.match_batch(eparts[k], host_arrays=harrs[k], copy_out=False, copy_reports=True, tile_rows=True)
-            ent = sr.hist_reduce(m, r.d_rows, r.n_rows, privacy=1 if ne > 1 else args.privacy, rows_in=True)
-            return r, ent
+                hist_hosts[k].copy_(ehists[k], non_blocking=False)
+                e2e_out[k] = (int(r.n_rep), None)
+                return
+            # keyed: the tile rows reduced and culled in HBM, the owned entries to the host
+            r = m.match_batch(mine, host_arrays=harrs[k], copy_out=False, copy_reports=True, tile_rows=True)
+            ent = sr.hist_reduce(m, r.d_rows, r.n_rows, privacy=args.privacy, rows_in=True)
+            e2e_out[k] = (int(r.n_rep), len(ent))
+
+        def e2e_worker(k, steps):
+            for _ in range(steps):
+                e2e_one(k)
 
         epool = _TPE(max_workers=ne)
-
-        def e2e_step():
-            outs = list(epool.map(e2e_part, range(ne)))
-            if keyed and ne > 1:  # the owner merge and the pair cull over every slice's entries
-                allent = np.concatenate([o[1] for o in outs])
-                e2e_hist['entries'] = sr.hist_reduce(ematchers[0], allent, len(allent), privacy=args.privacy,
-                                                     memory='host')
-            elif keyed:
-                e2e_hist['entries'] = outs[0][1]
-            return sum(int(o[0].n_rep) for o in outs)
-
-        e2e_hist = {}
-        e2e_step()
+        list(epool.map(e2e_worker, range(ne), [1] * ne))  # warm every worker
         torch.cuda.synchronize()
         te0 = time.perf_counter()
-        for _ in range(args.e2e_steps):
-            nrep = e2e_step()
+        list(epool.map(e2e_worker, range(ne), [args.e2e_steps] * ne))
         torch.cuda.synchronize()
         tel = time.perf_counter() - te0
         epool.shutdown()
-        e2e = {'value': round(mine.n_probes * args.e2e_steps / tel, 1), 'unit': 'probes/s',
-               'ms_per_step': round(1e3 * tel / args.e2e_steps, 3), 'streams': ne, 'reports': nrep,
-               'owned_entries': int(len(e2e_hist['entries'])) if keyed else None,
+        e2e = {'value': round(ne * mine.n_probes * args.e2e_steps / tel, 1), 'unit': 'probes/s',
+               'ms_per_step': round(1e3 * tel / (ne * args.e2e_steps), 3), 'streams': ne, 'reports': e2e_out[0][0],
+               'owned_entries': e2e_out[0][1],
                'what': 'SoA input in pinned host memory -> H2D -> match -> reports (dense, host) and the ' +
                        ('keyed (hour-tile, pair, speed) histogram entries after the privacy cull'
                         if keyed else '[hour][segment][speed] histogram') + ' (host); SURVEY 8(d) drop-in definition' +
-                       ('; %d host threads, one matcher / HIP stream / trace slice each, copies overlapping '
-                        'the other slices\' kernels' % ne if ne > 1 else '')}
+                       ("; %d worker threads, one matcher / HIP stream / pinned batch each, one batch's copies "
+                        "overlapping another's kernels" % ne if ne > 1 else '')}
 
     if rank == 0:
         line = {

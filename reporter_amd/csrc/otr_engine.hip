@@ -809,11 +809,29 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ra.rec = task_rec;
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
   ra.overflow_flag = task_ovf;
-  // bounds > 1.9 km skip the first tier (most outgrow 160 slots: C4 route 24 -> 15 ms);
-  // 1.5 km: C4 6.99M -> 7.21M probes/s but C2 -1.6 % (its 1.5-1.9 km steps then retry)
-  static const uint32_t direct_bmm =
-      getenv("OTR_DIRECT_BMM") ? (uint32_t)strtoul(getenv("OTR_DIRECT_BMM"), nullptr, 10) : 1900000u;  // A/B knob
-  ra.direct_bmm = direct_bmm;
+  // the first tier's size estimate (k_route route_unit): an exact search runs to its
+  // bounds unless its targets resolve first, so its keys grow with the area it can reach,
+  // est = c * density * reach^2, reach = min(length bound, time bound x 50 km/h capped by
+  // the mode's speed).  A search whose estimate exceeds the first tier's table starts in the
+  // retry tier that holds it.  c = 0.5 (C4's 60 s steps reach ~1.7 km and start in the
+  // 1024-slot tier: C4 1.69M -> 2.47M probes/s; c = 1.7, the full-exhaustion fit of C2,
+  // sent them to the 4096 tier, 1.07M; C2's 15 s steps stay in the first tier either way,
+  // profiles/r03_est_*).  OTR_EST_K scales c (A/B knob; 0 = every search starts in the
+  // first tier).
+  {
+    static const double est_scale = getenv("OTR_EST_K") ? atof(getenv("OTR_EST_K")) : 1.0;
+    const double mlat = g.grid_min_lat + 0.5 * g.grid_rows * g.grid_cell_deg;
+    const double area = (g.grid_rows * g.grid_cell_deg * kMetersPerDeg) *
+                        (g.grid_cols * g.grid_cell_deg * kMetersPerDeg * cos_deg(fmin(fabs(mlat), 89.0)));
+    ra.est_k = (float)(est_scale * 0.5 * (area > 0.0 ? (double)g.n_nodes / area : 0.0));
+    for (int m = 0; m < OTR_MODES; ++m) {
+      const double kph = mp.m[m].speed_kph > 0.0 && mp.m[m].speed_kph < 50.0 ? mp.m[m].speed_kph : 50.0;
+      ra.est_v[m] = (float)(kph / 3.6);
+    }
+    static const std::vector<int> tl = route_tiers();
+    ra.n_tiers = (int)std::min<size_t>(tl.size(), 8);
+    for (int t = 0; t < ra.n_tiers; ++t) ra.tier_keys[t] = (uint32_t)((tl[t] / 10) * 7 / 8);
+  }
   // device-side counters of the retry lists: [0..7] route tiers, [8] general tier 1,
   // [9] general tier 2, [10] route tasks left unrouted, [11] steps, [12..15] path tiers,
   // [16] path general 1, [17] path general 2, [18] paths left, [19] general overflow
@@ -918,8 +936,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     te(OTR_STAGE_ROUTE);
     // overflow retries with larger LDS tables (same results, fewer resident waves): each
     // tier takes its list on the device and runs a fixed grid over it — no host round
-    // trip between tiers.  First-tier overflows flagged 2 (long bounds)
-    // skip the 256-slot tier; OTR_TIERS (A/B knob) lists the retry kernels.
+    // trip between tiers.  Tier t takes the previous tier's overflows (flag 1) and the
+    // first-tier tasks whose size estimate starts them in a tier <= t (flags 16 + u, u <= t);
+    // OTR_TIERS (A/B knob) lists the retry kernels.
     tb(OTR_STAGE_ROUTE_BIG);
     static const std::vector<int> tiers = route_tiers();
     const int ntier = (int)tiers.size();
@@ -931,8 +950,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     constexpr unsigned kCollectGrid = 512;
     for (int tier = 0; tier < ntier; ++tier) {
       unsigned long long* c = cnt + tier;
-      k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, tier == 0 ? 0x2u : 0x6u,
-                                                            list + 0, c);
+      k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf,
+                                                            0x2u | (((2u << tier) - 1u) << 16), list + 0, c);
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.list_count = c;

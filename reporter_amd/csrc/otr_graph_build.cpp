@@ -12,8 +12,9 @@
 // level in the order Python 2 iterates {2:.., 1:.., 0:..} — levels 0, 1, 2.
 //
 // Flattener: edges shorter than 5 cm are contracted (their end nodes merged into the
-// smallest node id of the cluster), because the A* finality margin of the route search
-// holds only for edges >= 5 cm; edges whose ends merged vanish, the
+// smallest node id of the cluster): the route search's exact rounds settle a node once
+// its label is below the smallest pending length + its shortest in-edge,
+// so millimetre edges would only make the rounds narrow; edges whose ends merged vanish, the
 // others keep their shapes with the end points moved onto the surviving nodes, and a
 // vanished edge's segment-begin / segment-end flag moves to the neighbouring edge of
 // the same OSMLR segment.  Lengths are the shapes' equirectangular lengths (metres per

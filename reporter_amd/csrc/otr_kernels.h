@@ -1043,7 +1043,13 @@ struct RouteArgs {
   double inv_beta[OTR_MODES];
   int32_t* overflow_flag;     // per task: 1/2 retry in a larger LDS table, 3 the global-memory search,
                               // 5 / 6 the edge-state tiers
-  uint32_t direct_bmm;        // first tier: bounds above this go straight to the retry tiers
+  // first tier: a search whose expected size (keys) exceeds its table starts in the first
+  // retry tier that holds it (flag 16 + tier): expected keys = est_k * r^2 with r = the
+  // step's reach, min(length bound, time bound x est_v[mode])
+  float est_k;                // keys per m^2 of reach (calibrated on the graph's node density)
+  float est_v[OTR_MODES];     // m/s: the mode's typical speed (50 km/h, capped by the mode's)
+  uint32_t tier_keys[8];      // key capacity of each retry tier, in order
+  int n_tiers;
 };
 
 // k_tasks' inputs and outputs
@@ -1162,6 +1168,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   OTR_STAMP(ts_in);
   // ---- search inputs (only these stay live through the search)
   bool search, fits, forced;
+  int start_tier = -1;  // >= 0: the retry tier this (first-tier) task starts in
   uint32_t tnode = kEmpty, tpart = 0, gapT = 1, d0min = 0xFFFFFFFFu, root = 0, bmm = 0, mode_bit = 1;
   uint32_t pd = 0, pt = 0xFFFFFFFFu;  // pruning bounds relative to the root (length, time)
   int Kb;
@@ -1186,7 +1193,18 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     // targets are lanes of the group (wider steps go to a G = 1 tier); 32-bit tables leave
     // the tasks whose packed words need 64 bits to the WIDE tier
     fits = Kb <= Gr::GL && (WIDE || !general) && !((r1.y >> 17) & 1u);
-    if (G == 2 && !LIST && r0.w > a.direct_bmm) fits = false;
+    if (G == 2 && !LIST && have) {  // a search too big for this table starts in a retry tier
+      const int md = (int)((r1.y >> 8) & 3u);
+      float reach = (float)r0.w * 1e-3f;
+      if ((int32_t)r2.y >= 0) reach = fminf(reach, (float)r2.y * 0.1f * a.est_v[md]);
+      const float est = a.est_k * reach * reach;
+      constexpr int kFirstKeys = (CAP * OTR_LOAD1) / 8;
+      if (est > (float)kFirstKeys) {
+        start_tier = 0;
+        while (start_tier + 1 < a.n_tiers && (float)a.tier_keys[start_tier] < est) ++start_tier;
+        fits = false;
+      }
+    }
     mode_bit = 1u << ((r1.y >> 8) & 3u);
     bmm = r0.w;
     root = r0.z;
@@ -1330,16 +1348,16 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
       }
     }
   }
-  // general (flag 3): the global-memory search; overflow: retry with a bigger table; a
-  // first-tier search with a long bound (> 1.9 km) that outgrew 160 slots goes straight to
-  // the 1024-slot tier (flag 2); turn modes (flag 5): the edge-state LDS search (otr_edge.h)
+  // general (flag 3): the global-memory search; overflow: retry with a bigger table (1); a
+  // first-tier search expected beyond its table starts in retry tier t (16 + t); turn modes
+  // (flag 5): the edge-state LDS search (otr_edge.h)
   if (have && !ok && !forced && lane == 0) {
     const uint32_t meta = a.rec[3 * task + 1].y;
     const bool general = ((meta >> 16) & 1u) != 0u, turn = ((meta >> 17) & 1u) != 0u;
 #ifdef OTR_FORCE_GENERAL
     a.overflow_flag[task] = 3;  // test build: every search (edge-state ones too) in k_general
 #else
-    a.overflow_flag[task] = turn ? 5 : (general ? 3 : ((G == 2 && !LIST && bmm > 1900000u) ? 2 : 1));
+    a.overflow_flag[task] = turn ? 5 : (general ? 3 : (start_tier >= 0 ? 16 + start_tier : 1));
 #endif
   }
 #ifdef OTR_STAMPS
