@@ -567,11 +567,16 @@ constexpr uint32_t kNoRoute = 0xFFFFFFFFu;  // transition array: no valid route 
 __device__ inline int64_t bound_mm_of(double bound) { return (int64_t)floor(bound * 1000.0); }
 __device__ inline int64_t part_mm(double frac, uint32_t len_mm) { return (int64_t)llround(frac * (double)len_mm); }
 
-// home slot: Fibonacci hashing (the ids of one search are spatially clustered, nearly
-// consecutive) scaled to CAP by a high multiply, so CAP need not be a power of two
+// home slot: multiplicative hashing of the id's low 24 bits (the ids of one search are
+// spatially clustered, nearly consecutive): bits 8..23 of id x 0x9E3779 step by 0.618 of
+// their range per consecutive id (Fibonacci spreading), scaled to CAP by a multiply, so
+// CAP need not be a power of two.  24-bit multiplies are full-rate VALU ops (32-bit ones
+// take four passes), and every relaxation hashes its head.
 template <int CAP>
 __device__ inline uint32_t hslot(uint32_t node) {
-  return __umulhi(node * 0x9E3779B1u, (uint32_t)CAP);
+  static_assert(CAP < (1 << 16), "table size fits the 16-bit scale");
+  const uint32_t h = (__umul24(node & 0xFFFFFFu, 0x9E3779u) >> 8) & 0xFFFFu;
+  return __umul24(h, (uint32_t)CAP) >> 16;  // h * CAP / 2^16 < CAP
 }
 
 template <int CAP, int LM>
