@@ -10,6 +10,7 @@ timeout -k 10 600 python3 -u -m pytest tests -m gpu -q --timeout 900 --timeout-m
 echo tests $?; tail -2 $O/pytest_gpu.log
 timeout -k 10 300 python3 -u bench.py > $O/c2.json 2> $O/c2.err || exit 1
 echo c2 done
+timeout -k 10 300 python3 -u bench.py --streams 2 --cpu-traces 0 --e2e-steps 0 > $O/c2_s2.json 2> $O/c2_s2.err; echo c2s2 $?
 timeout -k 10 300 python3 -u bench.py --workload c2dep --e2e-steps 0 > $O/c2dep.json 2> $O/c2dep.err; echo c2dep $?
 timeout -k 10 300 python3 -u bench.py --workload c4 --e2e-steps 0 > $O/c4.json 2> $O/c4.err; echo c4 $?
 timeout -k 10 200 python3 -u bench.py --workload c5mix --e2e-steps 0 > $O/c5mix.json 2> $O/c5mix.err; echo c5mix $?
