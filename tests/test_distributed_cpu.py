@@ -4,7 +4,6 @@ here), builds the [hour][segment][speed] histogram, and the cross-rank combine
 (all-reduce-sum then owner slice, the gloo analogue of the RCCL reduce-scatter in
 bench.py) equals the single-process histogram of the whole set."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -15,12 +14,9 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(('127.0.0.1', 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _store(tmp_path):
+    # a FileStore rendezvous: a probed-then-released TCP port can be taken by a parallel test
+    return 'file://' + str(tmp_path / 'rdzv')
 
 
 def _workload(graph_dir):
@@ -42,11 +38,10 @@ def _hist_for(path, tr):
     return histogram(r, first, last, idx, len(G.seg_id), __import__('reporter_amd.tools.gen').tools.gen.T_BEGIN, 2)
 
 
-def _rank(rank, world, port, graph_dir, out):
+def _rank(rank, world, store, graph_dir, out):
     import sys
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    dist.init_process_group('gloo', init_method=store, rank=rank, world_size=world)
     from reporter_amd import simple_reporter as sr
     path, tr = _workload(graph_dir)
     mine = np.array([i for i, u in enumerate(tr.uuids) if sr.shard_of(u, world) == rank])
@@ -70,7 +65,7 @@ def _rank(rank, world, port, graph_dir, out):
 def test_two_rank_shard_and_combine(tmp_path, graph_dir):
     world = 2
     out = str(tmp_path / 'hist.npy')
-    mp.spawn(_rank, args=(world, _free_port(), graph_dir, out), nprocs=world, join=True)
+    mp.spawn(_rank, args=(world, _store(tmp_path), graph_dir, out), nprocs=world, join=True)
     path, tr = _workload(graph_dir)
     whole, rows = _hist_for(path, tr)
     combined = np.load(out)
@@ -91,11 +86,10 @@ def _entries_for(path, tr):
     return hist.reduce(hist.entries_from_rows(rows), 1), rows
 
 
-def _keyed_rank(rank, world, port, graph_dir, out, privacy):
+def _keyed_rank(rank, world, store, graph_dir, out, privacy):
     import sys
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    dist.init_process_group('gloo', init_method=store, rank=rank, world_size=world)
     from oracle import hist
     from reporter_amd import simple_reporter as sr
     path, tr = _workload(graph_dir)
@@ -131,7 +125,7 @@ def test_two_rank_keyed_histogram_exchange(tmp_path, graph_dir, privacy):
     from oracle import hist
     world = 2
     out = str(tmp_path / 'keyed.npy')
-    mp.spawn(_keyed_rank, args=(world, _free_port(), graph_dir, out, privacy), nprocs=world, join=True)
+    mp.spawn(_keyed_rank, args=(world, _store(tmp_path), graph_dir, out, privacy), nprocs=world, join=True)
     path, tr = _workload(graph_dir)
     _, rows = _entries_for(path, tr)
     whole = hist.reduce(hist.entries_from_rows(rows), privacy)

@@ -3,7 +3,6 @@ the product's bucketing mirror, the C-ABI line writer, and the 2-rank gloo excha
 that routes rows to their file's owner (simple_reporter.py:176-239)."""
 import json
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -72,19 +71,15 @@ def test_format_lines_match_oracle(graph_dir):
     assert tiles == want
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(('127.0.0.1', 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _store(tmp_path):
+    # a FileStore rendezvous: a probed-then-released TCP port can be taken by a parallel test
+    return 'file://' + str(tmp_path / 'rdzv')
 
 
-def _rank(rank, world, port, graph_dir, q):
+def _rank(rank, world, store, graph_dir, q):
     import sys
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    dist.init_process_group('gloo', init_method=store, rank=rank, world_size=world)
     from reporter_amd import simple_reporter as sr
     tr, res, first, last = _oracle_workload(graph_dir)
     # each rank holds the rows of its uuid shard (simple_reporter.py:116)
@@ -103,13 +98,13 @@ def _rank(rank, world, port, graph_dir, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_row_exchange(graph_dir):
+def test_two_rank_row_exchange(tmp_path, graph_dir):
     tr, res, first, last = _oracle_workload(graph_dir)
     want = ot.tiles(ot.rows_from_reports(res, first, last), 2)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = _free_port()
-    ps = [ctx.Process(target=_rank, args=(r, 2, port, graph_dir, q)) for r in range(2)]
+    store = _store(tmp_path)
+    ps = [ctx.Process(target=_rank, args=(r, 2, store, graph_dir, q)) for r in range(2)]
     for p in ps:
         p.start()
     outs = [q.get(timeout=300) for _ in ps]
