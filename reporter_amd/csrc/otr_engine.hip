@@ -1299,6 +1299,12 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   HIPCHK(hipMemcpyAsync(hc.data(), d_counters + 10 * bank, n_ctr * 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipMemcpyAsync(&h_fail[0], cnt + 10, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipMemcpyAsync(&h_fail[1], cnt + 18, 8, hipMemcpyDeviceToHost, stream));
+  // per-trace output counts in the same drain (one host wait per batch for all of them)
+  std::vector<int64_t> route_n(T), seg_n(T), way_n(T), rep_n(T);
+  HIPCHK(hipMemcpyAsync(route_n.data(), sa.route_n, 8 * T, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(seg_n.data(), sa.seg_n, 8 * T, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(rep_n.data(), sa.rep_n, 8 * T, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(way_n.data(), sa.way_n, 8 * T, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
   if (h_fail[0] + h_fail[1] > 0) {
     // beyond a 1M-state slab (never seen): name the traces (task/step -> state -> trace)
@@ -1353,11 +1359,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     (void)hipGetLastError();  // an unrecorded pair must not leave a sticky error for the next call
   }
   // ---- copy-out (tests / JSON path), compacting the capacity layout
-  std::vector<int64_t> route_n(T), seg_n(T), way_n(T), rep_n(T), h_cap_off(T + 1);
-  HIPCHK(hipMemcpy(route_n.data(), sa.route_n, 8 * T, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(seg_n.data(), sa.seg_n, 8 * T, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(rep_n.data(), sa.rep_n, 8 * T, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(way_n.data(), sa.way_n, 8 * T, hipMemcpyDeviceToHost));
   int64_t nroute = 0, nseg = 0, nrep = 0;
   for (int t = 0; t < T; ++t) {
     nroute += route_n[t];

@@ -3,12 +3,12 @@
 //   K0 k_select_states   thread/trace   interpolation_distance state selection
 //   K1 k_candidates      wave/state     grid-cell edge projection, LDS top-K
 //   K2 (emission)        fused into K5  sq_dist / (2 sigma_z^2)
-//   K_link               thread/trace   active-state chain, g, route bound
+//   K_link               wave/trace     active-state chain, g, route bound
 //   K3 k_route           wave/(step,src) bounded one-to-many search, LDS hash
 //   K4 (transition)      epilogue of K3 |route - g| / beta
-//   K5 k_viterbi         wave/trace     fp64 min-sum Viterbi + backtrack
-//   K6 k_paths           wave/step      winner path reconstruction
-//   K7 k_segments        thread/trace   route stitch, OSMLR segments, report()
+//   K5 k_viterbi         group/trace    fp64 min-sum Viterbi + backtrack (2 traces per wave)
+//   K6 k_paths           group/step     winner path reconstruction
+//   K7 k_segments        wave/trace     route stitch, OSMLR segments, report()
 //   K8 k_histogram       thread/trace   simple_reporter filter + hour buckets
 //
 // Every decision-path expression mirrors oracle/oracle.c operation for operation
