@@ -575,7 +575,11 @@ __device__ inline int64_t part_mm(double frac, uint32_t len_mm) { return (int64_
 template <int CAP>
 __device__ inline uint32_t hslot(uint32_t node) {
   static_assert(CAP < (1 << 16), "table size fits the 16-bit scale");
-  const uint32_t h = (__umul24(node & 0xFFFFFFu, 0x9E3779u) >> 8) & 0xFFFFu;
+  // v_mul_u32_u24 spelled out: only product bits 8..23 are used, which a 32-bit multiply
+  // gives as well, so the compiler otherwise picks the quarter-rate v_mul_lo_u32
+  uint32_t p;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(p) : "s"(0x9E3779u), "v"(node));
+  const uint32_t h = (p >> 8) & 0xFFFFu;
   return __umul24(h, (uint32_t)CAP) >> 16;  // h * CAP / 2^16 < CAP
 }
 
