@@ -1147,8 +1147,11 @@ __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
   a.rec[3 * o + 2] = make_uint4(0u, (uint32_t)bt, (uint32_t)to, (uint32_t)((uint64_t)to >> 32));
 }
 
+// waves per SIMD of the first tier (two searches per wave): 8 = 32 waves per CU, whose
+// 4.7 KB tables fill 150 of the CU's 160 KB of LDS; the search waits on LDS and L2 round
+// trips, so the eighth wave pays (20.2 ms against 21.5 at 7, profiles/r03_abw8_*)
 #ifndef OTR_ROUTE2_WAVES
-#define OTR_ROUTE2_WAVES 7
+#define OTR_ROUTE2_WAVES 8
 #endif
 
 // index of the q-th set bit of m (q < popcount(m))
