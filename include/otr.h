@@ -194,15 +194,16 @@ typedef struct otr_batch_result {
                                   trace by trace in report order */
   /* per route-search kernel: slot 0 the first tier (k_route<160,2>), 1..5 the LDS retry
    * tiers in order, 6 / 7 the global-memory search (32K / 1M-state slabs), 8 the 64-bit
-   * label LDS tier (steps whose length and time bits exceed 32), 9 the edge-state LDS
-   * tiers (modes with turn costs).  code: 7,000,000 + CAP*100 + targets of the edge-state
-   * tier, CAP*10+G
+   * label LDS tier (steps whose length and time bits exceed 32), 10 the first edge-state
+   * tier (modes with turn costs), 9 / 11 the larger edge-state tables (768, then 2048 states).
+   * code: 6,000,000 + CAP*100 + targets of the first edge-state tier, 7,000,000 + CAP*100 +
+   * targets of the larger ones, CAP*10+G
    * of an LDS tier, 900000 + CAP the 64-bit tier, -1 / -2 the global tiers, 0 unused.
    * work: searches, settled nodes (expanded states), relaxed edges, transition entries
    * written.  ms (OTR_BATCH_TIMING): HIP-event time of the kernel on the matcher's stream. */
-  int32_t route_tier_code[10];
-  float route_tier_ms[10];
-  uint64_t route_tier_work[10][4];
+  int32_t route_tier_code[12];
+  float route_tier_ms[12];
+  uint64_t route_tier_work[12][4];
 } otr_batch_result;
 
 int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result* out);

@@ -9,11 +9,13 @@ file, segment id, next id, speed bin): one entry per key with its number of
 observations.  The keyed exchange sends each entry to the rank owning its file
 (reporter_amd.simple_reporter.file_owner, the (hour, tile) partition of §8e); the owner
 sums the counts of equal keys it received and applies the privacy threshold to whole
-segment pairs: a (file, id, next_id) pair survives when its total count over all speed
-bins reaches `privacy` (simple_reporter.py:218-239 keeps runs of >= privacy identical
-(id, next_id) lines per file; the trailing-singleton quirk of that loop is a property of
-the line files and stays with oracle/tiles.sort_and_cull).  Checker for otr_hist_reduce
-(include/otr.h) and simple_reporter.exchange_hist.
+segment pairs exactly as the reference loop does on the file's lines
+(simple_reporter.py:218-239): a pair's run length is its total count over all speed bins
+(one line per tile row); the lines are sorted as strings, so the runs come in the string
+order of (id, next_id); every run is judged alone (kept iff >= privacy) except that a
+trailing run of one line is judged together with the run before it (both kept iff that
+run's length + 1 >= privacy).  Checker for otr_hist_reduce (include/otr.h)
+and simple_reporter.exchange_hist; oracle/tiles.sort_and_cull is the same rule on lines.
 """
 import math
 
@@ -81,8 +83,20 @@ def reduce(entries, privacy=1):
     pair_tot = {}
     for k in keys:
         pair_tot[k[:3]] = pair_tot.get(k[:3], 0) + acc[k]
+    keep = {p: t >= privacy for p, t in pair_tot.items()}
+    if privacy > 1:  # the reference loop's trailing run (simple_reporter.py:221-239)
+        files = {}
+        for f, i, nx in pair_tot:
+            files.setdefault(f, []).append((str(i) + ',', str(nx) + ',', i, nx))
+        for f, prs in files.items():
+            prs.sort()  # the string order of the lines' (id, next_id) prefix
+            if len(prs) >= 2 and pair_tot[(f, prs[-1][2], prs[-1][3])] == 1:
+                prev = (f, prs[-2][2], prs[-2][3])
+                k2 = pair_tot[prev] + 1 >= privacy
+                keep[prev] = k2
+                keep[(f, prs[-1][2], prs[-1][3])] = k2
     out = [(k[0], k[1], k[2], k[3], min(acc[k], 0xFFFFFFFF)) for k in keys
-           if privacy <= 1 or pair_tot[k[:3]] >= privacy]
+           if privacy <= 1 or keep[k[:3]]]
     return np.array(out, dtype=HIST_ENTRY) if out else np.zeros(0, HIST_ENTRY)
 
 

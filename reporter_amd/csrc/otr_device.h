@@ -56,11 +56,17 @@ __host__ __device__ inline int32_t time_bound_ds(const MatchParams& p, int64_t d
 }
 
 // turn degree from in-edge a (end heading ha) into out-edge b (begin heading hb): the
-// angle between the heading back along a and out along b, 0 (U-turn) .. 180 (straight)
-__host__ __device__ inline int turn_degree(int ha_end, int hb_begin) {
-  const int back = (ha_end + 180) % 360;
-  const int td = (hb_begin - back + 360) % 360;
+// angle between the heading back along a and out along b, 0 (U-turn) .. 180 (straight).
+// Headings are integer degrees 0..359 (seg_heading), so the wraps are one compare each
+// (the oracle's `% 360` form, oracle.c turn_degree, gives the same value on that range).
+__host__ __device__ inline int turn_from_back(int back, int hb_begin) {  // back = the in-edge's reversed heading
+  int td = hb_begin - back;
+  td += td < 0 ? 360 : 0;
   return td <= 180 ? td : 360 - td;
+}
+__host__ __device__ inline int heading_back(int ha_end) { return ha_end >= 180 ? ha_end - 180 : ha_end + 180; }
+__host__ __device__ inline int turn_degree(int ha_end, int hb_begin) {
+  return turn_from_back(heading_back(ha_end), hb_begin);
 }
 
 struct DevGraph {
@@ -90,6 +96,8 @@ struct DevGraph {
   uint32_t adj_t_stride, edge_t_stride;  // elements per mode
   const short2* edge_head;     // per edge {begin heading, end heading}, integer degrees
   const uint2* adj_e;          // 4 per node like adj: {edge id, begin heading | end heading << 16} (edge-state searches)
+  const uint4* erec;           // [mode][4 per node like adj]: the multi-source edge-state record (otr_medge.h erec_make)
+  uint32_t erec_stride;        // records per mode
   uint32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double grid_min_lat, grid_min_lon, grid_cell_deg;
   __device__ const uint32_t* et(int mode) const { return edge_t + (size_t)mode * edge_t_stride; }

@@ -369,7 +369,8 @@ __device__ bool edge_search(EdgeLds<CAP, TG>& L, const DevGraph& g, int md, bool
 
 // ------------------------------------------------------------------------------
 // K3e: edge-state route tasks (turn modes), a fixed grid over the device-side list of
-// the tasks flagged 5 (k_route) or 6 (this tier's overflows, for the larger table).
+// the tasks flagged 6 (what the first edge tier, otr_edge1.h, could not hold) or 7 (this
+// tier's overflows, for the 2048-state table).
 // ------------------------------------------------------------------------------
 // What outgrows the 2048-state table goes to k_general (3).  TG: the targets a search
 // holds (32 when every mode keeps <= 32 candidates, else 64).
@@ -420,7 +421,11 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
     const bool ok = edge_search<CAP, TG>(L, gr, md, search, ei, gr.edge_dst[ei], pd, pt, bt >= 0,
                                          Kb, tv, tpart, tpt, thb, counters ? &settled : nullptr,
                                          counters ? &relaxed : nullptr) &&
-                    Kb <= TG;
+                    Kb <= TG
+#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 1 / 2 fails every 384 / 2048-state search
+                    && !(a.force_edge & (CAP < 2048 ? 2 : 4))
+#endif
+        ;
     if (ok) {
       uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
       if (lane < Kb) {
@@ -444,7 +449,7 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
         a.trans_tc[trow - a.trans + (int64_t)i * Kb + lane] = valid ? rc : 0u;
       }
     } else if (lane == 0) {
-      a.overflow_flag[task] = CAP < 2048 ? 6 : 3;
+      a.overflow_flag[task] = CAP < 2048 ? 7 : 3;  // the 2048-state table, then k_general
     }
     if (counters) {
       settled = wave_sum_u32((uint32_t)settled);

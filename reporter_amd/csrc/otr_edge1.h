@@ -1,0 +1,401 @@
+// otr_edge1.h — K3e1: the lean single-source edge-state route search, the first tier of
+// the turn-cost modes (the deployed configuration, Batch.java:56-65: every mode's default
+// turn_penalty_factor is > 0).
+//
+// The semantics are otr_edge.h's (one source candidate per wave, states = edges, 64-bit
+// labels key << 38 | (cap - turn) << 17 | time, exact IN-criterion rounds, the bounds
+// pruning during the search, targets offered by every settled state at src(ej)); what
+// changes is the cost of a round, which is what bounds this search (measured: ~13 rounds
+// of ~600 wave instructions each, a third of the SIMD's VALU issue used at 4.25 waves):
+//   * one 16-B per-mode record per relaxation (DevGraph::erec: head, length, edge id,
+//     route time, begin and end headings) instead of four loads;
+//   * the state keeps its edge's reversed end heading, and turn degrees are two compares
+//     (otr_device.h turn_from_back), not two integer modulos;
+//   * the IN criterion adds the mode's smallest turn cost (every later offer to a state
+//     crosses a turn >= tmin and the state's own edge): lab(b) < kmin + len(b) + tmin is
+//     final, and a target is final once tlab < kmin + tpart + tmin — fewer rounds, the
+//     same final labels;
+//   * settled states keep their pending bit (a final label can never improve, so it is
+//     never pushed again): no write per settled state;
+//   * probe loops are not unrolled, the target map is consulted only when a 64-bit bloom
+//     of the target nodes (a wave-uniform register) admits the settled node, and the
+//     wave's scalar state is kept small (no SGPR spills);
+//   * small tables: the first tier holds CAP states (table + lists + targets + the turn
+//     table in ~7 KB at 256: 22 waves per CU); a search that outgrows it goes on to the
+//     next tier (flag 6, the single-source tiers of otr_edge.h), with the same results.
+#pragma once
+#include "otr_medge.h"
+
+namespace otr {
+
+template <int CAP>
+struct E1Lds {
+  static constexpr int TG = 32;   // targets (steps with more go to otr_edge.h's TG = 64 tier)
+  static constexpr int TM = 64;   // target-node map slots
+  static constexpr int WCAP = CAP <= 256 ? 40 : 96;  // states settled per round (the rest wait)
+  using Idx = typename std::conditional<(CAP <= 256), uint8_t, uint16_t>::type;
+  unsigned long long lab[CAP];  // gpack label, kGInf: none
+  uint32_t key[CAP];            // edge id | kInq (on the pending list, or settled); kEmpty
+  uint32_t node[CAP];           // dst(edge)
+  uint16_t hbk[CAP];            // the edge's end heading reversed
+  uint8_t mi[CAP];              // mi8_of(len(edge))
+  Idx pend[CAP];                // pending slots
+  Idx wsl[WCAP];                // this round's settled slots
+  unsigned long long wlab[WCAP];  //   and their labels
+  unsigned long long tlab[TG];  // the targets' best feasible offers
+  uint32_t tpart[TG], tpt[TG];  // entry parts (mm, 0.1 s)
+  uint16_t thb[TG];             // begin heading of the target edge
+  uint32_t tm_node[TM];         // target node -> target lanes
+  uint32_t tm_mask[TM];
+  unsigned long long bloom;     // bit tm_home(v) of every target node v
+  int32_t turn[181];
+  int turn_md;
+  uint32_t tmin;
+  int n_pend, n_keys, overflow;
+};
+
+__device__ inline uint32_t tm_home(uint32_t v) { return (v * 0x9E3779B1u) >> 26; }  // 64 slots
+
+template <int CAP>
+__device__ inline int e1_insert(E1Lds<CAP>& L, uint32_t e, bool& isnew) {
+  uint32_t h = hslot<CAP>(e);
+#pragma unroll 1
+  for (int probe = 0; probe < CAP; ++probe) {
+    const uint32_t k = atomicCAS(&L.key[h], kEmpty, e);
+    if (k == kEmpty) {
+      isnew = true;
+      return (int)h;
+    }
+    if ((k & kNodeMask) == e) return (int)h;
+    h = h + 1 == (uint32_t)CAP ? 0u : h + 1;
+  }
+  L.overflow = 1;
+  return -1;
+}
+
+template <int CAP>
+__device__ inline void e1_target_offers(E1Lds<CAP>& L, unsigned long long lb, uint32_t hbk, uint32_t v, uint32_t pd,
+                                        uint32_t pt) {
+  uint32_t h = tm_home(v), m = 0;
+#pragma unroll 1
+  for (int probe = 0; probe < E1Lds<CAP>::TM; ++probe) {
+    const uint32_t k = L.tm_node[h];
+    if (k == v) m = L.tm_mask[h];
+    if (k == v || k == kEmpty) break;
+    h = (h + 1) & (E1Lds<CAP>::TM - 1);
+  }
+#pragma unroll 1
+  while (m) {
+    const int q = __ffs((int)m) - 1;
+    m &= m - 1;
+    const uint32_t tc = (uint32_t)L.turn[turn_from_back((int)hbk, (int)L.thb[q])];
+    const EOffer o = e_step(lb, tc, L.tpart[q], L.tpt[q]);
+    if (e_feasible(o, pd, pt)) atomicMin(&L.tlab[q], gpack(o.k, o.c, o.t));
+  }
+}
+
+// relax the final state (label lb, reversed end heading hbk) through one out-edge: its
+// record fields (head w with access bits in dw, length, time, edge id, headings); returns
+// the slot when the edge's state became newly pending
+template <int CAP>
+__device__ inline int e1_relax(E1Lds<CAP>& L, unsigned long long lb, uint32_t hbk, uint32_t dw, uint32_t len,
+                               uint32_t tt, uint32_t b, uint32_t hb, uint32_t hend, uint32_t pd, uint32_t pt,
+                               uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext, uint32_t& dnext, bool& isnew) {
+  if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
+  ++relaxed;
+  const uint32_t tc = (uint32_t)L.turn[turn_from_back((int)hbk, (int)hb)];
+  const EOffer o = e_step(lb, tc, len, tt);
+  if (!e_feasible(o, pd, pt)) return -1;  // pruned (label-setting semantics)
+  const int sl = e1_insert(L, b, isnew);
+  if (sl < 0) return -1;
+  if (isnew) {
+    L.node[sl] = dw & kAdjDstMask;
+    L.hbk[sl] = (uint16_t)heading_back((int)hend);
+    L.mi[sl] = mi8_of(len);
+    L.lab[sl] = kGInf;
+  }
+  const unsigned long long nw = gpack(o.k, o.c, o.t);
+  const unsigned long long old = atomicMin(&L.lab[sl], nw);
+  if (nw >= old) return -1;
+  knext = o.k < knext ? o.k : knext;
+  dnext = o.d < dnext ? o.d : dnext;
+  return (atomicOr(&L.key[sl], kInq) & kInq) ? -1 : sl;
+}
+
+template <int CAP>
+__device__ inline void e1_turn_table(E1Lds<CAP>& L, const int32_t* turn_tab, int md) {
+  if (L.turn_md != md) {  // (uniform)
+    __syncthreads();
+    uint32_t m = 0xFFFFFFFFu;
+    for (int k = threadIdx.x; k < 181; k += OTR_WAVE) {
+      const int32_t t = turn_tab[181 * md + k];
+      L.turn[k] = t;
+      m = (uint32_t)t < m ? (uint32_t)t : m;
+    }
+    m = wave_min_u32(m);
+    if (threadIdx.x == 0) {
+      L.turn_md = md;
+      L.tmin = m;
+    }
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------
+// K3e1 kernel: a persistent grid over the device-side list of the turn-mode tasks (one
+// source candidate each), the 8 XCDs taking contiguous eighths of the list (consecutive
+// tasks = the candidates of one step, then the next steps of the trace: one neighbourhood).
+// A search that outgrows the table flags its task 6 (otr_edge.h's larger tables).
+// ------------------------------------------------------------------------------
+template <int CAP>
+__global__ __launch_bounds__(64) void k_route_e1(DevGraph gr, RouteArgs a, unsigned long long* counters) {
+  using LT = E1Lds<CAP>;
+  constexpr int TG = LT::TG, TM = LT::TM, WCAP = LT::WCAP;
+  constexpr int kMaxKeys = (CAP * 7) / 8;
+  __shared__ LT L;
+  if (threadIdx.x == 0) L.turn_md = -1;
+  const int64_t n = (int64_t)*a.list_count;
+  const int lane = (int)threadIdx.x;
+  const int64_t per = (n + 7) / 8;
+  const int64_t lo = (int64_t)(blockIdx.x & 7) * per;
+  const int64_t hi = lo + per < n ? lo + per : n;
+  const int64_t stride = (int64_t)(gridDim.x >> 3);
+  for (int64_t w = lo + (int64_t)(blockIdx.x >> 3); w < hi; w += stride) {
+    const int64_t task = a.task_list[w];
+    const uint4 r0 = a.rec[3 * task], r1 = a.rec[3 * task + 1], r2 = a.rec[3 * task + 2];
+    const int64_t s = r0.x, sp = r0.y;
+    const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
+    const int i = __ffsll((long long)mask) - 1;  // the task's one source
+    const int Kb = (int)(r1.y & 0xFFu);
+    const int md = (int)((r1.y >> 8) & 3u);
+    const bool forced = (r1.y >> 10) & 1u;
+    const uint32_t bmm = r0.w;
+    const int32_t bt = (int32_t)r2.y;
+    const bool timed = bt >= 0;
+    const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
+    const double pi = a.cand_p[sp * OTR_KMAX + i];
+    const uint32_t d0 = a.cprep[sp * OTR_KMAX + i].w;
+    const uint32_t t0 = timed ? a.cprep_t[sp * OTR_KMAX + i].y : 0u;
+    uint32_t ej = 0, tv = kEmpty, tpart = 0, tpt = 0;
+    double pj = 0;
+    bool needed = false;
+    if (lane < Kb) {
+      ej = a.cand_edge[s * OTR_KMAX + lane];
+      pj = a.cand_p[s * OTR_KMAX + lane];
+      const uint4 cq = a.cprep[s * OTR_KMAX + lane];
+      tpart = cq.x;
+      tpt = timed ? a.cprep_t[s * OTR_KMAX + lane].x : 0u;
+      needed = !(ej == ei && pj >= pi);
+      if (needed) tv = cq.y;
+    }
+    const bool root_ok = d0 <= bmm && (!timed || t0 <= (uint32_t)bt);
+    const bool search = Kb <= TG && !forced && root_ok && __ballot(needed) != 0ull;
+    const uint32_t pd = bmm >= d0 ? bmm - d0 : 0u;
+    const uint32_t pt = !timed ? 0xFFFFFFFFu : (t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u);
+    // ---- reset: keys, targets, the target map and its bloom
+    for (int k = lane; k < CAP; k += OTR_WAVE) L.key[k] = kEmpty;
+    if (lane < TG) L.tlab[lane] = kGInf;
+    L.tm_node[lane] = kEmpty;
+    L.tm_mask[lane] = 0u;
+    if (lane == 0) {
+      L.overflow = 0;
+      L.bloom = 0ull;
+    }
+    e1_turn_table(L, a.turn, md);
+    const bool tgt = search && lane < Kb && tv != kEmpty;
+    if (tgt) {
+      L.tpart[lane] = tpart;
+      L.tpt[lane] = tpt;
+      L.thb[lane] = (uint16_t)gr.edge_head[ej].x;
+      uint32_t h = tm_home(tv);
+#pragma unroll 1
+      for (int probe = 0; probe < TM; ++probe) {
+        const uint32_t k = atomicCAS(&L.tm_node[h], kEmpty, tv);
+        if (k == kEmpty || k == tv) {
+          atomicOr(&L.tm_mask[h], 1u << lane);
+          break;
+        }
+        h = (h + 1) & (TM - 1);
+      }
+      atomicOr(&L.bloom, 1ull << tm_home(tv));
+    }
+    __syncthreads();
+    // the bloom of the target nodes: a settled state consults the map only on a hit
+    const unsigned long long bloom = L.bloom;
+    bool ok = true;
+    uint32_t my_settled = 0, my_relaxed = 0;
+    if (search) {
+      if (lane == 0) {
+        bool isnew = false;
+        const int sl = e1_insert(L, ei, isnew);  // (an empty table: the home slot)
+        L.node[sl] = gr.edge_dst[ei];
+        L.hbk[sl] = (uint16_t)heading_back((int)(uint16_t)gr.edge_head[ei].y);
+        L.mi[sl] = 0;  // the root: label 0 is final at once (gap 1 mm)
+        L.lab[sl] = gpack(0u, 0u, 0u);
+        L.key[sl] = ei | kInq;
+        L.pend[0] = (typename LT::Idx)sl;
+      }
+      __syncthreads();
+      const uint4* er = gr.erec + (size_t)md * gr.erec_stride;
+      const uint32_t mode_bit = 1u << md;
+      const uint32_t tmin = L.tmin;
+      uint32_t kmin = 0, dmin = 0;  // the smallest pending key / length
+      int npend = 1, nkeys = 1;
+#pragma unroll 1
+      for (;;) {
+        // ---- targets: every later offer to a target has key >= kmin + tpart + tmin and
+        // length >= dmin + tpart; done when every needed target is final or unreachable
+        bool res = true;
+        if (tgt) {
+          const unsigned long long tl = L.tlab[lane];
+          res = (tl != kGInf && (uint64_t)g_k(tl) < (uint64_t)kmin + tpart + tmin) ||
+                (uint64_t)dmin + tpart > (uint64_t)pd;
+        }
+        if (__ballot(!res) == 0ull || npend == 0) break;
+        // ---- partition: final pending states (IN criterion) to the settled list; the
+        // rest stay and give the next kmin / dmin
+        uint32_t knext = 0xFFFFFFFFu, dnext = 0xFFFFFFFFu;
+        int kept = 0, nw = 0;
+#pragma unroll 1
+        for (int base = 0; base < npend; base += OTR_WAVE) {
+          const int k = base + lane;
+          const bool in = k < npend;
+          int sl = 0;
+          unsigned long long lb = 0;
+          bool take = false;
+          if (in) {
+            sl = L.pend[k];
+            lb = L.lab[sl];
+            take = (uint64_t)g_k(lb) < (uint64_t)kmin + in_gap8(L.mi[sl]) + tmin;
+          }
+          take = take && nw + prefix_count(__ballot(take)) < WCAP;
+          const bool keep = in && !take;
+          const unsigned long long mt = __ballot(take), mk = __ballot(keep);
+          __syncthreads();
+          if (take) {
+            const int wq = nw + prefix_count(mt);
+            L.wsl[wq] = (typename LT::Idx)sl;
+            L.wlab[wq] = lb;
+          } else if (keep) {
+            L.pend[kept + prefix_count(mk)] = (typename LT::Idx)sl;
+            knext = g_k(lb) < knext ? g_k(lb) : knext;
+            dnext = g_d(lb) < dnext ? g_d(lb) : dnext;
+          }
+          nw += __popcll(mt);
+          kept += __popcll(mk);
+          __syncthreads();
+        }
+        npend = kept;
+        // ---- relax: lane = (settled state, adjacency slot)
+        bool tail = false;
+#pragma unroll 1
+        for (int base = 0; base < 4 * nw; base += OTR_WAVE) {
+          const int k = base + lane;
+          int psl = -1;
+          bool isnew = false;
+          if (k < 4 * nw) {
+            const int sl = L.wsl[k >> 2];
+            const unsigned long long lb = L.wlab[k >> 2];
+            const uint32_t v = L.node[sl], hbk = L.hbk[sl];
+            const int slot = k & 3;
+            const uint4 r = ld16(er + 4 * (size_t)v + slot);
+            if (slot == 0) {
+              ++my_settled;
+              if ((bloom >> tm_home(v)) & 1ull) e1_target_offers(L, lb, hbk, v, pd, pt);
+            }
+            psl = e1_relax(L, lb, hbk, r.x & ~kAdjMore, r.y, timed ? er_t(r) : 0u, er_edge(r), er_hb(r), er_he(r), pd,
+                           pt, mode_bit, my_relaxed, knext, dnext, isnew);
+            tail = tail || (slot == 3 && (r.x & kAdjMore));
+          }
+          nkeys += __popcll(__ballot(isnew));
+          const unsigned long long mp = __ballot(psl >= 0);
+          if (psl >= 0) L.pend[npend + prefix_count(mp)] = (typename LT::Idx)psl;  // (< CAP: one entry per state)
+          npend += __popcll(mp);
+        }
+        if (__ballot(tail) != 0ull) {  // nodes with more than four out-edges: the CSR tail
+          if (lane == 0) {
+            L.n_pend = npend;
+            L.n_keys = 0;
+          }
+          __syncthreads();
+#pragma unroll 1
+          for (int base = 0; base < 4 * nw; base += OTR_WAVE) {
+            const int k = base + lane;
+            if (k < 4 * nw && (k & 3) == 3) {
+              const int sl = L.wsl[k >> 2];
+              const unsigned long long lb = L.wlab[k >> 2];
+              const uint32_t v = L.node[sl], hbk = L.hbk[sl];
+              if (er[4 * (size_t)v + 3].x & kAdjMore) {
+                const uint32_t* et = gr.et(md);
+#pragma unroll 1
+                for (uint32_t e = gr.node_row[v] + 4; e < gr.node_row[v + 1]; ++e) {
+                  const uint4 pk = ld16(gr.edge_pack + e);
+                  const short2 hh = gr.edge_head[e];
+                  bool nw2 = false;
+                  const int p2 = e1_relax(L, lb, hbk, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e,
+                                          (uint32_t)(uint16_t)hh.x, (uint32_t)(uint16_t)hh.y, pd, pt, mode_bit,
+                                          my_relaxed, knext, dnext, nw2);
+                  if (nw2) atomicAdd(&L.n_keys, 1);
+                  if (p2 >= 0) L.pend[atomicAdd(&L.n_pend, 1)] = (typename LT::Idx)p2;
+                }
+              }
+            }
+          }
+          __syncthreads();
+          npend = L.n_pend;
+          nkeys += L.n_keys;
+        }
+        __syncthreads();
+        kmin = wave_min_u32(knext);
+        dmin = wave_min_u32(dnext);
+        if (L.overflow || nkeys > kMaxKeys) {
+          ok = false;
+          break;
+        }
+      }
+    }
+#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 0 fails every first-tier edge search
+    if (a.force_edge & 1) ok = false;
+#endif
+    ok = ok && Kb <= TG;
+    if (ok) {
+      uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
+      if (lane < Kb) {
+        int64_t rr = -1, rt = 0;
+        uint32_t rc = 0;
+        if (forced) {
+          rr = -1;
+        } else if (ej == ei && pj >= pi) {
+          const uint2 li = a.clen[sp * OTR_KMAX + i];
+          rr = part_mm(pj - pi, li.x);
+          if (timed) rt = part_mm(pj - pi, li.y);
+        } else if (search) {
+          const unsigned long long tl = L.tlab[lane];
+          if (tl != kGInf) {
+            rr = (int64_t)d0 + g_d(tl);
+            rt = (int64_t)t0 + g_t(tl);
+            rc = g_c(tl);
+          }
+        }
+        const bool valid = rr >= 0 && rr <= (int64_t)bmm && (!timed || rt <= (int64_t)bt);
+        trow[(int64_t)i * Kb + lane] = valid ? (uint32_t)rr : kNoRoute;
+        a.trans_tc[trow - a.trans + (int64_t)i * Kb + lane] = valid ? rc : 0u;
+      }
+      if (counters) {
+        const uint32_t st = wave_sum_u32(my_settled), rl = wave_sum_u32(my_relaxed);
+        if (lane == 0) {
+          const int sh = cshard();
+          atomicAdd(&counters[3 * kCShards + sh], (unsigned long long)st);
+          atomicAdd(&counters[4 * kCShards + sh], (unsigned long long)rl);
+          atomicAdd(&counters[5 * kCShards + sh], search ? (unsigned long long)Kb : 0ull);
+          atomicAdd(&counters[6 * kCShards + sh], search ? 1ull : 0ull);
+        }
+      }
+    } else if (lane == 0) {
+      a.overflow_flag[task] = 6;  // the larger single-source tables (otr_edge.h)
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace otr

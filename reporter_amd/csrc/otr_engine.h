@@ -95,7 +95,7 @@ struct Matcher {
   std::vector<unsigned long long> h_seg_id, h_rep_id, h_rep_next;
   std::vector<uint8_t> h_seg_internal;
   std::vector<otr_tile_row> h_tile_rows;
-  hipEvent_t ev[44];  // 0..19 batch stages, 20..23 ingest, 24..43 route tiers
+  hipEvent_t ev[48];  // 0..19 batch stages, 20..23 ingest, 24..47 route tiers
   bool ev_init = false;
 
   template <class T>

@@ -13,6 +13,8 @@
 #include "otr_engine.h"
 #include "otr_kernels.h"
 #include "otr_edge.h"
+#include "otr_medge.h"
+#include "otr_edge1.h"
 #include "otr_ingest.h"
 
 namespace otr {
@@ -245,6 +247,18 @@ int engine_configure(const Config& cfg, std::string* err) {
       const uint32_t e = row[u] + k;
       adje[4ull * u + k] = make_uint2(e, (uint32_t)(uint16_t)head[e].x | ((uint32_t)(uint16_t)head[e].y << 16));
     }
+  // multi-source edge-state view (otr_medge.h): per mode one 16-B record per adjacency
+  // slot with the head, length, edge id, route time and both headings (one load per relaxation)
+  std::vector<uint4> erec((4ull * h.n_nodes + 4) * OTR_MODES, make_uint4(kAdjDstMask, 0u, 0u, 0u));
+  for (int m = 0; m < OTR_MODES; ++m) {
+    uint4* er = erec.data() + (4ull * h.n_nodes + 4) * m;
+    for (uint32_t u = 0; u < h.n_nodes; ++u)
+      for (uint32_t k = 0; k < 4 && row[u] + k < row[u + 1]; ++k) {
+        const uint32_t e = row[u] + k;
+        er[4ull * u + k] = erec_make(adj[4ull * u + k].x, len[e], e, et[m][e], (uint32_t)(uint16_t)head[e].x,
+                                     (uint32_t)(uint16_t)head[e].y);
+      }
+  }
   // candidate-search view: each grid-cell entry carries its edge's shape range and
   // attributes, 48 B per entry: {edge, shape begin, shape end, attr} + the first four shape points
   const uint32_t* cedge = (const uint32_t*)(base + h.array_offset[OTR_A_CELL_EDGE]);
@@ -314,6 +328,8 @@ int engine_configure(const Config& cfg, std::string* err) {
   }
   g.edge_head = (const short2*)upv(head.data(), sizeof(short2) * head.size());
   g.adj_e = (const uint2*)upv(adje.data(), sizeof(uint2) * adje.size());
+  g.erec = (const uint4*)upv(erec.data(), sizeof(uint4) * erec.size());
+  g.erec_stride = (uint32_t)(4ull * h.n_nodes + 4);
   g.cell_rec = (const uint4*)upv(crec.data(), sizeof(uint4) * crec.size());
   if (!alloc_ok) {
     if (err) *err = "device allocation for the graph failed";
@@ -374,7 +390,7 @@ enum Slot {
   S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
-  S_CLEN, S_CAND_NROOT, S_FLAGGED,
+  S_CLEN, S_CAND_NROOT, S_FLAGGED, S_MGROUPS, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST,
   S_NUM
 };
 
@@ -638,12 +654,14 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   out->n_probes = N;
   h_trace_status.assign(T, OTR_OK);
   // counter banks of OTR_COUNTERS kinds x kCShards: 0 the batch (and the first route
-  // tier), 2..6 the LDS retry tiers, 8..9 the global-memory tiers; folded at the end
-  // into n_ctr values behind them
+  // tier), 1 the 384-state edge tier, 2..6 the LDS retry tiers, 7 the 64-bit tier, 8..9 the
+  // global-memory tiers, 10 the multi-source edge tier, 11 the 2048-state edge tier; folded
+  // at the end into n_ctr values behind them
+  constexpr int kBanks = 12;
   const size_t bank = (size_t)OTR_COUNTERS * kCShards;
-  const size_t n_ctr = 10 * (size_t)OTR_COUNTERS;
-  unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, 10 * bank + n_ctr);
-  HIPCHK(hipMemsetAsync(d_counters, 0, 10 * bank * 8, stream));
+  const size_t n_ctr = kBanks * (size_t)OTR_COUNTERS;
+  unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, kBanks * bank + n_ctr);
+  HIPCHK(hipMemsetAsync(d_counters, 0, kBanks * bank * 8, stream));
   size_t scan_bytes = 0;
   auto scan = [&](const int64_t* src, int64_t* dst_np1, int64_t n) -> int {
     // dst[0] = 0, dst[1..n] = inclusive prefix sums
@@ -774,10 +792,15 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     ta.task_state = task_state;
     ta.task_mask = task_mask;
     ta.rec = task_rec;
+#if OTR_MEDGE
+    ta.flag_turn = nullptr;  // (the multi-source tier takes every turn-mode task)
+#else
+    ta.flag_turn = task_ovf;  // turn-mode tasks start in the first edge-state tier (flag 5)
+#endif
+    if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
     if (k32) k_tasks<2><<<grid_for((S + 1) / 2, 4), 256, 0, stream>>>(ta);
     else k_tasks<1><<<grid_for(S, 4), 256, 0, stream>>>(ta);
   }
-  if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
   // turn cost tables of this batch's parameters (oracle orc_turn_table)
   int32_t* d_turn = need<int32_t>(S_TURN, 181 * OTR_MODES);
   h_turn.resize(181 * OTR_MODES);
@@ -835,7 +858,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   // device-side counters of the retry lists: [0..7] route tiers, [8] general tier 1,
   // [9] general tier 2, [10] route tasks left unrouted, [11] steps, [12..15] path tiers,
   // [16] path general 1, [17] path general 2, [18] paths left, [19] general overflow
-  // count, [20] cap flag, [21] exact node path tier, [24] tasks the first route tier
+  // count, [20] cap flag, [21] exact node path tier, [22] multi-source edge groups (A/B
+  // build), [23] first edge-state tier, [24] tasks the first route tier
   // flagged, [25..26] edge-state route tiers, [27..28] edge-state path tiers, [29] exact
   // edge route tier, [30] exact node route tier, [31] exact edge path tier, [32..96) path
   // bump cursors
@@ -919,16 +943,28 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     if (CTR) k_route<C, G_, LIST_, false, true><<<GRID, 64, 0, stream>>>(g, ARGS, CTR);      \
     else k_route<C, G_, LIST_, false, false><<<GRID, 64, 0, stream>>>(g, ARGS, nullptr);     \
   } while (0)
-    // turn-mode (edge-based) tasks are `general` (k_tasks): the LDS tiers pass them on
+    // turn-mode (edge-state) tasks belong to the multi-source edge tier below: the node
+    // tiers pass them on unflagged, and when every mode has turn costs (the deployed
+    // configuration) no node task exists and the first node tier is not launched at all
     const bool turns = turn_modes != 0u;
-    if (route_g == 2) {
-      tb(OTR_STAGE_ROUTE);
+#ifdef OTR_FORCE_GENERAL
+    const bool node_tasks = true;  // (test build: the first tier flags every task for k_general)
+#else
+    const bool node_tasks = turn_modes != (1u << OTR_MODES) - 1u;
+#endif
+#ifdef OTR_FORCE_RETRY
+    {  // test build: OTR_FORCE_EDGE bits force the edge-state tiers to fail (tests/test_gpu_tiers.py)
+      const char* fe = getenv("OTR_FORCE_EDGE");
+      ra.force_edge = fe ? atoi(fe) : 0;
+    }
+#endif
+    tb(OTR_STAGE_ROUTE);
+    if (node_tasks && route_g == 2) {
       const int64_t units = (NT + 1) / 2;
       const unsigned grid = (unsigned)(8 * ((units + 7) / 8));
       OTR_ROUTE_LAUNCH(OTR_CAP1, 2, false, grid, ra, rwork);
       out->route_tier_code[0] = OTR_CAP1 * 10 + 2;
-    } else {
-      tb(OTR_STAGE_ROUTE);
+    } else if (node_tasks) {
       const unsigned grid = (unsigned)(8 * ((NT + 7) / 8));
       OTR_ROUTE_LAUNCH(256, 1, false, grid, ra, rwork);
       out->route_tier_code[0] = 2561;
@@ -945,6 +981,22 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // persistent grids: twice the resident waves of the widest tier (256 CUs x 4 SIMDs x
     // 8 waves), so no tier is starved; blocks past the list length exit at once
     const unsigned tgrid = 16384;
+#if OTR_MEDGE && !defined(OTR_FORCE_GENERAL)
+    // A/B build (-DOTR_MEDGE=1): the turn-mode tasks in the multi-source edge tier first,
+    // OTR_MS source candidates of a step per search (otr_medge.h); groups it cannot hold
+    // flag their tasks 5 (the single-source edge tiers below)
+    if (turns) {
+      uint64_t* groups = need<uint64_t>(S_MGROUPS, std::max<int64_t>(NT, 1));
+      if (!groups) {
+        if (err) *err = "device allocation failed (edge-state groups)";
+        return OTR_DEVICE_ERROR;
+      }
+      k_mgroups<OTR_MS><<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, cb.count, task_off, state_trace, b.mode,
+                                                               turn_modes, groups, cnt + 22);
+      // (no tier slot of its own: its time is in the route_big stage)
+      k_route_medge<OTR_MCAP, OTR_MS><<<4096, 64, 0, stream>>>(g, ra, groups, cnt + 22, nullptr);
+    }
+#endif
     // the first tier's flagged tasks, once; every later collect scans only them
     k_collect_flagged<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, flagged, cnt + 24);
     constexpr unsigned kCollectGrid = 512;
@@ -989,26 +1041,29 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       if (timing) (void)hipEventRecord(ev[24 + 2 * 8 + 1], stream);
     }
 #endif
-    // turn-mode tasks (flag 5): the edge-state LDS search, 384 then 2048 states; what
-    // outgrows it (flag 3) goes on below; slot 9 (bank 1): the edge-state tiers
-    if (timing) (void)hipEventRecord(ev[24 + 2 * 9], stream);
+    // edge-state tiers (turn-cost modes): the lean first tier (flag 5, otr_edge1.h, slot
+    // 10), then the 768- and 2048-state tables (flags 6, 7: otr_edge.h, slots 9 / 11); what
+    // outgrows those (flag 3) goes on below
     if (turns) {
-      out->route_tier_code[9] = 7000000 + OTR_ECAP * 100 + (k32 ? 32 : 64);
-      for (int et = 0; et < 2; ++et) {
-        unsigned long long* c = cnt + 25 + et;
-        k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, et == 0 ? 0x20u : 0x40u,
-                                                              list, c);
+      for (int et = 0; et < 3; ++et) {
+        const int slot = et == 0 ? 10 : (et == 1 ? 9 : 11);
+        out->route_tier_code[slot] = et == 0 ? 6000000 + OTR_E1CAP * 100 + 32
+                                             : 7000000 + (et == 1 ? OTR_ECAP : 2048) * 100 + (et == 2 || !k32 ? 64 : 32);
+        unsigned long long* c = cnt + (et == 0 ? 23 : 24 + et);
+        k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x20u << et, list, c);
         RouteArgs rb = ra;
         rb.task_list = list;
         rb.list_count = c;
-        unsigned long long* rcn = rwork ? d_counters + 1 * bank : nullptr;
-        // (the persistent grids hold every resident wave: ~19 per CU at 384 states)
-        if (et == 0 && k32) k_route_edge<OTR_ECAP, 32><<<8192, 64, 0, stream>>>(g, rb, rcn);
-        else if (et == 0) k_route_edge<OTR_ECAP, 64><<<8192, 64, 0, stream>>>(g, rb, rcn);
-        else k_route_edge<2048, 64><<<512, 64, 0, stream>>>(g, rb, rcn);
+        unsigned long long* rcn = rwork ? d_counters + (et == 0 ? 10 : (et == 1 ? 1 : 11)) * bank : nullptr;
+        if (timing) (void)hipEventRecord(ev[24 + 2 * slot], stream);
+        // persistent grids: every resident wave (~22 per CU at 256 states, 9 at 768, 3 at 2048)
+        if (et == 0) k_route_e1<OTR_E1CAP><<<8192, 64, 0, stream>>>(g, rb, rcn);
+        else if (et == 1 && k32) k_route_edge<OTR_ECAP, 32><<<4096, 64, 0, stream>>>(g, rb, rcn);
+        else if (et == 1) k_route_edge<OTR_ECAP, 64><<<4096, 64, 0, stream>>>(g, rb, rcn);
+        else k_route_edge<2048, 64><<<1024, 64, 0, stream>>>(g, rb, rcn);
+        if (timing) (void)hipEventRecord(ev[24 + 2 * slot + 1], stream);
       }
     }
-    if (timing) (void)hipEventRecord(ev[24 + 2 * 9 + 1], stream);
     // everything left — tasks whose labels need 64 bits, overflows of the largest LDS
     // tables (node and edge-state) — runs in the global-memory search: first on 32K-slot
     // slabs, then what outgrew those on 1M-slot slabs
@@ -1295,8 +1350,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   HIPCHK(hipGetLastError());
   std::vector<unsigned long long> hc(n_ctr);
   unsigned long long h_fail[2] = {0ull, 0ull};  // route tasks / paths beyond every search tier
-  k_ctr_fold<<<(unsigned)n_ctr, kCShards, 0, stream>>>(d_counters, d_counters + 10 * bank);
-  HIPCHK(hipMemcpyAsync(hc.data(), d_counters + 10 * bank, n_ctr * 8, hipMemcpyDeviceToHost, stream));
+  k_ctr_fold<<<(unsigned)n_ctr, kCShards, 0, stream>>>(d_counters, d_counters + kBanks * bank);
+  HIPCHK(hipMemcpyAsync(hc.data(), d_counters + kBanks * bank, n_ctr * 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipMemcpyAsync(&h_fail[0], cnt + 10, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipMemcpyAsync(&h_fail[1], cnt + 18, 8, hipMemcpyDeviceToHost, stream));
   // per-trace output counts in the same drain (one host wait per batch for all of them)
@@ -1331,9 +1386,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   };
   for (int k = 0; k < OTR_COUNTERS; ++k) out->counters[k] = ctr(0, k);
   // per route kernel: searches, settled, relaxed, transition entries (banks 0, 2..6, 8..9;
-  // slot 8, the 64-bit LDS tier: bank 7; slot 9, the edge-state tiers: bank 1)
-  for (int t = 0; t < 10; ++t) {
-    const int b = t == 0 ? 0 : (t < 6 ? 1 + t : (t < 8 ? 2 + t : (t == 8 ? 7 : 1)));
+  // slot 8, the 64-bit LDS tier: bank 7; slot 9, the 384-state edge tier: bank 1; slot 10,
+  // the multi-source edge tier: bank 10; slot 11, the 2048-state edge tier: bank 11)
+  for (int t = 0; t < 12; ++t) {
+    const int b = t == 0 ? 0 : (t < 6 ? 1 + t : (t < 8 ? 2 + t : (t == 8 ? 7 : (t == 9 ? 1 : t))));
     out->route_tier_work[t][0] = ctr(b, 6);
     out->route_tier_work[t][1] = ctr(b, 3);
     out->route_tier_work[t][2] = ctr(b, 4);
@@ -1353,7 +1409,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     for (int k = 0; k < 10; ++k)
       if (used[k]) (void)hipEventElapsedTime(&out->kernel_ms[k], ev[2 * k], ev[2 * k + 1]);
     out->route_tier_ms[0] = out->kernel_ms[OTR_STAGE_ROUTE];
-    for (int t = 1; t < 10; ++t)
+    for (int t = 1; t < 12; ++t)
       if (out->route_tier_code[t] != 0)
         (void)hipEventElapsedTime(&out->route_tier_ms[t], ev[24 + 2 * t], ev[24 + 2 * t + 1]);
     (void)hipGetLastError();  // an unrecorded pair must not leave a sticky error for the next call
@@ -1794,15 +1850,82 @@ __global__ void k_entry_reduce(const otr_hist_entry* e, int64_t n, const int64_t
   x.count = (uint32_t)(tot < 0xFFFFFFFFll ? tot : 0xFFFFFFFFll);
   out[r] = x;
 }
-// privacy: keep an entry when its pair's total count (over its bins) reaches privacy
-__global__ void k_entry_keep(const int64_t* pair_pos, const int64_t* pair_start, int64_t n_pairs, int64_t n,
-                             const int64_t* csum, int32_t privacy, int64_t* keep) {
+// The owner's privacy cull of simple_reporter.py:218-239 on keyed entries.  A pair's run
+// length in its file is its total count over the speed bins (one line per tile row); the
+// reference sorts a file's lines as strings, so its runs are in the string order of
+// (id, next_id) (dec_key), and the loop judges every run alone (kept iff >= privacy)
+// except that a trailing run of ONE line is judged together with the run before it (both
+// kept iff that run's length + 1 >= privacy).  Per file (files are
+// contiguous in the numeric entry order), one block finds the string-last and the
+// string-second pair (a top-2 reduction), then every entry gets its keep flag.
+struct PairFile {
+  unsigned long long s1, n1, s2, n2;  // dec_key of (id, next id): the string-last pair, the one before it
+  int64_t t1, t2;                     // their totals
+};
+__device__ inline bool pf_after(unsigned long long as, unsigned long long an, unsigned long long bs,
+                                unsigned long long bn) {
+  return as > bs || (as == bs && an > bn);
+}
+__device__ inline void pf_add(PairFile& T, unsigned long long s, unsigned long long n, int64_t t) {
+  if (pf_after(s, n, T.s1, T.n1)) {
+    T.s2 = T.s1;
+    T.n2 = T.n1;
+    T.t2 = T.t1;
+    T.s1 = s;
+    T.n1 = n;
+    T.t1 = t;
+  } else if (pf_after(s, n, T.s2, T.n2)) {
+    T.s2 = s;
+    T.n2 = n;
+    T.t2 = t;
+  }
+}
+__global__ void k_pair_file_heads(const otr_hist_entry* e, const int64_t* pair_start, int64_t n_pairs, int64_t* head) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_pairs) head[p] = p == 0 || e[pair_start[p]].file != e[pair_start[p - 1]].file ? 1 : 0;
+}
+// one 256-thread block per file over its pairs [ffirst[f], ffirst[f + 1]): the top two pairs
+// by (dec_key(id), dec_key(next_id)) and their totals (dec_key > 0: 0 marks "none")
+__global__ __launch_bounds__(256) void k_pair_file_top2(const otr_hist_entry* e, const int64_t* pair_start,
+                                                        int64_t n_pairs, int64_t n, const int64_t* csum,
+                                                        const int64_t* ffirst, int64_t nf, PairFile* F) {
+  const int64_t f = blockIdx.x;
+  const int64_t p0 = ffirst[f], p1 = f + 1 < nf ? ffirst[f + 1] : n_pairs;
+  PairFile T{0ull, 0ull, 0ull, 0ull, 0, 0};
+  for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+    const int64_t s = pair_start[p], t = p + 1 < n_pairs ? pair_start[p + 1] : n;
+    const otr_hist_entry& x = e[s];
+    pf_add(T, dec_key(x.id), dec_key(x.next_id), csum[t - 1] - (s > 0 ? csum[s - 1] : 0));
+  }
+  __shared__ PairFile sh[256];
+  sh[threadIdx.x] = T;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const PairFile U = sh[threadIdx.x + w];
+      if (U.s1) pf_add(T, U.s1, U.n1, U.t1);
+      if (U.s2) pf_add(T, U.s2, U.n2, U.t2);
+      sh[threadIdx.x] = T;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) F[f] = T;
+}
+__global__ void k_entry_keep(const otr_hist_entry* e, const int64_t* pair_pos, const int64_t* pair_start,
+                             int64_t n_pairs, int64_t n, const int64_t* csum, const int64_t* fidx, const PairFile* F,
+                             int32_t privacy, int64_t* keep) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t p = pair_pos[i] - 1;
   const int64_t s = pair_start[p], t = p + 1 < n_pairs ? pair_start[p + 1] : n;
   const int64_t tot = csum[t - 1] - (s > 0 ? csum[s - 1] : 0);
-  keep[i] = tot >= (int64_t)privacy ? 1 : 0;
+  bool k = tot >= (int64_t)privacy;
+  const PairFile& f = F[fidx[p] - 1];
+  if (f.s2 != 0ull && f.t1 == 1) {  // the file's string-last run is one line: judged with the run before it
+    const unsigned long long si = dec_key(e[i].id), sn = dec_key(e[i].next_id);
+    if ((si == f.s1 && sn == f.n1) || (si == f.s2 && sn == f.n2)) k = f.t2 + 1 >= (int64_t)privacy;
+  }
+  keep[i] = k ? 1 : 0;
 }
 
 int Matcher::copy_out(void* dst, const void* src, size_t bytes, int dst_memory, std::string* err) {
@@ -1919,8 +2042,23 @@ int Matcher::hist_reduce_impl(const void* in, int64_t n, int memory, int rows_in
     tb = tb_scan;
     HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, head, csum, nri, stream));
     HIPCHK(hipStreamSynchronize(stream));
+    // per file: the string-last and string-second pairs (the reference loop's trailing run)
+    int64_t* fidx = need<int64_t>(S_HE_FIDX, std::max<int64_t>(np, 1));
+    int64_t* fhead = need<int64_t>(S_HE_FHEAD, std::max<int64_t>(np, 1));
+    if (!fidx || !fhead) return fail("device allocation failed (histogram)");
+    k_pair_file_heads<<<grid_for(np, 256), 256, 0, stream>>>(e_red, rstart, np, fhead);
+    tb = tb_scan;
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, fhead, fidx, (int)np, stream));
+    int64_t nf = 0;
+    HIPCHK(hipMemcpyAsync(&nf, fidx + (np - 1), 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    PairFile* pf = need<PairFile>(S_HE_PFILE, std::max<int64_t>(nf, 1));
+    int64_t* ffirst = need<int64_t>(S_HE_FFIRST, std::max<int64_t>(nf, 1));
+    if (!pf || !ffirst) return fail("device allocation failed (histogram)");
+    k_scatter_index<<<grid_for(np, 256), 256, 0, stream>>>(fhead, fidx, np, ffirst);
+    k_pair_file_top2<<<(unsigned)nf, 256, 0, stream>>>(e_red, rstart, np, nr, csum, ffirst, nf, pf);
     int64_t* keep = head;  // counts no longer needed
-    k_entry_keep<<<grid_for(nr, 256), 256, 0, stream>>>(pos, rstart, np, nr, csum, privacy, keep);
+    k_entry_keep<<<grid_for(nr, 256), 256, 0, stream>>>(e_red, pos, rstart, np, nr, csum, fidx, pf, privacy, keep);
     int64_t* kpos = rstart;  // pair starts no longer needed after k_entry_keep
     tb = tb_scan;
     HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, keep, kpos, nri, stream));

@@ -28,9 +28,19 @@
 #ifndef OTR_LOAD1
 #define OTR_LOAD1 7
 #endif
-// the edge-state search's first table (states per search; turn-cost modes)
+// the single-source edge-state search's first table (states per search; turn-cost modes):
+// it takes what the multi-source tier (otr_medge.h) cannot hold — groups whose union of
+// states outgrows that table, i.e. the large searches (a third of them beyond 336 keys)
 #ifndef OTR_ECAP
-#define OTR_ECAP 384
+#define OTR_ECAP 768
+#endif
+// the lean first edge-state tier's table (otr_edge1.h)
+#ifndef OTR_E1CAP
+#define OTR_E1CAP 256
+#endif
+// A/B: the multi-source edge tier (otr_medge.h) ahead of the single-source ones
+#ifndef OTR_MEDGE
+#define OTR_MEDGE 0
 #endif
 
 namespace otr {
@@ -1059,6 +1069,8 @@ struct RouteArgs {
   float est_v[OTR_MODES];     // m/s: the mode's typical speed (50 km/h, capped by the mode's)
   uint32_t tier_keys[8];      // key capacity of each retry tier, in order
   int n_tiers;
+  int force_edge;             // test build only (OTR_FORCE_RETRY): bit 0 every multi-source edge group
+                              // fails, bit 1 every 384-state edge search, bit 2 every 2048-state one
 };
 
 // k_tasks' inputs and outputs
@@ -1081,6 +1093,7 @@ struct TaskArgs {
   int64_t* task_state;
   unsigned long long* task_mask;
   uint4* rec;                 // 3 per task (the K2c record, below)
+  int32_t* flag_turn;         // per task: 5 for a turn-mode task (the first edge-state tier's list), or null
 };
 
 // One lane group per step s (G states per wave: G = 2 when every mode keeps <= 32
@@ -1142,6 +1155,7 @@ __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
   const uint32_t meta = (uint32_t)a.cand_count[s] | ((uint32_t)md << 8) | ((a.forced[s] ? 1u : 0u) << 10) |
                         (sh << 11) | ((general ? 1u : 0u) << 16) | (turn << 17);
   const int64_t to = a.trans_off[s];
+  if (turn && a.flag_turn) a.flag_turn[o] = 5;  // the edge-state tiers (otr_edge1.h)
   a.rec[3 * o] = make_uint4((uint32_t)s, (uint32_t)sp, root, bmm);
   a.rec[3 * o + 1] = make_uint4(d0min, meta, (uint32_t)same, (uint32_t)(same >> 32));
   a.rec[3 * o + 2] = make_uint4(0u, (uint32_t)bt, (uint32_t)to, (uint32_t)((uint64_t)to >> 32));
@@ -1361,15 +1375,16 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     }
   }
   // general (flag 3): the global-memory search; overflow: retry with a bigger table (1); a
-  // first-tier search expected beyond its table starts in retry tier t (16 + t); turn modes
-  // (flag 5): the edge-state LDS search (otr_edge.h)
+  // first-tier search expected beyond its table starts in retry tier t (16 + t); turn modes:
+  // none here (k_tasks flagged them 5, for the edge-state tiers otr_edge1.h / otr_edge.h)
   if (have && !ok && !forced && lane == 0) {
     const uint32_t meta = a.rec[3 * task + 1].y;
     const bool general = ((meta >> 16) & 1u) != 0u, turn = ((meta >> 17) & 1u) != 0u;
 #ifdef OTR_FORCE_GENERAL
     a.overflow_flag[task] = 3;  // test build: every search (edge-state ones too) in k_general
 #else
-    a.overflow_flag[task] = turn ? 5 : (general ? 3 : (start_tier >= 0 ? 16 + start_tier : 1));
+    // (turn-mode tasks carry flag 5 from k_tasks, or belong to the multi-source tier)
+    if (!turn) a.overflow_flag[task] = general ? 3 : (start_tier >= 0 ? 16 + start_tier : 1);
 #endif
   }
 #ifdef OTR_STAMPS

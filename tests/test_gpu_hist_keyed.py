@@ -77,3 +77,16 @@ def test_device_output_and_edge_cases(workload):
     big['count'] = 0x7FFFFFFF
     assert np.array_equal(sr.hist_reduce(m, big, 3, memory='host'), oh.reduce(big))
     assert int(oh.reduce(big)['count'][0]) == 0xFFFFFFFF
+
+
+def test_owner_cull_trailing_singleton_equals_reference_loop(workload):
+    """The owner cull on crafted files (tests/test_hist_cull_cpu.py CRAFTED: trailing single-line
+    runs, string order != numeric order) on the device: the oracle's entries, and the pairs and
+    line counts the reference loop keeps (oracle/tiles.sort_and_cull)."""
+    from tests.test_hist_cull_cpu import CRAFTED, _pairs_from_entries, _pairs_from_lines, _rows
+    m = M.Matcher()
+    rows = _rows(CRAFTED)
+    for p in (2, 3):
+        got = sr.hist_reduce(m, rows, len(rows), privacy=p, rows_in=True, memory='host')
+        assert np.array_equal(got, oh.reduce(oh.entries_from_rows(rows), p))
+        assert _pairs_from_entries(got) == _pairs_from_lines(rows, p)

@@ -290,7 +290,8 @@ def test_semantics_gpu_parity(kat, slow, square, opts):
     errors, _ = compare(_lib.result_to_numpy(r), po.match_batch(po.Graph(qpath), b, po.params(**opts)))
     assert not errors, errors
     if opts.get('turn_penalty_factor', 1) != 0:
-        assert int(r.route_tier_work[9][0]) > 0  # turn modes: the edge-state search
+        # turn modes: the edge-state search (the multi-source tier, or the single-source ones)
+        assert int(r.route_tier_work[10][0]) + int(r.route_tier_work[9][0]) > 0
     spath, sid = slow
     M.configure(M.default_config(spath, **opts))
     b = K.batch([K.trace(p, dt=4) for p in K.slow_scenarios().values()])

@@ -1,0 +1,257 @@
+/*
+ * edge_stats.c — design statistics of the edge-state (turn-cost) route searches, on the
+ * CPU.  Includes the oracle's translation unit (TEST/ANALYSIS INFRASTRUCTURE ONLY, never
+ * the product) and simulates the GPU's exact-round search (otr_edge.h edge_search: IN
+ * criterion k < kmin + gap(state), early exit once every target is resolved) for every
+ * source candidate of every step of a trace sample, reporting what sizes the LDS tiers:
+ * table keys per search, settled states, rounds, and per step the union of the sources'
+ * states (what a multi-source search would hold).
+ *
+ * Build: gcc -O2 -shared -fPIC -o tools/libedgestats.so tools/edge_stats.c -lm -lpthread
+ * Use:   python tools/edge_stats.py
+ */
+#include "../oracle/oracle.c"
+
+typedef struct {
+  int64_t searches, keys, settled, rounds, rounds_tmin, settled_tmin, steps, union_keys, sum_keys, sources;
+  int64_t union_settle_events, sum_settle_events; /* (state, round) pairs: combined vs separate */
+  int64_t hist_keys[64];                          /* keys per search, 32-key buckets */
+  int64_t hist_union[64];                         /* union keys per step, 64-key buckets */
+  int64_t hist_rounds[64];                        /* rounds per search */
+  int64_t pend_max, max_rounds_sum, relaxed, groups;
+} es_stats;
+
+typedef struct {
+  uint32_t* stamp; /* per edge: generation of the search that touched it */
+  rkey* lab;
+  uint8_t* flag; /* 1 pending, 2 settled */
+  uint32_t* ustamp; /* per edge: step generation (union) */
+  uint64_t* umask;  /* per edge: rounds (< 64) in which some source of the step settled it */
+  uint32_t gen, ugen;
+  int64_t ukeys, uevents;
+  uint32_t* pend;
+  uint32_t* nxt;
+} es_ws;
+
+static const int64_t kInf = INT64_MAX / 4;
+
+static void es_touch(es_ws* W, uint32_t e) {
+  if (W->ustamp[e] != W->ugen) {
+    W->ustamp[e] = W->ugen;
+    W->umask[e] = 0;
+    W->ukeys++;
+  }
+}
+
+/* one simulated search; returns keys; *settled, *rounds out */
+static int64_t es_search(const rctx* X, es_ws* W, uint32_t ei, double pi, int ntg, const uint32_t* tv,
+                         const int64_t* tpart, const int64_t* tpt, const uint32_t* tej, int64_t tmin,
+                         int64_t* settled, int64_t* rounds, int64_t* relaxed, int64_t* pend_max, int record) {
+  const orc_graph* g = X->g;
+  const mode_data* md = X->md;
+  *settled = 0;
+  *rounds = 0;
+  const int64_t d0 = part_mm(1.0 - pi, g->len_mm[ei]);
+  const int64_t t0 = X->time_on ? part_mm(1.0 - pi, md->time_ds[ei]) : 0;
+  if (d0 > X->bmm || (X->time_on && t0 > X->bt)) return 0;
+  const int64_t pd = X->bmm - d0, pt = X->time_on ? X->bt - t0 : kInf;
+  W->gen++;
+  int64_t keys = 1;
+  uint32_t np = 0;
+  W->stamp[ei] = W->gen;
+  W->lab[ei] = (rkey){0, 0, 0};
+  W->flag[ei] = 1;
+  W->pend[np++] = ei;
+  if (record) es_touch(W, ei);
+  rkey tl[ORC_KMAX];
+  for (int j = 0; j < ntg; ++j) tl[j] = (rkey){kInf, kInf, kInf};
+  int64_t kmin = 0, dmin = 0;
+  for (;;) {
+    if (np == 0) break;
+    int unres = 0;
+    for (int j = 0; j < ntg; ++j) {
+      if (tv[j] == 0xFFFFFFFFu) continue;
+      const int res = (tl[j].k < kInf && tl[j].k < kmin + tpart[j] + tmin) || dmin + tpart[j] > pd;
+      if (!res) unres = 1;
+    }
+    if (!unres) break;
+    const int64_t r = *rounds;
+    ++*rounds;
+    int64_t knext = kInf, dnext = kInf;
+    uint32_t nf = 0, kept = 0;
+    for (uint32_t q = 0; q < np; ++q) {
+      const uint32_t b = W->pend[q];
+      const int64_t len = b == ei ? 0 : (int64_t)g->len_mm[b];
+      const int64_t mq = len >> 8 < 255 ? len >> 8 : 255;
+      const int64_t gap = (mq ? mq << 8 : 1) + (b == ei ? 0 : tmin);
+      if (W->lab[b].k < kmin + gap) W->nxt[nf++] = b;
+      else {
+        W->pend[kept++] = b;
+        if (W->lab[b].k < knext) knext = W->lab[b].k;
+        if (W->lab[b].d < dnext) dnext = W->lab[b].d;
+      }
+    }
+    np = kept;
+    for (uint32_t f = 0; f < nf; ++f) {
+      const uint32_t b = W->nxt[f];
+      W->flag[b] = 2;
+      ++*settled;
+      if (record && r < 64 && !(W->umask[b] >> r & 1)) {
+        W->umask[b] |= 1ull << r;
+        W->uevents++;
+      }
+      const rkey L = W->lab[b];
+      const uint32_t v = g->edge_dst[b];
+      for (int j = 0; j < ntg; ++j)
+        if (tv[j] == v) {
+          const int64_t c = md->turn[turn_degree(g, b, tej[j])];
+          rkey o = {L.k + tpart[j] + c, L.d + tpart[j], X->time_on ? L.t + tpt[j] : 0};
+          if (o.d <= pd && o.t <= pt && o.k - o.d <= ORC_TCCAP && rk_lt(o, tl[j])) tl[j] = o;
+        }
+      for (uint32_t e = g->node_row[v]; e < g->node_row[v + 1]; ++e) {
+        if (!(g->edge_attr[e] & md->mode_bit)) continue;
+        ++*relaxed;
+        const int64_t c = md->turn[turn_degree(g, b, e)];
+        rkey o = {L.k + g->len_mm[e] + c, L.d + g->len_mm[e], X->time_on ? L.t + md->time_ds[e] : 0};
+        if (!(o.d <= pd && o.t <= pt && o.k - o.d <= ORC_TCCAP)) continue;
+        if (W->stamp[e] != W->gen) {
+          W->stamp[e] = W->gen;
+          W->lab[e] = (rkey){kInf, kInf, kInf};
+          W->flag[e] = 0;
+          ++keys;
+          if (record) es_touch(W, e);
+        }
+        if (rk_lt(o, W->lab[e])) {
+          W->lab[e] = o;
+          if (o.k < knext) knext = o.k;
+          if (o.d < dnext) dnext = o.d;
+          if (W->flag[e] == 0) {
+            W->flag[e] = 1;
+            W->pend[np++] = e;
+          }
+        }
+      }
+    }
+    if (np > *pend_max) *pend_max = np;
+    kmin = knext;
+    dmin = dnext;
+  }
+  return keys;
+}
+
+int es_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int64_t* trace_off, const double* lat,
+           const double* lon, const int64_t* tms, int group, es_stats* S) {
+  memset(S, 0, sizeof(*S));
+  const uint32_t E = g->h.n_edges;
+  es_ws W;
+  memset(&W, 0, sizeof(W));
+  W.stamp = calloc(E + 1, 4);
+  W.lab = malloc(sizeof(rkey) * (E + 1));
+  W.flag = calloc(E + 1, 1);
+  W.ustamp = calloc(E + 1, 4);
+  W.umask = calloc(E + 1, 8);
+  W.pend = malloc(4 * (size_t)(E + 1));
+  W.nxt = malloc(4 * (size_t)(E + 1));
+  mode_data md;
+  mode_data_init(g, &p[0], 0, &md);
+  int64_t tmin = md.turn[0];
+  for (int i = 0; i <= 180; ++i)
+    if (md.turn[i] < tmin) tmin = md.turn[i];
+  const int kmax = p[0].max_candidates < ORC_KMAX ? p[0].max_candidates : ORC_KMAX;
+  static cand_t cands[4096][ORC_KMAX];
+  static int kc[4096], act[4096];
+  static int64_t sp[4096];
+  for (int32_t t = 0; t < n_traces; ++t) {
+    const int64_t b = trace_off[t], n = trace_off[t + 1] - b;
+    int ns = 0;
+    int64_t last = 0;
+    for (int64_t i = 0; i < n && ns < 4096; ++i) {
+      int st = i == 0 || i == n - 1 ||
+               gc_dist(lat[b + last], lon[b + last], lat[b + i], lon[b + i]) >= p[0].interpolation_distance;
+      if (st) {
+        last = i;
+        sp[ns++] = b + i;
+      }
+    }
+    int na = 0;
+    for (int s = 0; s < ns; ++s) {
+      double a = p[0].gps_accuracy;
+      double radius = p[0].search_radius > a ? p[0].search_radius : a;
+      if (radius > p[0].max_search_radius) radius = p[0].max_search_radius;
+      kc[s] = find_candidates(g, lat[sp[s]], lon[sp[s]], radius, md.mode_bit, kmax, cands[s]);
+      if (kc[s] > 0) act[na++] = s;
+    }
+    for (int k = 1; k < na; ++k) {
+      const int sa = act[k - 1], sb = act[k];
+      const double gcd = gc_dist(lat[sp[sa]], lon[sp[sa]], lat[sp[sb]], lon[sp[sb]]);
+      if (gcd > p[0].breakage_distance) continue;
+      rctx X;
+      step_ctx(&X, g, &md, &p[0], gcd, tms[sp[sb]] - tms[sp[sa]]);
+      uint32_t tv[ORC_KMAX], tej[ORC_KMAX];
+      int64_t tpart[ORC_KMAX], tpt[ORC_KMAX];
+      const int Kb = kc[sb];
+      W.ugen++;
+      W.ukeys = 0;
+      W.uevents = 0;
+      int64_t step_sum = 0, nsrc = 0, max_rounds = 0;
+      for (int i = 0; i < kc[sa]; ++i) {
+        const cand_t* ci = &cands[sa][i];
+        int need = 0;
+        for (int j = 0; j < Kb; ++j) {
+          const cand_t* cj = &cands[sb][j];
+          const int nd = !(cj->e == ci->e && cj->p >= ci->p);
+          tv[j] = nd ? g->edge_src[cj->e] : 0xFFFFFFFFu;
+          tej[j] = cj->e;
+          tpart[j] = part_mm(cj->p, g->len_mm[cj->e]);
+          tpt[j] = X.time_on ? part_mm(cj->p, md.time_ds[cj->e]) : 0;
+          need |= nd;
+        }
+        if (!need) continue;
+        if (group > 0 && nsrc > 0 && nsrc % group == 0) { /* a new group: its own union */
+          S->union_keys += W.ukeys;
+          S->union_settle_events += W.uevents;
+          S->hist_union[W.ukeys / 64 < 63 ? W.ukeys / 64 : 63]++;
+          S->groups++;
+          W.ugen++;
+          W.ukeys = 0;
+          W.uevents = 0;
+        }
+        int64_t st, rd, st2, rd2, rl = 0, rl2 = 0;
+        const int64_t keys =
+            es_search(&X, &W, ci->e, ci->p, Kb, tv, tpart, tpt, tej, 0, &st, &rd, &rl, &S->pend_max, 1);
+        (void)es_search(&X, &W, ci->e, ci->p, Kb, tv, tpart, tpt, tej, tmin, &st2, &rd2, &rl2, &S->pend_max, 0);
+        S->searches++;
+        S->keys += keys;
+        S->settled += st;
+        S->relaxed += rl;
+        S->rounds += rd;
+        S->settled_tmin += st2;
+        S->rounds_tmin += rd2;
+        S->sum_settle_events += st;
+        S->hist_keys[keys / 32 < 63 ? keys / 32 : 63]++;
+        S->hist_rounds[rd < 63 ? rd : 63]++;
+        step_sum += keys;
+        nsrc++;
+        if (rd > max_rounds) max_rounds = rd;
+      }
+      if (!nsrc) continue;
+      S->steps++;
+      S->sum_keys += step_sum;
+      S->union_keys += W.ukeys;
+      S->union_settle_events += W.uevents;
+      S->hist_union[W.ukeys / 64 < 63 ? W.ukeys / 64 : 63]++;
+      S->groups++;
+      S->sources += nsrc;
+      S->max_rounds_sum += max_rounds;
+    }
+  }
+  free(W.stamp);
+  free(W.lab);
+  free(W.flag);
+  free(W.ustamp);
+  free(W.umask);
+  free(W.pend);
+  free(W.nxt);
+  free(md.time_ds);
+  return 0;
+}
