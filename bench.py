@@ -10,9 +10,11 @@ Workload (N=1): SURVEY.md §8d config C2 — synthetic metro graph (1024x1024 st
 grid, ~1M nodes, ~3.5M directed edges, seed 2) and 10,000 traces x 100 probes at
 15 s sampling with sigma = 10 m noise (seed 2) = 1M probes, matched with the match_options
 generate_test_trace.py:44-52 sends (turn_penalty_factor 0) under the deployed
-max_route_time_factor 2 (Dockerfile:17).  N>1 (config C3 layout): N x 10,000 traces
-generated with one seed, sharded by int(sha1(uuid)[:3], 16) % N (simple_reporter.py:116),
-graph replicated per GPU, weak scaling.
+max_route_time_factor 2 (Dockerfile:17).  N>1: BASELINE config 3 (C3) — 1,000,000
+"veh%07d" uuids x 100 probes = 100M probes per step node-wide, sharded by
+int(sha1(uuid)[:3], 16) % N (simple_reporter.py:116), the graph replicated per GPU, each
+GPU matching its ~1M/N traces in device batches of --chunk-traces (strong scaling: the
+total is fixed), then the keyed histogram exchange.
 
 Besides the timed device-resident line the bench reports, for rank 0 at N=1:
   * roofline: the dominant route-search kernel of the workload (largest device time):
@@ -79,6 +81,11 @@ def route_bytes(work):
     return 24 * settled + 16 * relaxed + 8 * trans
 
 
+def local_ranks():
+    """Ranks of this job on this host (torch.distributed.run sets LOCAL_WORLD_SIZE)."""
+    return int(os.environ.get('LOCAL_WORLD_SIZE', os.environ.get('WORLD_SIZE', 1)))
+
+
 def usable_cores():
     """Host cores this process may use: its CPU affinity, capped by a cgroup CPU quota
     (cpu.max), which a shared GPU box sets below the machine's core count."""
@@ -125,8 +132,12 @@ def main():
                     help='matchers (one HIP stream + host thread each) sharing the batch; 2 overlaps one '
                          "stream's host syncs and kernel tails with the other's kernels (+1.6%% at C2) but "
                          'the two route launches then share the GPU, halving the per-launch roofline figure')
-    ap.add_argument('--workload', choices=['c2', 'c2dep', 'c3', 'c4', 'c5mix', 'c5'], default='c2',
-                    help='c2 (default, the headline): 100 probes @15 s, sigma 10 m; c2dep: the same traces '
+    ap.add_argument('--chunk-traces', type=int, default=125000,
+                    help='traces per device batch (a shard larger than this is matched in several batches per '
+                         'step; 125,000 = the N = 8 share of C3)')
+    ap.add_argument('--workload', choices=['c2', 'c2dep', 'c3', 'c4', 'c5mix', 'c5'], default=None,
+                    help='default: c2 at N = 1, c3 at N > 1.  c2 (the headline): 100 probes @15 s, sigma 10 m; '
+                         'c2dep: the same traces '
                          'matched with the deployed configuration only (what Batch.java requests get: mode '
                          'defaults, turn penalties auto 200 / bicycle 140 / pedestrian 100); c3: the C3 shard of '
                          '1M veh%%07d uuids x 100 probes this GPU owns; c4: 60 probes @60 s, sigma 50 m, '
@@ -153,6 +164,8 @@ def main():
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
+    if args.workload is None:  # the headline at N = 1; BASELINE config 3 across GPUs
+        args.workload = 'c2' if world == 1 else 'c3'
     import torch
     import torch.distributed as dist
     # OTR_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on one GPU
@@ -229,7 +242,8 @@ def main():
         if cap:
             mine_ids = mine_ids[:cap]
         mine = gen.make_traces_ids(gpath, mine_ids, W['points'], W['rate'], W['sigma'], W['seed'], W['bike'],
-                                   W['ped'], W['acc'], t_begin=T_BEGIN, t_spread=W.get('spread', 1800))
+                                   W['ped'], W['acc'], t_begin=T_BEGIN, t_spread=W.get('spread', 1800),
+                                   threads=max(1, min(16, usable_cores() // max(1, local_ranks()))))
     else:
         n_per = args.traces_per_gpu or W['traces']
         n_global = n_per * world
@@ -252,8 +266,12 @@ def main():
     # slice of this GPU's traces (reporter_service.py:51-52: one matcher per thread)
     from concurrent.futures import ThreadPoolExecutor
     ns = max(1, args.streams)
-    cuts = np.linspace(0, mine.n_traces, ns + 1).astype(np.int64)
-    parts = [mine.subset(np.arange(cuts[k], cuts[k + 1])) for k in range(ns)]
+    # device batches: contiguous slices of this GPU's traces, at most --chunk-traces each, at
+    # least one per stream; stream k matches batches k, k + ns, ... in turn
+    n_parts = max(ns, -(-mine.n_traces // max(1, args.chunk_traces)))
+    n_parts += (-n_parts) % ns
+    cuts = np.linspace(0, mine.n_traces, n_parts + 1).astype(np.int64)
+    parts = [mine.slice(int(cuts[k]), int(cuts[k + 1])) for k in range(n_parts)]
     matchers = [M.Matcher() for _ in range(ns)]
     dev = torch.device('cuda', local)
     # dense histogram hours: traces start within `spread` of T_BEGIN and last <= 100 min
@@ -262,6 +280,8 @@ def main():
         raise SystemExit('bench: the dense [hour][segment][speed] histogram of C5 would take %d GB; use --hist keyed'
                          % (hours * 60 * 8 * 4 // 1000))
     keyed = args.hist == 'keyed'
+    if not keyed and n_parts > ns:
+        raise SystemExit('bench: the dense histogram takes one device batch per stream; use --hist keyed')
     # the dense histogram's tensors exist only in dense mode (C5's would be 4 x 51 GB)
     hist_len = hours * n_segments * _lib.HIST_BINS if not keyed else world
     hist_len += (-hist_len) % world
@@ -284,40 +304,46 @@ def main():
     torch.cuda.synchronize()
 
     EW = _lib.HIST_ENTRY.itemsize
-    ebufs = [torch.zeros(0, dtype=torch.uint8, device=dev) for _ in range(ns)]  # per-stream local entries
-    n_local, n_rows, row_views = [0] * ns, [0] * ns, [None] * ns
+    ebufs = [torch.zeros(0, dtype=torch.uint8, device=dev) for _ in range(n_parts)]  # per-batch local entries
+    n_local, n_rows, row_views = [0] * n_parts, [0] * n_parts, [None] * n_parts
     hist_stats = {}
+    # one batch per stream on one GPU: its single owner reduces the rows themselves
+    rows_direct = keyed and world == 1 and n_parts == ns
 
-    def run_part(k, route_work=False):
-        r = matchers[k].match_batch(parts[k], device_arrays=darrs[k],
+    def run_one(k, j, route_work):
+        r = matchers[k].match_batch(parts[j], device_arrays=darrs[j],
                                     hist_device=None if keyed else hists[k].data_ptr(),
                                     hist_hours=0 if keyed else hours, hist_base_time=T_BEGIN, copy_out=False,
                                     timing=True, tile_rows=keyed or args.tiles > 0, route_work=route_work)
         if r.status != 0:
             raise RuntimeError('batch status %d (%d traces beyond every search tier)' % (r.status,
                                                                                           r.n_overflow_traces))
-        n_rows[k] = int(r.n_rows)
-        if keyed and world == 1:  # the only owner: its one reduce takes the rows themselves
-            row_views[k] = (torch.as_tensor(_DevBytes(r.d_rows, int(r.n_rows) * _lib.TILE_ROW.itemsize), device=dev)
+        n_rows[j] = int(r.n_rows)
+        if rows_direct:
+            row_views[j] = (torch.as_tensor(_DevBytes(r.d_rows, int(r.n_rows) * _lib.TILE_ROW.itemsize), device=dev)
                             if int(r.n_rows) > 0 else torch.zeros(0, dtype=torch.uint8, device=dev))
-        elif keyed:  # this GPU's (file, pair, speed bin) counts, on the matcher's stream
-            if ebufs[k].numel() < int(r.n_rows) * EW:
-                ebufs[k] = torch.empty(int(r.n_rows) * EW * 5 // 4 + EW, dtype=torch.uint8, device=dev)
-            n_local[k] = sr.hist_reduce(matchers[k], r.d_rows, r.n_rows, privacy=1, rows_in=True,
-                                        out=ebufs[k].data_ptr())
+        elif keyed:  # this batch's (file, pair, speed bin) counts, on the matcher's stream
+            if ebufs[j].numel() < int(r.n_rows) * EW:
+                ebufs[j] = torch.empty(int(r.n_rows) * EW * 5 // 4 + EW, dtype=torch.uint8, device=dev)
+            n_local[j] = sr.hist_reduce(matchers[k], r.d_rows, r.n_rows, privacy=1, rows_in=True,
+                                        out=ebufs[j].data_ptr())
         if args.tiles > 0:
             tc = time.perf_counter()
             kept = sr.cull_rows(matchers[k], None, args.tiles, device_ptr=r.d_rows, n=r.n_rows)
             tile_stats.append((int(r.n_rows), len(kept), time.perf_counter() - tc))
         return r
 
+    def run_part(k, route_work=False):
+        # (each result keeps its own counters and times; its rows were consumed in run_one)
+        return [run_one(k, j, route_work) for j in range(k, n_parts, ns)]
+
     owned = {'buf': torch.zeros(0, dtype=torch.uint8, device=dev), 'n': 0}
 
     def keyed_exchange():
-        """§8e: the streams' entries → all-to-all by (hour, tile) owner → the owner's
+        """§8e: the batches' entries → all-to-all by (hour, tile) owner → the owner's
         merge + privacy cull (one more sort-reduce, on the first matcher's stream)."""
         torch.cuda.synchronize()
-        if world == 1:
+        if rows_direct:
             rows = torch.cat(row_views)
             n_in = rows.numel() // _lib.TILE_ROW.itemsize
             if owned['buf'].numel() < max(n_in, 1) * EW:
@@ -326,11 +352,15 @@ def main():
                                         out=owned['buf'].data_ptr())
             hist_stats.update(rows=int(sum(n_rows)), owned=int(owned['n']))
             return
-        local_e = torch.cat([ebufs[k][:n_local[k] * EW] for k in range(ns)])
+        local_e = torch.cat([ebufs[j][:n_local[j] * EW] for j in range(n_parts)])
         if world > 1:
+            tx = time.perf_counter()
             send = local_e if backend == 'nccl' else local_e.cpu()
             recv = sr.exchange_hist(send, world)
             recv = recv if recv.is_cuda else recv.to(dev)
+            torch.cuda.synchronize()
+            hist_stats.update(exchange_ms=round(1e3 * (time.perf_counter() - tx), 3),
+                              exchange_bytes_sent=int(local_e.numel()), exchange_bytes_received=int(recv.numel()))
         else:
             recv = local_e
         n_in = recv.numel() // EW
@@ -343,7 +373,7 @@ def main():
 
     def step(route_work=False):
         hist_stats.clear()
-        rs = list(pool.map(lambda k: run_part(k, route_work), range(ns)))
+        rs = [r for rk in pool.map(lambda k: run_part(k, route_work), range(ns)) for r in rk]
         if keyed:
             keyed_exchange()
             torch.cuda.current_stream().synchronize()
@@ -397,7 +427,7 @@ def main():
             if int(r.route_tier_code[t]) != 0:
                 w = work_of.setdefault(t, np.zeros(4, np.int64))
                 w += np.array([int(x) for x in r.route_tier_work[t]], np.int64)
-    stage_ms = {s: round(float(np.mean([r.kernel_ms[i] for r in rs])), 3) for i, s in enumerate(_lib.STAGES)
+    stage_ms = {s: round(float(np.sum([r.kernel_ms[i] for r in rs])) / ns, 3) for i, s in enumerate(_lib.STAGES)
                 if rs[0].kernel_ms[i] > 0}
     tiers = {}
     for step_rs in results:
@@ -410,7 +440,7 @@ def main():
                 d['launches'] += 1
                 d['ms'] += float(r.route_tier_ms[t])
     for t, d in tiers.items():  # per-launch work of the instrumented step, times the launches
-        d['work'] = work_of.get(t, np.zeros(4, np.int64)) * (d['launches'] // max(1, ns))
+        d['work'] = work_of.get(t, np.zeros(4, np.int64)) * (d['launches'] // max(1, n_parts))
     dom_t = max(tiers, key=lambda t: tiers[t]['ms'])
     dom = tiers[dom_t]
     launch_ms = dom['ms'] / dom['launches']
@@ -457,9 +487,14 @@ def main():
                              sample.n_traces, W['points'], args.workload.upper(),
                              (' (rank 0 shard of %d)' % world) if world > 1 else '', threads, os.cpu_count() or 0,
                              dt)}
-        # the GPU output of the same traces: this batch (copy-out run, untimed), sliced
-        got_full = _lib.result_to_numpy(M.Matcher().match_batch(mine, copy_out=True))
-        errors, stats = compare(subset(got_full, idx, mine.offsets), want)
+        # the GPU output of the same traces (copy-out run, untimed): the whole batch when it
+        # is one device batch, else the sample's traces alone (traces are matched independently)
+        if n_parts == 1:
+            got_full = _lib.result_to_numpy(M.Matcher().match_batch(mine, copy_out=True))
+            got = subset(got_full, idx, mine.offsets)
+        else:
+            got = _lib.result_to_numpy(M.Matcher().match_batch(sample, copy_out=True))
+        errors, stats = compare(got, want)
         parity = {'traces': int(sample.n_traces), 'probes': int(sample.n_probes), 'ok': not errors,
                   'segments': stats.get('n_seg'), 'reports': stats.get('n_rep'), 'errors': errors[:3],
                   'floats_bitexact': all(v for k, v in stats.items() if k.endswith('_bitexact'))}
@@ -536,7 +571,7 @@ def main():
             'warmup': args.warmup,
             'ms_per_step': round(1e3 * elapsed / args.steps, 3),
             'higher_is_better': True,
-            'scaling': 'weak',
+            'scaling': 'strong' if args.workload == 'c3' and not args.traces_per_gpu else 'weak',
             'vs_baseline': None,
             'dtype': 'f64',
             'data': 'synthetic',
@@ -564,6 +599,7 @@ def main():
                        'histogram': ({'kind': 'keyed (SURVEY 8e)', 'privacy': args.privacy, **hist_stats}
                                      if keyed else {'kind': 'dense [hour][segment][speed]'}),
                        'streams': ns,
+                       'device_batches': n_parts,
                        'stage_ms_per_stream': stage_ms,
                        'route_kernels': tier_table,
                        'tile_stage': ({'privacy': args.tiles, 'rows': tile_stats[-1][0], 'kept': tile_stats[-1][1],

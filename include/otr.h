@@ -206,6 +206,7 @@ typedef struct otr_batch_result {
   uint64_t route_tier_work[12][4];
 } otr_batch_result;
 
+/* At most 2^26 (67,108,864) probes per call (OTR_BAD_REQUEST beyond: split the input). */
 int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result* out);
 
 /* simple_reporter's tile stage (simple_reporter.py:211-239) on device: sort the rows

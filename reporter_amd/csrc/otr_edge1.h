@@ -20,19 +20,24 @@
 //   * probe loops are not unrolled, the target map is consulted only when a 64-bit bloom
 //     of the target nodes (a wave-uniform register) admits the settled node, and the
 //     wave's scalar state is kept small (no SGPR spills);
-//   * small tables: the first tier holds CAP states (table + lists + targets + the turn
-//     table in ~7 KB at 256: 22 waves per CU); a search that outgrows it goes on to the
-//     next tier (flag 6, the single-source tiers of otr_edge.h), with the same results.
+//   * small tables: the first tier holds 256 states (table + lists + targets + the turn
+//     table in 7.3 KB: 21 waves per CU, 80 % of the C2 searches); a search that outgrows it
+//     goes on to 1024 states (this kernel again), then 2048 (otr_edge.h), same results.
 #pragma once
 #include "otr_medge.h"
 
 namespace otr {
 
+// waves per SIMD the compiler fits the kernel's registers for (8: 64 VGPRs)
+#ifndef OTR_E1WAVES
+#define OTR_E1WAVES 8
+#endif
+
 template <int CAP>
 struct E1Lds {
   static constexpr int TG = 32;   // targets (steps with more go to otr_edge.h's TG = 64 tier)
-  static constexpr int TM = 64;   // target-node map slots
-  static constexpr int WCAP = CAP <= 256 ? 40 : 96;  // states settled per round (the rest wait)
+  static constexpr int TM = 32;   // target-node map slots (a target node per target at most)
+  static constexpr int WCAP = CAP <= 256 ? 32 : 64;  // states settled per round (the rest wait)
   using Idx = typename std::conditional<(CAP <= 256), uint8_t, uint16_t>::type;
   unsigned long long lab[CAP];  // gpack label, kGInf: none
   uint32_t key[CAP];            // edge id | kInq (on the pending list, or settled); kEmpty
@@ -54,7 +59,8 @@ struct E1Lds {
   int n_pend, n_keys, overflow;
 };
 
-__device__ inline uint32_t tm_home(uint32_t v) { return (v * 0x9E3779B1u) >> 26; }  // 64 slots
+__device__ inline uint32_t tm_home(uint32_t v) { return (v * 0x9E3779B1u) >> 26; }  // 64 bloom bits
+__device__ inline uint32_t tm_slot(uint32_t v) { return (v * 0x9E3779B1u) >> 27; }  // 32 map slots
 
 template <int CAP>
 __device__ inline int e1_insert(E1Lds<CAP>& L, uint32_t e, bool& isnew) {
@@ -76,7 +82,7 @@ __device__ inline int e1_insert(E1Lds<CAP>& L, uint32_t e, bool& isnew) {
 template <int CAP>
 __device__ inline void e1_target_offers(E1Lds<CAP>& L, unsigned long long lb, uint32_t hbk, uint32_t v, uint32_t pd,
                                         uint32_t pt) {
-  uint32_t h = tm_home(v), m = 0;
+  uint32_t h = tm_slot(v), m = 0;
 #pragma unroll 1
   for (int probe = 0; probe < E1Lds<CAP>::TM; ++probe) {
     const uint32_t k = L.tm_node[h];
@@ -145,10 +151,12 @@ __device__ inline void e1_turn_table(E1Lds<CAP>& L, const int32_t* turn_tab, int
 // K3e1 kernel: a persistent grid over the device-side list of the turn-mode tasks (one
 // source candidate each), the 8 XCDs taking contiguous eighths of the list (consecutive
 // tasks = the candidates of one step, then the next steps of the trace: one neighbourhood).
-// A search that outgrows the table flags its task 6 (otr_edge.h's larger tables).
+// A search that outgrows the table flags its task for the next tier: 6 (this kernel with
+// 1024 states), 7 (otr_edge.h's 2048-state table).
 // ------------------------------------------------------------------------------
 template <int CAP>
-__global__ __launch_bounds__(64) void k_route_e1(DevGraph gr, RouteArgs a, unsigned long long* counters) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES, 8))) void k_route_e1(
+    DevGraph gr, RouteArgs a, unsigned long long* counters) {
   using LT = E1Lds<CAP>;
   constexpr int TG = LT::TG, TM = LT::TM, WCAP = LT::WCAP;
   constexpr int kMaxKeys = (CAP * 7) / 8;
@@ -195,8 +203,10 @@ __global__ __launch_bounds__(64) void k_route_e1(DevGraph gr, RouteArgs a, unsig
     // ---- reset: keys, targets, the target map and its bloom
     for (int k = lane; k < CAP; k += OTR_WAVE) L.key[k] = kEmpty;
     if (lane < TG) L.tlab[lane] = kGInf;
-    L.tm_node[lane] = kEmpty;
-    L.tm_mask[lane] = 0u;
+    if (lane < TM) {
+      L.tm_node[lane] = kEmpty;
+      L.tm_mask[lane] = 0u;
+    }
     if (lane == 0) {
       L.overflow = 0;
       L.bloom = 0ull;
@@ -207,7 +217,7 @@ __global__ __launch_bounds__(64) void k_route_e1(DevGraph gr, RouteArgs a, unsig
       L.tpart[lane] = tpart;
       L.tpt[lane] = tpt;
       L.thb[lane] = (uint16_t)gr.edge_head[ej].x;
-      uint32_t h = tm_home(tv);
+      uint32_t h = tm_slot(tv);
 #pragma unroll 1
       for (int probe = 0; probe < TM; ++probe) {
         const uint32_t k = atomicCAS(&L.tm_node[h], kEmpty, tv);
@@ -298,11 +308,14 @@ __global__ __launch_bounds__(64) void k_route_e1(DevGraph gr, RouteArgs a, unsig
             const unsigned long long lb = L.wlab[k >> 2];
             const uint32_t v = L.node[sl], hbk = L.hbk[sl];
             const int slot = k & 3;
-            const uint4 r = ld16(er + 4 * (size_t)v + slot);
+            // the record load is issued first and waited for only after the target offers
+            // (LDS work), so the two latencies overlap
+            uint4 r = er[4 * (size_t)v + slot];
             if (slot == 0) {
               ++my_settled;
               if ((bloom >> tm_home(v)) & 1ull) e1_target_offers(L, lb, hbk, v, pd, pt);
             }
+            asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w));  // (one 16-B load, not split)
             psl = e1_relax(L, lb, hbk, r.x & ~kAdjMore, r.y, timed ? er_t(r) : 0u, er_edge(r), er_hb(r), er_he(r), pd,
                            pt, mode_bit, my_relaxed, knext, dnext, isnew);
             tail = tail || (slot == 3 && (r.x & kAdjMore));
@@ -392,7 +405,7 @@ __global__ __launch_bounds__(64) void k_route_e1(DevGraph gr, RouteArgs a, unsig
         }
       }
     } else if (lane == 0) {
-      a.overflow_flag[task] = 6;  // the larger single-source tables (otr_edge.h)
+      a.overflow_flag[task] = CAP <= 256 ? 6 : 7;  // the next table: 1024 states, then 2048 (otr_edge.h)
     }
     __syncthreads();
   }

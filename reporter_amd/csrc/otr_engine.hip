@@ -369,6 +369,8 @@ int engine_configure(const Config& cfg, std::string* err) {
 // ---------------------------------------------------------------------------------
 // workspace slots
 // ---------------------------------------------------------------------------------
+constexpr int64_t kMaxBatchProbes = 1ll << 26;  // otr_match_batch (include/otr.h)
+
 enum Slot {
   S_TRACE_OFF, S_LAT, S_LON, S_TIME, S_ACC, S_MODE,
   S_STATE_CNT, S_TRACE_STATE_OFF, S_STATE_PROBE, S_STATE_TRACE,
@@ -652,6 +654,13 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     b.acc = in->accuracy;
   }
   out->n_probes = N;
+  // one wave per state in the per-state kernels: a dispatch counts its work-items in 32
+  // bits, so a batch holds at most 2^26 probes (callers split larger inputs; the JSON
+  // service batches at 16M)
+  if (N > kMaxBatchProbes) {
+    if (err) *err = "batch of " + std::to_string(N) + " probes: at most 67108864 per otr_match_batch call";
+    return OTR_BAD_REQUEST;
+  }
   h_trace_status.assign(T, OTR_OK);
   // counter banks of OTR_COUNTERS kinds x kCShards: 0 the batch (and the first route
   // tier), 1 the 384-state edge tier, 2..6 the LDS retry tiers, 7 the 64-bit tier, 8..9 the
@@ -959,15 +968,20 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     }
 #endif
     tb(OTR_STAGE_ROUTE);
-    if (node_tasks && route_g == 2) {
-      const int64_t units = (NT + 1) / 2;
-      const unsigned grid = (unsigned)(8 * ((units + 7) / 8));
-      OTR_ROUTE_LAUNCH(OTR_CAP1, 2, false, grid, ra, rwork);
-      out->route_tier_code[0] = OTR_CAP1 * 10 + 2;
-    } else if (node_tasks) {
-      const unsigned grid = (unsigned)(8 * ((NT + 7) / 8));
-      OTR_ROUTE_LAUNCH(256, 1, false, grid, ra, rwork);
-      out->route_tier_code[0] = 2561;
+    if (node_tasks) {
+      // one unit (G searches) per block, in launches of at most 2^25 blocks: a dispatch's
+      // grid size counts work-items in 32 bits (178M tasks at 12.5M probes would wrap)
+      const int64_t units = route_g == 2 ? (NT + 1) / 2 : NT;
+      constexpr int64_t kMaxUnits = 1ll << 25;
+      for (int64_t base = 0; base < units; base += kMaxUnits) {
+        RouteArgs rf = ra;
+        rf.unit_base = base;
+        const int64_t u = std::min<int64_t>(kMaxUnits, units - base);
+        const unsigned grid = (unsigned)(8 * ((u + 7) / 8));
+        if (route_g == 2) OTR_ROUTE_LAUNCH(OTR_CAP1, 2, false, grid, rf, rwork);
+        else OTR_ROUTE_LAUNCH(256, 1, false, grid, rf, rwork);
+      }
+      out->route_tier_code[0] = route_g == 2 ? OTR_CAP1 * 10 + 2 : 2561;
     }
     te(OTR_STAGE_ROUTE);
     // overflow retries with larger LDS tables (same results, fewer resident waves): each
@@ -1041,14 +1055,14 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       if (timing) (void)hipEventRecord(ev[24 + 2 * 8 + 1], stream);
     }
 #endif
-    // edge-state tiers (turn-cost modes): the lean first tier (flag 5, otr_edge1.h, slot
-    // 10), then the 768- and 2048-state tables (flags 6, 7: otr_edge.h, slots 9 / 11); what
-    // outgrows those (flag 3) goes on below
+    // edge-state tiers (turn-cost modes): the lean tier at 256 states (flag 5, otr_edge1.h,
+    // slot 10), at 1024 (flag 6, slot 9), then the 2048-state table (flag 7, otr_edge.h, slot
+    // 11); what outgrows those (flag 3) goes on below
     if (turns) {
       for (int et = 0; et < 3; ++et) {
         const int slot = et == 0 ? 10 : (et == 1 ? 9 : 11);
         out->route_tier_code[slot] = et == 0 ? 6000000 + OTR_E1CAP * 100 + 32
-                                             : 7000000 + (et == 1 ? OTR_ECAP : 2048) * 100 + (et == 2 || !k32 ? 64 : 32);
+                                             : (et == 1 ? 6000000 + 1024 * 100 + 32 : 7000000 + 2048 * 100 + 64);
         unsigned long long* c = cnt + (et == 0 ? 23 : 24 + et);
         k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x20u << et, list, c);
         RouteArgs rb = ra;
@@ -1056,10 +1070,11 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         rb.list_count = c;
         unsigned long long* rcn = rwork ? d_counters + (et == 0 ? 10 : (et == 1 ? 1 : 11)) * bank : nullptr;
         if (timing) (void)hipEventRecord(ev[24 + 2 * slot], stream);
-        // persistent grids: every resident wave (~22 per CU at 256 states, 9 at 768, 3 at 2048)
+        // persistent grids: every resident wave (~23 per CU at 256 states, 6 at 1024, 3 at
+        // 2048); steps with more than 32 targets (modes keeping > 32 candidates) skip the
+        // lean tiers (their TG = 32) for the 64-target table
         if (et == 0) k_route_e1<OTR_E1CAP><<<8192, 64, 0, stream>>>(g, rb, rcn);
-        else if (et == 1 && k32) k_route_edge<OTR_ECAP, 32><<<4096, 64, 0, stream>>>(g, rb, rcn);
-        else if (et == 1) k_route_edge<OTR_ECAP, 64><<<4096, 64, 0, stream>>>(g, rb, rcn);
+        else if (et == 1) k_route_e1<1024><<<4096, 64, 0, stream>>>(g, rb, rcn);
         else k_route_edge<2048, 64><<<1024, 64, 0, stream>>>(g, rb, rcn);
         if (timing) (void)hipEventRecord(ev[24 + 2 * slot + 1], stream);
       }
@@ -1361,6 +1376,34 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   HIPCHK(hipMemcpyAsync(rep_n.data(), sa.rep_n, 8 * T, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipMemcpyAsync(way_n.data(), sa.way_n, 8 * T, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
+  if (h_fail[0] + h_fail[1] > 0 && getenv("OTR_DEBUG_FAIL")) {  // diagnostic: which stage, which tiers
+    unsigned long long hc2[32];
+    HIPCHK(hipMemcpy(hc2, cnt, 8 * 32, hipMemcpyDeviceToHost));
+    fprintf(stderr, "otr: %llu route tasks, %llu paths beyond every tier; tier lists:", h_fail[0], h_fail[1]);
+    for (int k = 0; k < 32; ++k) fprintf(stderr, " %llu", hc2[k]);
+    fprintf(stderr, "\n");
+    if (h_fail[1]) {  // the first failing winner paths: state, its step's bound and winning route
+      const int64_t* steps_d = need<int64_t>(S_LIST2, 1);
+      std::vector<int64_t> ks(std::min<unsigned long long>(h_fail[1], 6));
+      HIPCHK(hipMemcpy(ks.data(), list, 8 * ks.size(), hipMemcpyDeviceToHost));
+      for (int64_t k : ks) {
+        int64_t s = 0, sp = 0, to = 0;
+        int32_t wi = 0, wj = 0, K = 0;
+        double bd = 0;
+        HIPCHK(hipMemcpy(&s, steps_d + k, 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&sp, sb.prev + s, 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&wj, need<int32_t>(S_WINNER, 1) + s, 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&wi, need<int32_t>(S_WINNER, 1) + sp, 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&K, cb.count + s, 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&to, trans_off + s, 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&bd, sb.bound + s, 8, hipMemcpyDeviceToHost));
+        uint32_t r = 0;
+        HIPCHK(hipMemcpy(&r, trans + to + (int64_t)wi * K + wj, 4, hipMemcpyDeviceToHost));
+        fprintf(stderr, "otr: step k %lld state %lld prev %lld winners %d/%d K %d trans_off %lld bound %.3f route %u\n",
+                (long long)k, (long long)s, (long long)sp, wi, wj, K, (long long)to, bd, r);
+      }
+    }
+  }
   if (h_fail[0] + h_fail[1] > 0) {
     // beyond a 1M-state slab (never seen): name the traces (task/step -> state -> trace)
     for (int which = 0; which < 2; ++which) {

@@ -1069,6 +1069,7 @@ struct RouteArgs {
   float est_v[OTR_MODES];     // m/s: the mode's typical speed (50 km/h, capped by the mode's)
   uint32_t tier_keys[8];      // key capacity of each retry tier, in order
   int n_tiers;
+  int64_t unit_base;          // first tier: the launch's first unit (launches of < 2^32 work-items)
   int force_edge;             // test build only (OTR_FORCE_RETRY): bit 0 every multi-source edge group
                               // fails, bit 1 every 384-state edge search, bit 2 every 2048-state one
 };
@@ -1434,8 +1435,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   uint32_t* sink = WIDE ? nullptr : sink_row;
 #endif
   if (!LIST) {  // the first tier: one unit per block, XCD-mapped (no loop: fewer live registers)
+    // units [unit_base, unit_base + gridDim.x): a launch's grid stays below 2^32 work-items
+    // (the dispatch packet's grid size), so a large batch is several launches
     const int64_t n_units = (a.n_tasks + G - 1) / G;
-    const int64_t w = xcd_remap(blockIdx.x, (n_units + 7) / 8);
+    const int64_t w = a.unit_base + xcd_remap(blockIdx.x, (int64_t)gridDim.x / 8);
     if (w < n_units) route_unit<CAP, G, LIST, WIDE, CNT>(gr, a, counters, Ls, w, a.n_tasks, sink, trec);
     return;
   }

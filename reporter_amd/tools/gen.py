@@ -86,6 +86,15 @@ class Traces:
     def n_probes(self):
         return int(self.offsets[-1])
 
+    def slice(self, a, b):
+        """The contiguous traces a..b-1 (views where possible)."""
+        q0, q1 = int(self.offsets[a]), int(self.offsets[b])
+        off = self.offsets[a:b + 1] - q0
+        acc = None if self.accuracy is None else self.accuracy[q0:q1]
+        tr = None if self.truth is None else self.truth[q0:q1]
+        uu = None if self.uuids is None else self.uuids[a:b]
+        return Traces(self.lat[q0:q1], self.lon[q0:q1], self.time[q0:q1], off, self.mode[a:b], acc, tr, uu)
+
     def subset(self, idx):
         idx = np.asarray(idx, dtype=np.int64)
         parts = [np.arange(self.offsets[i], self.offsets[i + 1]) for i in idx]
@@ -128,9 +137,10 @@ def make_traces(graph, n_traces, n_points, sample_rate, sigma, seed, frac_bicycl
 
 
 def make_traces_ids(graph, ids, n_points, sample_rate, sigma, seed, frac_bicycle=0.0, frac_ped=0.0,
-                    point_accuracy=None, t_begin=T_BEGIN, t_spread=86400 * 7):
+                    point_accuracy=None, t_begin=T_BEGIN, t_spread=86400 * 7, threads=1):
     """Traces of the vehicles numbered `ids` ("veh%07d" uuids), each drawn from its own
-    generator (seed, id): a uuid shard of a fleet is generated without the rest (C3)."""
+    generator (seed, id): a uuid shard of a fleet is generated without the rest (C3).
+    threads > 1: slices of `ids` generated concurrently (the same traces: per-id seeds)."""
     ids = np.ascontiguousarray(ids, np.int64)
     n_traces = len(ids)
     n = n_traces * n_points
@@ -140,13 +150,28 @@ def make_traces_ids(graph, ids, n_points, sample_rate, sigma, seed, frac_bicycle
     mode = np.zeros(n_traces, np.uint8)
     truth = np.zeros(n, np.uint32)
     P = ctypes.POINTER
-    rc = lib().otrgen_traces_ids(graph.encode(), n_traces, ids.ctypes.data_as(P(ctypes.c_int64)), n_points,
-                                 sample_rate, sigma, seed, frac_bicycle, frac_ped,
-                                 lat.ctypes.data_as(P(ctypes.c_double)), lon.ctypes.data_as(P(ctypes.c_double)),
-                                 tm.ctypes.data_as(P(ctypes.c_int64)), mode.ctypes.data_as(P(ctypes.c_uint8)),
-                                 truth.ctypes.data_as(P(ctypes.c_uint32)), int(t_begin), int(t_spread))
-    if rc != 0:
-        raise RuntimeError('otrgen_traces_ids failed: %d' % rc)
+
+    def run(a, b):
+        if b <= a:
+            return 0
+        q = a * n_points
+        return lib().otrgen_traces_ids(graph.encode(), b - a, ids[a:].ctypes.data_as(P(ctypes.c_int64)), n_points,
+                                       sample_rate, sigma, seed, frac_bicycle, frac_ped,
+                                       lat[q:].ctypes.data_as(P(ctypes.c_double)),
+                                       lon[q:].ctypes.data_as(P(ctypes.c_double)),
+                                       tm[q:].ctypes.data_as(P(ctypes.c_int64)),
+                                       mode[a:].ctypes.data_as(P(ctypes.c_uint8)),
+                                       truth[q:].ctypes.data_as(P(ctypes.c_uint32)), int(t_begin), int(t_spread))
+    nt = max(1, min(int(threads), n_traces // 1000 + 1))
+    cuts = np.linspace(0, n_traces, nt + 1).astype(np.int64)
+    if nt == 1:
+        rcs = [run(0, n_traces)]
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=nt) as ex:
+            rcs = list(ex.map(run, cuts[:-1].tolist(), cuts[1:].tolist()))
+    if any(rc != 0 for rc in rcs):
+        raise RuntimeError('otrgen_traces_ids failed: %s' % rcs)
     off = np.arange(n_traces + 1, dtype=np.int64) * n_points
     acc = None if point_accuracy is None else np.full(n, float(point_accuracy), np.float32)
     return Traces(lat, lon, tm, off, mode, acc, truth, ['veh%07d' % int(i) for i in ids])

@@ -75,3 +75,28 @@ def test_full_size_config(name, graph_dir):
     errors, stats = compare(subset(got, idx, tr.offsets), want)
     assert not errors, errors
     assert stats['n_seg'] > 0 and stats['n_rep'] > 0
+
+
+def test_c3_shard_in_one_batch(graph_dir):
+    """The C3 N = 8 share in ONE device batch (125,000 traces, 12.5M probes, ~178M route tasks):
+    more first-tier units than one dispatch can address (its grid size counts work-items in
+    32 bits), so the first tier runs as several launches.  Every trace must match (status 0)
+    and an evenly spread sample equals the oracle; a batch beyond 2^26 probes is refused."""
+    import hashlib
+    path = gen.graph_path('metro', graph_dir)
+    opts = dict(GTT, search_radius=50, gps_accuracy=16.45)
+    M.configure(M.default_config(path, **opts))
+    ids = np.array([u for u in range(1000000) if int(hashlib.sha1(('veh%07d' % u).encode()).hexdigest()[:3], 16) % 8 == 0])
+    tr = gen.make_traces_ids(path, ids[:125000], 100, 15, 10.0, 3, 0.0, 0.0, None, t_begin=gen.T_BEGIN, t_spread=1800,
+                             threads=16)
+    m = M.Matcher()
+    r = m.match_batch(tr, copy_out=False, route_work=True)
+    assert r.status == 0 and r.n_overflow_traces == 0
+    assert int(r.counters[5]) > (1 << 25) * 2  # route tasks: more than one first-tier launch holds
+    assert int(r.route_tier_work[0][0]) > (1 << 26)  # and the first tier searched them (not a quarter)
+    idx = np.linspace(0, tr.n_traces - 1, 60).astype(np.int64)
+    sample = tr.subset(idx)
+    got = _lib.result_to_numpy(M.Matcher().match_batch(sample, copy_out=True))
+    want = po.match_batch(po.Graph(path), sample, po.params(**opts), threads=16)
+    errors, _ = compare(got, want)
+    assert not errors, errors

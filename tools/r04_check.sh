@@ -19,3 +19,8 @@ if [ "$T" = tests ]; then
   echo tests $?
   tail -5 $O/pytest.log
 fi
+if [ "$T" = n2 ] || [ "$T" = tests ]; then
+  OTR_BENCH_BACKEND=gloo timeout -k 10 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 2 > $O/c3_n2_gloo.json 2> $O/c3_n2_gloo.err
+  echo c3_n2 $?
+fi
