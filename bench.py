@@ -371,12 +371,17 @@ def main():
         hist_stats.update(rows=int(sum(n_rows)), local_entries=int(sum(n_local)), received=int(n_in),
                           owned=int(owned['n']))
 
+    split = {}
+
     def step(route_work=False):
         hist_stats.clear()
+        t0 = time.perf_counter()
         rs = [r for rk in pool.map(lambda k: run_part(k, route_work), range(ns)) for r in rk]
+        t1 = time.perf_counter()
         if keyed:
             keyed_exchange()
             torch.cuda.current_stream().synchronize()
+            split.update(match=round(1e3 * (t1 - t0), 3), histogram=round(1e3 * (time.perf_counter() - t1), 3))
             return rs
         torch.sum(torch.stack(hists), dim=0, out=hist)  # combine the per-stream histograms
         if world > 1 and backend == 'nccl':
@@ -399,6 +404,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
+    timed_split = dict(split)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     probes = torch.tensor([float(mine.n_probes)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -601,6 +607,9 @@ def main():
                        'streams': ns,
                        'device_batches': n_parts,
                        'stage_ms_per_stream': stage_ms,
+                       # host wall time of the last timed step: the matcher calls (kernels, their
+                       # host syncs and copies) and the keyed histogram reduce / exchange
+                       'step_wall_ms': timed_split,
                        'route_kernels': tier_table,
                        'tile_stage': ({'privacy': args.tiles, 'rows': tile_stats[-1][0], 'kept': tile_stats[-1][1],
                                        'ms': round(1e3 * tile_stats[-1][2], 3)} if tile_stats else None),

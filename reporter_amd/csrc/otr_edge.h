@@ -422,8 +422,8 @@ __global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, uns
                                          Kb, tv, tpart, tpt, thb, counters ? &settled : nullptr,
                                          counters ? &relaxed : nullptr) &&
                     Kb <= TG
-#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 1 / 2 fails every 384 / 2048-state search
-                    && !(a.force_edge & (CAP < 2048 ? 2 : 4))
+#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 2 fails every 2048-state search (k_general takes them)
+                    && !(CAP >= 2048 && (a.force_edge & 4))
 #endif
         ;
     if (ok) {
@@ -501,8 +501,11 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
     const uint32_t thb = (uint32_t)gr.edge_head[ej].x;
     e_init(L);
     e_turn_table(L, turn_tab, md);
-    const bool ok = edge_search<CAP, 32>(L, gr, md, true, ei, gr.edge_dst[ei], pd, pt, bt >= 0, 1, ct.y, ct.x,
-                                         tpt, thb, nullptr, nullptr);
+    bool ok = edge_search<CAP, 32>(L, gr, md, true, ei, gr.edge_dst[ei], pd, pt, bt >= 0, 1, ct.y, ct.x,
+                                   tpt, thb, nullptr, nullptr);
+#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 3 / 4 fails every 384 / 2048-state winner path
+    if (a.force_edge & (CAP < 2048 ? 8 : 16)) ok = false;
+#endif
     const unsigned long long tl = L.tlab[0];
     int n = -1;
     if (ok && tl != kGInf) {
@@ -526,8 +529,10 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
         }
         cur = wave_min_u32(best);
       }
-      n = 0;
-      while (cur != kEmpty && cur != ei) {
+      // no in-edge offers the target's label: the next tier (never a zero-edge success;
+      // cur == ei is the legitimate empty path, ej entered straight from ei)
+      n = cur == kEmpty ? -1 : 0;
+      while (n >= 0 && cur != kEmpty && cur != ei) {
         if (n >= CAP) {
           n = -1;
           break;

@@ -168,7 +168,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
   const int64_t lo = (int64_t)(blockIdx.x & 7) * per;
   const int64_t hi = lo + per < n ? lo + per : n;
   const int64_t stride = (int64_t)(gridDim.x >> 3);
+  unsigned long long cyc_res = 0, cyc_part = 0, cyc_relax = 0, cyc_other = 0;  // (OTR_STAMPS)
   for (int64_t w = lo + (int64_t)(blockIdx.x >> 3); w < hi; w += stride) {
+    OTR_STAMP(ts0);
     const int64_t task = a.task_list[w];
     const uint4 r0 = a.rec[3 * task], r1 = a.rec[3 * task + 1], r2 = a.rec[3 * task + 2];
     const int64_t s = r0.x, sp = r0.y;
@@ -253,6 +255,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
       int npend = 1, nkeys = 1;
 #pragma unroll 1
       for (;;) {
+        OTR_STAMP(tr0);
         // ---- targets: every later offer to a target has key >= kmin + tpart + tmin and
         // length >= dmin + tpart; done when every needed target is final or unreachable
         bool res = true;
@@ -262,6 +265,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
                 (uint64_t)dmin + tpart > (uint64_t)pd;
         }
         if (__ballot(!res) == 0ull || npend == 0) break;
+        OTR_STAMP(tr1);
         // ---- partition: final pending states (IN criterion) to the settled list; the
         // rest stay and give the next kmin / dmin
         uint32_t knext = 0xFFFFFFFFu, dnext = 0xFFFFFFFFu;
@@ -296,6 +300,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           __syncthreads();
         }
         npend = kept;
+        OTR_STAMP(tr2);
         // ---- relax: lane = (settled state, adjacency slot)
         bool tail = false;
 #pragma unroll 1
@@ -358,17 +363,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           npend = L.n_pend;
           nkeys += L.n_keys;
         }
+        OTR_STAMP(tr3);
         __syncthreads();
         kmin = wave_min_u32(knext);
         dmin = wave_min_u32(dnext);
+#ifdef OTR_STAMPS
+        OTR_STAMP(tr4);
+        cyc_res += (tr1 - tr0) + (tr4 - tr3);
+        cyc_part += tr2 - tr1;
+        cyc_relax += tr3 - tr2;
+#endif
         if (L.overflow || nkeys > kMaxKeys) {
           ok = false;
           break;
         }
       }
     }
-#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 0 fails every first-tier edge search
-    if (a.force_edge & 1) ok = false;
+#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 0 / 1 fails every 256 / 1024-state search
+    if (a.force_edge & (CAP <= 256 ? 1 : 2)) ok = false;
 #endif
     ok = ok && Kb <= TG;
     if (ok) {
@@ -408,7 +420,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
       a.overflow_flag[task] = CAP <= 256 ? 6 : 7;  // the next table: 1024 states, then 2048 (otr_edge.h)
     }
     __syncthreads();
+#ifdef OTR_STAMPS
+    OTR_STAMP(ts1);
+    cyc_other += ts1 - ts0;
+#endif
   }
+#ifdef OTR_STAMPS  // phase cycles summed over waves: 16 resolution + round end, 17 partition, 18 relax, 19 all
+  if (threadIdx.x == 0 && a.stamps) {
+    const int sh = cshard();
+    atomicAdd(&a.stamps[16 * kCShards + sh], cyc_res);
+    atomicAdd(&a.stamps[17 * kCShards + sh], cyc_part);
+    atomicAdd(&a.stamps[18 * kCShards + sh], cyc_relax);
+    atomicAdd(&a.stamps[19 * kCShards + sh], cyc_other);
+  }
+#endif
 }
 
 }  // namespace otr

@@ -841,6 +841,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ra.rec = task_rec;
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
   ra.overflow_flag = task_ovf;
+  ra.stamps = d_counters;
   // the first tier's size estimate (k_route route_unit): an exact search runs to its
   // bounds unless its targets resolve first, so its keys grow with the area it can reach,
   // est = c * density * reach^2, reach = min(length bound, time bound x 50 km/h capped by
@@ -1180,6 +1181,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       pa.cand_count = cb.count;
       pa.trans_off = trans_off;
       pa.trans = trans;
+      pa.force_edge = ra.force_edge;
       tb(OTR_STAGE_PATHS);
       {
         const int64_t units = (S + 1) / 2;  // upper bound: two searches per wave

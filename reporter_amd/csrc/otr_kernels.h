@@ -1070,8 +1070,11 @@ struct RouteArgs {
   uint32_t tier_keys[8];      // key capacity of each retry tier, in order
   int n_tiers;
   int64_t unit_base;          // first tier: the launch's first unit (launches of < 2^32 work-items)
-  int force_edge;             // test build only (OTR_FORCE_RETRY): bit 0 every multi-source edge group
-                              // fails, bit 1 every 384-state edge search, bit 2 every 2048-state one
+  unsigned long long* stamps;  // diagnostic build (OTR_STAMPS): bank 0 of the work counters (phase cycles)
+  int force_edge;             // test build only (OTR_FORCE_RETRY, env OTR_FORCE_EDGE): bits 0 / 1 / 2 fail
+                              // every 256 / 1024 / 2048-state edge-state route search (the next tier
+                              // takes it; bit 0 also every multi-source group of the A/B build), bits
+                              // 3 / 4 every 384 / 2048-state edge-state winner path
 };
 
 // k_tasks' inputs and outputs
@@ -1740,6 +1743,7 @@ struct PathArgs {
   const int32_t* cand_count;
   const int64_t* trans_off;    // the route lengths k_route found (u32 mm per transition)
   const uint32_t* trans;
+  int force_edge;              // test build only (OTR_FORCE_RETRY): RouteArgs::force_edge bits 3-4
 };
 
 // G searches per wave (G = 2 for the first tier, lanes split 32/32), each a

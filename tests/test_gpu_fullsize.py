@@ -81,7 +81,7 @@ def test_c3_shard_in_one_batch(graph_dir):
     """The C3 N = 8 share in ONE device batch (125,000 traces, 12.5M probes, ~178M route tasks):
     more first-tier units than one dispatch can address (its grid size counts work-items in
     32 bits), so the first tier runs as several launches.  Every trace must match (status 0)
-    and an evenly spread sample equals the oracle; a batch beyond 2^26 probes is refused."""
+    and an evenly spread sample equals the oracle."""
     import hashlib
     path = gen.graph_path('metro', graph_dir)
     opts = dict(GTT, search_radius=50, gps_accuracy=16.45)

@@ -2,8 +2,13 @@
 (libotr_tiercheck.so, -DOTR_FORCE_RETRY) sends EVERY first-tier search down the
 retry kernels, and must still match the oracle field by field.  Parametrised over
 the retry-tier list (OTR_TIERS): the default 256 → 448x2 → 1024 → 2048 → 4096 chain, a chain
-that starts with two-searches-per-wave 384-slot tables, and direct 1024/4096; with
-OTR_DIRECT_BMM=0 every search skips the first tier on its own.
+that starts with two-searches-per-wave 384-slot tables, and direct 1024/4096; with the size
+estimate scaled up (OTR_EST_K=1000) every search starts in the last retry tier, with it off
+(OTR_EST_K=0) every search overflows into the first retry tier.
+The edge-state tiers (turn costs: the deployed per-mode defaults, a mode mix) the same way:
+OTR_FORCE_EDGE fails every search of the chosen tiers, so the next one does all the work —
+the 1024-state lean tier, the 2048-state table, k_general, and for winner paths the
+2048-state table and k_general.
 Runs in a child process (one library per process)."""
 import os
 import subprocess
@@ -43,17 +48,18 @@ print('tiers ok')
 '''
 
 
-@pytest.mark.parametrize('tiers,direct', [(None, None), ('384x2,512', None), ('512x2,2048', None), ('1024', '0')])
-def test_retry_tiers_equal_first_tier(graph_dir, tiers, direct):
+@pytest.mark.parametrize('tiers,est', [(None, None), ('384x2,512', None), ('512x2,2048', None), ('1024', '0'),
+                                       (None, '1000')])
+def test_retry_tiers_equal_first_tier(graph_dir, tiers, est):
     lib = os.path.join(ROOT, 'reporter_amd', 'libotr_tiercheck.so')
     assert os.path.exists(lib), 'build first: python -m reporter_amd.build'
     env = dict(os.environ, OTR_LIB=lib)
-    env.pop('OTR_TIERS', None)
-    env.pop('OTR_DIRECT_BMM', None)
+    for k in ('OTR_TIERS', 'OTR_EST_K', 'OTR_FORCE_EDGE'):
+        env.pop(k, None)
     if tiers:
         env['OTR_TIERS'] = tiers
-    if direct is not None:
-        env['OTR_DIRECT_BMM'] = direct
+    if est is not None:
+        env['OTR_EST_K'] = est
     p = subprocess.run([sys.executable, '-c', CHILD % (ROOT, graph_dir)], env=env, capture_output=True, text=True,
                        timeout=240)
     assert p.returncode == 0 and 'tiers ok' in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
@@ -99,3 +105,56 @@ def test_general_search_equals_oracle(graph_dir):
     p = subprocess.run([sys.executable, '-c', GENERAL_CHILD % (ROOT, graph_dir)], env=env, capture_output=True,
                        text=True, timeout=280)
     assert p.returncode == 0 and 'general ok' in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
+
+
+EDGE_CHILD = r'''
+import sys
+sys.path.insert(0, %r)
+from oracle import pyoracle as po
+from oracle.compare import compare
+from reporter_amd import matcher as M
+from reporter_amd import _lib
+from reporter_amd.tools import gen
+force = %d
+# the deployed configuration (every mode's default turn penalty), auto only and a mode mix
+for g, nt, npnt, sr, sig, seed, fb, fp in [('city', 40, 100, 15, 10.0, 2, 0.0, 0.0),
+                                           ('metro', 40, 100, 15, 10.0, 5, 0.25, 0.15)]:
+    path = gen.graph_path(g, %r)
+    M.configure(M.default_config(path))
+    tr = gen.make_traces(path, nt, npnt, sr, sig, seed, fb, fp)
+    m = M.Matcher()
+    r = m.match_batch(tr, copy_out=True, route_work=True)
+    assert r.status == 0, r.status
+    w = [int(r.route_tier_work[t][0]) for t in range(12)]
+    # slots: 10 the 256-state lean tier, 9 the 1024-state one, 11 the 2048 table, 6 k_general
+    if force & 1:
+        assert w[10] == 0 and w[9] + w[11] + w[6] > 0, w
+    if (force & 3) == 1:
+        assert w[9] > 0, w
+    if (force & 7) == 3:
+        assert w[9] == 0 and w[11] > 0, w
+    if (force & 7) == 7:
+        assert w[9] == 0 and w[11] == 0 and w[6] > 0, w
+    if force == 0:
+        assert w[10] > 0, w
+    got = _lib.result_to_numpy(r)
+    want = po.match_batch(po.Graph(path), tr, po.params(), threads=8)
+    errors, stats = compare(got, want)
+    assert not errors, errors
+print('edge tiers ok')
+'''
+
+
+@pytest.mark.parametrize('force', [0, 1, 3, 7, 24])
+def test_edge_tiers_equal_oracle(graph_dir, force):
+    """libotr_tiercheck.so with OTR_FORCE_EDGE: bits 0-2 fail every 256 / 1024 / 2048-state
+    edge-state route search, bits 3-4 every 384 / 2048-state winner path; the next tier takes
+    them (route_tier_work shows which did) and the output still equals the oracle."""
+    lib = os.path.join(ROOT, 'reporter_amd', 'libotr_tiercheck.so')
+    assert os.path.exists(lib), 'build first: python -m reporter_amd.build'
+    env = dict(os.environ, OTR_LIB=lib, OTR_FORCE_EDGE=str(force))
+    for k in ('OTR_TIERS', 'OTR_EST_K'):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, '-c', EDGE_CHILD % (ROOT, force, graph_dir)], env=env, capture_output=True,
+                       text=True, timeout=280)
+    assert p.returncode == 0 and 'edge tiers ok' in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]

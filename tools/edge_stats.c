@@ -19,6 +19,7 @@ typedef struct {
   int64_t hist_union[64];                         /* union keys per step, 64-key buckets */
   int64_t hist_rounds[64];                        /* rounds per search */
   int64_t pend_max, max_rounds_sum, relaxed, groups;
+  int64_t hist_bmm_keys[24][24]; /* [route bound / 100 m][keys / 32] */
 } es_stats;
 
 typedef struct {
@@ -229,6 +230,10 @@ int es_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
         S->rounds_tmin += rd2;
         S->sum_settle_events += st;
         S->hist_keys[keys / 32 < 63 ? keys / 32 : 63]++;
+        {
+          const int64_t bb = X.bmm / 100000 < 23 ? X.bmm / 100000 : 23, kb = keys / 32 < 23 ? keys / 32 : 23;
+          S->hist_bmm_keys[bb][kb]++;
+        }
         S->hist_rounds[rd < 63 ? rd : 63]++;
         step_sum += keys;
         nsrc++;

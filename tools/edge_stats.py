@@ -26,7 +26,7 @@ class Stats(ctypes.Structure):
         'sources', 'union_settle_events', 'sum_settle_events')] + [
         ('hist_keys', ctypes.c_int64 * 64), ('hist_union', ctypes.c_int64 * 64), ('hist_rounds', ctypes.c_int64 * 64),
         ('pend_max', ctypes.c_int64), ('max_rounds_sum', ctypes.c_int64), ('relaxed', ctypes.c_int64),
-        ('groups', ctypes.c_int64)]
+        ('groups', ctypes.c_int64), ('hist_bmm_keys', (ctypes.c_int64 * 24) * 24)]
 
 
 def main():
@@ -73,6 +73,13 @@ def main():
         'rounds_hist': {str(i): int(S.hist_rounds[i]) for i in range(64) if S.hist_rounds[i]},
     }
     print(json.dumps(out, indent=1))
+    hb = np.array([[S.hist_bmm_keys[i][j] for j in range(24)] for i in range(24)])
+    print('route bound (100 m) -> searches, mean keys, P(keys > 224)')
+    for i in range(24):
+        n_i = hb[i].sum()
+        if n_i:
+            mk = (hb[i] * (np.arange(24) * 32 + 16)).sum() / n_i
+            print('  %4d m: %7d  %6.1f  %.3f' % (i * 100, n_i, mk, hb[i][7:].sum() / n_i))
 
 
 if __name__ == '__main__':
