@@ -135,8 +135,9 @@ def main():
     ap.add_argument('--chunk-traces', type=int, default=125000,
                     help='traces per device batch (a shard larger than this is matched in several batches per '
                          'step; 125,000 = the N = 8 share of C3)')
-    ap.add_argument('--workload', choices=['c2', 'c2dep', 'c3', 'c4', 'c5mix', 'c5'], default=None,
-                    help='default: c2 at N = 1, c3 at N > 1.  c2 (the headline): 100 probes @15 s, sigma 10 m; '
+    ap.add_argument('--workload', choices=['c1', 'c2', 'c2dep', 'c3', 'c4', 'c5mix', 'c5'], default=None,
+                    help='default: c2 at N = 1, c3 at N > 1.  c1: the city graph, 1,000 traces x 300 probes @1 s, '
+                         'sigma 5 m (BASELINE config 1); c2 (the headline): 100 probes @15 s, sigma 10 m; '
                          'c2dep: the same traces '
                          'matched with the deployed configuration only (what Batch.java requests get: mode '
                          'defaults, turn penalties auto 200 / bicycle 140 / pedestrian 100); c3: the C3 shard of '
@@ -195,7 +196,7 @@ def main():
         raise SystemExit('libotr.so missing: run python __graft_entry__.py build first')
 
     gdir = os.path.join(ROOT, 'build', 'graphs')
-    gname = 'country' if args.workload == 'c5' else 'metro'
+    gname = {'c5': 'country', 'c1': 'city'}.get(args.workload, 'metro')
     if rank == 0:
         tg = time.time()
         gpath = gen.graph_path(gname, gdir)
@@ -207,7 +208,11 @@ def main():
     # gps_accuracy = the 95th percentile of the noise); max_route_time_factor stays the
     # deployed 2 (Dockerfile:17)
     gtt = {'turn_penalty_factor': 0, 'beta': 3, 'sigma_z': 4.07, 'breakage_distance': 2000}
-    W = {'c2': dict(points=100, rate=15, sigma=10.0, seed=2, bike=0.0, ped=0.0, acc=None, traces=10000,
+    # C1: generate_test_trace.py's 1 Hz traces with 5 m noise on the city graph,
+    # gps_accuracy = round(min(100, 1.645 * max(1, 5)), 2) = 8.22
+    W = {'c1': dict(points=300, rate=1, sigma=5.0, seed=1, bike=0.0, ped=0.0, acc=None, traces=1000,
+                    meili=dict(gtt, search_radius=50, gps_accuracy=8.22)),
+         'c2': dict(points=100, rate=15, sigma=10.0, seed=2, bike=0.0, ped=0.0, acc=None, traces=10000,
                     meili=dict(gtt, search_radius=50, gps_accuracy=16.45)),
          # the deployed configuration (Dockerfile:14-17,42-49 + the per-mode defaults): a
          # Batch.java request carries only mode and levels (Batch.java:56-65)
@@ -474,7 +479,8 @@ def main():
     # own shard at every N (after the timed region; the other ranks wait at the closing
     # barrier), so a multi-GPU line carries its own parity evidence
     cpu, parity = None, None
-    n_cpu = args.cpu_traces if args.cpu_traces is not None else {'c2': 6000, 'c2dep': 2000, 'c5mix': 6000, 'c4': 600,
+    n_cpu = args.cpu_traces if args.cpu_traces is not None else {'c1': 1000, 'c2': 6000, 'c2dep': 2000, 'c5mix': 6000,
+                                                                 'c4': 600,
                                                                  'c5': 3000, 'c3': 6000}[args.workload]
     if rank == 0 and n_cpu > 0:
         from oracle import pyoracle as po
@@ -583,10 +589,10 @@ def main():
             'data': 'synthetic',
             'config': {'workload': '%s: %s street grid (%d nodes, %d directed edges, %d OSMLR segments), '
                                    '%d traces x %d probes per GPU @%d s, sigma %g m%s; %s' % (
-                                       args.workload.upper(), 'country' if gname == 'country' else 'metro', n_nodes,
+                                       args.workload.upper(), gname, n_nodes,
                                        n_edges, n_segments, mine.n_traces,
                                        W['points'], W['rate'], W['sigma'],
-                                       {'c2': '', 'c3': ', C3 uuid shard (1M veh%07d uuids, sha1[:3] % N)',
+                                       {'c1': '', 'c2': '', 'c3': ', C3 uuid shard (1M veh%07d uuids, sha1[:3] % N)',
                                         'c4': ', accuracy 50 m, search radius 200 m',
                                         'c5mix': ', modes 60% auto / 25% bicycle / 15% pedestrian',
                                         'c2dep': '',
