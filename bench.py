@@ -55,12 +55,10 @@ def log(*a):
 
 def kernel_name(code, turns=False, first=False):
     """rocprofv3 name of a route kernel (otr_batch_result.route_tier_code); turns: kept for
-    callers (turn-mode tasks run in the edge-state kernels: code 8,000,000 + CAP * 100 + sources
-    for the multi-source tier, 7,000,000 + CAP * 100 + targets for the single-source ones)."""
+    callers (turn-mode tasks run in the edge-state kernels: code 6,000,000 + CAP * 100 + targets
+    for the lean tiers, 7,000,000 + CAP * 100 + targets for otr_edge.h's table)."""
     if code < 0:  # the global-memory search: -1 on 32K-state slabs, -2 on 1M-state slabs
         return 'k_general' if code == -1 else 'k_general (1M-state slabs)'
-    if code >= 8000000:  # the multi-source edge-state tier: 8,000,000 + CAP * 100 + sources
-        return 'k_route_medge<%d, %d>' % ((code - 8000000) // 100, code % 100)
     if 6000000 <= code < 7000000:  # the lean first edge-state tier: 6,000,000 + CAP * 100 + targets
         return 'k_route_e1<%d>' % ((code - 6000000) // 100)
     if code >= 7000000:  # the single-source edge-state tiers: 7,000,000 + CAP * 100 + targets

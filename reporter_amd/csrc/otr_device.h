@@ -96,7 +96,7 @@ struct DevGraph {
   uint32_t adj_t_stride, edge_t_stride;  // elements per mode
   const short2* edge_head;     // per edge {begin heading, end heading}, integer degrees
   const uint2* adj_e;          // 4 per node like adj: {edge id, begin heading | end heading << 16} (edge-state searches)
-  const uint4* erec;           // [mode][4 per node like adj]: the multi-source edge-state record (otr_medge.h erec_make)
+  const uint4* erec;           // [mode][4 per node like adj]: the edge-state search's record (otr_edge1.h erec_make)
   uint32_t erec_stride;        // records per mode
   uint32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double grid_min_lat, grid_min_lon, grid_cell_deg;

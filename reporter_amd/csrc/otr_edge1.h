@@ -24,10 +24,30 @@
 //     table in 7.3 KB: 21 waves per CU, 80 % of the C2 searches); a search that outgrows it
 //     goes on to 1024 states (this kernel again), then 2048 (otr_edge.h), same results.
 #pragma once
-#include "otr_medge.h"
+#include <type_traits>
+
+#include "otr_edge.h"
 
 namespace otr {
 
+// the per-mode edge-state adjacency record, one per (node, slot) like DevGraph::adj:
+// {dst | access << 28 | more << 31, len_mm, edge | end heading bits 0-3 << 28,
+//  route time (0.1 s, saturated at 2^17 - 1) | begin heading << 17 | end heading bits 4-8 << 26}
+__host__ __device__ inline uint4 erec_make(uint32_t dw, uint32_t len, uint32_t e, uint32_t t, uint32_t hb,
+                                           uint32_t he) {
+  return make_uint4(dw, len, (e & kAdjDstMask) | ((he & 15u) << 28),
+                    (t < 0x1FFFFu ? t : 0x1FFFFu) | ((hb & 0x1FFu) << 17) | ((he >> 4) << 26));
+}
+__device__ inline uint32_t er_edge(const uint4& r) { return r.z & kAdjDstMask; }
+__device__ inline uint32_t er_he(const uint4& r) { return (r.z >> 28) | ((r.w >> 26) << 4); }
+__device__ inline uint32_t er_hb(const uint4& r) { return (r.w >> 17) & 0x1FFu; }
+__device__ inline uint32_t er_t(const uint4& r) { return r.w & 0x1FFFFu; }
+
+
+// the partition touches each settled state's adjacency records (A/B knob)
+#ifndef OTR_E1PF
+#define OTR_E1PF 1
+#endif
 // waves per SIMD the compiler fits the kernel's registers for (8: 64 VGPRs)
 #ifndef OTR_E1WAVES
 #define OTR_E1WAVES 8
@@ -45,8 +65,9 @@ struct E1Lds {
   uint16_t hbk[CAP];            // the edge's end heading reversed
   uint8_t mi[CAP];              // mi8_of(len(edge))
   Idx pend[CAP];                // pending slots
-  Idx wsl[WCAP];                // this round's settled slots
-  unsigned long long wlab[WCAP];  //   and their labels
+  unsigned long long wlab[WCAP];  // this round's settled states: their labels
+  uint32_t wnode[WCAP];         //   their nodes
+  uint16_t whbk[WCAP];          //   their reversed end headings
   unsigned long long tlab[TG];  // the targets' best feasible offers
   uint32_t tpart[TG], tpt[TG];  // entry parts (mm, 0.1 s)
   uint16_t thb[TG];             // begin heading of the target edge
@@ -253,6 +274,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
       const uint32_t tmin = L.tmin;
       uint32_t kmin = 0, dmin = 0;  // the smallest pending key / length
       int npend = 1, nkeys = 1;
+      uint32_t pf = 0;  // (OTR_E1PF: the prefetch loads' sink)
 #pragma unroll 1
       for (;;) {
         OTR_STAMP(tr0);
@@ -276,10 +298,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           const bool in = k < npend;
           int sl = 0;
           unsigned long long lb = 0;
+          uint32_t nd = 0, hk = 0;
           bool take = false;
           if (in) {
             sl = L.pend[k];
             lb = L.lab[sl];
+            nd = L.node[sl];  // (read beside the label: the relax lanes then need no dependent read)
+            hk = L.hbk[sl];
             take = (uint64_t)g_k(lb) < (uint64_t)kmin + in_gap8(L.mi[sl]) + tmin;
           }
           take = take && nw + prefix_count(__ballot(take)) < WCAP;
@@ -288,8 +313,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           __syncthreads();
           if (take) {
             const int wq = nw + prefix_count(mt);
-            L.wsl[wq] = (typename LT::Idx)sl;
             L.wlab[wq] = lb;
+            L.wnode[wq] = nd;
+            L.whbk[wq] = (uint16_t)hk;
+#if OTR_E1PF
+            // touch the state's adjacency records now: the relax lanes' loads of them, after
+            // the barrier, then come from the near cache instead of L2 (pf is kept live
+            // until after the relax loop, so its register is not reused while in flight)
+            pf |= *(const volatile uint32_t*)(er + 4 * (size_t)nd);
+#endif
           } else if (keep) {
             L.pend[kept + prefix_count(mk)] = (typename LT::Idx)sl;
             knext = g_k(lb) < knext ? g_k(lb) : knext;
@@ -309,9 +341,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           int psl = -1;
           bool isnew = false;
           if (k < 4 * nw) {
-            const int sl = L.wsl[k >> 2];
             const unsigned long long lb = L.wlab[k >> 2];
-            const uint32_t v = L.node[sl], hbk = L.hbk[sl];
+            const uint32_t v = L.wnode[k >> 2], hbk = L.whbk[k >> 2];
             const int slot = k & 3;
             // the record load is issued first and waited for only after the target offers
             // (LDS work), so the two latencies overlap
@@ -330,6 +361,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           if (psl >= 0) L.pend[npend + prefix_count(mp)] = (typename LT::Idx)psl;  // (< CAP: one entry per state)
           npend += __popcll(mp);
         }
+#if OTR_E1PF
+        asm volatile("" ::"v"(pf));  // (the prefetches completed: their register is free again)
+#endif
         if (__ballot(tail) != 0ull) {  // nodes with more than four out-edges: the CSR tail
           if (lane == 0) {
             L.n_pend = npend;
@@ -340,9 +374,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           for (int base = 0; base < 4 * nw; base += OTR_WAVE) {
             const int k = base + lane;
             if (k < 4 * nw && (k & 3) == 3) {
-              const int sl = L.wsl[k >> 2];
               const unsigned long long lb = L.wlab[k >> 2];
-              const uint32_t v = L.node[sl], hbk = L.hbk[sl];
+              const uint32_t v = L.wnode[k >> 2], hbk = L.whbk[k >> 2];
               if (er[4 * (size_t)v + 3].x & kAdjMore) {
                 const uint32_t* et = gr.et(md);
 #pragma unroll 1

@@ -13,7 +13,6 @@
 #include "otr_engine.h"
 #include "otr_kernels.h"
 #include "otr_edge.h"
-#include "otr_medge.h"
 #include "otr_edge1.h"
 #include "otr_ingest.h"
 
@@ -247,7 +246,7 @@ int engine_configure(const Config& cfg, std::string* err) {
       const uint32_t e = row[u] + k;
       adje[4ull * u + k] = make_uint2(e, (uint32_t)(uint16_t)head[e].x | ((uint32_t)(uint16_t)head[e].y << 16));
     }
-  // multi-source edge-state view (otr_medge.h): per mode one 16-B record per adjacency
+  // edge-state view (otr_edge1.h): per mode one 16-B record per adjacency
   // slot with the head, length, edge id, route time and both headings (one load per relaxation)
   std::vector<uint4> erec((4ull * h.n_nodes + 4) * OTR_MODES, make_uint4(kAdjDstMask, 0u, 0u, 0u));
   for (int m = 0; m < OTR_MODES; ++m) {
@@ -392,7 +391,7 @@ enum Slot {
   S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
-  S_CLEN, S_CAND_NROOT, S_FLAGGED, S_MGROUPS, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST,
+  S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST,
   S_NUM
 };
 
@@ -801,11 +800,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     ta.task_state = task_state;
     ta.task_mask = task_mask;
     ta.rec = task_rec;
-#if OTR_MEDGE
-    ta.flag_turn = nullptr;  // (the multi-source tier takes every turn-mode task)
-#else
     ta.flag_turn = task_ovf;  // turn-mode tasks start in the first edge-state tier (flag 5)
-#endif
     if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
     if (k32) k_tasks<2><<<grid_for((S + 1) / 2, 4), 256, 0, stream>>>(ta);
     else k_tasks<1><<<grid_for(S, 4), 256, 0, stream>>>(ta);
@@ -868,8 +863,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   // device-side counters of the retry lists: [0..7] route tiers, [8] general tier 1,
   // [9] general tier 2, [10] route tasks left unrouted, [11] steps, [12..15] path tiers,
   // [16] path general 1, [17] path general 2, [18] paths left, [19] general overflow
-  // count, [20] cap flag, [21] exact node path tier, [22] multi-source edge groups (A/B
-  // build), [23] first edge-state tier, [24] tasks the first route tier
+  // count, [20] cap flag, [21] exact node path tier, [23] first edge-state tier, [24] tasks
+  // the first route tier
   // flagged, [25..26] edge-state route tiers, [27..28] edge-state path tiers, [29] exact
   // edge route tier, [30] exact node route tier, [31] exact edge path tier, [32..96) path
   // bump cursors
@@ -996,22 +991,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // persistent grids: twice the resident waves of the widest tier (256 CUs x 4 SIMDs x
     // 8 waves), so no tier is starved; blocks past the list length exit at once
     const unsigned tgrid = 16384;
-#if OTR_MEDGE && !defined(OTR_FORCE_GENERAL)
-    // A/B build (-DOTR_MEDGE=1): the turn-mode tasks in the multi-source edge tier first,
-    // OTR_MS source candidates of a step per search (otr_medge.h); groups it cannot hold
-    // flag their tasks 5 (the single-source edge tiers below)
-    if (turns) {
-      uint64_t* groups = need<uint64_t>(S_MGROUPS, std::max<int64_t>(NT, 1));
-      if (!groups) {
-        if (err) *err = "device allocation failed (edge-state groups)";
-        return OTR_DEVICE_ERROR;
-      }
-      k_mgroups<OTR_MS><<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, cb.count, task_off, state_trace, b.mode,
-                                                               turn_modes, groups, cnt + 22);
-      // (no tier slot of its own: its time is in the route_big stage)
-      k_route_medge<OTR_MCAP, OTR_MS><<<4096, 64, 0, stream>>>(g, ra, groups, cnt + 22, nullptr);
-    }
-#endif
     // the first tier's flagged tasks, once; every later collect scans only them
     k_collect_flagged<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, flagged, cnt + 24);
     constexpr unsigned kCollectGrid = 512;

@@ -28,19 +28,9 @@
 #ifndef OTR_LOAD1
 #define OTR_LOAD1 7
 #endif
-// the single-source edge-state search's first table (states per search; turn-cost modes):
-// it takes what the multi-source tier (otr_medge.h) cannot hold — groups whose union of
-// states outgrows that table, i.e. the large searches (a third of them beyond 336 keys)
-#ifndef OTR_ECAP
-#define OTR_ECAP 768
-#endif
 // the lean first edge-state tier's table (otr_edge1.h)
 #ifndef OTR_E1CAP
 #define OTR_E1CAP 256
-#endif
-// A/B: the multi-source edge tier (otr_medge.h) ahead of the single-source ones
-#ifndef OTR_MEDGE
-#define OTR_MEDGE 0
 #endif
 
 namespace otr {
@@ -1073,7 +1063,7 @@ struct RouteArgs {
   unsigned long long* stamps;  // diagnostic build (OTR_STAMPS): bank 0 of the work counters (phase cycles)
   int force_edge;             // test build only (OTR_FORCE_RETRY, env OTR_FORCE_EDGE): bits 0 / 1 / 2 fail
                               // every 256 / 1024 / 2048-state edge-state route search (the next tier
-                              // takes it; bit 0 also every multi-source group of the A/B build), bits
+                              // takes it), bits
                               // 3 / 4 every 384 / 2048-state edge-state winner path
 };
 
