@@ -56,10 +56,11 @@ def log(*a):
 def kernel_name(code, turns=False, first=False):
     """rocprofv3 name of a route kernel (otr_batch_result.route_tier_code); turns: kept for
     callers (turn-mode tasks run in the edge-state kernels: code 6,000,000 + CAP * 100 + targets
-    for the lean tiers, 7,000,000 + CAP * 100 + targets for otr_edge.h's table)."""
+    for the lean tiers; 7,000,000 + CAP * 100 + targets named otr_edge.h's table in earlier
+    builds)."""
     if code < 0:  # the global-memory search: -1 on 32K-state slabs, -2 on 1M-state slabs
         return 'k_general' if code == -1 else 'k_general (1M-state slabs)'
-    if 6000000 <= code < 7000000:  # the lean first edge-state tier: 6,000,000 + CAP * 100 + targets
+    if 6000000 <= code < 7000000:  # the lean edge-state tiers: 6,000,000 + CAP * 100 + targets
         return 'k_route_e1<%d>' % ((code - 6000000) // 100)
     if code >= 7000000:  # the single-source edge-state tiers: 7,000,000 + CAP * 100 + targets
         return 'k_route_edge<%d, %d>' % ((code - 7000000) // 100, code % 100)
@@ -642,11 +643,12 @@ def main():
             'end_to_end': e2e,
         }
         print(json.dumps(line), flush=True)
-        if parity is not None and not parity['ok']:
-            raise SystemExit('bench: GPU output differs from the oracle sample: %s' % parity['errors'])
     if world > 1:
         dist.barrier()  # rank 0's oracle sample and line come after the timed region
         dist.destroy_process_group()
+    # a parity failure ends rank 0 with an error only after the other ranks left the barrier
+    if rank == 0 and parity is not None and not parity['ok']:
+        raise SystemExit('bench: GPU output differs from the oracle sample: %s' % parity['errors'])
 
 
 if __name__ == '__main__':

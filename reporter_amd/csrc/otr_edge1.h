@@ -22,7 +22,7 @@
 //     wave's scalar state is kept small (no SGPR spills);
 //   * small tables: the first tier holds 256 states (table + lists + targets + the turn
 //     table in 7.3 KB: 21 waves per CU, 80 % of the C2 searches); a search that outgrows it
-//     goes on to 1024 states (this kernel again), then 2048 (otr_edge.h), same results.
+//     goes on to 512 and 1024 states (this kernel again), then k_general: same results.
 #pragma once
 #include <type_traits>
 
@@ -55,7 +55,7 @@ __device__ inline uint32_t er_t(const uint4& r) { return r.w & 0x1FFFFu; }
 
 template <int CAP>
 struct E1Lds {
-  static constexpr int TG = 32;   // targets (steps with more go to otr_edge.h's TG = 64 tier)
+  static constexpr int TG = 32;   // targets (steps with more go on to k_general)
   static constexpr int TM = 32;   // target-node map slots (a target node per target at most)
   static constexpr int WCAP = CAP <= 256 ? 32 : 64;  // states settled per round (the rest wait)
   using Idx = typename std::conditional<(CAP <= 256), uint8_t, uint16_t>::type;
@@ -172,8 +172,8 @@ __device__ inline void e1_turn_table(E1Lds<CAP>& L, const int32_t* turn_tab, int
 // K3e1 kernel: a persistent grid over the device-side list of the turn-mode tasks (one
 // source candidate each), the 8 XCDs taking contiguous eighths of the list (consecutive
 // tasks = the candidates of one step, then the next steps of the trace: one neighbourhood).
-// A search that outgrows the table flags its task for the next tier: 6 (this kernel with
-// 1024 states), 7 (otr_edge.h's 2048-state table).
+// A search that outgrows the table flags its task for the next tier: 6 (512 states), 7
+// (1024), 3 (k_general, global-memory labels).
 // ------------------------------------------------------------------------------
 template <int CAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES, 8))) void k_route_e1(
@@ -412,8 +412,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
         }
       }
     }
-#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 0 / 1 fails every 256 / 1024-state search
-    if (a.force_edge & (CAP <= 256 ? 1 : 2)) ok = false;
+#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 0 / 1 / 2 fails every 256 / 512 / 1024-state search
+    if (a.force_edge & (CAP <= 256 ? 1 : (CAP <= 512 ? 2 : 4))) ok = false;
 #endif
     ok = ok && Kb <= TG;
     if (ok) {
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
         }
       }
     } else if (lane == 0) {
-      a.overflow_flag[task] = CAP <= 256 ? 6 : 7;  // the next table: 1024 states, then 2048 (otr_edge.h)
+      a.overflow_flag[task] = CAP <= 256 ? 6 : (CAP <= 512 ? 7 : 3);  // the next table: 512, 1024, k_general
     }
     __syncthreads();
 #ifdef OTR_STAMPS

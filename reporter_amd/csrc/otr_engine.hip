@@ -1035,14 +1035,12 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       if (timing) (void)hipEventRecord(ev[24 + 2 * 8 + 1], stream);
     }
 #endif
-    // edge-state tiers (turn-cost modes): the lean tier at 256 states (flag 5, otr_edge1.h,
-    // slot 10), at 1024 (flag 6, slot 9), then the 2048-state table (flag 7, otr_edge.h, slot
-    // 11); what outgrows those (flag 3) goes on below
+    // edge-state tiers (turn-cost modes, otr_edge1.h): 256 states (flag 5, slot 10), 512
+    // (flag 6, slot 9), 1024 (flag 7, slot 11); what outgrows those (flag 3) goes on below
     if (turns) {
       for (int et = 0; et < 3; ++et) {
         const int slot = et == 0 ? 10 : (et == 1 ? 9 : 11);
-        out->route_tier_code[slot] = et == 0 ? 6000000 + OTR_E1CAP * 100 + 32
-                                             : (et == 1 ? 6000000 + 1024 * 100 + 32 : 7000000 + 2048 * 100 + 64);
+        out->route_tier_code[slot] = 6000000 + (et == 0 ? OTR_E1CAP : (et == 1 ? 512 : 1024)) * 100 + 32;
         unsigned long long* c = cnt + (et == 0 ? 23 : 24 + et);
         k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x20u << et, list, c);
         RouteArgs rb = ra;
@@ -1050,12 +1048,12 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         rb.list_count = c;
         unsigned long long* rcn = rwork ? d_counters + (et == 0 ? 10 : (et == 1 ? 1 : 11)) * bank : nullptr;
         if (timing) (void)hipEventRecord(ev[24 + 2 * slot], stream);
-        // persistent grids: every resident wave (~23 per CU at 256 states, 6 at 1024, 3 at
-        // 2048); steps with more than 32 targets (modes keeping > 32 candidates) skip the
-        // lean tiers (their TG = 32) for the 64-target table
+        // persistent grids: every resident wave (~22 per CU at 256 states, 13 at 512, 6 at
+        // 1024); steps with more than 32 targets (modes keeping > 32 candidates) pass the
+        // lean tiers (their TG = 32) on to k_general
         if (et == 0) k_route_e1<OTR_E1CAP><<<8192, 64, 0, stream>>>(g, rb, rcn);
-        else if (et == 1) k_route_e1<1024><<<4096, 64, 0, stream>>>(g, rb, rcn);
-        else k_route_edge<2048, 64><<<1024, 64, 0, stream>>>(g, rb, rcn);
+        else if (et == 1) k_route_e1<512><<<4096, 64, 0, stream>>>(g, rb, rcn);
+        else k_route_e1<1024><<<2048, 64, 0, stream>>>(g, rb, rcn);
         if (timing) (void)hipEventRecord(ev[24 + 2 * slot + 1], stream);
       }
     }

@@ -1062,7 +1062,7 @@ struct RouteArgs {
   int64_t unit_base;          // first tier: the launch's first unit (launches of < 2^32 work-items)
   unsigned long long* stamps;  // diagnostic build (OTR_STAMPS): bank 0 of the work counters (phase cycles)
   int force_edge;             // test build only (OTR_FORCE_RETRY, env OTR_FORCE_EDGE): bits 0 / 1 / 2 fail
-                              // every 256 / 1024 / 2048-state edge-state route search (the next tier
+                              // every 256 / 512 / 1024-state edge-state route search (the next tier
                               // takes it), bits
                               // 3 / 4 every 384 / 2048-state edge-state winner path
 };

@@ -7,8 +7,8 @@ estimate scaled up (OTR_EST_K=1000) every search starts in the last retry tier, 
 (OTR_EST_K=0) every search overflows into the first retry tier.
 The edge-state tiers (turn costs: the deployed per-mode defaults, a mode mix) the same way:
 OTR_FORCE_EDGE fails every search of the chosen tiers, so the next one does all the work —
-the 1024-state lean tier, the 2048-state table, k_general, and for winner paths the
-2048-state table and k_general.
+the 512- and 1024-state lean tiers, k_general, and for winner paths the 2048-state table
+and k_general.
 Runs in a child process (one library per process)."""
 import os
 import subprocess
@@ -126,7 +126,7 @@ for g, nt, npnt, sr, sig, seed, fb, fp in [('city', 40, 100, 15, 10.0, 2, 0.0, 0
     r = m.match_batch(tr, copy_out=True, route_work=True)
     assert r.status == 0, r.status
     w = [int(r.route_tier_work[t][0]) for t in range(12)]
-    # slots: 10 the 256-state lean tier, 9 the 1024-state one, 11 the 2048 table, 6 k_general
+    # slots: 10 the 256-state lean tier, 9 the 512-state one, 11 the 1024-state one, 6 k_general
     if force & 1:
         assert w[10] == 0 and w[9] + w[11] + w[6] > 0, w
     if (force & 3) == 1:
@@ -147,7 +147,7 @@ print('edge tiers ok')
 
 @pytest.mark.parametrize('force', [0, 1, 3, 7, 24])
 def test_edge_tiers_equal_oracle(graph_dir, force):
-    """libotr_tiercheck.so with OTR_FORCE_EDGE: bits 0-2 fail every 256 / 1024 / 2048-state
+    """libotr_tiercheck.so with OTR_FORCE_EDGE: bits 0-2 fail every 256 / 512 / 1024-state
     edge-state route search, bits 3-4 every 384 / 2048-state winner path; the next tier takes
     them (route_tier_work shows which did) and the output still equals the oracle."""
     lib = os.path.join(ROOT, 'reporter_amd', 'libotr_tiercheck.so')
