@@ -20,6 +20,7 @@ typedef struct {
   int64_t hist_rounds[64];                        /* rounds per search */
   int64_t pend_max, max_rounds_sum, relaxed, groups;
   int64_t hist_bmm_keys[24][24]; /* [route bound / 100 m][keys / 32] */
+  int64_t settled_out, rounds_out, scans_tmin, scans_out; /* + the OUT criterion; pending entries examined */
 } es_stats;
 
 typedef struct {
@@ -47,7 +48,8 @@ static void es_touch(es_ws* W, uint32_t e) {
 /* one simulated search; returns keys; *settled, *rounds out */
 static int64_t es_search(const rctx* X, es_ws* W, uint32_t ei, double pi, int ntg, const uint32_t* tv,
                          const int64_t* tpart, const int64_t* tpt, const uint32_t* tej, int64_t tmin,
-                         int64_t* settled, int64_t* rounds, int64_t* relaxed, int64_t* pend_max, int record) {
+                         int64_t* settled, int64_t* rounds, int64_t* relaxed, int64_t* pend_max, int record,
+                         const int64_t* minout, int64_t* scans) {
   const orc_graph* g = X->g;
   const mode_data* md = X->md;
   *settled = 0;
@@ -80,12 +82,22 @@ static int64_t es_search(const rctx* X, es_ws* W, uint32_t ei, double pi, int nt
     ++*rounds;
     int64_t knext = kInf, dnext = kInf;
     uint32_t nf = 0, kept = 0;
+    /* OUT criterion (minout != NULL): every later offer leaves a pending state u through
+       one of its head's out-edges: key >= k(u) + minout(head(u)) + tmin */
+    int64_t othr = minout ? kInf : -1; /* (-1: no state passes by OUT alone) */
+    if (minout)
+      for (uint32_t q = 0; q < np; ++q) {
+        const uint32_t b = W->pend[q];
+        const int64_t o = W->lab[b].k + minout[g->edge_dst[b]] + tmin;
+        if (o < othr) othr = o;
+      }
+    if (scans) *scans += np;
     for (uint32_t q = 0; q < np; ++q) {
       const uint32_t b = W->pend[q];
       const int64_t len = b == ei ? 0 : (int64_t)g->len_mm[b];
       const int64_t mq = len >> 8 < 255 ? len >> 8 : 255;
       const int64_t gap = (mq ? mq << 8 : 1) + (b == ei ? 0 : tmin);
-      if (W->lab[b].k < kmin + gap) W->nxt[nf++] = b;
+      if (W->lab[b].k < kmin + gap || W->lab[b].k < othr) W->nxt[nf++] = b;
       else {
         W->pend[kept++] = b;
         if (W->lab[b].k < knext) knext = W->lab[b].k;
@@ -158,6 +170,14 @@ int es_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
   int64_t tmin = md.turn[0];
   for (int i = 0; i <= 180; ++i)
     if (md.turn[i] < tmin) tmin = md.turn[i];
+  /* per node: the shortest out-edge the mode may use (quantized down to 256 mm) */
+  int64_t* minout = malloc(8 * (size_t)(g->h.n_nodes + 1));
+  for (uint32_t v = 0; v < g->h.n_nodes; ++v) {
+    int64_t m = kInf / 2;
+    for (uint32_t e = g->node_row[v]; e < g->node_row[v + 1]; ++e)
+      if ((g->edge_attr[e] & md.mode_bit) && (int64_t)g->len_mm[e] < m) m = g->len_mm[e];
+    minout[v] = m >= kInf / 2 ? m : (m >> 8) << 8;
+  }
   const int kmax = p[0].max_candidates < ORC_KMAX ? p[0].max_candidates : ORC_KMAX;
   static cand_t cands[4096][ORC_KMAX];
   static int kc[4096], act[4096];
@@ -219,8 +239,19 @@ int es_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
         }
         int64_t st, rd, st2, rd2, rl = 0, rl2 = 0;
         const int64_t keys =
-            es_search(&X, &W, ci->e, ci->p, Kb, tv, tpart, tpt, tej, 0, &st, &rd, &rl, &S->pend_max, 1);
-        (void)es_search(&X, &W, ci->e, ci->p, Kb, tv, tpart, tpt, tej, tmin, &st2, &rd2, &rl2, &S->pend_max, 0);
+            es_search(&X, &W, ci->e, ci->p, Kb, tv, tpart, tpt, tej, 0, &st, &rd, &rl, &S->pend_max, 1, NULL, NULL);
+        (void)es_search(&X, &W, ci->e, ci->p, Kb, tv, tpart, tpt, tej, tmin, &st2, &rd2, &rl2, &S->pend_max, 0, NULL,
+                        &S->scans_tmin);
+        int64_t st3, rd3, rl3 = 0;
+        (void)es_search(&X, &W, ci->e, ci->p, Kb, tv, tpart, tpt, tej, tmin, &st3, &rd3, &rl3, &S->pend_max, 0, minout,
+                        &S->scans_out);
+        if (getenv("ES_DEBUG") && (st3 != st2 || rd3 != rd2)) {
+          static int shown = 0;
+          if (shown++ < 5) fprintf(stderr, "search %lld: tmin st %lld rd %lld | out st %lld rd %lld\n",
+                                   (long long)S->searches, (long long)st2, (long long)rd2, (long long)st3, (long long)rd3);
+        }
+        S->settled_out += st3;
+        S->rounds_out += rd3;
         S->searches++;
         S->keys += keys;
         S->settled += st;
@@ -257,6 +288,7 @@ int es_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
   free(W.umask);
   free(W.pend);
   free(W.nxt);
+  free(minout);
   free(md.time_ds);
   return 0;
 }

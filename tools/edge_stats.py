@@ -26,7 +26,9 @@ class Stats(ctypes.Structure):
         'sources', 'union_settle_events', 'sum_settle_events')] + [
         ('hist_keys', ctypes.c_int64 * 64), ('hist_union', ctypes.c_int64 * 64), ('hist_rounds', ctypes.c_int64 * 64),
         ('pend_max', ctypes.c_int64), ('max_rounds_sum', ctypes.c_int64), ('relaxed', ctypes.c_int64),
-        ('groups', ctypes.c_int64), ('hist_bmm_keys', (ctypes.c_int64 * 24) * 24)]
+        ('groups', ctypes.c_int64), ('hist_bmm_keys', (ctypes.c_int64 * 24) * 24),
+        ('settled_out', ctypes.c_int64), ('rounds_out', ctypes.c_int64), ('scans_tmin', ctypes.c_int64),
+        ('scans_out', ctypes.c_int64)]
 
 
 def main():
@@ -63,6 +65,8 @@ def main():
         'keys_per_search': S.keys / n, 'settled_per_search': S.settled / n, 'relaxed_per_search': S.relaxed / n,
         'rounds_per_search': S.rounds / n,
         'settled_per_search_tmin': S.settled_tmin / n, 'rounds_per_search_tmin': S.rounds_tmin / n,
+        'settled_per_search_out': S.settled_out / n, 'rounds_per_search_out': S.rounds_out / n,
+        'pending_scanned_per_search_tmin': S.scans_tmin / n, 'pending_scanned_per_search_out': S.scans_out / n,
         'groups': S.groups, 'sources_per_group': S.sources / st, 'sum_keys_per_step': S.sum_keys / st,
         'union_keys_per_step': S.union_keys / st, 'max_rounds_per_step': S.max_rounds_sum / st,
         'settle_events_separate_per_step': S.sum_settle_events / st,
