@@ -14,6 +14,7 @@
 #include "otr_kernels.h"
 #include "otr_edge.h"
 #include "otr_edge1.h"
+#include "otr_edge2.h"
 #include "otr_ingest.h"
 
 namespace otr {
@@ -1041,6 +1042,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       for (int et = 0; et < 3; ++et) {
         const int slot = et == 0 ? 10 : (et == 1 ? 9 : 11);
         out->route_tier_code[slot] = 6000000 + (et == 0 ? OTR_E1CAP : (et == 1 ? 512 : 1024)) * 100 + 32;
+#ifdef OTR_E2CAP  // A/B build: the first edge tier runs two searches per wave (otr_edge2.h)
+        if (et == 0) out->route_tier_code[slot] = 6000000 + OTR_E2CAP * 100 + 2 * 32 + 1;
+#endif
         unsigned long long* c = cnt + (et == 0 ? 23 : 24 + et);
         k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x20u << et, list, c);
         RouteArgs rb = ra;
@@ -1051,7 +1055,11 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         // persistent grids: every resident wave (~22 per CU at 256 states, 13 at 512, 6 at
         // 1024); steps with more than 32 targets (modes keeping > 32 candidates) pass the
         // lean tiers (their TG = 32) on to k_general
+#ifdef OTR_E2CAP
+        if (et == 0) k_route_e2<OTR_E2CAP><<<8192, 64, 0, stream>>>(g, rb, rcn);
+#else
         if (et == 0) k_route_e1<OTR_E1CAP><<<8192, 64, 0, stream>>>(g, rb, rcn);
+#endif
         else if (et == 1) k_route_e1<512><<<4096, 64, 0, stream>>>(g, rb, rcn);
         else k_route_e1<1024><<<2048, 64, 0, stream>>>(g, rb, rcn);
         if (timing) (void)hipEventRecord(ev[24 + 2 * slot + 1], stream);
