@@ -147,7 +147,7 @@ typedef struct otr_tile_row {
 
 #define OTR_NO_ID 0xFFFFFFFFFFFFFFFFull
 
-/* kernel_ms slots */
+/* kernel_ms slots (OTR_STAGE_LINK: K_link, the per-state search inputs and the task records) */
 enum { OTR_STAGE_STATES = 0, OTR_STAGE_CANDIDATES, OTR_STAGE_LINK, OTR_STAGE_ROUTE, OTR_STAGE_ROUTE_BIG,
        OTR_STAGE_VITERBI, OTR_STAGE_PATHS, OTR_STAGE_PATHS_BIG, OTR_STAGE_SEGMENTS, OTR_STAGE_HISTOGRAM,
        OTR_STAGE_TOTAL };

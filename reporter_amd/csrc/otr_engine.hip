@@ -392,7 +392,7 @@ enum Slot {
   S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
-  S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST,
+  S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST, S_HE_PKEY,
   S_NUM
 };
 
@@ -734,9 +734,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   sb.ntrans = need<int64_t>(S_NTRANS, S);
   int64_t* task_off = need<int64_t>(S_TASK_OFF, S + 1);
   int64_t* trans_off = need<int64_t>(S_TRANS_OFF, S + 1);
-  tb(OTR_STAGE_LINK);
+  tb(OTR_STAGE_LINK);  // (K_link, the search inputs and the task records: through k_tasks)
   k_link<<<grid_for(T, 4), 256, 0, stream>>>(b, mp, trace_state_off, state_probe, cb.count, sb);
-  te(OTR_STAGE_LINK);
   // K2b: per-state search inputs
   PrepArgs pr{};
   pr.n_states = S;
@@ -806,6 +805,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     if (k32) k_tasks<2><<<grid_for((S + 1) / 2, 4), 256, 0, stream>>>(ta);
     else k_tasks<1><<<grid_for(S, 4), 256, 0, stream>>>(ta);
   }
+  te(OTR_STAGE_LINK);
   // turn cost tables of this batch's parameters (oracle orc_turn_table)
   int32_t* d_turn = need<int32_t>(S_TURN, 181 * OTR_MODES);
   h_turn.resize(181 * OTR_MODES);
@@ -1914,18 +1914,30 @@ __global__ void k_pair_file_heads(const otr_hist_entry* e, const int64_t* pair_s
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p < n_pairs) head[p] = p == 0 || e[pair_start[p]].file != e[pair_start[p - 1]].file ? 1 : 0;
 }
+// every pair's string-order keys (dec_key of id and next id) and total, one thread per
+// pair: the per-file reduction below then only compares
+struct PairKey {
+  unsigned long long s, n;
+  int64_t t;
+};
+__global__ void k_pair_keys(const otr_hist_entry* e, const int64_t* pair_start, int64_t n_pairs, int64_t n,
+                            const int64_t* csum, PairKey* K) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  const int64_t s = pair_start[p], t = p + 1 < n_pairs ? pair_start[p + 1] : n;
+  const otr_hist_entry& x = e[s];
+  K[p] = PairKey{dec_key(x.id), dec_key(x.next_id), csum[t - 1] - (s > 0 ? csum[s - 1] : 0)};
+}
 // one 256-thread block per file over its pairs [ffirst[f], ffirst[f + 1]): the top two pairs
 // by (dec_key(id), dec_key(next_id)) and their totals (dec_key > 0: 0 marks "none")
-__global__ __launch_bounds__(256) void k_pair_file_top2(const otr_hist_entry* e, const int64_t* pair_start,
-                                                        int64_t n_pairs, int64_t n, const int64_t* csum,
-                                                        const int64_t* ffirst, int64_t nf, PairFile* F) {
+__global__ __launch_bounds__(256) void k_pair_file_top2(const PairKey* K, int64_t n_pairs, const int64_t* ffirst,
+                                                        int64_t nf, PairFile* F) {
   const int64_t f = blockIdx.x;
   const int64_t p0 = ffirst[f], p1 = f + 1 < nf ? ffirst[f + 1] : n_pairs;
   PairFile T{0ull, 0ull, 0ull, 0ull, 0, 0};
   for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-    const int64_t s = pair_start[p], t = p + 1 < n_pairs ? pair_start[p + 1] : n;
-    const otr_hist_entry& x = e[s];
-    pf_add(T, dec_key(x.id), dec_key(x.next_id), csum[t - 1] - (s > 0 ? csum[s - 1] : 0));
+    const PairKey k = K[p];
+    pf_add(T, k.s, k.n, k.t);
   }
   __shared__ PairFile sh[256];
   sh[threadIdx.x] = T;
@@ -1941,19 +1953,16 @@ __global__ __launch_bounds__(256) void k_pair_file_top2(const otr_hist_entry* e,
   }
   if (threadIdx.x == 0) F[f] = T;
 }
-__global__ void k_entry_keep(const otr_hist_entry* e, const int64_t* pair_pos, const int64_t* pair_start,
-                             int64_t n_pairs, int64_t n, const int64_t* csum, const int64_t* fidx, const PairFile* F,
-                             int32_t privacy, int64_t* keep) {
+__global__ void k_entry_keep(const int64_t* pair_pos, int64_t n, const PairKey* K, const int64_t* fidx,
+                             const PairFile* F, int32_t privacy, int64_t* keep) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t p = pair_pos[i] - 1;
-  const int64_t s = pair_start[p], t = p + 1 < n_pairs ? pair_start[p + 1] : n;
-  const int64_t tot = csum[t - 1] - (s > 0 ? csum[s - 1] : 0);
-  bool k = tot >= (int64_t)privacy;
+  const PairKey pk = K[p];
+  bool k = pk.t >= (int64_t)privacy;
   const PairFile& f = F[fidx[p] - 1];
   if (f.s2 != 0ull && f.t1 == 1) {  // the file's string-last run is one line: judged with the run before it
-    const unsigned long long si = dec_key(e[i].id), sn = dec_key(e[i].next_id);
-    if ((si == f.s1 && sn == f.n1) || (si == f.s2 && sn == f.n2)) k = f.t2 + 1 >= (int64_t)privacy;
+    if ((pk.s == f.s1 && pk.n == f.n1) || (pk.s == f.s2 && pk.n == f.n2)) k = f.t2 + 1 >= (int64_t)privacy;
   }
   keep[i] = k ? 1 : 0;
 }
@@ -2085,10 +2094,13 @@ int Matcher::hist_reduce_impl(const void* in, int64_t n, int memory, int rows_in
     PairFile* pf = need<PairFile>(S_HE_PFILE, std::max<int64_t>(nf, 1));
     int64_t* ffirst = need<int64_t>(S_HE_FFIRST, std::max<int64_t>(nf, 1));
     if (!pf || !ffirst) return fail("device allocation failed (histogram)");
+    PairKey* pkey = need<PairKey>(S_HE_PKEY, std::max<int64_t>(np, 1));
+    if (!pkey) return fail("device allocation failed (histogram)");
     k_scatter_index<<<grid_for(np, 256), 256, 0, stream>>>(fhead, fidx, np, ffirst);
-    k_pair_file_top2<<<(unsigned)nf, 256, 0, stream>>>(e_red, rstart, np, nr, csum, ffirst, nf, pf);
+    k_pair_keys<<<grid_for(np, 256), 256, 0, stream>>>(e_red, rstart, np, nr, csum, pkey);
+    k_pair_file_top2<<<(unsigned)nf, 256, 0, stream>>>(pkey, np, ffirst, nf, pf);
     int64_t* keep = head;  // counts no longer needed
-    k_entry_keep<<<grid_for(nr, 256), 256, 0, stream>>>(e_red, pos, rstart, np, nr, csum, fidx, pf, privacy, keep);
+    k_entry_keep<<<grid_for(nr, 256), 256, 0, stream>>>(pos, nr, pkey, fidx, pf, privacy, keep);
     int64_t* kpos = rstart;  // pair starts no longer needed after k_entry_keep
     tb = tb_scan;
     HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, keep, kpos, nri, stream));

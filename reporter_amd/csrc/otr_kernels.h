@@ -2507,18 +2507,18 @@ struct TileLineLess {
 // in 18 base-11 digits (digit d → d + 1, padding → 0), is an integer whose numeric
 // order is the string order of the decimal strings (a proper prefix sorts first).
 // 11^18 < 2^63.  Fields are stable-sorted least significant first (LSD over fields).
+// Digits are taken least significant first by constant divisions (multiply-high), the
+// weight of the last digit being 11^(18 - n); a number of more than 18 digits keys on its
+// leading 18.
 __host__ __device__ inline unsigned long long dec_key(unsigned long long v) {
-  const int n = dec_digits(v);
-  unsigned long long p = 1;
-  for (int k = 1; k < n; ++k) p *= 10ull;
-  unsigned long long key = 0;
-  for (int k = 0; k < 18; ++k) {
-    unsigned long long d = 0;
-    if (k < n) {
-      d = (v / p) % 10ull + 1ull;
-      p /= 10ull;
-    }
-    key = key * 11ull + d;
+  int n = dec_digits(v);
+  for (; n > 18; --n) v /= 10ull;
+  unsigned long long m = 1, key = 0;
+  for (int k = n; k < 18; ++k) m *= 11ull;
+  for (int k = 0; k < n; ++k) {
+    key += (v % 10ull + 1ull) * m;
+    v /= 10ull;
+    m *= 11ull;
   }
   return key;
 }
