@@ -617,6 +617,13 @@ def main():
                        # host wall time of the last timed step: the matcher calls (kernels, their
                        # host syncs and copies) and the keyed histogram reduce / exchange
                        'step_wall_ms': timed_split,
+                       # one stream, one batch: the step = the matcher's timed stages + the
+                       # owner's keyed reduce + what neither covers (host syncs, launches)
+                       'step_accounting': ({'stage_sum_ms': round(sum(stage_ms.values()), 3),
+                                            'owner_reduce_ms': timed_split.get('histogram'),
+                                            'unaccounted_ms': round(1e3 * elapsed / args.steps - sum(stage_ms.values())
+                                                                    - (timed_split.get('histogram') or 0.0), 3)}
+                                           if ns == 1 and n_parts == 1 and world == 1 else None),
                        'route_kernels': tier_table,
                        'tile_stage': ({'privacy': args.tiles, 'rows': tile_stats[-1][0], 'kept': tile_stats[-1][1],
                                        'ms': round(1e3 * tile_stats[-1][2], 3)} if tile_stats else None),

@@ -20,9 +20,9 @@
 //   * probe loops are not unrolled, the target map is consulted only when a 64-bit bloom
 //     of the target nodes (a wave-uniform register) admits the settled node, and the
 //     wave's scalar state is kept small (no SGPR spills);
-//   * small tables: the first tier holds 256 states (table + lists + targets + the turn
-//     table in 7.3 KB: 21 waves per CU, 80 % of the C2 searches); a search that outgrows it
-//     goes on to 512 and 1024 states (this kernel again), then k_general: same results.
+//   * small tables: the first tier holds 320 states (table + lists + targets + the turn
+//     table in 8.4 KB: 19 waves per CU, ~93 % of the C2 searches); a search that outgrows
+//     it goes on to 512 and 1024 states (this kernel again), then k_general: same results.
 #pragma once
 #include <type_traits>
 
@@ -49,6 +49,10 @@ __device__ inline uint32_t er_t(const uint4& r) { return r.w & 0x1FFFFu; }
 #ifndef OTR_E1PF
 #define OTR_E1PF 0
 #endif
+// the first tier's settled-list size (states settled per round at most)
+#ifndef OTR_E1WCAP
+#define OTR_E1WCAP 64
+#endif
 // waves per SIMD the compiler fits the kernel's registers for (8: 64 VGPRs)
 #ifndef OTR_E1WAVES
 #define OTR_E1WAVES 8
@@ -58,7 +62,8 @@ template <int CAP>
 struct E1Lds {
   static constexpr int TG = 32;   // targets (steps with more go on to k_general)
   static constexpr int TM = 32;   // target-node map slots (a target node per target at most)
-  static constexpr int WCAP = CAP <= 256 ? 32 : 64;  // states settled per round (the rest wait)
+  // states settled per round (the rest wait; a round's relax passes cover 16 states each)
+  static constexpr int WCAP = CAP == OTR_E1CAP ? OTR_E1WCAP : (CAP <= 256 ? 32 : 64);
   using Idx = typename std::conditional<(CAP <= 256), uint8_t, uint16_t>::type;
   unsigned long long lab[CAP];  // gpack label, kGInf: none
   uint32_t key[CAP];            // edge id | kInq (on the pending list, or settled); kEmpty
@@ -181,7 +186,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
     DevGraph gr, RouteArgs a, unsigned long long* counters) {
   using LT = E1Lds<CAP>;
   constexpr int TG = LT::TG, TM = LT::TM, WCAP = LT::WCAP;
-  constexpr int kMaxKeys = (CAP * 7) / 8;
+  constexpr int kMaxKeys = CAP == OTR_E1CAP ? (CAP * OTR_E1LOAD) / 16 : (CAP * 7) / 8;
   __shared__ LT L;
   if (threadIdx.x == 0) L.turn_md = -1;
   const int64_t n = (int64_t)*a.list_count;

@@ -28,9 +28,13 @@
 #ifndef OTR_LOAD1
 #define OTR_LOAD1 7
 #endif
-// the lean first edge-state tier's table (otr_edge1.h)
+// the lean first edge-state tier's table (otr_edge1.h): 320 states (c2dep: 256 3.96M,
+// 320 4.37M, 384 4.17M probes/s); its load limit in sixteenths (14: 7/8)
 #ifndef OTR_E1CAP
-#define OTR_E1CAP 256
+#define OTR_E1CAP 320
+#endif
+#ifndef OTR_E1LOAD
+#define OTR_E1LOAD 14
 #endif
 
 namespace otr {
