@@ -1,6 +1,8 @@
 """Read-only numpy view of a flattened graph file (layout: include/otr_graph_format.h)."""
 import struct
 
+import os
+
 import numpy as np
 
 _HDR = struct.Struct('<8sII8I3d17Q')
@@ -169,6 +171,10 @@ def write_graph(path, node_ll, edges, segments=(), cell_deg=0.0005):
     hdr = _HDR.pack(b'OTRGRPH1', 1, 0, n_nodes, E, len(shape), len(segments), rows * cols, len(cell_edge),
                     rows, cols, gmin_lat, gmin_lon, cell_deg, *offs)
     blob[:_HDR.size] = hdr
-    with open(path, 'wb') as f:
+    # written beside the target and renamed over it: a reader (another test process
+    # building the same graph) never sees a partial file
+    tmp = '%s.%d.tmp' % (path, os.getpid())
+    with open(tmp, 'wb') as f:
         f.write(bytes(blob))
+    os.replace(tmp, path)
     return new_id
