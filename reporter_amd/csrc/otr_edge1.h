@@ -20,8 +20,8 @@
 //   * probe loops are not unrolled, the target map is consulted only when a 64-bit bloom
 //     of the target nodes (a wave-uniform register) admits the settled node, and the
 //     wave's scalar state is kept small (no SGPR spills);
-//   * small tables: the first tier holds 320 states (table + lists + targets + the turn
-//     table in 8.4 KB: 19 waves per CU, ~93 % of the C2 searches); a search that outgrows
+//   * small tables: the first tier holds 384 states (table + lists + targets + the turn
+//     table in 10.1 KB: 16 waves per CU, ~97 % of the C2 searches); a search that outgrows
 //     it goes on to 512 and 1024 states (this kernel again), then k_general: same results.
 #pragma once
 #include <type_traits>
@@ -51,7 +51,7 @@ __device__ inline uint32_t er_t(const uint4& r) { return r.w & 0x1FFFFu; }
 #endif
 // the first tier's settled-list size (states settled per round at most)
 #ifndef OTR_E1WCAP
-#define OTR_E1WCAP 64
+#define OTR_E1WCAP 32
 #endif
 // waves per SIMD the compiler fits the kernel's registers for (8: 64 VGPRs)
 #ifndef OTR_E1WAVES

@@ -28,10 +28,12 @@
 #ifndef OTR_LOAD1
 #define OTR_LOAD1 7
 #endif
-// the lean first edge-state tier's table (otr_edge1.h): 320 states (c2dep: 256 3.96M,
-// 320 4.37M, 384 4.17M probes/s); its load limit in sixteenths (14: 7/8)
+// the lean first edge-state tier's table (otr_edge1.h): 384 states with a 32-state settled
+// list, the largest table that keeps 16 waves per CU (10.1 KB of LDS each; c2dep: 256
+// states 3.96M, 320 4.37M, 352 4.80M, 368 4.90M, 384 5.01M probes/s, 384 with a 64-state
+// list 4.17M); its load limit in sixteenths (14: 7/8; 15: slower)
 #ifndef OTR_E1CAP
-#define OTR_E1CAP 320
+#define OTR_E1CAP 384
 #endif
 #ifndef OTR_E1LOAD
 #define OTR_E1LOAD 14
