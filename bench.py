@@ -61,8 +61,6 @@ def kernel_name(code, turns=False, first=False):
     if code < 0:  # the global-memory search: -1 on 32K-state slabs, -2 on 1M-state slabs
         return 'k_general' if code == -1 else 'k_general (1M-state slabs)'
     if 6000000 <= code < 7000000:  # the lean edge-state tiers: 6,000,000 + CAP * 100 + targets
-        if code % 100 == 65:  # (A/B build: two searches per wave, otr_edge2.h)
-            return 'k_route_e2<%d>' % ((code - 6000000) // 100)
         return 'k_route_e1<%d>' % ((code - 6000000) // 100)
     if code >= 7000000:  # the single-source edge-state tiers: 7,000,000 + CAP * 100 + targets
         return 'k_route_edge<%d, %d>' % ((code - 7000000) // 100, code % 100)

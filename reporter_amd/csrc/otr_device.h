@@ -155,6 +155,30 @@ __device__ inline int lane_id() { return (int)__lane_id(); }
 // Speed only; any placement gives the same results.  grid = 8 * per.
 __device__ inline int64_t xcd_remap(int64_t b, int64_t per) { return (b & 7) * per + (b >> 3); }
 
+// A dynamic work queue over a list of n units split into 8 contiguous ranges, one per XCD
+// (the dispatcher deals workgroups to XCDs round robin by blockIdx.x % 8): a one-wave
+// workgroup claims its range's next unit with one atomic on its XCD's counter (counters
+// 128 B apart, zeroed before the launch).  A wave that drew short searches takes more of
+// them, and the grid may hold any number of resident waves: a fixed stride over a grid
+// larger than the resident waves runs in generations whose last one can be a small tail.
+struct XcdQueue {
+  int64_t lo, hi;
+  unsigned long long* ctr;
+  __device__ XcdQueue(unsigned long long* q, int64_t n) {
+    const int64_t per = (n + 7) / 8;
+    lo = (int64_t)(blockIdx.x & 7) * per;
+    hi = lo + per < n ? lo + per : n;
+    ctr = q + 16 * (blockIdx.x & 7);
+  }
+  __device__ int64_t next() {  // (wave-uniform; one-wave workgroups)
+    unsigned long long v = 0;
+    if (threadIdx.x == 0) v = atomicAdd(ctr, 1ull);
+    const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return lo + (int64_t)(((unsigned long long)h << 32) | l);
+  }
+};
+
 // One 16-B load whose four words are all materialised here: keeps the compiler from
 // splitting a record load into dependent pieces sunk into the branches that use them.
 __device__ inline uint4 ld16(const uint4* p) {

@@ -20,9 +20,11 @@
 //   * probe loops are not unrolled, the target map is consulted only when a 64-bit bloom
 //     of the target nodes (a wave-uniform register) admits the settled node, and the
 //     wave's scalar state is kept small (no SGPR spills);
-//   * small tables: the first tier holds 384 states (table + lists + targets + the turn
-//     table in 10.1 KB: 16 waves per CU, ~97 % of the C2 searches); a search that outgrows
-//     it goes on to 512 and 1024 states (this kernel again), then k_general: same results.
+//   * small tables: the first tier holds 368 states (table + lists + targets + the turn
+//     table in 10.2 KB: 16 waves per CU, ~97 % of the C2 searches); a search that outgrows
+//     it goes on to 512 and 1024 states (this kernel again), then k_general: same results;
+//   * a state's head node, reversed end heading and IN-gap code share one 64-bit LDS word,
+//     and a settled state's label and that word one 16-B list entry.
 #pragma once
 #include <type_traits>
 
@@ -67,13 +69,9 @@ struct E1Lds {
   using Idx = typename std::conditional<(CAP <= 256), uint8_t, uint16_t>::type;
   unsigned long long lab[CAP];  // gpack label, kGInf: none
   uint32_t key[CAP];            // edge id | kInq (on the pending list, or settled); kEmpty
-  uint32_t node[CAP];           // dst(edge)
-  uint16_t hbk[CAP];            // the edge's end heading reversed
-  uint8_t mi[CAP];              // mi8_of(len(edge))
+  unsigned long long meta[CAP]; // e1_meta: dst(edge), its end heading reversed, mi8_of(len(edge))
   Idx pend[CAP];                // pending slots
-  unsigned long long wlab[WCAP];  // this round's settled states: their labels
-  uint32_t wnode[WCAP];         //   their nodes
-  uint16_t whbk[WCAP];          //   their reversed end headings
+  uint4 wst[WCAP];              // this round's settled states: {label, meta} (one 16-B access)
   unsigned long long tlab[TG];  // the targets' best feasible offers
   uint32_t tpart[TG], tpt[TG];  // entry parts (mm, 0.1 s)
   uint16_t thb[TG];             // begin heading of the target edge
@@ -84,10 +82,23 @@ struct E1Lds {
   int turn_md;
   uint32_t tmin;
   int n_pend, n_keys, overflow;
+#ifdef OTR_E1PAD  // (experiment: LDS padding that lowers the first tier's occupancy)
+  char pad[CAP == OTR_E1CAP ? OTR_E1PAD : 1];
+#endif
 };
 
 __device__ inline uint32_t tm_home(uint32_t v) { return (v * 0x9E3779B1u) >> 26; }  // 64 bloom bits
 __device__ inline uint32_t tm_slot(uint32_t v) { return (v * 0x9E3779B1u) >> 27; }  // 32 map slots
+
+// a state's static fields in one LDS word (written once when the state enters the table,
+// read with its label when it is settled): head node (28 bits), the edge's end heading
+// reversed (9), its IN-gap code mi8_of(len) (8)
+__device__ inline unsigned long long e1_meta(uint32_t node, uint32_t hbk, uint32_t mi) {
+  return (unsigned long long)node | ((unsigned long long)hbk << 28) | ((unsigned long long)mi << 37);
+}
+__device__ inline uint32_t em_node(unsigned long long m) { return (uint32_t)m & kAdjDstMask; }
+__device__ inline uint32_t em_hbk(unsigned long long m) { return (uint32_t)(m >> 28) & 0x1FFu; }
+__device__ inline uint8_t em_mi(unsigned long long m) { return (uint8_t)(m >> 37); }
 
 template <int CAP>
 __device__ inline int e1_insert(E1Lds<CAP>& L, uint32_t e, bool& isnew) {
@@ -142,9 +153,7 @@ __device__ inline int e1_relax(E1Lds<CAP>& L, unsigned long long lb, uint32_t hb
   const int sl = e1_insert(L, b, isnew);
   if (sl < 0) return -1;
   if (isnew) {
-    L.node[sl] = dw & kAdjDstMask;
-    L.hbk[sl] = (uint16_t)heading_back((int)hend);
-    L.mi[sl] = mi8_of(len);
+    L.meta[sl] = e1_meta(dw & kAdjDstMask, (uint32_t)heading_back((int)hend), mi8_of(len));
     L.lab[sl] = kGInf;
   }
   const unsigned long long nw = gpack(o.k, o.c, o.t);
@@ -177,7 +186,8 @@ __device__ inline void e1_turn_table(E1Lds<CAP>& L, const int32_t* turn_tab, int
 // ------------------------------------------------------------------------------
 // K3e1 kernel: a persistent grid over the device-side list of the turn-mode tasks (one
 // source candidate each), the 8 XCDs taking contiguous eighths of the list (consecutive
-// tasks = the candidates of one step, then the next steps of the trace: one neighbourhood).
+// tasks = the candidates of one step, then the next steps of the trace: one neighbourhood),
+// each wave claiming its next task from its XCD's queue (XcdQueue).
 // A search that outgrows the table flags its task for the next tier: 6 (512 states), 7
 // (1024), 3 (k_general, global-memory labels).
 // ------------------------------------------------------------------------------
@@ -189,14 +199,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
   constexpr int kMaxKeys = CAP == OTR_E1CAP ? (CAP * OTR_E1LOAD) / 16 : (CAP * 7) / 8;
   __shared__ LT L;
   if (threadIdx.x == 0) L.turn_md = -1;
-  const int64_t n = (int64_t)*a.list_count;
   const int lane = (int)threadIdx.x;
-  const int64_t per = (n + 7) / 8;
-  const int64_t lo = (int64_t)(blockIdx.x & 7) * per;
-  const int64_t hi = lo + per < n ? lo + per : n;
-  const int64_t stride = (int64_t)(gridDim.x >> 3);
+  XcdQueue q(a.queue, (int64_t)*a.list_count);
   unsigned long long cyc_res = 0, cyc_part = 0, cyc_relax = 0, cyc_other = 0;  // (OTR_STAMPS)
-  for (int64_t w = lo + (int64_t)(blockIdx.x >> 3); w < hi; w += stride) {
+  for (int64_t w = q.next(); w < q.hi; w = q.next()) {
     OTR_STAMP(ts0);
     const int64_t task = a.task_list[w];
     const uint4 r0 = a.rec[3 * task], r1 = a.rec[3 * task + 1], r2 = a.rec[3 * task + 2];
@@ -267,9 +273,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
       if (lane == 0) {
         bool isnew = false;
         const int sl = e1_insert(L, ei, isnew);  // (an empty table: the home slot)
-        L.node[sl] = gr.edge_dst[ei];
-        L.hbk[sl] = (uint16_t)heading_back((int)(uint16_t)gr.edge_head[ei].y);
-        L.mi[sl] = 0;  // the root: label 0 is final at once (gap 1 mm)
+        // the root: label 0 is final at once (mi 0: gap 1 mm)
+        L.meta[sl] = e1_meta(gr.edge_dst[ei], (uint32_t)heading_back((int)(uint16_t)gr.edge_head[ei].y), 0u);
         L.lab[sl] = gpack(0u, 0u, 0u);
         L.key[sl] = ei | kInq;
         L.pend[0] = (typename LT::Idx)sl;
@@ -303,37 +308,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           const int k = base + lane;
           const bool in = k < npend;
           int sl = 0;
-          unsigned long long lb = 0;
-          uint32_t nd = 0, hk = 0;
+          unsigned long long lb = 0, mt = 0;
           bool take = false;
           if (in) {
             sl = L.pend[k];
             lb = L.lab[sl];
-            nd = L.node[sl];  // (read beside the label: the relax lanes then need no dependent read)
-            hk = L.hbk[sl];
-            take = (uint64_t)g_k(lb) < (uint64_t)kmin + in_gap8(L.mi[sl]) + tmin;
+            mt = L.meta[sl];  // (read beside the label: the relax lanes then need no dependent read)
+            take = (uint64_t)g_k(lb) < (uint64_t)kmin + in_gap8(em_mi(mt)) + tmin;
           }
           take = take && nw + prefix_count(__ballot(take)) < WCAP;
           const bool keep = in && !take;
-          const unsigned long long mt = __ballot(take), mk = __ballot(keep);
+          const unsigned long long mtk = __ballot(take), mk = __ballot(keep);
           __syncthreads();
           if (take) {
-            const int wq = nw + prefix_count(mt);
-            L.wlab[wq] = lb;
-            L.wnode[wq] = nd;
-            L.whbk[wq] = (uint16_t)hk;
+            const int wq = nw + prefix_count(mtk);
+            L.wst[wq] = make_uint4((uint32_t)lb, (uint32_t)(lb >> 32), (uint32_t)mt, (uint32_t)(mt >> 32));
 #if OTR_E1PF
             // touch the state's adjacency records now: the relax lanes' loads of them, after
             // the barrier, then come from the near cache instead of L2 (pf is kept live
             // until after the relax loop, so its register is not reused while in flight)
-            pf |= *(const volatile uint32_t*)(er + 4 * (size_t)nd);
+            pf |= *(const volatile uint32_t*)(er + 4 * (size_t)em_node(mt));
 #endif
           } else if (keep) {
             L.pend[kept + prefix_count(mk)] = (typename LT::Idx)sl;
             knext = g_k(lb) < knext ? g_k(lb) : knext;
             dnext = g_d(lb) < dnext ? g_d(lb) : dnext;
           }
-          nw += __popcll(mt);
+          nw += __popcll(mtk);
           kept += __popcll(mk);
           __syncthreads();
         }
@@ -347,8 +348,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           int psl = -1;
           bool isnew = false;
           if (k < 4 * nw) {
-            const unsigned long long lb = L.wlab[k >> 2];
-            const uint32_t v = L.wnode[k >> 2], hbk = L.whbk[k >> 2];
+            const uint4 ws = L.wst[k >> 2];
+            const unsigned long long lb = ((unsigned long long)ws.y << 32) | ws.x;
+            const unsigned long long wm = ((unsigned long long)ws.w << 32) | ws.z;
+            const uint32_t v = em_node(wm), hbk = em_hbk(wm);
             const int slot = k & 3;
             // the record load is issued first and waited for only after the target offers
             // (LDS work), so the two latencies overlap
@@ -380,8 +383,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           for (int base = 0; base < 4 * nw; base += OTR_WAVE) {
             const int k = base + lane;
             if (k < 4 * nw && (k & 3) == 3) {
-              const unsigned long long lb = L.wlab[k >> 2];
-              const uint32_t v = L.wnode[k >> 2], hbk = L.whbk[k >> 2];
+              const uint4 ws = L.wst[k >> 2];
+              const unsigned long long lb = ((unsigned long long)ws.y << 32) | ws.x;
+              const unsigned long long wm = ((unsigned long long)ws.w << 32) | ws.z;
+              const uint32_t v = em_node(wm), hbk = em_hbk(wm);
               if (er[4 * (size_t)v + 3].x & kAdjMore) {
                 const uint32_t* et = gr.et(md);
 #pragma unroll 1

@@ -14,7 +14,6 @@
 #include "otr_kernels.h"
 #include "otr_edge.h"
 #include "otr_edge1.h"
-#include "otr_edge2.h"
 #include "otr_ingest.h"
 
 namespace otr {
@@ -392,7 +391,7 @@ enum Slot {
   S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
-  S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST, S_HE_PKEY,
+  S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST, S_HE_PKEY, S_QUEUE,
   S_NUM
 };
 
@@ -964,6 +963,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       ra.force_edge = fe ? atoi(fe) : 0;
     }
 #endif
+    // the list tiers' work queues (XcdQueue): 8 counters per launch, 128 B apart
+    constexpr int kQueueWords = 16 * 8;
+    unsigned long long* queues = need<unsigned long long>(S_QUEUE, 16 * kQueueWords);
+    HIPCHK(hipMemsetAsync(queues, 0, 8 * 16 * kQueueWords, stream));
     tb(OTR_STAGE_ROUTE);
     if (node_tasks) {
       // one unit (G searches) per block, in launches of at most 2^25 blocks: a dispatch's
@@ -1002,6 +1005,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.list_count = c;
+      rb.queue = queues + tier * kQueueWords;
       unsigned long long* rcn = rwork ? d_counters + (2 + tier) * bank : nullptr;
       out->route_tier_code[1 + tier] = tiers[tier];
       if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier)], stream);
@@ -1029,6 +1033,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       RouteArgs rb = ra;
       rb.task_list = list;
       rb.list_count = c;
+      rb.queue = queues + 8 * kQueueWords;
       out->route_tier_code[8] = 900000 + 2048;
       if (timing) (void)hipEventRecord(ev[24 + 2 * 8], stream);
       if (rwork) k_route<2048, 1, true, true, true><<<4096, 64, 0, stream>>>(g, rb, d_counters + 7 * bank);
@@ -1042,24 +1047,19 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       for (int et = 0; et < 3; ++et) {
         const int slot = et == 0 ? 10 : (et == 1 ? 9 : 11);
         out->route_tier_code[slot] = 6000000 + (et == 0 ? OTR_E1CAP : (et == 1 ? 512 : 1024)) * 100 + 32;
-#ifdef OTR_E2CAP  // A/B build: the first edge tier runs two searches per wave (otr_edge2.h)
-        if (et == 0) out->route_tier_code[slot] = 6000000 + OTR_E2CAP * 100 + 2 * 32 + 1;
-#endif
         unsigned long long* c = cnt + (et == 0 ? 23 : 24 + et);
         k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x20u << et, list, c);
         RouteArgs rb = ra;
         rb.task_list = list;
         rb.list_count = c;
+        rb.queue = queues + (9 + et) * kQueueWords;
         unsigned long long* rcn = rwork ? d_counters + (et == 0 ? 10 : (et == 1 ? 1 : 11)) * bank : nullptr;
         if (timing) (void)hipEventRecord(ev[24 + 2 * slot], stream);
-        // persistent grids: every resident wave (~22 per CU at 256 states, 13 at 512, 6 at
-        // 1024); steps with more than 32 targets (modes keeping > 32 candidates) pass the
-        // lean tiers (their TG = 32) on to k_general
-#ifdef OTR_E2CAP
-        if (et == 0) k_route_e2<OTR_E2CAP><<<8192, 64, 0, stream>>>(g, rb, rcn);
-#else
+        // persistent grids of at least every resident wave (16 per CU at 384 states, 13 at
+        // 512, 6 at 1024) claiming tasks from per-XCD queues; steps with more than 32
+        // targets (modes keeping > 32 candidates) pass the lean tiers (their TG = 32) on to
+        // k_general
         if (et == 0) k_route_e1<OTR_E1CAP><<<8192, 64, 0, stream>>>(g, rb, rcn);
-#endif
         else if (et == 1) k_route_e1<512><<<4096, 64, 0, stream>>>(g, rb, rcn);
         else k_route_e1<1024><<<2048, 64, 0, stream>>>(g, rb, rcn);
         if (timing) (void)hipEventRecord(ev[24 + 2 * slot + 1], stream);

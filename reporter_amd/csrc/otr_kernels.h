@@ -28,12 +28,11 @@
 #ifndef OTR_LOAD1
 #define OTR_LOAD1 7
 #endif
-// the lean first edge-state tier's table (otr_edge1.h): 384 states with a 32-state settled
-// list, the largest table that keeps 16 waves per CU (10.1 KB of LDS each; c2dep: 256
-// states 3.96M, 320 4.37M, 352 4.80M, 368 4.90M, 384 5.01M probes/s, 384 with a 64-state
-// list 4.17M); its load limit in sixteenths (14: 7/8; 15: slower)
+// the lean first edge-state tier's table (otr_edge1.h): 368 states with a 32-state settled
+// list, 10.2 KB of LDS, 16 waves per CU (c2dep, work queues: 368 5.71M, 384 at 15 waves
+// 5.35M probes/s); its load limit in sixteenths (14: 7/8; 15: slower)
 #ifndef OTR_E1CAP
-#define OTR_E1CAP 384
+#define OTR_E1CAP 368
 #endif
 #ifndef OTR_E1LOAD
 #define OTR_E1LOAD 14
@@ -1066,6 +1065,7 @@ struct RouteArgs {
   uint32_t tier_keys[8];      // key capacity of each retry tier, in order
   int n_tiers;
   int64_t unit_base;          // first tier: the launch's first unit (launches of < 2^32 work-items)
+  unsigned long long* queue;  // list tiers: this launch's 8 per-XCD unit counters (XcdQueue), zeroed
   unsigned long long* stamps;  // diagnostic build (OTR_STAMPS): bank 0 of the work counters (phase cycles)
   int force_edge;             // test build only (OTR_FORCE_RETRY, env OTR_FORCE_EDGE): bits 0 / 1 / 2 fail
                               // every 256 / 512 / 1024-state edge-state route search (the next tier
@@ -1443,7 +1443,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   }
   const int64_t n_tasks = (int64_t)*a.list_count;
   const int64_t n_units = (n_tasks + G - 1) / G;
-  for (int64_t w = blockIdx.x; w < n_units; w += gridDim.x) {
+  XcdQueue q(a.queue, n_units);
+  for (int64_t w = q.next(); w < q.hi; w = q.next()) {
     route_unit<CAP, G, LIST, WIDE, CNT>(gr, a, counters, Ls, w, n_tasks, sink, trec);
     __syncthreads();  // the next unit re-initialises the tables
   }
