@@ -20,11 +20,13 @@
 //   * probe loops are not unrolled, the target map is consulted only when a 64-bit bloom
 //     of the target nodes (a wave-uniform register) admits the settled node, and the
 //     wave's scalar state is kept small (no SGPR spills);
-//   * small tables: the first tier holds 368 states (table + lists + targets + the turn
-//     table in 10.2 KB: 16 waves per CU, ~97 % of the C2 searches); a search that outgrows
+//   * small tables: the first tier holds 360 states (table + lists + targets + the turn
+//     table in 10.1 KB: 16 waves per CU, ~96 % of the C2 searches); a search that outgrows
 //     it goes on to 512 and 1024 states (this kernel again), then k_general: same results;
 //   * a state's head node, reversed end heading and IN-gap code share one 64-bit LDS word,
-//     and a settled state's label and that word one 16-B list entry.
+//     and a settled state's label and that word one 16-B list entry;
+//   * the relax step is branch-free on its common path (e1_relax_sink);
+//   * waves claim tasks from per-XCD queues (XcdQueue, otr_device.h).
 #pragma once
 #include <type_traits>
 
@@ -55,6 +57,11 @@ __device__ inline uint32_t er_t(const uint4& r) { return r.w & 0x1FFFFu; }
 #ifndef OTR_E1WCAP
 #define OTR_E1WCAP 32
 #endif
+// the main relax loop without branches on its common path (e1_relax_sink), with this
+// many scratch words (0: the branching e1_relax)
+#ifndef OTR_E1SINK
+#define OTR_E1SINK 16
+#endif
 // waves per SIMD the compiler fits the kernel's registers for (8: 64 VGPRs)
 #ifndef OTR_E1WAVES
 #define OTR_E1WAVES 8
@@ -82,6 +89,9 @@ struct E1Lds {
   int turn_md;
   uint32_t tmin;
   int n_pend, n_keys, overflow;
+#if OTR_E1SINK
+  unsigned long long sink[OTR_E1SINK];  // e1_relax_sink: the lanes' scratch words (never read)
+#endif
 #ifdef OTR_E1PAD  // (experiment: LDS padding that lowers the first tier's occupancy)
   char pad[CAP == OTR_E1CAP ? OTR_E1PAD : 1];
 #endif
@@ -163,6 +173,63 @@ __device__ inline int e1_relax(E1Lds<CAP>& L, unsigned long long lb, uint32_t hb
   dnext = o.d < dnext ? o.d : dnext;
   return (atomicOr(&L.key[sl], kInq) & kInq) ? -1 : sl;
 }
+
+#if OTR_E1SINK
+// e1_relax with its common path branch-free (as relax_sink, otr_kernels.h): every lane
+// issues the insert, the new state's stores, the label and the pending-bit atomics, a lane
+// with nothing to do aiming them at its own scratch word L.sink[lane], so the exec-mask
+// bookkeeping of the nested ifs (scalar-unit work) is gone.  Only a probe chain past the
+// home slot branches.  Same slots, labels and pending list as e1_relax.
+template <int CAP>
+__device__ inline int e1_relax_sink(E1Lds<CAP>& L, unsigned long long lb, uint32_t hbk, uint32_t dw, uint32_t len,
+                                    uint32_t tt, uint32_t b, uint32_t hb, uint32_t hend, uint32_t pd, uint32_t pt,
+                                    uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext, uint32_t& dnext,
+                                    bool& isnew) {
+  unsigned long long* mine = &L.sink[threadIdx.x % OTR_E1SINK];  // (lanes sharing a word: a few-way atomic)
+  uint32_t* mine32 = reinterpret_cast<uint32_t*>(mine);
+  const bool mode_ok = (((dw >> 28) & 7u) & mode_bit) != 0u;
+  relaxed += mode_ok ? 1u : 0u;
+  const uint32_t tc = (uint32_t)L.turn[turn_from_back((int)hbk, (int)hb)];
+  const EOffer o = e_step(lb, tc, len, tt);
+  bool go = mode_ok && e_feasible(o, pd, pt);
+  const uint32_t h0 = hslot<CAP>(b);
+  const uint32_t k0 = atomicCAS(go ? &L.key[h0] : mine32, kEmpty, b);
+  isnew = go && k0 == kEmpty;
+  int sl = (go && (k0 == kEmpty || (k0 & kNodeMask) == b)) ? (int)h0 : -1;
+  const bool coll = go && sl < 0;
+  if (__ballot(coll) != 0ull) {  // the home slot holds another edge: linear probing
+    if (coll) {
+      uint32_t hh = h0;
+#pragma unroll 1
+      for (int probe = 1; probe < CAP; ++probe) {
+        hh = hh + 1 == (uint32_t)CAP ? 0u : hh + 1;
+        const uint32_t k = atomicCAS(&L.key[hh], kEmpty, b);
+        if (k == kEmpty) {
+          isnew = true;
+          sl = (int)hh;
+          break;
+        }
+        if ((k & kNodeMask) == b) {
+          sl = (int)hh;
+          break;
+        }
+      }
+      if (sl < 0) L.overflow = 1;
+    }
+  }
+  go = go && sl >= 0;
+  const bool fresh = go && isnew;
+  *(fresh ? &L.meta[sl] : mine) = e1_meta(dw & kAdjDstMask, (uint32_t)heading_back((int)hend), mi8_of(len));
+  *(fresh ? &L.lab[sl] : mine) = kGInf;
+  const unsigned long long nw = gpack(o.k, o.c, o.t);
+  const unsigned long long old = atomicMin(go ? &L.lab[sl] : mine, nw);
+  const bool imp = go && nw < old;
+  knext = (imp && o.k < knext) ? o.k : knext;
+  dnext = (imp && o.d < dnext) ? o.d : dnext;
+  const uint32_t was = atomicOr(imp ? &L.key[sl] : mine32, kInq);
+  return (imp && !(was & kInq)) ? sl : -1;
+}
+#endif
 
 template <int CAP>
 __device__ inline void e1_turn_table(E1Lds<CAP>& L, const int32_t* turn_tab, int md) {
@@ -361,8 +428,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
               if ((bloom >> tm_home(v)) & 1ull) e1_target_offers(L, lb, hbk, v, pd, pt);
             }
             asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w));  // (one 16-B load, not split)
+#if OTR_E1SINK
+            psl = e1_relax_sink(L, lb, hbk, r.x & ~kAdjMore, r.y, timed ? er_t(r) : 0u, er_edge(r), er_hb(r), er_he(r),
+                                pd, pt, mode_bit, my_relaxed, knext, dnext, isnew);
+#else
             psl = e1_relax(L, lb, hbk, r.x & ~kAdjMore, r.y, timed ? er_t(r) : 0u, er_edge(r), er_hb(r), er_he(r), pd,
                            pt, mode_bit, my_relaxed, knext, dnext, isnew);
+#endif
             tail = tail || (slot == 3 && (r.x & kAdjMore));
           }
           nkeys += __popcll(__ballot(isnew));

@@ -972,8 +972,19 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       // one unit (G searches) per block, in launches of at most 2^25 blocks: a dispatch's
       // grid size counts work-items in 32 bits (178M tasks at 12.5M probes would wrap)
       const int64_t units = route_g == 2 ? (NT + 1) / 2 : NT;
+#if OTR_FIRST_Q
+      {
+        RouteArgs rf = ra;
+        rf.queue = queues + 12 * kQueueWords;
+        if (route_g == 2) OTR_ROUTE_LAUNCH(OTR_CAP1, 2, false, 16384, rf, rwork);
+        else OTR_ROUTE_LAUNCH(256, 1, false, 16384, rf, rwork);
+      }
+      constexpr int64_t kMaxUnits = 0;  // (no chunked launches)
+      for (int64_t base = 0; kMaxUnits > 0 && base < units; base += kMaxUnits) {
+#else
       constexpr int64_t kMaxUnits = 1ll << 25;
       for (int64_t base = 0; base < units; base += kMaxUnits) {
+#endif
         RouteArgs rf = ra;
         rf.unit_base = base;
         const int64_t u = std::min<int64_t>(kMaxUnits, units - base);
@@ -998,7 +1009,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // the first tier's flagged tasks, once; every later collect scans only them
     k_collect_flagged<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, flagged, cnt + 24);
     constexpr unsigned kCollectGrid = 512;
-    for (int tier = 0; tier < ntier; ++tier) {
+    for (int tier = 0; tier < (node_tasks ? ntier : 0); ++tier) {  // (no node task: no node tier)
       unsigned long long* c = cnt + tier;
       k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf,
                                                             0x2u | (((2u << tier) - 1u) << 16), list + 0, c);
@@ -1416,8 +1427,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   };
   for (int k = 0; k < OTR_COUNTERS; ++k) out->counters[k] = ctr(0, k);
   // per route kernel: searches, settled, relaxed, transition entries (banks 0, 2..6, 8..9;
-  // slot 8, the 64-bit LDS tier: bank 7; slot 9, the 384-state edge tier: bank 1; slot 10,
-  // the multi-source edge tier: bank 10; slot 11, the 2048-state edge tier: bank 11)
+  // slot 8, the 64-bit LDS tier: bank 7; the edge-state tiers: slot 10 the first (bank 10),
+  // slot 9 the 512-state one (bank 1), slot 11 the 1024-state one (bank 11))
   for (int t = 0; t < 12; ++t) {
     const int b = t == 0 ? 0 : (t < 6 ? 1 + t : (t < 8 ? 2 + t : (t == 8 ? 7 : (t == 9 ? 1 : t))));
     out->route_tier_work[t][0] = ctr(b, 6);

@@ -28,11 +28,15 @@
 #ifndef OTR_LOAD1
 #define OTR_LOAD1 7
 #endif
-// the lean first edge-state tier's table (otr_edge1.h): 368 states with a 32-state settled
-// list, 10.2 KB of LDS, 16 waves per CU (c2dep, work queues: 368 5.71M, 384 at 15 waves
-// 5.35M probes/s); its load limit in sixteenths (14: 7/8; 15: slower)
+#ifndef OTR_FIRST_Q
+#define OTR_FIRST_Q 0
+#endif
+// the lean first edge-state tier's table (otr_edge1.h): 360 states with a 32-state settled
+// list and 16 relax scratch words, 10.1 KB of LDS, 16 waves per CU (c2dep with work queues:
+// branching relax at 368 states 5.71M, 384 at 15 waves 5.35M; branch-free relax at 360
+// states 6.12M probes/s); its load limit in sixteenths (14: 7/8; 15: slower)
 #ifndef OTR_E1CAP
-#define OTR_E1CAP 368
+#define OTR_E1CAP 360
 #endif
 #ifndef OTR_E1LOAD
 #define OTR_E1LOAD 14
@@ -1433,12 +1437,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   __shared__ uint32_t sink_row[OTR_WAVE];  // relax_sink's per-lane scratch words (32-bit tables)
   uint32_t* sink = WIDE ? nullptr : sink_row;
 #endif
-  if (!LIST) {  // the first tier: one unit per block, XCD-mapped (no loop: fewer live registers)
+  if (!LIST) {
+    const int64_t n_units = (a.n_tasks + G - 1) / G;
+#if OTR_FIRST_Q  // A/B build: a persistent first tier over per-XCD work queues
+    XcdQueue q(a.queue, n_units);
+    for (int64_t w = q.next(); w < q.hi; w = q.next()) {
+      route_unit<CAP, G, LIST, WIDE, CNT>(gr, a, counters, Ls, w, a.n_tasks, sink, trec);
+      __syncthreads();
+    }
+#else
+    // the first tier: one unit per block, XCD-mapped (no loop: fewer live registers);
     // units [unit_base, unit_base + gridDim.x): a launch's grid stays below 2^32 work-items
     // (the dispatch packet's grid size), so a large batch is several launches
-    const int64_t n_units = (a.n_tasks + G - 1) / G;
     const int64_t w = a.unit_base + xcd_remap(blockIdx.x, (int64_t)gridDim.x / 8);
     if (w < n_units) route_unit<CAP, G, LIST, WIDE, CNT>(gr, a, counters, Ls, w, a.n_tasks, sink, trec);
+#endif
     return;
   }
   const int64_t n_tasks = (int64_t)*a.list_count;
