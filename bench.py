@@ -46,7 +46,7 @@ T_BEGIN = 1483228800
 # HBM bytes per launch of the dominant kernel from separate FETCH_SIZE / WRITE_SIZE
 # --pmc passes of this command (tools/profile_gpu.sh, tools/pmc_summary.py), when the
 # committed summary holds the kernel
-PMC_SUMMARY = os.environ.get('OTR_PMC_SUMMARY', os.path.join(ROOT, 'profiles', 'r03_final_pmc.json'))
+PMC_SUMMARY = os.environ.get('OTR_PMC_SUMMARY', os.path.join(ROOT, 'profiles', 'r04_final_pmc.json'))
 
 
 def log(*a):

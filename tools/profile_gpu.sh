@@ -11,10 +11,10 @@ O=gpurun_out/prof
 mkdir -p $O
 STEPS=${STEPS:-5}
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- \
-  python3 bench.py --steps $STEPS --warmup 2 --cpu-traces 0 > $O/bench_kt.json 2> $O/bench_kt.err
+  python3 bench.py --steps $STEPS --warmup 2 --cpu-traces 0 --e2e-steps 0 > $O/bench_kt.json 2> $O/bench_kt.err
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/$c -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --cpu-traces 0 > $O/bench_$c.json 2> $O/bench_$c.err
+    python3 bench.py --steps 2 --warmup 1 --cpu-traces 0 --e2e-steps 0 > $O/bench_$c.json 2> $O/bench_$c.err
   timeout -k 10 200 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/cal_$c -o run -- \
     ./reporter_amd/tools/calib_fetch > $O/calib.json 2> $O/calib_$c.err
 done
