@@ -195,10 +195,10 @@ typedef struct otr_batch_result {
   /* per route-search kernel: slot 0 the first tier (k_route<160,2>), 1..5 the LDS retry
    * tiers in order, 6 / 7 the global-memory search (32K / 1M-state slabs), 8 the 64-bit
    * label LDS tier (steps whose length and time bits exceed 32), 10 the first edge-state
-   * tier (modes with turn costs), 9 / 11 the larger edge-state tables (768, then 2048 states).
-   * code: 6,000,000 + CAP*100 + targets of the first edge-state tier, 7,000,000 + CAP*100 +
-   * targets of the larger ones, CAP*10+G
-   * of an LDS tier, 900000 + CAP the 64-bit tier, -1 / -2 the global tiers, 0 unused.
+   * tier (modes with turn costs), 9 / 11 the larger edge-state tables (512, then 1024 states).
+   * code: 6,000,000 + CAP*100 + targets of an edge-state tier, CAP*10+G of an LDS tier,
+   * 900000 + CAP the 64-bit tier, -1 / -2 the global tiers, 0 unused (a tier with no task
+   * kind to run: the node tiers when every mode has turn costs).
    * work: searches, settled nodes (expanded states), relaxed edges, transition entries
    * written.  ms (OTR_BATCH_TIMING): HIP-event time of the kernel on the matcher's stream. */
   int32_t route_tier_code[12];

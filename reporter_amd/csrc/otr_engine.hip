@@ -662,9 +662,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   }
   h_trace_status.assign(T, OTR_OK);
   // counter banks of OTR_COUNTERS kinds x kCShards: 0 the batch (and the first route
-  // tier), 1 the 384-state edge tier, 2..6 the LDS retry tiers, 7 the 64-bit tier, 8..9 the
-  // global-memory tiers, 10 the multi-source edge tier, 11 the 2048-state edge tier; folded
-  // at the end into n_ctr values behind them
+  // tier), 1 the 512-state edge tier, 2..6 the LDS retry tiers, 7 the 64-bit tier, 8..9 the
+  // global-memory tiers, 10 the first edge tier, 11 the 1024-state edge tier; folded at
+  // the end into n_ctr values behind them
   constexpr int kBanks = 12;
   const size_t bank = (size_t)OTR_COUNTERS * kCShards;
   const size_t n_ctr = kBanks * (size_t)OTR_COUNTERS;
@@ -948,7 +948,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     if (CTR) k_route<C, G_, LIST_, false, true><<<GRID, 64, 0, stream>>>(g, ARGS, CTR);      \
     else k_route<C, G_, LIST_, false, false><<<GRID, 64, 0, stream>>>(g, ARGS, nullptr);     \
   } while (0)
-    // turn-mode (edge-state) tasks belong to the multi-source edge tier below: the node
+    // turn-mode (edge-state) tasks belong to the edge-state tiers below: the node
     // tiers pass them on unflagged, and when every mode has turn costs (the deployed
     // configuration) no node task exists and the first node tier is not launched at all
     const bool turns = turn_modes != 0u;

@@ -1180,11 +1180,12 @@ __device__ inline int nth_set_bit(unsigned long long m, int q) {
 
 // one unit = G search tasks of the wave (ordinal w of the task range or list).  LIST =
 // false: the first tier, one unit per block over all tasks (XCD-mapped); LIST = true: a
-// retry tier, a fixed grid striding over the device-side task list (its length never
-// crosses to the host).  WIDE: the table keeps 64-bit packed words and takes the tasks
-// whose (length << sh | time) words do not fit 32 bits (`general` in the record).  The
-// LDS tiers run node-mode tasks; turn-mode (edge-based) tasks are `general` from k_tasks
-// and go to k_general.
+// retry tier, a fixed grid whose waves claim units of the device-side task list from
+// per-XCD queues (its length never crosses to the host).  WIDE: the table keeps 64-bit
+// packed words and takes the tasks whose (length << sh | time) words do not fit 32 bits
+// (`general` in the record).  The LDS tiers run node-mode tasks; turn-mode (edge-state)
+// tasks carry flag 5 from k_tasks and run in the edge-state tiers (otr_edge1.h), then
+// k_general.
 template <int CAP, int G, bool LIST, bool WIDE = false, bool CNT = true>
 __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& a, unsigned long long* counters,
                                            SearchLds<CAP, WIDE ? 2 : 0>* Ls, int64_t w, int64_t n_tasks,
@@ -1387,7 +1388,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
 #ifdef OTR_FORCE_GENERAL
     a.overflow_flag[task] = 3;  // test build: every search (edge-state ones too) in k_general
 #else
-    // (turn-mode tasks carry flag 5 from k_tasks, or belong to the multi-source tier)
+    // (turn-mode tasks carry flag 5 from k_tasks: the edge-state tiers take them)
     if (!turn) a.overflow_flag[task] = general ? 3 : (start_tier >= 0 ? 16 + start_tier : 1);
 #endif
   }

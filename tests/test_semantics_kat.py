@@ -290,7 +290,7 @@ def test_semantics_gpu_parity(kat, slow, square, opts):
     errors, _ = compare(_lib.result_to_numpy(r), po.match_batch(po.Graph(qpath), b, po.params(**opts)))
     assert not errors, errors
     if opts.get('turn_penalty_factor', 1) != 0:
-        # turn modes: the edge-state search (the multi-source tier, or the single-source ones)
+        # turn modes: the edge-state search (the first edge tier, or the 512-state one)
         assert int(r.route_tier_work[10][0]) + int(r.route_tier_work[9][0]) > 0
     spath, sid = slow
     M.configure(M.default_config(spath, **opts))
