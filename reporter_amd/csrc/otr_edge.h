@@ -481,9 +481,9 @@ __global__ __launch_bounds__(64) void k_paths_edge(DevGraph gr, PathArgs a, cons
   __shared__ EdgeLds<CAP, 32> L;
   __shared__ uint32_t s_rev[CAP];
   if (threadIdx.x == 0) L.turn_md = -1;
-  const int64_t n_list = (int64_t)*list_count;
   const int lane = (int)threadIdx.x;
-  for (int64_t w = blockIdx.x; w < n_list; w += gridDim.x) {
+  XcdQueue q(a.queue, (int64_t)*list_count);  // (waves claim steps: no fixed-stride generations)
+  for (int64_t w = q.next(); w < q.hi; w = q.next()) {
     const int64_t k = step_list[w];
     const int64_t s = a.steps[k];
     const int64_t sp = a.prev[s];

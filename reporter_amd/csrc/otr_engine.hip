@@ -391,7 +391,7 @@ enum Slot {
   S_IN_ACC, S_IN_KEEP, S_IN_KPOS, S_IN_KIDX, S_IN_KEY_A, S_IN_KEY_B, S_IN_VAL_A, S_IN_VAL_B, S_IN_HEAD, S_IN_GID,
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
-  S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST, S_HE_PKEY, S_QUEUE,
+  S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST, S_HE_PKEY, S_QUEUE, S_PQUEUE,
   S_NUM
 };
 
@@ -1185,13 +1185,19 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       }
       te(OTR_STAGE_PATHS);
       tb(OTR_STAGE_PATHS_BIG);
-      // large-table retries for table overflows (flag 1), on device-side lists
+      // large-table retries for table overflows (flag 1), on device-side lists; each
+      // launch's waves claim steps from its own per-XCD queue (XcdQueue)
+      constexpr int kPQWords = 16 * 8;
+      unsigned long long* pq = need<unsigned long long>(S_PQUEUE, 8 * kPQWords);
+      HIPCHK(hipMemsetAsync(pq, 0, 8 * 8 * kPQWords, stream));
       for (int tier = 0; tier < 3; ++tier) {
         unsigned long long* c = cnt + 12 + tier;
         k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0x2u, list, c);
-        if (tier == 0) k_paths<512, 1><<<16384, 64, 0, stream>>>(g, pa, list, c);
-        else if (tier == 1) k_paths<1024, 1><<<8192, 64, 0, stream>>>(g, pa, list, c);
-        else k_paths<4096, 1><<<4096, 64, 0, stream>>>(g, pa, list, c);
+        PathArgs pb = pa;
+        pb.queue = pq + tier * kPQWords;
+        if (tier == 0) k_paths<512, 1><<<16384, 64, 0, stream>>>(g, pb, list, c);
+        else if (tier == 1) k_paths<1024, 1><<<8192, 64, 0, stream>>>(g, pb, list, c);
+        else k_paths<4096, 1><<<4096, 64, 0, stream>>>(g, pb, list, c);
       }
       // turn-cost winners (flag 5): the edge-state LDS search, 384 then 2048 states
       if (turn_modes != 0u) {
@@ -1199,8 +1205,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
           unsigned long long* c = cnt + 27 + et;
           k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, et == 0 ? 0x20u : 0x40u,
                                                                        list, c);
-          if (et == 0) k_paths_edge<384><<<4096, 64, 0, stream>>>(g, pa, d_turn, list, c, 6);
-          else k_paths_edge<2048><<<512, 64, 0, stream>>>(g, pa, d_turn, list, c, 3);
+          PathArgs pb = pa;
+          pb.queue = pq + (3 + et) * kPQWords;
+          if (et == 0) k_paths_edge<384><<<4096, 64, 0, stream>>>(g, pb, d_turn, list, c, 6);
+          else k_paths_edge<2048><<<512, 64, 0, stream>>>(g, pb, d_turn, list, c, 3);
         }
       }
       // 64-bit labels, the largest-table overflows and what the edge tiers left: k_general

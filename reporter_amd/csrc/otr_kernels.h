@@ -1755,6 +1755,7 @@ struct PathArgs {
   const int64_t* trans_off;    // the route lengths k_route found (u32 mm per transition)
   const uint32_t* trans;
   int force_edge;              // test build only (OTR_FORCE_RETRY): RouteArgs::force_edge bits 3-4
+  unsigned long long* queue;   // list tiers: this launch's per-XCD step counters (XcdQueue), zeroed
 };
 
 // G searches per wave (G = 2 for the first tier, lanes split 32/32), each a
@@ -1768,10 +1769,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
   const int gl = Gr::gl();
   const int64_t n_list = (int64_t)(step_list ? *list_count : *a.n_steps_dev);
   const int64_t n_units = (n_list + G - 1) / G;
-  // first tier: grid = 8 x (upper bound of units / 8), XCD-mapped, one unit per block
-  const int64_t w0 = step_list ? (int64_t)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x / 8);
-  const int64_t wstep = step_list ? (int64_t)gridDim.x : ((int64_t)gridDim.x + n_units);
-  for (int64_t w = w0; w < n_units; w += wstep) {
+  // first tier: grid = 8 x (upper bound of units / 8), XCD-mapped, one unit per block;
+  // retry tiers: waves claim units from per-XCD queues
+  XcdQueue q(a.queue, step_list ? n_units : 0);
+  const int64_t wend = step_list ? q.hi : n_units;
+  for (int64_t w = step_list ? q.next() : xcd_remap(blockIdx.x, gridDim.x / 8); w < wend;
+       w = step_list ? q.next() : wend) {
   const int64_t iw = w * G + Gr::g();
   const bool have = iw < n_list;
   const int64_t k = have ? (step_list ? step_list[iw] : iw) : 0;
