@@ -570,7 +570,9 @@ static std::vector<int> route_tiers() {
     const int cap = atoi(item.c_str());
     const int gw = item.find('x') != std::string::npos ? atoi(item.c_str() + item.find('x') + 1) : 1;
     const int code = cap * 10 + gw;
-    if (code == 2561 || code == 5121 || code == 10241 || code == 20481 || code == 3842 || code == 4482 || code == 5122) t.push_back(code);
+    if (code == 2561 || code == 5121 || code == 7681 || code == 10241 || code == 20481 || code == 3842 || code == 4482 ||
+        code == 5122)
+      t.push_back(code);
     i = j + 1;
   }
   if (t.size() > 4) t.resize(4);  // at most 5 retry tiers (otr_batch_result route_tier_*)
@@ -1024,6 +1026,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       switch (tiers[tier]) {
         case 2561: OTR_TIER(256, 1); break;
         case 5121: OTR_TIER(512, 1); break;
+        case 7681: OTR_TIER(768, 1); break;
         case 10241: OTR_TIER(1024, 1); break;
         case 20481: OTR_TIER(2048, 1); break;
         case 3842: OTR_TIER(384, 2); break;
