@@ -78,12 +78,14 @@ def main():
     }
     print(json.dumps(out, indent=1))
     hb = np.array([[S.hist_bmm_keys[i][j] for j in range(24)] for i in range(24)])
-    print('route bound (100 m) -> searches, mean keys, P(keys > 224)')
+    print('route bound (100 m) -> searches, mean keys, P(keys > 224), P(keys > 320), share of all keys > 320')
+    over = hb[:, 10:].sum()
     for i in range(24):
         n_i = hb[i].sum()
         if n_i:
             mk = (hb[i] * (np.arange(24) * 32 + 16)).sum() / n_i
-            print('  %4d m: %7d  %6.1f  %.3f' % (i * 100, n_i, mk, hb[i][7:].sum() / n_i))
+            print('  %4d m: %7d  %6.1f  %.3f  %.3f  %.3f' % (i * 100, n_i, mk, hb[i][7:].sum() / n_i, hb[i][10:].sum() / n_i,
+                                                           hb[i][10:].sum() / max(over, 1)))
 
 
 if __name__ == '__main__':
