@@ -165,10 +165,13 @@ struct XcdQueue {
   int64_t lo, hi;
   unsigned long long* ctr;
   __device__ XcdQueue(unsigned long long* q, int64_t n) {
-    const int64_t per = (n + 7) / 8;
-    lo = (int64_t)(blockIdx.x & 7) * per;
+    // (a grid of fewer than 8 workgroups would leave ranges unclaimed: one range then)
+    const int parts = gridDim.x >= 8 ? 8 : 1;
+    const int x = parts == 8 ? (int)(blockIdx.x & 7) : 0;
+    const int64_t per = (n + parts - 1) / parts;
+    lo = (int64_t)x * per;
     hi = lo + per < n ? lo + per : n;
-    ctr = q + 16 * (blockIdx.x & 7);
+    ctr = q + 16 * x;
   }
   __device__ int64_t next() {  // (wave-uniform; one-wave workgroups)
     unsigned long long v = 0;

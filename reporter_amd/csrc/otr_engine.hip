@@ -1005,9 +1005,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     tb(OTR_STAGE_ROUTE_BIG);
     static const std::vector<int> tiers = route_tiers();
     const int ntier = (int)tiers.size();
-    // persistent grids: twice the resident waves of the widest tier (256 CUs x 4 SIMDs x
-    // 8 waves), so no tier is starved; blocks past the list length exit at once
-    const unsigned tgrid = 16384;
+    // persistent grids over per-XCD queues: about twice a tier's resident waves (256 CUs x
+    // 4 SIMDs x 8 waves for the small tables, fewer for the big ones, whose LDS admits
+    // fewer); a block that finds its queue drained exits at once
     // the first tier's flagged tasks, once; every later collect scans only them
     k_collect_flagged<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, flagged, cnt + 24);
     constexpr unsigned kCollectGrid = 512;
@@ -1022,7 +1022,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       unsigned long long* rcn = rwork ? d_counters + (2 + tier) * bank : nullptr;
       out->route_tier_code[1 + tier] = tiers[tier];
       if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier)], stream);
-#define OTR_TIER(C, G_) OTR_ROUTE_LAUNCH(C, G_, true, tgrid, rb, rcn)
+#define OTR_TIER(C, G_) OTR_ROUTE_LAUNCH(C, G_, true, (C) <= 512 ? 16384u : 16384u * 512u / (C), rb, rcn)
       switch (tiers[tier]) {
         case 2561: OTR_TIER(256, 1); break;
         case 5121: OTR_TIER(512, 1); break;
@@ -1950,9 +1950,9 @@ __global__ void k_pair_keys(const otr_hist_entry* e, const int64_t* pair_start, 
   const otr_hist_entry& x = e[s];
   K[p] = PairKey{dec_key(x.id), dec_key(x.next_id), csum[t - 1] - (s > 0 ? csum[s - 1] : 0)};
 }
-// one 256-thread block per file over its pairs [ffirst[f], ffirst[f + 1]): the top two pairs
+// one 1024-thread block per file over its pairs [ffirst[f], ffirst[f + 1]): the top two pairs
 // by (dec_key(id), dec_key(next_id)) and their totals (dec_key > 0: 0 marks "none")
-__global__ __launch_bounds__(256) void k_pair_file_top2(const PairKey* K, int64_t n_pairs, const int64_t* ffirst,
+__global__ __launch_bounds__(1024) void k_pair_file_top2(const PairKey* K, int64_t n_pairs, const int64_t* ffirst,
                                                         int64_t nf, PairFile* F) {
   const int64_t f = blockIdx.x;
   const int64_t p0 = ffirst[f], p1 = f + 1 < nf ? ffirst[f + 1] : n_pairs;
@@ -1961,10 +1961,10 @@ __global__ __launch_bounds__(256) void k_pair_file_top2(const PairKey* K, int64_
     const PairKey k = K[p];
     pf_add(T, k.s, k.n, k.t);
   }
-  __shared__ PairFile sh[256];
+  __shared__ PairFile sh[1024];
   sh[threadIdx.x] = T;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
+  for (int w = 512; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) {
       const PairFile U = sh[threadIdx.x + w];
       if (U.s1) pf_add(T, U.s1, U.n1, U.t1);
@@ -2120,7 +2120,7 @@ int Matcher::hist_reduce_impl(const void* in, int64_t n, int memory, int rows_in
     if (!pkey) return fail("device allocation failed (histogram)");
     k_scatter_index<<<grid_for(np, 256), 256, 0, stream>>>(fhead, fidx, np, ffirst);
     k_pair_keys<<<grid_for(np, 256), 256, 0, stream>>>(e_red, rstart, np, nr, csum, pkey);
-    k_pair_file_top2<<<(unsigned)nf, 256, 0, stream>>>(pkey, np, ffirst, nf, pf);
+    k_pair_file_top2<<<(unsigned)nf, 1024, 0, stream>>>(pkey, np, ffirst, nf, pf);
     int64_t* keep = head;  // counts no longer needed
     k_entry_keep<<<grid_for(nr, 256), 256, 0, stream>>>(pos, nr, pkey, fidx, pf, privacy, keep);
     int64_t* kpos = rstart;  // pair starts no longer needed after k_entry_keep
