@@ -15,6 +15,9 @@
 //     crosses a turn >= tmin and the state's own edge): lab(b) < kmin + len(b) + tmin is
 //     final, and a target is final once tlab < kmin + tpart + tmin — fewer rounds, the
 //     same final labels;
+//   * a target is also resolved once the smallest pending route time plus its entry time
+//     breaks the time bound (no later offer can be feasible): ~7 % fewer rounds at C2
+//     (tools/edge_stats.py);
 //   * settled states keep their pending bit (a final label can never improve, so it is
 //     never pushed again): no write per settled state;
 //   * probe loops are not unrolled, the target map is consulted only when a 64-bit bloom
@@ -154,7 +157,8 @@ __device__ inline void e1_target_offers(E1Lds<CAP>& L, unsigned long long lb, ui
 template <int CAP>
 __device__ inline int e1_relax(E1Lds<CAP>& L, unsigned long long lb, uint32_t hbk, uint32_t dw, uint32_t len,
                                uint32_t tt, uint32_t b, uint32_t hb, uint32_t hend, uint32_t pd, uint32_t pt,
-                               uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext, uint32_t& dnext, bool& isnew) {
+                               uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext, uint32_t& dnext, uint32_t& tnext,
+                               bool& isnew) {
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
   const uint32_t tc = (uint32_t)L.turn[turn_from_back((int)hbk, (int)hb)];
@@ -171,6 +175,7 @@ __device__ inline int e1_relax(E1Lds<CAP>& L, unsigned long long lb, uint32_t hb
   if (nw >= old) return -1;
   knext = o.k < knext ? o.k : knext;
   dnext = o.d < dnext ? o.d : dnext;
+  tnext = o.t < tnext ? o.t : tnext;
   return (atomicOr(&L.key[sl], kInq) & kInq) ? -1 : sl;
 }
 
@@ -184,7 +189,7 @@ template <int CAP>
 __device__ inline int e1_relax_sink(E1Lds<CAP>& L, unsigned long long lb, uint32_t hbk, uint32_t dw, uint32_t len,
                                     uint32_t tt, uint32_t b, uint32_t hb, uint32_t hend, uint32_t pd, uint32_t pt,
                                     uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext, uint32_t& dnext,
-                                    bool& isnew) {
+                                    uint32_t& tnext, bool& isnew) {
   unsigned long long* mine = &L.sink[threadIdx.x % OTR_E1SINK];  // (lanes sharing a word: a few-way atomic)
   uint32_t* mine32 = reinterpret_cast<uint32_t*>(mine);
   const bool mode_ok = (((dw >> 28) & 7u) & mode_bit) != 0u;
@@ -226,6 +231,7 @@ __device__ inline int e1_relax_sink(E1Lds<CAP>& L, unsigned long long lb, uint32
   const bool imp = go && nw < old;
   knext = (imp && o.k < knext) ? o.k : knext;
   dnext = (imp && o.d < dnext) ? o.d : dnext;
+  tnext = (imp && o.t < tnext) ? o.t : tnext;
   const uint32_t was = atomicOr(imp ? &L.key[sl] : mine32, kInq);
   return (imp && !(was & kInq)) ? sl : -1;
 }
@@ -350,25 +356,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
       const uint4* er = gr.erec + (size_t)md * gr.erec_stride;
       const uint32_t mode_bit = 1u << md;
       const uint32_t tmin = L.tmin;
-      uint32_t kmin = 0, dmin = 0;  // the smallest pending key / length
+      uint32_t kmin = 0, dmin = 0, tmn = 0;  // the smallest pending key / length / time
       int npend = 1, nkeys = 1;
       uint32_t pf = 0;  // (OTR_E1PF: the prefetch loads' sink)
 #pragma unroll 1
       for (;;) {
         OTR_STAMP(tr0);
-        // ---- targets: every later offer to a target has key >= kmin + tpart + tmin and
-        // length >= dmin + tpart; done when every needed target is final or unreachable
+        // ---- targets: every later offer to a target has key >= kmin + tpart + tmin,
+        // length >= dmin + tpart and route time >= tmn + tpt (every later label descends
+        // from a pending one); done when every needed target is final or unreachable
         bool res = true;
         if (tgt) {
           const unsigned long long tl = L.tlab[lane];
           res = (tl != kGInf && (uint64_t)g_k(tl) < (uint64_t)kmin + tpart + tmin) ||
-                (uint64_t)dmin + tpart > (uint64_t)pd;
+                (uint64_t)dmin + tpart > (uint64_t)pd || (uint64_t)tmn + tpt > (uint64_t)pt;
         }
         if (__ballot(!res) == 0ull || npend == 0) break;
         OTR_STAMP(tr1);
         // ---- partition: final pending states (IN criterion) to the settled list; the
         // rest stay and give the next kmin / dmin
-        uint32_t knext = 0xFFFFFFFFu, dnext = 0xFFFFFFFFu;
+        uint32_t knext = 0xFFFFFFFFu, dnext = 0xFFFFFFFFu, tnext = 0xFFFFFFFFu;
         int kept = 0, nw = 0;
 #pragma unroll 1
         for (int base = 0; base < npend; base += OTR_WAVE) {
@@ -400,6 +407,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
             L.pend[kept + prefix_count(mk)] = (typename LT::Idx)sl;
             knext = g_k(lb) < knext ? g_k(lb) : knext;
             dnext = g_d(lb) < dnext ? g_d(lb) : dnext;
+            tnext = g_t(lb) < tnext ? g_t(lb) : tnext;
           }
           nw += __popcll(mtk);
           kept += __popcll(mk);
@@ -430,10 +438,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
             asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w));  // (one 16-B load, not split)
 #if OTR_E1SINK
             psl = e1_relax_sink(L, lb, hbk, r.x & ~kAdjMore, r.y, timed ? er_t(r) : 0u, er_edge(r), er_hb(r), er_he(r),
-                                pd, pt, mode_bit, my_relaxed, knext, dnext, isnew);
+                                pd, pt, mode_bit, my_relaxed, knext, dnext, tnext, isnew);
 #else
             psl = e1_relax(L, lb, hbk, r.x & ~kAdjMore, r.y, timed ? er_t(r) : 0u, er_edge(r), er_hb(r), er_he(r), pd,
-                           pt, mode_bit, my_relaxed, knext, dnext, isnew);
+                           pt, mode_bit, my_relaxed, knext, dnext, tnext, isnew);
 #endif
             tail = tail || (slot == 3 && (r.x & kAdjMore));
           }
@@ -468,7 +476,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
                   bool nw2 = false;
                   const int p2 = e1_relax(L, lb, hbk, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e,
                                           (uint32_t)(uint16_t)hh.x, (uint32_t)(uint16_t)hh.y, pd, pt, mode_bit,
-                                          my_relaxed, knext, dnext, nw2);
+                                          my_relaxed, knext, dnext, tnext, nw2);
                   if (nw2) atomicAdd(&L.n_keys, 1);
                   if (p2 >= 0) L.pend[atomicAdd(&L.n_pend, 1)] = (typename LT::Idx)p2;
                 }
@@ -483,6 +491,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
         __syncthreads();
         kmin = wave_min_u32(knext);
         dmin = wave_min_u32(dnext);
+        tmn = wave_min_u32(tnext);
 #ifdef OTR_STAMPS
         OTR_STAMP(tr4);
         cyc_res += (tr1 - tr0) + (tr4 - tr3);

@@ -21,6 +21,7 @@ typedef struct {
   int64_t pend_max, max_rounds_sum, relaxed, groups;
   int64_t hist_bmm_keys[24][24]; /* [route bound / 100 m][keys / 32] */
   int64_t settled_out, rounds_out, scans_tmin, scans_out; /* + the OUT criterion; pending entries examined */
+  int64_t settled_tterm, rounds_tterm;                     /* + the time-bound target resolution */
 } es_stats;
 
 typedef struct {
@@ -45,6 +46,8 @@ static void es_touch(es_ws* W, uint32_t e) {
   }
 }
 
+static int g_tterm; /* also resolve a target once every pending label's time + its entry time breaks the bound */
+
 /* one simulated search; returns keys; *settled, *rounds out */
 static int64_t es_search(const rctx* X, es_ws* W, uint32_t ei, double pi, int ntg, const uint32_t* tv,
                          const int64_t* tpart, const int64_t* tpt, const uint32_t* tej, int64_t tmin,
@@ -68,19 +71,20 @@ static int64_t es_search(const rctx* X, es_ws* W, uint32_t ei, double pi, int nt
   if (record) es_touch(W, ei);
   rkey tl[ORC_KMAX];
   for (int j = 0; j < ntg; ++j) tl[j] = (rkey){kInf, kInf, kInf};
-  int64_t kmin = 0, dmin = 0;
+  int64_t kmin = 0, dmin = 0, tminp = 0;
   for (;;) {
     if (np == 0) break;
     int unres = 0;
     for (int j = 0; j < ntg; ++j) {
       if (tv[j] == 0xFFFFFFFFu) continue;
-      const int res = (tl[j].k < kInf && tl[j].k < kmin + tpart[j] + tmin) || dmin + tpart[j] > pd;
+      const int res = (tl[j].k < kInf && tl[j].k < kmin + tpart[j] + tmin) || dmin + tpart[j] > pd ||
+                      (g_tterm && X->time_on && tminp + tpt[j] > pt);
       if (!res) unres = 1;
     }
     if (!unres) break;
     const int64_t r = *rounds;
     ++*rounds;
-    int64_t knext = kInf, dnext = kInf;
+    int64_t knext = kInf, dnext = kInf, tnext = kInf;
     uint32_t nf = 0, kept = 0;
     /* OUT criterion (minout != NULL): every later offer leaves a pending state u through
        one of its head's out-edges: key >= k(u) + minout(head(u)) + tmin */
@@ -102,6 +106,7 @@ static int64_t es_search(const rctx* X, es_ws* W, uint32_t ei, double pi, int nt
         W->pend[kept++] = b;
         if (W->lab[b].k < knext) knext = W->lab[b].k;
         if (W->lab[b].d < dnext) dnext = W->lab[b].d;
+        if (W->lab[b].t < tnext) tnext = W->lab[b].t;
       }
     }
     np = kept;
@@ -138,6 +143,7 @@ static int64_t es_search(const rctx* X, es_ws* W, uint32_t ei, double pi, int nt
           W->lab[e] = o;
           if (o.k < knext) knext = o.k;
           if (o.d < dnext) dnext = o.d;
+          if (o.t < tnext) tnext = o.t;
           if (W->flag[e] == 0) {
             W->flag[e] = 1;
             W->pend[np++] = e;
@@ -148,6 +154,7 @@ static int64_t es_search(const rctx* X, es_ws* W, uint32_t ei, double pi, int nt
     if (np > *pend_max) *pend_max = np;
     kmin = knext;
     dmin = dnext;
+    tminp = tnext;
   }
   return keys;
 }
@@ -252,6 +259,12 @@ int es_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
         }
         S->settled_out += st3;
         S->rounds_out += rd3;
+        g_tterm = 1;
+        int64_t st4, rd4, rl4 = 0;
+        (void)es_search(&X, &W, ci->e, ci->p, Kb, tv, tpart, tpt, tej, tmin, &st4, &rd4, &rl4, &S->pend_max, 0, NULL, NULL);
+        g_tterm = 0;
+        S->settled_tterm += st4;
+        S->rounds_tterm += rd4;
         S->searches++;
         S->keys += keys;
         S->settled += st;
