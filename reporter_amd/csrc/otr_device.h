@@ -173,13 +173,18 @@ struct XcdQueue {
     hi = lo + per < n ? lo + per : n;
     ctr = q + 16 * x;
   }
-  __device__ int64_t next() {  // (wave-uniform; one-wave workgroups)
+  // claim(): the atomic, its result in lane 0 (not waited for); take(): the claimed unit
+  __device__ unsigned long long claim() {
     unsigned long long v = 0;
     if (threadIdx.x == 0) v = atomicAdd(ctr, 1ull);
+    return v;
+  }
+  __device__ int64_t take(unsigned long long v) const {
     const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
     const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
     return lo + (int64_t)(((unsigned long long)h << 32) | l);
   }
+  __device__ int64_t next() { return take(claim()); }  // (wave-uniform; one-wave workgroups)
 };
 
 // One 16-B load whose four words are all materialised here: keeps the compiler from
