@@ -56,9 +56,12 @@ __device__ inline uint32_t er_t(const uint4& r) { return r.w & 0x1FFFFu; }
 #ifndef OTR_E1PF
 #define OTR_E1PF 0
 #endif
-// the first tier's settled-list size (states settled per round at most)
+// the first tier's settled-list size (states settled per round at most), and the larger tiers'
 #ifndef OTR_E1WCAP
 #define OTR_E1WCAP 32
+#endif
+#ifndef OTR_E1WCAP2
+#define OTR_E1WCAP2 64
 #endif
 // the main relax loop without branches on its common path (e1_relax_sink), with this
 // many scratch words (0: the branching e1_relax)
@@ -75,7 +78,7 @@ struct E1Lds {
   static constexpr int TG = 32;   // targets (steps with more go on to k_general)
   static constexpr int TM = 32;   // target-node map slots (a target node per target at most)
   // states settled per round (the rest wait; a round's relax passes cover 16 states each)
-  static constexpr int WCAP = CAP == OTR_E1CAP ? OTR_E1WCAP : (CAP <= 256 ? 32 : 64);
+  static constexpr int WCAP = CAP == OTR_E1CAP ? OTR_E1WCAP : (CAP <= 256 ? 32 : OTR_E1WCAP2);
   using Idx = typename std::conditional<(CAP <= 256), uint8_t, uint16_t>::type;
   unsigned long long lab[CAP];  // gpack label, kGInf: none
   uint32_t key[CAP];            // edge id | kInq (on the pending list, or settled); kEmpty
