@@ -5,8 +5,9 @@
 // The semantics are otr_edge.h's (one source candidate per wave, states = edges, 64-bit
 // labels key << 38 | (cap - turn) << 17 | time, exact IN-criterion rounds, the bounds
 // pruning during the search, targets offered by every settled state at src(ej)); what
-// changes is the cost of a round, which is what bounds this search (measured: ~13 rounds
-// of ~600 wave instructions each, a third of the SIMD's VALU issue used at 4.25 waves):
+// changes is the cost of a round, which is what bounds this search (otr_edge.h's kernel,
+// measured: ~13 rounds of ~600 wave instructions each, a third of the SIMD's VALU issue
+// used at 4.25 waves per SIMD; this one: 4 waves per SIMD):
 //   * one 16-B per-mode record per relaxation (DevGraph::erec: head, length, edge id,
 //     route time, begin and end headings) instead of four loads;
 //   * the state keeps its edge's reversed end heading, and turn degrees are two compares
@@ -97,9 +98,6 @@ struct E1Lds {
   int n_pend, n_keys, overflow;
 #if OTR_E1SINK
   unsigned long long sink[OTR_E1SINK];  // e1_relax_sink: the lanes' scratch words (never read)
-#endif
-#ifdef OTR_E1PAD  // (experiment: LDS padding that lowers the first tier's occupancy)
-  char pad[CAP == OTR_E1CAP ? OTR_E1PAD : 1];
 #endif
 };
 
