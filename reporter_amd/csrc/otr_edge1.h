@@ -195,11 +195,14 @@ __device__ inline int e1_relax_sink(E1Lds<CAP>& L, unsigned long long lb, uint32
   uint32_t* mine32 = reinterpret_cast<uint32_t*>(mine);
   const bool mode_ok = (((dw >> 28) & 7u) & mode_bit) != 0u;
   relaxed += mode_ok ? 1u : 0u;
-  const uint32_t tc = (uint32_t)L.turn[turn_from_back((int)hbk, (int)hb)];
-  const EOffer o = e_step(lb, tc, len, tt);
-  bool go = mode_ok && e_feasible(o, pd, pt);
+  // the insert needs only the length and time bounds (neither depends on the turn), so
+  // its CAS and the turn-table read are in flight together; an offer that then breaks the
+  // turn-cost cap leaves a key without a label (never pending: same labels)
+  bool go = mode_ok && g_d(lb) + len <= pd && g_t(lb) + tt <= pt;
   const uint32_t h0 = hslot<CAP>(b);
   const uint32_t k0 = atomicCAS(go ? &L.key[h0] : mine32, kEmpty, b);
+  const uint32_t tc = (uint32_t)L.turn[turn_from_back((int)hbk, (int)hb)];
+  const EOffer o = e_step(lb, tc, len, tt);
   isnew = go && k0 == kEmpty;
   int sl = (go && (k0 == kEmpty || (k0 & kNodeMask) == b)) ? (int)h0 : -1;
   const bool coll = go && sl < 0;
@@ -228,8 +231,9 @@ __device__ inline int e1_relax_sink(E1Lds<CAP>& L, unsigned long long lb, uint32
   *(fresh ? &L.meta[sl] : mine) = e1_meta(dw & kAdjDstMask, (uint32_t)heading_back((int)hend), mi8_of(len));
   *(fresh ? &L.lab[sl] : mine) = kGInf;
   const unsigned long long nw = gpack(o.k, o.c, o.t);
-  const unsigned long long old = atomicMin(go ? &L.lab[sl] : mine, nw);
-  const bool imp = go && nw < old;
+  const bool feas = go && o.c <= kTcCap;
+  const unsigned long long old = atomicMin(feas ? &L.lab[sl] : mine, nw);
+  const bool imp = feas && nw < old;
   knext = (imp && o.k < knext) ? o.k : knext;
   dnext = (imp && o.d < dnext) ? o.d : dnext;
   tnext = (imp && o.t < tnext) ? o.t : tnext;
