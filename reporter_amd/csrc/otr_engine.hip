@@ -1124,8 +1124,13 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   va.subpath = need<int32_t>(S_SUBPATH, S);
   tb(OTR_STAGE_VITERBI);
   {
-    // two traces per wave when no mode keeps more than 32 candidates (K <= 32 lanes)
-    if (k32) {
+    // two traces per wave when no mode keeps more than 32 candidates (K <= 32 lanes); a
+    // batch too small to fill the GPU that way (fewer than 8,192 traces: C1's 1,000) runs
+    // one trace per wave with each step's predecessor scan split over the two halves
+    static const int64_t split_below = getenv("OTR_VIT_SPLIT") ? atoll(getenv("OTR_VIT_SPLIT")) : 8192;  // A/B knob
+    if (k32 && T < split_below) {
+      k_viterbi<1, true><<<(unsigned)(T < 1048576 ? T : 1048576), 64, 0, stream>>>(va, d_counters);
+    } else if (k32) {
       const int64_t w = (T + 1) / 2;
       k_viterbi<2><<<(unsigned)(w < 1048576 ? w : 1048576), 64, 0, stream>>>(va, d_counters);
     } else {

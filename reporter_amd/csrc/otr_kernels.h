@@ -1568,12 +1568,63 @@ __device__ __forceinline__ void vit_scan(const uint32_t* tr, const uint32_t* tcr
   *bi_io = bi;
 }
 
+// vit_scan over the predecessors i = h, h + 2, ... only (SPLIT: the two halves of a wave
+// scan the even and the odd predecessors of candidate j; vit_pair joins them)
+template <bool TURNS, int U = 8>
+__device__ __forceinline__ void vit_scan_half(const uint32_t* tr, const uint32_t* tcr, const double* s_cost, int Kp,
+                                              int K, int j, int h, double gcd, double inv_beta, bool turn,
+                                              double* best_io, int* bi_io) {
+  double best = *best_io;
+  int bi = *bi_io;
+  for (int i0 = h; i0 < Kp; i0 += 2 * U) {
+    uint32_t tv[U], tc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + 2 * u < Kp ? i0 + 2 * u : Kp - 1;  // (rows past Kp: a valid row, skipped below)
+      tv[u] = tr[(int64_t)i * K + j];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + 2 * u < Kp ? i0 + 2 * u : Kp - 1;
+      tc[u] = (TURNS && turn) ? tcr[(int64_t)i * K + j] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (i0 + 2 * u >= Kp || tv[u] == kNoRoute) continue;
+      const double dg = fabs(div1000((double)tv[u]) - gcd);
+      const double ti = (TURNS ? div1000((double)tc[u]) + dg : dg) * inv_beta;
+      const double ci = s_cost[i0 + 2 * u];
+      if (ci == __builtin_huge_val()) continue;
+      const double c = ci + ti;
+      if (c < best) {
+        best = c;
+        bi = i0 + 2 * u;
+      }
+    }
+  }
+  *best_io = best;
+  *bi_io = bi;
+}
+// the lexicographic (cost, index) minimum of lane and lane ^ 32: the argmin the ascending
+// scan over all predecessors finds (strict <: the lowest index among equal minima)
+__device__ __forceinline__ void vit_pair(double* best, int* bi) {
+  const double ob = __shfl_xor(*best, 32);
+  const int obi = __shfl_xor(*bi, 32);
+  if (obi >= 0 && (*bi < 0 || ob < *best || (ob == *best && obi < *bi))) {
+    *best = ob;
+    *bi = obi;
+  }
+}
+
 // One wave per G traces (group g = lane / GL), lane j = candidate j of the current state.
 // The state loop runs to the longer trace of the wave; every per-state decision is
 // group-uniform and the LDS hand-over of the state costs sits between two wave-uniform
 // barriers.
-template <int G>
+// SPLIT (G = 1, batches of few traces): a state with K <= 32 candidates scans its
+// predecessors in two halves (lanes j and j + 32), halving the step's serial chain.
+template <int G, bool SPLIT = false>
 __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long long* counters) {
+  static_assert(!SPLIT || G == 1, "the split scan uses the second half of a one-trace wave");
   constexpr int GL = OTR_WAVE / G;
   constexpr int NL = VitLds<G>::N;
   __shared__ double s_cost[G][OTR_KMAX / G];
@@ -1615,7 +1666,22 @@ __global__ __launch_bounds__(64) void k_viterbi(ViterbiArgs a, unsigned long lon
       bool brk = prev_s < 0;
       if (act && !brk) {
         double best = __builtin_huge_val();
-        if (lane < K) {
+        const bool split = SPLIT && K <= 32;  // (group-uniform)
+        if (split) {
+          const uint32_t* tr = a.trans + a.trans_off[s];
+          const uint32_t* tcr = a.trans_tc + a.trans_off[s];
+          const double gcd = a.g[s];
+          const int j = lane & 31;
+          if (j < K) {
+            if (wturns) vit_scan_half<true>(tr, tcr, cst, Kp, K, j, lane >> 5, gcd, inv_beta, turns, &best, &bi);
+            else vit_scan_half<false>(tr, tcr, cst, Kp, K, j, lane >> 5, gcd, inv_beta, false, &best, &bi);
+          }
+          vit_pair(&best, &bi);
+          if (lane >= 32) {
+            best = __builtin_huge_val();
+            bi = -1;
+          }
+        } else if (lane < K) {
           // the array holds route lengths (u32 mm); the transition cost (turn_cost +
           // |route - gc|) / beta (K4) is evaluated here.  Without turn costs (group-
           // uniform) the 0 + x term is left out (0 + x == x exactly)
