@@ -55,15 +55,11 @@ def log(*a):
 
 def kernel_name(code, turns=False, first=False):
     """rocprofv3 name of a route kernel (otr_batch_result.route_tier_code); turns: kept for
-    callers (turn-mode tasks run in the edge-state kernels: code 6,000,000 + CAP * 100 + targets
-    for the lean tiers; 7,000,000 + CAP * 100 + targets named otr_edge.h's table in earlier
-    builds)."""
+    callers (turn-mode tasks run in the edge-state kernels: code 6,000,000 + CAP * 100 + targets)."""
     if code < 0:  # the global-memory search: -1 on 32K-state slabs, -2 on 1M-state slabs
         return 'k_general' if code == -1 else 'k_general (1M-state slabs)'
     if 6000000 <= code < 7000000:  # the lean edge-state tiers: 6,000,000 + CAP * 100 + targets
         return 'k_route_e1<%d>' % ((code - 6000000) // 100)
-    if code >= 7000000:  # the single-source edge-state tiers: 7,000,000 + CAP * 100 + targets
-        return 'k_route_edge<%d, %d>' % ((code - 7000000) // 100, code % 100)
     # the timed launches run the LDS route kernels compiled without work counting (the
     # last template argument, CNT = false; the instrumented step runs CNT = true)
     if 900000 <= code < 1000000:  # the 64-bit label tier: 900,000 + CAP
@@ -159,13 +155,18 @@ def main():
     ap.add_argument('--tiles', type=int, default=0,
                     help='privacy > 0: the step also runs the device tile stage (K9 rows, K10 sort + cull, '
                          'simple_reporter.py:176-239) on each matcher (not part of the headline config)')
+    ap.add_argument('--dist', action='store_true',
+                    help='run the N > 1 path (process group, uuid shards, keyed all-to-all exchange to the '
+                         '(hour, tile) owner) even at N = 1: RCCL at world size 1 on one GPU')
     args = ap.parse_args()
 
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
+    # the distributed path: every N > 1 run, and N = 1 with --dist (RCCL at world size 1)
+    dist_on = world > 1 or args.dist
     if args.workload is None:  # the headline at N = 1; BASELINE config 3 across GPUs
-        args.workload = 'c2' if world == 1 else 'c3'
+        args.workload = 'c2' if not dist_on else 'c3'
     import torch
     import torch.distributed as dist
     # OTR_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on one GPU
@@ -175,14 +176,18 @@ def main():
     if backend != 'nccl':
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
-    if world > 1:
+    if dist_on:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29531')
+        os.environ.setdefault('RANK', str(rank))
+        os.environ.setdefault('WORLD_SIZE', str(world))
         if backend == 'nccl':
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
             dist.init_process_group(backend)
 
     def barrier():
-        if world > 1:
+        if dist_on:
             if backend == 'nccl':
                 dist.barrier(device_ids=[local])
             else:
@@ -253,7 +258,7 @@ def main():
         n_global = n_per * world
         allt = gen.make_traces(gpath, n_global, W['points'], W['rate'], W['sigma'], W['seed'], W['bike'],
                                W['ped'], W['acc'], t_begin=T_BEGIN, t_spread=1800)
-        if world > 1:
+        if dist_on:
             shard = np.array([int(hashlib.sha1(u.encode()).hexdigest()[:3], 16) % world for u in allt.uuids])
             mine = allt.subset(np.flatnonzero(shard == rank))
         else:
@@ -312,7 +317,7 @@ def main():
     n_local, n_rows, row_views = [0] * n_parts, [0] * n_parts, [None] * n_parts
     hist_stats = {}
     # one batch per stream on one GPU: its single owner reduces the rows themselves
-    rows_direct = keyed and world == 1 and n_parts == ns
+    rows_direct = keyed and not dist_on and n_parts == ns
 
     def run_one(k, j, route_work):
         r = matchers[k].match_batch(parts[j], device_arrays=darrs[j],
@@ -357,7 +362,7 @@ def main():
             hist_stats.update(rows=int(sum(n_rows)), owned=int(owned['n']))
             return
         local_e = torch.cat([ebufs[j][:n_local[j] * EW] for j in range(n_parts)])
-        if world > 1:
+        if dist_on:
             tx = time.perf_counter()
             send = local_e if backend == 'nccl' else local_e.cpu()
             recv = sr.exchange_hist(send, world)
@@ -388,9 +393,9 @@ def main():
             split.update(match=round(1e3 * (t1 - t0), 3), histogram=round(1e3 * (time.perf_counter() - t1), 3))
             return rs
         torch.sum(torch.stack(hists), dim=0, out=hist)  # combine the per-stream histograms
-        if world > 1 and backend == 'nccl':
+        if dist_on and backend == 'nccl':
             dist.reduce_scatter_tensor(hist_out, hist, op=dist.ReduceOp.SUM)
-        elif world > 1:
+        elif dist_on:
             hc = hist.cpu()
             dist.all_reduce(hc, op=dist.ReduceOp.SUM)
             hist_out.copy_(hc[rank * hist_out.numel():(rank + 1) * hist_out.numel()])
@@ -411,7 +416,7 @@ def main():
     timed_split = dict(split)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     probes = torch.tensor([float(mine.n_probes)], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         if backend != 'nccl':
             el, probes = el.cpu(), probes.cpu()
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -606,7 +611,7 @@ def main():
                            ('keyed (hour-tile, pair, speed) entries all-to-all to the tile owner over ' +
                             ('RCCL' if backend == 'nccl' else 'gloo (rehearsal)')) if keyed else
                            (('RCCL reduce-scatter' if backend == 'nccl' else 'gloo all-reduce (rehearsal)') +
-                            ' of the dense [hour][segment][speed] histogram'))) if world > 1 else 'single GPU',
+                            ' of the dense [hour][segment][speed] histogram'))) if dist_on else 'single GPU',
                        'histogram': ({'kind': 'keyed (SURVEY 8e)', 'privacy': args.privacy, **hist_stats}
                                      if keyed else {'kind': 'dense [hour][segment][speed]'}),
                        'streams': ns,
@@ -650,7 +655,7 @@ def main():
             'end_to_end': e2e,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()  # rank 0's oracle sample and line come after the timed region
         dist.destroy_process_group()
     # a parity failure ends rank 0 with an error only after the other ranks left the barrier

@@ -206,8 +206,17 @@ typedef struct otr_batch_result {
   uint64_t route_tier_work[12][4];
 } otr_batch_result;
 
-/* At most 2^26 (67,108,864) probes per call (OTR_BAD_REQUEST beyond: split the input). */
+/* At most otr_max_batch_probes() = 2^26 - 64 (67,108,800) probes per call
+ * (OTR_BAD_REQUEST beyond: split the input). */
 int otr_match_batch(otr_matcher* m, const otr_trace_batch* in, otr_batch_result* out);
+
+/* The batch limit and its reason: a kernel dispatch counts its work-items in 32 bits, and
+ * the per-state / per-trace kernels give every state / trace a 64-lane wave.
+ * otr_launch_max_items: the most work-items one of those launches dispatches for a batch
+ * of n_states states and n_traces traces (states_per_wave 1 or 2: k_prep / k_tasks);
+ * a batch of otr_max_batch_probes() probes stays below 2^32.  Host-only (no device). */
+int64_t otr_max_batch_probes(void);
+uint64_t otr_launch_max_items(int64_t n_states, int64_t n_traces, int32_t states_per_wave);
 
 /* simple_reporter's tile stage (simple_reporter.py:211-239) on device: sort the rows
  * by file, then in the line order of segments.sort() (:218, string order of the whole

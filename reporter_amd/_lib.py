@@ -38,7 +38,8 @@ EXPORTS = ['otr_configure', 'otr_configure_json', 'otr_matcher_new', 'otr_matche
            'otr_report', 'otr_report_segments', 'otr_free', 'otr_last_error', 'otr_match_batch',
            'otr_graph_info', 'otr_matcher_stream', 'otr_device', 'otr_report_batch', 'otr_coalesce',
            'otr_tiles_cull', 'otr_tiles_format', 'otr_ingest', 'otr_report_lists_device', 'otr_hist_reduce',
-           'otr_tilehier_row', 'otr_tilehier_col', 'otr_tilehier_file', 'otr_tilehier_files', 'otr_flatten']
+           'otr_tilehier_row', 'otr_tilehier_col', 'otr_tilehier_file', 'otr_tilehier_files', 'otr_flatten',
+           'otr_max_batch_probes', 'otr_launch_max_items']
 
 
 class FlatGraph(ctypes.Structure):
@@ -158,6 +159,9 @@ def lib():
                                    ctypes.c_int32, P(ctypes.c_void_p), P(ctypes.c_size_t)]
     L.otr_ingest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, P(IngestFormat),
                              P(IngestResult)]
+    L.otr_max_batch_probes.restype = ctypes.c_int64
+    L.otr_launch_max_items.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32]
+    L.otr_launch_max_items.restype = ctypes.c_uint64
     L.otr_tilehier_row.argtypes = [ctypes.c_int32, ctypes.c_double]
     L.otr_tilehier_row.restype = ctypes.c_int32
     L.otr_tilehier_col.argtypes = [ctypes.c_int32, ctypes.c_double]

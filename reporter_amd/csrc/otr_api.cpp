@@ -11,6 +11,7 @@
 
 #include "../../include/otr.h"
 #include "otr_engine.h"
+#include "otr_launch.h"
 #include "otr_json.h"
 #include "otr_format.h"
 #include "otr_report.h"
@@ -449,3 +450,9 @@ int otr_tiles_format(const otr_tile_row* rows, int64_t n, const char* source, co
 }
 
 }  // extern "C"
+
+extern "C" int64_t otr_max_batch_probes(void) { return otr::kMaxBatchProbes; }
+
+extern "C" uint64_t otr_launch_max_items(int64_t n_states, int64_t n_traces, int32_t states_per_wave) {
+  return otr::max_launch_items(n_states, n_traces, states_per_wave == 2 ? 2 : 1);
+}

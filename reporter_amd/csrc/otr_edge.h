@@ -18,7 +18,8 @@
 //     decides unreachability (the bounds are on the length);
 //   * the same pruning as search_run (time, length and turn cost all prune); every offer
 //     comes from a final label, so the labels are the oracle's label-setting ones.
-// One source edge per task (k_tasks), one search per wave (G = 1).
+// One search per wave (G = 1).  The route tiers of the turn modes are otr_edge1.h's
+// k_route_e1; this header's edge_search is the winner-path search (k_paths_edge).
 #pragma once
 #include "otr_general.h"
 
@@ -365,105 +366,6 @@ __device__ bool edge_search(EdgeLds<CAP, TG>& L, const DevGraph& g, int md, bool
   if (relaxed) *relaxed += my_relaxed;
   __syncthreads();
   return !L.overflow;
-}
-
-// ------------------------------------------------------------------------------
-// K3e: edge-state route tasks (turn modes), a fixed grid over the device-side list of
-// the tasks flagged 6 (what the first edge tier, otr_edge1.h, could not hold) or 7 (this
-// tier's overflows, for the 2048-state table).
-// ------------------------------------------------------------------------------
-// What outgrows the 2048-state table goes to k_general (3).  TG: the targets a search
-// holds (32 when every mode keeps <= 32 candidates, else 64).
-template <int CAP, int TG>
-__global__ __launch_bounds__(64) void k_route_edge(DevGraph gr, RouteArgs a, unsigned long long* counters) {
-  __shared__ EdgeLds<CAP, TG> L;
-  if (threadIdx.x == 0) L.turn_md = -1;
-  const int64_t n_tasks = (int64_t)*a.list_count;
-  const int lane = (int)threadIdx.x;
-  for (int64_t w = blockIdx.x; w < n_tasks; w += gridDim.x) {
-    const int64_t task = a.task_list[w];
-    const uint4 r0 = a.rec[3 * task], r1 = a.rec[3 * task + 1], r2 = a.rec[3 * task + 2];
-    const int64_t s = r0.x, sp = r0.y;
-    const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
-    const int i = __ffsll((long long)mask) - 1;  // the task's one source
-    const int Kb = (int)(r1.y & 0xFFu);
-    const int md = (int)((r1.y >> 8) & 3u);
-    const bool forced = (r1.y >> 10) & 1u;
-    const uint32_t bmm = r0.w;
-    const int32_t bt = (int32_t)r2.y;
-    const uint32_t ei = a.cand_edge[sp * OTR_KMAX + i];
-    const double pi = a.cand_p[sp * OTR_KMAX + i];
-    const uint32_t d0 = a.cprep[sp * OTR_KMAX + i].w;
-    const uint32_t t0 = bt >= 0 ? a.cprep_t[sp * OTR_KMAX + i].y : 0u;
-    const uint2 li = a.clen[sp * OTR_KMAX + i];
-    uint32_t ej = 0, tv = kEmpty, tpart = 0, tpt = 0, thb = 0;
-    double pj = 0;
-    bool needed = false;
-    if (lane < Kb) {
-      ej = a.cand_edge[s * OTR_KMAX + lane];
-      pj = a.cand_p[s * OTR_KMAX + lane];
-      const uint4 cq = a.cprep[s * OTR_KMAX + lane];
-      tpart = cq.x;
-      tpt = bt >= 0 ? a.cprep_t[s * OTR_KMAX + lane].x : 0u;
-      needed = !(ej == ei && pj >= pi);
-      if (needed) {
-        tv = cq.y;
-        thb = (uint32_t)gr.edge_head[ej].x;
-      }
-    }
-    const bool root_ok = d0 <= bmm && (bt < 0 || t0 <= (uint32_t)bt);
-    const bool search = Kb <= TG && !forced && root_ok && __ballot(needed) != 0ull;
-    const uint32_t pd = bmm >= d0 ? bmm - d0 : 0u;
-    const uint32_t pt = bt >= 0 && t0 <= (uint32_t)bt ? (uint32_t)bt - t0 : 0u;
-    e_init(L);
-    e_turn_table(L, a.turn, md);
-    unsigned long long settled = 0, relaxed = 0;
-    const bool ok = edge_search<CAP, TG>(L, gr, md, search, ei, gr.edge_dst[ei], pd, pt, bt >= 0,
-                                         Kb, tv, tpart, tpt, thb, counters ? &settled : nullptr,
-                                         counters ? &relaxed : nullptr) &&
-                    Kb <= TG
-#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 2 fails every 2048-state search (k_general takes them)
-                    && !(CAP >= 2048 && (a.force_edge & 4))
-#endif
-        ;
-    if (ok) {
-      uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
-      if (lane < Kb) {
-        int64_t r = -1, rt = 0;
-        uint32_t rc = 0;
-        if (forced) {
-          r = -1;
-        } else if (ej == ei && pj >= pi) {
-          r = part_mm(pj - pi, li.x);
-          if (bt >= 0) rt = part_mm(pj - pi, li.y);
-        } else if (search) {
-          const unsigned long long tl = L.tlab[lane];
-          if (tl != kGInf) {
-            r = (int64_t)d0 + g_d(tl);
-            rt = (int64_t)t0 + g_t(tl);
-            rc = g_c(tl);
-          }
-        }
-        const bool valid = r >= 0 && r <= (int64_t)bmm && (bt < 0 || rt <= (int64_t)bt);
-        trow[(int64_t)i * Kb + lane] = valid ? (uint32_t)r : kNoRoute;
-        a.trans_tc[trow - a.trans + (int64_t)i * Kb + lane] = valid ? rc : 0u;
-      }
-    } else if (lane == 0) {
-      a.overflow_flag[task] = CAP < 2048 ? 7 : 3;  // the 2048-state table, then k_general
-    }
-    if (counters) {
-      settled = wave_sum_u32((uint32_t)settled);
-      relaxed = wave_sum_u32((uint32_t)relaxed);
-      if (lane == 0) {
-        const int sh = cshard();
-        atomicAdd(&counters[3 * kCShards + sh], settled);
-        atomicAdd(&counters[4 * kCShards + sh], relaxed);
-        atomicAdd(&counters[5 * kCShards + sh], ok && search ? (unsigned long long)Kb : 0ull);
-        atomicAdd(&counters[6 * kCShards + sh], search ? 1ull : 0ull);
-      }
-    }
-    __syncthreads();
-  }
 }
 
 // ------------------------------------------------------------------------------

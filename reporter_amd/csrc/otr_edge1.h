@@ -509,7 +509,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
         }
       }
     }
-#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 0 / 1 / 2 fails every 256 / 512 / 1024-state search
+#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 0 / 1 / 2 fails every OTR_E1CAP (360) / 512 / 1024-state search
     if (a.force_edge & (CAP < 512 ? 1 : (CAP < 1024 ? 2 : 4))) ok = false;
 #endif
     ok = ok && Kb <= TG;

@@ -15,8 +15,10 @@
 #include "otr_edge.h"
 #include "otr_edge1.h"
 #include "otr_ingest.h"
+#include "otr_launch.h"
 
 namespace otr {
+static_assert(kTraceWaves == 4, "grid_trace_rows (otr_launch.h) assumes 4 traces per block");
 
 #define HIPCHK(x)                                                                        \
   do {                                                                                   \
@@ -368,7 +370,6 @@ int engine_configure(const Config& cfg, std::string* err) {
 // ---------------------------------------------------------------------------------
 // workspace slots
 // ---------------------------------------------------------------------------------
-constexpr int64_t kMaxBatchProbes = 1ll << 26;  // otr_match_batch (include/otr.h)
 
 enum Slot {
   S_TRACE_OFF, S_LAT, S_LON, S_TIME, S_ACC, S_MODE,
@@ -655,11 +656,14 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     b.acc = in->accuracy;
   }
   out->n_probes = N;
-  // one wave per state in the per-state kernels: a dispatch counts its work-items in 32
-  // bits, so a batch holds at most 2^26 probes (callers split larger inputs; the JSON
-  // service batches at 16M)
-  if (N > kMaxBatchProbes) {
-    if (err) *err = "batch of " + std::to_string(N) + " probes: at most 67108864 per otr_match_batch call";
+  // one wave per state / trace in the per-state and per-trace kernels: a dispatch counts
+  // its work-items in 32 bits, so a batch holds at most kMaxBatchProbes = 2^26 - 64 probes
+  // (otr_launch.h: the widest launch of such a batch, k_candidates at states = probes,
+  // stays below 2^32; callers split larger inputs, the JSON service batches at 16M)
+  if (N > kMaxBatchProbes || max_launch_items(N, N, 1) > kMaxDispatchItems) {
+    if (err)
+      *err = "batch of " + std::to_string(N) + " probes: at most " + std::to_string(kMaxBatchProbes) +
+             " per otr_match_batch call";
     return OTR_BAD_REQUEST;
   }
   h_trace_status.assign(T, OTR_OK);
@@ -717,7 +721,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   }
   if (S > 0) {
     tb(OTR_STAGE_CANDIDATES);
-    k_candidates<<<(unsigned)(8 * ((S + 7) / 8)), 64, 0, stream>>>(g, b, mp, S, state_probe, state_trace, cb,
+    k_candidates<<<(unsigned)grid_candidates(S).blocks, 64, 0, stream>>>(g, b, mp, S, state_probe, state_trace, cb,
                                                                    d_counters);
     te(OTR_STAGE_CANDIDATES);
   }
@@ -736,7 +740,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   int64_t* task_off = need<int64_t>(S_TASK_OFF, S + 1);
   int64_t* trans_off = need<int64_t>(S_TRANS_OFF, S + 1);
   tb(OTR_STAGE_LINK);  // (K_link, the search inputs and the task records: through k_tasks)
-  k_link<<<grid_for(T, 4), 256, 0, stream>>>(b, mp, trace_state_off, state_probe, cb.count, sb);
+  k_link<<<(unsigned)grid_link(T).blocks, 256, 0, stream>>>(b, mp, trace_state_off, state_probe, cb.count, sb);
   // K2b: per-state search inputs
   PrepArgs pr{};
   pr.n_states = S;
@@ -760,8 +764,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   bool k32 = true;
   for (int m = 0; m < OTR_MODES; ++m) k32 = k32 && mp.m[m].kmax <= 32;
   if (S > 0) {
-    if (k32) k_prep<2><<<grid_for((S + 1) / 2, 4), 256, 0, stream>>>(g, pr);
-    else k_prep<1><<<grid_for(S, 4), 256, 0, stream>>>(g, pr);
+    if (k32) k_prep<2><<<(unsigned)grid_per_state_waves(S, 2).blocks, 256, 0, stream>>>(g, pr);
+    else k_prep<1><<<(unsigned)grid_per_state_waves(S, 1).blocks, 256, 0, stream>>>(g, pr);
   }
   // the step's task count: the distinct roots (k_prep) of the previous state's candidates
   if (S > 0) k_ntask<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, pr.nroot, sb.ntask);
@@ -803,8 +807,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     ta.rec = task_rec;
     ta.flag_turn = task_ovf;  // turn-mode tasks start in the first edge-state tier (flag 5)
     if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
-    if (k32) k_tasks<2><<<grid_for((S + 1) / 2, 4), 256, 0, stream>>>(ta);
-    else k_tasks<1><<<grid_for(S, 4), 256, 0, stream>>>(ta);
+    if (k32) k_tasks<2><<<(unsigned)grid_per_state_waves(S, 2).blocks, 256, 0, stream>>>(ta);
+    else k_tasks<1><<<(unsigned)grid_per_state_waves(S, 1).blocks, 256, 0, stream>>>(ta);
   }
   te(OTR_STAGE_LINK);
   // turn cost tables of this batch's parameters (oracle orc_turn_table)
@@ -1055,8 +1059,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       if (timing) (void)hipEventRecord(ev[24 + 2 * 8 + 1], stream);
     }
 #endif
-    // edge-state tiers (turn-cost modes, otr_edge1.h): 256 states (flag 5, slot 10), 512
-    // (flag 6, slot 9), 1024 (flag 7, slot 11); what outgrows those (flag 3) goes on below
+    // edge-state tiers (turn-cost modes, otr_edge1.h): OTR_E1CAP (360) states (flag 5, slot
+    // 10), 512 (flag 6, slot 9), 1024 (flag 7, slot 11); what outgrows those (flag 3) goes on below
     if (turns) {
       for (int et = 0; et < 3; ++et) {
         const int slot = et == 0 ? 10 : (et == 1 ? 9 : 11);
@@ -1188,8 +1192,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       pa.force_edge = ra.force_edge;
       tb(OTR_STAGE_PATHS);
       {
-        const int64_t units = (S + 1) / 2;  // upper bound: two searches per wave
-        k_paths<OTR_CAP1, 2><<<(unsigned)(8 * ((units + 7) / 8)), 64, 0, stream>>>(g, pa, nullptr, nullptr);
+        // (steps <= states: two searches per wave)
+        k_paths<OTR_CAP1, 2><<<(unsigned)grid_paths(S).blocks, 64, 0, stream>>>(g, pa, nullptr, nullptr);
       }
       te(OTR_STAGE_PATHS);
       tb(OTR_STAGE_PATHS_BIG);
@@ -1324,7 +1328,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   sa.transition_levels = in->transition_levels;
   for (int m = 0; m < OTR_MODES; ++m) sa.queue_kph[m] = mp.m[m].queue_kph;
   tb(OTR_STAGE_SEGMENTS);
-  k_segments<<<(unsigned)(8 * ((T + 7) / 8)), 64, 0, stream>>>(g, sa, d_counters);
+  k_segments<<<(unsigned)grid_segments(T).blocks, 64, 0, stream>>>(g, sa, d_counters);
   te(OTR_STAGE_SEGMENTS);
   // ---- K8: hour buckets → histogram
   HistArgs ha{};
@@ -1348,7 +1352,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   tb(OTR_STAGE_HISTOGRAM);
   // K8 also counts the rows (n_rows) when K9 does not
   if (hist_len || !(in->flags & OTR_BATCH_TILE_ROWS))
-    k_histogram<<<grid_for(T, kTraceWaves), 256, 0, stream>>>(ha);
+    k_histogram<<<(unsigned)grid_trace_rows(T).blocks, 256, 0, stream>>>(ha);
   te(OTR_STAGE_HISTOGRAM);
   // ---- K9: simple_reporter tile rows (optional)
   if (in->flags & OTR_BATCH_TILE_ROWS) {
@@ -1365,14 +1369,14 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     ta.quantisation = ha.quantisation;
     ta.rules = in->tile_rules;
     ta.row_cnt = need<int64_t>(S_ROW_CNT, T);
-    k_tile_rows<<<grid_for(T, kTraceWaves), 256, 0, stream>>>(ta);
+    k_tile_rows<<<(unsigned)grid_trace_rows(T).blocks, 256, 0, stream>>>(ta);
     int64_t* row_off = need<int64_t>(S_ROW_OFF, T + 1);
     if ((rc = scan(ta.row_cnt, row_off, T))) return rc;
     int64_t R = 0;
     if ((rc = read_i64(row_off + T, &R))) return rc;
     ta.row_off = row_off;
     ta.rows = need<otr_tile_row>(S_ROWS, R > 0 ? R : 1);
-    if (R > 0) k_tile_rows<<<grid_for(T, kTraceWaves), 256, 0, stream>>>(ta);
+    if (R > 0) k_tile_rows<<<(unsigned)grid_trace_rows(T).blocks, 256, 0, stream>>>(ta);
     out->d_rows = ta.rows;
     out->n_rows = R;
   }
@@ -1541,7 +1545,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ca.rep_t1 = need<double>(S_C_REP_T1, n1(nrep));
   ca.rep_length = need<int32_t>(S_C_REP_LEN, n1(nrep));
   ca.rep_queue = need<int32_t>(S_C_REP_QUEUE, n1(nrep));
-  k_compact<<<(unsigned)T, 64, 0, stream>>>(ca);
+  k_compact<<<(unsigned)grid_compact(T).blocks, 64, 0, stream>>>(ca);
   int64_t* seg_way_off = need<int64_t>(S_C_SEG_WAY_OFF, (size_t)nseg + 1);
   if ((rc = scan(ca.seg_way_n, seg_way_off, nseg))) return rc;
   HIPCHK(hipGetLastError());

@@ -1072,9 +1072,8 @@ struct RouteArgs {
   unsigned long long* queue;  // list tiers: this launch's 8 per-XCD unit counters (XcdQueue), zeroed
   unsigned long long* stamps;  // diagnostic build (OTR_STAMPS): bank 0 of the work counters (phase cycles)
   int force_edge;             // test build only (OTR_FORCE_RETRY, env OTR_FORCE_EDGE): bits 0 / 1 / 2 fail
-                              // every 256 / 512 / 1024-state edge-state route search (the next tier
-                              // takes it), bits
-                              // 3 / 4 every 384 / 2048-state edge-state winner path
+                              // every OTR_E1CAP (360) / 512 / 1024-state edge-state route search (the
+                              // next tier takes it), bits 3 / 4 every 384 / 2048-state winner path
 };
 
 // k_tasks' inputs and outputs

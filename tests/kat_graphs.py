@@ -310,3 +310,34 @@ def stale_traces():
     """Probes 20 s apart: near S on W-S (and near the Y-S road), then on V-Z."""
     return [[(-60, 2), (-3, 3), (230, 2), (270, 2)],
             [(-60, 2), (-5, -2), (210, 2), (250, 2)]]
+
+
+def build_zero(path):
+    """A zero-length edge under turn costs (the edge-state IN criterion's gap):
+    a junction split in two nodes at the same point, J (0, 0) and J2 (0, 0), joined by a
+    two-way edge of stored length 0 (routing length 1 mm; heading 0 from
+    its degenerate shape).  W (-100, 0) - J - J2 - E (100, 0) is the main street, J - N
+    (0, 100) and J2 - S (0, -100) the side streets, all two-way 50 km/h level 1.  Routes
+    cross J -> J2 with the turns into and out of the zero-length edge, and a U-turn at J2
+    or J offers to the zero-length state again through the smallest turn."""
+    nodes = [ll(-100, 0), ll(0, 0), ll(0, 0), ll(100, 0), ll(0, 100), ll(0, -100)]
+    W, J, J2, E, N, S = range(6)
+    edges, ids = [], {}
+    ids['WJ>'], ids['WJ<'] = two_way(edges, W, J, 71, level=1, speed=50)
+    ids['Z>'], ids['Z<'] = two_way(edges, J, J2, 72, level=1, speed=50, length=0.0)
+    ids['J2E>'], ids['J2E<'] = two_way(edges, J2, E, 73, level=1, speed=50)
+    ids['JN>'], ids['JN<'] = two_way(edges, J, N, 74, level=1, speed=50)
+    ids['J2S>'], ids['J2S<'] = two_way(edges, J2, S, 75, level=1, speed=50)
+    segs = [dict(id=osmlr(1, 405, 1), edges=[ids['WJ>'], ids['Z>'], ids['J2E>']]),
+            dict(id=osmlr(1, 405, 2), edges=[ids['J2E<'], ids['Z<'], ids['WJ<']])]
+    new = write_graph(path, nodes, edges, segs)
+    return {k: int(new[v]) for k, v in ids.items()}
+
+
+def zero_traces():
+    """Across the split junction: west to east, west to south, north to east, and east to
+    north (through the zero-length edge the other way)."""
+    return [[(-80, 2), (-30, 2), (30, 2), (80, 2)],
+            [(-80, 2), (-30, 2), (2, -30), (2, -80)],
+            [(2, 80), (2, 30), (30, -2), (80, -2)],
+            [(80, -2), (30, -2), (-2, 30), (-2, 80)]]

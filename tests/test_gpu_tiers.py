@@ -126,7 +126,7 @@ for g, nt, npnt, sr, sig, seed, fb, fp in [('city', 40, 100, 15, 10.0, 2, 0.0, 0
     r = m.match_batch(tr, copy_out=True, route_work=True)
     assert r.status == 0, r.status
     w = [int(r.route_tier_work[t][0]) for t in range(12)]
-    # slots: 10 the 256-state lean tier, 9 the 512-state one, 11 the 1024-state one, 6 k_general
+    # slots: 10 the OTR_E1CAP (360)-state lean tier, 9 the 512-state one, 11 the 1024-state one, 6 k_general
     if force & 1:
         assert w[10] == 0 and w[9] + w[11] + w[6] > 0, w
     if (force & 3) == 1:

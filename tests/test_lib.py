@@ -23,6 +23,26 @@ def test_struct_layout():
     assert ctypes.sizeof(_lib.BatchResult) > 0
 
 
+def test_batch_limit_launch_plan():
+    """The batch limit keeps every per-state / per-trace dispatch below 2^32 work-items
+    (otr_launch.h; a wave per state: 64 work-items, k_candidates in groups of 8 states)."""
+    L = _lib.lib()
+    cap = L.otr_max_batch_probes()
+    assert cap == (1 << 26) - 64
+    lim = (1 << 32) - 1
+    for n in (cap, (1 << 26) - 1, 1 << 26, (1 << 26) + 1):
+        for g in (1, 2):
+            items = L.otr_launch_max_items(n, n, g)
+            # 64 work-items per state, the state count rounded up to 8 (k_candidates)
+            assert items == 64 * 8 * ((n + 7) // 8)
+            assert (items <= lim) == (n <= (1 << 26) - 8), (n, g, items)
+    # every accepted batch fits: states <= probes and traces <= probes
+    for s, t in ((cap, 1), (1, cap), (cap, cap), (cap // 2, cap)):
+        assert L.otr_launch_max_items(s, t, 1) <= lim
+    # the first refused size is the first whose widest launch could exceed it by design
+    assert L.otr_launch_max_items(0, 0, 1) == 0
+
+
 def test_not_configured_errors():
     from reporter_amd import matcher as M
     # a bad config fails loudly (no fallback)

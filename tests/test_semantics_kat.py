@@ -201,6 +201,27 @@ def stale(graph_dir):
     return path, K.build_stale(path)
 
 
+@pytest.fixture(scope='module')
+def zero(graph_dir):
+    path = os.path.join(graph_dir, 'kat_zero.otrg')
+    return path, K.build_zero(path)
+
+
+def test_zero_length_edge_routes(zero):
+    """A zero-length edge is routed as 1 mm, so every label strictly grows
+    along a path and the edge-state IN gap (>= 1 mm + the smallest turn) stays a lower bound
+    of any later offer: west to east crosses it straight on (route 200 m + 1 mm) and the
+    matched trace follows W-J, J-J2, J2-E under the deployed turn costs."""
+    path, ids = zero
+    g = po.Graph(path)
+    d, t, c = g.route(ids['WJ>'], 0.5, ids['J2E>'], 0.5, 1000.0, dt_sec=20, prm=po.params())
+    assert abs(d - 100.001) < 0.05
+    b, r = _match(path, K.zero_traces()[0], 4)
+    rt = [int(e) for e in r['route_edge']]
+    k = rt.index(ids['WJ>'])
+    assert rt[k:k + 3] == [ids['WJ>'], ids['Z>'], ids['J2E>']]
+
+
 def test_turn_cost_detour_wins(block):
     """A detour shorter than the turn penalty it avoids: eastbound at x = -10 to westbound
     at x = -40.  The U-turn at P1 is 50 m with turn cost 200 m (+ 3.663 m straight on at R):
@@ -303,13 +324,13 @@ def test_semantics_gpu_parity(kat, slow, square, opts):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('opts', [{}, {'turn_penalty_factor': 0}, {'max_route_time_factor': 0}])
-def test_pruning_semantics_gpu_parity(block, bypass, stale, opts):
+def test_pruning_semantics_gpu_parity(block, bypass, stale, zero, opts):
     """The graphs where the route key (length + turn cost) and the pruning during the search
-    decide the answer: bit-exact with the oracle under the deployed options, without turn
-    costs and without a time bound."""
+    decide the answer, and a zero-length edge under turn costs: bit-exact with the oracle
+    under the deployed options, without turn costs and without a time bound."""
     from reporter_amd import matcher as M
     for (path, _), trs, dt in ((block, [K.block_trace()], 10), (bypass, [K.bypass_trace()], 20),
-                               (stale, K.stale_traces(), 20)):
+                               (stale, K.stale_traces(), 20), (zero, K.zero_traces(), 4)):
         M.configure(M.default_config(path, **opts))
         b = K.batch([K.trace(p, dt=dt) for p in trs])
         got = M.Matcher().match_batch_numpy(b)

@@ -22,6 +22,7 @@ typedef struct {
   int64_t hist_bmm_keys[24][24]; /* [route bound / 100 m][keys / 32] */
   int64_t settled_out, rounds_out, scans_tmin, scans_out; /* + the OUT criterion; pending entries examined */
   int64_t settled_tterm, rounds_tterm;                     /* + the time-bound target resolution */
+  int64_t settled_ast, rounds_ast, settled_ast1, rounds_ast1; /* + A* lower-bound resolution: per target / one anchor */
 } es_stats;
 
 typedef struct {
@@ -46,6 +47,18 @@ static void es_touch(es_ws* W, uint32_t e) {
   }
 }
 
+
+/* A* lower-bound target resolution (analysis): planar chord metric, rho_d / rho_t = the
+ * smallest length / time per chord-mm over every edge, so every path's length (time) is
+ * >= rho * the chord between its ends */
+static double g_rho_d, g_rho_t, g_kx, g_ky;
+static double pl_chord_mm(const orc_graph* g, uint32_t u, uint32_t v) {
+  const double dx = (double)(g->node_ll[2 * u + 1] - g->node_ll[2 * v + 1]) * g_kx;
+  const double dy = (double)(g->node_ll[2 * u] - g->node_ll[2 * v]) * g_ky;
+  return sqrt(dx * dx + dy * dy);
+}
+static int g_ast; /* 1: per-target anchors, 2: one anchor (the first needed target's node) */
+static uint32_t g_anchor;
 static int g_tterm; /* also resolve a target once every pending label's time + its entry time breaks the bound */
 
 /* one simulated search; returns keys; *settled, *rounds out */
@@ -77,8 +90,23 @@ static int64_t es_search(const rctx* X, es_ws* W, uint32_t ei, double pi, int nt
     int unres = 0;
     for (int j = 0; j < ntg; ++j) {
       if (tv[j] == 0xFFFFFFFFu) continue;
-      const int res = (tl[j].k < kInf && tl[j].k < kmin + tpart[j] + tmin) || dmin + tpart[j] > pd ||
+      int res = (tl[j].k < kInf && tl[j].k < kmin + tpart[j] + tmin) || dmin + tpart[j] > pd ||
                       (g_tterm && X->time_on && tminp + tpt[j] > pt);
+      if (!res && g_ast) {
+        /* every later offer to j descends from a pending state b (head v): length >= d(b) +
+           rho_d * chord(v, src(j)), time likewise */
+        double ad = 1e300, at = 1e300;
+        const uint32_t anc = g_ast == 1 ? tv[j] : g_anchor;
+        const double rj = g_ast == 1 ? 0.0 : pl_chord_mm(g, g_anchor, tv[j]);
+        for (uint32_t q = 0; q < np; ++q) {
+          const uint32_t b = W->pend[q];
+          const double ch = pl_chord_mm(g, g->edge_dst[b], anc) - rj;
+          const double xd = (double)W->lab[b].d + g_rho_d * ch, xt = (double)W->lab[b].t + g_rho_t * ch;
+          if (xd < ad) ad = xd;
+          if (xt < at) at = xt;
+        }
+        if (ad + (double)tpart[j] > (double)pd + 1e-3 || (X->time_on && at + (double)tpt[j] > (double)pt + 1e-3)) res = 1;
+      }
       if (!res) unres = 1;
     }
     if (!unres) break;
@@ -174,6 +202,27 @@ int es_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
   W.nxt = malloc(4 * (size_t)(E + 1));
   mode_data md;
   mode_data_init(g, &p[0], 0, &md);
+  {
+    double lat0 = 0;
+    for (uint32_t v = 0; v < g->h.n_nodes; ++v) lat0 += g->node_ll[2 * v] * 1e-6;
+    lat0 /= g->h.n_nodes;
+    g_ky = kM * 1e-6 * 1000.0;
+    g_kx = kM * 1e-6 * 1000.0 * cos_deg(lat0) * 0.98; /* (margin for the latitude spread) */
+    g_rho_d = 1e300;
+    g_rho_t = 1e300;
+    int64_t zt = 0;
+    for (uint32_t e = 0; e < E; ++e) {
+      if (!(g->edge_attr[e] & md.mode_bit)) continue;
+      const double ch = pl_chord_mm(g, g->edge_src[e], g->edge_dst[e]);
+      if (ch <= 0) continue;
+      const double rd = (double)g->len_mm[e] / ch, rt = (double)md.time_ds[e] / ch;
+      if (rd < g_rho_d) g_rho_d = rd;
+      if (rt < g_rho_t) g_rho_t = rt;
+      if (md.time_ds[e] == 0) zt++;
+    }
+    fprintf(stderr, "rho_d %.6f rho_t %.8f (1/rho_t %.1f mm per 0.1 s) zero-time edges %lld\n", g_rho_d, g_rho_t,
+            1.0 / g_rho_t, (long long)zt);
+  }
   int64_t tmin = md.turn[0];
   for (int i = 0; i <= 180; ++i)
     if (md.turn[i] < tmin) tmin = md.turn[i];
@@ -262,6 +311,18 @@ int es_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
         g_tterm = 1;
         int64_t st4, rd4, rl4 = 0;
         (void)es_search(&X, &W, ci->e, ci->p, Kb, tv, tpart, tpt, tej, tmin, &st4, &rd4, &rl4, &S->pend_max, 0, NULL, NULL);
+        int64_t st5, rd5, rl5 = 0, st6, rd6, rl6 = 0;
+        g_ast = 1;
+        (void)es_search(&X, &W, ci->e, ci->p, Kb, tv, tpart, tpt, tej, tmin, &st5, &rd5, &rl5, &S->pend_max, 0, NULL, NULL);
+        g_ast = 2;
+        g_anchor = 0xFFFFFFFFu;
+        for (int j = 0; j < Kb && g_anchor == 0xFFFFFFFFu; ++j) if (tv[j] != 0xFFFFFFFFu) g_anchor = tv[j];
+        (void)es_search(&X, &W, ci->e, ci->p, Kb, tv, tpart, tpt, tej, tmin, &st6, &rd6, &rl6, &S->pend_max, 0, NULL, NULL);
+        g_ast = 0;
+        S->settled_ast += st5;
+        S->rounds_ast += rd5;
+        S->settled_ast1 += st6;
+        S->rounds_ast1 += rd6;
         g_tterm = 0;
         S->settled_tterm += st4;
         S->rounds_tterm += rd4;
@@ -302,6 +363,144 @@ int es_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
   free(W.pend);
   free(W.nxt);
   free(minout);
+  free(md.time_ds);
+  return 0;
+}
+
+/* Viterbi-side pruning statistics (analysis): with step t-1's accumulated costs known,
+ * how many source candidates of step t need a search at all?  Sources in ascending cost
+ * order; a source is skippable when its cost is infinite (no predecessor reached it) or
+ * when every target already has a cheaper offer U_j < cost(i) (transitions are >= 0). */
+typedef struct {
+  int64_t steps, sources, inf_sources, skip_local, searched_local, brk;
+} vp_stats;
+
+int vp_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int64_t* trace_off, const double* lat,
+           const double* lon, const int64_t* tms, vp_stats* S) {
+  memset(S, 0, sizeof(*S));
+  mode_data md;
+  mode_data_init(g, &p[0], 0, &md);
+  const double inv2s2 = 1.0 / (p[0].sigma_z * p[0].sigma_z * 2.0), inv_beta = 1.0 / p[0].beta;
+  const int kmax = p[0].max_candidates < ORC_KMAX ? p[0].max_candidates : ORC_KMAX;
+  static cand_t cands[4096][ORC_KMAX];
+  static int kc[4096], act[4096];
+  static int64_t sp[4096];
+  nodemap_t nm;
+  nm_init(&nm, 1024);
+  double trans[ORC_KMAX * ORC_KMAX];
+  for (int32_t t = 0; t < n_traces; ++t) {
+    const int64_t b = trace_off[t], n = trace_off[t + 1] - b;
+    int ns = 0;
+    int64_t last = 0;
+    for (int64_t i = 0; i < n && ns < 4096; ++i) {
+      int st = i == 0 || i == n - 1 ||
+               gc_dist(lat[b + last], lon[b + last], lat[b + i], lon[b + i]) >= p[0].interpolation_distance;
+      if (st) {
+        last = i;
+        sp[ns++] = b + i;
+      }
+    }
+    int na = 0;
+    for (int s = 0; s < ns; ++s) {
+      double a = p[0].gps_accuracy;
+      double radius = p[0].search_radius > a ? p[0].search_radius : a;
+      if (radius > p[0].max_search_radius) radius = p[0].max_search_radius;
+      kc[s] = find_candidates(g, lat[sp[s]], lon[sp[s]], radius, md.mode_bit, kmax, cands[s]);
+      if (kc[s] > 0) act[na++] = s;
+    }
+    double cost[ORC_KMAX], ncost[ORC_KMAX];
+    if (na > 0)
+      for (int j = 0; j < kc[act[0]]; ++j) cost[j] = cands[act[0]][j].d2 * inv2s2;
+    for (int k = 1; k < na; ++k) {
+      const int sa = act[k - 1], sb = act[k];
+      const int Ka = kc[sa], Kb = kc[sb];
+      const cand_t *ca = cands[sa], *cb = cands[sb];
+      const double gcd = gc_dist(lat[sp[sa]], lon[sp[sa]], lat[sp[sb]], lon[sp[sb]]);
+      const int forced = gcd > p[0].breakage_distance;
+      rctx X;
+      step_ctx(&X, g, &md, &p[0], gcd, tms[sp[sb]] - tms[sp[sa]]);
+      int needed[ORC_KMAX];
+      for (int i = 0; i < Ka; ++i) {
+        for (int j = 0; j < Kb; ++j) trans[i * ORC_KMAX + j] = INFINITY;
+        needed[i] = 0;
+        if (forced) continue;
+        int need = 0;
+        for (int j = 0; j < Kb; ++j)
+          if (!(cb[j].e == ca[i].e && cb[j].p >= ca[i].p)) need = 1;
+        needed[i] = need;
+        if (need) search(&X, ca[i].e, ca[i].p, &nm);
+        for (int j = 0; j < Kb; ++j) {
+          rkey r;
+          if (route_of(&X, &nm, ca[i].e, ca[i].p, cb[j].e, cb[j].p, &r))
+            trans[i * ORC_KMAX + j] = ((double)(r.k - r.d) / 1000.0 + fabs((double)r.d / 1000.0 - gcd)) * inv_beta;
+        }
+      }
+      /* the statistics */
+      if (!forced) {
+        S->steps++;
+        int ord[ORC_KMAX];
+        for (int i = 0; i < Ka; ++i) ord[i] = i;
+        for (int x = 1; x < Ka; ++x) /* insertion sort by (cost, index) */
+          for (int y = x; y > 0 && cost[ord[y]] < cost[ord[y - 1]]; --y) {
+            const int tmp = ord[y];
+            ord[y] = ord[y - 1];
+            ord[y - 1] = tmp;
+          }
+        double U[ORC_KMAX];
+        for (int j = 0; j < Kb; ++j) U[j] = INFINITY;
+        /* same-edge forward targets need no search: their offers count toward U first */
+        for (int i = 0; i < Ka; ++i)
+          for (int j = 0; j < Kb; ++j)
+            if (cb[j].e == ca[i].e && cb[j].p >= ca[i].p && trans[i * ORC_KMAX + j] != INFINITY &&
+                cost[i] != INFINITY && cost[i] + trans[i * ORC_KMAX + j] < U[j])
+              U[j] = cost[i] + trans[i * ORC_KMAX + j];
+        for (int x = 0; x < Ka; ++x) {
+          const int i = ord[x];
+          if (!needed[i]) continue;
+          S->sources++;
+          if (cost[i] == INFINITY) {
+            S->inf_sources++;
+            continue;
+          }
+          int skip = 1;
+          for (int j = 0; j < Kb && skip; ++j) {
+            if (cb[j].e == ca[i].e && cb[j].p >= ca[i].p) continue;
+            if (!(U[j] < cost[i])) skip = 0;
+          }
+          if (skip) {
+            S->skip_local++;
+            continue;
+          }
+          S->searched_local++;
+          for (int j = 0; j < Kb; ++j)
+            if (trans[i * ORC_KMAX + j] != INFINITY && cost[i] + trans[i * ORC_KMAX + j] < U[j])
+              U[j] = cost[i] + trans[i * ORC_KMAX + j];
+        }
+      }
+      int any = 0;
+      for (int j = 0; j < Kb; ++j) {
+        double best = INFINITY;
+        int bi = -1;
+        for (int i = 0; i < Ka; ++i) {
+          const double tr = trans[i * ORC_KMAX + j];
+          if (tr == INFINITY || cost[i] == INFINITY) continue;
+          const double c = cost[i] + tr;
+          if (c < best) {
+            best = c;
+            bi = i;
+          }
+        }
+        ncost[j] = bi >= 0 ? best + cb[j].d2 * inv2s2 : INFINITY;
+        if (bi >= 0) any = 1;
+      }
+      if (!any) {
+        S->brk++;
+        for (int j = 0; j < Kb; ++j) ncost[j] = cb[j].d2 * inv2s2;
+      }
+      memcpy(cost, ncost, sizeof(cost));
+    }
+  }
+  nm_free(&nm);
   free(md.time_ds);
   return 0;
 }

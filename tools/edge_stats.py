@@ -28,7 +28,9 @@ class Stats(ctypes.Structure):
         ('pend_max', ctypes.c_int64), ('max_rounds_sum', ctypes.c_int64), ('relaxed', ctypes.c_int64),
         ('groups', ctypes.c_int64), ('hist_bmm_keys', (ctypes.c_int64 * 24) * 24),
         ('settled_out', ctypes.c_int64), ('rounds_out', ctypes.c_int64), ('scans_tmin', ctypes.c_int64),
-        ('scans_out', ctypes.c_int64), ('settled_tterm', ctypes.c_int64), ('rounds_tterm', ctypes.c_int64)]
+        ('scans_out', ctypes.c_int64), ('settled_tterm', ctypes.c_int64), ('rounds_tterm', ctypes.c_int64),
+        ('settled_ast', ctypes.c_int64), ('rounds_ast', ctypes.c_int64), ('settled_ast1', ctypes.c_int64),
+        ('rounds_ast1', ctypes.c_int64)]
 
 
 def main():
@@ -67,6 +69,8 @@ def main():
         'settled_per_search_tmin': S.settled_tmin / n, 'rounds_per_search_tmin': S.rounds_tmin / n,
         'settled_per_search_out': S.settled_out / n, 'rounds_per_search_out': S.rounds_out / n,
         'settled_per_search_tterm': S.settled_tterm / n, 'rounds_per_search_tterm': S.rounds_tterm / n,
+        'settled_per_search_astar': S.settled_ast / n, 'rounds_per_search_astar': S.rounds_ast / n,
+        'settled_per_search_astar1': S.settled_ast1 / n, 'rounds_per_search_astar1': S.rounds_ast1 / n,
         'pending_scanned_per_search_tmin': S.scans_tmin / n, 'pending_scanned_per_search_out': S.scans_out / n,
         'groups': S.groups, 'sources_per_group': S.sources / st, 'sum_keys_per_step': S.sum_keys / st,
         'union_keys_per_step': S.union_keys / st, 'max_rounds_per_step': S.max_rounds_sum / st,
