@@ -632,7 +632,11 @@ def main():
                                        'ms': round(1e3 * tile_stats[-1][2], 3)} if tile_stats else None),
                        'work': {'states': int(sum(r.n_states for r in rs)), 'grid_cells': int(counters[0]),
                                 'shape_segments_tested': int(counters[1]), 'candidates': int(counters[2]),
-                                'output_segments': int(counters[7])}},
+                                'output_segments': int(counters[7]),
+                                # edge-state searches that outgrew a table and went on in the next
+                                # one from their HBM dump (otr_edge1.h), turn-cost modes only
+                                'edge_searches_dumped': int(counters[23]),
+                                'edge_searches_resumed': int(counters[22])}},
             'roofline': {'kernel': kernel_name(dom['code'], turns, dom_t == 0) + ' (dominant route-search kernel of this workload)',
                          'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': traffic,

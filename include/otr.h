@@ -186,7 +186,8 @@ typedef struct otr_batch_result {
                                   6 transition entries, 7 output segments, 8 tile rows,
                                   9/10 settled/relaxed of the large-table retry, 13 search rounds
                                   and 14 table keys (first-tier route launch),
-                                  16-19 diagnostic-build search phase cycles */
+                                  16-21 diagnostic-build search phase cycles, 22/23 edge-state
+                                  searches resumed from / dumped to HBM (next table) */
   float kernel_ms[16];         /* OTR_BATCH_TIMING: device time per stage, OTR_STAGE_* */
   int32_t* trace_status;       /* host, per trace (with COPY_OUT / COPY_REPORTS): OTR_OK, or
                                   OTR_MATCH_ERROR when its search outgrew the largest LDS table */

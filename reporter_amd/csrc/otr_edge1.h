@@ -262,6 +262,103 @@ __device__ inline void e1_turn_table(E1Lds<CAP>& L, const int32_t* turn_tab, int
 }
 
 // ------------------------------------------------------------------------------
+// Resuming an outgrown search in the next table.  A search stops between two rounds when
+// its keys pass the table's load limit (no relaxation lost: the table never filled), and
+// its whole state goes to a dump slot in HBM: the round's frontier values (kmin, dmin,
+// tmn), the targets' best offers, and every key of the table with its label — settled
+// states too, whose final labels must keep rejecting later offers.  The next tier's wave
+// re-inserts the keys into its larger table, rebuilds each state's static word from the
+// graph (head node, reversed end heading, IN-gap code), refills the pending list and goes
+// on with the next round: the same rounds the search would have run in one big table, so
+// the same labels, without redoing the part already searched.
+// Slot layout (u64 words): [0..1] {entries, pending, kmin, dmin}, [2..3] {tmn, settled,
+// relaxed, 0}, [8..39] the targets' offers, [40..40+CAP) labels, then CAP u32 keys
+// (edge id | kInq | kDumpPend).
+// ------------------------------------------------------------------------------
+constexpr uint32_t kDumpPend = 0x40000000u;  // dump key bit: the state is on the pending list
+__host__ __device__ constexpr uint32_t e1_dump_words(int cap) { return 40u + (uint32_t)cap + ((uint32_t)cap + 1u) / 2u; }
+
+template <int CAP>
+__device__ inline void e1_dump(E1Lds<CAP>& L, unsigned long long* D, int npend, uint32_t kmin, uint32_t dmin,
+                               uint32_t tmn, uint32_t settled, uint32_t relaxed) {
+  const int lane = (int)threadIdx.x;
+  for (int k = lane; k < npend; k += OTR_WAVE) L.key[L.pend[k]] |= kDumpPend;  // (one list entry per state)
+  __syncthreads();
+  unsigned long long* dl = D + 40;
+  uint32_t* dk = reinterpret_cast<uint32_t*>(dl + CAP);
+  int n = 0;
+#pragma unroll 1
+  for (int base = 0; base < CAP; base += OTR_WAVE) {
+    const int k = base + lane;
+    const uint32_t kw = k < CAP ? L.key[k] : kEmpty;
+    const bool has = kw != kEmpty;
+    const unsigned long long m = __ballot(has);
+    if (has) {
+      const int pos = n + prefix_count(m);
+      dl[pos] = L.lab[k];
+      dk[pos] = kw;
+    }
+    n += __popcll(m);
+  }
+  if (lane < E1Lds<CAP>::TG) D[8 + lane] = L.tlab[lane];
+  if (lane == 0) {
+    reinterpret_cast<uint4*>(D)[0] = make_uint4((uint32_t)n, (uint32_t)npend, kmin, dmin);
+    reinterpret_cast<uint4*>(D)[1] = make_uint4(tmn, settled, relaxed, 0u);
+  }
+}
+
+// the dumped search back into this (empty, larger) table; returns its key count, the
+// pending list in L.pend[0..npend)
+template <int CAP>
+__device__ inline int e1_restore(E1Lds<CAP>& L, const DevGraph& gr, const unsigned long long* D, uint32_t in_cap,
+                                 uint32_t ei, int& npend, uint32_t& kmin, uint32_t& dmin, uint32_t& tmn,
+                                 uint32_t& settled, uint32_t& relaxed) {
+  const int lane = (int)threadIdx.x;
+  const uint4 h0 = reinterpret_cast<const uint4*>(D)[0], h1 = reinterpret_cast<const uint4*>(D)[1];
+  const int n = (int)h0.x;
+  kmin = h0.z;
+  dmin = h0.w;
+  tmn = h1.x;
+  if (lane == 0) {
+    settled += h1.y;
+    relaxed += h1.z;
+  }
+  if (lane < E1Lds<CAP>::TG) L.tlab[lane] = D[8 + lane];
+  const unsigned long long* dl = D + 40;
+  const uint32_t* dk = reinterpret_cast<const uint32_t*>(dl + in_cap);
+  int np = 0;
+#pragma unroll 1
+  for (int base = 0; base < n; base += OTR_WAVE) {
+    const int k = base + lane;
+    bool pend = false;
+    int sl = 0;
+    if (k < n) {
+      const uint32_t kw = dk[k];
+      const unsigned long long lb = dl[k];
+      const uint32_t e = kw & kNodeMask;
+      uint32_t h = hslot<CAP>(e);
+#pragma unroll 1
+      for (int probe = 0; probe < CAP; ++probe) {  // (distinct keys, a larger table: an empty slot)
+        if (atomicCAS(&L.key[h], kEmpty, e) == kEmpty) break;
+        h = h + 1 == (uint32_t)CAP ? 0u : h + 1;
+      }
+      sl = (int)h;
+      L.key[sl] = kw & (kNodeMask | kInq);
+      L.lab[sl] = lb;
+      const short2 hh = gr.edge_head[e];
+      L.meta[sl] = e1_meta(gr.edge_dst[e], (uint32_t)heading_back((int)(uint16_t)hh.y),
+                           e == ei ? 0u : (uint32_t)mi8_of(gr.len_mm[e]));
+      pend = (kw & kDumpPend) != 0u;
+    }
+    const unsigned long long mp = __ballot(pend);
+    if (pend) L.pend[np + prefix_count(mp)] = (typename E1Lds<CAP>::Idx)sl;
+    np += __popcll(mp);
+  }
+  npend = np;
+  return n;
+}
+
+// ------------------------------------------------------------------------------
 // K3e1 kernel: a persistent grid over the device-side list of the turn-mode tasks (one
 // source candidate each), the 8 XCDs taking contiguous eighths of the list (consecutive
 // tasks = the candidates of one step, then the next steps of the trace: one neighbourhood),
@@ -345,10 +442,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
     __syncthreads();
     // the bloom of the target nodes: a settled state consults the map only on a hit
     const unsigned long long bloom = L.bloom;
-    bool ok = true;
+    bool ok = true, dump = false;
     uint32_t my_settled = 0, my_relaxed = 0;
+    uint32_t kmin = 0, dmin = 0, tmn = 0;  // the smallest pending key / length / time
+    int npend = 1, nkeys = 1;
+    // a search the previous (smaller) table outgrew goes on from its dump (e1_restore)
+    const int32_t rslot = (a.e1_in != nullptr && search) ? a.task_dump[task] : -1;
     if (search) {
-      if (lane == 0) {
+      if (rslot >= 0) {
+        nkeys = e1_restore(L, gr, a.e1_in + (size_t)rslot * a.e1_in_words, a.e1_in_cap, ei, npend, kmin, dmin, tmn,
+                           my_settled, my_relaxed);
+      } else if (lane == 0) {
         bool isnew = false;
         const int sl = e1_insert(L, ei, isnew);  // (an empty table: the home slot)
         // the root: label 0 is final at once (mi 0: gap 1 mm)
@@ -361,9 +465,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
       const uint4* er = gr.erec + (size_t)md * gr.erec_stride;
       const uint32_t mode_bit = 1u << md;
       const uint32_t tmin = L.tmin;
-      uint32_t kmin = 0, dmin = 0, tmn = 0;  // the smallest pending key / length / time
-      int npend = 1, nkeys = 1;
       uint32_t pf = 0;  // (OTR_E1PF: the prefetch loads' sink)
+#ifdef OTR_FORCE_RETRY
+      int rounds = 0;
+#endif
 #pragma unroll 1
       for (;;) {
         OTR_STAMP(tr0);
@@ -505,12 +610,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
 #endif
         if (L.overflow || nkeys > kMaxKeys) {
           ok = false;
+          dump = !L.overflow;  // (a full table lost a relaxation: that search restarts)
           break;
         }
+#ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 5 / 6 stops every OTR_E1CAP / 512-state search
+                        // after 2 / 4 rounds, to be resumed in the next table
+        ++rounds;
+        if (((a.force_edge & 32) && CAP == OTR_E1CAP && rounds == 2) ||
+            ((a.force_edge & 64) && CAP == 512 && rounds == 4)) {
+          ok = false;
+          dump = true;
+          break;
+        }
+#endif
       }
     }
 #ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 0 / 1 / 2 fails every OTR_E1CAP (360) / 512 / 1024-state search
-    if (a.force_edge & (CAP < 512 ? 1 : (CAP < 1024 ? 2 : 4))) ok = false;
+    if (a.force_edge & (CAP < 512 ? 1 : (CAP < 1024 ? 2 : 4))) {
+      ok = false;
+      dump = false;
+    }
 #endif
     ok = ok && Kb <= TG;
     if (ok) {
@@ -544,10 +663,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           atomicAdd(&counters[4 * kCShards + sh], (unsigned long long)rl);
           atomicAdd(&counters[5 * kCShards + sh], search ? (unsigned long long)Kb : 0ull);
           atomicAdd(&counters[6 * kCShards + sh], search ? 1ull : 0ull);
+          if (rslot >= 0) atomicAdd(&counters[22 * kCShards + sh], 1ull);  // (resumed from a dump)
         }
       }
-    } else if (lane == 0) {
-      a.overflow_flag[task] = CAP < 512 ? 6 : (CAP < 1024 ? 7 : 3);  // the next table: 512, 1024, k_general
+    } else {
+      // the next table (512, 1024 states, then k_general) resumes the search from its dump
+      // when it stopped between two rounds and a dump slot is free, else starts it afresh
+      int32_t slot = -1;
+      if (dump && a.e1_out != nullptr) {
+        unsigned long long v = 0;
+        if (lane == 0) v = atomicAdd(a.e1_out_ctr, 1ull);
+        v = (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+        if (v < (unsigned long long)a.e1_out_slots) slot = (int32_t)v;
+      }
+      if (slot >= 0) e1_dump(L, a.e1_out + (size_t)slot * a.e1_out_words, npend, kmin, dmin, tmn, 0u, 0u);
+      if (counters && slot >= 0 && lane == 0) atomicAdd(&counters[23 * kCShards + cshard()], 1ull);
+      if (lane == 0) {
+        a.overflow_flag[task] = CAP < 512 ? 6 : (CAP < 1024 ? 7 : 3);
+        if (a.task_dump != nullptr) a.task_dump[task] = slot;
+      }
     }
     __syncthreads();
 #ifdef OTR_STAMPS

@@ -393,6 +393,7 @@ enum Slot {
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
   S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST, S_HE_PKEY, S_QUEUE, S_PQUEUE,
+  S_E1DUMP0, S_E1DUMP1, S_TASK_DUMP,
   S_NUM
 };
 
@@ -1062,6 +1063,32 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // edge-state tiers (turn-cost modes, otr_edge1.h): OTR_E1CAP (360) states (flag 5, slot
     // 10), 512 (flag 6, slot 9), 1024 (flag 7, slot 11); what outgrows those (flag 3) goes on below
     if (turns) {
+      // dump slots of the first two edge tiers: a search they outgrow between two rounds
+      // resumes in the next table (otr_edge1.h e1_dump / e1_restore) instead of starting
+      // over; slots for 1/16 of the tasks (C2, deployed: 4.4 % outgrow the first table),
+      // at most 4 GB / 1 GB — searches beyond them, or when the memory is not there,
+      // restart in the next table (same results)
+      static const bool resume = !getenv("OTR_E1RESUME") || atoi(getenv("OTR_E1RESUME")) != 0;  // A/B knob
+      unsigned long long* dump[2] = {nullptr, nullptr};
+      uint32_t dslots[2] = {0u, 0u};
+      int32_t* task_dump = nullptr;
+      const uint32_t dwords[2] = {e1_dump_words(OTR_E1CAP), e1_dump_words(512)};
+      if (resume) {
+        const int64_t cap_bytes[2] = {4ll << 30, 1ll << 30};
+        const int64_t want[2] = {std::max<int64_t>(NT / 16, 4096), std::max<int64_t>(NT / 64, 1024)};
+        try {
+          task_dump = need<int32_t>(S_TASK_DUMP, NT);
+          for (int q = 0; q < 2; ++q) {
+            const int64_t n = std::min<int64_t>(want[q], cap_bytes[q] / (8 * (int64_t)dwords[q]));
+            dump[q] = need<unsigned long long>(q == 0 ? S_E1DUMP0 : S_E1DUMP1, (size_t)n * dwords[q]);
+            dslots[q] = (uint32_t)n;
+          }
+        } catch (const DeviceOom&) {
+          (void)hipGetLastError();  // (no dumps beyond what was allocated: those searches restart)
+          if (!task_dump) dump[0] = dump[1] = nullptr;
+          if (!dump[0]) dump[1] = nullptr;
+        }
+      }
       for (int et = 0; et < 3; ++et) {
         const int slot = et == 0 ? 10 : (et == 1 ? 9 : 11);
         out->route_tier_code[slot] = 6000000 + (et == 0 ? OTR_E1CAP : (et == 1 ? 512 : 1024)) * 100 + 32;
@@ -1071,6 +1098,14 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         rb.task_list = list;
         rb.list_count = c;
         rb.queue = queues + (9 + et) * kQueueWords;
+        rb.e1_in = et > 0 ? dump[et - 1] : nullptr;
+        rb.e1_in_words = et > 0 ? dwords[et - 1] : 0u;
+        rb.e1_in_cap = et == 1 ? OTR_E1CAP : 512;
+        rb.e1_out = et < 2 ? dump[et] : nullptr;
+        rb.e1_out_ctr = queues + (13 + et) * kQueueWords;  // (queues 13, 14: zeroed above)
+        rb.e1_out_words = et < 2 ? dwords[et] : 0u;
+        rb.e1_out_slots = et < 2 ? dslots[et] : 0u;
+        rb.task_dump = task_dump;
         unsigned long long* rcn = rwork ? d_counters + (et == 0 ? 10 : (et == 1 ? 1 : 11)) * bank : nullptr;
         if (timing) (void)hipEventRecord(ev[24 + 2 * slot], stream);
         // persistent grids of at least every resident wave (16 per CU at 384 states, 13 at
@@ -1462,6 +1497,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   }
   out->counters[5] = (uint64_t)NT;
   out->counters[6] = (uint64_t)NTR;
+  // edge-state searches resumed from a dump (the 512- and 1024-state tiers) and dumped
+  // (the first two edge tiers), with OTR_BATCH_ROUTE_WORK
+  out->counters[22] = ctr(1, 22) + ctr(11, 22);
+  out->counters[23] = ctr(10, 23) + ctr(1, 23);
   if (!(in->flags & OTR_BATCH_TILE_ROWS)) out->n_rows = (int64_t)out->counters[8];
   else out->counters[8] = (uint64_t)out->n_rows;  // K9 counted them (K8 may not have run)
   out->d_hist = ha.hist;

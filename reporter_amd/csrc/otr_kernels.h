@@ -1073,7 +1073,17 @@ struct RouteArgs {
   unsigned long long* stamps;  // diagnostic build (OTR_STAMPS): bank 0 of the work counters (phase cycles)
   int force_edge;             // test build only (OTR_FORCE_RETRY, env OTR_FORCE_EDGE): bits 0 / 1 / 2 fail
                               // every OTR_E1CAP (360) / 512 / 1024-state edge-state route search (the
-                              // next tier takes it), bits 3 / 4 every 384 / 2048-state winner path
+                              // next tier takes it), bits 3 / 4 every 384 / 2048-state winner path;
+                              // bits 5 / 6 stop every OTR_E1CAP / 512-state search after 2 / 4 rounds
+                              // and resume it in the next table (otr_edge1.h e1_dump / e1_restore)
+  // edge-state tiers: a search that outgrows its table is dumped between two rounds and
+  // resumed in the next table (otr_edge1.h)
+  const unsigned long long* e1_in;  // the previous tier's dumps (null: every search starts afresh)
+  uint32_t e1_in_words, e1_in_cap;  // u64 words per dump slot, the table size that wrote them
+  unsigned long long* e1_out;       // this tier's dump slots (null: outgrown searches restart)
+  unsigned long long* e1_out_ctr;   // slots taken (device counter, zeroed per batch)
+  uint32_t e1_out_words, e1_out_slots;
+  int32_t* task_dump;               // per task: its slot in the next tier's input, -1: restart
 };
 
 // k_tasks' inputs and outputs

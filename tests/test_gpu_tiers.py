@@ -137,6 +137,11 @@ for g, nt, npnt, sr, sig, seed, fb, fp in [('city', 40, 100, 15, 10.0, 2, 0.0, 0
         assert w[9] == 0 and w[11] == 0 and w[6] > 0, w
     if force == 0:
         assert w[10] > 0, w
+    resumed, dumped = int(r.counters[22]), int(r.counters[23])
+    if force & 32:  # every first-table search stopped after 2 rounds and resumed at 512 states
+        assert w[10] > 0 and w[9] > 0 and resumed > 0 and dumped >= resumed, (w, resumed, dumped)
+    if force & 64:  # and every 512-state search after 4 rounds, resumed at 1024
+        assert w[11] > 0 and resumed > 0, (w, resumed, dumped)
     got = _lib.result_to_numpy(r)
     want = po.match_batch(po.Graph(path), tr, po.params(), threads=8)
     errors, stats = compare(got, want)
@@ -145,11 +150,13 @@ print('edge tiers ok')
 '''
 
 
-@pytest.mark.parametrize('force', [0, 1, 3, 7, 24])
+@pytest.mark.parametrize('force', [0, 1, 3, 7, 24, 32, 96, 34])
 def test_edge_tiers_equal_oracle(graph_dir, force):
-    """libotr_tiercheck.so with OTR_FORCE_EDGE: bits 0-2 fail every 256 / 512 / 1024-state
+    """libotr_tiercheck.so with OTR_FORCE_EDGE: bits 0-2 fail every 360 / 512 / 1024-state
     edge-state route search, bits 3-4 every 384 / 2048-state winner path; the next tier takes
-    them (route_tier_work shows which did) and the output still equals the oracle."""
+    them (route_tier_work shows which did) and the output still equals the oracle.  Bits 5-6
+    stop every 360 / 512-state search after 2 / 4 rounds: the next table resumes it from its
+    dump in HBM (34: resumed at 512, then failed there and restarted at 1024)."""
     lib = os.path.join(ROOT, 'reporter_amd', 'libotr_tiercheck.so')
     assert os.path.exists(lib), 'build first: python -m reporter_amd.build'
     env = dict(os.environ, OTR_LIB=lib, OTR_FORCE_EDGE=str(force))
