@@ -471,13 +471,21 @@ def main():
                                           'gbs': round(route_bytes(d['work'] / d['launches']) /
                                                        (max(d['ms'], 1e-9) / d['launches'] * 1e-3) / 1e9, 1)}
                   for t, d in sorted(tiers.items())}
-    traffic, traffic_src = None, None
-    # (the PMC summary is of the default C2 command: other workloads report no traffic)
-    if os.path.exists(PMC_SUMMARY) and args.workload == 'c2' and args.streams == 1:
-        k = json.load(open(PMC_SUMMARY)).get('kernels', {}).get(kernel_name(dom['code'], turns, dom_t == 0), {})
+    traffic, traffic_src, l2_hit = None, None, None
+    # FETCH_SIZE + WRITE_SIZE of the dominant kernel from the committed PMC summary of this
+    # workload's bench command (tools/profile_set.sh + tools/profile_summary.py:
+    # profiles/<round>_pmc_<workload>.json; OTR_PMC_SUMMARY overrides)
+    psum = PMC_SUMMARY if os.environ.get('OTR_PMC_SUMMARY') else None
+    if psum is None:
+        import glob
+        cands = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_pmc_%s.json' % args.workload)))
+        psum = cands[-1] if cands else (PMC_SUMMARY if args.workload == 'c2' else None)
+    if psum and os.path.exists(psum) and args.streams == 1:
+        k = json.load(open(psum)).get('kernels', {}).get(kernel_name(dom['code'], turns, dom_t == 0), {})
         if 'fetch_bytes_per_launch' in k and 'write_bytes_per_launch' in k:
             traffic = int(k['fetch_bytes_per_launch'] + k['write_bytes_per_launch'])
-            traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
+            traffic_src = os.path.relpath(psum, ROOT)
+            l2_hit = k.get('l2_hit')
 
     # ---- rank 0: oracle sample (CPU baseline) and its bit-exact comparison, on rank 0's
     # own shard at every N (after the timed region; the other ranks wait at the closing
@@ -640,7 +648,7 @@ def main():
             'roofline': {'kernel': kernel_name(dom['code'], turns, dom_t == 0) + ' (dominant route-search kernel of this workload)',
                          'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': traffic,
-                         'traffic_source': traffic_src, 'launch_ms': round(launch_ms, 3),
+                         'traffic_source': traffic_src, 'l2_hit': l2_hit, 'launch_ms': round(launch_ms, 3),
                          'algorithmic_bytes': int(dom_bytes),
                          'bytes_formula': 'SURVEY 8(d): 24 B x settled + 16 B x relaxed + 8 B x transitions',
                          'searches': int(dom['work'][0] // dom['launches']),

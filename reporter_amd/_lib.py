@@ -159,9 +159,10 @@ def lib():
                                    ctypes.c_int32, P(ctypes.c_void_p), P(ctypes.c_size_t)]
     L.otr_ingest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, P(IngestFormat),
                              P(IngestResult)]
-    L.otr_max_batch_probes.restype = ctypes.c_int64
-    L.otr_launch_max_items.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32]
-    L.otr_launch_max_items.restype = ctypes.c_uint64
+    if hasattr(L, 'otr_max_batch_probes'):  # (an A/B build of an earlier round may lack them)
+        L.otr_max_batch_probes.restype = ctypes.c_int64
+        L.otr_launch_max_items.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32]
+        L.otr_launch_max_items.restype = ctypes.c_uint64
     L.otr_tilehier_row.argtypes = [ctypes.c_int32, ctypes.c_double]
     L.otr_tilehier_row.restype = ctypes.c_int32
     L.otr_tilehier_col.argtypes = [ctypes.c_int32, ctypes.c_double]

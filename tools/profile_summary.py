@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Summary of one workload of tools/profile_set.sh: per kernel the launches and average
+duration (kernel trace), FETCH_SIZE and WRITE_SIZE per launch (their own --pmc passes,
+KiB counters -> bytes; gfx950: the raw sum, see DESIGN.md §4 on the calibration), the
+L2 (TCC) hit rate, and measured HBM GB/s = (fetch + write) / duration against 8 TB/s.
+
+  python tools/profile_summary.py gpurun_out/r05p/c2dep > profiles/r05_pmc_c2dep.json
+"""
+import csv
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+PEAK_GBS = 8000.0
+
+
+def short(name):
+    name = re.sub(r'^void ', '', name)
+    name = re.sub(r'\(.*$', '', name)
+    return re.sub(r'^otr::', '', name)
+
+
+def find(d, suffix):
+    for root, _, files in os.walk(d):
+        for f in files:
+            if f.endswith(suffix):
+                return os.path.join(root, f)
+    return None
+
+
+def per_dispatch(path, names):
+    """{kernel: ({counter: average over the kernel's dispatches}, dispatches)}: one row per
+    dispatch and counter (rocprofv3 csv)."""
+    acc = defaultdict(lambda: defaultdict(list))
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if any(r['Counter_Name'].startswith(n) for n in names):
+                acc[short(r['Kernel_Name'])][r['Counter_Name']].append(float(r['Counter_Value']))
+    return {k: ({c: sum(v) / len(v) for c, v in cs.items()}, max(len(v) for v in cs.values())) for k, cs in acc.items()}
+
+
+def main(d):
+    kt = find(os.path.join(d, 'kt'), 'kernel_trace.csv')
+    dur = defaultdict(list)
+    with open(kt) as f:
+        for r in csv.DictReader(f):
+            dur[short(r['Kernel_Name'])].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) * 1e-6)
+    fetch = per_dispatch(find(os.path.join(d, 'FETCH_SIZE'), 'counter_collection.csv'), ['FETCH_SIZE'])
+    write = per_dispatch(find(os.path.join(d, 'WRITE_SIZE'), 'counter_collection.csv'), ['WRITE_SIZE'])
+    l2 = per_dispatch(find(os.path.join(d, 'TCC_HIT_sum'), 'counter_collection.csv'), ['TCC_HIT', 'TCC_MISS'])
+    out = {'source': os.path.relpath(d), 'kernels': {}}
+    for k in sorted(dur, key=lambda k: -sum(dur[k])):
+        if not k.startswith('k_'):
+            continue
+        e = {'launches': len(dur[k]), 'avg_ms': round(sum(dur[k]) / len(dur[k]), 4),
+             'total_ms': round(sum(dur[k]), 3)}
+        if k in fetch:
+            e['fetch_bytes_per_launch'] = round(sum(fetch[k][0].values()) * 1024.0)
+        if k in write:
+            e['write_bytes_per_launch'] = round(sum(write[k][0].values()) * 1024.0)
+        if k in l2:
+            h = sum(v for c, v in l2[k][0].items() if c.startswith('TCC_HIT'))
+            m = sum(v for c, v in l2[k][0].items() if c.startswith('TCC_MISS'))
+            e['l2_hit'] = round(h / (h + m), 4) if h + m > 0 else None
+        if 'fetch_bytes_per_launch' in e and 'write_bytes_per_launch' in e and e['avg_ms'] > 0:
+            gbs = (e['fetch_bytes_per_launch'] + e['write_bytes_per_launch']) / (e['avg_ms'] * 1e-3) / 1e9
+            e['hbm_gbs'] = round(gbs, 1)
+            e['hbm_frac'] = round(gbs / PEAK_GBS, 4)
+        out['kernels'][k] = e
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == '__main__':
+    main(sys.argv[1])
