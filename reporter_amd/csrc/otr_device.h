@@ -96,8 +96,10 @@ struct DevGraph {
   uint32_t adj_t_stride, edge_t_stride;  // elements per mode
   const short2* edge_head;     // per edge {begin heading, end heading}, integer degrees
   const uint2* adj_e;          // 4 per node like adj: {edge id, begin heading | end heading << 16} (edge-state searches)
-  const uint4* erec;           // [mode][4 per node like adj]: the edge-state search's record (otr_edge1.h erec_make)
-  uint32_t erec_stride;        // records per mode
+  const uint4* erec;           // [4 per edge state b]: b's out-edge slots {e | access | more, len_mm, turn degree b -> e
+                               // | end heading of b << 8, dst(b)} (otr_edge1.h, the edge-state search)
+  const uint32_t* erec_t;      // [mode][4 per edge state]: the slot's route time, 0.1 s (saturated at 2^17 - 1)
+  size_t erec_stride;          // records per mode of erec_t
   uint32_t n_nodes, n_edges, n_segments, grid_rows, grid_cols;
   double grid_min_lat, grid_min_lon, grid_cell_deg;
   __device__ const uint32_t* et(int mode) const { return edge_t + (size_t)mode * edge_t_stride; }

@@ -8,10 +8,9 @@
 // changes is the cost of a round, which is what bounds this search (otr_edge.h's kernel,
 // measured: ~13 rounds of ~600 wave instructions each, a third of the SIMD's VALU issue
 // used at 4.25 waves per SIMD; this one: 4 waves per SIMD):
-//   * one 16-B per-mode record per relaxation (DevGraph::erec: head, length, edge id,
-//     route time, begin and end headings) instead of four loads;
-//   * the state keeps its edge's reversed end heading, and turn degrees are two compares
-//     (otr_device.h turn_from_back), not two integer modulos;
+//   * one 16-B record per relaxation, indexed by the settled state (edge) and the out-edge
+//     slot (DevGraph::erec: the out-edge's id, access and length, the turn degree from the
+//     state into it, resolved at graph load), beside one 4-B per-mode route time;
 //   * the IN criterion adds the mode's smallest turn cost (every later offer to a state
 //     crosses a turn >= tmin and the state's own edge): lab(b) < kmin + len(b) + tmin is
 //     final, and a target is final once tlab < kmin + tpart + tmin — fewer rounds, the
@@ -27,8 +26,9 @@
 //   * small tables: the first tier holds 360 states (table + lists + targets + the turn
 //     table in 10.1 KB: 16 waves per CU, ~96 % of the C2 searches); a search that outgrows
 //     it goes on to 512 and 1024 states (this kernel again), then k_general: same results;
-//   * a state's head node, reversed end heading and IN-gap code share one 64-bit LDS word,
-//     and a settled state's label and that word one 16-B list entry;
+//   * a state is its label, its key (edge id) and its IN-gap code in LDS (15 B with the
+//     pending index: 21 waves per CU), a settled state's label, edge and code one 16-B list
+//     entry;
 //   * the relax step is branch-free on its common path (e1_relax_sink);
 //   * waves claim tasks from per-XCD queues (XcdQueue, otr_device.h).
 #pragma once
@@ -38,25 +38,13 @@
 
 namespace otr {
 
-// the per-mode edge-state adjacency record, one per (node, slot) like DevGraph::adj:
-// {dst | access << 28 | more << 31, len_mm, edge | end heading bits 0-3 << 28,
-//  route time (0.1 s, saturated at 2^17 - 1) | begin heading << 17 | end heading bits 4-8 << 26}
-__host__ __device__ inline uint4 erec_make(uint32_t dw, uint32_t len, uint32_t e, uint32_t t, uint32_t hb,
-                                           uint32_t he) {
-  return make_uint4(dw, len, (e & kAdjDstMask) | ((he & 15u) << 28),
-                    (t < 0x1FFFFu ? t : 0x1FFFFu) | ((hb & 0x1FFu) << 17) | ((he >> 4) << 26));
-}
-__device__ inline uint32_t er_edge(const uint4& r) { return r.z & kAdjDstMask; }
-__device__ inline uint32_t er_he(const uint4& r) { return (r.z >> 28) | ((r.w >> 26) << 4); }
-__device__ inline uint32_t er_hb(const uint4& r) { return (r.w >> 17) & 0x1FFu; }
-__device__ inline uint32_t er_t(const uint4& r) { return r.w & 0x1FFFFu; }
+// the edge-state record of slot k of state b (DevGraph::erec[4 b + k]):
+// {e | access << 28 | more << 31, len_mm(e), turn degree b -> e | end heading of b << 8, dst(b)}
+__device__ inline uint32_t er_edge(const uint4& r) { return r.x & kAdjDstMask; }
+__device__ inline uint32_t er_deg(const uint4& r) { return r.z & 0xFFu; }
+__device__ inline uint32_t er_hbk(const uint4& r) { return (uint32_t)heading_back((int)((r.z >> 8) & 0x1FFu)); }
 
 
-// the partition touches each settled state's adjacency records (A/B knob; measured off:
-// the touch is a blocking system-scope load, 3.77M -> 3.89M probes/s without it at c2dep)
-#ifndef OTR_E1PF
-#define OTR_E1PF 0
-#endif
 // the first tier's settled-list size (states settled per round at most), and the larger tiers'
 #ifndef OTR_E1WCAP
 #define OTR_E1WCAP 32
@@ -83,9 +71,9 @@ struct E1Lds {
   using Idx = typename std::conditional<(CAP <= 256), uint8_t, uint16_t>::type;
   unsigned long long lab[CAP];  // gpack label, kGInf: none
   uint32_t key[CAP];            // edge id | kInq (on the pending list, or settled); kEmpty
-  unsigned long long meta[CAP]; // e1_meta: dst(edge), its end heading reversed, mi8_of(len(edge))
+  uint8_t mi[CAP];              // mi8_of(len(edge)): the IN criterion's gap (0 at the root)
   Idx pend[CAP];                // pending slots
-  uint4 wst[WCAP];              // this round's settled states: {label, meta} (one 16-B access)
+  uint4 wst[WCAP];              // this round's settled states: {label lo, hi, edge, mi} (one 16-B access)
   unsigned long long tlab[TG];  // the targets' best feasible offers
   uint32_t tpart[TG], tpt[TG];  // entry parts (mm, 0.1 s)
   uint16_t thb[TG];             // begin heading of the target edge
@@ -104,15 +92,6 @@ struct E1Lds {
 __device__ inline uint32_t tm_home(uint32_t v) { return (v * 0x9E3779B1u) >> 26; }  // 64 bloom bits
 __device__ inline uint32_t tm_slot(uint32_t v) { return (v * 0x9E3779B1u) >> 27; }  // 32 map slots
 
-// a state's static fields in one LDS word (written once when the state enters the table,
-// read with its label when it is settled): head node (28 bits), the edge's end heading
-// reversed (9), its IN-gap code mi8_of(len) (8)
-__device__ inline unsigned long long e1_meta(uint32_t node, uint32_t hbk, uint32_t mi) {
-  return (unsigned long long)node | ((unsigned long long)hbk << 28) | ((unsigned long long)mi << 37);
-}
-__device__ inline uint32_t em_node(unsigned long long m) { return (uint32_t)m & kAdjDstMask; }
-__device__ inline uint32_t em_hbk(unsigned long long m) { return (uint32_t)(m >> 28) & 0x1FFu; }
-__device__ inline uint8_t em_mi(unsigned long long m) { return (uint8_t)(m >> 37); }
 
 template <int CAP>
 __device__ inline int e1_insert(E1Lds<CAP>& L, uint32_t e, bool& isnew) {
@@ -152,23 +131,21 @@ __device__ inline void e1_target_offers(E1Lds<CAP>& L, unsigned long long lb, ui
   }
 }
 
-// relax the final state (label lb, reversed end heading hbk) through one out-edge: its
-// record fields (head w with access bits in dw, length, time, edge id, headings); returns
-// the slot when the edge's state became newly pending
+// relax the final state (label lb) through one out-edge b: access bits in dw, length,
+// time, the turn degree into b; returns the slot when b's state became newly pending
 template <int CAP>
-__device__ inline int e1_relax(E1Lds<CAP>& L, unsigned long long lb, uint32_t hbk, uint32_t dw, uint32_t len,
-                               uint32_t tt, uint32_t b, uint32_t hb, uint32_t hend, uint32_t pd, uint32_t pt,
-                               uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext, uint32_t& dnext, uint32_t& tnext,
-                               bool& isnew) {
+__device__ inline int e1_relax(E1Lds<CAP>& L, unsigned long long lb, uint32_t dw, uint32_t len, uint32_t tt,
+                               uint32_t b, uint32_t deg, uint32_t pd, uint32_t pt, uint32_t mode_bit,
+                               uint32_t& relaxed, uint32_t& knext, uint32_t& dnext, uint32_t& tnext, bool& isnew) {
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
-  const uint32_t tc = (uint32_t)L.turn[turn_from_back((int)hbk, (int)hb)];
+  const uint32_t tc = (uint32_t)L.turn[deg];
   const EOffer o = e_step(lb, tc, len, tt);
   if (!e_feasible(o, pd, pt)) return -1;  // pruned (label-setting semantics)
   const int sl = e1_insert(L, b, isnew);
   if (sl < 0) return -1;
   if (isnew) {
-    L.meta[sl] = e1_meta(dw & kAdjDstMask, (uint32_t)heading_back((int)hend), mi8_of(len));
+    L.mi[sl] = mi8_of(len);
     L.lab[sl] = kGInf;
   }
   const unsigned long long nw = gpack(o.k, o.c, o.t);
@@ -187,10 +164,10 @@ __device__ inline int e1_relax(E1Lds<CAP>& L, unsigned long long lb, uint32_t hb
 // bookkeeping of the nested ifs (scalar-unit work) is gone.  Only a probe chain past the
 // home slot branches.  Same slots, labels and pending list as e1_relax.
 template <int CAP>
-__device__ inline int e1_relax_sink(E1Lds<CAP>& L, unsigned long long lb, uint32_t hbk, uint32_t dw, uint32_t len,
-                                    uint32_t tt, uint32_t b, uint32_t hb, uint32_t hend, uint32_t pd, uint32_t pt,
-                                    uint32_t mode_bit, uint32_t& relaxed, uint32_t& knext, uint32_t& dnext,
-                                    uint32_t& tnext, bool& isnew) {
+__device__ inline int e1_relax_sink(E1Lds<CAP>& L, unsigned long long lb, uint32_t dw, uint32_t len, uint32_t tt,
+                                    uint32_t b, uint32_t deg, uint32_t pd, uint32_t pt, uint32_t mode_bit,
+                                    uint32_t& relaxed, uint32_t& knext, uint32_t& dnext, uint32_t& tnext,
+                                    bool& isnew) {
   unsigned long long* mine = &L.sink[threadIdx.x % OTR_E1SINK];  // (lanes sharing a word: a few-way atomic)
   uint32_t* mine32 = reinterpret_cast<uint32_t*>(mine);
   const bool mode_ok = (((dw >> 28) & 7u) & mode_bit) != 0u;
@@ -201,7 +178,7 @@ __device__ inline int e1_relax_sink(E1Lds<CAP>& L, unsigned long long lb, uint32
   bool go = mode_ok && g_d(lb) + len <= pd && g_t(lb) + tt <= pt;
   const uint32_t h0 = hslot<CAP>(b);
   const uint32_t k0 = atomicCAS(go ? &L.key[h0] : mine32, kEmpty, b);
-  const uint32_t tc = (uint32_t)L.turn[turn_from_back((int)hbk, (int)hb)];
+  const uint32_t tc = (uint32_t)L.turn[deg];
   const EOffer o = e_step(lb, tc, len, tt);
   isnew = go && k0 == kEmpty;
   int sl = (go && (k0 == kEmpty || (k0 & kNodeMask) == b)) ? (int)h0 : -1;
@@ -228,7 +205,7 @@ __device__ inline int e1_relax_sink(E1Lds<CAP>& L, unsigned long long lb, uint32
   }
   go = go && sl >= 0;
   const bool fresh = go && isnew;
-  *(fresh ? &L.meta[sl] : mine) = e1_meta(dw & kAdjDstMask, (uint32_t)heading_back((int)hend), mi8_of(len));
+  *(fresh ? &L.mi[sl] : reinterpret_cast<uint8_t*>(mine)) = mi8_of(len);
   *(fresh ? &L.lab[sl] : mine) = kGInf;
   const unsigned long long nw = gpack(o.k, o.c, o.t);
   const bool feas = go && o.c <= kTcCap;
@@ -268,7 +245,7 @@ __device__ inline void e1_turn_table(E1Lds<CAP>& L, const int32_t* turn_tab, int
 // tmn), the targets' best offers, and every key of the table with its label — settled
 // states too, whose final labels must keep rejecting later offers.  The next tier's wave
 // re-inserts the keys into its larger table, rebuilds each state's static word from the
-// graph (head node, reversed end heading, IN-gap code), refills the pending list and goes
+// graph (its IN-gap code), refills the pending list and goes
 // on with the next round: the same rounds the search would have run in one big table, so
 // the same labels, without redoing the part already searched.
 // Slot layout (u64 words): [0..1] {entries, pending, kmin, dmin}, [2..3] {tmn, settled,
@@ -345,9 +322,7 @@ __device__ inline int e1_restore(E1Lds<CAP>& L, const DevGraph& gr, const unsign
       sl = (int)h;
       L.key[sl] = kw & (kNodeMask | kInq);
       L.lab[sl] = lb;
-      const short2 hh = gr.edge_head[e];
-      L.meta[sl] = e1_meta(gr.edge_dst[e], (uint32_t)heading_back((int)(uint16_t)hh.y),
-                           e == ei ? 0u : (uint32_t)mi8_of(gr.len_mm[e]));
+      L.mi[sl] = e == ei ? (uint8_t)0 : mi8_of(gr.len_mm[e]);
       pend = (kw & kDumpPend) != 0u;
     }
     const unsigned long long mp = __ballot(pend);
@@ -456,16 +431,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
         bool isnew = false;
         const int sl = e1_insert(L, ei, isnew);  // (an empty table: the home slot)
         // the root: label 0 is final at once (mi 0: gap 1 mm)
-        L.meta[sl] = e1_meta(gr.edge_dst[ei], (uint32_t)heading_back((int)(uint16_t)gr.edge_head[ei].y), 0u);
+        L.mi[sl] = 0;
         L.lab[sl] = gpack(0u, 0u, 0u);
         L.key[sl] = ei | kInq;
         L.pend[0] = (typename LT::Idx)sl;
       }
       __syncthreads();
-      const uint4* er = gr.erec + (size_t)md * gr.erec_stride;
+      const uint4* er = gr.erec;
+      const uint32_t* ert = gr.erec_t + (size_t)md * gr.erec_stride;
       const uint32_t mode_bit = 1u << md;
       const uint32_t tmin = L.tmin;
-      uint32_t pf = 0;  // (OTR_E1PF: the prefetch loads' sink)
 #ifdef OTR_FORCE_RETRY
       int rounds = 0;
 #endif
@@ -492,13 +467,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           const int k = base + lane;
           const bool in = k < npend;
           int sl = 0;
-          unsigned long long lb = 0, mt = 0;
+          unsigned long long lb = 0;
+          uint32_t kw = 0, mq = 0;
           bool take = false;
           if (in) {
             sl = L.pend[k];
             lb = L.lab[sl];
-            mt = L.meta[sl];  // (read beside the label: the relax lanes then need no dependent read)
-            take = (uint64_t)g_k(lb) < (uint64_t)kmin + in_gap8(em_mi(mt)) + tmin;
+            kw = L.key[sl];  // (read beside the label: the relax lanes then need no dependent read)
+            mq = L.mi[sl];
+            take = (uint64_t)g_k(lb) < (uint64_t)kmin + in_gap8((uint8_t)mq) + tmin;
           }
           take = take && nw + prefix_count(__ballot(take)) < WCAP;
           const bool keep = in && !take;
@@ -506,13 +483,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           __syncthreads();
           if (take) {
             const int wq = nw + prefix_count(mtk);
-            L.wst[wq] = make_uint4((uint32_t)lb, (uint32_t)(lb >> 32), (uint32_t)mt, (uint32_t)(mt >> 32));
-#if OTR_E1PF
-            // touch the state's adjacency records now: the relax lanes' loads of them, after
-            // the barrier, then come from the near cache instead of L2 (pf is kept live
-            // until after the relax loop, so its register is not reused while in flight)
-            pf |= *(const volatile uint32_t*)(er + 4 * (size_t)em_node(mt));
-#endif
+            L.wst[wq] = make_uint4((uint32_t)lb, (uint32_t)(lb >> 32), kw & kNodeMask, mq);
           } else if (keep) {
             L.pend[kept + prefix_count(mk)] = (typename LT::Idx)sl;
             knext = g_k(lb) < knext ? g_k(lb) : knext;
@@ -535,34 +506,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           if (k < 4 * nw) {
             const uint4 ws = L.wst[k >> 2];
             const unsigned long long lb = ((unsigned long long)ws.y << 32) | ws.x;
-            const unsigned long long wm = ((unsigned long long)ws.w << 32) | ws.z;
-            const uint32_t v = em_node(wm), hbk = em_hbk(wm);
-            const int slot = k & 3;
-            // the record load is issued first and waited for only after the target offers
-            // (LDS work), so the two latencies overlap
-            uint4 r = er[4 * (size_t)v + slot];
-            if (slot == 0) {
+            const size_t ri = 4 * (size_t)ws.z + (k & 3);  // the settled state's slot record
+            // the slot's route time, loaded beside the record and unconditionally
+            const uint32_t tq = ert[ri];
+            const uint4 r = ld16(er + ri);
+            const uint32_t tt = timed ? tq : 0u;
+            if ((k & 3) == 0) {  // the state's head node (r.w) may be a target's source
               ++my_settled;
-              if ((bloom >> tm_home(v)) & 1ull) e1_target_offers(L, lb, hbk, v, pd, pt);
+              if ((bloom >> tm_home(r.w)) & 1ull) e1_target_offers(L, lb, er_hbk(r), r.w, pd, pt);
             }
-            asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w));  // (one 16-B load, not split)
 #if OTR_E1SINK
-            psl = e1_relax_sink(L, lb, hbk, r.x & ~kAdjMore, r.y, timed ? er_t(r) : 0u, er_edge(r), er_hb(r), er_he(r),
-                                pd, pt, mode_bit, my_relaxed, knext, dnext, tnext, isnew);
+            psl = e1_relax_sink(L, lb, r.x & ~kAdjMore, r.y, tt, er_edge(r), er_deg(r), pd, pt, mode_bit, my_relaxed,
+                                knext, dnext, tnext, isnew);
 #else
-            psl = e1_relax(L, lb, hbk, r.x & ~kAdjMore, r.y, timed ? er_t(r) : 0u, er_edge(r), er_hb(r), er_he(r), pd,
-                           pt, mode_bit, my_relaxed, knext, dnext, tnext, isnew);
+            psl = e1_relax(L, lb, r.x & ~kAdjMore, r.y, tt, er_edge(r), er_deg(r), pd, pt, mode_bit, my_relaxed, knext,
+                           dnext, tnext, isnew);
 #endif
-            tail = tail || (slot == 3 && (r.x & kAdjMore));
+            tail = tail || ((k & 3) == 3 && (r.x & kAdjMore));
           }
           nkeys += __popcll(__ballot(isnew));
           const unsigned long long mp = __ballot(psl >= 0);
           if (psl >= 0) L.pend[npend + prefix_count(mp)] = (typename LT::Idx)psl;  // (< CAP: one entry per state)
           npend += __popcll(mp);
         }
-#if OTR_E1PF
-        asm volatile("" ::"v"(pf));  // (the prefetches completed: their register is free again)
-#endif
         if (__ballot(tail) != 0ull) {  // nodes with more than four out-edges: the CSR tail
           if (lane == 0) {
             L.n_pend = npend;
@@ -575,18 +541,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
             if (k < 4 * nw && (k & 3) == 3) {
               const uint4 ws = L.wst[k >> 2];
               const unsigned long long lb = ((unsigned long long)ws.y << 32) | ws.x;
-              const unsigned long long wm = ((unsigned long long)ws.w << 32) | ws.z;
-              const uint32_t v = em_node(wm), hbk = em_hbk(wm);
-              if (er[4 * (size_t)v + 3].x & kAdjMore) {
+              const uint4 r3 = er[4 * (size_t)ws.z + 3];
+              if (r3.x & kAdjMore) {
                 const uint32_t* et = gr.et(md);
+                const uint32_t v = r3.w, hbk = er_hbk(r3);
 #pragma unroll 1
                 for (uint32_t e = gr.node_row[v] + 4; e < gr.node_row[v + 1]; ++e) {
                   const uint4 pk = ld16(gr.edge_pack + e);
-                  const short2 hh = gr.edge_head[e];
+                  const uint32_t deg = (uint32_t)turn_from_back((int)hbk, (int)(uint16_t)gr.edge_head[e].x);
                   bool nw2 = false;
-                  const int p2 = e1_relax(L, lb, hbk, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e,
-                                          (uint32_t)(uint16_t)hh.x, (uint32_t)(uint16_t)hh.y, pd, pt, mode_bit,
-                                          my_relaxed, knext, dnext, tnext, nw2);
+                  const int p2 = e1_relax(L, lb, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e, deg, pd, pt,
+                                          mode_bit, my_relaxed, knext, dnext, tnext, nw2);
                   if (nw2) atomicAdd(&L.n_keys, 1);
                   if (p2 >= 0) L.pend[atomicAdd(&L.n_pend, 1)] = (typename LT::Idx)p2;
                 }

@@ -248,17 +248,28 @@ int engine_configure(const Config& cfg, std::string* err) {
       const uint32_t e = row[u] + k;
       adje[4ull * u + k] = make_uint2(e, (uint32_t)(uint16_t)head[e].x | ((uint32_t)(uint16_t)head[e].y << 16));
     }
-  // edge-state view (otr_edge1.h): per mode one 16-B record per adjacency
-  // slot with the head, length, edge id, route time and both headings (one load per relaxation)
-  std::vector<uint4> erec((4ull * h.n_nodes + 4) * OTR_MODES, make_uint4(kAdjDstMask, 0u, 0u, 0u));
-  for (int m = 0; m < OTR_MODES; ++m) {
-    uint4* er = erec.data() + (4ull * h.n_nodes + 4) * m;
-    for (uint32_t u = 0; u < h.n_nodes; ++u)
-      for (uint32_t k = 0; k < 4 && row[u] + k < row[u + 1]; ++k) {
-        const uint32_t e = row[u] + k;
-        er[4ull * u + k] = erec_make(adj[4ull * u + k].x, len[e], e, et[m][e], (uint32_t)(uint16_t)head[e].x,
-                                     (uint32_t)(uint16_t)head[e].y);
+  // edge-state view (otr_edge1.h): per edge state b (arrived at v = dst(b)) one 16-B record
+  // per out-edge slot k < 4 of v: {e | access(e) << 28 | more << 31, len_mm(e), the turn
+  // degree b -> e | b's end heading << 8, v}, and per mode the slot's route time in a
+  // parallel array: a relaxation is one record load and one time load at the same index,
+  // with the turn already resolved
+  const size_t es = 4ull * h.n_edges + 4;
+  std::vector<uint4> erec(es, make_uint4(kAdjDstMask, 0u, 0u, 0u));
+  std::vector<uint32_t> erec_t(es * OTR_MODES, 0u);
+  for (uint32_t b = 0; b < h.n_edges; ++b) {
+    const uint32_t v = dst[b], deg = row[v + 1] - row[v];
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t hend = (uint32_t)(uint16_t)head[b].y << 8;  // b's end heading (target offers)
+      if (k >= deg) {
+        erec[4ull * b + k] = make_uint4(kAdjDstMask, 0u, hend, v);  // (access 0: never relaxed)
+        continue;
       }
+      const uint32_t e = row[v] + k;
+      const uint32_t x = e | ((attr[e] & OTR_ATTR_ACCESS_MASK) << 28) | ((k == 3 && deg > 4) ? kAdjMore : 0u);
+      erec[4ull * b + k] =
+          make_uint4(x, len[e], (uint32_t)turn_degree((int)head[b].y, (int)head[e].x) | hend, v);
+      for (int m = 0; m < OTR_MODES; ++m) erec_t[es * m + 4ull * b + k] = std::min(et[m][e], 0x1FFFFu);
+    }
   }
   // candidate-search view: each grid-cell entry carries its edge's shape range and
   // attributes, 48 B per entry: {edge, shape begin, shape end, attr} + the first four shape points
@@ -330,7 +341,8 @@ int engine_configure(const Config& cfg, std::string* err) {
   g.edge_head = (const short2*)upv(head.data(), sizeof(short2) * head.size());
   g.adj_e = (const uint2*)upv(adje.data(), sizeof(uint2) * adje.size());
   g.erec = (const uint4*)upv(erec.data(), sizeof(uint4) * erec.size());
-  g.erec_stride = (uint32_t)(4ull * h.n_nodes + 4);
+  g.erec_t = (const uint32_t*)upv(erec_t.data(), 4ull * erec_t.size());
+  g.erec_stride = es;
   g.cell_rec = (const uint4*)upv(crec.data(), sizeof(uint4) * crec.size());
   if (!alloc_ok) {
     if (err) *err = "device allocation for the graph failed";

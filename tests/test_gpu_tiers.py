@@ -139,7 +139,8 @@ for g, nt, npnt, sr, sig, seed, fb, fp in [('city', 40, 100, 15, 10.0, 2, 0.0, 0
         assert w[10] > 0, w
     resumed, dumped = int(r.counters[22]), int(r.counters[23])
     if force & 32:  # every first-table search stopped after 2 rounds and resumed at 512 states
-        assert w[10] > 0 and w[9] > 0 and resumed > 0 and dumped >= resumed, (w, resumed, dumped)
+        # (a search counts in its tier only when it completes there: bit 1 fails every 512-state one)
+        assert dumped > 0 and (force & 2 or (w[9] > 0 and resumed > 0 and dumped >= resumed)), (w, resumed, dumped)
     if force & 64:  # and every 512-state search after 4 rounds, resumed at 1024
         assert w[11] > 0 and resumed > 0, (w, resumed, dumped)
     got = _lib.result_to_numpy(r)
