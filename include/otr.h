@@ -184,7 +184,8 @@ typedef struct otr_batch_result {
                                   1 shape segments tested, 2 candidates, 3 settled nodes and
                                   4 relaxed edges (first-tier route launch), 5 search tasks,
                                   6 transition entries, 7 output segments, 8 tile rows,
-                                  9/10 settled/relaxed of the large-table retry, 13 search rounds
+                                  9/10 settled/relaxed of the large-table retry, 11/12 node
+                                  searches resumed from / dumped to HBM (next retry table), 13 search rounds
                                   and 14 table keys (first-tier route launch),
                                   16-21 diagnostic-build search phase cycles, 22/23 edge-state
                                   searches resumed from / dumped to HBM (next table) */

@@ -140,7 +140,9 @@ def build_all(force=False):
     with ThreadPoolExecutor(max_workers=3) as ex:
         futs = [ex.submit(build_otr, force),
                 # test build: every first-tier search goes down the retry tiers (tests/test_gpu_tiers.py)
-                ex.submit(build_otr, force, False, 'tiercheck', ['OTR_FORCE_RETRY']),
+                # (and every node retry tier resumes / dumps: OTR_ND_IN_MIN / OTR_ND_OUT_MIN 0)
+                ex.submit(build_otr, force, False, 'tiercheck', ['OTR_FORCE_RETRY', 'OTR_ND_IN_MIN=0',
+                                                                 'OTR_ND_OUT_MIN=0']),
                 # test build: every search in the global-memory kernel (tests/test_gpu_tiers.py)
                 ex.submit(build_otr, force, False, 'generalcheck', ['OTR_FORCE_GENERAL'])]
         lib = futs[0].result()

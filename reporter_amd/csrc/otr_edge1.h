@@ -422,10 +422,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
     uint32_t kmin = 0, dmin = 0, tmn = 0;  // the smallest pending key / length / time
     int npend = 1, nkeys = 1;
     // a search the previous (smaller) table outgrew goes on from its dump (e1_restore)
-    const int32_t rslot = (a.e1_in != nullptr && search) ? a.task_dump[task] : -1;
+    const int32_t rslot = (a.dump_in != nullptr && search) ? a.task_dump[task] : -1;
     if (search) {
       if (rslot >= 0) {
-        nkeys = e1_restore(L, gr, a.e1_in + (size_t)rslot * a.e1_in_words, a.e1_in_cap, ei, npend, kmin, dmin, tmn,
+        nkeys = e1_restore(L, gr, a.dump_in + (size_t)rslot * a.dump_in_words, a.dump_in_cap, ei, npend, kmin, dmin, tmn,
                            my_settled, my_relaxed);
       } else if (lane == 0) {
         bool isnew = false;
@@ -635,13 +635,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
       // the next table (512, 1024 states, then k_general) resumes the search from its dump
       // when it stopped between two rounds and a dump slot is free, else starts it afresh
       int32_t slot = -1;
-      if (dump && a.e1_out != nullptr) {
+      if (dump && a.dump_out != nullptr) {
         unsigned long long v = 0;
-        if (lane == 0) v = atomicAdd(a.e1_out_ctr, 1ull);
+        if (lane == 0) v = atomicAdd(a.dump_ctr, 1ull);
         v = (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-        if (v < (unsigned long long)a.e1_out_slots) slot = (int32_t)v;
+        if (v < (unsigned long long)a.dump_out_slots) slot = (int32_t)v;
       }
-      if (slot >= 0) e1_dump(L, a.e1_out + (size_t)slot * a.e1_out_words, npend, kmin, dmin, tmn, 0u, 0u);
+      if (slot >= 0) e1_dump(L, a.dump_out + (size_t)slot * a.dump_out_words, npend, kmin, dmin, tmn, 0u, 0u);
       if (counters && slot >= 0 && lane == 0) atomicAdd(&counters[23 * kCShards + cshard()], 1ull);
       if (lane == 0) {
         a.overflow_flag[task] = CAP < 512 ? 6 : (CAP < 1024 ? 7 : 3);

@@ -405,7 +405,7 @@ enum Slot {
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
   S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST, S_HE_PKEY, S_QUEUE, S_PQUEUE,
-  S_E1DUMP0, S_E1DUMP1, S_TASK_DUMP,
+  S_E1DUMP0, S_E1DUMP1, S_TASK_DUMP, S_NDUMP0, S_NDUMP1,
   S_NUM
 };
 
@@ -986,6 +986,20 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     constexpr int kQueueWords = 16 * 8;
     unsigned long long* queues = need<unsigned long long>(S_QUEUE, 16 * kQueueWords);
     HIPCHK(hipMemsetAsync(queues, 0, 8 * 16 * kQueueWords, stream));
+    // retry-tier dumps (search_run NDump, otr_edge1.h): per task, the dump slot its search
+    // left for the next tier; every tier that fails a task writes it (-1: restart), so the
+    // first node tier, which flags every task a retry tier will see, initialises it
+    static const bool nresume = !getenv("OTR_NRESUME") || atoi(getenv("OTR_NRESUME")) != 0;  // A/B knob
+    static const bool eresume = !getenv("OTR_E1RESUME") || atoi(getenv("OTR_E1RESUME")) != 0;  // A/B knob
+    int32_t* task_dump = nullptr;
+    if ((nresume && node_tasks) || (eresume && turns)) {
+      try {
+        task_dump = need<int32_t>(S_TASK_DUMP, NT);
+      } catch (const DeviceOom&) {
+        (void)hipGetLastError();  // (no dumps: outgrown searches restart, same results)
+      }
+    }
+    ra.task_dump = task_dump;
     tb(OTR_STAGE_ROUTE);
     if (node_tasks) {
       // one unit (G searches) per block, in launches of at most 2^25 blocks: a dispatch's
@@ -1028,6 +1042,32 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // the first tier's flagged tasks, once; every later collect scans only them
     k_collect_flagged<<<grid_for(NT, 1024), 1024, 0, stream>>>(NT, task_ovf, flagged, cnt + 24);
     constexpr unsigned kCollectGrid = 512;
+    // node dump slots: tier t writes buffer t % 2 and tier t + 1 resumes from it; slots for a
+    // quarter of the tasks, at most OTR_NDUMP_GB (4) GB per buffer (C4: 4 % of the 1024-slot
+    // searches outgrow it, 10 KB each); beyond them, or without the memory, searches restart
+    unsigned long long* ndump[2] = {nullptr, nullptr};
+    uint32_t nslots[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    // (tables compiled with the resume / dump code, otr_kernels.h OTR_ND_IN_MIN / OTR_ND_OUT_MIN)
+    auto nd_in = [&](int t) { return t > 0 && t < ntier && tiers[t] / 10 >= OTR_ND_IN_MIN; };
+    auto nd_out = [&](int t) { return t + 1 < ntier && tiers[t] / 10 >= OTR_ND_OUT_MIN && nd_in(t + 1); };
+    if (nresume && node_tasks && task_dump && ntier > 1) {
+      static const double gb = getenv("OTR_NDUMP_GB") ? atof(getenv("OTR_NDUMP_GB")) : 4.0;
+      const int64_t cap_bytes = (int64_t)(gb * (double)(1ll << 30));
+      size_t words[2] = {0, 0};
+      for (int t = 0; t + 1 < ntier && t < 8; ++t) {
+        if (!nd_out(t)) continue;
+        const uint32_t w = nd_words(tiers[t] / 10);
+        nslots[t] = (uint32_t)std::min<int64_t>(std::max<int64_t>(NT / 4, 1024), cap_bytes / (8 * (int64_t)w));
+        words[t & 1] = std::max<size_t>(words[t & 1], (size_t)nslots[t] * w);
+      }
+      try {
+        for (int q = 0; q < 2; ++q)
+          if (words[q]) ndump[q] = need<unsigned long long>(q == 0 ? S_NDUMP0 : S_NDUMP1, words[q]);
+      } catch (const DeviceOom&) {
+        (void)hipGetLastError();
+      }
+      if ((words[0] && !ndump[0]) || (words[1] && !ndump[1])) ndump[0] = ndump[1] = nullptr;
+    }
     for (int tier = 0; tier < (node_tasks ? ntier : 0); ++tier) {  // (no node task: no node tier)
       unsigned long long* c = cnt + tier;
       k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf,
@@ -1036,6 +1076,14 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       rb.task_list = list;
       rb.list_count = c;
       rb.queue = queues + tier * kQueueWords;
+      const bool din = nd_in(tier) && nd_out(tier - 1) && ndump[(tier + 1) & 1] != nullptr;
+      const bool dout = nd_out(tier) && ndump[tier & 1] != nullptr;
+      rb.dump_in = din ? ndump[(tier + 1) & 1] : nullptr;
+      rb.dump_in_words = din ? nd_words(tiers[tier - 1] / 10) : 0u;
+      rb.dump_out = dout ? ndump[tier & 1] : nullptr;
+      rb.dump_ctr = queues + 15 * kQueueWords + 16 * tier;  // (queue 15: zeroed above; one line per tier)
+      rb.dump_out_words = dout ? nd_words(tiers[tier] / 10) : 0u;
+      rb.dump_out_slots = dout ? nslots[tier] : 0u;
       unsigned long long* rcn = rwork ? d_counters + (2 + tier) * bank : nullptr;
       out->route_tier_code[1 + tier] = tiers[tier];
       if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier)], stream);
@@ -1080,16 +1128,13 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       // over; slots for 1/16 of the tasks (C2, deployed: 4.4 % outgrow the first table),
       // at most 4 GB / 1 GB — searches beyond them, or when the memory is not there,
       // restart in the next table (same results)
-      static const bool resume = !getenv("OTR_E1RESUME") || atoi(getenv("OTR_E1RESUME")) != 0;  // A/B knob
       unsigned long long* dump[2] = {nullptr, nullptr};
       uint32_t dslots[2] = {0u, 0u};
-      int32_t* task_dump = nullptr;
       const uint32_t dwords[2] = {e1_dump_words(OTR_E1CAP), e1_dump_words(512)};
-      if (resume) {
+      if (eresume && task_dump) {
         const int64_t cap_bytes[2] = {4ll << 30, 1ll << 30};
         const int64_t want[2] = {std::max<int64_t>(NT / 16, 4096), std::max<int64_t>(NT / 64, 1024)};
         try {
-          task_dump = need<int32_t>(S_TASK_DUMP, NT);
           for (int q = 0; q < 2; ++q) {
             const int64_t n = std::min<int64_t>(want[q], cap_bytes[q] / (8 * (int64_t)dwords[q]));
             dump[q] = need<unsigned long long>(q == 0 ? S_E1DUMP0 : S_E1DUMP1, (size_t)n * dwords[q]);
@@ -1097,7 +1142,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
           }
         } catch (const DeviceOom&) {
           (void)hipGetLastError();  // (no dumps beyond what was allocated: those searches restart)
-          if (!task_dump) dump[0] = dump[1] = nullptr;
           if (!dump[0]) dump[1] = nullptr;
         }
       }
@@ -1110,13 +1154,13 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         rb.task_list = list;
         rb.list_count = c;
         rb.queue = queues + (9 + et) * kQueueWords;
-        rb.e1_in = et > 0 ? dump[et - 1] : nullptr;
-        rb.e1_in_words = et > 0 ? dwords[et - 1] : 0u;
-        rb.e1_in_cap = et == 1 ? OTR_E1CAP : 512;
-        rb.e1_out = et < 2 ? dump[et] : nullptr;
-        rb.e1_out_ctr = queues + (13 + et) * kQueueWords;  // (queues 13, 14: zeroed above)
-        rb.e1_out_words = et < 2 ? dwords[et] : 0u;
-        rb.e1_out_slots = et < 2 ? dslots[et] : 0u;
+        rb.dump_in = et > 0 ? dump[et - 1] : nullptr;
+        rb.dump_in_words = et > 0 ? dwords[et - 1] : 0u;
+        rb.dump_in_cap = et == 1 ? OTR_E1CAP : 512;
+        rb.dump_out = et < 2 ? dump[et] : nullptr;
+        rb.dump_ctr = queues + (13 + et) * kQueueWords;  // (queues 13, 14: zeroed above)
+        rb.dump_out_words = et < 2 ? dwords[et] : 0u;
+        rb.dump_out_slots = et < 2 ? dslots[et] : 0u;
         rb.task_dump = task_dump;
         unsigned long long* rcn = rwork ? d_counters + (et == 0 ? 10 : (et == 1 ? 1 : 11)) * bank : nullptr;
         if (timing) (void)hipEventRecord(ev[24 + 2 * slot], stream);
@@ -1513,6 +1557,12 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   // (the first two edge tiers), with OTR_BATCH_ROUTE_WORK
   out->counters[22] = ctr(1, 22) + ctr(11, 22);
   out->counters[23] = ctr(10, 23) + ctr(1, 23);
+  // node searches resumed from / dumped to a retry tier's dump (the node retry tiers, banks 2..6)
+  out->counters[11] = out->counters[12] = 0;
+  for (int b = 2; b < 7; ++b) {
+    out->counters[11] += ctr(b, 11);
+    out->counters[12] += ctr(b, 12);
+  }
   if (!(in->flags & OTR_BATCH_TILE_ROWS)) out->n_rows = (int64_t)out->counters[8];
   else out->counters[8] = (uint64_t)out->n_rows;  // K9 counted them (K8 may not have run)
   out->d_hist = ha.hist;

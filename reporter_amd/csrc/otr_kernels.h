@@ -771,18 +771,48 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Pac
   return (imp && !(was & kInq)) ? sl : -1;  // newly pending: the caller appends it
 }
 
+// Resuming an outgrown node search in the next retry table (as otr_edge1.h does for the
+// edge-state tiers): a search that passes its table's load limit stops between two rounds
+// (no relaxation lost) and its table goes to a dump slot in HBM — every key with its label
+// and minin code (settled nodes too, whose final labels keep rejecting later offers; the
+// pending ones carry kInq), and the round's kmin; the next table re-inserts the keys,
+// rebuilds the pending list and goes on with the next round: the same rounds as one big
+// table, so the same labels.  32-bit labels only (the retry tiers).  Slot (u64 words):
+// [0] entries n, [1] kmin, [2, 2 + n) label | key << 32, then the n minin codes (u16).
+struct NDump {
+  const unsigned long long* in;  // the dump this group's search resumes (null: a fresh search)
+  unsigned long long* base;      // this tier's dump slots (null: an outgrown search restarts)
+  unsigned long long* ctr;       // slots taken (zeroed per batch)
+  uint32_t words, slots;
+#ifdef OTR_FORCE_RETRY
+  int stop_rounds;  // test build: a search with dump slots stops after this many rounds (0: off)
+#endif
+};
+__host__ __device__ constexpr uint32_t nd_words(int cap) { return 2u + (uint32_t)cap + ((uint32_t)cap + 3u) / 4u; }
+// which retry tables carry the resume code (compile time: the code costs the hot tiers ~2 %
+// even unused): tables of at least OTR_ND_IN_MIN slots resume, of at least OTR_ND_OUT_MIN
+// slots dump (C4: the 1024-slot tier's 4 % outgrowers; the smaller tiers' overflows are few)
+#ifndef OTR_ND_IN_MIN
+#define OTR_ND_IN_MIN 2048
+#endif
+#ifndef OTR_ND_OUT_MIN
+#define OTR_ND_OUT_MIN 1024
+#endif
+
 // G searches per wave, one per lane group, each in its own table Ls[g]: search g is
 // rooted at `start` (label 0); lanes gl < n_tgt of the group hold a target node tnode,
 // its minin gapT (in_gap units: mm, >= 1) and partial length tpart (mm).  active = false:
 // the group idles.  K packs the labels (route time tracked when K.sh > 0, from adj_t /
 // edge_t: the mode's times).  pd / pt prune the relaxations (relative length and time
 // bounds, relax_one); pd also decides when a target is unreachable.  Returns false (per
-// lane, group-uniform) on an LDS-table overflow.
-template <int CAP, int LM, int G = 1>
+// lane, group-uniform) on an LDS-table overflow.  nd (retry tiers): the group's dump to
+// resume, and this tier's dump slots; *dslot: the slot an outgrown search went to (-1: none).
+template <int CAP, int LM, int G = 1, bool RIN = false, bool ROUT = false>
 __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack& K, uint32_t mode_bit, bool active,
                            uint32_t start, uint32_t pd, uint32_t pt, uint32_t tnode, uint32_t tpart, uint32_t gapT,
                            int n_tgt, unsigned long long* settled, unsigned long long* relaxed,
-                           unsigned long long* rounds, unsigned long long* stamps = nullptr, uint32_t* sink = nullptr) {
+                           unsigned long long* rounds, unsigned long long* stamps = nullptr, uint32_t* sink = nullptr,
+                           const NDump* nd = nullptr, int* dslot = nullptr) {
   using Gr = Grp<G>;
   // load-factor limit (probe chains stay short): 7/8 (the exact searches run to the
   // bounds, so a fuller first-tier table keeps more of them out of the retry tiers: C2
@@ -795,7 +825,45 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
   constexpr int WCAP = SearchLds<CAP, LM>::WCAP;
   const bool timed = K.sh != 0u;  // group-uniform
   const uint32_t* adjt = g.adj_t + (size_t)__builtin_ctz(mode_bit) * g.adj_t_stride;
-  if (active && gl == 0) {
+  uint32_t kmin = 0;           // the smallest pending length (0xFFFFFFFF: nothing pending)
+  int npend = active ? 1 : 0;  // pending-list length (group-uniform register)
+  // resume: the outgrown search's table, keys re-inserted (distinct: every CAS lands)
+  const bool resume = RIN && LM == 0 && active && nd->in != nullptr;  // (group-uniform)
+  const int nres = resume ? (int)nd->in[0] : 0;
+  const int nrx = RIN ? Gr::umax(nres) : 0;
+  if (RIN && nrx > 0) {
+    const unsigned long long* D = nd->in;
+    const uint16_t* M = (const uint16_t*)(D + 2 + nres);
+    int np = 0;
+    for (int base = 0; base < nrx; base += Gr::GL) {
+      const int k = base + gl;
+      bool pend = false;
+      int sl = 0;
+      if (k < nres) {
+        const unsigned long long e = D[2 + k];
+        const uint32_t key = (uint32_t)(e >> 32), node = key & kNodeMask;
+        uint32_t h = hslot<CAP>(node);
+        for (int probe = 0; probe < CAP; ++probe) {
+          if (atomicCAS(&L.key[h], kEmpty, node) == kEmpty) break;
+          h = h + 1 == (uint32_t)CAP ? 0u : h + 1;
+        }
+        sl = (int)h;
+        L.key[sl] = key;
+        L.lab[sl] = (typename LabelT<LM>::T)(uint32_t)e;
+        L.mi[sl] = M[k];
+        pend = (key & kInq) != 0u;
+      }
+      const unsigned long long mp = __ballot(pend);
+      if (pend) L.pend[np + Gr::prefix(mp)] = (Idx)sl;
+      np += Gr::count(mp);
+    }
+    if (resume) {
+      npend = np;
+      kmin = (uint32_t)D[1];
+      if (gl == 0) L.n_keys = nres;
+    }
+  }
+  if (!resume && active && gl == 0) {
     bool isnew;
     const int sl = lds_insert(L, start, &isnew);
     L.mi[sl] = 0;
@@ -814,9 +882,10 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
   __syncthreads();
   uint32_t my_settled = 0, my_relaxed = 0, my_rounds = 0;
   unsigned long long cyc[4] = {0, 0, 0, 0};
-  uint32_t kmin = 0;  // the smallest pending length (0xFFFFFFFF: nothing pending)
-  bool done = !active;
-  int npend = active ? 1 : 0;  // pending-list length (group-uniform register)
+  bool done = !active, grew = false;  // grew: stopped between rounds at the load limit
+#ifdef OTR_FORCE_RETRY
+  int force_round = 0;
+#endif
   int nkeys = 0;               // keys the main relax loop added (group-uniform; L.n_keys has the rest)
   for (;;) {
     OTR_STAMP(t0);
@@ -941,13 +1010,59 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
     __syncthreads();
     OTR_STAMP(t4);
     cyc[3] += t4 - t3;
-    kmin = Gr::min_u32(knext);
+    // a finished group's kmin stays that of its last round (G = 2: the other group may run
+    // on; an outgrown search's dump needs the kmin it stopped with)
+    const uint32_t km = Gr::min_u32(knext);
+    if (!done) kmin = km;
     const int keys = L.n_keys + nkeys;
-    if (!done && (L.overflow || keys > kMaxKeys)) done = true;
+    if (!done && (L.overflow || keys > kMaxKeys)) {
+      grew = !L.overflow && keys > kMaxKeys;
+      done = true;
+    }
+#ifdef OTR_FORCE_RETRY
+    ++force_round;
+    if (ROUT && !done && nd->base != nullptr && nd->stop_rounds > 0 && force_round >= nd->stop_rounds &&
+        !L.overflow) {
+      grew = true;
+      done = true;
+    }
+#endif
     __syncthreads();
-    if (done && active && gl == 0 && keys > kMaxKeys) L.overflow = 1;
+    if (done && active && gl == 0 && (keys > kMaxKeys || grew)) L.overflow = 1;
   }
   if (gl == 0) L.n_keys += nkeys;  // the table's key count, for the caller
+  if (ROUT) *dslot = -1;
+  if (ROUT && LM == 0 && __ballot(grew && active && nd->base != nullptr) != 0ull) {
+    // dump the outgrown tables to claimed slots: keys in slot order, compacted by ballot
+    int v = 0;
+    if (grew && active && nd->base != nullptr && gl == 0) v = (int)atomicAdd(nd->ctr, 1ull);
+    v = __shfl(v, 0, Gr::GL);  // (the group's lane 0)
+    const bool dump = grew && active && nd->base != nullptr && (uint32_t)v < nd->slots;  // (group-uniform)
+    unsigned long long* D = dump ? nd->base + (size_t)v * nd->words : nullptr;
+    int n = 0;
+    for (int base = 0; base < CAP; base += Gr::GL) {
+      const int k = base + gl;
+      const uint32_t key = (dump && k < CAP) ? L.key[k] : kEmpty;
+      const bool has = key != kEmpty;
+      const unsigned long long m = __ballot(has);
+      if (has) D[2 + n + Gr::prefix(m)] = (unsigned long long)(uint32_t)L.lab[k] | ((unsigned long long)key << 32);
+      n += Gr::count(m);
+    }
+    uint16_t* M = dump ? (uint16_t*)(D + 2 + n) : nullptr;
+    int q = 0;
+    for (int base = 0; base < CAP; base += Gr::GL) {
+      const int k = base + gl;
+      const bool has = dump && k < CAP && L.key[k] != kEmpty;
+      const unsigned long long m = __ballot(has);
+      if (has) M[q + Gr::prefix(m)] = L.mi[k];
+      q += Gr::count(m);
+    }
+    if (dump && gl == 0) {
+      D[0] = (unsigned long long)(uint32_t)n;
+      D[1] = kmin;
+    }
+    *dslot = dump ? v : -1;
+  }
 #ifdef OTR_STAMPS
   if (stamps && threadIdx.x == 0)
     for (int q = 0; q < 4; ++q) atomicAdd(&stamps[q * kCShards + cshard()], cyc[q]);
@@ -1075,15 +1190,17 @@ struct RouteArgs {
                               // every OTR_E1CAP (360) / 512 / 1024-state edge-state route search (the
                               // next tier takes it), bits 3 / 4 every 384 / 2048-state winner path;
                               // bits 5 / 6 stop every OTR_E1CAP / 512-state search after 2 / 4 rounds
-                              // and resume it in the next table (otr_edge1.h e1_dump / e1_restore)
-  // edge-state tiers: a search that outgrows its table is dumped between two rounds and
-  // resumed in the next table (otr_edge1.h)
-  const unsigned long long* e1_in;  // the previous tier's dumps (null: every search starts afresh)
-  uint32_t e1_in_words, e1_in_cap;  // u64 words per dump slot, the table size that wrote them
-  unsigned long long* e1_out;       // this tier's dump slots (null: outgrown searches restart)
-  unsigned long long* e1_out_ctr;   // slots taken (device counter, zeroed per batch)
-  uint32_t e1_out_words, e1_out_slots;
-  int32_t* task_dump;               // per task: its slot in the next tier's input, -1: restart
+                              // and resume it in the next table (otr_edge1.h e1_dump / e1_restore);
+                              // bit 7 stops every node retry-tier search that has dump slots after 2
+                              // rounds (search_run, NDump): resumed tier after tier to the last
+  // retry tiers (node and edge-state): a search that outgrows its table is dumped between
+  // two rounds and resumed in the next table (search_run NDump, otr_edge1.h e1_dump)
+  const unsigned long long* dump_in;  // the previous tier's dumps (null: every search starts afresh)
+  uint32_t dump_in_words, dump_in_cap;  // u64 words per dump slot, the table size that wrote them
+  unsigned long long* dump_out;       // this tier's dump slots (null: outgrown searches restart)
+  unsigned long long* dump_ctr;       // slots taken (device counter, zeroed per batch)
+  uint32_t dump_out_words, dump_out_slots;
+  int32_t* task_dump;                 // per task: its slot in the next tier's input, -1: restart
 };
 
 // k_tasks' inputs and outputs
@@ -1303,9 +1420,29 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   }
   unsigned long long settled = 0, relaxed = 0, rounds = 0;
   OTR_STAMP(ts_set);
+  // a retry tier resumes the search the previous tier outgrew (its dump slot, task_dump)
+  // and dumps what outgrows this table for the next one (NDump)
+  NDump nd{};
+  int dslot = -1;
+  constexpr bool kIn = LIST && !WIDE && CAP >= OTR_ND_IN_MIN, kOut = LIST && !WIDE && CAP >= OTR_ND_OUT_MIN;
+  constexpr bool kDumps = kIn || kOut;
+  if (kIn) {
+    const int32_t rs = (a.dump_in != nullptr && search) ? a.task_dump[task] : -1;
+    nd.in = rs >= 0 ? a.dump_in + (size_t)rs * a.dump_in_words : nullptr;
+  }
+  if (kOut) {
+    nd.base = a.dump_out;
+    nd.ctr = a.dump_ctr;
+    nd.words = a.dump_out_words;
+    nd.slots = a.dump_out_slots;
+#ifdef OTR_FORCE_RETRY
+    nd.stop_rounds = (a.force_edge >> 7) & 1 ? 2 + Gr::g() : 0;  // (G = 2: the groups stop in different rounds)
+#endif
+  }
   search_init<CAP, LM, G>(Ls);
-  bool ok = search_run<CAP, LM, G>(Ls, gr, K, mode_bit, search, root, pd, pt, tnode, tpart, gapT, Kb, &settled,
-                                   &relaxed, &rounds, counters ? counters + 16 * kCShards : nullptr, sink) &&
+  bool ok = search_run<CAP, LM, G, kIn, kOut>(Ls, gr, K, mode_bit, search, root, pd, pt, tnode, tpart, gapT, Kb, &settled,
+                                   &relaxed, &rounds, counters ? counters + 16 * kCShards : nullptr, sink,
+                                   kDumps ? &nd : nullptr, kDumps ? &dslot : nullptr) &&
             fits;
 #ifdef OTR_FORCE_RETRY
   if (G == 2 && !LIST) ok = false;  // test build: every first-tier task takes the retry tiers
@@ -1400,6 +1537,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     // (turn-mode tasks carry flag 5 from k_tasks: the edge-state tiers take them)
     if (!turn) a.overflow_flag[task] = general ? 3 : (start_tier >= 0 ? 16 + start_tier : 1);
 #endif
+    if (!WIDE && !turn && a.task_dump != nullptr) a.task_dump[task] = dslot;  // (-1: the next tier restarts it)
   }
 #ifdef OTR_STAMPS
   if (G == 2 && counters && threadIdx.x == 0) {  // task setup and transition rows, wave cycles
@@ -1415,11 +1553,15 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     relaxed = wave_sum_u32((uint32_t)relaxed);
     rounds = wave_sum_u32((uint32_t)rounds);
     const int nk = have && search ? L.n_keys : 0;
-    unsigned long long kk = 0, ntrw = 0, nsearch = 0;
+    unsigned long long kk = 0, ntrw = 0, nsearch = 0, nres = 0, ndmp = 0;
+    const int rd = (kDumps && nd.in != nullptr ? 1 : 0) | (dslot >= 0 ? 2 : 0);
     for (int q = 0; q < G; ++q) {
       kk += (unsigned long long)__builtin_amdgcn_readlane(nk, q * Gr::GL);
       ntrw += (unsigned long long)__builtin_amdgcn_readlane(ntr, q * Gr::GL);
       nsearch += (unsigned long long)__builtin_amdgcn_readlane((int)(have && search), q * Gr::GL);
+      const int rdq = __builtin_amdgcn_readlane(rd, q * Gr::GL);
+      nres += rdq & 1;
+      ndmp += rdq >> 1;
     }
     if (threadIdx.x == 0) {
       const int sh = cshard();
@@ -1429,6 +1571,8 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
       atomicAdd(&counters[6 * kCShards + sh], nsearch);
       atomicAdd(&counters[13 * kCShards + sh], rounds);
       atomicAdd(&counters[14 * kCShards + sh], kk);
+      if (nres) atomicAdd(&counters[11 * kCShards + sh], nres);  // resumed from a dump
+      if (ndmp) atomicAdd(&counters[12 * kCShards + sh], ndmp);  // dumped for the next tier
     }
   }
 }

@@ -4,7 +4,10 @@ retry kernels, and must still match the oracle field by field.  Parametrised ove
 the retry-tier list (OTR_TIERS): the default 256 → 448x2 → 1024 → 2048 → 4096 chain, a chain
 that starts with two-searches-per-wave 384-slot tables, and direct 1024/4096; with the size
 estimate scaled up (OTR_EST_K=1000) every search starts in the last retry tier, with it off
-(OTR_EST_K=0) every search overflows into the first retry tier.
+(OTR_EST_K=0) every search overflows into the first retry tier; with OTR_FORCE_EDGE=128 every
+retry-tier search that has dump slots stops after 2 rounds (3 in a table's second lane group)
+and the next tier resumes it from its dump in HBM (search_run NDump), tier after tier, so the
+last tier finishes them.
 The edge-state tiers (turn costs: the deployed per-mode defaults, a mode mix) the same way:
 OTR_FORCE_EDGE fails every search of the chosen tiers, so the next one does all the work —
 the 512- and 1024-state lean tiers, k_general, and for winner paths the 2048-state table
@@ -39,6 +42,8 @@ for g, nt, npnt, sr, sig, seed, acc, over in [('city', 40, 100, 15, 10.0, 2, Non
     assert r.status == 0, r.status
     c = [int(r.counters[k]) for k in range(24)]
     assert c[9] > 0, c  # the retry tiers settled nodes (and wrote every transition row)
+    if %r:  # forced stops: dumped in one tier, resumed in the next
+        assert c[12] > 0 and c[11] > 0 and c[12] >= c[11], c
     from reporter_amd import _lib
     got = _lib.result_to_numpy(r)
     want = po.match_batch(po.Graph(path), tr, po.params(**{k: float(v) for k, v in over.items()}), threads=8)
@@ -48,9 +53,10 @@ print('tiers ok')
 '''
 
 
-@pytest.mark.parametrize('tiers,est', [(None, None), ('384x2,512', None), ('512x2,2048', None), ('1024', '0'),
-                                       (None, '1000')])
-def test_retry_tiers_equal_first_tier(graph_dir, tiers, est):
+@pytest.mark.parametrize('tiers,est,stop', [(None, None, False), ('384x2,512', None, False),
+                                            ('512x2,2048', None, False), ('1024', '0', False),
+                                            (None, '1000', False), (None, None, True), ('384x2,512', '0', True)])
+def test_retry_tiers_equal_first_tier(graph_dir, tiers, est, stop):
     lib = os.path.join(ROOT, 'reporter_amd', 'libotr_tiercheck.so')
     assert os.path.exists(lib), 'build first: python -m reporter_amd.build'
     env = dict(os.environ, OTR_LIB=lib)
@@ -60,8 +66,10 @@ def test_retry_tiers_equal_first_tier(graph_dir, tiers, est):
         env['OTR_TIERS'] = tiers
     if est is not None:
         env['OTR_EST_K'] = est
-    p = subprocess.run([sys.executable, '-c', CHILD % (ROOT, graph_dir)], env=env, capture_output=True, text=True,
-                       timeout=240)
+    if stop:
+        env['OTR_FORCE_EDGE'] = '128'
+    p = subprocess.run([sys.executable, '-c', CHILD % (ROOT, graph_dir, stop)], env=env, capture_output=True,
+                       text=True, timeout=240)
     assert p.returncode == 0 and 'tiers ok' in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
 
 
