@@ -405,7 +405,7 @@ enum Slot {
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
   S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST, S_HE_PKEY, S_QUEUE, S_PQUEUE,
-  S_E1DUMP0, S_E1DUMP1, S_TASK_DUMP, S_NDUMP0, S_NDUMP1,
+  S_E1DUMP0, S_E1DUMP1, S_TASK_DUMP, S_NDUMP0, S_NDUMP1, S_SORT_LIST, S_SORT_HIST,
   S_NUM
 };
 
@@ -530,6 +530,67 @@ __global__ void k_collect_tier_from(const int64_t* cand, const unsigned long lon
     if (sel) flag[task] = 0;
     block_append(sel, task, list, count);
   }
+}
+
+// Spatial order of a retry list (the edge-state tier's 15.7M tasks at C2, deployed): a
+// counting sort by the root's id >> shift (4,096 buckets; graph ids are spatially ordered,
+// so a bucket is a small patch of the map).  The list tiers split their list into 8
+// contiguous ranges, one per XCD (XcdQueue): sorted, each XCD's waves search one band of
+// the map and its 4 MB L2 holds that band's records instead of the whole graph's.  Pass 1
+// counts (LDS histogram per block, then one global add per non-empty bucket), pass 2 scans
+// the 4,096 counts, pass 3 places each task (local rank by LDS atomic + the block's range
+// reserved per bucket).  Order inside a bucket is arbitrary: tasks are independent.
+constexpr int kSortBuckets = 4096;
+__global__ __launch_bounds__(1024) void k_sort_hist(const int64_t* list, const unsigned long long* n_in,
+                                                    const uint4* rec, int shift, uint32_t* hist) {
+  __shared__ uint32_t h[kSortBuckets];
+  const int64_t n = (int64_t)*n_in, i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((int64_t)blockIdx.x * blockDim.x >= n) return;  // (block-uniform)
+  for (int b = threadIdx.x; b < kSortBuckets; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  if (i < n) atomicAdd(&h[min(rec[3 * list[i]].z >> shift, (uint32_t)kSortBuckets - 1u)], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < kSortBuckets; b += blockDim.x)
+    if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+__global__ __launch_bounds__(1024) void k_sort_scan(uint32_t* hist) {  // one block: exclusive scan in place
+  __shared__ uint32_t part[1024];
+  constexpr int per = kSortBuckets / 1024;
+  uint32_t v[per], t = 0;
+  for (int q = 0; q < per; ++q) t += (v[q] = hist[threadIdx.x * per + q]);
+  part[threadIdx.x] = t;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan of the block sums
+    const uint32_t x = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint32_t base = part[threadIdx.x] - t;
+  for (int q = 0; q < per; ++q) {
+    hist[threadIdx.x * per + q] = base;
+    base += v[q];
+  }
+}
+__global__ __launch_bounds__(1024) void k_sort_place(const int64_t* list, const unsigned long long* n_in,
+                                                     const uint4* rec, int shift, uint32_t* cursor, int64_t* out) {
+  __shared__ uint32_t h[kSortBuckets];
+  const int64_t n = (int64_t)*n_in, i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((int64_t)blockIdx.x * blockDim.x >= n) return;
+  for (int b = threadIdx.x; b < kSortBuckets; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  int64_t task = 0;
+  uint32_t key = 0, r = 0;
+  if (i < n) {
+    task = list[i];
+    key = min(rec[3 * task].z >> shift, (uint32_t)kSortBuckets - 1u);
+    r = atomicAdd(&h[key], 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kSortBuckets; b += blockDim.x)
+    if (h[b]) h[b] = atomicAdd(&cursor[b], h[b]);  // this block's range of bucket b
+  __syncthreads();
+  if (i < n) out[h[key] + r] = task;
 }
 
 // the same over a device-counted list (steps of the path stage): entries list_in[0..*n_in)
@@ -1152,6 +1213,29 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         k_collect_tier_from<<<kCollectGrid, 1024, 0, stream>>>(flagged, cnt + 24, task_ovf, 0x20u << et, list, c);
         RouteArgs rb = ra;
         rb.task_list = list;
+        // the first edge tier's list in spatial order (k_sort_*: one band of the map per XCD)
+        static const bool esort = !getenv("OTR_SORT") || atoi(getenv("OTR_SORT")) != 0;  // A/B knob
+        int64_t* list2 = nullptr;
+        uint32_t* hist = nullptr;
+        if (et == 0 && esort && NT >= 65536) {
+          try {
+            list2 = need<int64_t>(S_SORT_LIST, NT);
+            hist = need<uint32_t>(S_SORT_HIST, kSortBuckets);
+          } catch (const DeviceOom&) {
+            (void)hipGetLastError();  // (no memory for the copy: the list stays in task order)
+            list2 = nullptr;
+          }
+        }
+        if (list2 && hist) {
+          int bits = 0;
+          while (bits < 32 && (g.n_edges >> bits) > 0u) ++bits;
+          const int shift = bits > 12 ? bits - 12 : 0;
+          HIPCHK(hipMemsetAsync(hist, 0, 4 * kSortBuckets, stream));
+          k_sort_hist<<<grid_for(NT, 1024), 1024, 0, stream>>>(list, c, task_rec, shift, hist);
+          k_sort_scan<<<1, 1024, 0, stream>>>(hist);
+          k_sort_place<<<grid_for(NT, 1024), 1024, 0, stream>>>(list, c, task_rec, shift, hist, list2);
+          rb.task_list = list2;
+        }
         rb.list_count = c;
         rb.queue = queues + (9 + et) * kQueueWords;
         rb.dump_in = et > 0 ? dump[et - 1] : nullptr;
