@@ -369,7 +369,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
     const double pi = a.cand_p[sp * OTR_KMAX + i];
     const uint32_t d0 = a.cprep[sp * OTR_KMAX + i].w;
     const uint32_t t0 = timed ? a.cprep_t[sp * OTR_KMAX + i].y : 0u;
-    uint32_t ej = 0, tv = kEmpty, tpart = 0, tpt = 0;
+    uint32_t ej = 0, tv = kEmpty, tpart = 0, tpt = 0, thb = 0;
     double pj = 0;
     bool needed = false;
     if (lane < Kb) {
@@ -377,6 +377,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
       pj = a.cand_p[s * OTR_KMAX + lane];
       const uint4 cq = a.cprep[s * OTR_KMAX + lane];
       tpart = cq.x;
+      thb = cq.z;  // (turn modes: the begin heading of ej, k_prep)
       tpt = timed ? a.cprep_t[s * OTR_KMAX + lane].x : 0u;
       needed = !(ej == ei && pj >= pi);
       if (needed) tv = cq.y;
@@ -401,7 +402,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
     if (tgt) {
       L.tpart[lane] = tpart;
       L.tpt[lane] = tpt;
-      L.thb[lane] = (uint16_t)gr.edge_head[ej].x;
+      L.thb[lane] = (uint16_t)thb;
       uint32_t h = tm_slot(tv);
 #pragma unroll 1
       for (int probe = 0; probe < TM; ++probe) {

@@ -1077,7 +1077,8 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
 // ------------------------------------------------------------------------------
 // K2b: per-state search inputs, computed once per state instead of once per search
 // task (a step has ~9 tasks): per candidate j {entry part mm, source node, minin(source
-// node) (the IN criterion's gap of a target), exit part mm}.
+// node) (the IN criterion's gap of a target; turn modes: the begin heading of the edge,
+// which the edge-state search's target turn needs), exit part mm}.
 // ------------------------------------------------------------------------------
 struct PrepArgs {
   int64_t n_states;
@@ -1088,7 +1089,7 @@ struct PrepArgs {
   const double* cand_p;
   const int32_t* state_trace;
   const uint8_t* mode;
-  uint4* cprep;   // [S][OTR_KMAX]: {part(p), src(e), minin(src(e)), part(1 - p)}
+  uint4* cprep;   // [S][OTR_KMAX]: {part(p), src(e), minin(src(e)) | turn modes: heading(e), part(1 - p)}
   uint2* cprep_t; // [S][OTR_KMAX]: {part_t(p), part_t(1 - p)}: the same parts of the edge's route time
   uint2* clen;    // [S][OTR_KMAX]: {len_mm(e), route time(e)}: a same-edge transition's whole-edge terms
   int32_t* nroot; // [S]: the search tasks of the step leaving the state (k_tasks' grouping)
@@ -1113,8 +1114,8 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
     const double p = a.cand_p[s * OTR_KMAX + lane];
     const uint32_t len = g.len_mm[e];
     const uint32_t tn = g.edge_src[e];
-    a.cprep[s * OTR_KMAX + lane] =
-        make_uint4((uint32_t)part_mm(p, len), tn, g.node_minin[tn], (uint32_t)part_mm(1.0 - p, len));
+    const uint32_t z = turn ? (uint32_t)(uint16_t)g.edge_head[e].x : g.node_minin[tn];
+    a.cprep[s * OTR_KMAX + lane] = make_uint4((uint32_t)part_mm(p, len), tn, z, (uint32_t)part_mm(1.0 - p, len));
     const uint32_t et = g.et(md)[e];
     a.cprep_t[s * OTR_KMAX + lane] = make_uint2((uint32_t)part_mm(p, et), (uint32_t)part_mm(1.0 - p, et));
     a.clen[s * OTR_KMAX + lane] = make_uint2(len, et);
@@ -1201,6 +1202,7 @@ struct RouteArgs {
   unsigned long long* dump_ctr;       // slots taken (device counter, zeroed per batch)
   uint32_t dump_out_words, dump_out_slots;
   int32_t* task_dump;                 // per task: its slot in the next tier's input, -1: restart
+  const uint4* list_rec;              // (optional) per list entry w: {task, 0}, rec[3 task ..] (k_sort_place)
 };
 
 // k_tasks' inputs and outputs
