@@ -405,7 +405,7 @@ enum Slot {
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
   S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST, S_HE_PKEY, S_QUEUE, S_PQUEUE,
-  S_E1DUMP0, S_E1DUMP1, S_TASK_DUMP, S_NDUMP0, S_NDUMP1, S_SORT_LIST, S_SORT_HIST, S_SORT_REC,
+  S_E1DUMP0, S_E1DUMP1, S_TASK_DUMP, S_NDUMP0, S_NDUMP1, S_SORT_LIST, S_SORT_HIST,
   S_NUM
 };
 
@@ -572,12 +572,8 @@ __global__ __launch_bounds__(1024) void k_sort_scan(uint32_t* hist) {  // one bl
     base += v[q];
   }
 }
-// out_rec (optional): beside each placed task, its id and its 3 task-record words
-// ({task lo, task hi, 0, 0}, rec[3 task .. 3 task + 2]), so the search loads one 64-B entry
-// instead of the list entry and then the record it points to
 __global__ __launch_bounds__(1024) void k_sort_place(const int64_t* list, const unsigned long long* n_in,
-                                                     const uint4* rec, int shift, uint32_t* cursor, int64_t* out,
-                                                     uint4* out_rec) {
+                                                     const uint4* rec, int shift, uint32_t* cursor, int64_t* out) {
   __shared__ uint32_t h[kSortBuckets];
   const int64_t n = (int64_t)*n_in, i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if ((int64_t)blockIdx.x * blockDim.x >= n) return;
@@ -594,16 +590,7 @@ __global__ __launch_bounds__(1024) void k_sort_place(const int64_t* list, const 
   for (int b = threadIdx.x; b < kSortBuckets; b += blockDim.x)
     if (h[b]) h[b] = atomicAdd(&cursor[b], h[b]);  // this block's range of bucket b
   __syncthreads();
-  if (i < n) {
-    const uint32_t pos = h[key] + r;
-    out[pos] = task;
-    if (out_rec) {
-      out_rec[4 * (size_t)pos] = make_uint4((uint32_t)task, (uint32_t)((uint64_t)task >> 32), 0u, 0u);
-      out_rec[4 * (size_t)pos + 1] = rec[3 * task];
-      out_rec[4 * (size_t)pos + 2] = rec[3 * task + 1];
-      out_rec[4 * (size_t)pos + 3] = rec[3 * task + 2];
-    }
-  }
+  if (i < n) out[h[key] + r] = task;
 }
 
 // the same over a device-counted list (steps of the path stage): entries list_in[0..*n_in)
@@ -1230,12 +1217,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         static const bool esort = !getenv("OTR_SORT") || atoi(getenv("OTR_SORT")) != 0;  // A/B knob
         int64_t* list2 = nullptr;
         uint32_t* hist = nullptr;
-        uint4* lrec = nullptr;
         if (et == 0 && esort && NT >= 65536) {
           try {
             list2 = need<int64_t>(S_SORT_LIST, NT);
             hist = need<uint32_t>(S_SORT_HIST, kSortBuckets);
-            lrec = need<uint4>(S_SORT_REC, 4 * (size_t)NT);
           } catch (const DeviceOom&) {
             (void)hipGetLastError();  // (no memory for the copy: the list stays in task order)
             list2 = nullptr;
@@ -1248,9 +1233,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
           HIPCHK(hipMemsetAsync(hist, 0, 4 * kSortBuckets, stream));
           k_sort_hist<<<grid_for(NT, 1024), 1024, 0, stream>>>(list, c, task_rec, shift, hist);
           k_sort_scan<<<1, 1024, 0, stream>>>(hist);
-          k_sort_place<<<grid_for(NT, 1024), 1024, 0, stream>>>(list, c, task_rec, shift, hist, list2, lrec);
+          k_sort_place<<<grid_for(NT, 1024), 1024, 0, stream>>>(list, c, task_rec, shift, hist, list2);
           rb.task_list = list2;
-          rb.list_rec = lrec;
         }
         rb.list_count = c;
         rb.queue = queues + (9 + et) * kQueueWords;

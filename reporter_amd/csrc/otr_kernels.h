@@ -1202,7 +1202,6 @@ struct RouteArgs {
   unsigned long long* dump_ctr;       // slots taken (device counter, zeroed per batch)
   uint32_t dump_out_words, dump_out_slots;
   int32_t* task_dump;                 // per task: its slot in the next tier's input, -1: restart
-  const uint4* list_rec;              // (optional) per list entry w: {task, 0}, rec[3 task ..] (k_sort_place)
 };
 
 // k_tasks' inputs and outputs
