@@ -536,16 +536,51 @@ struct WorkE {
   W lab;
 };
 
+// minin(node) as stored in the search table: 16-mm units rounded down, saturating at
+// 65535 (1.05 km).  A lower bound of the shortest in-edge keeps the IN criterion exact.
+__device__ inline uint16_t mi_of(uint32_t m) { return (uint16_t)((m >> 4) < 65535u ? (m >> 4) : 65535u); }
+// the IN criterion's margin of a node: any later offer is >= kmin + this (every edge >= 1 mm)
+__device__ inline uint32_t in_gap(uint16_t mq) { return mq ? (uint32_t)mq << 4 : 1u; }
+// The same in one byte (the large retry tables, whose LDS bytes per slot set their
+// occupancy): a 4-bit exponent, 4-bit mantissa float of 16-mm units, rounded down (>= 94 %
+// of the length, up to 8 km): code c < 16 is c units, else (16 + c % 16) << (c / 16 - 1).
+__device__ inline uint8_t mf8_of(uint32_t m) {
+  const uint32_t u = m >> 4;
+  if (u < 16u) return (uint8_t)u;
+  const int e = 27 - __clz((int)u);  // u in [2^(e+4), 2^(e+5))
+  if (e > 14) return 255;
+  return (uint8_t)(((e + 1) << 4) | ((u >> e) & 15u));
+}
+__device__ inline uint32_t mf8_gap(uint8_t c) {
+  const uint32_t u = c < 16u ? (uint32_t)c : (16u | (c & 15u)) << ((c >> 4) - 1);
+  return u ? u << 4 : 1u;
+}
+
 template <int CAP, int LM>
 struct SearchLds {
   static constexpr bool PRED = LM == 1;
+  // one-byte minin codes (mf8) in the retry tables of 384..1024 slots: 11 B per slot
+  // instead of 12 (C4: the 1024-slot tier 13 waves per CU instead of 12, 263.9 -> 257.0 ms;
+  // 448x2 14 instead of 13, 21.5 -> 19.6 ms; the 2048-slot table keeps its 6 waves either
+  // way and the 2-byte codes)
+  static constexpr bool MI8 = CAP >= 384 && CAP <= 1024 && !PRED;
+  using MiT = typename std::conditional<MI8, uint8_t, uint16_t>::type;
+  __device__ static MiT code(uint32_t m) {
+    if constexpr (MI8) return mf8_of(m);
+    else return mi_of(m);
+  }
+  __device__ static uint32_t gap(MiT c) {
+    if constexpr (MI8) return mf8_gap(c);
+    else return in_gap(c);
+  }
   using W = typename LabelT<LM>::W;
   typename LabelT<LM>::T lab[CAP];  // label (| pred edge)
   uint32_t key[CAP];                  // node id | INQ / REL bits, 0xFFFFFFFF empty
-  uint16_t mi[CAP];                   // minin(node) in 16-mm units, rounded down (mi_of): the IN criterion
+  MiT mi[CAP];                        // minin(node) code (mi_of, or mf8_of): the IN criterion's gap
   using Idx = typename std::conditional<(CAP <= 256 && !PRED), uint8_t, uint16_t>::type;
   // nodes settled per round (at most); k_paths (PRED) reuses pend + work as CAP u32 words
-  static constexpr int WCAP = CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : 128));
+  // (1024 slots: 120, the 1-B codes' table then fits 13 waves per CU's LDS)
+  static constexpr int WCAP = CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : (CAP <= 1024 ? 120 : 128)));
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
   WorkE<W> work[WCAP];                // this round's settled nodes: {node, label}
   int n_pend, n_keys, overflow;
@@ -553,11 +588,6 @@ struct SearchLds {
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
-// minin(node) as stored in the search table: 16-mm units rounded down, saturating at
-// 65535 (1.05 km).  A lower bound of the shortest in-edge keeps the IN criterion exact.
-__device__ inline uint16_t mi_of(uint32_t m) { return (uint16_t)((m >> 4) < 65535u ? (m >> 4) : 65535u); }
-// the IN criterion's margin of a node: any later offer is >= kmin + this (every edge >= 1 mm)
-__device__ inline uint32_t in_gap(uint16_t mq) { return mq ? (uint32_t)mq << 4 : 1u; }
 constexpr uint32_t kInq = 0x80000000u;   // key bit: the node is on the pending list
 constexpr uint32_t kRel = 0x40000000u;   // key bit: the node is settled (its label is final)
 constexpr uint32_t kNodeMask = 0x0FFFFFFFu;
@@ -708,7 +738,7 @@ __device__ inline int relax_one(SearchLds<CAP, LM>& L, const Pack& K, uint32_t d
   const W nw = ((W)nd << K.sh) | (W)tt;  // tt <= pt <= bt < 2^sh - 1
   const int sl = lds_insert<CAP, LM, COUNT>(L, dw & kAdjDstMask, &isnew);
   if (sl < 0) return -1;
-  if (isnew) L.mi[sl] = mi_of(minin);
+  if (isnew) L.mi[sl] = SearchLds<CAP, LM>::code(minin);
   const typename LabelT<LM>::T nb = LabelT<LM>::make(nw, edge);
   const typename LabelT<LM>::T old = atomicMin(&L.lab[sl], nb);
   if (LabelT<LM>::label(nb) < LabelT<LM>::label(old)) {
@@ -763,7 +793,8 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Pac
     }
   }
   go = go && sl >= 0;
-  *((go && isnew) ? &L.mi[sl] : reinterpret_cast<uint16_t*>(mine)) = mi_of(minin);
+  using MiT = typename SearchLds<CAP, 0>::MiT;
+  *((go && isnew) ? &L.mi[sl] : reinterpret_cast<MiT*>(mine)) = SearchLds<CAP, 0>::code(minin);
   const uint32_t old = atomicMin(go ? &L.lab[sl] : mine, nw);
   const bool imp = go && nw < old;
   knext = (imp && nd < knext) ? nd : knext;
@@ -778,7 +809,8 @@ __device__ inline int relax_sink(SearchLds<CAP, 0>& L, uint32_t* sink, const Pac
 // pending ones carry kInq), and the round's kmin; the next table re-inserts the keys,
 // rebuilds the pending list and goes on with the next round: the same rounds as one big
 // table, so the same labels.  32-bit labels only (the retry tiers).  Slot (u64 words):
-// [0] entries n, [1] kmin, [2, 2 + n) label | key << 32, then the n minin codes (u16).
+// [0] entries n, [1] kmin, [2, 2 + n) label | key << 32, then the n IN gaps (u32 mm: the
+// tables' codes differ, SearchLds::code / gap; re-encoding a gap keeps a lower bound).
 struct NDump {
   const unsigned long long* in;  // the dump this group's search resumes (null: a fresh search)
   unsigned long long* base;      // this tier's dump slots (null: an outgrown search restarts)
@@ -788,7 +820,7 @@ struct NDump {
   int stop_rounds;  // test build: a search with dump slots stops after this many rounds (0: off)
 #endif
 };
-__host__ __device__ constexpr uint32_t nd_words(int cap) { return 2u + (uint32_t)cap + ((uint32_t)cap + 3u) / 4u; }
+__host__ __device__ constexpr uint32_t nd_words(int cap) { return 2u + (uint32_t)cap + ((uint32_t)cap + 1u) / 2u; }
 // which retry tables carry the resume code (compile time: the code costs the hot tiers ~2 %
 // even unused): tables of at least OTR_ND_IN_MIN slots resume, of at least OTR_ND_OUT_MIN
 // slots dump (C4: the 1024-slot tier's 4 % outgrowers; the smaller tiers' overflows are few)
@@ -833,7 +865,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
   const int nrx = RIN ? Gr::umax(nres) : 0;
   if (RIN && nrx > 0) {
     const unsigned long long* D = nd->in;
-    const uint16_t* M = (const uint16_t*)(D + 2 + nres);
+    const uint32_t* M = (const uint32_t*)(D + 2 + nres);
     int np = 0;
     for (int base = 0; base < nrx; base += Gr::GL) {
       const int k = base + gl;
@@ -850,7 +882,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
         sl = (int)h;
         L.key[sl] = key;
         L.lab[sl] = (typename LabelT<LM>::T)(uint32_t)e;
-        L.mi[sl] = M[k];
+        L.mi[sl] = SearchLds<CAP, LM>::code(M[k]);
         pend = (key & kInq) != 0u;
       }
       const unsigned long long mp = __ballot(pend);
@@ -877,7 +909,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
   if (active && gl < n_tgt && tnode != kEmpty) {
     bool isnew;
     tslot = lds_insert(L, tnode, &isnew);
-    if (tslot >= 0 && isnew) L.mi[tslot] = mi_of(gapT);
+    if (tslot >= 0 && isnew) L.mi[tslot] = SearchLds<CAP, LM>::code(gapT);
   }
   __syncthreads();
   uint32_t my_settled = 0, my_relaxed = 0, my_rounds = 0;
@@ -913,7 +945,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
         lb = LabelT<LM>::label(L.lab[sl]);
         key = L.key[sl];
         d = K.d(lb);
-        take = (uint64_t)d < (uint64_t)kmin + in_gap(L.mi[sl]);  // final (IN criterion)
+        take = (uint64_t)d < (uint64_t)kmin + SearchLds<CAP, LM>::gap(L.mi[sl]);  // final (IN criterion)
       }
       // at most WCAP settles per round; the rest stay pending (still final later)
       take = take && nw + Gr::prefix(__ballot(take)) < WCAP;
@@ -1048,13 +1080,13 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
       if (has) D[2 + n + Gr::prefix(m)] = (unsigned long long)(uint32_t)L.lab[k] | ((unsigned long long)key << 32);
       n += Gr::count(m);
     }
-    uint16_t* M = dump ? (uint16_t*)(D + 2 + n) : nullptr;
+    uint32_t* M = dump ? (uint32_t*)(D + 2 + n) : nullptr;
     int q = 0;
     for (int base = 0; base < CAP; base += Gr::GL) {
       const int k = base + gl;
       const bool has = dump && k < CAP && L.key[k] != kEmpty;
       const unsigned long long m = __ballot(has);
-      if (has) M[q + Gr::prefix(m)] = L.mi[k];
+      if (has) M[q + Gr::prefix(m)] = SearchLds<CAP, LM>::gap(L.mi[k]);
       q += Gr::count(m);
     }
     if (dump && gl == 0) {
