@@ -208,7 +208,9 @@ constexpr uint32_t kAdjDstMask = 0x0FFFFFFFu;
 constexpr uint32_t kAdjMore = 0x80000000u;
 
 __device__ inline int prefix_count(unsigned long long mask) {
-  return __popcll(mask & ((1ull << lane_id()) - 1ull));
+  // set bits of `mask` below my lane: v_mbcnt_lo + v_mbcnt_hi (two VALU ops instead of a
+  // 64-bit shift, two masks and two bit counts)
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
 }  // namespace otr

@@ -470,7 +470,11 @@ struct Grp {
   __device__ static unsigned long long mine(unsigned long long m) {
     return G == 1 ? m : (m >> (GL * g())) & ((1ull << GL) - 1ull);
   }
-  __device__ static int prefix(unsigned long long m) { return __popcll(mine(m) & ((1ull << gl()) - 1ull)); }
+  // my group's set bits below my lane (G = 1: mbcnt, prefix_count)
+  __device__ static int prefix(unsigned long long m) {
+    if (G == 1) return prefix_count(m);
+    return __popcll(mine(m) & ((1ull << gl()) - 1ull));
+  }
   __device__ static int count(unsigned long long m) { return __popcll(mine(m)); }
   // maximum over groups of a group-uniform value (a wave-uniform loop bound)
   __device__ static int umax(int v) {
