@@ -467,17 +467,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
         for (int base = 0; base < npend; base += OTR_WAVE) {
           const int k = base + lane;
           const bool in = k < npend;
-          int sl = 0;
-          unsigned long long lb = 0;
-          uint32_t kw = 0, mq = 0;
-          bool take = false;
-          if (in) {
-            sl = L.pend[k];
-            lb = L.lab[sl];
-            kw = L.key[sl];  // (read beside the label: the relax lanes then need no dependent read)
-            mq = L.mi[sl];
-            take = (uint64_t)g_k(lb) < (uint64_t)kmin + in_gap8((uint8_t)mq) + tmin;
-          }
+          // the reads are unconditional (a lane past the list reads entry 0: npend > 0 here),
+          // so no exec-mask branch around them
+          const int sl = L.pend[in ? k : 0];
+          const unsigned long long lb = L.lab[sl];
+          const uint32_t kw = L.key[sl];  // (read beside the label: the relax lanes then need no dependent read)
+          const uint32_t mq = L.mi[sl];
+          bool take = in && (uint64_t)g_k(lb) < (uint64_t)kmin + in_gap8((uint8_t)mq) + tmin;
           take = take && nw + prefix_count(__ballot(take)) < WCAP;
           const bool keep = in && !take;
           const unsigned long long mtk = __ballot(take), mk = __ballot(keep);
@@ -498,7 +494,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
         npend = kept;
         OTR_STAMP(tr2);
         // ---- relax: lane = (settled state, adjacency slot)
-        bool tail = false;
+        uint32_t tail = 0u;  // (a lane word, not a lane mask: VALU ors instead of scalar mask updates)
 #pragma unroll 1
         for (int base = 0; base < 4 * nw; base += OTR_WAVE) {
           const int k = base + lane;
@@ -523,14 +519,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
             psl = e1_relax(L, lb, r.x & ~kAdjMore, r.y, tt, er_edge(r), er_deg(r), pd, pt, mode_bit, my_relaxed, knext,
                            dnext, tnext, isnew);
 #endif
-            tail = tail || ((k & 3) == 3 && (r.x & kAdjMore));
+            tail |= ((k & 3) == 3) ? (r.x & kAdjMore) : 0u;
           }
           nkeys += __popcll(__ballot(isnew));
           const unsigned long long mp = __ballot(psl >= 0);
           if (psl >= 0) L.pend[npend + prefix_count(mp)] = (typename LT::Idx)psl;  // (< CAP: one entry per state)
           npend += __popcll(mp);
         }
-        if (__ballot(tail) != 0ull) {  // nodes with more than four out-edges: the CSR tail
+        if (__ballot(tail != 0u) != 0ull) {  // nodes with more than four out-edges: the CSR tail
           if (lane == 0) {
             L.n_pend = npend;
             L.n_keys = 0;
