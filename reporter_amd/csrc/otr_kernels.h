@@ -940,17 +940,13 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
     for (int base = 0; base < npx; base += Gr::GL) {
       const int k = base + gl;
       const bool in = k < np;
-      int sl = 0;
-      uint32_t d = 0, key = 0;
-      W lb = 0;
-      bool take = false;
-      if (in) {
-        sl = L.pend[k];
-        lb = LabelT<LM>::label(L.lab[sl]);
-        key = L.key[sl];
-        d = K.d(lb);
-        take = (uint64_t)d < (uint64_t)kmin + SearchLds<CAP, LM>::gap(L.mi[sl]);  // final (IN criterion)
-      }
+      // unconditional reads (k < CAP; a lane past its group's list reads slot 0), so no
+      // exec-mask branch around them
+      const int sl = in ? (int)L.pend[k] : 0;
+      const W lb = LabelT<LM>::label(L.lab[sl]);
+      const uint32_t key = L.key[sl];
+      const uint32_t d = K.d(lb);
+      bool take = in && (uint64_t)d < (uint64_t)kmin + SearchLds<CAP, LM>::gap(L.mi[sl]);  // final (IN criterion)
       // at most WCAP settles per round; the rest stay pending (still final later)
       take = take && nw + Gr::prefix(__ballot(take)) < WCAP;
       const unsigned long long mt = __ballot(take), mk = __ballot(in && !take);
@@ -975,7 +971,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
     // relax: lane = (work node, adjacency slot), so a round's dependent chain is a single
     // relaxation; slot 3 of a node with more than 4 out-edges also walks the CSR tail
     const int nwx = Gr::umax(4 * nw);
-    bool tail = false;
+    uint32_t tail = 0u;  // (a lane word, not a lane mask: VALU ors instead of scalar mask updates)
     for (int base = 0; base < nwx; base += Gr::GL) {
       const int k = base + gl;
       int psl = -1;
@@ -1002,7 +998,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
           psl = relax_one<CAP, LM, false>(L, K, r.x & ~kAdjMore, r.y, tt, r.z, wk.lab, e0 + slot, pd, pt, mode_bit,
                                           my_relaxed, knext, isnew);
         }
-        tail = tail || (slot == 3 && (r.x & kAdjMore));
+        tail |= slot == 3 ? (r.x & kAdjMore) : 0u;
       }
       nkeys += Gr::count(__ballot(isnew));
       // append newly pending nodes by ballot (no shared counter)
@@ -1014,7 +1010,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
       }
       npend += Gr::count(mp);
     }
-    if (__ballot(tail) != 0ull) {
+    if (__ballot(tail != 0u) != 0ull) {
       // rare: slot 3 of a node with more than 4 out-edges walks the CSR tail; appends
       // through the shared counter
       if (gl == 0) L.n_pend = npend;
