@@ -707,16 +707,17 @@ __host__ __device__ inline bool pack_fits(uint32_t bmm, uint32_t sh) {
 // minin(T) (IN criterion), so L(T) below that — or T settled — makes T's (length, time)
 // final; if even min(L(T), kmin + minin(T)) cannot make L + tpart fit the relative bound
 // pd (= B - the sources' smallest exit part), T is unreachable for every source.
+// (branch-free: the slot's words are read unconditionally, slot 0 for a lane without one)
 template <int CAP, int LM>
 __device__ inline bool target_resolved(const SearchLds<CAP, LM>& L, const Pack& K, int tslot, uint32_t tpart,
                                        uint32_t gapT, uint32_t pd, uint32_t kmin, bool pend_empty) {
-  if (tslot < 0 || pend_empty) return true;
-  if (L.key[tslot] & kRel) return true;
-  const typename LabelT<LM>::W lw = LabelT<LM>::label(L.lab[tslot]);
+  const int ts = tslot < 0 ? 0 : tslot;
+  const uint32_t key = L.key[ts];
+  const typename LabelT<LM>::W lw = LabelT<LM>::label(L.lab[ts]);
   const int64_t lab = lw == LabelT<LM>::kNone ? INT64_MAX / 4 : (int64_t)K.d(lw);
   const int64_t next = (int64_t)kmin + (int64_t)gapT;
-  if (lab < next) return true;
-  return (lab < next ? lab : next) + (int64_t)tpart > (int64_t)pd;
+  const bool unreach = (lab < next ? lab : next) + (int64_t)tpart > (int64_t)pd;
+  return (tslot < 0) | pend_empty | ((key & kRel) != 0u) | (lab < next) | unreach;
 }
 
 // Relax edge (u → dw) with u's FINAL packed label pu: the offer (length nd, time tt) is
@@ -927,7 +928,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
     OTR_STAMP(t0);
     const int np = done ? 0 : npend;
     OTR_STAMP(t1);
-    const bool res = done || gl >= n_tgt || target_resolved(L, K, tslot, tpart, gapT, pd, kmin, np == 0);
+    const bool res = done | (gl >= n_tgt) | target_resolved(L, K, tslot, tpart, gapT, pd, kmin, np == 0);
     done = done || Gr::mine(__ballot(!res)) == 0ull || np == 0;
     OTR_STAMP(t2);
     cyc[0] += t1 - t0;
