@@ -451,12 +451,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
         // ---- targets: every later offer to a target has key >= kmin + tpart + tmin,
         // length >= dmin + tpart and route time >= tmn + tpt (every later label descends
         // from a pending one); done when every needed target is final or unreachable
-        bool res = true;
-        if (tgt) {
-          const unsigned long long tl = L.tlab[lane];
-          res = (tl != kGInf && (uint64_t)g_k(tl) < (uint64_t)kmin + tpart + tmin) ||
-                (uint64_t)dmin + tpart > (uint64_t)pd || (uint64_t)tmn + tpt > (uint64_t)pt;
-        }
+        // (branch-free: every lane reads a target word, lanes >= TG their lane - TG's)
+        const unsigned long long tl = L.tlab[lane & (TG - 1)];
+        const bool res = !tgt | ((tl != kGInf) & ((uint64_t)g_k(tl) < (uint64_t)kmin + tpart + tmin)) |
+                         ((uint64_t)dmin + tpart > (uint64_t)pd) | ((uint64_t)tmn + tpt > (uint64_t)pt);
         if (__ballot(!res) == 0ull || npend == 0) break;
         OTR_STAMP(tr1);
         // ---- partition: final pending states (IN criterion) to the settled list; the
@@ -597,14 +595,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
     if (ok) {
       uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
       if (lane < Kb) {
+        // the target's edge and fraction re-read here (L2-warm) rather than held in
+        // registers through the search
+        const uint32_t ej2 = a.cand_edge[s * OTR_KMAX + lane];
+        const double pj2 = a.cand_p[s * OTR_KMAX + lane];
         int64_t rr = -1, rt = 0;
         uint32_t rc = 0;
         if (forced) {
           rr = -1;
-        } else if (ej == ei && pj >= pi) {
+        } else if (ej2 == ei && pj2 >= pi) {
           const uint2 li = a.clen[sp * OTR_KMAX + i];
-          rr = part_mm(pj - pi, li.x);
-          if (timed) rt = part_mm(pj - pi, li.y);
+          rr = part_mm(pj2 - pi, li.x);
+          if (timed) rt = part_mm(pj2 - pi, li.y);
         } else if (search) {
           const unsigned long long tl = L.tlab[lane];
           if (tl != kGInf) {
