@@ -958,10 +958,10 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
         const uint32_t node = key & kNodeMask;
         L.work[nw + Gr::prefix(mt)] = WorkE<W>{node, lb};
         L.key[sl] = node | kRel;
-      } else if (in) {
-        L.pend[kept + Gr::prefix(mk)] = (Idx)sl;
-        knext = d < knext ? d : knext;
       }
+      const bool keep = in && !take;
+      if (keep) L.pend[kept + Gr::prefix(mk)] = (Idx)sl;
+      knext = (keep && d < knext) ? d : knext;
       nw += Gr::count(mt);
       kept += Gr::count(mk);
       __syncthreads();
@@ -1005,9 +1005,9 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
       // append newly pending nodes by ballot (no shared counter)
       const unsigned long long mp = __ballot(psl >= 0);
       if (psl >= 0) {
+        // (< CAP: the pending nodes are distinct keys of the table; clamped, not branched)
         const int p = npend + Gr::prefix(mp);
-        if (p < CAP) L.pend[p] = (Idx)psl;
-        else L.overflow = 1;
+        L.pend[p < CAP ? p : CAP - 1] = (Idx)psl;
       }
       npend += Gr::count(mp);
     }
