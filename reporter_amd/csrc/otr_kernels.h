@@ -988,12 +988,13 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
         const uint4 r = ld16(g.adj + 4 * (size_t)wnode + slot);
         const uint32_t tt = timed ? tq : 0u;
         if constexpr (LM == 0) {
-          if (sink)
-            psl = relax_sink<CAP>(L, sink, K, r.x & ~kAdjMore, r.y, tt, r.z, wk.lab, pd, pt, mode_bit, my_relaxed,
-                                  knext, isnew);
-          else
-            psl = relax_one<CAP, LM, false>(L, K, r.x & ~kAdjMore, r.y, tt, r.z, wk.lab, 0u, pd, pt, mode_bit,
-                                            my_relaxed, knext, isnew);
+#ifdef OTR_NO_SINK  // (A/B build: the branching relax_one)
+          psl = relax_one<CAP, LM, false>(L, K, r.x & ~kAdjMore, r.y, tt, r.z, wk.lab, 0u, pd, pt, mode_bit,
+                                          my_relaxed, knext, isnew);
+#else  // (every 32-bit table has its scratch row: no run-time test of `sink`)
+          psl = relax_sink<CAP>(L, sink, K, r.x & ~kAdjMore, r.y, tt, r.z, wk.lab, pd, pt, mode_bit, my_relaxed,
+                                knext, isnew);
+#endif
         } else {
           const uint32_t e0 = LM == 1 ? g.node_row[wnode] : 0u;  // edge id = CSR row start + slot
           psl = relax_one<CAP, LM, false>(L, K, r.x & ~kAdjMore, r.y, tt, r.z, wk.lab, e0 + slot, pd, pt, mode_bit,
