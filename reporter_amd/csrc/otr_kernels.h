@@ -1005,6 +1005,16 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
       nkeys += Gr::count(__ballot(isnew));
       // append newly pending nodes by ballot (no shared counter)
       const unsigned long long mp = __ballot(psl >= 0);
+#ifndef OTR_NO_SINK
+      if constexpr (LM == 0 && G == 1) {
+        // branch-free (the one-search retry tables: C4's 1024-slot tier 240.1 -> 237.0 ms;
+        // the two-search first tier is faster with the branch): a lane with nothing to
+        // append writes its scratch word (< CAP: the pending nodes are distinct keys of the
+        // table; clamped)
+        const int p = npend + Gr::prefix(mp);
+        *(psl >= 0 ? &L.pend[p < CAP ? p : CAP - 1] : reinterpret_cast<Idx*>(sink + lane_id())) = (Idx)psl;
+      } else
+#endif
       if (psl >= 0) {
         // (< CAP: the pending nodes are distinct keys of the table; clamped, not branched)
         const int p = npend + Gr::prefix(mp);
