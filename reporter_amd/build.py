@@ -129,12 +129,23 @@ def build_parsecheck(force=False):
     return lib
 
 
+def build_mincheck(force=False):
+    """tools/libmincheck.so: host build of the node tables' IN-gap codes (CPU tests only)."""
+    src = os.path.join(PKG, 'tools', 'mincheck.cpp')
+    lib = os.path.join(PKG, 'tools', 'libmincheck.so')
+    deps = [src, os.path.join(CSRC, 'otr_mincode.h')]
+    if force or not _newer(lib, deps):
+        _run([HIPCC, '-x', 'hip', '--cuda-host-only', '-O2', '-std=c++17', '-fPIC', '-shared', '-o', lib, src])
+    return lib
+
+
 def build_all(force=False):
     """Everything, the three libotr builds in parallel (each compiles its HIP sources for
     gfx950).  force=True recompiles every object (what the driver's build() does)."""
     from concurrent.futures import ThreadPoolExecutor
     build_gen(force)
     build_parsecheck(force)
+    build_mincheck(force)
     build_oracle(force)
     build_calib(force)
     with ThreadPoolExecutor(max_workers=3) as ex:

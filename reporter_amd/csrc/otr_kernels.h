@@ -18,6 +18,7 @@
 #include <type_traits>
 
 #include "otr_device.h"
+#include "otr_mincode.h"  // IN-gap codes of the node tables (mi_of / in_gap, mf8_of / mf8_gap)
 #include "otr_report.h"
 
 // the first tier's table (slots per search, two searches per wave) and its load limit in
@@ -540,25 +541,6 @@ struct WorkE {
   W lab;
 };
 
-// minin(node) as stored in the search table: 16-mm units rounded down, saturating at
-// 65535 (1.05 km).  A lower bound of the shortest in-edge keeps the IN criterion exact.
-__device__ inline uint16_t mi_of(uint32_t m) { return (uint16_t)((m >> 4) < 65535u ? (m >> 4) : 65535u); }
-// the IN criterion's margin of a node: any later offer is >= kmin + this (every edge >= 1 mm)
-__device__ inline uint32_t in_gap(uint16_t mq) { return mq ? (uint32_t)mq << 4 : 1u; }
-// The same in one byte (the large retry tables, whose LDS bytes per slot set their
-// occupancy): a 4-bit exponent, 4-bit mantissa float of 16-mm units, rounded down (>= 94 %
-// of the length, up to 8 km): code c < 16 is c units, else (16 + c % 16) << (c / 16 - 1).
-__device__ inline uint8_t mf8_of(uint32_t m) {
-  const uint32_t u = m >> 4;
-  if (u < 16u) return (uint8_t)u;
-  const int e = 27 - __clz((int)u);  // u in [2^(e+4), 2^(e+5))
-  if (e > 14) return 255;
-  return (uint8_t)(((e + 1) << 4) | ((u >> e) & 15u));
-}
-__device__ inline uint32_t mf8_gap(uint8_t c) {
-  const uint32_t u = c < 16u ? (uint32_t)c : (16u | (c & 15u)) << ((c >> 4) - 1);
-  return u ? u << 4 : 1u;
-}
 
 template <int CAP, int LM>
 struct SearchLds {
