@@ -472,6 +472,8 @@ def main():
                                                        (max(d['ms'], 1e-9) / d['launches'] * 1e-3) / 1e9, 1)}
                   for t, d in sorted(tiers.items())}
     traffic, traffic_src, l2_hit = None, None, None
+    from reporter_amd.build import source_hash
+    build_id = '%s:%s' % (source_hash(), os.path.basename(os.environ.get('OTR_LIB') or 'libotr.so'))
     # FETCH_SIZE + WRITE_SIZE of the dominant kernel from the committed PMC summary of this
     # workload's bench command (tools/profile_set.sh + tools/profile_summary.py:
     # profiles/<round>_pmc_<workload>.json; OTR_PMC_SUMMARY overrides)
@@ -480,8 +482,14 @@ def main():
         import glob
         cands = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_pmc_%s.json' % args.workload)))
         psum = cands[-1] if cands else (PMC_SUMMARY if args.workload == 'c2' else None)
+    # (only a summary recorded from this build: same sources, the product library)
     if psum and os.path.exists(psum) and args.streams == 1:
-        k = json.load(open(psum)).get('kernels', {}).get(kernel_name(dom['code'], turns, dom_t == 0), {})
+        pj = json.load(open(psum))
+        k = pj.get('kernels', {}).get(kernel_name(dom['code'], turns, dom_t == 0), {})
+        if pj.get('build') != build_id:
+            k = {}
+            traffic_src = 'null: %s was recorded from build %s, this run is %s' % (
+                os.path.relpath(psum, ROOT), pj.get('build'), build_id)
         if 'fetch_bytes_per_launch' in k and 'write_bytes_per_launch' in k:
             traffic = int(k['fetch_bytes_per_launch'] + k['write_bytes_per_launch'])
             traffic_src = os.path.relpath(psum, ROOT)
@@ -662,6 +670,7 @@ def main():
                                            'partition': int(counters[18]), 'relax': int(counters[19]),
                                            'setup': int(counters[20]), 'rows': int(counters[21])}
                                           if counters[19] else None)},
+            'build': build_id,
             'cpu_baseline': cpu,
             'parity': parity,
             'end_to_end': e2e,

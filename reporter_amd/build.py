@@ -26,6 +26,20 @@ HIP_FLAGS = ['--offload-arch=' + ARCH, '-O3', '-std=c++17', '-fPIC', '-ffp-contr
              '-I' + os.path.join(ROOT, 'include')]
 
 
+def source_hash():
+    """Identity of the libotr.so sources (the HIP/C++ sources, headers and compile flags):
+    a PMC summary recorded from one build is attached to bench lines of that build only."""
+    import hashlib
+    h = hashlib.sha1(' '.join(HIP_FLAGS[1:]).encode())
+    for d in (CSRC, os.path.join(ROOT, 'include')):
+        for f in sorted(os.listdir(d)):
+            if f.endswith(('.h', '.hip', '.cpp')):
+                h.update(f.encode())
+                with open(os.path.join(d, f), 'rb') as fh:
+                    h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def hip_runtime_dir():
     spec = importlib.util.find_spec('torch')
     if spec and spec.origin:

@@ -100,6 +100,15 @@ struct Matcher {
 
   template <class T>
   T* need(int slot, size_t n);
+  // optional workspace (the retry tiers' resume dumps, the spatial sort's copy): taken
+  // only while the device keeps a reserve free for the mandatory buffers of later stages,
+  // nullptr otherwise (the searches then restart: same results)
+  template <class T>
+  T* want(int slot, size_t n);
+  // frees the optional workspace after the stream drains (a mandatory need() that cannot
+  // allocate retries once after it); not while the route stage's kernels hold it
+  bool release_optional();
+  bool opt_busy = false;
   // entry points: a device allocation failure inside returns OTR_DEVICE_ERROR (no kernel
   // runs on a missing buffer); the *_impl bodies do the work
   int run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err);

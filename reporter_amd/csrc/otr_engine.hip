@@ -176,6 +176,10 @@ int engine_configure(const Config& cfg, std::string* err) {
     if (err) *err = "graph has more than 2^28 nodes";
     return OTR_BAD_REQUEST;
   }
+  if (h.n_edges >= (1u << 28)) {  // the edge-state records pack the out-edge id in 28 bits (erec)
+    if (err) *err = "graph has more than 2^28 directed edges";
+    return OTR_BAD_REQUEST;
+  }
   const uint32_t* dst = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_DST]);
   const float* lenf = (const float*)(base + h.array_offset[OTR_A_EDGE_LEN]);
   const uint32_t* attr = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_ATTR]);
@@ -417,6 +421,11 @@ struct DeviceOom {
   size_t bytes;
 };
 
+static bool optional_slot(int s) {
+  return s == S_E1DUMP0 || s == S_E1DUMP1 || s == S_TASK_DUMP || s == S_NDUMP0 || s == S_NDUMP1 ||
+         s == S_SORT_LIST || s == S_SORT_HIST;
+}
+
 template <class T>
 T* Matcher::need(int slot, size_t n) {
   if ((int)bufs.size() < S_NUM) bufs.resize(S_NUM);
@@ -427,7 +436,13 @@ T* Matcher::need(int slot, size_t n) {
     b.p = nullptr;
     b.bytes = 0;
     size_t nb = bytes + bytes / 4;
-    if (hipMalloc(&b.p, nb) != hipSuccess && hipMalloc(&b.p, bytes) != hipSuccess) {
+    bool ok = hipMalloc(&b.p, nb) == hipSuccess || hipMalloc(&b.p, bytes) == hipSuccess;
+    if (!ok && !optional_slot(slot) && release_optional()) {
+      (void)hipGetLastError();  // the optional workspace is gone: once more
+      nb = bytes;
+      ok = hipMalloc(&b.p, bytes) == hipSuccess;
+    }
+    if (!ok) {
       (void)hipGetLastError();  // clear the sticky allocation error
       b.p = nullptr;
       throw DeviceOom{slot, bytes};
@@ -435,6 +450,53 @@ T* Matcher::need(int slot, size_t n) {
     b.bytes = b.p ? nb : 0;
   }
   return (T*)b.p;
+}
+
+// the free device memory an optional buffer must leave (OTR_OPT_RESERVE_GB, default 8 GB or
+// an eighth of the device, whichever is more): the later stages' mandatory buffers
+static size_t opt_reserve() {
+  static const double gb = getenv("OTR_OPT_RESERVE_GB") ? atof(getenv("OTR_OPT_RESERVE_GB")) : -1.0;
+  if (gb >= 0) return (size_t)std::min(gb * (double)(1ll << 30), 1e18);
+  size_t fr = 0, tot = 0;
+  (void)hipMemGetInfo(&fr, &tot);
+  return std::max<size_t>(8ull << 30, tot / 8);
+}
+
+template <class T>
+T* Matcher::want(int slot, size_t n) {
+  if ((int)bufs.size() < S_NUM) bufs.resize(S_NUM);
+  DevBuf& b = bufs[slot];
+  const size_t bytes = (n ? n : 1) * sizeof(T);
+  if (b.bytes >= bytes) return (T*)b.p;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < bytes || fr - bytes < opt_reserve()) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (hipMalloc(&b.p, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    b.p = nullptr;
+    return nullptr;
+  }
+  b.bytes = bytes;
+  return (T*)b.p;
+}
+
+bool Matcher::release_optional() {
+  if (opt_busy) return false;
+  bool any = false;
+  for (int s = 0; s < (int)bufs.size(); ++s)
+    if (optional_slot(s) && bufs[s].p) {
+      if (!any && stream) (void)hipStreamSynchronize(stream);  // (no queued kernel still reads it)
+      any = true;
+      (void)hipFree(bufs[s].p);
+      bufs[s].p = nullptr;
+      bufs[s].bytes = 0;
+    }
+  return any;
 }
 
 static int oom_error(hipStream_t stream, const DeviceOom& o, std::string* err) {
@@ -657,8 +719,11 @@ static std::vector<int> route_tiers() {
 
 int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err) {
   try {
-    return run_impl(in, mp, out, err);
+    const int rc = run_impl(in, mp, out, err);
+    opt_busy = false;
+    return rc;
   } catch (const DeviceOom& o) {
+    opt_busy = false;
     return oom_error(stream, o, err);
   }
 }
@@ -969,7 +1034,15 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       void* p[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
       const size_t bytes[5] = {4 * c, 8 * c, 4 * c, 8 * c, 4 * c};
       bool good = true;
-      for (int q = 0; q < 5 && good; ++q) good = hipMalloc(&p[q], bytes[q]) == hipSuccess;
+      for (int attempt = 0; attempt < 2; ++attempt) {
+        good = true;
+        for (int q = 0; q < 5 && good; ++q) good = hipMalloc(&p[q], bytes[q]) == hipSuccess;
+        if (good) break;
+        (void)hipGetLastError();
+        for (void*& q : p)
+          if (q) (void)hipFree(q), q = nullptr;
+        if (attempt > 0 || !release_optional()) break;  // (the optional workspace gone: once more)
+      }
       if (good)
         good = hipMemsetAsync(p[0], 0xFF, 4 * c, stream) == hipSuccess &&
                hipMemsetAsync(p[1], 0xFF, 8 * c, stream) == hipSuccess &&
@@ -1052,14 +1125,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // first node tier, which flags every task a retry tier will see, initialises it
     static const bool nresume = !getenv("OTR_NRESUME") || atoi(getenv("OTR_NRESUME")) != 0;  // A/B knob
     static const bool eresume = !getenv("OTR_E1RESUME") || atoi(getenv("OTR_E1RESUME")) != 0;  // A/B knob
-    int32_t* task_dump = nullptr;
-    if ((nresume && node_tasks) || (eresume && turns)) {
-      try {
-        task_dump = need<int32_t>(S_TASK_DUMP, NT);
-      } catch (const DeviceOom&) {
-        (void)hipGetLastError();  // (no dumps: outgrown searches restart, same results)
-      }
-    }
+    int32_t* task_dump = nullptr;  // (optional: without it outgrown searches restart, same results)
+    if ((nresume && node_tasks) || (eresume && turns)) task_dump = want<int32_t>(S_TASK_DUMP, NT);
+    opt_busy = true;  // the optional workspace stays until the route stage's kernels are queued
     ra.task_dump = task_dump;
     tb(OTR_STAGE_ROUTE);
     if (node_tasks) {
@@ -1121,12 +1189,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         nslots[t] = (uint32_t)std::min<int64_t>(std::max<int64_t>(NT / 4, 1024), cap_bytes / (8 * (int64_t)w));
         words[t & 1] = std::max<size_t>(words[t & 1], (size_t)nslots[t] * w);
       }
-      try {
-        for (int q = 0; q < 2; ++q)
-          if (words[q]) ndump[q] = need<unsigned long long>(q == 0 ? S_NDUMP0 : S_NDUMP1, words[q]);
-      } catch (const DeviceOom&) {
-        (void)hipGetLastError();
-      }
+      for (int q = 0; q < 2; ++q)
+        if (words[q]) ndump[q] = want<unsigned long long>(q == 0 ? S_NDUMP0 : S_NDUMP1, words[q]);
       if ((words[0] && !ndump[0]) || (words[1] && !ndump[1])) ndump[0] = ndump[1] = nullptr;
     }
     for (int tier = 0; tier < (node_tasks ? ntier : 0); ++tier) {  // (no node task: no node tier)
@@ -1194,17 +1258,13 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       const uint32_t dwords[2] = {e1_dump_words(OTR_E1CAP), e1_dump_words(512)};
       if (eresume && task_dump) {
         const int64_t cap_bytes[2] = {4ll << 30, 1ll << 30};
-        const int64_t want[2] = {std::max<int64_t>(NT / 16, 4096), std::max<int64_t>(NT / 64, 1024)};
-        try {
-          for (int q = 0; q < 2; ++q) {
-            const int64_t n = std::min<int64_t>(want[q], cap_bytes[q] / (8 * (int64_t)dwords[q]));
-            dump[q] = need<unsigned long long>(q == 0 ? S_E1DUMP0 : S_E1DUMP1, (size_t)n * dwords[q]);
-            dslots[q] = (uint32_t)n;
-          }
-        } catch (const DeviceOom&) {
-          (void)hipGetLastError();  // (no dumps beyond what was allocated: those searches restart)
-          if (!dump[0]) dump[1] = nullptr;
+        const int64_t wanted[2] = {std::max<int64_t>(NT / 16, 4096), std::max<int64_t>(NT / 64, 1024)};
+        for (int q = 0; q < 2; ++q) {  // (no dumps beyond what was allocated: those searches restart)
+          const int64_t n = std::min<int64_t>(wanted[q], cap_bytes[q] / (8 * (int64_t)dwords[q]));
+          dump[q] = want<unsigned long long>(q == 0 ? S_E1DUMP0 : S_E1DUMP1, (size_t)n * dwords[q]);
+          dslots[q] = dump[q] ? (uint32_t)n : 0u;
         }
+        if (!dump[0]) dump[1] = nullptr, dslots[1] = 0u;
       }
       for (int et = 0; et < 3; ++et) {
         const int slot = et == 0 ? 10 : (et == 1 ? 9 : 11);
@@ -1218,13 +1278,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         int64_t* list2 = nullptr;
         uint32_t* hist = nullptr;
         if (et == 0 && esort && NT >= 65536) {
-          try {
-            list2 = need<int64_t>(S_SORT_LIST, NT);
-            hist = need<uint32_t>(S_SORT_HIST, kSortBuckets);
-          } catch (const DeviceOom&) {
-            (void)hipGetLastError();  // (no memory for the copy: the list stays in task order)
-            list2 = nullptr;
-          }
+          list2 = want<int64_t>(S_SORT_LIST, NT);  // (no memory for the copy: the list stays in task order)
+          hist = list2 ? want<uint32_t>(S_SORT_HIST, kSortBuckets) : nullptr;
         }
         if (list2 && hist) {
           int bits = 0;
@@ -1258,6 +1313,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         if (timing) (void)hipEventRecord(ev[24 + 2 * slot + 1], stream);
       }
     }
+    opt_busy = false;  // (every user of the optional workspace is queued)
     // everything left — tasks whose labels need 64 bits, overflows of the largest LDS
     // tables (node and edge-state) — runs in the global-memory search: first on 32K-slot
     // slabs, then what outgrew those on 1M-slot slabs

@@ -22,11 +22,7 @@ __host__ __device__ inline uint32_t in_gap(uint16_t mq) { return mq ? (uint32_t)
 __host__ __device__ inline uint8_t mf8_of(uint32_t m) {
   const uint32_t u = m >> 4;
   if (u < 16u) return (uint8_t)u;
-#if defined(__HIP_DEVICE_COMPILE__)
-  const int e = 27 - __clz((int)u);  // u in [2^(e+4), 2^(e+5)) (the device's count, as measured)
-#else
-  const int e = 27 - __builtin_clz(u);  // (host checker; u >= 16 here)
-#endif
+  const int e = 27 - __builtin_clz(u);  // u in [2^(e+4), 2^(e+5)); u >= 16 (one count for host and device)
   if (e > 14) return 255;
   return (uint8_t)(((e + 1) << 4) | ((u >> e) & 15u));
 }

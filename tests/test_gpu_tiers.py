@@ -42,25 +42,51 @@ for g, nt, npnt, sr, sig, seed, acc, over in [('city', 40, 100, 15, 10.0, 2, Non
     assert r.status == 0, r.status
     c = [int(r.counters[k]) for k in range(24)]
     assert c[9] > 0, c  # the retry tiers settled nodes (and wrote every transition row)
-    if %r:  # forced stops: dumped in one tier, resumed in the next
+    stop, max_dumps = %r, %r
+    if stop and max_dumps is None:  # forced stops: dumped in one tier, resumed in the next
         assert c[12] > 0 and c[11] > 0 and c[12] >= c[11], c
+    if max_dumps is not None:  # dump slots short (or none): the rest restart, same results
+        assert c[12] <= max_dumps and c[11] <= c[12], (c, max_dumps)
+        if stop and max_dumps > 0:
+            assert c[12] > 0, c
     from reporter_amd import _lib
     got = _lib.result_to_numpy(r)
     want = po.match_batch(po.Graph(path), tr, po.params(**{k: float(v) for k, v in over.items()}), threads=8)
     errors, stats = compare(got, want)
     assert not errors, errors
+    # the timed launches (route_work off: the kernels compiled without the work counting,
+    # other task pairings, dump-slot and queue claims) give the same output, field by field
+    r2 = M.Matcher().match_batch(tr, copy_out=True, route_work=False)
+    assert r2.status == 0, r2.status
+    errors, stats = compare(_lib.result_to_numpy(r2), got)
+    assert not errors and all(stats.values()), (errors, stats)  # (floats bit-exact too)
 print('tiers ok')
 '''
 
 
-@pytest.mark.parametrize('tiers,est,stop', [(None, None, False), ('384x2,512', None, False),
-                                            ('512x2,2048', None, False), ('1024', '0', False),
-                                            (None, '1000', False), (None, None, True), ('384x2,512', '0', True)])
-def test_retry_tiers_equal_first_tier(graph_dir, tiers, est, stop):
+def _nd_words(cap):  # otr_kernels.h nd_words: u64 words of one node dump slot
+    return 2 + cap + (cap + 1) // 2
+
+
+# (tiers, size-estimate scale, forced stops, extra environment).  The 768-slot list with the
+# estimate at 0.7 sends most C4-like searches through the two-search 448-slot tables, whose
+# groups stop in different rounds: the list of round 5's nondeterministic run (a finished
+# group's kmin overwritten by its partner's later rounds, dumped with the wrong kmin;
+# DESIGN.md §3.4).  OTR_NDUMP_GB small: dump slots run short, the rest restart.
+# OTR_OPT_RESERVE_GB huge: no optional buffer at all (no dumps, no task_dump).
+TIER_CASES = [(None, None, False, {}), ('384x2,512', None, False, {}), ('512x2,2048', None, False, {}),
+              ('1024', '0', False, {}), (None, '1000', False, {}), (None, None, True, {}),
+              ('384x2,512', '0', True, {}), ('256,448x2,768,2048', '0.7', False, {}),
+              ('256,448x2,768,2048', '0.7', True, {}), (None, None, True, {'OTR_NDUMP_GB': '0.0002'}),
+              (None, None, True, {'OTR_OPT_RESERVE_GB': '1000000'})]
+
+
+@pytest.mark.parametrize('tiers,est,stop,extra', TIER_CASES)
+def test_retry_tiers_equal_first_tier(graph_dir, tiers, est, stop, extra):
     lib = os.path.join(ROOT, 'reporter_amd', 'libotr_tiercheck.so')
     assert os.path.exists(lib), 'build first: python -m reporter_amd.build'
     env = dict(os.environ, OTR_LIB=lib)
-    for k in ('OTR_TIERS', 'OTR_EST_K', 'OTR_FORCE_EDGE'):
+    for k in ('OTR_TIERS', 'OTR_EST_K', 'OTR_FORCE_EDGE', 'OTR_NDUMP_GB', 'OTR_OPT_RESERVE_GB'):
         env.pop(k, None)
     if tiers:
         env['OTR_TIERS'] = tiers
@@ -68,8 +94,15 @@ def test_retry_tiers_equal_first_tier(graph_dir, tiers, est, stop):
         env['OTR_EST_K'] = est
     if stop:
         env['OTR_FORCE_EDGE'] = '128'
-    p = subprocess.run([sys.executable, '-c', CHILD % (ROOT, graph_dir, stop)], env=env, capture_output=True,
-                       text=True, timeout=240)
+    env.update(extra)
+    max_dumps = None
+    if 'OTR_NDUMP_GB' in extra:  # every node tier but the last dumps (the test build), at most this many slots
+        caps = [256, 448, 1024, 2048]
+        max_dumps = sum(int(float(extra['OTR_NDUMP_GB']) * 2 ** 30) // (8 * _nd_words(c)) for c in caps)
+    if 'OTR_OPT_RESERVE_GB' in extra:
+        max_dumps = 0
+    p = subprocess.run([sys.executable, '-c', CHILD % (ROOT, graph_dir, stop, max_dumps)], env=env,
+                       capture_output=True, text=True, timeout=240)
     assert p.returncode == 0 and 'tiers ok' in p.stdout, p.stdout[-2000:] + p.stderr[-4000:]
 
 
@@ -155,6 +188,10 @@ for g, nt, npnt, sr, sig, seed, fb, fp in [('city', 40, 100, 15, 10.0, 2, 0.0, 0
     want = po.match_batch(po.Graph(path), tr, po.params(), threads=8)
     errors, stats = compare(got, want)
     assert not errors, errors
+    r2 = M.Matcher().match_batch(tr, copy_out=True, route_work=False)  # the timed kernels: same output
+    assert r2.status == 0, r2.status
+    errors, stats = compare(_lib.result_to_numpy(r2), got)
+    assert not errors and all(stats.values()), (errors, stats)  # (floats bit-exact too)
 print('edge tiers ok')
 '''
 

@@ -51,6 +51,13 @@ def main(d):
     write = per_dispatch(find(os.path.join(d, 'WRITE_SIZE'), 'counter_collection.csv'), ['WRITE_SIZE'])
     l2 = per_dispatch(find(os.path.join(d, 'TCC_HIT_sum'), 'counter_collection.csv'), ['TCC_HIT', 'TCC_MISS'])
     out = {'source': os.path.relpath(d), 'kernels': {}}
+    # the build the profiled bench command ran (bench.py's 'build': sources hash + library):
+    # bench.py attaches this summary's traffic only to lines of the same build
+    try:
+        with open(os.path.join(d, 'bench_kt.json')) as f:
+            out['build'] = json.loads(f.read().strip().splitlines()[-1]).get('build')
+    except (OSError, ValueError, IndexError):
+        out['build'] = None
     for k in sorted(dur, key=lambda k: -sum(dur[k])):
         if not k.startswith('k_'):
             continue
