@@ -141,6 +141,8 @@ def main():
                          '(60%% auto / 25%% bicycle / 15%% pedestrian) on the metro graph; c5: the country graph '
                          '(50M nodes), this GPU\'s N = 8 share (125,000) of 1M vehicles over 24 h, C5 mode mix')
     ap.add_argument('--e2e-steps', type=int, default=3, help='host-to-host drop-in steps (0 = skip)')
+    ap.add_argument('--json-traces', type=int, default=2000,
+                    help='traces of the JSON drop-in leg (Batch.java bodies; 0 = skip)')
     ap.add_argument('--e2e-streams', type=int, default=2,
                     help='worker threads (matchers, HIP streams, pinned batches) of the host-to-host measurement')
     ap.add_argument('--opt', action='append', default=[],
@@ -593,6 +595,22 @@ def main():
                        ("; %d worker threads, one matcher / HIP stream / pinned batch each, one batch's copies "
                         "overlapping another's kernels" % ne if ne > 1 else '')}
 
+    # ---- rank 0, N = 1: the JSON drop-in path as its callers use it (never `value`):
+    # Batch.java bodies of this workload's traces, whole and in BatchingProcessor-sized
+    # windows, through one otr_report_batch call and through coalesced blocking callers
+    # (reporter_amd/tools/dropin.py), with the host split of each
+    json_dropin = None
+    if rank == 0 and world == 1 and args.json_traces > 0:
+        from reporter_amd.tools import dropin
+        tj = time.perf_counter()
+        json_dropin = dropin.measure(M, matchers[0], mine.slice(0, min(args.json_traces, mine.n_traces)), config=cfg)
+        json_dropin['vs_value'] = {
+            k: round(json_dropin[g][c]['probes_per_s'] / value, 3)
+            for k, g, c in (('whole_batch_call', 'whole_traces', 'batch_c_call'),
+                            ('whole_coalesced_256', 'whole_traces', 'coalesced_256_threads'),
+                            ('windows_coalesced_256', 'streaming_windows', 'coalesced_256_threads'))}
+        log('json drop-in leg %.1f s' % (time.perf_counter() - tj))
+
     if rank == 0:
         line = {
             'metric': 'GPS probes matched/sec (whole node)',
@@ -674,6 +692,7 @@ def main():
             'cpu_baseline': cpu,
             'parity': parity,
             'end_to_end': e2e,
+            'json_dropin': json_dropin,
         }
         print(json.dumps(line), flush=True)
     if dist_on:

@@ -82,6 +82,19 @@ int otr_report_batch(otr_matcher* m, int32_t n, const char* const* bodies, const
  * max_traces <= 0 drains the queue and stops the dispatcher. */
 int otr_coalesce(int32_t max_traces, int32_t max_wait_us);
 
+/* Where the JSON request path's host time goes (new; diagnostics for the drop-in
+ * callers of otr_report / otr_report_batch / the coalescer): summed over every internal
+ * request-processing call of the process since the last reset — calls (a batch call, or
+ * one coalesced batch), items (bodies), device batches, and the wall seconds of its
+ * phases: scan (body parse + validation into SoA, host threads), soa (gather of each
+ * device batch's arrays), device (otr_match_batch: H2D, kernels, D2H of the compacted
+ * reports), format (report() bodies, host threads); total is their sum plus grouping. */
+typedef struct otr_service_split {
+  int64_t calls, items, device_batches;
+  double scan_s, soa_s, device_s, format_s, total_s;
+} otr_service_split;
+int otr_service_stats(otr_service_split* out, int reset);
+
 void otr_free(char* p);
 const char* otr_last_error(void);
 

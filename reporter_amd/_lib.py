@@ -39,7 +39,14 @@ EXPORTS = ['otr_configure', 'otr_configure_json', 'otr_matcher_new', 'otr_matche
            'otr_graph_info', 'otr_matcher_stream', 'otr_device', 'otr_report_batch', 'otr_coalesce',
            'otr_tiles_cull', 'otr_tiles_format', 'otr_ingest', 'otr_report_lists_device', 'otr_hist_reduce',
            'otr_tilehier_row', 'otr_tilehier_col', 'otr_tilehier_file', 'otr_tilehier_files', 'otr_flatten',
-           'otr_max_batch_probes', 'otr_launch_max_items']
+           'otr_max_batch_probes', 'otr_launch_max_items', 'otr_service_stats']
+
+
+class ServiceSplit(ctypes.Structure):
+    """otr_service_split (include/otr.h): the JSON request path's host split."""
+    _fields_ = [('calls', ctypes.c_int64), ('items', ctypes.c_int64), ('device_batches', ctypes.c_int64),
+                ('scan_s', ctypes.c_double), ('soa_s', ctypes.c_double), ('device_s', ctypes.c_double),
+                ('format_s', ctypes.c_double), ('total_s', ctypes.c_double)]
 
 
 class FlatGraph(ctypes.Structure):
@@ -153,6 +160,8 @@ def lib():
     L.otr_report_batch.argtypes = [ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_char_p), P(ctypes.c_size_t),
                                    ctypes.c_int, P(ctypes.c_int32), P(ctypes.c_void_p), P(ctypes.c_size_t)]
     L.otr_coalesce.argtypes = [ctypes.c_int32, ctypes.c_int32]
+    if hasattr(L, 'otr_service_stats'):  # (an A/B build of an earlier round may lack it)
+        L.otr_service_stats.argtypes = [P(ServiceSplit), ctypes.c_int]
     L.otr_tiles_cull.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                  ctypes.c_int32, P(ctypes.c_void_p), P(ctypes.c_int64)]
     L.otr_tiles_format.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_char_p,
@@ -239,3 +248,10 @@ def result_to_numpy(r):
     out['status'] = r.status
     out['n_overflow'] = r.n_overflow_traces
     return out
+
+
+def service_stats(reset=False):
+    """otr_service_stats: the JSON path's host split since the last reset (dict)."""
+    st = ServiceSplit()
+    lib().otr_service_stats(ctypes.byref(st), 1 if reset else 0)
+    return {k: getattr(st, k) for k, _ in ServiceSplit._fields_}

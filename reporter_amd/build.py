@@ -127,8 +127,8 @@ def build_loadgen(force=False):
     exe = os.path.join(PKG, 'tools', 'loadgen')
     lib = os.path.join(PKG, 'libotr.so')
     if force or not _newer(exe, [src, lib, os.path.join(ROOT, 'include', 'otr.h')]):
-        _run(['g++', '-O2', '-std=c++17', '-o', exe, src, '-L' + PKG, '-l:libotr.so', '-Wl,-rpath,' + PKG,
-              '-lpthread'])
+        _run(['g++', '-O2', '-g', '-rdynamic', '-std=c++17', '-o', exe, src, '-L' + PKG, '-l:libotr.so',
+              '-Wl,-rpath,' + PKG, '-lpthread'])
     return exe
 
 

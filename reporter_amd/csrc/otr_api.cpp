@@ -228,6 +228,11 @@ int otr_report_batch(otr_matcher* m, int32_t n, const char* const* bodies, const
 
 int otr_coalesce(int32_t max_traces, int32_t max_wait_us) { return otrsvc::coalesce_configure(max_traces, max_wait_us); }
 
+int otr_service_stats(otr_service_split* out, int reset) {
+  otrsvc::stats(out, reset != 0);
+  return OTR_OK;
+}
+
 // report() alone: reporter_service.py:79-179 (as simple_reporter.py:168 calls it)
 int otr_report_segments(const char* match_json, size_t match_len, const char* trace_json, size_t trace_len,
                         int threshold_sec, const int32_t* report_levels, int n_report_levels,

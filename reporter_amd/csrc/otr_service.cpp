@@ -20,7 +20,7 @@
 namespace otrsvc {
 namespace {
 
-// OTR_SERVICE_TIMING=1: per-phase host timing of process() on stderr (diagnostics)
+// OTR_SERVICE_TIMING=1: also print every process() call's host split on stderr
 bool service_timing() {
   static const bool on = getenv("OTR_SERVICE_TIMING") != nullptr;
   return on;
@@ -30,6 +30,10 @@ double now_s() {
 }
 // per calling thread: concurrent process() calls (coalescer off) never share them
 thread_local double g_t_soa = 0, g_t_run = 0, g_t_fmt = 0;
+thread_local int64_t g_batches = 0;
+// the process-wide split (otr_service_stats)
+std::mutex g_stats_mu;
+otr_service_split g_stats{};
 
 int host_threads() {
   static const int n = [] {
@@ -140,7 +144,7 @@ void run_group(otr::Matcher& m, const std::vector<Item*>& items, std::vector<otr
       ++b;
     }
     const int T = (int)(b - a);
-    const double ta = service_timing() ? now_s() : 0;
+    const double ta = now_s();
     std::vector<int64_t> off(T + 1, 0);
     for (int t = 0; t < T; ++t) off[t + 1] = off[t] + (int64_t)req[run[a + t]].lat.size();
     std::vector<double> lat(np), lon(np);
@@ -172,9 +176,9 @@ void run_group(otr::Matcher& m, const std::vector<Item*>& items, std::vector<otr
     bt.flags = OTR_BATCH_COPY_REPORTS;
     otr_batch_result res;
     std::string err;
-    const double tb = service_timing() ? now_s() : 0;
+    const double tb = now_s();
     const int rc = m.run(&bt, mp, &res, &err);
-    const double tc = service_timing() ? now_s() : 0;
+    const double tc = now_s();
     parallel_for(T, [&](int t) {
       Item* it = items[run[a + t]];
       if (rc != OTR_OK) {
@@ -189,21 +193,26 @@ void run_group(otr::Matcher& m, const std::vector<Item*>& items, std::vector<otr
         otrfmt::match_body(it->out, res, t);
       }
     });
-    if (service_timing()) {
-      g_t_soa += tb - ta;
-      g_t_run += tc - tb;
-      g_t_fmt += now_s() - tc;
-    }
+    g_t_soa += tb - ta;
+    g_t_run += tc - tb;
+    g_t_fmt += now_s() - tc;
+    ++g_batches;
     a = b;
   }
 }
 
 }  // namespace
 
+void stats(otr_service_split* out, bool reset) {
+  std::lock_guard<std::mutex> lk(g_stats_mu);
+  if (out) *out = g_stats;
+  if (reset) g_stats = otr_service_split{};
+}
+
 void process(otr::Matcher& m, const std::vector<Item*>& items) {
   const int n = (int)items.size();
   if (n == 0) return;
-  const double t0 = service_timing() ? now_s() : 0;
+  const double t0 = now_s();
   std::vector<otrreq::Request> req(n);
   const bool configured = otr::graph_state().ready;
   parallel_for(n, [&](int i) {
@@ -232,12 +241,24 @@ void process(otr::Matcher& m, const std::vector<Item*>& items) {
       r.code = it->code;
     }
   });
-  const double t1 = service_timing() ? now_s() : 0;
+  const double t1 = now_s();
   g_t_soa = g_t_run = g_t_fmt = 0;
+  g_batches = 0;
   std::map<std::string, std::vector<int>> groups;
   for (int i = 0; i < n; ++i)
     if (req[i].code == 0) groups[group_key(*items[i], req[i]) + (items[i]->report ? "R" : "M")].push_back(i);
   for (auto& g : groups) run_group(m, items, req, g.second);
+  {
+    std::lock_guard<std::mutex> lk(g_stats_mu);
+    g_stats.calls += 1;
+    g_stats.items += n;
+    g_stats.device_batches += g_batches;
+    g_stats.scan_s += t1 - t0;
+    g_stats.soa_s += g_t_soa;
+    g_stats.device_s += g_t_run;
+    g_stats.format_s += g_t_fmt;
+    g_stats.total_s += now_s() - t0;
+  }
   if (service_timing())
     fprintf(stderr, "otr_service: %d items, %zu groups, %d host threads: scan %.1f ms, soa %.1f ms, "
                     "device batch %.1f ms, format %.1f ms, total %.1f ms\n",
@@ -247,8 +268,32 @@ void process(otr::Matcher& m, const std::vector<Item*>& items) {
 
 // ---------------------------------------------------------------------------------
 // Coalescer: callers on many threads (Kafka stream threads, HTTP server threads) hand
-// their request to one dispatcher thread that runs them as shared device batches.
+// their request to dispatcher threads that run them as shared device batches.  Several
+// dispatchers (OTR_COALESCE_DISPATCHERS, default 2), each with its own matcher and HIP
+// stream: while one batch's kernels run, the next batch is gathered, scanned and launched
+// and the previous one formatted, so small requests (BatchingProcessor.java:26-29: ~10
+// points each) do not leave the GPU idle between batches.
 namespace {
+
+// a gathering dispatcher stops waiting once no request has arrived for this long
+// (OTR_COALESCE_GAP_US, default 100): blocked callers resubmit within microseconds of
+// their responses, so a quiet gap means every active caller is queued, and waiting the
+// rest of max_wait_us would only idle the GPU
+int coalesce_gap_us() {
+  static const int n = [] {
+    const char* e = getenv("OTR_COALESCE_GAP_US");
+    return e ? std::max(0, atoi(e)) : 100;
+  }();
+  return n;
+}
+
+int coalesce_dispatchers() {
+  static const int n = [] {
+    const char* e = getenv("OTR_COALESCE_DISPATCHERS");
+    return e ? std::max(1, std::min(8, atoi(e))) : 2;
+  }();
+  return n;
+}
 
 struct Pending {
   Item* item;
@@ -261,15 +306,35 @@ struct Coalescer {
   std::deque<Pending*> q;
   int max_traces = 0, max_wait_us = 0;
   bool running = false, stop = false;
+  int active = 0;  // dispatcher threads alive
+  std::chrono::steady_clock::time_point last_arrival{};
 
   void loop() {
-    otr::Matcher m;
-    std::unique_lock<std::mutex> lk(mu);
+    {
+      otr::Matcher m;  // (destroyed before this dispatcher reports itself gone: a caller
+                       // that stops the coalescer may then tear the process down)
+      std::unique_lock<std::mutex> lk(mu);
+      run(m, lk);
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    if (--active == 0) running = false;
+    cv_done.notify_all();
+    cv_work.notify_all();  // (the other dispatchers see the drained queue too)
+  }
+
+  void run(otr::Matcher& m, std::unique_lock<std::mutex>& lk) {
     for (;;) {
       cv_work.wait(lk, [&] { return stop || !q.empty(); });
       if (q.empty()) break;  // stop requested and drained
+      // gather: until max_traces are queued, max_wait_us after the first, or a quiet gap
       const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(max_wait_us);
-      cv_work.wait_until(lk, deadline, [&] { return stop || (int)q.size() >= max_traces; });
+      const auto gap = std::chrono::microseconds(coalesce_gap_us());
+      for (;;) {
+        const auto until = std::min(deadline, last_arrival + gap);
+        if (cv_work.wait_until(lk, until, [&] { return stop || (int)q.size() >= max_traces; })) break;
+        const auto now = std::chrono::steady_clock::now();
+        if (now >= deadline || now >= last_arrival + gap) break;
+      }
       std::vector<Pending*> batch;
       while (!q.empty() && (int)batch.size() < max_traces) {
         batch.push_back(q.front());
@@ -283,9 +348,8 @@ struct Coalescer {
       lk.lock();
       for (Pending* p : batch) p->done = true;
       cv_done.notify_all();
+      if (!q.empty()) cv_work.notify_one();  // (another dispatcher may be idle)
     }
-    running = false;
-    cv_done.notify_all();
   }
 };
 
@@ -318,7 +382,8 @@ int coalesce_configure(int max_traces, int max_wait_us) {
   c.max_wait_us = max_wait_us < 0 ? 0 : max_wait_us;
   if (!c.running) {
     c.running = true;
-    std::thread([&c] { c.loop(); }).detach();
+    c.active = coalesce_dispatchers();
+    for (int k = 0; k < c.active; ++k) std::thread([&c] { c.loop(); }).detach();
   }
   return OTR_OK;
 }
@@ -333,6 +398,7 @@ void coalesce_submit(otr::Matcher& fallback, Item* item) {
     return;
   }
   c.q.push_back(&p);
+  c.last_arrival = std::chrono::steady_clock::now();
   if ((int)c.q.size() >= c.max_traces || c.q.size() == 1) c.cv_work.notify_one();
   c.cv_done.wait(lk, [&] { return p.done; });
 }

@@ -26,6 +26,8 @@ struct Item {
 
 // Runs every item through one or more device batches on matcher m.
 void process(otr::Matcher& m, const std::vector<Item*>& items);
+// The host split of every process() call so far (otr_service_stats); reset: start over.
+void stats(otr_service_split* out, bool reset);
 
 // Request coalescing across threads (otr_coalesce in include/otr.h).
 bool coalesce_enabled();

@@ -124,12 +124,13 @@ def _crafted_rank(rank, world, store, out, privacy):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('privacy', [2, 3])
-def test_two_rank_owner_cull_equals_reference_loop(tmp_path, privacy):
-    """gloo world 2: the owners' union after the keyed exchange keeps exactly the pairs
-    (and line counts) the reference loop keeps on the whole set's files."""
+@pytest.mark.parametrize('world,privacy', [(2, 2), (2, 3), (4, 2), (8, 2), (8, 3)])
+def test_owner_cull_equals_reference_loop(tmp_path, world, privacy):
+    """gloo world 2, 4, 8: the owners' union after the keyed exchange keeps exactly the
+    pairs (and line counts) the reference loop keeps on the whole set's files (at N = 8
+    some ranks hold no line and some owners receive no entry)."""
     out = str(tmp_path / 'owned.npy')
-    mp.spawn(_crafted_rank, args=(2, _store(tmp_path), out, privacy), nprocs=2, join=True)
+    mp.spawn(_crafted_rank, args=(world, _store(tmp_path), out, privacy), nprocs=world, join=True)
     got = _pairs_from_entries(np.load(out))
     want = _pairs_from_lines(_rows(CRAFTED), privacy)
     assert want and got == want

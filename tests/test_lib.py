@@ -77,7 +77,8 @@ def test_struct_layouts_against_c_header(tmp_path):
         import pytest
         pytest.skip('no C compiler')
     structs = {'otr_trace_batch': _lib.TraceBatch, 'otr_ingest_format': _lib.IngestFormat,
-               'otr_ingest_result': _lib.IngestResult, 'otr_batch_result': _lib.BatchResult}
+               'otr_ingest_result': _lib.IngestResult, 'otr_batch_result': _lib.BatchResult,
+               'otr_service_split': _lib.ServiceSplit}
     prog = ['#include <stdio.h>', '#include <stddef.h>', '#include "otr.h"', 'int main(void) {']
     for cname, cls in structs.items():
         prog.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))

@@ -98,13 +98,15 @@ def _rank(rank, world, store, graph_dir, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_row_exchange(tmp_path, graph_dir):
+@pytest.mark.parametrize('world', [2, 4, 8])
+def test_row_exchange(tmp_path, graph_dir, world):
     tr, res, first, last = _oracle_workload(graph_dir)
-    want = ot.tiles(ot.rows_from_reports(res, first, last), 2)
+    all_rows = ot.rows_from_reports(res, first, last)
+    want = ot.tiles(all_rows, 2)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     store = _store(tmp_path)
-    ps = [ctx.Process(target=_rank, args=(r, 2, store, graph_dir, q)) for r in range(2)]
+    ps = [ctx.Process(target=_rank, args=(r, world, store, graph_dir, q)) for r in range(world)]
     for p in ps:
         p.start()
     outs = [q.get(timeout=300) for _ in ps]
@@ -116,7 +118,9 @@ def test_two_rank_row_exchange(tmp_path, graph_dir):
         assert not (set(t) & set(merged))  # a file lives on exactly one owner
         merged.update(t)
     assert merged == want and len(want) > 0
-    assert all(n > 0 for _, _, n in outs)
+    assert sum(n for _, _, n in outs) == len(all_rows)  # every row reached exactly one owner
+    if world == 2:
+        assert all(n > 0 for _, _, n in outs)
 
 
 def test_java_clean_matches_python_cull_on_numeric_order():

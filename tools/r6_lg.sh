@@ -1,0 +1,21 @@
+#!/bin/bash
+# loadgen on c2dep bodies (diagnostic)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/${1:-r6lg}
+mkdir -p $O
+timeout -k 10 300 python3 -u - <<'PY' > $O/prep.log 2>&1 || exit 1
+import json, os, sys
+sys.path.insert(0, '.')
+from reporter_amd import matcher as M
+from reporter_amd.tools import gen, dropin
+gp = gen.graph_path('metro', 'build/graphs')
+tr = gen.make_traces(gp, 2000, 100, 15, 10.0, 2, t_begin=1483228800, t_spread=1800)
+json.dump(M.default_config(gp), open('/tmp/lg_cfg.json', 'w'))
+open('/tmp/lg_bodies.txt', 'wb').write(b'\n'.join(dropin.bodies(tr)[0]) + b'\n')
+open('/tmp/lg_small.txt', 'wb').write(b'\n'.join(dropin.bodies(tr, 12)[0]) + b'\n')
+print('prepared')
+PY
+for D in 1 2; do
+  OTR_COALESCE_DISPATCHERS=$D timeout -k 10 120 reporter_amd/tools/loadgen /tmp/lg_cfg.json /tmp/lg_bodies.txt 64 4096 2000 > $O/lg_d$D.json 2> $O/lg_d$D.err; echo "d$D rc=$?"
+done
