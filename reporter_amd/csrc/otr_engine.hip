@@ -924,6 +924,34 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     if (err) *err = "device allocation failed (transitions)";
     return OTR_DEVICE_ERROR;
   }
+  // the first tier's size estimate (k_tasks, for route_unit): an exact search runs to its
+  // bounds unless its targets resolve first, so its keys grow with the area it can reach,
+  // est = c * density * reach^2, reach = min(length bound, time bound x 50 km/h capped by
+  // the mode's speed).  A search whose estimate exceeds the first tier's table starts in the
+  // retry tier that holds it: k_tasks flags it and the first tier passes it on without
+  // loading its step.  c = 0.5 (C4's 60 s steps reach ~1.7 km and start in the
+  // 1024-slot tier: C4 1.69M -> 2.47M probes/s; c = 1.7, the full-exhaustion fit of C2,
+  // sent them to the 4096 tier, 1.07M; C2's 15 s steps stay in the first tier either way,
+  // profiles/r03_est_*).  OTR_EST_K scales c (A/B knob; 0 = every search starts in the
+  // first tier).
+  static const int route_g = getenv("OTR_ROUTE_G") ? atoi(getenv("OTR_ROUTE_G")) : 2;  // A/B knob
+  float est_k = 0.f, est_v[OTR_MODES];
+  uint32_t est_tier_keys[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  int n_est_tiers = 0;
+  {
+    static const double est_scale = getenv("OTR_EST_K") ? atof(getenv("OTR_EST_K")) : 1.0;
+    const double mlat = g.grid_min_lat + 0.5 * g.grid_rows * g.grid_cell_deg;
+    const double area = (g.grid_rows * g.grid_cell_deg * kMetersPerDeg) *
+                        (g.grid_cols * g.grid_cell_deg * kMetersPerDeg * cos_deg(fmin(fabs(mlat), 89.0)));
+    est_k = (float)(est_scale * 0.5 * (area > 0.0 ? (double)g.n_nodes / area : 0.0));
+    for (int m = 0; m < OTR_MODES; ++m) {
+      const double kph = mp.m[m].speed_kph > 0.0 && mp.m[m].speed_kph < 50.0 ? mp.m[m].speed_kph : 50.0;
+      est_v[m] = (float)(kph / 3.6);
+    }
+    static const std::vector<int> tl = route_tiers();
+    n_est_tiers = (int)std::min<size_t>(tl.size(), 8);
+    for (int t = 0; t < n_est_tiers; ++t) est_tier_keys[t] = (uint32_t)((tl[t] / 10) * 7 / 8);
+  }
   if (S > 0) {  // tasks and their records (K2 + K2c)
     TaskArgs ta{};
     ta.n_states = S;
@@ -945,6 +973,12 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     ta.task_mask = task_mask;
     ta.rec = task_rec;
     ta.flag_turn = task_ovf;  // turn-mode tasks start in the first edge-state tier (flag 5)
+    // the two-search first tier's table: a step expected beyond it is flagged here
+    ta.est_first_keys = route_g == 2 ? (OTR_CAP1 * OTR_LOAD1) / 8 : 0;
+    ta.est_k = est_k;
+    for (int m = 0; m < OTR_MODES; ++m) ta.est_v[m] = est_v[m];
+    ta.n_tiers = n_est_tiers;
+    for (int t = 0; t < n_est_tiers; ++t) ta.tier_keys[t] = est_tier_keys[t];
     if (NT > 0) HIPCHK(hipMemsetAsync(task_ovf, 0, 4 * NT, stream));
     if (k32) k_tasks<2><<<(unsigned)grid_per_state_waves(S, 2).blocks, 256, 0, stream>>>(ta);
     else k_tasks<1><<<(unsigned)grid_per_state_waves(S, 1).blocks, 256, 0, stream>>>(ta);
@@ -982,29 +1016,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   for (int m = 0; m < OTR_MODES; ++m) ra.inv_beta[m] = mp.m[m].inv_beta;
   ra.overflow_flag = task_ovf;
   ra.stamps = d_counters;
-  // the first tier's size estimate (k_route route_unit): an exact search runs to its
-  // bounds unless its targets resolve first, so its keys grow with the area it can reach,
-  // est = c * density * reach^2, reach = min(length bound, time bound x 50 km/h capped by
-  // the mode's speed).  A search whose estimate exceeds the first tier's table starts in the
-  // retry tier that holds it.  c = 0.5 (C4's 60 s steps reach ~1.7 km and start in the
-  // 1024-slot tier: C4 1.69M -> 2.47M probes/s; c = 1.7, the full-exhaustion fit of C2,
-  // sent them to the 4096 tier, 1.07M; C2's 15 s steps stay in the first tier either way,
-  // profiles/r03_est_*).  OTR_EST_K scales c (A/B knob; 0 = every search starts in the
-  // first tier).
-  {
-    static const double est_scale = getenv("OTR_EST_K") ? atof(getenv("OTR_EST_K")) : 1.0;
-    const double mlat = g.grid_min_lat + 0.5 * g.grid_rows * g.grid_cell_deg;
-    const double area = (g.grid_rows * g.grid_cell_deg * kMetersPerDeg) *
-                        (g.grid_cols * g.grid_cell_deg * kMetersPerDeg * cos_deg(fmin(fabs(mlat), 89.0)));
-    ra.est_k = (float)(est_scale * 0.5 * (area > 0.0 ? (double)g.n_nodes / area : 0.0));
-    for (int m = 0; m < OTR_MODES; ++m) {
-      const double kph = mp.m[m].speed_kph > 0.0 && mp.m[m].speed_kph < 50.0 ? mp.m[m].speed_kph : 50.0;
-      ra.est_v[m] = (float)(kph / 3.6);
-    }
-    static const std::vector<int> tl = route_tiers();
-    ra.n_tiers = (int)std::min<size_t>(tl.size(), 8);
-    for (int t = 0; t < ra.n_tiers; ++t) ra.tier_keys[t] = (uint32_t)((tl[t] / 10) * 7 / 8);
-  }
+  ra.est_k = est_k;
+  for (int m = 0; m < OTR_MODES; ++m) ra.est_v[m] = est_v[m];
+  ra.n_tiers = n_est_tiers;
+  for (int t = 0; t < n_est_tiers; ++t) ra.tier_keys[t] = est_tier_keys[t];
   // device-side counters of the retry lists: [0..7] route tiers, [8] general tier 1,
   // [9] general tier 2, [10] route tasks left unrouted, [11] steps, [12..15] path tiers,
   // [16] path general 1, [17] path general 2, [18] paths left, [19] general overflow
@@ -1091,7 +1106,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ga.n_overflow = cnt + 19;
   if (NT > 0) {
     // two searches per wave (CAP 160 tables); wider steps and overflows retry below
-    static const int route_g = getenv("OTR_ROUTE_G") ? atoi(getenv("OTR_ROUTE_G")) : 2;  // A/B knob
     // the LDS tiers count their work only when asked (OTR_BATCH_ROUTE_WORK): the end-of-
     // wave counter atomics cost ~7% of the first tier (tools/ab_libs.sh)
     unsigned long long* rwork = (in->flags & OTR_BATCH_ROUTE_WORK) ? d_counters : nullptr;
@@ -1134,19 +1148,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       // one unit (G searches) per block, in launches of at most 2^25 blocks: a dispatch's
       // grid size counts work-items in 32 bits (178M tasks at 12.5M probes would wrap)
       const int64_t units = route_g == 2 ? (NT + 1) / 2 : NT;
-#if OTR_FIRST_Q
-      {
-        RouteArgs rf = ra;
-        rf.queue = queues + 12 * kQueueWords;
-        if (route_g == 2) OTR_ROUTE_LAUNCH(OTR_CAP1, 2, false, 16384, rf, rwork);
-        else OTR_ROUTE_LAUNCH(256, 1, false, 16384, rf, rwork);
-      }
-      constexpr int64_t kMaxUnits = 0;  // (no chunked launches)
-      for (int64_t base = 0; kMaxUnits > 0 && base < units; base += kMaxUnits) {
-#else
       constexpr int64_t kMaxUnits = 1ll << 25;
       for (int64_t base = 0; base < units; base += kMaxUnits) {
-#endif
         RouteArgs rf = ra;
         rf.unit_base = base;
         const int64_t u = std::min<int64_t>(kMaxUnits, units - base);

@@ -29,9 +29,6 @@
 #ifndef OTR_LOAD1
 #define OTR_LOAD1 7
 #endif
-#ifndef OTR_FIRST_Q
-#define OTR_FIRST_Q 0
-#endif
 // the lean first edge-state tier's table (otr_edge1.h): 360 states with a 32-state settled
 // list and 16 relax scratch words, 10.1 KB of LDS, 16 waves per CU (c2dep with work queues:
 // branching relax at 368 states 5.71M, 384 at 15 waves 5.35M; branch-free relax at 360
@@ -1251,6 +1248,13 @@ struct TaskArgs {
   unsigned long long* task_mask;
   uint4* rec;                 // 3 per task (the K2c record, below)
   int32_t* flag_turn;         // per task: 5 for a turn-mode task (the first edge-state tier's list), or null
+  // the two-search first tier's size estimate (RouteArgs est_*): a node-mode step whose
+  // estimated keys exceed est_first_keys (0: no estimate) starts in a retry tier
+  int est_first_keys;
+  float est_k;
+  float est_v[OTR_MODES];
+  uint32_t tier_keys[8];
+  int n_tiers;
 };
 
 // One lane group per step s (G states per wave: G = 2 when every mode keeps <= 32
@@ -1262,10 +1266,13 @@ struct TaskArgs {
 // source edge is its own task (the edge-state search).  The task's representative (its lowest source) writes task_state,
 // task_mask and the task record k_route reads:
 //   rec[3t]   = {s, sp, root, bound_mm}
-//   rec[3t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16 | turn << 17, mask lo, mask hi}
+//   rec[3t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16 | turn << 17 | pre << 18,
+//                mask lo, mask hi}
 //   rec[3t+2] = {0, time bound bt, trans_off[s] lo, hi}
 // general: the task runs in the global-memory search (a bound whose packed labels would
-// not fit 32 bits, or a turn mode: edge-based labels).
+// not fit 32 bits, or a turn mode: edge-based labels).  pre (4 bits): 1 | the retry tier
+// << 1 of a step whose size estimate exceeds the first tier's table (the first tier flags
+// it 16 + tier without loading its step); the estimate is per step (bound, time bound, mode).
 template <int G>
 __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
   constexpr int GL = OTR_WAVE / G;
@@ -1309,8 +1316,19 @@ __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
 #else
   const bool general = !pack_fits(bmm, sh) || turn;
 #endif
+  uint32_t pre = 0u;
+  if (a.est_first_keys > 0 && !general && !turn && !a.forced[s]) {
+    float reach = (float)bmm * 1e-3f;
+    if (bt >= 0) reach = fminf(reach, (float)bt * 0.1f * a.est_v[md]);
+    const float est = a.est_k * reach * reach;
+    if (est > (float)a.est_first_keys) {
+      uint32_t st = 0;
+      while ((int)st + 1 < a.n_tiers && (float)a.tier_keys[st] < est) ++st;
+      pre = 1u | (st << 1);
+    }
+  }
   const uint32_t meta = (uint32_t)a.cand_count[s] | ((uint32_t)md << 8) | ((a.forced[s] ? 1u : 0u) << 10) |
-                        (sh << 11) | ((general ? 1u : 0u) << 16) | (turn << 17);
+                        (sh << 11) | ((general ? 1u : 0u) << 16) | (turn << 17) | (pre << 18);
   const int64_t to = a.trans_off[s];
   if (turn && a.flag_turn) a.flag_turn[o] = 5;  // the edge-state tiers (otr_edge1.h)
   a.rec[3 * o] = make_uint4((uint32_t)s, (uint32_t)sp, root, bmm);
@@ -1377,17 +1395,11 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     // targets are lanes of the group (wider steps go to a G = 1 tier); 32-bit tables leave
     // the tasks whose packed words need 64 bits to the WIDE tier
     fits = Kb <= Gr::GL && (WIDE || !general) && !((r1.y >> 17) & 1u);
-    if (G == 2 && !LIST && have) {  // a search too big for this table starts in a retry tier
-      const int md = (int)((r1.y >> 8) & 3u);
-      float reach = (float)r0.w * 1e-3f;
-      if ((int32_t)r2.y >= 0) reach = fminf(reach, (float)r2.y * 0.1f * a.est_v[md]);
-      const float est = a.est_k * reach * reach;
-      constexpr int kFirstKeys = (CAP * OTR_LOAD1) / 8;
-      if (est > (float)kFirstKeys) {
-        start_tier = 0;
-        while (start_tier + 1 < a.n_tiers && (float)a.tier_keys[start_tier] < est) ++start_tier;
-        fits = false;
-      }
+    // a step too big for this table starts in a retry tier (k_tasks' estimate): no load of it
+    const bool pre = G == 2 && !LIST && have && ((r1.y >> 18) & 1u);
+    if (pre) {
+      start_tier = (int)((r1.y >> 19) & 7u);
+      fits = false;
     }
     mode_bit = 1u << ((r1.y >> 8) & 3u);
     bmm = r0.w;
@@ -1398,7 +1410,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     double pj = 0;
     bool needed = false;
     uint4 cq = make_uint4(0u, 0u, 0u, 0u);
-    if (have && lane < Kb) {
+    if (have && !pre && lane < Kb) {
       ej = a.cand_edge[s * OTR_KMAX + lane];
       pj = a.cand_p[s * OTR_KMAX + lane];
       cq = a.cprep[s * OTR_KMAX + lane];
@@ -1406,7 +1418,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     }
     // the task's sources staged one per lane (lane q: the q-th set bit of mask), read in
     // the loop by group shuffles: one parallel load instead of a dependent one per source
-    const int nsrc = have ? __popcll(mask) : 0;
+    const int nsrc = have && !pre ? __popcll(mask) : 0;
     const int iq = lane < nsrc ? nth_set_bit(mask, lane) : 0;
     uint32_t e_q = 0, t_q = 0;
     double p_q = 0;
@@ -1620,19 +1632,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
 #endif
   if (!LIST) {
     const int64_t n_units = (a.n_tasks + G - 1) / G;
-#if OTR_FIRST_Q  // A/B build: a persistent first tier over per-XCD work queues
-    XcdQueue q(a.queue, n_units);
-    for (int64_t w = q.next(); w < q.hi; w = q.next()) {
-      route_unit<CAP, G, LIST, WIDE, CNT>(gr, a, counters, Ls, w, a.n_tasks, sink, trec);
-      __syncthreads();
-    }
-#else
-    // the first tier: one unit per block, XCD-mapped (no loop: fewer live registers);
-    // units [unit_base, unit_base + gridDim.x): a launch's grid stays below 2^32 work-items
-    // (the dispatch packet's grid size), so a large batch is several launches
+    // the first tier (task-major; the default is k_route_step): one unit per block,
+    // XCD-mapped (no loop: fewer live registers); units [unit_base, unit_base + gridDim.x):
+    // a launch's grid stays below 2^32 work-items (the dispatch packet's grid size), so a
+    // large batch is several launches
     const int64_t w = a.unit_base + xcd_remap(blockIdx.x, (int64_t)gridDim.x / 8);
     if (w < n_units) route_unit<CAP, G, LIST, WIDE, CNT>(gr, a, counters, Ls, w, a.n_tasks, sink, trec);
-#endif
     return;
   }
   const int64_t n_tasks = (int64_t)*a.list_count;
