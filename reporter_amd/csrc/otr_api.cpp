@@ -219,10 +219,12 @@ int otr_report_batch(otr_matcher* m, int32_t n, const char* const* bodies, const
     ptrs[i] = &items[i];
   }
   otrsvc::process(m->m, ptrs);
-  for (int32_t i = 0; i < n; ++i) {
+  // the responses' copies on the host threads (C2: 70 MB of report() bodies per 2,000 traces)
+  otrsvc::parallel(n, [&](int i) {
     codes[i] = items[i].code;
     dup_out(items[i].out, &outs[i], out_lens ? &out_lens[i] : nullptr);
-  }
+    std::string().swap(items[i].out);  // (freed here, in parallel, not at return)
+  });
   return OTR_OK;
 }
 

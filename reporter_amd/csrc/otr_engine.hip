@@ -728,6 +728,14 @@ int Matcher::run(const otr_trace_batch* in, const ModeParams& mp, otr_batch_resu
   }
 }
 
+// a persistent grid (work queues or a grid stride over a device-side list) of at most
+// `full` blocks, but never more than the list can hold (`units`, known on the host: tasks
+// or steps): a small batch does not launch thousands of workgroups that find nothing
+static unsigned pgrid(unsigned full, int64_t units) {
+  const int64_t u = std::max<int64_t>(8, (units + 7) / 8 * 8);
+  return (unsigned)std::min<int64_t>((int64_t)full, u);
+}
+
 int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch_result* out, std::string* err) {
   GraphState& gs = graph_state();
   std::shared_lock<std::shared_mutex> graph_lock(gs.mu);  // a reconfigure waits for this batch
@@ -1215,7 +1223,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       unsigned long long* rcn = rwork ? d_counters + (2 + tier) * bank : nullptr;
       out->route_tier_code[1 + tier] = tiers[tier];
       if (timing) (void)hipEventRecord(ev[24 + 2 * (1 + tier)], stream);
-#define OTR_TIER(C, G_) OTR_ROUTE_LAUNCH(C, G_, true, (C) <= 512 ? 16384u : 16384u * 512u / (C), rb, rcn)
+#define OTR_TIER(C, G_) \
+  OTR_ROUTE_LAUNCH(C, G_, true, pgrid((C) <= 512 ? 16384u : 16384u * 512u / (C), (NT + (G_) - 1) / (G_)), rb, rcn)
       switch (tiers[tier]) {
         case 2561: OTR_TIER(256, 1); break;
         case 5121: OTR_TIER(512, 1); break;
@@ -1243,8 +1252,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       rb.queue = queues + 8 * kQueueWords;
       out->route_tier_code[8] = 900000 + 2048;
       if (timing) (void)hipEventRecord(ev[24 + 2 * 8], stream);
-      if (rwork) k_route<2048, 1, true, true, true><<<4096, 64, 0, stream>>>(g, rb, d_counters + 7 * bank);
-      else k_route<2048, 1, true, true, false><<<4096, 64, 0, stream>>>(g, rb, nullptr);
+      if (rwork) k_route<2048, 1, true, true, true><<<pgrid(4096, NT), 64, 0, stream>>>(g, rb, d_counters + 7 * bank);
+      else k_route<2048, 1, true, true, false><<<pgrid(4096, NT), 64, 0, stream>>>(g, rb, nullptr);
       if (timing) (void)hipEventRecord(ev[24 + 2 * 8 + 1], stream);
     }
 #endif
@@ -1310,9 +1319,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         // 512, 6 at 1024) claiming tasks from per-XCD queues; steps with more than 32
         // targets (modes keeping > 32 candidates) pass the lean tiers (their TG = 32) on to
         // k_general
-        if (et == 0) k_route_e1<OTR_E1CAP><<<8192, 64, 0, stream>>>(g, rb, rcn);
-        else if (et == 1) k_route_e1<512><<<4096, 64, 0, stream>>>(g, rb, rcn);
-        else k_route_e1<1024><<<2048, 64, 0, stream>>>(g, rb, rcn);
+        if (et == 0) k_route_e1<OTR_E1CAP><<<pgrid(8192, NT), 64, 0, stream>>>(g, rb, rcn);
+        else if (et == 1) k_route_e1<512><<<pgrid(4096, NT), 64, 0, stream>>>(g, rb, rcn);
+        else k_route_e1<1024><<<pgrid(2048, NT), 64, 0, stream>>>(g, rb, rcn);
         if (timing) (void)hipEventRecord(ev[24 + 2 * slot + 1], stream);
       }
     }
@@ -1333,7 +1342,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       ga.counters = d_counters + (8 + gt) * bank;
       out->route_tier_code[6 + gt] = -1 - gt;
       if (timing) (void)hipEventRecord(ev[24 + 2 * (6 + gt)], stream);
-      k_general<<<gs2.n, kGenThreads, 0, stream>>>(g, ga, gs2);
+      k_general<<<pgrid(gs2.n, NT), kGenThreads, 0, stream>>>(g, ga, gs2);
       if (timing) (void)hipEventRecord(ev[24 + 2 * (6 + gt) + 1], stream);
     }
     // tasks still flagged (beyond a 1M-state slab): their traces get OTR_MATCH_ERROR
@@ -1441,9 +1450,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0x2u, list, c);
         PathArgs pb = pa;
         pb.queue = pq + tier * kPQWords;
-        if (tier == 0) k_paths<512, 1><<<16384, 64, 0, stream>>>(g, pb, list, c);
-        else if (tier == 1) k_paths<1024, 1><<<8192, 64, 0, stream>>>(g, pb, list, c);
-        else k_paths<4096, 1><<<4096, 64, 0, stream>>>(g, pb, list, c);
+        if (tier == 0) k_paths<512, 1><<<pgrid(16384, S), 64, 0, stream>>>(g, pb, list, c);
+        else if (tier == 1) k_paths<1024, 1><<<pgrid(8192, S), 64, 0, stream>>>(g, pb, list, c);
+        else k_paths<4096, 1><<<pgrid(4096, S), 64, 0, stream>>>(g, pb, list, c);
       }
       // turn-cost winners (flag 5): the edge-state LDS search, 384 then 2048 states
       if (turn_modes != 0u) {
@@ -1453,8 +1462,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
                                                                        list, c);
           PathArgs pb = pa;
           pb.queue = pq + (3 + et) * kPQWords;
-          if (et == 0) k_paths_edge<384><<<4096, 64, 0, stream>>>(g, pb, d_turn, list, c, 6);
-          else k_paths_edge<2048><<<512, 64, 0, stream>>>(g, pb, d_turn, list, c, 3);
+          if (et == 0) k_paths_edge<384><<<pgrid(4096, S), 64, 0, stream>>>(g, pb, d_turn, list, c, 6);
+          else k_paths_edge<2048><<<pgrid(512, S), 64, 0, stream>>>(g, pb, d_turn, list, c, 3);
         }
       }
       // 64-bit labels, the largest-table overflows and what the edge tiers left: k_general
@@ -1477,7 +1486,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         ga.list_count = c;
         ga.flag = step_ovf;
         ga.counters = nullptr;
-        k_general<<<gs2.n, kGenThreads, 0, stream>>>(g, ga, gs2);
+        k_general<<<pgrid(gs2.n, S), kGenThreads, 0, stream>>>(g, ga, gs2);
       }
       // steps still flagged (beyond a 1M-state slab): named after the final sync
       k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0xAu, list, cnt + 18);

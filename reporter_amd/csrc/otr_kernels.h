@@ -1496,7 +1496,17 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   // ---- transition rows: re-read the step (cached) rather than hold it live through the search
   asm volatile("" ::: "memory");
   uint32_t ntr = 0;  // transition entries this search wrote (K4), for the work counters
-  if (have && (ok || forced)) {
+  if (have && forced && Kb > Gr::GL) {
+    // a step beyond the breakage distance with more targets than the group has lanes (a
+    // mode keeping > 32 candidates, G = 2): no route for any of them, written by stride
+    const uint4 r1 = trec[Gr::g()][1], r2 = trec[Gr::g()][2];
+    const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
+    uint32_t* trow = a.trans + (int64_t)(((uint64_t)r2.w << 32) | r2.z);
+    for (int q = 0; q < __popcll(mask); ++q) {  // (group-uniform)
+      const int i = nth_set_bit(mask, q);
+      for (int j = lane; j < Kb; j += Gr::GL) trow[(int64_t)i * Kb + j] = kNoRoute;
+    }
+  } else if (have && (ok || forced)) {
     const uint4 r0 = trec[Gr::g()][0], r1 = trec[Gr::g()][1], r2 = trec[Gr::g()][2];
     const int64_t s = r0.x;
     const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <cstdio>
@@ -202,6 +203,8 @@ void run_group(otr::Matcher& m, const std::vector<Item*>& items, std::vector<otr
 }
 
 }  // namespace
+
+void parallel(int n, const std::function<void(int)>& f) { parallel_for(n, f); }
 
 void stats(otr_service_split* out, bool reset) {
   std::lock_guard<std::mutex> lk(g_stats_mu);

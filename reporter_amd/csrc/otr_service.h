@@ -8,6 +8,7 @@
 // batch (report/transition levels, threshold, match_options overrides), matched in one
 // otr_match_batch per group, and formatted back on host threads.
 #pragma once
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -28,6 +29,8 @@ struct Item {
 void process(otr::Matcher& m, const std::vector<Item*>& items);
 // The host split of every process() call so far (otr_service_stats); reset: start over.
 void stats(otr_service_split* out, bool reset);
+// f(i) for i in [0, n) over the service's host threads
+void parallel(int n, const std::function<void(int)>& f);
 
 // Request coalescing across threads (otr_coalesce in include/otr.h).
 bool coalesce_enabled();

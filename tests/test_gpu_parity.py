@@ -94,3 +94,25 @@ def test_more_than_32_candidates(graph_dir, matcher):
     assert not errors, errors
     assert stats['n_seg'] > 0
     assert got['status'] == 0
+
+
+def test_forced_steps_more_than_32_candidates(graph_dir, matcher):
+    """A gap beyond the breakage distance (the trace jumps 3.3 km half-way: a forced
+    step, no route for any candidate pair) at states keeping more than 32 candidates: the
+    two-search first tier writes the step's no-route rows for every target, also those
+    beyond its 32-lane groups; bit-exact with the oracle."""
+    over = {'search_radius': 200, 'max_search_radius': 200, 'max_candidates': 64, 'turn_penalty_factor': 0}
+    path = gen.graph_path('metro', graph_dir)
+    M.configure(M.default_config(path, **over))
+    traces = gen.make_traces(path, 30, 60, 30, 30.0, 9, 0.0, 0.0, 50.0)
+    for t in range(traces.n_traces):  # the second half 0.03 deg (3.3 km) north
+        a, b = int(traces.offsets[t]), int(traces.offsets[t + 1])
+        traces.lat[(a + b) // 2:b] += 0.03
+    got = matcher.match_batch_numpy(traces)
+    assert int(np.max(got['cand_count'])) > 32
+    prm = po.params(**{k: float(v) for k, v in over.items()})
+    want = po.match_batch(po.Graph(path), traces, prm, threads=8)
+    errors, stats = compare(got, want)
+    assert not errors, errors
+    assert stats['n_seg'] > 0
+    assert got['status'] == 0
