@@ -210,15 +210,16 @@ typedef struct otr_batch_result {
   /* per route-search kernel: slot 0 the first tier (k_route<160,2>), 1..5 the LDS retry
    * tiers in order, 6 / 7 the global-memory search (32K / 1M-state slabs), 8 the 64-bit
    * label LDS tier (steps whose length and time bits exceed 32), 10 the first edge-state
-   * tier (modes with turn costs), 9 / 11 the larger edge-state tables (512, then 1024 states).
+   * tier (modes with turn costs), 9 / 11 the larger edge-state tables (512, then 1024 states),
+   * 12 the small-search first tier (k_route<80,4>: steps expected to stay small), 13..15 unused.
    * code: 6,000,000 + CAP*100 + targets of an edge-state tier, CAP*10+G of an LDS tier,
    * 900000 + CAP the 64-bit tier, -1 / -2 the global tiers, 0 unused (a tier with no task
    * kind to run: the node tiers when every mode has turn costs).
    * work: searches, settled nodes (expanded states), relaxed edges, transition entries
    * written.  ms (OTR_BATCH_TIMING): HIP-event time of the kernel on the matcher's stream. */
-  int32_t route_tier_code[12];
-  float route_tier_ms[12];
-  uint64_t route_tier_work[12][4];
+  int32_t route_tier_code[16];
+  float route_tier_ms[16];
+  uint64_t route_tier_work[16][4];
 } otr_batch_result;
 
 /* At most otr_max_batch_probes() = 2^26 - 64 (67,108,800) probes per call

@@ -111,8 +111,8 @@ class BatchResult(ctypes.Structure):
                 ('stats_len', P(ctypes.c_double)), ('d_hist', ctypes.c_void_p), ('hist_len', ctypes.c_int64),
                 ('counters', ctypes.c_uint64 * 24), ('kernel_ms', ctypes.c_float * 16),
                 ('trace_status', P(ctypes.c_int32)), ('d_rows', ctypes.c_void_p),
-                ('route_tier_code', ctypes.c_int32 * 12), ('route_tier_ms', ctypes.c_float * 12),
-                ('route_tier_work', (ctypes.c_uint64 * 4) * 12)]
+                ('route_tier_code', ctypes.c_int32 * 16), ('route_tier_ms', ctypes.c_float * 16),
+                ('route_tier_work', (ctypes.c_uint64 * 4) * 16)]
 
 
 # otr_hist_entry (include/otr.h), 32 bytes

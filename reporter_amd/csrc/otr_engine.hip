@@ -391,7 +391,7 @@ enum Slot {
   S_TRACE_OFF, S_LAT, S_LON, S_TIME, S_ACC, S_MODE,
   S_STATE_CNT, S_TRACE_STATE_OFF, S_STATE_PROBE, S_STATE_TRACE,
   S_CAND_EDGE, S_CAND_P, S_CAND_SQD, S_CAND_COUNT, S_CAND_RADIUS,
-  S_PREV, S_G, S_BOUND, S_FORCED, S_NTASK, S_NTRANS, S_TASK_OFF, S_TRANS_OFF, S_NUNIT, S_UNIT_OFF, S_UNIT,
+  S_PREV, S_G, S_BOUND, S_FORCED, S_NTASK, S_NTRANS, S_TASK_OFF, S_TRANS_OFF, S_NTASK4, S_TASK4_OFF, S_UNIT,
   S_TASK_STATE, S_TASK_MASK, S_TASK_OVF, S_TRANS,
   S_BP, S_BRK, S_END_WIN, S_WINNER, S_SUBPATH,
   S_PATH_OFF, S_PATH_LEN, S_PATH, S_STEP_OVF,
@@ -409,7 +409,7 @@ enum Slot {
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
   S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST, S_HE_PKEY, S_QUEUE, S_PQUEUE,
-  S_E1DUMP0, S_E1DUMP1, S_TASK_DUMP, S_NDUMP0, S_NDUMP1, S_SORT_LIST, S_SORT_HIST,
+  S_E1DUMP0, S_E1DUMP1, S_TASK_DUMP, S_NDUMP0, S_NDUMP1, S_SORT_LIST, S_SORT_HIST, S_EREC_TC,
   S_NUM
 };
 
@@ -435,6 +435,7 @@ T* Matcher::need(int slot, size_t n) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
+    if (slot == S_EREC_TC) tc_valid = false;  // (its contents are built once per graph and turn tables)
     size_t nb = bytes + bytes / 4;
     bool ok = hipMalloc(&b.p, nb) == hipSuccess || hipMalloc(&b.p, bytes) == hipSuccess;
     if (!ok && !optional_slot(slot) && release_optional()) {
@@ -665,11 +666,55 @@ __global__ void k_collect_tier_list(const unsigned long long* n_in, int32_t* fla
   block_append(sel, i, list, count);
 }
 
+// per edge-state slot and turn mode: {route time, turn cost mm} (the turn degree the record
+// carries looked up in the mode's table; an unused slot's degree may be out of range: 0)
+__global__ void k_erec_tc(const uint4* erec, const uint32_t* erec_t, size_t es, const int32_t* turn,
+                          uint32_t turn_modes, uint2* out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= es) return;
+  const uint32_t deg = erec[i].z & 0xFFu;
+  for (int m = 0; m < OTR_MODES; ++m)
+    if ((turn_modes >> m) & 1u)
+      out[es * m + i] = make_uint2(erec_t[es * m + i], deg <= 180u ? (uint32_t)turn[181 * m + deg] : 0u);
+}
+
 // states that need a path: a step inside a sub-path
 __global__ void k_step_list(int64_t n_states, const int64_t* prev, const uint8_t* brk, const int32_t* cand_count,
                             int64_t* list, unsigned long long* count) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   block_append(s < n_states && cand_count[s] > 0 && prev[s] >= 0 && !brk[s], s, list, count);
+}
+
+// the same steps in two lists within list[0, n_states): the small-search path tier's from
+// the front (count_front), the rest from the back (count_back); *n_all = n_states (the
+// retry collects scan the whole index range, whose gap keeps its zero flags)
+__global__ void k_step_lists(int64_t n_states, const int64_t* prev, const uint8_t* brk, const int32_t* cand_count,
+                             PathClass pc, int64_t* list, unsigned long long* count_front,
+                             unsigned long long* count_back, unsigned long long* n_all) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s == 0) *n_all = (unsigned long long)n_states;
+  const bool hit = s < n_states && cand_count[s] > 0 && prev[s] >= 0 && !brk[s];
+  bool small = false;
+  if (hit) {
+    const int64_t sp = prev[s];
+    const int md = pc.mode[pc.state_trace[s]] < OTR_MODES ? pc.mode[pc.state_trace[s]] : 0;
+    const uint32_t r = pc.trans[pc.trans_off[s] + (int64_t)pc.winner[sp] * cand_count[s] + pc.winner[s]];
+    const double b = fmin(floor(pc.bound[s] * 1000.0), (double)r) * 1e-3;  // (k_paths' bound, m)
+    small = !((pc.turn_modes >> md) & 1u) && pc.est4 * (float)(b * b) <= pc.small_keys;
+  }
+  // one atomic per wave and list
+  const unsigned long long mf = __ballot(hit && small), mb = __ballot(hit && !small);
+  const int lane = (int)(threadIdx.x % OTR_WAVE);
+  unsigned long long bf = 0, bb = 0;
+  if (lane == 0) {
+    if (mf) bf = atomicAdd(count_front, (unsigned long long)__popcll(mf));
+    if (mb) bb = atomicAdd(count_back, (unsigned long long)__popcll(mb));
+  }
+  bf = __shfl(bf, 0);
+  bb = __shfl(bb, 0);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  if (hit && small) list[bf + __popcll(mf & below)] = s;
+  if (hit && !small) list[n_states - 1 - (int64_t)(bb + __popcll(mb & below))] = s;
 }
 
 // work counters: fold the kCShards shards of every (bank, kind) into one value before the
@@ -695,6 +740,11 @@ static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + b
 // tier before the 4096 one (2.5x its occupancy): C4 4.57M -> 4.79M probes/s.  The last tier is always the 4096-slot one (its
 // overflows are per-trace errors).  OTR_TIERS overrides the list for A/B runs, e.g.
 // "256,512x2,1024,4096".
+// the small-search tier's default size limit (keys of k_ntask's estimate; OTR_SMALL_KEYS)
+constexpr double kSmallKeys = 24.0;
+// the small-search path tier's (keys of k_step_lists' estimate; OTR_SMALL_PATH_KEYS)
+constexpr double kSmallPathKeys = 16.0;
+
 static std::vector<int> route_tiers() {
   std::vector<int> t;
   const char* env = getenv("OTR_TIERS");
@@ -816,9 +866,10 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   h_trace_status.assign(T, OTR_OK);
   // counter banks of OTR_COUNTERS kinds x kCShards: 0 the batch (and the first route
   // tier), 1 the 512-state edge tier, 2..6 the LDS retry tiers, 7 the 64-bit tier, 8..9 the
-  // global-memory tiers, 10 the first edge tier, 11 the 1024-state edge tier; folded at
+  // global-memory tiers, 10 the first edge tier, 11 the 1024-state edge tier, 12 the
+  // small-search first tier; folded at
   // the end into n_ctr values behind them
-  constexpr int kBanks = 12;
+  constexpr int kBanks = 13;
   const size_t bank = (size_t)OTR_COUNTERS * kCShards;
   const size_t n_ctr = kBanks * (size_t)OTR_COUNTERS;
   unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, kBanks * bank + n_ctr);
@@ -914,34 +965,17 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     if (k32) k_prep<2><<<(unsigned)grid_per_state_waves(S, 2).blocks, 256, 0, stream>>>(g, pr);
     else k_prep<1><<<(unsigned)grid_per_state_waves(S, 1).blocks, 256, 0, stream>>>(g, pr);
   }
-  // the step's task count: the distinct roots (k_prep) of the previous state's candidates
-  if (S > 0) k_ntask<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, pr.nroot, sb.ntask);
-  if ((rc = scan(sb.ntask, task_off, S))) return rc;
-  if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
-  int64_t NT = 0, NTR = 0;
-  HIPCHK(hipMemcpyAsync(&NT, task_off + S, 8, hipMemcpyDeviceToHost, stream));
-  HIPCHK(hipMemcpyAsync(&NTR, trans_off + S, 8, hipMemcpyDeviceToHost, stream));
-  HIPCHK(hipStreamSynchronize(stream));
-  int64_t* task_state = need<int64_t>(S_TASK_STATE, NT);
-  unsigned long long* task_mask = need<unsigned long long>(S_TASK_MASK, NT);
-  int32_t* task_ovf = need<int32_t>(S_TASK_OVF, NT);
-  uint32_t* trans = need<uint32_t>(S_TRANS, NTR);
-  uint32_t* trans_tc = need<uint32_t>(S_TRANS_TC, turn_modes ? NTR : 1);  // read for turn modes only
-  uint4* task_rec = need<uint4>(S_TASK_REC, 3 * (size_t)std::max<int64_t>(NT, 1));
-  if (!task_state || !task_mask || !task_ovf || !trans || !trans_tc || !task_rec) {
-    if (err) *err = "device allocation failed (transitions)";
-    return OTR_DEVICE_ERROR;
-  }
-  // the first tier's size estimate (k_tasks, for route_unit): an exact search runs to its
-  // bounds unless its targets resolve first, so its keys grow with the area it can reach,
-  // est = c * density * reach^2, reach = min(length bound, time bound x 50 km/h capped by
-  // the mode's speed).  A search whose estimate exceeds the first tier's table starts in the
-  // retry tier that holds it: k_tasks flags it and the first tier passes it on without
-  // loading its step.  c = 0.5 (C4's 60 s steps reach ~1.7 km and start in the
+  // the first tier's size estimate (k_ntask, k_tasks, for route_unit): an exact search runs
+  // to its bounds unless its targets resolve first, so its keys grow with the area it can
+  // reach, est = c * density * reach^2, reach = min(length bound, time bound x 50 km/h
+  // capped by the mode's speed).  A search whose estimate exceeds the first tier's table
+  // starts in the retry tier that holds it: k_tasks flags it and the first tier passes it
+  // on without loading its step.  c = 0.5 (C4's 60 s steps reach ~1.7 km and start in the
   // 1024-slot tier: C4 1.69M -> 2.47M probes/s; c = 1.7, the full-exhaustion fit of C2,
   // sent them to the 4096 tier, 1.07M; C2's 15 s steps stay in the first tier either way,
   // profiles/r03_est_*).  OTR_EST_K scales c (A/B knob; 0 = every search starts in the
-  // first tier).
+  // first tier).  A step whose estimate is at most OTR_SMALL_KEYS keys (and has at most
+  // 16 targets) goes to the small-search tier, four searches per wave (k_ntask).
   static const int route_g = getenv("OTR_ROUTE_G") ? atoi(getenv("OTR_ROUTE_G")) : 2;  // A/B knob
   float est_k = 0.f, est_v[OTR_MODES];
   uint32_t est_tier_keys[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
@@ -959,6 +993,49 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     static const std::vector<int> tl = route_tiers();
     n_est_tiers = (int)std::min<size_t>(tl.size(), 8);
     for (int t = 0; t < n_est_tiers; ++t) est_tier_keys[t] = (uint32_t)((tl[t] / 10) * 7 / 8);
+  }
+  static const double small_keys = getenv("OTR_SMALL_KEYS") ? atof(getenv("OTR_SMALL_KEYS")) : kSmallKeys;  // A/B knob
+  const bool small_tier = route_g == 2 && k32 && small_keys > 0.0 && est_k > 0.f;
+  int64_t* ntask4 = small_tier ? need<int64_t>(S_NTASK4, S) : nullptr;
+  int64_t* task4_off = small_tier ? need<int64_t>(S_TASK4_OFF, S + 1) : nullptr;
+  if (small_tier && (!ntask4 || !task4_off)) {
+    if (err) *err = "device allocation failed (task map)";
+    return OTR_DEVICE_ERROR;
+  }
+  // the step's task count: the distinct roots (k_prep) of the previous state's candidates
+  if (S > 0) {
+    SmallArgs sa{};
+    sa.ntask4 = ntask4;
+    sa.bound = sb.bound;
+    sa.bt = sb.bt;
+    sa.forced = sb.forced;
+    sa.cand_count = cb.count;
+    sa.state_trace = state_trace;
+    sa.mode = b.mode;
+    sa.turn_modes = turn_modes;
+    sa.est_k = est_k;
+    for (int m = 0; m < OTR_MODES; ++m) sa.est_v[m] = est_v[m];
+    sa.small_keys = (float)small_keys;
+    k_ntask<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, pr.nroot, sb.ntask, sa);
+  }
+  if ((rc = scan(sb.ntask, task_off, S))) return rc;
+  if (small_tier && (rc = scan(ntask4, task4_off, S))) return rc;
+  if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
+  int64_t NT = 0, NTR = 0, NT4 = 0;  // NT: every task; [0, NT4) the small tier's
+  HIPCHK(hipMemcpyAsync(&NT, task_off + S, 8, hipMemcpyDeviceToHost, stream));
+  if (small_tier) HIPCHK(hipMemcpyAsync(&NT4, task4_off + S, 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(&NTR, trans_off + S, 8, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  NT += NT4;
+  int64_t* task_state = need<int64_t>(S_TASK_STATE, NT);
+  unsigned long long* task_mask = need<unsigned long long>(S_TASK_MASK, NT);
+  int32_t* task_ovf = need<int32_t>(S_TASK_OVF, NT);
+  uint32_t* trans = need<uint32_t>(S_TRANS, NTR);
+  uint32_t* trans_tc = need<uint32_t>(S_TRANS_TC, turn_modes ? NTR : 1);  // read for turn modes only
+  uint4* task_rec = need<uint4>(S_TASK_REC, 3 * (size_t)std::max<int64_t>(NT, 1));
+  if (!task_state || !task_mask || !task_ovf || !trans || !trans_tc || !task_rec) {
+    if (err) *err = "device allocation failed (transitions)";
+    return OTR_DEVICE_ERROR;
   }
   if (S > 0) {  // tasks and their records (K2 + K2c)
     TaskArgs ta{};
@@ -980,6 +1057,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     ta.task_state = task_state;
     ta.task_mask = task_mask;
     ta.rec = task_rec;
+    ta.ntask4 = ntask4;
+    ta.task4_off = task4_off;
+    ta.nt4 = NT4;
     ta.flag_turn = task_ovf;  // turn-mode tasks start in the first edge-state tier (flag 5)
     // the two-search first tier's table: a step expected beyond it is flagged here
     ta.est_first_keys = route_g == 2 ? (OTR_CAP1 * OTR_LOAD1) / 8 : 0;
@@ -997,6 +1077,21 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   h_turn.resize(181 * OTR_MODES);
   for (int m = 0; m < OTR_MODES; ++m) turn_table(mp.m[m].turn_penalty_factor, h_turn.data() + 181 * m);
   HIPCHK(hipMemcpyAsync(d_turn, h_turn.data(), 4 * 181 * OTR_MODES, hipMemcpyHostToDevice, stream));
+  // the edge-state tiers' per-slot {route time, turn cost} of this batch's turn tables
+  // (otr_edge1.h: a relaxation loads its turn cost beside the record, no turn table in LDS),
+  // built when the graph or a turn mode's table changed (a configuration's first batch)
+  uint2* erec_tc = nullptr;
+  if (turn_modes != 0u && NT > 0) {
+    erec_tc = need<uint2>(S_EREC_TC, g.erec_stride * OTR_MODES);
+    if (!tc_valid || tc_graph != (const void*)g.erec || tc_modes != turn_modes || tc_turn != h_turn) {
+      k_erec_tc<<<grid_for((int64_t)g.erec_stride, 256), 256, 0, stream>>>(g.erec, g.erec_t, g.erec_stride, d_turn,
+                                                                           turn_modes, erec_tc);
+      tc_valid = true;
+      tc_graph = (const void*)g.erec;
+      tc_modes = turn_modes;
+      tc_turn = h_turn;
+    }
+  }
   // ---- K3/K4: routing + transition costs
   RouteArgs ra{};
   ra.task_state = task_state;
@@ -1016,6 +1111,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ra.mode = b.mode;
   ra.bt = sb.bt;
   ra.turn = d_turn;
+  ra.erec_tc = erec_tc;
   ra.trans_tc = trans_tc;
   ra.cprep = pr.cprep;
   ra.cprep_t = pr.cprep_t;
@@ -1154,12 +1250,29 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     tb(OTR_STAGE_ROUTE);
     if (node_tasks) {
       // one unit (G searches) per block, in launches of at most 2^25 blocks: a dispatch's
-      // grid size counts work-items in 32 bits (178M tasks at 12.5M probes would wrap)
-      const int64_t units = route_g == 2 ? (NT + 1) / 2 : NT;
+      // grid size counts work-items in 32 bits (178M tasks at 12.5M probes would wrap).
+      // The small tier (four searches per wave, tasks [0, NT4)) first, then the two-search
+      // tier over the rest
       constexpr int64_t kMaxUnits = 1ll << 25;
+      if (NT4 > 0) {
+        unsigned long long* rc4 = rwork ? d_counters + 12 * bank : nullptr;
+        if (timing) (void)hipEventRecord(ev[24 + 2 * 12], stream);
+        const int64_t units = (NT4 + 3) / 4;
+        for (int64_t base = 0; base < units; base += kMaxUnits) {
+          RouteArgs rf = ra;
+          rf.n_tasks = NT4;
+          rf.unit_base = base;
+          const int64_t u = std::min<int64_t>(kMaxUnits, units - base);
+          OTR_ROUTE_LAUNCH(OTR_CAP4, 4, false, (unsigned)(8 * ((u + 7) / 8)), rf, rc4);
+        }
+        if (timing) (void)hipEventRecord(ev[24 + 2 * 12 + 1], stream);
+        out->route_tier_code[12] = OTR_CAP4 * 10 + 4;
+      }
+      const int64_t units = route_g == 2 ? (NT - NT4 + 1) / 2 : NT;
       for (int64_t base = 0; base < units; base += kMaxUnits) {
         RouteArgs rf = ra;
         rf.unit_base = base;
+        rf.task_base = NT4;
         const int64_t u = std::min<int64_t>(kMaxUnits, units - base);
         const unsigned grid = (unsigned)(8 * ((u + 7) / 8));
         if (route_g == 2) OTR_ROUTE_LAUNCH(OTR_CAP1, 2, false, grid, rf, rwork);
@@ -1392,7 +1505,34 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   {
     int64_t* steps = need<int64_t>(S_LIST2, std::max<int64_t>(S, 1));
     unsigned long long* nsteps_d = cnt + 11;
-    if (S > 0) k_step_list<<<grid_for(S, 1024), 1024, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, nsteps_d);
+    // the small-search path tier (four searches per wave): steps whose winning route
+    // bounds a search of at most OTR_SMALL_PATH_KEYS keys (estimate: 4 x the node density
+    // x r^2, the diamond of road distance r around the root and its frontier); the
+    // two-search tier takes the rest
+    static const double small_path_keys =
+        getenv("OTR_SMALL_PATH_KEYS") ? atof(getenv("OTR_SMALL_PATH_KEYS")) : kSmallPathKeys;  // A/B knob
+    const bool small_paths = small_path_keys > 0.0 && est_k > 0.f;
+    unsigned long long* nsteps4_d = cnt + 21;  // (the front list's count)
+    unsigned long long* nall_d = cnt + 22;     // (S: the collects' index range)
+    if (S > 0 && small_paths) {
+      PathClass pc{};
+      pc.winner = va.winner;
+      pc.trans_off = trans_off;
+      pc.trans = trans;
+      pc.bound = sb.bound;
+      pc.state_trace = state_trace;
+      pc.mode = b.mode;
+      pc.turn_modes = turn_modes;
+      pc.est4 = 8.f * est_k;  // (est_k = half the node density)
+      pc.small_keys = (float)small_path_keys;
+      HIPCHK(hipMemsetAsync(nsteps4_d, 0, 16, stream));
+      k_step_lists<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, va.brk, cb.count, pc, steps, nsteps4_d, nsteps_d,
+                                                          nall_d);
+    } else if (S > 0) {
+      k_step_list<<<grid_for(S, 1024), 1024, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, nsteps_d);
+    }
+    // the retry collects' index range: every step index (front and back lists), or the list
+    const unsigned long long* nscan_d = small_paths ? nall_d : nsteps_d;
     int32_t* step_ovf = need<int32_t>(S_STEP_OVF, S + 1);
     int64_t capacity = kShards * ((int64_t)S * 24 / kShards + 1024);
     bool paths_fit = S == 0;
@@ -1434,7 +1574,16 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       pa.trans = trans;
       pa.force_edge = ra.force_edge;
       tb(OTR_STAGE_PATHS);
-      {
+      if (small_paths) {
+        // the front list four searches per wave, the back list two (grids for S steps each:
+        // blocks past a list's device count exit at once)
+        PathArgs p4 = pa;
+        p4.n_steps_dev = nsteps4_d;
+        k_paths<OTR_CAP4, 4><<<(unsigned)(8 * ((S + 31) / 32)), 64, 0, stream>>>(g, p4, nullptr, nullptr);
+        PathArgs p2 = pa;
+        p2.from_back = true;
+        k_paths<OTR_CAP1, 2><<<(unsigned)grid_paths(S).blocks, 64, 0, stream>>>(g, p2, nullptr, nullptr);
+      } else {
         // (steps <= states: two searches per wave)
         k_paths<OTR_CAP1, 2><<<(unsigned)grid_paths(S).blocks, 64, 0, stream>>>(g, pa, nullptr, nullptr);
       }
@@ -1447,7 +1596,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       HIPCHK(hipMemsetAsync(pq, 0, 8 * 8 * kPQWords, stream));
       for (int tier = 0; tier < 3; ++tier) {
         unsigned long long* c = cnt + 12 + tier;
-        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0x2u, list, c);
+        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, 0x2u, list, c);
         PathArgs pb = pa;
         pb.queue = pq + tier * kPQWords;
         if (tier == 0) k_paths<512, 1><<<pgrid(16384, S), 64, 0, stream>>>(g, pb, list, c);
@@ -1458,7 +1607,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       if (turn_modes != 0u) {
         for (int et = 0; et < 2; ++et) {
           unsigned long long* c = cnt + 27 + et;
-          k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, et == 0 ? 0x20u : 0x40u,
+          k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, et == 0 ? 0x20u : 0x40u,
                                                                        list, c);
           PathArgs pb = pa;
           pb.queue = pq + (3 + et) * kPQWords;
@@ -1477,7 +1626,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       ga.cap_flag = (int32_t*)(cnt + 20);
       for (int gt = 0; gt < 2; ++gt) {
         unsigned long long* c = cnt + 16 + gt;
-        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, gt == 0 ? 0xAu : 0x2u, list,
+        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, gt == 0 ? 0xAu : 0x2u, list,
                                                                      c);
         GSlabs gs2;
         if ((rc = slabs(gt, &gs2))) return rc;
@@ -1489,7 +1638,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         k_general<<<pgrid(gs2.n, S), kGenThreads, 0, stream>>>(g, ga, gs2);
       }
       // steps still flagged (beyond a 1M-state slab): named after the final sync
-      k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0xAu, list, cnt + 18);
+      k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, 0xAu, list, cnt + 18);
       te(OTR_STAGE_PATHS_BIG);
       unsigned long long capflag = 0;
       std::vector<unsigned long long> cur(kShards);
@@ -1689,10 +1838,11 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     return hc[(size_t)b * OTR_COUNTERS + (size_t)k];
   };
   for (int k = 0; k < OTR_COUNTERS; ++k) out->counters[k] = ctr(0, k);
+  for (int k : {3, 4, 13, 14}) out->counters[k] += ctr(12, k);  // (the first tier: both launches)
   // per route kernel: searches, settled, relaxed, transition entries (banks 0, 2..6, 8..9;
   // slot 8, the 64-bit LDS tier: bank 7; the edge-state tiers: slot 10 the first (bank 10),
   // slot 9 the 512-state one (bank 1), slot 11 the 1024-state one (bank 11))
-  for (int t = 0; t < 12; ++t) {
+  for (int t = 0; t < 13; ++t) {
     const int b = t == 0 ? 0 : (t < 6 ? 1 + t : (t < 8 ? 2 + t : (t == 8 ? 7 : (t == 9 ? 1 : t))));
     out->route_tier_work[t][0] = ctr(b, 6);
     out->route_tier_work[t][1] = ctr(b, 3);
@@ -1722,10 +1872,11 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   if (timing) {
     for (int k = 0; k < 10; ++k)
       if (used[k]) (void)hipEventElapsedTime(&out->kernel_ms[k], ev[2 * k], ev[2 * k + 1]);
-    out->route_tier_ms[0] = out->kernel_ms[OTR_STAGE_ROUTE];
-    for (int t = 1; t < 12; ++t)
+    for (int t = 1; t < 13; ++t)
       if (out->route_tier_code[t] != 0)
         (void)hipEventElapsedTime(&out->route_tier_ms[t], ev[24 + 2 * t], ev[24 + 2 * t + 1]);
+    // (the route stage holds the small tier's launches, then the two-search tier's)
+    out->route_tier_ms[0] = out->kernel_ms[OTR_STAGE_ROUTE] - out->route_tier_ms[12];
     (void)hipGetLastError();  // an unrecorded pair must not leave a sticky error for the next call
   }
   // ---- copy-out (tests / JSON path), compacting the capacity layout

@@ -458,7 +458,7 @@ __device__ inline uint32_t wave_min_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-// G independent searches per wave, GL = 64 / G lanes each (G = 1 or 2).  Per-group
+// G independent searches per wave, GL = 64 / G lanes each (G = 1, 2 or 4).  Per-group
 // ballots, prefix counts, minima and wave-uniform loop bounds.
 template <int G>
 struct Grp {
@@ -477,12 +477,17 @@ struct Grp {
   // maximum over groups of a group-uniform value (a wave-uniform loop bound)
   __device__ static int umax(int v) {
     if (G == 1) return __builtin_amdgcn_readfirstlane(v);
-    const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 32);
-    return a > b ? a : b;
+    const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, GL);
+    if (G == 2) return a > b ? a : b;
+    const int c = __builtin_amdgcn_readlane(v, 2 * GL), d = __builtin_amdgcn_readlane(v, 3 * GL);
+    const int ab = a > b ? a : b, cd = c > d ? c : d;
+    return ab > cd ? ab : cd;
   }
   __device__ static bool all(bool v) {
     if (G == 1) return __builtin_amdgcn_readfirstlane((int)v) != 0;
-    return __builtin_amdgcn_readlane((int)v, 0) != 0 && __builtin_amdgcn_readlane((int)v, 32) != 0;
+    const bool ab = __builtin_amdgcn_readlane((int)v, 0) != 0 && __builtin_amdgcn_readlane((int)v, GL) != 0;
+    if (G == 2) return ab;
+    return ab && __builtin_amdgcn_readlane((int)v, 2 * GL) != 0 && __builtin_amdgcn_readlane((int)v, 3 * GL) != 0;
   }
   __device__ static uint32_t min_u32(uint32_t v) {
     if (G == 1) return wave_min_u32(v);
@@ -492,6 +497,14 @@ struct Grp {
     v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
     v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
     v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    if (G == 4) {  // a group is one DPP row: lane 15 of the row holds its minimum
+      const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+      const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+      const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+      const int q = g();
+      return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
+    }
     v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
     const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
     const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
@@ -563,7 +576,8 @@ struct SearchLds {
   using Idx = typename std::conditional<(CAP <= 256 && !PRED), uint8_t, uint16_t>::type;
   // nodes settled per round (at most); k_paths (PRED) reuses pend + work as CAP u32 words
   // (1024 slots: 120, the 1-B codes' table then fits 13 waves per CU's LDS)
-  static constexpr int WCAP = CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : (CAP <= 1024 ? 120 : 128)));
+  // (the small tier's 80-slot tables: 16, so four tables fit 32 waves per CU: 4.5 KB per wave)
+  static constexpr int WCAP = CAP <= 96 ? (PRED ? 20 : 16) : CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : (CAP <= 1024 ? 120 : 128)));
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
   WorkE<W> work[WCAP];                // this round's settled nodes: {node, label}
   int n_pend, n_keys, overflow;
@@ -687,6 +701,10 @@ __host__ __device__ inline bool pack_fits(uint32_t bmm, uint32_t sh) {
 // final; if even min(L(T), kmin + minin(T)) cannot make L + tpart fit the relative bound
 // pd (= B - the sources' smallest exit part), T is unreachable for every source.
 // (branch-free: the slot's words are read unconditionally, slot 0 for a lane without one)
+// Measured and dropped: a time rule (T unreachable once it has no feasible
+// label and the smallest pending time + its entry time breaks the time bound) settled
+// 3.2 % fewer nodes at C2 and made the first tier 2.5 % slower (the per-round minimum,
+// six more registers).
 template <int CAP, int LM>
 __device__ inline bool target_resolved(const SearchLds<CAP, LM>& L, const Pack& K, int tslot, uint32_t tpart,
                                        uint32_t gapT, uint32_t pd, uint32_t kmin, bool pend_empty) {
@@ -1161,12 +1179,53 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
   if (lane == 0) a.nroot[s] = nr;
 }
 
-// search tasks of each step: one per distinct root among the previous state's candidates
-__global__ void k_ntask(int64_t n_states, const int64_t* prev, const int32_t* nroot, int64_t* ntask) {
+// the small-search first tier (k_route<OTR_CAP4, 4>): which steps' tasks it takes
+// (SmallArgs::ntask4 null: none, every task in the two-search tier)
+#ifndef OTR_CAP4
+#define OTR_CAP4 80
+#endif
+struct SmallArgs {
+  int64_t* ntask4;            // per state: the step's tasks when they go to the small tier, else 0
+  const double* bound;
+  const int32_t* bt;
+  const uint8_t* forced;
+  const int32_t* cand_count;
+  const int32_t* state_trace;
+  const uint8_t* mode;
+  uint32_t turn_modes;
+  float est_k;                // k_tasks' size estimate (keys = est_k * reach^2)
+  float est_v[OTR_MODES];
+  float small_keys;           // a step whose estimate is at most this many keys is small
+};
+
+// search tasks of each step: one per distinct root among the previous state's candidates.
+// With the small tier on, a step goes to it (ntask4) or to the two-search tier (ntask):
+// node mode, 32-bit labels, not forced, at most 16 targets (a lane group of 16) and a
+// size estimate (k_tasks' rule) of at most small_keys keys; the two classes get separate
+// task ranges (small first), so each first-tier kernel runs over a contiguous range.
+__global__ void k_ntask(int64_t n_states, const int64_t* prev, const int32_t* nroot, int64_t* ntask, SmallArgs sa) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_states) return;
   const int64_t sp = prev[s];  // -1: first state of a sub-trace, -2: no candidates (k_link)
-  ntask[s] = sp >= 0 ? nroot[sp] : 0;
+  const int64_t n = sp >= 0 ? nroot[sp] : 0;
+  bool small = false;
+  if (sa.ntask4 != nullptr && n > 0 && sa.cand_count[s] <= OTR_WAVE / 4 && !sa.forced[s]) {
+    const int md = sa.mode[sa.state_trace[s]] < OTR_MODES ? sa.mode[sa.state_trace[s]] : 0;
+    const uint32_t bmm = (uint32_t)bound_mm_of(sa.bound[s]);
+    const int32_t bt = sa.bt[s];
+#ifdef OTR_FORCE_GENERAL
+    const bool general = true;  // (test build: every search in k_general)
+#else
+    const bool general = !pack_fits(bmm, pack_shift(bt)) || ((sa.turn_modes >> md) & 1u);
+#endif
+    if (!general) {
+      float reach = (float)bmm * 1e-3f;
+      if (bt >= 0) reach = fminf(reach, (float)bt * 0.1f * sa.est_v[md]);
+      small = sa.est_k * reach * reach <= sa.small_keys;
+    }
+  }
+  if (sa.ntask4 != nullptr) sa.ntask4[s] = small ? n : 0;
+  ntask[s] = small ? 0 : n;
 }
 
 // ------------------------------------------------------------------------------
@@ -1196,6 +1255,8 @@ struct RouteArgs {
   const uint4* rec;           // per task, 3 x uint4 (k_tasks)
   const unsigned long long* list_count;  // retry tiers: length of task_list, on the device
   const int32_t* turn;        // [OTR_MODES][181] turn cost tables (mm), turn modes only
+  const uint2* erec_tc;       // [OTR_MODES][DevGraph::erec_stride]: per edge-state slot {route time, turn
+                              // cost mm} of the turn modes (the edge-state tiers, otr_edge1.h)
   uint32_t* trans_tc;         // turn cost (mm) per transition, turn modes only
   double inv_beta[OTR_MODES];
   int32_t* overflow_flag;     // per task: 1/2 retry in a larger LDS table, 3 the global-memory search,
@@ -1208,6 +1269,7 @@ struct RouteArgs {
   uint32_t tier_keys[8];      // key capacity of each retry tier, in order
   int n_tiers;
   int64_t unit_base;          // first tier: the launch's first unit (launches of < 2^32 work-items)
+  int64_t task_base;          // first tier: its first task (the small tier's tasks come first)
   unsigned long long* queue;  // list tiers: this launch's 8 per-XCD unit counters (XcdQueue), zeroed
   unsigned long long* stamps;  // diagnostic build (OTR_STAMPS): bank 0 of the work counters (phase cycles)
   int force_edge;             // test build only (OTR_FORCE_RETRY, env OTR_FORCE_EDGE): bits 0 / 1 / 2 fail
@@ -1247,6 +1309,9 @@ struct TaskArgs {
   int64_t* task_state;
   unsigned long long* task_mask;
   uint4* rec;                 // 3 per task (the K2c record, below)
+  const int64_t* ntask4;      // small-tier steps' task counts (k_ntask), or null
+  const int64_t* task4_off;   // their exclusive offsets: small-tier tasks are [0, nt4)
+  int64_t nt4;                // two-search tasks are nt4 + task_off[s]
   int32_t* flag_turn;         // per task: 5 for a turn-mode task (the first edge-state tier's list), or null
   // the two-search first tier's size estimate (RouteArgs est_*): a node-mode step whose
   // estimated keys exceed est_first_keys (0: no estimate) starts in a retry tier
@@ -1304,8 +1369,12 @@ __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
   const bool rep = lane < Ka && (__ffsll((long long)same) - 1) == lane;
   const unsigned long long reps = group_bits<G>(__ballot(rep));
   if (!rep) return;
-  const int64_t o = a.task_off[s] + __popcll(reps & ((1ull << lane) - 1ull));
-  if (o >= a.task_off[s + 1]) return;  // the count (k_prep's nroot) and this rule agree; never write past it
+  // the step's task range: the small tier's first, then the two-search tier's (k_ntask)
+  const int64_t n4 = a.ntask4 != nullptr ? a.ntask4[s] : 0;
+  const int64_t tbase = n4 > 0 ? a.task4_off[s] : a.nt4 + a.task_off[s];
+  const int64_t tend = n4 > 0 ? tbase + n4 : a.nt4 + a.task_off[s + 1];
+  const int64_t o = tbase + __popcll(reps & ((1ull << lane) - 1ull));
+  if (o >= tend) return;  // the count (k_prep's nroot) and this rule agree; never write past it
   a.task_state[o] = s;
   a.task_mask[o] = same;
   const uint32_t bmm = (uint32_t)bound_mm_of(a.bound[s]);
@@ -1364,7 +1433,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
   constexpr int LM = WIDE ? 2 : 0;
   using Gr = Grp<G>;
   const int lane = Gr::gl();
-  const int64_t tw = w * G + Gr::g();
+  const int64_t tw = (LIST ? 0 : a.task_base) + w * G + Gr::g();
   const bool have = tw < n_tasks;
   const int64_t task = have ? (LIST ? a.task_list[tw] : tw) : 0;
   OTR_STAMP(ts_in);
@@ -1396,7 +1465,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
     // the tasks whose packed words need 64 bits to the WIDE tier
     fits = Kb <= Gr::GL && (WIDE || !general) && !((r1.y >> 17) & 1u);
     // a step too big for this table starts in a retry tier (k_tasks' estimate): no load of it
-    const bool pre = G == 2 && !LIST && have && ((r1.y >> 18) & 1u);
+    const bool pre = G >= 2 && !LIST && have && ((r1.y >> 18) & 1u);
     if (pre) {
       start_tier = (int)((r1.y >> 19) & 7u);
       fits = false;
@@ -1484,7 +1553,7 @@ __device__ __forceinline__ void route_unit(const DevGraph& gr, const RouteArgs& 
                                    kDumps ? &nd : nullptr, kDumps ? &dslot : nullptr) &&
             fits;
 #ifdef OTR_FORCE_RETRY
-  if (G == 2 && !LIST) ok = false;  // test build: every first-tier task takes the retry tiers
+  if (G >= 2 && !LIST) ok = false;  // test build: every first-tier task takes the retry tiers
 #endif
   OTR_STAMP(ts_srch);
   SearchLds<CAP, LM>& L = Ls[Gr::g()];
@@ -1641,7 +1710,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR
   uint32_t* sink = WIDE ? nullptr : sink_row;
 #endif
   if (!LIST) {
-    const int64_t n_units = (a.n_tasks + G - 1) / G;
+    const int64_t n_units = (a.n_tasks - a.task_base + G - 1) / G;
     // the first tier (task-major; the default is k_route_step): one unit per block,
     // XCD-mapped (no loop: fewer live registers); units [unit_base, unit_base + gridDim.x):
     // a launch's grid stays below 2^32 work-items (the dispatch packet's grid size), so a
@@ -2017,14 +2086,33 @@ struct PathArgs {
   const uint32_t* trans;
   int force_edge;              // test build only (OTR_FORCE_RETRY): RouteArgs::force_edge bits 3-4
   unsigned long long* queue;   // list tiers: this launch's per-XCD step counters (XcdQueue), zeroed
+  bool from_back;              // first tier: its steps are the last *n_steps_dev of steps[0, n_steps)
+                               // (k_step_lists: the small-search tier's at the front)
 };
 
-// G searches per wave (G = 2 for the first tier, lanes split 32/32), each a
-// single-target search from the winner's root with predecessor labels.  First tier:
-// step_list == null, the step count is read on the device (n_steps_dev), one unit per
-// block; retry tiers: a fixed grid strides over step_list[0 .. *list_count).
+// winner-path steps for the small-search path tier (k_paths<OTR_CAP4, 4>): the search is
+// bounded by the winning route r (k_paths), so its keys grow with r^2; a node-mode step
+// whose estimate est4 * min(B, r)^2 is at most small_keys goes to the front of the step
+// list, the rest to the back (k_step_lists)
+struct PathClass {
+  const int32_t* winner;
+  const int64_t* trans_off;
+  const uint32_t* trans;
+  const double* bound;
+  const int32_t* state_trace;
+  const uint8_t* mode;
+  uint32_t turn_modes;
+  float est4;                 // keys per m^2 of route length
+  float small_keys;
+};
+
+// G searches per wave (G = 2 for the first tier, lanes split 32/32; G = 4 the small-search
+// tier, 16 lanes each), each a single-target search from the winner's root with
+// predecessor labels.  First tiers: step_list == null, the step count is read on the
+// device (n_steps_dev), one unit per block; retry tiers: a fixed grid strides over
+// step_list[0 .. *list_count).
 template <int CAP, int G>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 : 8, 8))) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, const unsigned long long* list_count) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G >= 2 ? 6 : 8, 8))) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, const unsigned long long* list_count) {
   using Gr = Grp<G>;
   __shared__ SearchLds<CAP, true> Ls[G];
   const int gl = Gr::gl();
@@ -2038,7 +2126,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
        w = step_list ? q.next() : wend) {
   const int64_t iw = w * G + Gr::g();
   const bool have = iw < n_list;
-  const int64_t k = have ? (step_list ? step_list[iw] : iw) : 0;
+  const int64_t k = have ? (step_list ? step_list[iw] : (a.from_back ? a.n_steps - n_list + iw : iw)) : 0;
   const int64_t s = have ? a.steps[k] : 0;
   const int64_t sp = have ? a.prev[s] : 0;
   bool active = false;

@@ -512,6 +512,8 @@ int vp_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
  * the target node (rho_d, rho_t as for the edge search). */
 typedef struct {
   int64_t searches, settled_base, settled_astar, exhausted_base, exhausted_astar, settled_order, exhausted_order;
+  int64_t settled_tt, exhausted_tt; /* mode 3: the base rule + the time rule (no feasible label and the
+                                       smallest pending time + the entry time breaks the time bound) */
 } ns_stats;
 static double g_ns_c = 0.5; /* heuristic weight (of rho_d) of the A*-ordered variant */
 void ns_set_c(double c) { g_ns_c = c; }
@@ -607,7 +609,7 @@ int ns_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
           }
         }
 #define NS_H(x) (mode == 2 ? g_ns_c * g_rho_d * fmax(0.0, sqrt(((double)g->node_ll[2 * (x) + 1] * g_kx - Ax) * ((double)g->node_ll[2 * (x) + 1] * g_kx - Ax) + ((double)g->node_ll[2 * (x)] * g_ky - Ay) * ((double)g->node_ll[2 * (x)] * g_ky - Ay)) - R - 1.0) : 0.0)
-        for (int mode = 0; mode < 3; ++mode) {
+        for (int mode = 0; mode < 4; ++mode) {
           ++gen;
           heap_t hp = {0};
           const uint32_t root = g->edge_dst[ci->e];
@@ -627,8 +629,17 @@ int ns_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
             for (int j = 0; j < Kb && !unres; ++j) {
               if (tv[j] == 0xFFFFFFFFu) continue;
               if (stamp[tv[j]] == gen && done[tv[j]]) continue;
-              if (mode < 2 && top.d + tpart[j] > pd) continue;
+              if ((mode < 2 || mode == 3) && top.d + tpart[j] > pd) continue;
               int r = 0;
+              if (mode == 3 && X.time_on) {
+                const int has = stamp[tv[j]] == gen && lab[tv[j]].t + tpt[j] <= pt;  /* a feasible label */
+                if (!has) {
+                  int64_t tmn = kInf;
+                  for (size_t q = 0; q < hp.n; ++q)
+                    if (hp.d[q].k.t < tmn) tmn = hp.d[q].k.t;
+                  if (tmn + tpt[j] > pt) r = 1;
+                }
+              }
               if (mode >= 1 && (settled & 3) == 0) {
                 double ad = 1e300, at = 1e300;
                 for (size_t q = 0; q < hp.n; ++q) {
@@ -676,6 +687,9 @@ int ns_run(const orc_graph* g, const orc_params* p, int32_t n_traces, const int6
           if (mode == 0) {
             S->settled_base += settled;
             S->exhausted_base += exhausted;
+          } else if (mode == 3) {
+            S->settled_tt += settled;
+            S->exhausted_tt += exhausted;
           } else if (mode == 2) {
             S->settled_order += settled;
             S->exhausted_order += exhausted;

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summary of one workload of tools/profile_set.sh: per kernel the launches and average
-duration (kernel trace), FETCH_SIZE and WRITE_SIZE per launch (their own --pmc passes,
+duration (kernel trace; the full-size launches: the kernel's largest grid), FETCH_SIZE and WRITE_SIZE per launch (their own --pmc passes,
 KiB counters -> bytes; gfx950: the raw sum, see DESIGN.md §4 on the calibration), the
 L2 (TCC) hit rate, and measured HBM GB/s = (fetch + write) / duration against 8 TB/s.
 
@@ -31,22 +31,39 @@ def find(d, suffix):
 
 
 def per_dispatch(path, names):
-    """{kernel: ({counter: average over the kernel's dispatches}, dispatches)}: one row per
-    dispatch and counter (rocprofv3 csv)."""
-    acc = defaultdict(lambda: defaultdict(list))
+    """{kernel: ({counter: average over the kernel's full-size dispatches}, dispatches)}: one
+    row per dispatch and counter (rocprofv3 csv).  Full size: the kernel's largest grid (the
+    bench batch; the bench's smaller launches — the JSON drop-in leg, oracle samples — are
+    left out so the per-launch figures are the workload's)."""
+    rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
             if any(r['Counter_Name'].startswith(n) for n in names):
-                acc[short(r['Kernel_Name'])][r['Counter_Name']].append(float(r['Counter_Value']))
+                rows.append((short(r['Kernel_Name']), int(r['Grid_Size']), r['Counter_Name'], float(r['Counter_Value'])))
+    big = defaultdict(int)
+    for k, gsz, _, _ in rows:
+        big[k] = max(big[k], gsz)
+    acc = defaultdict(lambda: defaultdict(list))
+    for k, gsz, c, v in rows:
+        if gsz == big[k]:
+            acc[k][c].append(v)
     return {k: ({c: sum(v) / len(v) for c, v in cs.items()}, max(len(v) for v in cs.values())) for k, cs in acc.items()}
 
 
 def main(d):
     kt = find(os.path.join(d, 'kt'), 'kernel_trace.csv')
-    dur = defaultdict(list)
+    rows = []
     with open(kt) as f:
         for r in csv.DictReader(f):
-            dur[short(r['Kernel_Name'])].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) * 1e-6)
+            gsz = int(r['Grid_Size_X']) * int(r['Grid_Size_Y']) * int(r['Grid_Size_Z'])
+            rows.append((short(r['Kernel_Name']), gsz, (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) * 1e-6))
+    big = defaultdict(int)
+    for k, gsz, _ in rows:
+        big[k] = max(big[k], gsz)
+    dur = defaultdict(list)  # the full-size launches (the kernel's largest grid), as per_dispatch
+    for k, gsz, ms in rows:
+        if gsz == big[k]:
+            dur[k].append(ms)
     fetch = per_dispatch(find(os.path.join(d, 'FETCH_SIZE'), 'counter_collection.csv'), ['FETCH_SIZE'])
     write = per_dispatch(find(os.path.join(d, 'WRITE_SIZE'), 'counter_collection.csv'), ['WRITE_SIZE'])
     l2 = per_dispatch(find(os.path.join(d, 'TCC_HIT_sum'), 'counter_collection.csv'), ['TCC_HIT', 'TCC_MISS'])
