@@ -87,6 +87,7 @@ struct DevGraph {
   const uint32_t* cell_edge;
   const uint4* cell_rec;       // per cell entry 3 x 16 B: {edge, shape begin, shape end, attr}, shape points 0-1, 2-3
   const uint4* edge_pack;      // {dst, len_mm, attr, minin(dst)}: one 16-B load per relaxed edge (CSR tail)
+  const uint4* eprep;          // {len_mm, src, minin(src), dst}: a candidate edge's terms in one load (k_prep)
   const uint4* adj;            // 4 x uint4 per node: {dst | access<<28 | more<<31, len_mm, minin(dst), 0}
   const uint32_t* node_minin;  // per node: its shortest in-edge, mm (0xFFFFFFFF: none), the IN criterion
   const uint32_t* len_mm;      // routing length, whole millimetres

@@ -10,8 +10,7 @@
 // used at 4.25 waves per SIMD; this one: 4 waves per SIMD):
 //   * one 16-B record per relaxation, indexed by the settled state (edge) and the out-edge
 //     slot (DevGraph::erec: the out-edge's id, access and length, the turn degree from the
-//     state into it, resolved at graph load), beside one 8-B per-mode {route time, turn
-//     cost} (RouteArgs::erec_tc, built per configuration: no turn table in LDS);
+//     state into it, resolved at graph load), beside one 4-B per-mode route time;
 //   * the IN criterion adds the mode's smallest turn cost (every later offer to a state
 //     crosses a turn >= tmin and the state's own edge): lab(b) < kmin + len(b) + tmin is
 //     final, and a target is final once tlab < kmin + tpart + tmin — fewer rounds, the
@@ -24,12 +23,12 @@
 //   * probe loops are not unrolled, the target map is consulted only when a 64-bit bloom
 //     of the target nodes (a wave-uniform register) admits the settled node, and the
 //     wave's scalar state is kept small (no SGPR spills);
-//   * small tables: the first tier holds 360 states (~96 % of the C2 searches); a search
-//     that outgrows it goes on to 512 and 1024 states (this kernel again), then k_general:
-//     same results;
+//   * small tables: the first tier holds 360 states (table + lists + targets + the turn
+//     table in 10.1 KB: 16 waves per CU, ~96 % of the C2 searches); a search that outgrows
+//     it goes on to 512 and 1024 states (this kernel again), then k_general: same results;
 //   * a state is its label, its key (edge id) and its IN-gap code in LDS (15 B with the
-//     pending index), a settled state's label, edge and code one 16-B list entry: 6.9 KB
-//     per wave with the lists and targets, 23 waves per CU;
+//     pending index: 21 waves per CU), a settled state's label, edge and code one 16-B list
+//     entry;
 //   * the relax step is branch-free on its common path (e1_relax_sink);
 //   * waves claim tasks from per-XCD queues (XcdQueue, otr_device.h).
 #pragma once
@@ -81,9 +80,7 @@ struct E1Lds {
   uint32_t tm_node[TM];         // target node -> target lanes
   uint32_t tm_mask[TM];
   unsigned long long bloom;     // bit tm_home(v) of every target node v
-  // (no turn table: a relaxation loads its slot's turn cost beside the record, RouteArgs::
-  // erec_tc, and the target offers read the mode's table in global memory: 724 B less per
-  // wave, 23 waves per CU instead of 21)
+  int32_t turn[181];
   int turn_md;
   uint32_t tmin;
   int n_pend, n_keys, overflow;
@@ -114,8 +111,8 @@ __device__ inline int e1_insert(E1Lds<CAP>& L, uint32_t e, bool& isnew) {
 }
 
 template <int CAP>
-__device__ inline void e1_target_offers(E1Lds<CAP>& L, const int32_t* turn, unsigned long long lb, uint32_t hbk,
-                                        uint32_t v, uint32_t pd, uint32_t pt) {
+__device__ inline void e1_target_offers(E1Lds<CAP>& L, unsigned long long lb, uint32_t hbk, uint32_t v, uint32_t pd,
+                                        uint32_t pt) {
   uint32_t h = tm_slot(v), m = 0;
 #pragma unroll 1
   for (int probe = 0; probe < E1Lds<CAP>::TM; ++probe) {
@@ -128,20 +125,21 @@ __device__ inline void e1_target_offers(E1Lds<CAP>& L, const int32_t* turn, unsi
   while (m) {
     const int q = __ffs((int)m) - 1;
     m &= m - 1;
-    const uint32_t tc = (uint32_t)turn[turn_from_back((int)hbk, (int)L.thb[q])];
+    const uint32_t tc = (uint32_t)L.turn[turn_from_back((int)hbk, (int)L.thb[q])];
     const EOffer o = e_step(lb, tc, L.tpart[q], L.tpt[q]);
     if (e_feasible(o, pd, pt)) atomicMin(&L.tlab[q], gpack(o.k, o.c, o.t));
   }
 }
 
 // relax the final state (label lb) through one out-edge b: access bits in dw, length,
-// time, the turn cost into b; returns the slot when b's state became newly pending
+// time, the turn degree into b; returns the slot when b's state became newly pending
 template <int CAP>
 __device__ inline int e1_relax(E1Lds<CAP>& L, unsigned long long lb, uint32_t dw, uint32_t len, uint32_t tt,
-                               uint32_t b, uint32_t tc, uint32_t pd, uint32_t pt, uint32_t mode_bit,
+                               uint32_t b, uint32_t deg, uint32_t pd, uint32_t pt, uint32_t mode_bit,
                                uint32_t& relaxed, uint32_t& knext, uint32_t& dnext, uint32_t& tnext, bool& isnew) {
   if (!(((dw >> 28) & 7u) & mode_bit)) return -1;
   ++relaxed;
+  const uint32_t tc = (uint32_t)L.turn[deg];
   const EOffer o = e_step(lb, tc, len, tt);
   if (!e_feasible(o, pd, pt)) return -1;  // pruned (label-setting semantics)
   const int sl = e1_insert(L, b, isnew);
@@ -167,19 +165,20 @@ __device__ inline int e1_relax(E1Lds<CAP>& L, unsigned long long lb, uint32_t dw
 // home slot branches.  Same slots, labels and pending list as e1_relax.
 template <int CAP>
 __device__ inline int e1_relax_sink(E1Lds<CAP>& L, unsigned long long lb, uint32_t dw, uint32_t len, uint32_t tt,
-                                    uint32_t b, uint32_t tc, uint32_t pd, uint32_t pt, uint32_t mode_bit,
+                                    uint32_t b, uint32_t deg, uint32_t pd, uint32_t pt, uint32_t mode_bit,
                                     uint32_t& relaxed, uint32_t& knext, uint32_t& dnext, uint32_t& tnext,
                                     bool& isnew) {
   unsigned long long* mine = &L.sink[threadIdx.x % OTR_E1SINK];  // (lanes sharing a word: a few-way atomic)
   uint32_t* mine32 = reinterpret_cast<uint32_t*>(mine);
   const bool mode_ok = (((dw >> 28) & 7u) & mode_bit) != 0u;
   relaxed += mode_ok ? 1u : 0u;
-  // the insert needs only the length and time bounds (neither depends on the turn); an
-  // offer that then breaks the turn-cost cap leaves a key without a label (never pending:
-  // same labels)
+  // the insert needs only the length and time bounds (neither depends on the turn), so
+  // its CAS and the turn-table read are in flight together; an offer that then breaks the
+  // turn-cost cap leaves a key without a label (never pending: same labels)
   bool go = mode_ok && g_d(lb) + len <= pd && g_t(lb) + tt <= pt;
   const uint32_t h0 = hslot<CAP>(b);
   const uint32_t k0 = atomicCAS(go ? &L.key[h0] : mine32, kEmpty, b);
+  const uint32_t tc = (uint32_t)L.turn[deg];
   const EOffer o = e_step(lb, tc, len, tt);
   isnew = go && k0 == kEmpty;
   int sl = (go && (k0 == kEmpty || (k0 & kNodeMask) == b)) ? (int)h0 : -1;
@@ -220,7 +219,6 @@ __device__ inline int e1_relax_sink(E1Lds<CAP>& L, unsigned long long lb, uint32
 }
 #endif
 
-// the mode's smallest turn cost (the IN criterion's tmin), when the mode changes
 template <int CAP>
 __device__ inline void e1_turn_table(E1Lds<CAP>& L, const int32_t* turn_tab, int md) {
   if (L.turn_md != md) {  // (uniform)
@@ -228,6 +226,7 @@ __device__ inline void e1_turn_table(E1Lds<CAP>& L, const int32_t* turn_tab, int
     uint32_t m = 0xFFFFFFFFu;
     for (int k = threadIdx.x; k < 181; k += OTR_WAVE) {
       const int32_t t = turn_tab[181 * md + k];
+      L.turn[k] = t;
       m = (uint32_t)t < m ? (uint32_t)t : m;
     }
     m = wave_min_u32(m);
@@ -440,8 +439,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
       }
       __syncthreads();
       const uint4* er = gr.erec;
-      const uint2* ertc = a.erec_tc + (size_t)md * gr.erec_stride;  // {route time, turn cost} per slot
-      const int32_t* turn = a.turn + 181 * md;
+      const uint32_t* ert = gr.erec_t + (size_t)md * gr.erec_stride;
       const uint32_t mode_bit = 1u << md;
       const uint32_t tmin = L.tmin;
 #ifdef OTR_FORCE_RETRY
@@ -504,19 +502,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
             const uint4 ws = L.wst[k >> 2];
             const unsigned long long lb = ((unsigned long long)ws.y << 32) | ws.x;
             const size_t ri = 4 * (size_t)ws.z + (k & 3);  // the settled state's slot record
-            // the slot's route time and turn cost, loaded beside the record and unconditionally
-            const uint2 tq = ertc[ri];
+            // the slot's route time, loaded beside the record and unconditionally
+            const uint32_t tq = ert[ri];
             const uint4 r = ld16(er + ri);
-            const uint32_t tt = timed ? tq.x : 0u;
+            const uint32_t tt = timed ? tq : 0u;
             if ((k & 3) == 0) {  // the state's head node (r.w) may be a target's source
               ++my_settled;
-              if ((bloom >> tm_home(r.w)) & 1ull) e1_target_offers(L, turn, lb, er_hbk(r), r.w, pd, pt);
+              if ((bloom >> tm_home(r.w)) & 1ull) e1_target_offers(L, lb, er_hbk(r), r.w, pd, pt);
             }
 #if OTR_E1SINK
-            psl = e1_relax_sink(L, lb, r.x & ~kAdjMore, r.y, tt, er_edge(r), tq.y, pd, pt, mode_bit, my_relaxed,
+            psl = e1_relax_sink(L, lb, r.x & ~kAdjMore, r.y, tt, er_edge(r), er_deg(r), pd, pt, mode_bit, my_relaxed,
                                 knext, dnext, tnext, isnew);
 #else
-            psl = e1_relax(L, lb, r.x & ~kAdjMore, r.y, tt, er_edge(r), tq.y, pd, pt, mode_bit, my_relaxed, knext,
+            psl = e1_relax(L, lb, r.x & ~kAdjMore, r.y, tt, er_edge(r), er_deg(r), pd, pt, mode_bit, my_relaxed, knext,
                            dnext, tnext, isnew);
 #endif
             tail |= ((k & 3) == 3) ? (r.x & kAdjMore) : 0u;
@@ -547,8 +545,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
                   const uint4 pk = ld16(gr.edge_pack + e);
                   const uint32_t deg = (uint32_t)turn_from_back((int)hbk, (int)(uint16_t)gr.edge_head[e].x);
                   bool nw2 = false;
-                  const int p2 = e1_relax(L, lb, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e,
-                                          (uint32_t)turn[deg], pd, pt, mode_bit, my_relaxed, knext, dnext, tnext, nw2);
+                  const int p2 = e1_relax(L, lb, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e, deg, pd, pt,
+                                          mode_bit, my_relaxed, knext, dnext, tnext, nw2);
                   if (nw2) atomicAdd(&L.n_keys, 1);
                   if (p2 >= 0) L.pend[atomicAdd(&L.n_pend, 1)] = (typename LT::Idx)p2;
                 }

@@ -85,12 +85,6 @@ struct Matcher {
   std::vector<DevBuf> bufs;
   GSlab gslab[2];
   std::vector<int32_t> h_turn;
-  // the edge-state tiers' per-slot {route time, turn cost} (S_EREC_TC): built for the graph
-  // and the turn tables it was built from (otr_edge1.h); need() reallocating it clears tc_valid
-  std::vector<int32_t> tc_turn;
-  const void* tc_graph = nullptr;
-  uint32_t tc_modes = 0;
-  bool tc_valid = false;
   // host result storage (OTR_BATCH_COPY_OUT)
   std::vector<int64_t> h_trace_state_off, h_state_probe, h_trace_route_off, h_trace_seg_off, h_seg_way_off,
       h_trace_rep_off;

@@ -215,6 +215,13 @@ int engine_configure(const Config& cfg, std::string* err) {
   for (uint32_t e = 0; e < h.n_edges; ++e) minin[dst[e]] = std::min(minin[dst[e]], len[e]);
   std::vector<uint4> pack(h.n_edges + 1);
   for (uint32_t e = 0; e < h.n_edges; ++e) pack[e] = make_uint4(dst[e], len[e], attr[e], minin[dst[e]]);
+  // per edge what k_prep needs of a candidate's edge in one 16-B gather: {len_mm, src,
+  // minin(src), dst} (no dependent minin load; C5's country graph misses the L2 there)
+  std::vector<uint4> eprep(h.n_edges + 1, make_uint4(0u, 0u, 0u, 0u));
+  {
+    const uint32_t* srcv = (const uint32_t*)(base + h.array_offset[OTR_A_EDGE_SRC]);
+    for (uint32_t e = 0; e < h.n_edges; ++e) eprep[e] = make_uint4(len[e], srcv[e], minin[srcv[e]], dst[e]);
+  }
   // per-node adjacency records: the first 4 out-edges of a node in one 64-B record,
   // {dst | access<<28 | more<<31, len_mm, minin(dst), 0} per edge
   std::vector<uint4> adj(4ull * h.n_nodes + 4, make_uint4(kAdjDstMask, 0u, 0u, 0u));
@@ -329,6 +336,7 @@ int engine_configure(const Config& cfg, std::string* err) {
   g.cell_edge = (const uint32_t*)up(OTR_A_CELL_EDGE, 4ull * h.n_cell_entries);
   g.len_mm = (const uint32_t*)upv(len.data(), 4ull * len.size());
   g.edge_pack = (const uint4*)upv(pack.data(), sizeof(uint4) * pack.size());
+  g.eprep = (const uint4*)upv(eprep.data(), sizeof(uint4) * eprep.size());
   g.adj = (const uint4*)upv(adj.data(), sizeof(uint4) * adj.size());
   g.node_minin = (const uint32_t*)upv(minin.data(), 4ull * minin.size());
   {
@@ -409,7 +417,7 @@ enum Slot {
   S_IN_GFIRST, S_IN_GKEY, S_IN_WS, S_IN_KLEN, S_IN_KFLAG, S_IN_POFF, S_IN_TPOS, S_IN_BAD, S_IN_TMP,
   S_IN_T_OFF, S_IN_T_LAT, S_IN_T_LON, S_IN_T_TIME, S_IN_T_ACC, S_IN_T_MODE, S_IN_T_UOFF, S_IN_T_ULEN,
   S_CLEN, S_CAND_NROOT, S_FLAGGED, S_HE_FIDX, S_HE_FHEAD, S_HE_PFILE, S_HE_FFIRST, S_HE_PKEY, S_QUEUE, S_PQUEUE,
-  S_E1DUMP0, S_E1DUMP1, S_TASK_DUMP, S_NDUMP0, S_NDUMP1, S_SORT_LIST, S_SORT_HIST, S_EREC_TC,
+  S_E1DUMP0, S_E1DUMP1, S_TASK_DUMP, S_NDUMP0, S_NDUMP1, S_SORT_LIST, S_SORT_HIST,
   S_NUM
 };
 
@@ -435,7 +443,6 @@ T* Matcher::need(int slot, size_t n) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
-    if (slot == S_EREC_TC) tc_valid = false;  // (its contents are built once per graph and turn tables)
     size_t nb = bytes + bytes / 4;
     bool ok = hipMalloc(&b.p, nb) == hipSuccess || hipMalloc(&b.p, bytes) == hipSuccess;
     if (!ok && !optional_slot(slot) && release_optional()) {
@@ -666,55 +673,11 @@ __global__ void k_collect_tier_list(const unsigned long long* n_in, int32_t* fla
   block_append(sel, i, list, count);
 }
 
-// per edge-state slot and turn mode: {route time, turn cost mm} (the turn degree the record
-// carries looked up in the mode's table; an unused slot's degree may be out of range: 0)
-__global__ void k_erec_tc(const uint4* erec, const uint32_t* erec_t, size_t es, const int32_t* turn,
-                          uint32_t turn_modes, uint2* out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= es) return;
-  const uint32_t deg = erec[i].z & 0xFFu;
-  for (int m = 0; m < OTR_MODES; ++m)
-    if ((turn_modes >> m) & 1u)
-      out[es * m + i] = make_uint2(erec_t[es * m + i], deg <= 180u ? (uint32_t)turn[181 * m + deg] : 0u);
-}
-
 // states that need a path: a step inside a sub-path
 __global__ void k_step_list(int64_t n_states, const int64_t* prev, const uint8_t* brk, const int32_t* cand_count,
                             int64_t* list, unsigned long long* count) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   block_append(s < n_states && cand_count[s] > 0 && prev[s] >= 0 && !brk[s], s, list, count);
-}
-
-// the same steps in two lists within list[0, n_states): the small-search path tier's from
-// the front (count_front), the rest from the back (count_back); *n_all = n_states (the
-// retry collects scan the whole index range, whose gap keeps its zero flags)
-__global__ void k_step_lists(int64_t n_states, const int64_t* prev, const uint8_t* brk, const int32_t* cand_count,
-                             PathClass pc, int64_t* list, unsigned long long* count_front,
-                             unsigned long long* count_back, unsigned long long* n_all) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s == 0) *n_all = (unsigned long long)n_states;
-  const bool hit = s < n_states && cand_count[s] > 0 && prev[s] >= 0 && !brk[s];
-  bool small = false;
-  if (hit) {
-    const int64_t sp = prev[s];
-    const int md = pc.mode[pc.state_trace[s]] < OTR_MODES ? pc.mode[pc.state_trace[s]] : 0;
-    const uint32_t r = pc.trans[pc.trans_off[s] + (int64_t)pc.winner[sp] * cand_count[s] + pc.winner[s]];
-    const double b = fmin(floor(pc.bound[s] * 1000.0), (double)r) * 1e-3;  // (k_paths' bound, m)
-    small = !((pc.turn_modes >> md) & 1u) && pc.est4 * (float)(b * b) <= pc.small_keys;
-  }
-  // one atomic per wave and list
-  const unsigned long long mf = __ballot(hit && small), mb = __ballot(hit && !small);
-  const int lane = (int)(threadIdx.x % OTR_WAVE);
-  unsigned long long bf = 0, bb = 0;
-  if (lane == 0) {
-    if (mf) bf = atomicAdd(count_front, (unsigned long long)__popcll(mf));
-    if (mb) bb = atomicAdd(count_back, (unsigned long long)__popcll(mb));
-  }
-  bf = __shfl(bf, 0);
-  bb = __shfl(bb, 0);
-  const unsigned long long below = (1ull << lane) - 1ull;
-  if (hit && small) list[bf + __popcll(mf & below)] = s;
-  if (hit && !small) list[n_states - 1 - (int64_t)(bb + __popcll(mb & below))] = s;
 }
 
 // work counters: fold the kCShards shards of every (bank, kind) into one value before the
@@ -742,8 +705,6 @@ static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + b
 // "256,512x2,1024,4096".
 // the small-search tier's default size limit (keys of k_ntask's estimate; OTR_SMALL_KEYS)
 constexpr double kSmallKeys = 24.0;
-// the small-search path tier's (keys of k_step_lists' estimate; OTR_SMALL_PATH_KEYS)
-constexpr double kSmallPathKeys = 16.0;
 
 static std::vector<int> route_tiers() {
   std::vector<int> t;
@@ -1027,13 +988,11 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   HIPCHK(hipMemcpyAsync(&NTR, trans_off + S, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
   NT += NT4;
-  int64_t* task_state = need<int64_t>(S_TASK_STATE, NT);
-  unsigned long long* task_mask = need<unsigned long long>(S_TASK_MASK, NT);
   int32_t* task_ovf = need<int32_t>(S_TASK_OVF, NT);
   uint32_t* trans = need<uint32_t>(S_TRANS, NTR);
   uint32_t* trans_tc = need<uint32_t>(S_TRANS_TC, turn_modes ? NTR : 1);  // read for turn modes only
   uint4* task_rec = need<uint4>(S_TASK_REC, 3 * (size_t)std::max<int64_t>(NT, 1));
-  if (!task_state || !task_mask || !task_ovf || !trans || !trans_tc || !task_rec) {
+  if (!task_ovf || !trans || !trans_tc || !task_rec) {
     if (err) *err = "device allocation failed (transitions)";
     return OTR_DEVICE_ERROR;
   }
@@ -1054,8 +1013,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     ta.cprep_t = pr.cprep_t;
     ta.trans_off = trans_off;
     ta.turn_modes = turn_modes;
-    ta.task_state = task_state;
-    ta.task_mask = task_mask;
     ta.rec = task_rec;
     ta.ntask4 = ntask4;
     ta.task4_off = task4_off;
@@ -1077,25 +1034,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   h_turn.resize(181 * OTR_MODES);
   for (int m = 0; m < OTR_MODES; ++m) turn_table(mp.m[m].turn_penalty_factor, h_turn.data() + 181 * m);
   HIPCHK(hipMemcpyAsync(d_turn, h_turn.data(), 4 * 181 * OTR_MODES, hipMemcpyHostToDevice, stream));
-  // the edge-state tiers' per-slot {route time, turn cost} of this batch's turn tables
-  // (otr_edge1.h: a relaxation loads its turn cost beside the record, no turn table in LDS),
-  // built when the graph or a turn mode's table changed (a configuration's first batch)
-  uint2* erec_tc = nullptr;
-  if (turn_modes != 0u && NT > 0) {
-    erec_tc = need<uint2>(S_EREC_TC, g.erec_stride * OTR_MODES);
-    if (!tc_valid || tc_graph != (const void*)g.erec || tc_modes != turn_modes || tc_turn != h_turn) {
-      k_erec_tc<<<grid_for((int64_t)g.erec_stride, 256), 256, 0, stream>>>(g.erec, g.erec_t, g.erec_stride, d_turn,
-                                                                           turn_modes, erec_tc);
-      tc_valid = true;
-      tc_graph = (const void*)g.erec;
-      tc_modes = turn_modes;
-      tc_turn = h_turn;
-    }
-  }
   // ---- K3/K4: routing + transition costs
   RouteArgs ra{};
-  ra.task_state = task_state;
-  ra.task_mask = task_mask;
   ra.task_list = nullptr;
   ra.n_tasks = NT;
   ra.prev = sb.prev;
@@ -1111,7 +1051,6 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ra.mode = b.mode;
   ra.bt = sb.bt;
   ra.turn = d_turn;
-  ra.erec_tc = erec_tc;
   ra.trans_tc = trans_tc;
   ra.cprep = pr.cprep;
   ra.cprep_t = pr.cprep_t;
@@ -1201,8 +1140,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   ga.mode_of_trace = b.mode;
   ga.turn_modes = turn_modes;
   ga.turn = d_turn;
-  ga.task_state = task_state;
-  ga.task_mask = task_mask;
+  ga.rec = task_rec;
   ga.trans_off = trans_off;
   ga.trans = trans;
   ga.trans_tc = trans_tc;
@@ -1258,6 +1196,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         unsigned long long* rc4 = rwork ? d_counters + 12 * bank : nullptr;
         if (timing) (void)hipEventRecord(ev[24 + 2 * 12], stream);
         const int64_t units = (NT4 + 3) / 4;
+        // (a block per unit: a persistent grid over per-XCD queues was slower, C5 26.5 ->
+        // 35.6 ms)
         for (int64_t base = 0; base < units; base += kMaxUnits) {
           RouteArgs rf = ra;
           rf.n_tasks = NT4;
@@ -1505,34 +1445,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   {
     int64_t* steps = need<int64_t>(S_LIST2, std::max<int64_t>(S, 1));
     unsigned long long* nsteps_d = cnt + 11;
-    // the small-search path tier (four searches per wave): steps whose winning route
-    // bounds a search of at most OTR_SMALL_PATH_KEYS keys (estimate: 4 x the node density
-    // x r^2, the diamond of road distance r around the root and its frontier); the
-    // two-search tier takes the rest
-    static const double small_path_keys =
-        getenv("OTR_SMALL_PATH_KEYS") ? atof(getenv("OTR_SMALL_PATH_KEYS")) : kSmallPathKeys;  // A/B knob
-    const bool small_paths = small_path_keys > 0.0 && est_k > 0.f;
-    unsigned long long* nsteps4_d = cnt + 21;  // (the front list's count)
-    unsigned long long* nall_d = cnt + 22;     // (S: the collects' index range)
-    if (S > 0 && small_paths) {
-      PathClass pc{};
-      pc.winner = va.winner;
-      pc.trans_off = trans_off;
-      pc.trans = trans;
-      pc.bound = sb.bound;
-      pc.state_trace = state_trace;
-      pc.mode = b.mode;
-      pc.turn_modes = turn_modes;
-      pc.est4 = 8.f * est_k;  // (est_k = half the node density)
-      pc.small_keys = (float)small_path_keys;
-      HIPCHK(hipMemsetAsync(nsteps4_d, 0, 16, stream));
-      k_step_lists<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, va.brk, cb.count, pc, steps, nsteps4_d, nsteps_d,
-                                                          nall_d);
-    } else if (S > 0) {
-      k_step_list<<<grid_for(S, 1024), 1024, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, nsteps_d);
-    }
-    // the retry collects' index range: every step index (front and back lists), or the list
-    const unsigned long long* nscan_d = small_paths ? nall_d : nsteps_d;
+    if (S > 0) k_step_list<<<grid_for(S, 1024), 1024, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, nsteps_d);
     int32_t* step_ovf = need<int32_t>(S_STEP_OVF, S + 1);
     int64_t capacity = kShards * ((int64_t)S * 24 / kShards + 1024);
     bool paths_fit = S == 0;
@@ -1573,17 +1486,12 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       pa.trans_off = trans_off;
       pa.trans = trans;
       pa.force_edge = ra.force_edge;
+      // the path retry tiers' work queues (XcdQueue)
+      constexpr int kPQWords = 16 * 8;
+      unsigned long long* pq = need<unsigned long long>(S_PQUEUE, 8 * kPQWords);
+      HIPCHK(hipMemsetAsync(pq, 0, 8 * 8 * kPQWords, stream));
       tb(OTR_STAGE_PATHS);
-      if (small_paths) {
-        // the front list four searches per wave, the back list two (grids for S steps each:
-        // blocks past a list's device count exit at once)
-        PathArgs p4 = pa;
-        p4.n_steps_dev = nsteps4_d;
-        k_paths<OTR_CAP4, 4><<<(unsigned)(8 * ((S + 31) / 32)), 64, 0, stream>>>(g, p4, nullptr, nullptr);
-        PathArgs p2 = pa;
-        p2.from_back = true;
-        k_paths<OTR_CAP1, 2><<<(unsigned)grid_paths(S).blocks, 64, 0, stream>>>(g, p2, nullptr, nullptr);
-      } else {
+      {
         // (steps <= states: two searches per wave)
         k_paths<OTR_CAP1, 2><<<(unsigned)grid_paths(S).blocks, 64, 0, stream>>>(g, pa, nullptr, nullptr);
       }
@@ -1591,12 +1499,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       tb(OTR_STAGE_PATHS_BIG);
       // large-table retries for table overflows (flag 1), on device-side lists; each
       // launch's waves claim steps from its own per-XCD queue (XcdQueue)
-      constexpr int kPQWords = 16 * 8;
-      unsigned long long* pq = need<unsigned long long>(S_PQUEUE, 8 * kPQWords);
-      HIPCHK(hipMemsetAsync(pq, 0, 8 * 8 * kPQWords, stream));
       for (int tier = 0; tier < 3; ++tier) {
         unsigned long long* c = cnt + 12 + tier;
-        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, 0x2u, list, c);
+        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0x2u, list, c);
         PathArgs pb = pa;
         pb.queue = pq + tier * kPQWords;
         if (tier == 0) k_paths<512, 1><<<pgrid(16384, S), 64, 0, stream>>>(g, pb, list, c);
@@ -1607,7 +1512,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       if (turn_modes != 0u) {
         for (int et = 0; et < 2; ++et) {
           unsigned long long* c = cnt + 27 + et;
-          k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, et == 0 ? 0x20u : 0x40u,
+          k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, et == 0 ? 0x20u : 0x40u,
                                                                        list, c);
           PathArgs pb = pa;
           pb.queue = pq + (3 + et) * kPQWords;
@@ -1626,7 +1531,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       ga.cap_flag = (int32_t*)(cnt + 20);
       for (int gt = 0; gt < 2; ++gt) {
         unsigned long long* c = cnt + 16 + gt;
-        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, gt == 0 ? 0xAu : 0x2u, list,
+        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, gt == 0 ? 0xAu : 0x2u, list,
                                                                      c);
         GSlabs gs2;
         if ((rc = slabs(gt, &gs2))) return rc;
@@ -1638,7 +1543,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         k_general<<<pgrid(gs2.n, S), kGenThreads, 0, stream>>>(g, ga, gs2);
       }
       // steps still flagged (beyond a 1M-state slab): named after the final sync
-      k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, 0xAu, list, cnt + 18);
+      k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0xAu, list, cnt + 18);
       te(OTR_STAGE_PATHS_BIG);
       unsigned long long capflag = 0;
       std::vector<unsigned long long> cur(kShards);
@@ -1821,11 +1726,17 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       if (!nf) continue;
       std::vector<int64_t> idx(nf), st(nf);
       HIPCHK(hipMemcpy(idx.data(), which == 0 ? fail_tasks : list, 8 * nf, hipMemcpyDeviceToHost));
-      const int64_t* src = which == 0 ? task_state : need<int64_t>(S_LIST2, 1);
+      const int64_t* src = need<int64_t>(S_LIST2, 1);  // (steps: the step list; tasks: their records)
       for (unsigned long long k = 0; k < nf; ++k) {
         int64_t sidx = 0;
         int32_t t = 0;
-        HIPCHK(hipMemcpy(&sidx, src + idx[k], 8, hipMemcpyDeviceToHost));
+        if (which == 0) {
+          uint32_t s32 = 0;
+          HIPCHK(hipMemcpy(&s32, task_rec + 3 * idx[k], 4, hipMemcpyDeviceToHost));
+          sidx = s32;
+        } else {
+          HIPCHK(hipMemcpy(&sidx, src + idx[k], 8, hipMemcpyDeviceToHost));
+        }
         HIPCHK(hipMemcpy(&t, state_trace + sidx, 4, hipMemcpyDeviceToHost));
         if (t >= 0 && t < T && h_trace_status[t] == OTR_OK) {
           h_trace_status[t] = OTR_MATCH_ERROR;

@@ -68,8 +68,7 @@ struct GenArgs {
   uint32_t turn_modes;          // bit m: mode m has turn costs
   const int32_t* turn;          // [OTR_MODES][181] turn cost table, mm
   // route mode
-  const int64_t* task_state;
-  const unsigned long long* task_mask;
+  const uint4* rec;                     // per route task: k_tasks' record (state s, source mask)
   const int64_t* trans_off;
   uint32_t* trans;
   uint32_t* trans_tc;
@@ -406,8 +405,9 @@ __global__ __launch_bounds__(kGenThreads) void k_general(DevGraph G, GenArgs a, 
       // from the common root per group of sources with equal exit times (the time bound
       // prunes each group at its own bt - t0; the length bound at B - the group's smallest
       // exit part); turn costs: the task has one source edge
-      const int64_t s = a.task_state[item];
-      const unsigned long long mask = a.task_mask[item];
+      const uint4 r0 = a.rec[3 * item], r1 = a.rec[3 * item + 1];
+      const int64_t s = r0.x;
+      const unsigned long long mask = ((unsigned long long)r1.w << 32) | r1.z;
       const int64_t sp = a.prev[s];
       const int Kb = a.cand_count[s];
       bool ok = true;

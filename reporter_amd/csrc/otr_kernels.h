@@ -552,6 +552,11 @@ struct WorkE {
 };
 
 
+// settles per round of the small tier's 80-slot tables (four tables per wave in 32 waves'
+// LDS: at most 28)
+#ifndef OTR_WCAP4
+#define OTR_WCAP4 16
+#endif
 template <int CAP, int LM>
 struct SearchLds {
   static constexpr bool PRED = LM == 1;
@@ -577,7 +582,7 @@ struct SearchLds {
   // nodes settled per round (at most); k_paths (PRED) reuses pend + work as CAP u32 words
   // (1024 slots: 120, the 1-B codes' table then fits 13 waves per CU's LDS)
   // (the small tier's 80-slot tables: 16, so four tables fit 32 waves per CU: 4.5 KB per wave)
-  static constexpr int WCAP = CAP <= 96 ? (PRED ? 20 : 16) : CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : (CAP <= 1024 ? 120 : 128)));
+  static constexpr int WCAP = CAP <= 96 ? OTR_WCAP4 : CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : (CAP <= 1024 ? 120 : 128)));
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
   WorkE<W> work[WCAP];                // this round's settled nodes: {node, label}
   int n_pend, n_keys, overflow;
@@ -1150,24 +1155,22 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
   if (K <= 0) return;
   const int md = a.mode[a.state_trace[s]] < OTR_MODES ? a.mode[a.state_trace[s]] : 0;
   const bool turn = (a.turn_modes >> md) & 1u;
-  if (lane < K) {
-    const uint32_t e = a.cand_edge[s * OTR_KMAX + lane];
-    const double p = a.cand_p[s * OTR_KMAX + lane];
-    const uint32_t len = g.len_mm[e];
-    const uint32_t tn = g.edge_src[e];
-    const uint32_t z = turn ? (uint32_t)(uint16_t)g.edge_head[e].x : g.node_minin[tn];
-    a.cprep[s * OTR_KMAX + lane] = make_uint4((uint32_t)part_mm(p, len), tn, z, (uint32_t)part_mm(1.0 - p, len));
-    const uint32_t et = g.et(md)[e];
-    a.cprep_t[s * OTR_KMAX + lane] = make_uint2((uint32_t)part_mm(p, et), (uint32_t)part_mm(1.0 - p, et));
-    a.clen[s * OTR_KMAX + lane] = make_uint2(len, et);
-  }
   // distinct search tasks (K <= OTR_KMAX: one candidate per lane): a lane is its task's
   // first holder when no lower lane has the same key (root, exit time) (k_tasks' rule)
   uint32_t root = 0xFFFFFFFFu, t0 = 0u;
   if (lane < K) {
     const uint32_t e = a.cand_edge[s * OTR_KMAX + lane];
-    root = turn ? e : g.edge_dst[e];
-    if (!turn) t0 = (uint32_t)part_mm(1.0 - a.cand_p[s * OTR_KMAX + lane], g.et(md)[e]);
+    const double p = a.cand_p[s * OTR_KMAX + lane];
+    const uint4 ep = g.eprep[e];  // {len_mm, src, minin(src), dst}: one gather beside the time's
+    const uint32_t et = g.et(md)[e];
+    const uint32_t len = ep.x, tn = ep.y;
+    const uint32_t z = turn ? (uint32_t)(uint16_t)g.edge_head[e].x : ep.z;
+    const uint32_t x1 = (uint32_t)part_mm(1.0 - p, len), t1 = (uint32_t)part_mm(1.0 - p, et);
+    a.cprep[s * OTR_KMAX + lane] = make_uint4((uint32_t)part_mm(p, len), tn, z, x1);
+    a.cprep_t[s * OTR_KMAX + lane] = make_uint2((uint32_t)part_mm(p, et), t1);
+    a.clen[s * OTR_KMAX + lane] = make_uint2(len, et);
+    root = turn ? e : ep.w;
+    if (!turn) t0 = t1;
   }
   bool first = lane < K;
   for (int k = 0; k < K; ++k) {
@@ -1233,8 +1236,6 @@ __global__ void k_ntask(int64_t n_states, const int64_t* prev, const int32_t* nr
 // every source candidate sharing the root.
 // ------------------------------------------------------------------------------
 struct RouteArgs {
-  const int64_t* task_state;
-  const unsigned long long* task_mask;
   const int64_t* task_list;   // optional indirection (overflow retry), else null
   int64_t n_tasks;
   const int64_t* prev;
@@ -1255,8 +1256,6 @@ struct RouteArgs {
   const uint4* rec;           // per task, 3 x uint4 (k_tasks)
   const unsigned long long* list_count;  // retry tiers: length of task_list, on the device
   const int32_t* turn;        // [OTR_MODES][181] turn cost tables (mm), turn modes only
-  const uint2* erec_tc;       // [OTR_MODES][DevGraph::erec_stride]: per edge-state slot {route time, turn
-                              // cost mm} of the turn modes (the edge-state tiers, otr_edge1.h)
   uint32_t* trans_tc;         // turn cost (mm) per transition, turn modes only
   double inv_beta[OTR_MODES];
   int32_t* overflow_flag;     // per task: 1/2 retry in a larger LDS table, 3 the global-memory search,
@@ -1306,9 +1305,8 @@ struct TaskArgs {
   const uint2* cprep_t;       // k_prep
   const int64_t* trans_off;
   uint32_t turn_modes;
-  int64_t* task_state;
-  unsigned long long* task_mask;
-  uint4* rec;                 // 3 per task (the K2c record, below)
+  uint4* rec;                 // 3 per task (the K2c record, below; the state and source mask of a task
+                              // are read from it everywhere: no separate per-task arrays)
   const int64_t* ntask4;      // small-tier steps' task counts (k_ntask), or null
   const int64_t* task4_off;   // their exclusive offsets: small-tier tasks are [0, nt4)
   int64_t nt4;                // two-search tasks are nt4 + task_off[s]
@@ -1328,8 +1326,8 @@ struct TaskArgs {
 // task: one search rooted at that node, pruned at bt - that time and at B - the smallest
 // exit part — length pruning is monotone in the label order, so each source's labels
 // within its own length bound are the shared ones.  Turn modes: every
-// source edge is its own task (the edge-state search).  The task's representative (its lowest source) writes task_state,
-// task_mask and the task record k_route reads:
+// source edge is its own task (the edge-state search).  The task's representative (its lowest source) writes the task
+// record every route kernel reads (its state and source mask included):
 //   rec[3t]   = {s, sp, root, bound_mm}
 //   rec[3t+1] = {d0min, Kb | mode << 8 | forced << 10 | sh << 11 | general << 16 | turn << 17 | pre << 18,
 //                mask lo, mask hi}
@@ -1375,8 +1373,6 @@ __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
   const int64_t tend = n4 > 0 ? tbase + n4 : a.nt4 + a.task_off[s + 1];
   const int64_t o = tbase + __popcll(reps & ((1ull << lane) - 1ull));
   if (o >= tend) return;  // the count (k_prep's nroot) and this rule agree; never write past it
-  a.task_state[o] = s;
-  a.task_mask[o] = same;
   const uint32_t bmm = (uint32_t)bound_mm_of(a.bound[s]);
   const int32_t bt = a.bt[s];
   const uint32_t sh = pack_shift(bt);
@@ -2086,33 +2082,16 @@ struct PathArgs {
   const uint32_t* trans;
   int force_edge;              // test build only (OTR_FORCE_RETRY): RouteArgs::force_edge bits 3-4
   unsigned long long* queue;   // list tiers: this launch's per-XCD step counters (XcdQueue), zeroed
-  bool from_back;              // first tier: its steps are the last *n_steps_dev of steps[0, n_steps)
-                               // (k_step_lists: the small-search tier's at the front)
 };
 
-// winner-path steps for the small-search path tier (k_paths<OTR_CAP4, 4>): the search is
-// bounded by the winning route r (k_paths), so its keys grow with r^2; a node-mode step
-// whose estimate est4 * min(B, r)^2 is at most small_keys goes to the front of the step
-// list, the rest to the back (k_step_lists)
-struct PathClass {
-  const int32_t* winner;
-  const int64_t* trans_off;
-  const uint32_t* trans;
-  const double* bound;
-  const int32_t* state_trace;
-  const uint8_t* mode;
-  uint32_t turn_modes;
-  float est4;                 // keys per m^2 of route length
-  float small_keys;
-};
-
-// G searches per wave (G = 2 for the first tier, lanes split 32/32; G = 4 the small-search
-// tier, 16 lanes each), each a single-target search from the winner's root with
-// predecessor labels.  First tiers: step_list == null, the step count is read on the
-// device (n_steps_dev), one unit per block; retry tiers: a fixed grid strides over
-// step_list[0 .. *list_count).
+// G searches per wave (G = 2 for the first tier, lanes split 32/32), each a
+// single-target search from the winner's root with predecessor labels.  First tier:
+// step_list == null, the step count is read on the device (n_steps_dev), one unit per
+// block; retry tiers: a fixed grid strides over step_list[0 .. *list_count).
+// (Measured and dropped, DESIGN.md §6: a four-search 80-slot first tier for steps with a
+// short winning route: C5 paths 13.1 -> 18.8 ms.)
 template <int CAP, int G>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G >= 2 ? 6 : 8, 8))) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, const unsigned long long* list_count) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 : 8, 8))) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, const unsigned long long* list_count) {
   using Gr = Grp<G>;
   __shared__ SearchLds<CAP, true> Ls[G];
   const int gl = Gr::gl();
@@ -2126,7 +2105,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G >= 2 ? 6 :
        w = step_list ? q.next() : wend) {
   const int64_t iw = w * G + Gr::g();
   const bool have = iw < n_list;
-  const int64_t k = have ? (step_list ? step_list[iw] : (a.from_back ? a.n_steps - n_list + iw : iw)) : 0;
+  const int64_t k = have ? (step_list ? step_list[iw] : iw) : 0;
   const int64_t s = have ? a.steps[k] : 0;
   const int64_t sp = have ? a.prev[s] : 0;
   bool active = false;
