@@ -680,6 +680,38 @@ __global__ void k_step_list(int64_t n_states, const int64_t* prev, const uint8_t
   block_append(s < n_states && cand_count[s] > 0 && prev[s] >= 0 && !brk[s], s, list, count);
 }
 
+// the same steps in two lists within list[0, n_states): the small-search path tier's from
+// the front (count_front), the rest from the back (count_back); *n_all = n_states (the
+// retry collects scan the whole index range, whose gap keeps its zero flags)
+__global__ void k_step_lists(int64_t n_states, const int64_t* prev, const uint8_t* brk, const int32_t* cand_count,
+                             PathClass pc, int64_t* list, unsigned long long* count_front,
+                             unsigned long long* count_back, unsigned long long* n_all) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s == 0) *n_all = (unsigned long long)n_states;
+  const bool hit = s < n_states && cand_count[s] > 0 && prev[s] >= 0 && !brk[s];
+  bool small = false;
+  if (hit) {
+    const int64_t sp = prev[s];
+    const int md = pc.mode[pc.state_trace[s]] < OTR_MODES ? pc.mode[pc.state_trace[s]] : 0;
+    const uint32_t r = pc.trans[pc.trans_off[s] + (int64_t)pc.winner[sp] * cand_count[s] + pc.winner[s]];
+    const double b = fmin(floor(pc.bound[s] * 1000.0), (double)r) * 1e-3;  // (k_paths' bound, m)
+    small = !((pc.turn_modes >> md) & 1u) && pc.est4 * (float)(b * b) <= pc.small_keys;
+  }
+  // one atomic per wave and list
+  const unsigned long long mf = __ballot(hit && small), mb = __ballot(hit && !small);
+  const int lane = (int)(threadIdx.x % OTR_WAVE);
+  unsigned long long bf = 0, bb = 0;
+  if (lane == 0) {
+    if (mf) bf = atomicAdd(count_front, (unsigned long long)__popcll(mf));
+    if (mb) bb = atomicAdd(count_back, (unsigned long long)__popcll(mb));
+  }
+  bf = __shfl(bf, 0);
+  bb = __shfl(bb, 0);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  if (hit && small) list[bf + __popcll(mf & below)] = s;
+  if (hit && !small) list[n_states - 1 - (int64_t)(bb + __popcll(mb & below))] = s;
+}
+
 // work counters: fold the kCShards shards of every (bank, kind) into one value before the
 // copy-out (one block of kCShards threads per pair)
 __global__ __launch_bounds__(kCShards) void k_ctr_fold(const unsigned long long* in, unsigned long long* out) {
@@ -705,6 +737,8 @@ static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + b
 // "256,512x2,1024,4096".
 // the small-search tier's default size limit (keys of k_ntask's estimate; OTR_SMALL_KEYS)
 constexpr double kSmallKeys = 24.0;
+// the small-search path tier's (keys of k_step_lists' estimate; OTR_SMALL_PATH_KEYS)
+constexpr double kSmallPathKeys = 16.0;
 
 static std::vector<int> route_tiers() {
   std::vector<int> t;
@@ -880,8 +914,25 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   }
   if (S > 0) {
     tb(OTR_STAGE_CANDIDATES);
-    k_candidates<<<(unsigned)grid_candidates(S).blocks, 64, 0, stream>>>(g, b, mp, S, state_probe, state_trace, cb,
-                                                                   d_counters);
+    // two states per wave when no mode keeps more than 32 candidates (lane groups of 32) and
+    // no search radius can exceed 100 m (windows of a few cells: C2 1.86 -> 1.72 ms, C5 16.1
+    // -> 11.8 ms; C4's 200 m windows take 15.9 -> 22.1 ms with half the lanes each, so they
+    // keep a wave per state).  A probe's radius is min(max_search_radius, max(search_radius,
+    // accuracy)): without per-probe accuracies the mode's gps_accuracy stands for it.
+    bool kc32 = true;
+    for (int m = 0; m < OTR_MODES; ++m) {
+      const MatchParams& q = mp.m[m];
+      const double rmax = b.acc ? q.max_search_radius
+                                : std::min(q.max_search_radius, std::max(q.search_radius, q.gps_accuracy));
+      kc32 = kc32 && q.kmax <= 32 && rmax <= 100.0;
+    }
+    static const int cand_g = getenv("OTR_CAND_G") ? atoi(getenv("OTR_CAND_G")) : 2;  // A/B knob
+    if (kc32 && cand_g == 2)
+      k_candidates<2><<<(unsigned)grid_candidates((S + 1) / 2).blocks, 64, 0, stream>>>(g, b, mp, S, state_probe,
+                                                                                       state_trace, cb, d_counters);
+    else
+      k_candidates<1><<<(unsigned)grid_candidates(S).blocks, 64, 0, stream>>>(g, b, mp, S, state_probe, state_trace, cb,
+                                                                        d_counters);
     te(OTR_STAGE_CANDIDATES);
   }
   // ---- K_link + task map
@@ -1445,7 +1496,42 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   {
     int64_t* steps = need<int64_t>(S_LIST2, std::max<int64_t>(S, 1));
     unsigned long long* nsteps_d = cnt + 11;
-    if (S > 0) k_step_list<<<grid_for(S, 1024), 1024, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, nsteps_d);
+    // the small-search path tier (four searches per wave): steps whose winning route
+    // bounds a search of at most OTR_SMALL_PATH_KEYS keys (estimate: 4 x the node density
+    // x r^2, the diamond of road distance r around the root and its frontier); the
+    // two-search tier takes the rest.  Both lists' lengths come back to the host (one
+    // synchronisation) so each tier launches the blocks its list needs and no more (a grid
+    // sized for every step costs a dispatch per empty block: C5 paths 13.2 -> 18.8 ms
+    // instead of 8.3).  Only in batches whose route tasks went mostly to the small route
+    // tier (C5, C1): at C2 (3 % small) the synchronisation cost more than the tier saved.
+    static const double small_path_keys =
+        getenv("OTR_SMALL_PATH_KEYS") ? atof(getenv("OTR_SMALL_PATH_KEYS")) : kSmallPathKeys;  // A/B knob
+    const bool small_paths = small_path_keys > 0.0 && est_k > 0.f && (small_path_keys >= 1e8 || 2 * NT4 >= NT);
+    unsigned long long* nsteps4_d = cnt + 21;  // (the front list's count)
+    unsigned long long* nall_d = cnt + 22;     // (S: the collects' index range)
+    unsigned long long h_nsteps[2] = {0ull, 0ull};  // (front, back)
+    if (S > 0 && small_paths) {
+      PathClass pc{};
+      pc.winner = va.winner;
+      pc.trans_off = trans_off;
+      pc.trans = trans;
+      pc.bound = sb.bound;
+      pc.state_trace = state_trace;
+      pc.mode = b.mode;
+      pc.turn_modes = turn_modes;
+      pc.est4 = 8.f * est_k;  // (est_k = half the node density)
+      pc.small_keys = (float)small_path_keys;
+      HIPCHK(hipMemsetAsync(nsteps4_d, 0, 16, stream));
+      k_step_lists<<<grid_for(S, 256), 256, 0, stream>>>(S, sb.prev, va.brk, cb.count, pc, steps, nsteps4_d, nsteps_d,
+                                                          nall_d);
+      HIPCHK(hipMemcpyAsync(&h_nsteps[0], nsteps4_d, 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(&h_nsteps[1], nsteps_d, 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+    } else if (S > 0) {
+      k_step_list<<<grid_for(S, 1024), 1024, 0, stream>>>(S, sb.prev, va.brk, cb.count, steps, nsteps_d);
+    }
+    // the retry collects' index range: every step index (front and back lists), or the list
+    const unsigned long long* nscan_d = small_paths ? nall_d : nsteps_d;
     int32_t* step_ovf = need<int32_t>(S_STEP_OVF, S + 1);
     int64_t capacity = kShards * ((int64_t)S * 24 / kShards + 1024);
     bool paths_fit = S == 0;
@@ -1491,7 +1577,22 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       unsigned long long* pq = need<unsigned long long>(S_PQUEUE, 8 * kPQWords);
       HIPCHK(hipMemsetAsync(pq, 0, 8 * 8 * kPQWords, stream));
       tb(OTR_STAGE_PATHS);
-      {
+      if (small_paths) {
+        // the front list four searches per wave, the back list two, each grid sized by its
+        // list's length (blocks past a list's end exit at once, but cost a dispatch each)
+        if (h_nsteps[0] > 0) {
+          PathArgs p4 = pa;
+          p4.n_steps_dev = nsteps4_d;
+          k_paths<OTR_CAP4, 4><<<(unsigned)grid_paths((int64_t)(h_nsteps[0] + 1) / 2).blocks, 64, 0, stream>>>(
+              g, p4, nullptr, nullptr);
+        }
+        if (h_nsteps[1] > 0) {
+          PathArgs p2 = pa;
+          p2.from_back = true;
+          k_paths<OTR_CAP1, 2><<<(unsigned)grid_paths((int64_t)h_nsteps[1]).blocks, 64, 0, stream>>>(g, p2, nullptr,
+                                                                                                     nullptr);
+        }
+      } else {
         // (steps <= states: two searches per wave)
         k_paths<OTR_CAP1, 2><<<(unsigned)grid_paths(S).blocks, 64, 0, stream>>>(g, pa, nullptr, nullptr);
       }
@@ -1501,7 +1602,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       // launch's waves claim steps from its own per-XCD queue (XcdQueue)
       for (int tier = 0; tier < 3; ++tier) {
         unsigned long long* c = cnt + 12 + tier;
-        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0x2u, list, c);
+        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, 0x2u, list, c);
         PathArgs pb = pa;
         pb.queue = pq + tier * kPQWords;
         if (tier == 0) k_paths<512, 1><<<pgrid(16384, S), 64, 0, stream>>>(g, pb, list, c);
@@ -1512,7 +1613,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       if (turn_modes != 0u) {
         for (int et = 0; et < 2; ++et) {
           unsigned long long* c = cnt + 27 + et;
-          k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, et == 0 ? 0x20u : 0x40u,
+          k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, et == 0 ? 0x20u : 0x40u,
                                                                        list, c);
           PathArgs pb = pa;
           pb.queue = pq + (3 + et) * kPQWords;
@@ -1531,7 +1632,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       ga.cap_flag = (int32_t*)(cnt + 20);
       for (int gt = 0; gt < 2; ++gt) {
         unsigned long long* c = cnt + 16 + gt;
-        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, gt == 0 ? 0xAu : 0x2u, list,
+        k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, gt == 0 ? 0xAu : 0x2u, list,
                                                                      c);
         GSlabs gs2;
         if ((rc = slabs(gt, &gs2))) return rc;
@@ -1543,7 +1644,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         k_general<<<pgrid(gs2.n, S), kGenThreads, 0, stream>>>(g, ga, gs2);
       }
       // steps still flagged (beyond a 1M-state slab): named after the final sync
-      k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nsteps_d, step_ovf, 0xAu, list, cnt + 18);
+      k_collect_tier_list<<<grid_for(S, 1024), 1024, 0, stream>>>(nscan_d, step_ovf, 0xAu, list, cnt + 18);
       te(OTR_STAGE_PATHS_BIG);
       unsigned long long capflag = 0;
       std::vector<unsigned long long> cur(kShards);

@@ -168,32 +168,129 @@ __device__ inline bool project_edge(const DevGraph& g, uint4 rec, uint4 pts01, u
   return true;
 }
 
-constexpr int kWin = 16;  // flattened cell windows up to 16 x 16 cells
+// Wave sum (mod 2^32) by DPP row shifts and row broadcasts, result read from lane 63.
+__device__ inline uint32_t wave_sum_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_candidates(DevGraph g, BatchDev b, ModeParams mp, int64_t n_states,
-                                                   const int64_t* state_probe, const int32_t* state_trace,
-                                                   CandBuf out, unsigned long long* counters) {
-  __shared__ double s_d2[2 * OTR_WAVE];  // candidate list (≤ kmax + 64 entries), one buffer:
-  __shared__ double s_p[2 * OTR_WAVE];   // compaction stages each lane's ≤ 2 entries in registers
-  __shared__ uint32_t s_e[2 * OTR_WAVE];
-  __shared__ uint32_t s_bnd[kWin][kWin + 1];  // cell_row boundaries of the window, per row
-  __shared__ uint32_t s_pre[kWin + 1];        // entries before each row
-  const int lane = threadIdx.x;
-  const int64_t s = xcd_remap(blockIdx.x, (n_states + 7) / 8);
-  if (s >= n_states) return;
+// Wave minimum by DPP row shifts and row broadcasts (GFX9), result read from lane 63.
+__device__ inline uint32_t wave_min_u32(uint32_t v) {
+  const int I = -1;
+  auto mn = [](uint32_t a, int b) { return a < (uint32_t)b ? a : (uint32_t)b; };
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// G independent searches per wave, GL = 64 / G lanes each (G = 1, 2 or 4).  Per-group
+// ballots, prefix counts, minima and wave-uniform loop bounds.
+template <int G>
+struct Grp {
+  static constexpr int GL = OTR_WAVE / G;
+  __device__ static int g() { return G == 1 ? 0 : (int)threadIdx.x / GL; }
+  __device__ static int gl() { return G == 1 ? (int)threadIdx.x : (int)threadIdx.x % GL; }
+  __device__ static unsigned long long mine(unsigned long long m) {
+    return G == 1 ? m : (m >> (GL * g())) & ((1ull << GL) - 1ull);
+  }
+  // my group's set bits below my lane (G = 1: mbcnt, prefix_count)
+  __device__ static int prefix(unsigned long long m) {
+    if (G == 1) return prefix_count(m);
+    return __popcll(mine(m) & ((1ull << gl()) - 1ull));
+  }
+  __device__ static int count(unsigned long long m) { return __popcll(mine(m)); }
+  // maximum over groups of a group-uniform value (a wave-uniform loop bound)
+  __device__ static int umax(int v) {
+    if (G == 1) return __builtin_amdgcn_readfirstlane(v);
+    const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, GL);
+    if (G == 2) return a > b ? a : b;
+    const int c = __builtin_amdgcn_readlane(v, 2 * GL), d = __builtin_amdgcn_readlane(v, 3 * GL);
+    const int ab = a > b ? a : b, cd = c > d ? c : d;
+    return ab > cd ? ab : cd;
+  }
+  __device__ static bool all(bool v) {
+    if (G == 1) return __builtin_amdgcn_readfirstlane((int)v) != 0;
+    const bool ab = __builtin_amdgcn_readlane((int)v, 0) != 0 && __builtin_amdgcn_readlane((int)v, GL) != 0;
+    if (G == 2) return ab;
+    return ab && __builtin_amdgcn_readlane((int)v, 2 * GL) != 0 && __builtin_amdgcn_readlane((int)v, 3 * GL) != 0;
+  }
+  __device__ static uint32_t min_u32(uint32_t v) {
+    if (G == 1) return wave_min_u32(v);
+    const int I = -1;
+    auto mn = [](uint32_t a, int b) { return a < (uint32_t)b ? a : (uint32_t)b; };
+    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    if (G == 4) {  // a group is one DPP row: lane 15 of the row holds its minimum
+      const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+      const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+      const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+      const int q = g();
+      return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
+    }
+    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    return g() ? b : a;
+  }
+};
+
+constexpr int kWin = 16;  // flattened cell windows up to 16 x 16 cells
+// waves per SIMD of the two-states-per-wave candidate search (its registers)
+#ifndef OTR_CAND2_WAVES
+#define OTR_CAND2_WAVES 5
+#endif
+
+// K1: G states per wave (lane groups of GL = 64 / G; G = 2 when every mode keeps at most
+// 32 candidates: the search is a chain of dependent loads — probe, cell window, cell
+// records — so two states per wave keep twice the chains in flight).  Every loop runs to
+// the longer group's trip count (a group past its own idles), so the wave stays converged.
+template <int G>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? OTR_CAND2_WAVES : 8, 8))) void k_candidates(
+    DevGraph g, BatchDev b, ModeParams mp, int64_t n_states, const int64_t* state_probe, const int32_t* state_trace,
+    CandBuf out, unsigned long long* counters) {
+  using Gr = Grp<G>;
+  constexpr int GL = Gr::GL;
+  constexpr int LB = 2 * GL;                  // candidate list (<= kmax + GL entries), one buffer:
+  __shared__ double s_d2[G][LB];              // compaction stages each lane's <= 2 entries in registers
+  __shared__ double s_p[G][LB];
+  __shared__ uint32_t s_e[G][LB];
+  __shared__ uint32_t s_bnd[G][kWin][kWin + 1];  // cell_row boundaries of the window, per row
+  __shared__ uint32_t s_pre[G][kWin + 1];        // entries before each row
+  const int gi = Gr::g(), lane = Gr::gl();
+  const int64_t n_units = (n_states + G - 1) / G;
+  const int64_t s = xcd_remap(blockIdx.x, (n_units + 7) / 8) * G + gi;
+  if (Gr::umax(s < n_states ? 1 : 0) == 0) return;  // (wave-uniform)
+  const bool have = s < n_states;
 #ifdef OTR_STAMPS_CAND
   const unsigned long long cs0 = __builtin_amdgcn_s_memtime();
   unsigned long long cs1 = cs0, cs2 = cs0;
 #endif
-  const int64_t probe = state_probe[s];
-  const int mode = b.mode[state_trace[s]] < OTR_MODES ? b.mode[state_trace[s]] : 0;
-  const MatchParams& P = mp.m[mode];
+  const int64_t probe = have ? state_probe[s] : 0;
+  const int mode = have && b.mode[state_trace[s]] < OTR_MODES ? b.mode[state_trace[s]] : 0;
+  // the mode's parameters by selects (G = 2: the mode is a per-group register, and a
+  // register-indexed kernel argument would go through scratch)
+  auto pick = [&](auto f) { return mode == 0 ? f(mp.m[0]) : (mode == 1 ? f(mp.m[1]) : f(mp.m[OTR_MODES - 1])); };
   const uint32_t mode_bit = 1u << mode;
-  const int kmax = P.kmax;
+  const int kmax = pick([](const MatchParams& q) { return q.kmax; });
   const double plat = b.lat[probe], plon = b.lon[probe];
-  const double a = (b.acc && b.acc[probe] >= 0.f) ? (double)b.acc[probe] : P.gps_accuracy;
-  double radius = P.search_radius > a ? P.search_radius : a;
-  if (radius > P.max_search_radius) radius = P.max_search_radius;
+  const double a = (b.acc && b.acc[probe] >= 0.f) ? (double)b.acc[probe]
+                                                  : pick([](const MatchParams& q) { return q.gps_accuracy; });
+  const double sr0 = pick([](const MatchParams& q) { return q.search_radius; });
+  const double srmax = pick([](const MatchParams& q) { return q.max_search_radius; });
+  double radius = sr0 > a ? sr0 : a;
+  if (radius > srmax) radius = srmax;
   const double mpl = kMetersPerDeg * cos_deg(plat);
   const double cd = g.grid_cell_deg;
   const double dlat = radius / kMetersPerDeg, dlon = radius / mpl;
@@ -208,32 +305,36 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
   const double r2 = radius * radius;
   int n = 0;
   unsigned long long tests = 0;
-  // merge one wave's worth of qualifying candidates into the LDS top-K list
+  double* L_d2 = s_d2[gi];
+  double* L_p = s_p[gi];
+  uint32_t* L_e = s_e[gi];
+  // merge one pass's qualifying candidates into the group's LDS top-K list (every lane of
+  // the wave calls it: the barriers are the wave's)
   auto merge = [&](bool ok, double d2, double frac, uint32_t e) {
     const unsigned long long mask = __ballot(ok);
     if (!mask) return;
     if (ok) {
-      const int pos = n + prefix_count(mask);
-      s_d2[pos] = d2;
-      s_p[pos] = frac;
-      s_e[pos] = e;
+      const int pos = n + Gr::prefix(mask);
+      L_d2[pos] = d2;
+      L_p[pos] = frac;
+      L_e[pos] = e;
     }
-    n += __popcll(mask);
+    n += Gr::count(mask);
     __syncthreads();
-    if (n > kmax) {  // rank-compact to the kmax best (all (d2, edge) keys distinct)
+    if (Gr::umax(n > kmax ? 1 : 0)) {  // rank-compact to the kmax best (all (d2, edge) keys distinct)
       double dv[2], pv[2];
       uint32_t ev[2];
       int rk[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int idx = lane + h * OTR_WAVE;
+        const int idx = lane + h * GL;
         rk[h] = OTR_KMAX * 2;
-        if (idx < n) {
-          dv[h] = s_d2[idx];
-          pv[h] = s_p[idx];
-          ev[h] = s_e[idx];
+        if (n > kmax && idx < n) {
+          dv[h] = L_d2[idx];
+          pv[h] = L_p[idx];
+          ev[h] = L_e[idx];
           int rank = 0;
-          for (int m = 0; m < n; ++m) rank += cand_less(s_d2[m], s_e[m], dv[h], ev[h]);
+          for (int m = 0; m < n; ++m) rank += cand_less(L_d2[m], L_e[m], dv[h], ev[h]);
           rk[h] = rank;
         }
       }
@@ -241,45 +342,52 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
 #pragma unroll
       for (int h = 0; h < 2; ++h)
         if (rk[h] < kmax) {
-          s_d2[rk[h]] = dv[h];
-          s_p[rk[h]] = pv[h];
-          s_e[rk[h]] = ev[h];
+          L_d2[rk[h]] = dv[h];
+          L_p[rk[h]] = pv[h];
+          L_e[rk[h]] = ev[h];
         }
       __syncthreads();
-      n = kmax;
+      n = n > kmax ? kmax : n;
     }
   };
   const int nr = (int)(r1 - r0 + 1), nc = (int)(c1 - c0 + 1);
-  if (nr >= 1 && nc >= 1 && nr <= kWin && nc <= kWin) {
+  const bool win = have && nr >= 1 && nc >= 1 && nr <= kWin && nc <= kWin;
+  const bool slow = have && !win && nr >= 1 && nc >= 1;  // (a window past kWin cells: cell by cell)
+  if (Gr::umax(win ? 1 : 0)) {
     // The cells of one grid row are contiguous in cell_edge: flatten the window into
-    // one entry range per row and sweep all rows with full waves.
-    for (int idx = lane; idx < nr * (nc + 1); idx += OTR_WAVE) {
-      const int rr = idx / (nc + 1), cc = idx % (nc + 1);
-      s_bnd[rr][cc] = g.cell_row[(r0 + rr) * (int64_t)g.grid_cols + c0 + cc];
+    // one entry range per row and sweep all rows with full lane groups.
+    const int nb = win ? nr * (nc + 1) : 0;
+    const int nbx = Gr::umax(nb);
+    for (int idx = lane; idx < nbx; idx += GL) {
+      if (idx < nb) {
+        const int rr = idx / (nc + 1), cc = idx % (nc + 1);
+        s_bnd[gi][rr][cc] = g.cell_row[(r0 + rr) * (int64_t)g.grid_cols + c0 + cc];
+      }
     }
     __syncthreads();
-    if (lane == 0) {
+    if (win && lane == 0) {
       uint32_t acc = 0;
       for (int rr = 0; rr < nr; ++rr) {
-        s_pre[rr] = acc;
-        acc += s_bnd[rr][nc] - s_bnd[rr][0];
+        s_pre[gi][rr] = acc;
+        acc += s_bnd[gi][rr][nc] - s_bnd[gi][rr][0];
       }
-      s_pre[nr] = acc;
+      s_pre[gi][nr] = acc;
     }
     __syncthreads();
 #ifdef OTR_STAMPS_CAND
     cs1 = __builtin_amdgcn_s_memtime();
 #endif
-    const uint32_t total = s_pre[nr];
-    for (uint32_t base = 0; base < total; base += OTR_WAVE) {
+    const uint32_t total = win ? s_pre[gi][nr] : 0u;
+    const uint32_t totx = (uint32_t)Gr::umax((int)total);
+    for (uint32_t base = 0; base < totx; base += GL) {
       const uint32_t k = base + lane;
       bool ok = false;
       double d2 = 0, frac = 0;
       uint4 rec = make_uint4(0u, 0u, 0u, 0u);
       if (k < total) {
         int rr = 0;
-        while (rr + 1 < nr && s_pre[rr + 1] <= k) ++rr;
-        const uint32_t q = s_bnd[rr][0] + (k - s_pre[rr]);
+        while (rr + 1 < nr && s_pre[gi][rr + 1] <= k) ++rr;
+        const uint32_t q = s_bnd[gi][rr][0] + (k - s_pre[gi][rr]);
         rec = ld16(g.cell_rec + 3 * (size_t)q);
         const uint4 p01 = ld16(g.cell_rec + 3 * (size_t)q + 1), p23 = ld16(g.cell_rec + 3 * (size_t)q + 2);
         int64_t sr, sc;
@@ -287,7 +395,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
         // owned by the cell holding the snapped point: entry q lies in that cell's range
         if (ok) {
           const int64_t wr = sr - r0, wc = sc - c0;
-          ok = wr >= 0 && wr < nr && wc >= 0 && wc < nc && s_bnd[wr][wc] <= q && q < s_bnd[wr][wc + 1];
+          ok = wr >= 0 && wr < nr && wc >= 0 && wc < nc && s_bnd[gi][wr][wc] <= q && q < s_bnd[gi][wr][wc + 1];
         }
       }
       merge(ok, d2, frac, rec.x);
@@ -295,46 +403,53 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
 #ifdef OTR_STAMPS_CAND
     cs2 = __builtin_amdgcn_s_memtime();
 #endif
-  } else {
-    for (int64_t r = r0; r <= r1; ++r)
-      for (int64_t c = c0; c <= c1; ++c) {
-        const uint32_t cell = (uint32_t)(r * g.grid_cols + c);
-        const uint32_t beg = g.cell_row[cell], end = g.cell_row[cell + 1];
-        for (uint32_t base = beg; base < end; base += OTR_WAVE) {
-          const uint32_t q = base + lane;
-          bool ok = false;
-          double d2 = 0, frac = 0;
-          uint4 rec = make_uint4(0u, 0u, 0u, 0u);
-          if (q < end) {
-            rec = ld16(g.cell_rec + 3 * (size_t)q);
-            const uint4 p01 = ld16(g.cell_rec + 3 * (size_t)q + 1), p23 = ld16(g.cell_rec + 3 * (size_t)q + 2);
-            int64_t sr, sc;
-            ok = project_edge(g, rec, p01, p23, mode_bit, plat, plon, mpl, r2, &sr, &sc, &d2, &frac, &tests) &&
-                 sr == r &&
-                 sc == c;
-          }
-          merge(ok, d2, frac, rec.x);
+  }
+  if (Gr::umax(slow ? 1 : 0)) {
+    // cell by cell (the longer group's cell count; entries of a cell by passes of GL lanes)
+    const int ncell = slow ? nr * nc : 0;
+    const int ncx = Gr::umax(ncell);
+    for (int ci = 0; ci < ncx; ++ci) {
+      const bool act = ci < ncell;
+      const int64_t r = r0 + (act ? ci / nc : 0), c = c0 + (act ? ci % nc : 0);
+      const uint32_t cell = (uint32_t)(r * g.grid_cols + c);
+      const uint32_t beg = act ? g.cell_row[cell] : 0u, end = act ? g.cell_row[cell + 1] : 0u;
+      const int cnt = (int)(end - beg), cntx = Gr::umax(cnt);
+      for (int base = 0; base < cntx; base += GL) {
+        const uint32_t q = beg + (uint32_t)(base + lane);
+        bool ok = false;
+        double d2 = 0, frac = 0;
+        uint4 rec = make_uint4(0u, 0u, 0u, 0u);
+        if (base + lane < cnt) {
+          rec = ld16(g.cell_rec + 3 * (size_t)q);
+          const uint4 p01 = ld16(g.cell_rec + 3 * (size_t)q + 1), p23 = ld16(g.cell_rec + 3 * (size_t)q + 2);
+          int64_t sr, sc;
+          ok = project_edge(g, rec, p01, p23, mode_bit, plat, plon, mpl, r2, &sr, &sc, &d2, &frac, &tests) &&
+               sr == r && sc == c;
         }
+        merge(ok, d2, frac, rec.x);
       }
+    }
   }
   // final ordering
-  const size_t o = (size_t)s * OTR_KMAX;
-  for (int idx = lane; idx < n; idx += OTR_WAVE) {
-    const double d = s_d2[idx];
-    const uint32_t ee = s_e[idx];
-    int rank = 0;
-    for (int m = 0; m < n; ++m) rank += cand_less(s_d2[m], s_e[m], d, ee);
-    out.edge[o + rank] = ee;
-    out.p[o + rank] = s_p[idx];
-    out.sqd[o + rank] = d;
+  if (have) {
+    const size_t o = (size_t)s * OTR_KMAX;
+    for (int idx = lane; idx < n; idx += GL) {
+      const double d = L_d2[idx];
+      const uint32_t ee = L_e[idx];
+      int rank = 0;
+      for (int m = 0; m < n; ++m) rank += cand_less(L_d2[m], L_e[m], d, ee);
+      out.edge[o + rank] = ee;
+      out.p[o + rank] = L_p[idx];
+      out.sqd[o + rank] = d;
+    }
+    if (lane == 0) {
+      out.count[s] = n;
+      out.radius[s] = radius;
+    }
   }
-  if (lane == 0) {
-    out.count[s] = n;
-    out.radius[s] = radius;
-  }
-  for (int off = 32; off > 0; off >>= 1) tests += __shfl_xor(tests, off);
+  for (int off = GL / 2; off > 0; off >>= 1) tests += __shfl_xor(tests, off);  // (within the group)
 #ifdef OTR_STAMPS_CAND
-  if (lane == 0 && counters) {
+  if (threadIdx.x == 0 && counters) {
     const unsigned long long cs3 = __builtin_amdgcn_s_memtime();
     const int sh = cshard();
     atomicAdd(&counters[16 * kCShards + sh], cs1 - cs0);
@@ -342,7 +457,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
     atomicAdd(&counters[18 * kCShards + sh], cs3 - cs2);
   }
 #endif
-  if (lane == 0 && counters) {
+  if (have && lane == 0 && counters) {
     const int sh = cshard();
     atomicAdd(&counters[0 * kCShards + sh], (unsigned long long)((r1 - r0 + 1) * (c1 - c0 + 1)));
     atomicAdd(&counters[1 * kCShards + sh], tests);
@@ -434,84 +549,6 @@ __device__ inline unsigned long long group_bits(unsigned long long m) {
 // (label << 32 | edge id) so the minimum also records the smallest-id predecessor
 // edge among those achieving the label (the oracle's walk_path rule).
 // ------------------------------------------------------------------------------
-// Wave sum (mod 2^32) by DPP row shifts and row broadcasts, result read from lane 63.
-__device__ inline uint32_t wave_sum_u32(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-// Wave minimum by DPP row shifts and row broadcasts (GFX9), result read from lane 63.
-__device__ inline uint32_t wave_min_u32(uint32_t v) {
-  const int I = -1;
-  auto mn = [](uint32_t a, int b) { return a < (uint32_t)b ? a : (uint32_t)b; };
-  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
-  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
-  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
-  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
-  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-  v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-// G independent searches per wave, GL = 64 / G lanes each (G = 1, 2 or 4).  Per-group
-// ballots, prefix counts, minima and wave-uniform loop bounds.
-template <int G>
-struct Grp {
-  static constexpr int GL = OTR_WAVE / G;
-  __device__ static int g() { return G == 1 ? 0 : (int)threadIdx.x / GL; }
-  __device__ static int gl() { return G == 1 ? (int)threadIdx.x : (int)threadIdx.x % GL; }
-  __device__ static unsigned long long mine(unsigned long long m) {
-    return G == 1 ? m : (m >> (GL * g())) & ((1ull << GL) - 1ull);
-  }
-  // my group's set bits below my lane (G = 1: mbcnt, prefix_count)
-  __device__ static int prefix(unsigned long long m) {
-    if (G == 1) return prefix_count(m);
-    return __popcll(mine(m) & ((1ull << gl()) - 1ull));
-  }
-  __device__ static int count(unsigned long long m) { return __popcll(mine(m)); }
-  // maximum over groups of a group-uniform value (a wave-uniform loop bound)
-  __device__ static int umax(int v) {
-    if (G == 1) return __builtin_amdgcn_readfirstlane(v);
-    const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, GL);
-    if (G == 2) return a > b ? a : b;
-    const int c = __builtin_amdgcn_readlane(v, 2 * GL), d = __builtin_amdgcn_readlane(v, 3 * GL);
-    const int ab = a > b ? a : b, cd = c > d ? c : d;
-    return ab > cd ? ab : cd;
-  }
-  __device__ static bool all(bool v) {
-    if (G == 1) return __builtin_amdgcn_readfirstlane((int)v) != 0;
-    const bool ab = __builtin_amdgcn_readlane((int)v, 0) != 0 && __builtin_amdgcn_readlane((int)v, GL) != 0;
-    if (G == 2) return ab;
-    return ab && __builtin_amdgcn_readlane((int)v, 2 * GL) != 0 && __builtin_amdgcn_readlane((int)v, 3 * GL) != 0;
-  }
-  __device__ static uint32_t min_u32(uint32_t v) {
-    if (G == 1) return wave_min_u32(v);
-    const int I = -1;
-    auto mn = [](uint32_t a, int b) { return a < (uint32_t)b ? a : (uint32_t)b; };
-    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
-    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
-    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
-    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
-    if (G == 4) {  // a group is one DPP row: lane 15 of the row holds its minimum
-      const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
-      const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
-      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
-      const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-      const int q = g();
-      return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
-    }
-    v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
-    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-    return g() ? b : a;
-  }
-};
-
 // Label word of a search table, by label mode LM: 0 the packed (length << sh | time) word
 // in 32 bits; 1 (PRED) that word << 32 | the smallest predecessor edge; 2 (WIDE) the
 // packed word in 64 bits, for steps whose length and time bits exceed 32 (long gaps
@@ -582,7 +619,7 @@ struct SearchLds {
   // nodes settled per round (at most); k_paths (PRED) reuses pend + work as CAP u32 words
   // (1024 slots: 120, the 1-B codes' table then fits 13 waves per CU's LDS)
   // (the small tier's 80-slot tables: 16, so four tables fit 32 waves per CU: 4.5 KB per wave)
-  static constexpr int WCAP = CAP <= 96 ? OTR_WCAP4 : CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : (CAP <= 1024 ? 120 : 128)));
+  static constexpr int WCAP = CAP <= 96 ? (PRED ? 20 : OTR_WCAP4) : CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : (CAP <= 1024 ? 120 : 128)));
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
   WorkE<W> work[WCAP];                // this round's settled nodes: {node, label}
   int n_pend, n_keys, overflow;
@@ -2082,16 +2119,33 @@ struct PathArgs {
   const uint32_t* trans;
   int force_edge;              // test build only (OTR_FORCE_RETRY): RouteArgs::force_edge bits 3-4
   unsigned long long* queue;   // list tiers: this launch's per-XCD step counters (XcdQueue), zeroed
+  bool from_back;              // first tier: its steps are the last *n_steps_dev of steps[0, n_steps)
+                               // (k_step_lists: the small-search tier's at the front)
 };
 
-// G searches per wave (G = 2 for the first tier, lanes split 32/32), each a
-// single-target search from the winner's root with predecessor labels.  First tier:
-// step_list == null, the step count is read on the device (n_steps_dev), one unit per
-// block; retry tiers: a fixed grid strides over step_list[0 .. *list_count).
-// (Measured and dropped, DESIGN.md §6: a four-search 80-slot first tier for steps with a
-// short winning route: C5 paths 13.1 -> 18.8 ms.)
+// winner-path steps for the small-search path tier (k_paths<OTR_CAP4, 4>): the search is
+// bounded by the winning route r (k_paths), so its keys grow with r^2; a node-mode step
+// whose estimate est4 * min(B, r)^2 is at most small_keys goes to the front of the step
+// list, the rest to the back (k_step_lists)
+struct PathClass {
+  const int32_t* winner;
+  const int64_t* trans_off;
+  const uint32_t* trans;
+  const double* bound;
+  const int32_t* state_trace;
+  const uint8_t* mode;
+  uint32_t turn_modes;
+  float est4;                 // keys per m^2 of route length
+  float small_keys;
+};
+
+// G searches per wave (G = 2 for the first tier, lanes split 32/32; G = 4 the small-search
+// tier, 16 lanes each), each a single-target search from the winner's root with
+// predecessor labels.  First tiers: step_list == null, the step count is read on the
+// device (n_steps_dev), one unit per block; retry tiers: a fixed grid strides over
+// step_list[0 .. *list_count).
 template <int CAP, int G>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 : 8, 8))) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, const unsigned long long* list_count) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G >= 2 ? 6 : 8, 8))) void k_paths(DevGraph gr, PathArgs a, const int64_t* step_list, const unsigned long long* list_count) {
   using Gr = Grp<G>;
   __shared__ SearchLds<CAP, true> Ls[G];
   const int gl = Gr::gl();
@@ -2105,7 +2159,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(G == 2 ? 6 :
        w = step_list ? q.next() : wend) {
   const int64_t iw = w * G + Gr::g();
   const bool have = iw < n_list;
-  const int64_t k = have ? (step_list ? step_list[iw] : iw) : 0;
+  const int64_t k = have ? (step_list ? step_list[iw] : (a.from_back ? a.n_steps - n_list + iw : iw)) : 0;
   const int64_t s = have ? a.steps[k] : 0;
   const int64_t sp = have ? a.prev[s] : 0;
   bool active = false;

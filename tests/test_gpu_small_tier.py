@@ -1,8 +1,9 @@
-"""The small-search first tier (k_route<80,4>: four searches per wave, otr_kernels.h k_ntask)
-gives the two-search tier's results: the same batches with the tier off (OTR_SMALL_KEYS=0),
-at its default size limit, and with every eligible step sent to it (1e9: many of those
-searches outgrow the 80-slot table and go on to the retry tiers), each equal to the oracle
-field by field and to one another bit for bit.
+"""The small-search first tiers (k_route<80,4> and k_paths<80,4>: four searches per wave,
+otr_kernels.h k_ntask, otr_engine.hip k_step_lists) give the two-search tiers' results: the
+same batches with the tiers off (OTR_SMALL_KEYS=0, OTR_SMALL_PATH_KEYS=0), at their default
+size limits, and with every eligible step sent to them (1e9: many of those searches outgrow
+the 80-slot tables and go on to the retry tiers), each equal to the oracle field by field
+and to one another bit for bit.
 Runs in a child process per setting (the knob is read once per process)."""
 import os
 import subprocess
@@ -53,10 +54,11 @@ print('small ok')
 
 def _run(graph_dir, tmp_path, keys):
     env = dict(os.environ)
-    for k in ('OTR_SMALL_KEYS', 'OTR_TIERS', 'OTR_EST_K', 'OTR_LIB'):
+    for k in ('OTR_SMALL_KEYS', 'OTR_SMALL_PATH_KEYS', 'OTR_TIERS', 'OTR_EST_K', 'OTR_LIB'):
         env.pop(k, None)
-    if keys is not None:
+    if keys is not None:  # (route and winner-path small tiers alike)
         env['OTR_SMALL_KEYS'] = keys
+        env['OTR_SMALL_PATH_KEYS'] = keys
     dst = str(tmp_path / ('out_%s.pkl' % keys))
     p = subprocess.run([sys.executable, '-c', CHILD % (ROOT, graph_dir, dst)], env=env, capture_output=True,
                        text=True, timeout=240)
