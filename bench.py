@@ -465,7 +465,7 @@ def main():
     achieved = dom_bytes / (launch_ms * 1e-3) / 1e9
     # turn-cost modes run the route kernels compiled with the turn walk
     turns = float(W['meili'].get('turn_penalty_factor', 1.0)) > 0.0
-    tier_table = {kernel_name(d['code'], turns, t in (0, 12)): {'ms_per_launch': round(d['ms'] / d['launches'], 3),
+    tier_table = {kernel_name(d['code'], turns, t in (0, 12, 13)): {'ms_per_launch': round(d['ms'] / d['launches'], 3),
                                           'searches_per_launch': int(d['work'][0] // d['launches']),
                                           'settled_per_launch': int(d['work'][1] // d['launches']),
                                           'relaxed_per_launch': int(d['work'][2] // d['launches']),
@@ -487,7 +487,7 @@ def main():
     # (only a summary recorded from this build: same sources, the product library)
     if psum and os.path.exists(psum) and args.streams == 1:
         pj = json.load(open(psum))
-        k = pj.get('kernels', {}).get(kernel_name(dom['code'], turns, dom_t in (0, 12)), {})
+        k = pj.get('kernels', {}).get(kernel_name(dom['code'], turns, dom_t in (0, 12, 13)), {})
         if pj.get('build') != build_id:
             k = {}
             traffic_src = 'null: %s was recorded from build %s, this run is %s' % (
@@ -671,7 +671,7 @@ def main():
                                 # one from their HBM dump (otr_edge1.h), turn-cost modes only
                                 'edge_searches_dumped': int(counters[23]),
                                 'edge_searches_resumed': int(counters[22])}},
-            'roofline': {'kernel': kernel_name(dom['code'], turns, dom_t in (0, 12)) + ' (dominant route-search kernel of this workload)',
+            'roofline': {'kernel': kernel_name(dom['code'], turns, dom_t in (0, 12, 13)) + ' (dominant route-search kernel of this workload)',
                          'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': traffic,
                          'traffic_source': traffic_src, 'l2_hit': l2_hit, 'launch_ms': round(launch_ms, 3),

@@ -211,7 +211,8 @@ typedef struct otr_batch_result {
    * tiers in order, 6 / 7 the global-memory search (32K / 1M-state slabs), 8 the 64-bit
    * label LDS tier (steps whose length and time bits exceed 32), 10 the first edge-state
    * tier (modes with turn costs), 9 / 11 the larger edge-state tables (512, then 1024 states),
-   * 12 the small-search first tier (k_route<80,4>: steps expected to stay small), 13..15 unused.
+   * 12 the small-search first tier (k_route<80,4>: steps expected to stay small), 13 the
+   * tiny-search first tier (k_route<40,8>: at most 8 targets, tinier still), 14..15 unused.
    * code: 6,000,000 + CAP*100 + targets of an edge-state tier, CAP*10+G of an LDS tier,
    * 900000 + CAP the 64-bit tier, -1 / -2 the global tiers, 0 unused (a tier with no task
    * kind to run: the node tiers when every mode has turn costs).

@@ -399,7 +399,7 @@ enum Slot {
   S_TRACE_OFF, S_LAT, S_LON, S_TIME, S_ACC, S_MODE,
   S_STATE_CNT, S_TRACE_STATE_OFF, S_STATE_PROBE, S_STATE_TRACE,
   S_CAND_EDGE, S_CAND_P, S_CAND_SQD, S_CAND_COUNT, S_CAND_RADIUS,
-  S_PREV, S_G, S_BOUND, S_FORCED, S_NTASK, S_NTRANS, S_TASK_OFF, S_TRANS_OFF, S_NTASK4, S_TASK4_OFF, S_UNIT,
+  S_PREV, S_G, S_BOUND, S_FORCED, S_NTASK, S_NTRANS, S_TASK_OFF, S_TRANS_OFF, S_NTASK4, S_TASK4_OFF, S_NTASK8, S_TASK8_OFF, S_UNIT,
   S_TASK_STATE, S_TASK_MASK, S_TASK_OVF, S_TRANS,
   S_BP, S_BRK, S_END_WIN, S_WINNER, S_SUBPATH,
   S_PATH_OFF, S_PATH_LEN, S_PATH, S_STEP_OVF,
@@ -737,6 +737,8 @@ static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + b
 // "256,512x2,1024,4096".
 // the small-search tier's default size limit (keys of k_ntask's estimate; OTR_SMALL_KEYS)
 constexpr double kSmallKeys = 24.0;
+// the tiny-search tier's (eight searches per wave, at most 8 targets; OTR_TINY_KEYS)
+constexpr double kTinyKeys = 12.0;
 // the small-search path tier's (keys of k_step_lists' estimate; OTR_SMALL_PATH_KEYS)
 constexpr double kSmallPathKeys = 16.0;
 
@@ -862,9 +864,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   // counter banks of OTR_COUNTERS kinds x kCShards: 0 the batch (and the first route
   // tier), 1 the 512-state edge tier, 2..6 the LDS retry tiers, 7 the 64-bit tier, 8..9 the
   // global-memory tiers, 10 the first edge tier, 11 the 1024-state edge tier, 12 the
-  // small-search first tier; folded at
+  // small-search first tier, 13 the tiny-search one; folded at
   // the end into n_ctr values behind them
-  constexpr int kBanks = 13;
+  constexpr int kBanks = 14;
   const size_t bank = (size_t)OTR_COUNTERS * kCShards;
   const size_t n_ctr = kBanks * (size_t)OTR_COUNTERS;
   unsigned long long* d_counters = need<unsigned long long>(S_COUNTERS, kBanks * bank + n_ctr);
@@ -1007,10 +1009,14 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     for (int t = 0; t < n_est_tiers; ++t) est_tier_keys[t] = (uint32_t)((tl[t] / 10) * 7 / 8);
   }
   static const double small_keys = getenv("OTR_SMALL_KEYS") ? atof(getenv("OTR_SMALL_KEYS")) : kSmallKeys;  // A/B knob
+  static const double tiny_keys = getenv("OTR_TINY_KEYS") ? atof(getenv("OTR_TINY_KEYS")) : kTinyKeys;  // A/B knob
   const bool small_tier = route_g == 2 && k32 && small_keys > 0.0 && est_k > 0.f;
+  const bool tiny_tier = small_tier && tiny_keys > 0.0;
   int64_t* ntask4 = small_tier ? need<int64_t>(S_NTASK4, S) : nullptr;
   int64_t* task4_off = small_tier ? need<int64_t>(S_TASK4_OFF, S + 1) : nullptr;
-  if (small_tier && (!ntask4 || !task4_off)) {
+  int64_t* ntask8 = tiny_tier ? need<int64_t>(S_NTASK8, S) : nullptr;
+  int64_t* task8_off = tiny_tier ? need<int64_t>(S_TASK8_OFF, S + 1) : nullptr;
+  if ((small_tier && (!ntask4 || !task4_off)) || (tiny_tier && (!ntask8 || !task8_off))) {
     if (err) *err = "device allocation failed (task map)";
     return OTR_DEVICE_ERROR;
   }
@@ -1018,6 +1024,8 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   if (S > 0) {
     SmallArgs sa{};
     sa.ntask4 = ntask4;
+    sa.ntask8 = ntask8;
+    sa.tiny_keys = (float)tiny_keys;
     sa.bound = sb.bound;
     sa.bt = sb.bt;
     sa.forced = sb.forced;
@@ -1032,13 +1040,16 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   }
   if ((rc = scan(sb.ntask, task_off, S))) return rc;
   if (small_tier && (rc = scan(ntask4, task4_off, S))) return rc;
+  if (tiny_tier && (rc = scan(ntask8, task8_off, S))) return rc;
   if ((rc = scan(sb.ntrans, trans_off, S))) return rc;
-  int64_t NT = 0, NTR = 0, NT4 = 0;  // NT: every task; [0, NT4) the small tier's
+  // NT: every task; [0, NT8) the tiny tier's, [NT8, NT8 + NT4) the small tier's
+  int64_t NT = 0, NTR = 0, NT4 = 0, NT8 = 0;
   HIPCHK(hipMemcpyAsync(&NT, task_off + S, 8, hipMemcpyDeviceToHost, stream));
   if (small_tier) HIPCHK(hipMemcpyAsync(&NT4, task4_off + S, 8, hipMemcpyDeviceToHost, stream));
+  if (tiny_tier) HIPCHK(hipMemcpyAsync(&NT8, task8_off + S, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipMemcpyAsync(&NTR, trans_off + S, 8, hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
-  NT += NT4;
+  NT += NT4 + NT8;
   int32_t* task_ovf = need<int32_t>(S_TASK_OVF, NT);
   uint32_t* trans = need<uint32_t>(S_TRANS, NTR);
   uint32_t* trans_tc = need<uint32_t>(S_TRANS_TC, turn_modes ? NTR : 1);  // read for turn modes only
@@ -1068,6 +1079,9 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     ta.ntask4 = ntask4;
     ta.task4_off = task4_off;
     ta.nt4 = NT4;
+    ta.ntask8 = ntask8;
+    ta.task8_off = task8_off;
+    ta.nt8 = NT8;
     ta.flag_turn = task_ovf;  // turn-mode tasks start in the first edge-state tier (flag 5)
     // the two-search first tier's table: a step expected beyond it is flagged here
     ta.est_first_keys = route_g == 2 ? (OTR_CAP1 * OTR_LOAD1) / 8 : 0;
@@ -1243,15 +1257,35 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
       // The small tier (four searches per wave, tasks [0, NT4)) first, then the two-search
       // tier over the rest
       constexpr int64_t kMaxUnits = 1ll << 25;
-      if (NT4 > 0) {
+      // the tiny tier (eight searches per wave, tasks [0, NT8)) only in batches that are
+      // mostly tiny steps (C5); elsewhere its few tasks join the small tier's range (they are
+      // adjacent), which saves a launch (C1: 18k tiny tasks cost 2 %)
+      const bool tiny_run = NT8 > 0 && (2 * NT8 >= NT || tiny_keys >= 1e8);  // (1e8: tests force it)
+      const int64_t small_lo = tiny_run ? NT8 : 0;
+      if (tiny_run) {
+        unsigned long long* rc8 = rwork ? d_counters + 13 * bank : nullptr;
+        if (timing) (void)hipEventRecord(ev[24 + 2 * 13], stream);
+        const int64_t units = (NT8 + 7) / 8;
+        for (int64_t base = 0; base < units; base += kMaxUnits) {
+          RouteArgs rf = ra;
+          rf.n_tasks = NT8;
+          rf.unit_base = base;
+          const int64_t u = std::min<int64_t>(kMaxUnits, units - base);
+          OTR_ROUTE_LAUNCH(OTR_CAP8, 8, false, (unsigned)(8 * ((u + 7) / 8)), rf, rc8);
+        }
+        if (timing) (void)hipEventRecord(ev[24 + 2 * 13 + 1], stream);
+        out->route_tier_code[13] = OTR_CAP8 * 10 + 8;
+      }
+      if (NT8 + NT4 - small_lo > 0) {
         unsigned long long* rc4 = rwork ? d_counters + 12 * bank : nullptr;
         if (timing) (void)hipEventRecord(ev[24 + 2 * 12], stream);
-        const int64_t units = (NT4 + 3) / 4;
+        const int64_t units = (NT8 + NT4 - small_lo + 3) / 4;
         // (a block per unit: a persistent grid over per-XCD queues was slower, C5 26.5 ->
         // 35.6 ms)
         for (int64_t base = 0; base < units; base += kMaxUnits) {
           RouteArgs rf = ra;
-          rf.n_tasks = NT4;
+          rf.n_tasks = NT8 + NT4;
+          rf.task_base = small_lo;
           rf.unit_base = base;
           const int64_t u = std::min<int64_t>(kMaxUnits, units - base);
           OTR_ROUTE_LAUNCH(OTR_CAP4, 4, false, (unsigned)(8 * ((u + 7) / 8)), rf, rc4);
@@ -1259,11 +1293,11 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
         if (timing) (void)hipEventRecord(ev[24 + 2 * 12 + 1], stream);
         out->route_tier_code[12] = OTR_CAP4 * 10 + 4;
       }
-      const int64_t units = route_g == 2 ? (NT - NT4 + 1) / 2 : NT;
+      const int64_t units = route_g == 2 ? (NT - NT8 - NT4 + 1) / 2 : NT;
       for (int64_t base = 0; base < units; base += kMaxUnits) {
         RouteArgs rf = ra;
         rf.unit_base = base;
-        rf.task_base = NT4;
+        rf.task_base = NT8 + NT4;
         const int64_t u = std::min<int64_t>(kMaxUnits, units - base);
         const unsigned grid = (unsigned)(8 * ((u + 7) / 8));
         if (route_g == 2) OTR_ROUTE_LAUNCH(OTR_CAP1, 2, false, grid, rf, rwork);
@@ -1506,7 +1540,7 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     // tier (C5, C1): at C2 (3 % small) the synchronisation cost more than the tier saved.
     static const double small_path_keys =
         getenv("OTR_SMALL_PATH_KEYS") ? atof(getenv("OTR_SMALL_PATH_KEYS")) : kSmallPathKeys;  // A/B knob
-    const bool small_paths = small_path_keys > 0.0 && est_k > 0.f && (small_path_keys >= 1e8 || 2 * NT4 >= NT);
+    const bool small_paths = small_path_keys > 0.0 && est_k > 0.f && (small_path_keys >= 1e8 || 2 * (NT4 + NT8) >= NT);
     unsigned long long* nsteps4_d = cnt + 21;  // (the front list's count)
     unsigned long long* nall_d = cnt + 22;     // (S: the collects' index range)
     unsigned long long h_nsteps[2] = {0ull, 0ull};  // (front, back)
@@ -1850,11 +1884,11 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
     return hc[(size_t)b * OTR_COUNTERS + (size_t)k];
   };
   for (int k = 0; k < OTR_COUNTERS; ++k) out->counters[k] = ctr(0, k);
-  for (int k : {3, 4, 13, 14}) out->counters[k] += ctr(12, k);  // (the first tier: both launches)
+  for (int k : {3, 4, 13, 14}) out->counters[k] += ctr(12, k) + ctr(13, k);  // (the first tier: every launch)
   // per route kernel: searches, settled, relaxed, transition entries (banks 0, 2..6, 8..9;
   // slot 8, the 64-bit LDS tier: bank 7; the edge-state tiers: slot 10 the first (bank 10),
   // slot 9 the 512-state one (bank 1), slot 11 the 1024-state one (bank 11))
-  for (int t = 0; t < 13; ++t) {
+  for (int t = 0; t < 14; ++t) {
     const int b = t == 0 ? 0 : (t < 6 ? 1 + t : (t < 8 ? 2 + t : (t == 8 ? 7 : (t == 9 ? 1 : t))));
     out->route_tier_work[t][0] = ctr(b, 6);
     out->route_tier_work[t][1] = ctr(b, 3);
@@ -1884,11 +1918,11 @@ int Matcher::run_impl(const otr_trace_batch* in, const ModeParams& mp, otr_batch
   if (timing) {
     for (int k = 0; k < 10; ++k)
       if (used[k]) (void)hipEventElapsedTime(&out->kernel_ms[k], ev[2 * k], ev[2 * k + 1]);
-    for (int t = 1; t < 13; ++t)
+    for (int t = 1; t < 14; ++t)
       if (out->route_tier_code[t] != 0)
         (void)hipEventElapsedTime(&out->route_tier_ms[t], ev[24 + 2 * t], ev[24 + 2 * t + 1]);
-    // (the route stage holds the small tier's launches, then the two-search tier's)
-    out->route_tier_ms[0] = out->kernel_ms[OTR_STAGE_ROUTE] - out->route_tier_ms[12];
+    // (the route stage holds the tiny and small tiers' launches, then the two-search tier's)
+    out->route_tier_ms[0] = out->kernel_ms[OTR_STAGE_ROUTE] - out->route_tier_ms[12] - out->route_tier_ms[13];
     (void)hipGetLastError();  // an unrecorded pair must not leave a sticky error for the next call
   }
   // ---- copy-out (tests / JSON path), compacting the capacity layout

@@ -192,7 +192,7 @@ __device__ inline uint32_t wave_min_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-// G independent searches per wave, GL = 64 / G lanes each (G = 1, 2 or 4).  Per-group
+// G independent searches per wave, GL = 64 / G lanes each (G = 1, 2, 4 or 8).  Per-group
 // ballots, prefix counts, minima and wave-uniform loop bounds.
 template <int G>
 struct Grp {
@@ -211,6 +211,15 @@ struct Grp {
   // maximum over groups of a group-uniform value (a wave-uniform loop bound)
   __device__ static int umax(int v) {
     if (G == 1) return __builtin_amdgcn_readfirstlane(v);
+    if (G == 8) {
+      int m = __builtin_amdgcn_readlane(v, 0);
+#pragma unroll
+      for (int q = 1; q < 8; ++q) {
+        const int x = __builtin_amdgcn_readlane(v, q * GL);
+        m = x > m ? x : m;
+      }
+      return m;
+    }
     const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, GL);
     if (G == 2) return a > b ? a : b;
     const int c = __builtin_amdgcn_readlane(v, 2 * GL), d = __builtin_amdgcn_readlane(v, 3 * GL);
@@ -219,12 +228,26 @@ struct Grp {
   }
   __device__ static bool all(bool v) {
     if (G == 1) return __builtin_amdgcn_readfirstlane((int)v) != 0;
+    if (G == 8) {
+      bool r = true;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) r = r && __builtin_amdgcn_readlane((int)v, q * GL) != 0;
+      return r;
+    }
     const bool ab = __builtin_amdgcn_readlane((int)v, 0) != 0 && __builtin_amdgcn_readlane((int)v, GL) != 0;
     if (G == 2) return ab;
     return ab && __builtin_amdgcn_readlane((int)v, 2 * GL) != 0 && __builtin_amdgcn_readlane((int)v, 3 * GL) != 0;
   }
   __device__ static uint32_t min_u32(uint32_t v) {
     if (G == 1) return wave_min_u32(v);
+    if (G == 8) {  // (8-lane groups: a butterfly of lane swaps within the group)
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        const uint32_t x = (uint32_t)__shfl_xor((int)v, o, 8);
+        v = x < v ? x : v;
+      }
+      return v;
+    }
     const int I = -1;
     auto mn = [](uint32_t a, int b) { return a < (uint32_t)b ? a : (uint32_t)b; };
     v = mn(v, __builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
@@ -619,7 +642,7 @@ struct SearchLds {
   // nodes settled per round (at most); k_paths (PRED) reuses pend + work as CAP u32 words
   // (1024 slots: 120, the 1-B codes' table then fits 13 waves per CU's LDS)
   // (the small tier's 80-slot tables: 16, so four tables fit 32 waves per CU: 4.5 KB per wave)
-  static constexpr int WCAP = CAP <= 96 ? (PRED ? 20 : OTR_WCAP4) : CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : (CAP <= 1024 ? 120 : 128)));
+  static constexpr int WCAP = CAP <= 48 ? 8 : CAP <= 96 ? (PRED ? 20 : OTR_WCAP4) : CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : (CAP <= 1024 ? 120 : 128)));
   Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
   WorkE<W> work[WCAP];                // this round's settled nodes: {node, label}
   int n_pend, n_keys, overflow;
@@ -1224,8 +1247,14 @@ __global__ __launch_bounds__(256) void k_prep(DevGraph g, PrepArgs a) {
 #ifndef OTR_CAP4
 #define OTR_CAP4 80
 #endif
+// the tiny-search tier (k_route<OTR_CAP8, 8>: eight searches per wave, 8 lanes each)
+#ifndef OTR_CAP8
+#define OTR_CAP8 40
+#endif
 struct SmallArgs {
   int64_t* ntask4;            // per state: the step's tasks when they go to the small tier, else 0
+  int64_t* ntask8;            // per state: ... to the tiny tier (null: none)
+  float tiny_keys;            // a step of at most 8 targets whose estimate is at most this is tiny
   const double* bound;
   const int32_t* bt;
   const uint8_t* forced;
@@ -1248,7 +1277,7 @@ __global__ void k_ntask(int64_t n_states, const int64_t* prev, const int32_t* nr
   if (s >= n_states) return;
   const int64_t sp = prev[s];  // -1: first state of a sub-trace, -2: no candidates (k_link)
   const int64_t n = sp >= 0 ? nroot[sp] : 0;
-  bool small = false;
+  bool small = false, tiny = false;
   if (sa.ntask4 != nullptr && n > 0 && sa.cand_count[s] <= OTR_WAVE / 4 && !sa.forced[s]) {
     const int md = sa.mode[sa.state_trace[s]] < OTR_MODES ? sa.mode[sa.state_trace[s]] : 0;
     const uint32_t bmm = (uint32_t)bound_mm_of(sa.bound[s]);
@@ -1261,11 +1290,14 @@ __global__ void k_ntask(int64_t n_states, const int64_t* prev, const int32_t* nr
     if (!general) {
       float reach = (float)bmm * 1e-3f;
       if (bt >= 0) reach = fminf(reach, (float)bt * 0.1f * sa.est_v[md]);
-      small = sa.est_k * reach * reach <= sa.small_keys;
+      const float est = sa.est_k * reach * reach;
+      small = est <= sa.small_keys;
+      tiny = sa.ntask8 != nullptr && sa.cand_count[s] <= OTR_WAVE / 8 && est <= sa.tiny_keys;
     }
   }
-  if (sa.ntask4 != nullptr) sa.ntask4[s] = small ? n : 0;
-  ntask[s] = small ? 0 : n;
+  if (sa.ntask8 != nullptr) sa.ntask8[s] = tiny ? n : 0;
+  if (sa.ntask4 != nullptr) sa.ntask4[s] = small && !tiny ? n : 0;
+  ntask[s] = small || tiny ? 0 : n;
 }
 
 // ------------------------------------------------------------------------------
@@ -1345,8 +1377,11 @@ struct TaskArgs {
   uint4* rec;                 // 3 per task (the K2c record, below; the state and source mask of a task
                               // are read from it everywhere: no separate per-task arrays)
   const int64_t* ntask4;      // small-tier steps' task counts (k_ntask), or null
-  const int64_t* task4_off;   // their exclusive offsets: small-tier tasks are [0, nt4)
-  int64_t nt4;                // two-search tasks are nt4 + task_off[s]
+  const int64_t* task4_off;   // their exclusive offsets: small-tier tasks are [nt8, nt8 + nt4)
+  int64_t nt4;                // two-search tasks are nt8 + nt4 + task_off[s]
+  const int64_t* ntask8;      // tiny-tier steps' task counts, or null
+  const int64_t* task8_off;   // their exclusive offsets: tiny-tier tasks are [0, nt8)
+  int64_t nt8;
   int32_t* flag_turn;         // per task: 5 for a turn-mode task (the first edge-state tier's list), or null
   // the two-search first tier's size estimate (RouteArgs est_*): a node-mode step whose
   // estimated keys exceed est_first_keys (0: no estimate) starts in a retry tier
@@ -1406,8 +1441,9 @@ __global__ __launch_bounds__(256) void k_tasks(TaskArgs a) {
   if (!rep) return;
   // the step's task range: the small tier's first, then the two-search tier's (k_ntask)
   const int64_t n4 = a.ntask4 != nullptr ? a.ntask4[s] : 0;
-  const int64_t tbase = n4 > 0 ? a.task4_off[s] : a.nt4 + a.task_off[s];
-  const int64_t tend = n4 > 0 ? tbase + n4 : a.nt4 + a.task_off[s + 1];
+  const int64_t n8 = a.ntask8 != nullptr ? a.ntask8[s] : 0;
+  const int64_t tbase = n8 > 0 ? a.task8_off[s] : (n4 > 0 ? a.nt8 + a.task4_off[s] : a.nt8 + a.nt4 + a.task_off[s]);
+  const int64_t tend = n8 > 0 ? tbase + n8 : (n4 > 0 ? tbase + n4 : a.nt8 + a.nt4 + a.task_off[s + 1]);
   const int64_t o = tbase + __popcll(reps & ((1ull << lane) - 1ull));
   if (o >= tend) return;  // the count (k_prep's nroot) and this rule agree; never write past it
   const uint32_t bmm = (uint32_t)bound_mm_of(a.bound[s]);
