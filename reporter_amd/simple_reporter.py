@@ -2,15 +2,22 @@
 batched HIP API.  S3 download/upload (simple_reporter.py:51-129, 247-254) is out of
 scope (network); inputs and outputs are local files.
 
+The product path (every stage on the device):
+  report(m, traces, privacy, ...)  windows → one batch → K9 tile rows → K10 sort + cull in HBM
+                                   → CSV lines per tile (= report_tiles_device)
+  text_tiles_device(m, text, p)    shard / raw probe text → tiles, every stage in HBM
+                                   (K11 ingest :99-111,136-160 → K1-K10)
+  stream_tiles_device(m, tr, p)    the Java streaming output stage (AnonymisingProcessor)
   shard_key(uuid)                  sha1(uuid)[0:3]                (:116)
   windows(times, inactivity)       inactivity windows             (:150-160)
+
+The host mirror of the reference's loops (small inputs, and the goldens that pin K9/K10:
+tests/test_golden_tiles.py, tests/test_gpu_tiles.py compares the two paths):
   bucket(first, last, reports, q, mode, source)
                                    filter + hour buckets → rows   (:176-196)
   cull(lines, privacy)             privacy cull incl. the trailing-singleton merge (:218-239)
-  match_traces(traces, ...)        windows → otr_match_batch → rows per tile
+  match_traces(traces, ...)        windows → otr_match_batch → rows per tile (host bucketing)
   report_tiles(tiles, privacy)     sort + cull                    (:211-245)
-  text_tiles_device(m, text, p)    shard / raw probe text → tiles, every stage in HBM
-                                   (K11 ingest :99-111,136-160 → K1-K10)
 """
 import hashlib
 import math
@@ -278,6 +285,13 @@ def report_tiles_device(matcher, traces, privacy, mode='auto', report_levels=(0,
                             threshold_sec=threshold_sec, quantisation=quantisation, copy_out=False, tile_rows=True)
     kept = cull_rows(matcher, None, privacy, device_ptr=r.d_rows, n=r.n_rows)
     return rows_to_tiles(kept, quantisation, mode, source)
+
+
+def report(matcher, traces, privacy, **kw):
+    """simple_reporter's match() + report() + cull for a batch of traces, the product path:
+    every stage on the device (report_tiles_device).  The host functions bucket / cull /
+    match_traces / report_tiles give the same tiles (tests/test_gpu_tiles.py)."""
+    return report_tiles_device(matcher, traces, privacy, **kw)
 
 
 def text_tiles_device(matcher, text, privacy, rules=0, mode='auto', report_levels=(0, 1), transition_levels=(0, 1),

@@ -100,6 +100,7 @@ def test_report_tiles_device_equals_host_path(city):
     want = sr.report_tiles(sr.match_traces(m, tr), 2)
     got = sr.report_tiles_device(m, tr, 2)
     assert got == want and len(got) > 0
+    assert sr.report(m, tr, 2) == want  # (the module's product entry point: the device path)
 
 
 @pytest.fixture(scope='module')

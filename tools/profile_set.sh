@@ -16,7 +16,7 @@ shift
 for W in "$@"; do
   O=gpurun_out/$TAG/$W
   mkdir -p $O
-  ARGS="--workload $W --cpu-traces 0 --e2e-steps 0"
+  ARGS="--workload $W --cpu-traces 0 --e2e-steps 0 --json-traces 0"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- \
     python3 bench.py $ARGS --steps 5 --warmup 2 > $O/bench_kt.json 2> $O/bench_kt.err
   for P in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
