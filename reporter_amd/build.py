@@ -30,7 +30,9 @@ def source_hash():
     """Identity of the libotr.so sources (the HIP/C++ sources, headers and compile flags):
     a PMC summary recorded from one build is attached to bench lines of that build only."""
     import hashlib
-    h = hashlib.sha1(' '.join(HIP_FLAGS[1:]).encode())
+    # (the flags without the include path: the same sources built in another checkout —
+    # the GPU box's copy, /root/repo or its symlink target — are the same build)
+    h = hashlib.sha1(' '.join(f for f in HIP_FLAGS[1:] if not f.startswith('-I')).encode())
     for d in (CSRC, os.path.join(ROOT, 'include')):
         for f in sorted(os.listdir(d)):
             if f.endswith(('.h', '.hip', '.cpp')):
