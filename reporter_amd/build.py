@@ -167,9 +167,12 @@ def build_all(force=False):
     with ThreadPoolExecutor(max_workers=3) as ex:
         futs = [ex.submit(build_otr, force),
                 # test build: every first-tier search goes down the retry tiers (tests/test_gpu_tiers.py)
-                # (and every node retry tier resumes / dumps: OTR_ND_IN_MIN / OTR_ND_OUT_MIN 0)
+                # (and every node retry tier resumes / dumps: OTR_ND_IN_MIN / OTR_ND_OUT_MIN 0;
+                # short pending lists in the 1024- / 2048-slot and the first edge-state tables,
+                # so searches whose frontier outgrows them take the restart path)
                 ex.submit(build_otr, force, False, 'tiercheck', ['OTR_FORCE_RETRY', 'OTR_ND_IN_MIN=0',
-                                                                 'OTR_ND_OUT_MIN=0']),
+                                                                 'OTR_ND_OUT_MIN=0', 'OTR_PCAP1024=96',
+                                                                 'OTR_PCAP2048=160', 'OTR_E1PCAP=64']),
                 # test build: every search in the global-memory kernel (tests/test_gpu_tiers.py)
                 ex.submit(build_otr, force, False, 'generalcheck', ['OTR_FORCE_GENERAL'])]
         lib = futs[0].result()

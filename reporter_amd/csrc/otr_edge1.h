@@ -57,6 +57,11 @@ __device__ inline uint32_t er_hbk(const uint4& r) { return (uint32_t)heading_bac
 #ifndef OTR_E1SINK
 #define OTR_E1SINK 16
 #endif
+// pending-list entries of the first table (at most OTR_E1CAP)
+// (96: 23 waves per CU, but the 512-state tier's restarts cost more, 7.3 -> 9.6 ms)
+#ifndef OTR_E1PCAP
+#define OTR_E1PCAP OTR_E1CAP
+#endif
 // waves per SIMD the compiler fits the kernel's registers for (8: 64 VGPRs)
 #ifndef OTR_E1WAVES
 #define OTR_E1WAVES 8
@@ -72,7 +77,10 @@ struct E1Lds {
   unsigned long long lab[CAP];  // gpack label, kGInf: none
   uint32_t key[CAP];            // edge id | kInq (on the pending list, or settled); kEmpty
   uint8_t mi[CAP];              // mi8_of(len(edge)): the IN criterion's gap (0 at the root)
-  Idx pend[CAP];                // pending slots
+  // pending list capacity: the first table's may be shorter (OTR_E1PCAP: LDS for more
+  // resident waves; a search whose frontier outgrows it restarts in the next table)
+  static constexpr int PCAP = CAP == OTR_E1CAP ? OTR_E1PCAP : CAP;
+  Idx pend[PCAP];               // pending slots
   uint4 wst[WCAP];              // this round's settled states: {label lo, hi, edge, mi} (one 16-B access)
   unsigned long long tlab[TG];  // the targets' best feasible offers
   uint32_t tpart[TG], tpt[TG];  // entry parts (mm, 0.1 s)
@@ -521,7 +529,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
           }
           nkeys += __popcll(__ballot(isnew));
           const unsigned long long mp = __ballot(psl >= 0);
-          if (psl >= 0) L.pend[npend + prefix_count(mp)] = (typename LT::Idx)psl;  // (< CAP: one entry per state)
+          if (psl >= 0 && (LT::PCAP == CAP || npend + prefix_count(mp) < LT::PCAP))  // (< CAP: one entry per state)
+            L.pend[npend + prefix_count(mp)] = (typename LT::Idx)psl;
           npend += __popcll(mp);
         }
         if (__ballot(tail != 0u) != 0ull) {  // nodes with more than four out-edges: the CSR tail
@@ -548,7 +557,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
                   const int p2 = e1_relax(L, lb, pk.x | ((pk.z & 7u) << 28), pk.y, timed ? et[e] : 0u, e, deg, pd, pt,
                                           mode_bit, my_relaxed, knext, dnext, tnext, nw2);
                   if (nw2) atomicAdd(&L.n_keys, 1);
-                  if (p2 >= 0) L.pend[atomicAdd(&L.n_pend, 1)] = (typename LT::Idx)p2;
+                  if (p2 >= 0) {
+                    const int p = atomicAdd(&L.n_pend, 1);
+                    if (LT::PCAP == CAP || p < LT::PCAP) L.pend[p] = (typename LT::Idx)p2;
+                  }
                 }
               }
             }
@@ -568,9 +580,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OTR_E1WAVES,
         cyc_part += tr2 - tr1;
         cyc_relax += tr3 - tr2;
 #endif
-        if (L.overflow || nkeys > kMaxKeys) {
+        // (a pending list past its capacity lost appends, as a full table loses a
+        // relaxation: that search restarts)
+        const bool pover = LT::PCAP < CAP && npend > LT::PCAP;
+        if (L.overflow || pover || nkeys > kMaxKeys) {
           ok = false;
-          dump = !L.overflow;  // (a full table lost a relaxation: that search restarts)
+          dump = !L.overflow && !pover;  // (a full table lost a relaxation: that search restarts)
           break;
         }
 #ifdef OTR_FORCE_RETRY  // test build: OTR_FORCE_EDGE bit 5 / 6 stops every OTR_E1CAP / 512-state search

@@ -612,6 +612,18 @@ struct WorkE {
 };
 
 
+#ifndef OTR_PCAP1024
+#define OTR_PCAP1024 512
+#endif
+#ifndef OTR_PCAP2048
+#define OTR_PCAP2048 512
+#endif
+#ifndef OTR_PCAP448
+#define OTR_PCAP448 448
+#endif
+#ifndef OTR_WCAP1024
+#define OTR_WCAP1024 120
+#endif
 // settles per round of the small tier's 80-slot tables (four tables per wave in 32 waves'
 // LDS: at most 28)
 #ifndef OTR_WCAP4
@@ -642,8 +654,12 @@ struct SearchLds {
   // nodes settled per round (at most); k_paths (PRED) reuses pend + work as CAP u32 words
   // (1024 slots: 120, the 1-B codes' table then fits 13 waves per CU's LDS)
   // (the small tier's 80-slot tables: 16, so four tables fit 32 waves per CU: 4.5 KB per wave)
-  static constexpr int WCAP = CAP <= 48 ? 8 : CAP <= 96 ? (PRED ? 20 : OTR_WCAP4) : CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : (CAP <= 1024 ? 120 : 128)));
-  Idx pend[CAP];                      // pending slots (k_paths reuses pend+work as CAP u32)
+  static constexpr int WCAP = CAP <= 48 ? 8 : CAP <= 96 ? (PRED ? 20 : OTR_WCAP4) : CAP <= 160 ? 48 : (PRED ? CAP / 4 : (CAP <= 512 ? 64 : (CAP <= 1024 ? OTR_WCAP1024 : 128)));
+  // pending list capacity: the 1024-slot table's may be shorter (OTR_PCAP1024: LDS for
+  // more resident waves; a search whose frontier outgrows it restarts in the next table)
+  static constexpr int PCAP = PRED ? CAP
+                                    : (CAP == 1024 ? OTR_PCAP1024 : (CAP == 2048 ? OTR_PCAP2048 : (CAP == 448 ? OTR_PCAP448 : CAP)));
+  Idx pend[PCAP];                     // pending slots (k_paths reuses pend+work as CAP u32)
   WorkE<W> work[WCAP];                // this round's settled nodes: {node, label}
   int n_pend, n_keys, overflow;
 };
@@ -953,8 +969,12 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
         pend = (key & kInq) != 0u;
       }
       const unsigned long long mp = __ballot(pend);
-      if (pend) L.pend[np + Gr::prefix(mp)] = (Idx)sl;
+      if (pend && np + Gr::prefix(mp) < SearchLds<CAP, LM>::PCAP) L.pend[np + Gr::prefix(mp)] = (Idx)sl;
       np += Gr::count(mp);
+    }
+    if (resume && np > SearchLds<CAP, LM>::PCAP) {  // (a frontier past the pending list: restart)
+      if (gl == 0) L.overflow = 1;
+      np = SearchLds<CAP, LM>::PCAP;
     }
     if (resume) {
       npend = np;
@@ -1074,15 +1094,21 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
         // append writes its scratch word (< CAP: the pending nodes are distinct keys of the
         // table; clamped)
         const int p = npend + Gr::prefix(mp);
-        *(psl >= 0 ? &L.pend[p < CAP ? p : CAP - 1] : reinterpret_cast<Idx*>(sink + lane_id())) = (Idx)psl;
+        constexpr int PC = SearchLds<CAP, LM>::PCAP;
+        *(psl >= 0 ? &L.pend[p < PC ? p : PC - 1] : reinterpret_cast<Idx*>(sink + lane_id())) = (Idx)psl;
       } else
 #endif
       if (psl >= 0) {
         // (< CAP: the pending nodes are distinct keys of the table; clamped, not branched)
         const int p = npend + Gr::prefix(mp);
-        L.pend[p < CAP ? p : CAP - 1] = (Idx)psl;
+        L.pend[p < SearchLds<CAP, LM>::PCAP ? p : SearchLds<CAP, LM>::PCAP - 1] = (Idx)psl;
       }
       npend += Gr::count(mp);
+    }
+    // (a pending list past its capacity lost appends: the search restarts in the next table)
+    if (SearchLds<CAP, LM>::PCAP < CAP && npend > SearchLds<CAP, LM>::PCAP) {
+      if (gl == 0) L.overflow = 1;
+      npend = SearchLds<CAP, LM>::PCAP;
     }
     if (__ballot(tail != 0u) != 0ull) {
       // rare: slot 3 of a node with more than 4 out-edges walks the CSR tail; appends
@@ -1103,7 +1129,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
                                         my_relaxed, knext, isnew);
               if (psl >= 0) {
                 const int p = atomicAdd(&L.n_pend, 1);
-                if (p < CAP) L.pend[p] = (Idx)psl;
+                if (p < SearchLds<CAP, LM>::PCAP) L.pend[p] = (Idx)psl;
                 else L.overflow = 1;
               }
             }
@@ -1111,7 +1137,7 @@ __device__ bool search_run(SearchLds<CAP, LM>* Ls, const DevGraph& g, const Pack
       }
       __syncthreads();
       npend = L.n_pend;
-      if (npend > CAP) npend = CAP;
+      if (npend > SearchLds<CAP, LM>::PCAP) npend = SearchLds<CAP, LM>::PCAP;
     }
     __syncthreads();
     OTR_STAMP(t4);
